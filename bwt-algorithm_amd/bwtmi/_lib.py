@@ -1,0 +1,154 @@
+"""ctypes binding of libbwtmi.so (C ABI in include/bwtmi.h).
+
+The shared library is built in-tree (``make -C bwt-algorithm_amd``) and loaded
+from the package's parent directory.  There is deliberately no fallback: if
+the library or a gfx950 device is missing, the calls below raise.
+"""
+from __future__ import annotations
+
+import atexit
+import ctypes as C
+import os
+import threading
+from typing import Dict, Optional
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("BWTMI_LIB", os.path.join(_PKG_ROOT, "libbwtmi.so"))
+
+FMT = {"strfinder": 0, "bed": 1, "vcf": 2, "trf_table": 3, "trf_dat": 4}
+
+
+class BwtmiError(RuntimeError):
+    pass
+
+
+class Hit(C.Structure):
+    _fields_ = [("start", C.c_int64), ("end", C.c_int64), ("unit_len", C.c_int32),
+                ("prim_len", C.c_int32), ("copies", C.c_int64)]
+
+
+class Params(C.Structure):
+    _fields_ = [("min_copies", C.c_int32), ("max_unit_len", C.c_int32),
+                ("show_progress", C.c_int32), ("tier2", C.c_int32), ("threads", C.c_int32),
+                ("build_index", C.c_int32), ("sa_sample", C.c_int32), ("reserved", C.c_int32)]
+
+
+_lib = None
+_lock = threading.Lock()
+
+# name -> (restype, argtypes)
+_P = C.c_void_p
+_SIGS = {
+    "bwtmi_last_error": (C.c_char_p, []),
+    "bwtmi_version": (C.c_char_p, []),
+    "bwtmi_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "bwtmi_open": (C.c_int, [C.c_int, C.POINTER(_P)]),
+    "bwtmi_close": (C.c_int, [_P]),
+    "bwtmi_free": (None, [_P]),
+    "bwtmi_last_timing": (C.c_int, [_P, C.POINTER(C.c_double)]),
+    "bwtmi_strict_scan": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                    C.POINTER(C.POINTER(Hit)), C.POINTER(C.c_int64)]),
+    "bwtmi_index_build": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_uint32, C.POINTER(_P)]),
+    "bwtmi_index_free": (C.c_int, [_P]),
+    "bwtmi_index_size": (C.c_int64, [_P]),
+    "bwtmi_index_get_sa": (C.c_int, [_P, _P]),
+    "bwtmi_index_get_bwt": (C.c_int, [_P, _P]),
+    "bwtmi_index_get_counts": (C.c_int, [_P, _P, _P]),
+    "bwtmi_index_occ_len": (C.c_int64, [_P]),
+    "bwtmi_index_get_occ": (C.c_int, [_P, C.c_uint8, _P]),
+    "bwtmi_index_sampled_len": (C.c_int64, [_P]),
+    "bwtmi_index_get_sampled": (C.c_int, [_P, _P]),
+    "bwtmi_index_kmer_count": (C.c_int64, [_P]),
+    "bwtmi_index_get_kmer": (C.c_int, [_P, _P, _P]),
+    "bwtmi_index_lcp": (C.c_int, [_P, _P, _P]),
+    "bwtmi_backward_search_batch": (C.c_int, [_P, _P, _P, _P, C.c_int64, _P]),
+    "bwtmi_job_create": (C.c_int, [C.POINTER(Params), C.POINTER(_P)]),
+    "bwtmi_job_free": (C.c_int, [_P]),
+    "bwtmi_job_add_contig": (C.c_int, [_P, C.c_char_p, _P, C.c_int64, C.c_int64, C.c_int64,
+                                       C.POINTER(C.c_int32)]),
+    "bwtmi_job_scan": (C.c_int, [_P, _P]),
+    "bwtmi_job_upload": (C.c_int, [_P, _P]),
+    "bwtmi_job_reset": (C.c_int, [_P]),
+    "bwtmi_job_add_hits": (C.c_int, [_P, C.c_int32, _P, C.c_int64]),
+    "bwtmi_job_raw_count": (C.c_int64, [_P]),
+    "bwtmi_job_postprocess": (C.c_int, [_P]),
+    "bwtmi_job_count": (C.c_int64, [_P]),
+    "bwtmi_job_render": (C.c_int, [_P, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
+    "bwtmi_job_write": (C.c_int, [_P, C.c_int, C.c_char_p]),
+    "bwtmi_job_get_records": (C.c_int, [_P, _P, _P]),
+    "bwtmi_job_get_string": (C.c_int64, [_P, C.c_int64, C.c_int, _P, C.c_int64]),
+    "bwtmi_job_export": (C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
+    "bwtmi_job_import": (C.c_int, [_P, _P, C.c_int64]),
+    "bwtmi_job_stage_ms": (C.c_int, [_P, C.POINTER(C.c_double)]),
+"bwtmi_align_region": (C.c_int, [C.c_char_p, C.c_int64, C.c_int64, C.c_int64, C.c_char_p, C.c_int64,
+                                     C.c_double, C.c_int64, C.c_int64, _P, C.POINTER(C.c_double), _P,
+                                     C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    "bwtmi_job_load_fasta": (C.c_int, [_P, C.c_char_p, C.c_int32]),
+    "bwtmi_job_contig_count": (C.c_int32, [_P]),
+    "bwtmi_job_contig_info": (C.c_int64, [_P, C.c_int32, C.c_char_p, C.c_int64, C.POINTER(C.c_int64),
+                                          C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "bwtmi_job_contig_seq": (C.c_int, [_P, C.c_int32, _P]),
+}
+EXPORTED = tuple(_SIGS)
+
+
+def lib():
+    """Load libbwtmi.so (raises BwtmiError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise BwtmiError(f"{LIB_PATH} not found: build it with `make -C {_PKG_ROOT}` "
+                                 "(there is no CPU fallback)")
+            L = C.CDLL(LIB_PATH)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = lib().bwtmi_last_error()
+        raise BwtmiError(f"libbwtmi error {rc}: {msg.decode(errors='replace') if msg else ''}")
+
+
+_ctxs: Dict[int, C.c_void_p] = {}
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(lib().bwtmi_device_count(C.byref(n)))
+    return n.value
+
+
+def ctx(device: Optional[int] = None) -> C.c_void_p:
+    """Per-process device context (opened once per device, closed at exit)."""
+    if device is None:
+        device = int(os.environ.get("BWTMI_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    with _lock:
+        h = _ctxs.get(device)
+        if h is None:
+            h = C.c_void_p()
+            check(lib().bwtmi_open(device, C.byref(h)))
+            _ctxs[device] = h
+    return h
+
+
+@atexit.register
+def _close_all():
+    if _lib is None:
+        return
+    for h in list(_ctxs.values()):
+        _lib.bwtmi_close(h)
+    _ctxs.clear()
+
+
+def last_timing(h) -> tuple:
+    out = (C.c_double * 3)()
+    check(lib().bwtmi_last_timing(h, out))
+    return tuple(out)

@@ -1,0 +1,251 @@
+"""Repeat records and the native job wrapper.
+
+``TandemRepeat`` keeps the reference's field names and formatters
+(bwt.py:429-641) so user code that consumed the reference's objects keeps
+working; the bulk path never materialises them -- ``RepeatList`` is a lazy
+view over the records held by the native job, and ``save_results`` renders
+them natively (bwt.py:4141-4198).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import Hit, Params, check, lib
+
+
+@dataclass
+class TandemRepeat:
+    chrom: str
+    start: int
+    end: int
+    motif: str
+    copies: float
+    length: int
+    tier: int
+    confidence: float = 1.0
+    consensus_motif: Optional[str] = None
+    mismatch_rate: float = 0.0
+    max_mismatches_per_copy: int = 0
+    n_copies_evaluated: int = 0
+    strand: str = "+"
+    percent_matches: float = 0.0
+    percent_indels: float = 0.0
+    score: int = 0
+    composition: Optional[Dict[str, float]] = None
+    entropy: float = 0.0
+    actual_sequence: Optional[str] = None
+    variations: Optional[List[str]] = None
+
+    # formatters: same columns and number formats as bwt.py:454-513
+    def _cons(self) -> str:
+        return self.consensus_motif or self.motif
+
+    def _comp(self):
+        return self.composition or {"A": 25.0, "C": 25.0, "G": 25.0, "T": 25.0}
+
+    def to_bed(self) -> str:
+        return (f"{self.chrom}\t{self.start}\t{self.end}\t{self._cons()}\t{self.copies:.1f}\t"
+                f"{self.tier}\t{self.mismatch_rate:.3f}\t{self.strand}")
+
+    def to_vcf_info(self) -> str:
+        return ";".join([f"MOTIF={self.motif}", f"CONS_MOTIF={self._cons()}",
+                         f"COPIES={self.copies:.1f}", f"TIER={self.tier}",
+                         f"CONF={self.confidence:.2f}", f"MM_RATE={self.mismatch_rate:.3f}",
+                         f"MAX_MM_PER_COPY={self.max_mismatches_per_copy}",
+                         f"N_COPIES_EVAL={self.n_copies_evaluated}", f"STRAND={self.strand}"])
+
+    def to_trf_table(self) -> str:
+        c, p = self._comp(), len(self._cons())
+        return (f"{self.start}--{self.end}\t{p}\t{self.copies:.1f}\t{p}\t"
+                f"{self.percent_matches:.0f}\t{self.percent_indels:.0f}\t{self.score}\t"
+                f"{c['A']:.0f}\t{c['C']:.0f}\t{c['G']:.0f}\t{c['T']:.0f}\t{self.entropy:.2f}")
+
+    def to_trf_dat(self) -> str:
+        c, cons = self._comp(), self._cons()
+        seq = self.actual_sequence or (cons * int(self.copies))
+        return (f"{self.start} {self.end} {len(cons)} {self.copies:.1f} {len(cons)} "
+                f"{self.percent_matches:.0f} {self.percent_indels:.0f} {self.score} "
+                f"{c['A']:.0f} {c['C']:.0f} {c['G']:.0f} {c['T']:.0f} {self.entropy:.2f} {cons} {seq}")
+
+
+def _composition(s: str) -> Dict[str, float]:
+    if not s:
+        return {"A": 0.0, "C": 0.0, "G": 0.0, "T": 0.0}
+    u = s.upper()
+    return {b: (u.count(b) / len(s)) * 100.0 for b in "ACGT"}
+
+
+def _entropy(s: str) -> float:
+    if not s:
+        return 0.0
+    seen: Dict[str, int] = {}
+    for ch in s:
+        seen[ch] = seen.get(ch, 0) + 1
+    e = 0.0
+    for c in seen.values():
+        p = c / len(s)
+        e -= p * math.log2(p)
+    return e
+
+
+class Job:
+    """Owner of one native bwtmi_job (contigs, raw hits, final records)."""
+
+    def __init__(self, min_copies=3, max_unit_len=120, show_progress=False, tier2=True,
+                 threads=0, build_index=False, sa_sample=32):
+        self.params = Params(min_copies, max_unit_len, int(bool(show_progress)), int(bool(tier2)),
+                             threads, int(bool(build_index)), sa_sample, 0)
+        self.h = C.c_void_p()
+        check(lib().bwtmi_job_create(C.byref(self.params), C.byref(self.h)))
+        self.names: List[str] = []
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h and _lib._lib is not None:
+            _lib._lib.bwtmi_job_free(h)
+            self.h = None
+
+    # contigs ------------------------------------------------------------
+    def add_contig(self, name: str, full: bytes, trim_left: int, trim_right: int) -> int:
+        cid = C.c_int32()
+        buf = C.create_string_buffer(full, len(full)) if full else None
+        check(lib().bwtmi_job_add_contig(self.h, name.encode(), buf, len(full), trim_left, trim_right,
+                                         C.byref(cid)))
+        self.names.append(name)
+        return cid.value
+
+    def load_fasta(self, path: str, flank_trim: int) -> None:
+        check(lib().bwtmi_job_load_fasta(self.h, path.encode(), flank_trim))
+        self.names = [self.contig_info(i)[0] for i in range(self.contig_count())]
+
+    def contig_count(self) -> int:
+        return lib().bwtmi_job_contig_count(self.h)
+
+    def contig_info(self, i: int):
+        fl, tl, tr = C.c_int64(), C.c_int64(), C.c_int64()
+        n = lib().bwtmi_job_contig_info(self.h, i, None, 0, C.byref(fl), C.byref(tl), C.byref(tr))
+        buf = C.create_string_buffer(n + 1)
+        lib().bwtmi_job_contig_info(self.h, i, buf, n + 1, None, None, None)
+        return buf.value.decode(errors="surrogateescape"), fl.value, tl.value, tr.value
+
+    def contig_seq(self, i: int) -> bytes:
+        _, fl, _, _ = self.contig_info(i)
+        buf = C.create_string_buffer(max(fl, 1))
+        check(lib().bwtmi_job_contig_seq(self.h, i, buf))
+        return buf.raw[:fl]
+
+    # pipeline -----------------------------------------------------------
+    def upload(self, dev_ctx) -> None:
+        check(lib().bwtmi_job_upload(dev_ctx, self.h))
+
+    def scan(self, dev_ctx) -> None:
+        check(lib().bwtmi_job_scan(dev_ctx, self.h))
+
+    def reset(self) -> None:
+        check(lib().bwtmi_job_reset(self.h))
+
+    def add_hits(self, cid: int, hits: np.ndarray) -> None:
+        """hits: int64[k,5] rows (start, end, unit_len, prim_len, copies)."""
+        hits = np.asarray(hits, dtype=np.int64).reshape(-1, 5)
+        arr = (Hit * max(len(hits), 1))()
+        for i, (s, e, L, p, c) in enumerate(hits.tolist()):
+            arr[i] = Hit(s, e, L, p, c)
+        check(lib().bwtmi_job_add_hits(self.h, cid, arr, len(hits)))
+
+    def raw_count(self) -> int:
+        return lib().bwtmi_job_raw_count(self.h)
+
+    def postprocess(self) -> None:
+        check(lib().bwtmi_job_postprocess(self.h))
+
+    def count(self) -> int:
+        return lib().bwtmi_job_count(self.h)
+
+    def render(self, fmt: str = "strfinder") -> bytes:
+        p, n = C.c_void_p(), C.c_int64()
+        check(lib().bwtmi_job_render(self.h, _lib.FMT[fmt], C.byref(p), C.byref(n)))
+        try:
+            return C.string_at(p, n.value)
+        finally:
+            lib().bwtmi_free(p)
+
+    def write(self, fmt: str, path: str) -> None:
+        check(lib().bwtmi_job_write(self.h, _lib.FMT[fmt], path.encode()))
+
+    def export(self) -> bytes:
+        p, n = C.c_void_p(), C.c_int64()
+        check(lib().bwtmi_job_export(self.h, C.byref(p), C.byref(n)))
+        try:
+            return C.string_at(p, n.value)
+        finally:
+            lib().bwtmi_free(p)
+
+    def import_records(self, blob: bytes) -> None:
+        buf = C.create_string_buffer(blob, len(blob))
+        check(lib().bwtmi_job_import(self.h, buf, len(blob)))
+
+    def stage_ms(self) -> List[float]:
+        out = (C.c_double * 8)()
+        check(lib().bwtmi_job_stage_ms(self.h, out))
+        return list(out)
+
+    # record view --------------------------------------------------------
+    def _string(self, i: int, which: int) -> str:
+        n = lib().bwtmi_job_get_string(self.h, i, which, None, 0)
+        if n <= 0:
+            return ""
+        buf = C.create_string_buffer(n)
+        lib().bwtmi_job_get_string(self.h, i, which, buf, n)
+        return buf.raw[:n].decode("ascii", errors="replace")
+
+    def records(self) -> "RepeatList":
+        return RepeatList(self)
+
+
+class RepeatList(Sequence):
+    """Lazy sequence of TandemRepeat over a job's final records (sorted as the
+    reference returns them)."""
+
+    def __init__(self, job: Job):
+        self.job = job
+        n = job.count()
+        self._n = n
+        self._ints = np.zeros((max(n, 1), 9), dtype=np.int64)
+        self._dbls = np.zeros((max(n, 1), 3), dtype=np.float64)
+        if n:
+            check(lib().bwtmi_job_get_records(job.h, self._ints.ctypes.data_as(C.c_void_p),
+                                              self._dbls.ctypes.data_as(C.c_void_p)))
+        self._cache: Dict[int, TandemRepeat] = {}
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(self._n))]
+        if i < 0:
+            i += self._n
+        if not 0 <= i < self._n:
+            raise IndexError(i)
+        r = self._cache.get(i)
+        if r is None:
+            s, e, ln, tier, neval, maxmm, _, _, chrom = self._ints[i].tolist()
+            copies, mm, conf = self._dbls[i].tolist()
+            motif = self.job._string(i, 0)
+            var = self.job._string(i, 2)
+            r = TandemRepeat(chrom=self.job.names[chrom], start=s, end=e, motif=motif, copies=copies,
+                             length=ln, tier=tier, confidence=conf, consensus_motif=motif,
+                             mismatch_rate=mm, max_mismatches_per_copy=maxmm,
+                             n_copies_evaluated=neval, strand=self.job._string(i, 4),
+                             percent_matches=max(0.0, 100.0 - mm * 100.0),
+                             composition=_composition(motif), entropy=_entropy(motif),
+                             actual_sequence=self.job._string(i, 3),
+                             variations=var.split(";") if var else None)
+            self._cache[i] = r
+        return r

@@ -1,0 +1,179 @@
+"""Deterministic synthetic FASTA generator.
+
+The reference ships no large-input generator (only the 142 bp
+`test_tandem_repeats.py:81-138` toy), so the benchmark contigs are produced
+here.  Everything is driven by splitmix64 in counter mode, computed with
+explicit uint64 arithmetic, so the bytes are identical on every machine and
+numpy version:
+
+* background: i.i.d. uniform ACGT, base i = top 2 bits of mix(bg + (i+1)·γ);
+* planted tandem arrays after every gap ~U[200, 2000]: unit length 60 %
+  U{1..6}, 30 % U{7..30}, 10 % U{31..120}; copies U{3..30}; random unit;
+* optional "imperfect" variant: each base inside a planted array is
+  substituted with probability `sub_rate` (C5 uses 0.02);
+* output: upper case, 60-column lines, headers ``>contig{k}``.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+from typing import Iterable, List, Optional, Tuple
+
+import numpy as np
+
+GAMMA = 0x9E3779B97F4A7C15
+MASK64 = (1 << 64) - 1
+SEED_BASE = 0x5EED0000
+ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
+
+
+def _mix_int(z: int) -> int:
+    z &= MASK64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & MASK64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & MASK64
+    return z ^ (z >> 31)
+
+
+def _mix_np(z: np.ndarray) -> np.ndarray:
+    z = z.astype(np.uint64, copy=False)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+class _Stream:
+    """Sequential splitmix64 stream (output k = mix(state0 + (k+1)·γ))."""
+
+    def __init__(self, seed: int):
+        self.state = seed & MASK64
+
+    def next(self) -> int:
+        self.state = (self.state + GAMMA) & MASK64
+        return _mix_int(self.state)
+
+    def below(self, m: int) -> int:
+        return self.next() % m
+
+
+def _counter_block(seed: int, start: int, count: int) -> np.ndarray:
+    idx = np.arange(start + 1, start + count + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed & MASK64) + idx * np.uint64(GAMMA)
+    return _mix_np(z)
+
+
+def generate_contig(length: int, index: int, sub_rate: float = 0.0,
+                    plants: Optional[List[Tuple[int, int, int]]] = None) -> bytes:
+    """Return the sequence bytes of synthetic contig `index`.
+
+    `plants`, when given, receives (start, unit_len, copies) per planted array.
+    """
+    seed = SEED_BASE + index
+    bg_seed = _mix_int(seed ^ 0xB6)
+    pl_seed = _mix_int(seed ^ 0x91A7)
+    sub_seed = _mix_int(seed ^ 0x5B5)
+
+    seq = np.empty(length, dtype=np.uint8)
+    chunk = 1 << 22
+    for s in range(0, length, chunk):
+        c = min(chunk, length - s)
+        seq[s:s + c] = ACGT[(_counter_block(bg_seed, s, c) >> np.uint64(62)).astype(np.intp)]
+
+    rng = _Stream(pl_seed)
+    cur = 0
+    sub_thresh = int(sub_rate * float(1 << 64)) if sub_rate > 0 else 0
+    while True:
+        cur += 200 + rng.below(1801)
+        if cur >= length:
+            break
+        u = rng.below(100)
+        if u < 60:
+            unit = 1 + rng.below(6)
+        elif u < 90:
+            unit = 7 + rng.below(24)
+        else:
+            unit = 31 + rng.below(90)
+        copies = 3 + rng.below(28)
+        motif = bytearray()
+        while len(motif) < unit:
+            w = rng.next()
+            for k in range(32):
+                if len(motif) == unit:
+                    break
+                motif.append(b"ACGT"[(w >> (62 - 2 * k)) & 3])
+        span = min(unit * copies, length - cur)
+        arr = np.frombuffer(bytes(motif) * copies, dtype=np.uint8)[:span]
+        seq[cur:cur + span] = arr
+        if sub_thresh:
+            r = _counter_block(sub_seed, cur, span)
+            hit = r < np.uint64(sub_thresh)
+            if hit.any():
+                code = np.searchsorted(ACGT, seq[cur:cur + span][hit])
+                shift = 1 + ((r[hit] >> np.uint64(8)) % np.uint64(3)).astype(np.intp)
+                seg = seq[cur:cur + span]
+                seg[hit] = ACGT[(code + shift) % 4]
+        if plants is not None:
+            plants.append((cur, unit, copies))
+        cur += span
+    return seq.tobytes()
+
+
+def format_fasta_record(name: str, seq: bytes, width: int = 60) -> bytes:
+    arr = np.frombuffer(seq, dtype=np.uint8)
+    full = len(arr) // width
+    out = [b">" + name.encode() + b"\n"]
+    if full:
+        body = np.empty((full, width + 1), dtype=np.uint8)
+        body[:, :width] = arr[:full * width].reshape(full, width)
+        body[:, width] = 10
+        out.append(body.tobytes())
+    if len(arr) % width:
+        out.append(arr[full * width:].tobytes() + b"\n")
+    return b"".join(out)
+
+
+def write_fasta(path: str, lengths: Iterable[int], sub_rate: float = 0.0,
+                first_index: int = 1) -> str:
+    """Write contigs ``contig{k}`` (k from `first_index`); return sha256 of the file."""
+    h = hashlib.sha256()
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        for k, n in enumerate(lengths, first_index):
+            rec = format_fasta_record(f"contig{k}", generate_contig(n, k, sub_rate))
+            h.update(rec)
+            f.write(rec)
+    os.replace(tmp, path)
+    return h.hexdigest()
+
+
+CONFIGS = {
+    # BASELINE.json configs
+    "C2": dict(lengths=[1_000_000], sub_rate=0.0),
+    "C3": dict(lengths=[100_000_000], sub_rate=0.0),
+    "C4": dict(lengths=[12_500_000] * 8, sub_rate=0.0),
+    "C5": dict(lengths=[100_000_000], sub_rate=0.02),
+}
+
+
+def main(argv=None) -> int:
+    import argparse
+    ap = argparse.ArgumentParser(description="seeded synthetic FASTA (splitmix64)")
+    ap.add_argument("out")
+    ap.add_argument("--config", choices=sorted(CONFIGS))
+    ap.add_argument("--lengths", type=lambda s: [int(x) for x in s.split(",")])
+    ap.add_argument("--sub-rate", type=float, default=None)
+    ap.add_argument("--first-index", type=int, default=1)
+    a = ap.parse_args(argv)
+    if a.config:
+        cfg = dict(CONFIGS[a.config])
+    else:
+        cfg = dict(lengths=a.lengths or [1_000_000], sub_rate=0.0)
+    if a.sub_rate is not None:
+        cfg["sub_rate"] = a.sub_rate
+    print(write_fasta(a.out, cfg["lengths"], cfg["sub_rate"], a.first_index))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

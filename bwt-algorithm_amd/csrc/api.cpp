@@ -1,0 +1,581 @@
+// api.cpp -- the extern "C" boundary of libbwtmi.so (include/bwtmi.h).
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "device.h"
+
+namespace bwtmi {
+
+static thread_local std::string g_err;
+
+void set_error(const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+void fail(int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    throw Error{code};
+}
+
+template <class F>
+static int guard(F &&f) {
+    try {
+        f();
+        return BWTMI_OK;
+    } catch (const Error &e) {
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        g_err = "out of host memory";
+        return BWTMI_E_NOMEM;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return BWTMI_E_STATE;
+    }
+}
+
+// device copy of one contig's trimmed sequence, padded for vector loads
+struct DevContig {
+    DBuf buf;
+    int64_t n = -1;
+};
+
+struct JobDev {
+    int device = -1;
+    std::vector<DevContig> seqs;
+};
+
+}  // namespace bwtmi
+
+using namespace bwtmi;
+
+struct bwtmi_ctx {
+    Ctx c;
+};
+struct bwtmi_index {
+    DeviceIndex *d = nullptr;
+    bwtmi_ctx *ctx = nullptr;
+};
+struct bwtmi_job {
+    Job j;
+    JobDev dev;
+};
+
+#define CHECK_ARG(cond, msg)                     \
+    do {                                         \
+        if (!(cond)) fail(BWTMI_E_ARG, "%s", msg); \
+    } while (0)
+
+extern "C" {
+
+const char *bwtmi_last_error(void) { return g_err.c_str(); }
+const char *bwtmi_version(void) { return "bwtmi 0.1 (gfx950)"; }
+void bwtmi_free(void *p) { std::free(p); }
+
+int bwtmi_device_count(int *count) {
+    return guard([&] {
+        CHECK_ARG(count, "null count");
+        int n = 0;
+        hipError_t e = hipGetDeviceCount(&n);
+        *count = (e == hipSuccess) ? n : 0;
+    });
+}
+
+int bwtmi_open(int device, bwtmi_ctx **out) {
+    return guard([&] {
+        CHECK_ARG(out, "null out");
+        *out = nullptr;
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+            fail(BWTMI_E_NODEVICE, "no HIP device available (libbwtmi has no CPU fallback)");
+        if (device < 0 || device >= n) fail(BWTMI_E_NODEVICE, "device %d out of range (%d devices)", device, n);
+        hipDeviceProp_t prop;
+        HIPCHECK(hipGetDeviceProperties(&prop, device));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            fail(BWTMI_E_NODEVICE, "device %d is %s; libbwtmi is built for gfx950 only", device, prop.gcnArchName);
+        auto *ctx = new bwtmi_ctx();
+        ctx->c.device = device;
+        HIPCHECK(hipSetDevice(device));
+        HIPCHECK(hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking));
+        HIPCHECK(hipEventCreate(&ctx->c.ev0));
+        HIPCHECK(hipEventCreate(&ctx->c.ev1));
+        *out = ctx;
+    });
+}
+
+int bwtmi_close(bwtmi_ctx *ctx) {
+    return guard([&] {
+        if (!ctx) return;
+        ctx->c.activate();
+        (void)hipStreamSynchronize(ctx->c.stream);
+        for (auto &s : ctx->c.slot) s.release();
+        for (auto &h : ctx->c.host) h.release();
+        (void)hipEventDestroy(ctx->c.ev0);
+        (void)hipEventDestroy(ctx->c.ev1);
+        (void)hipStreamDestroy(ctx->c.stream);
+        delete ctx;
+    });
+}
+
+int bwtmi_last_timing(bwtmi_ctx *ctx, double *out3) {
+    return guard([&] {
+        CHECK_ARG(ctx && out3, "null argument");
+        out3[0] = ctx->c.last_total_ms;
+        out3[1] = ctx->c.last_dom_ms;
+        out3[2] = ctx->c.last_dom_launches;
+    });
+}
+
+// ------------------------------------------------------------ strict scan
+static void upload_text(Ctx &c, DBuf &buf, const uint8_t *seq, int64_t n) {
+    buf.ensure((size_t)n + 128);
+    HIPCHECK(hipMemsetAsync((uint8_t *)buf.p + n, 0, 128, c.stream));
+    if (n) HIPCHECK(hipMemcpyAsync(buf.p, seq, (size_t)n, hipMemcpyHostToDevice, c.stream));
+}
+
+int bwtmi_strict_scan(bwtmi_ctx *ctx, const uint8_t *seq, int64_t n, int32_t min_unit, int32_t max_unit,
+                      int32_t max_mismatch, int32_t min_copies, bwtmi_hit **hits, int64_t *nhits) {
+    return guard([&] {
+        CHECK_ARG(ctx && hits && nhits && (seq || n == 0) && n >= 0, "bad argument");
+        CHECK_ARG(max_mismatch == 0, "only max_mismatch == 0 (the CLI path) is implemented on the device");
+        *hits = nullptr;
+        *nhits = 0;
+        if (n > 0 && seq[n - 1] == '$') --n;   // bwt.py:1915-1916
+        Ctx &c = ctx->c;
+        c.activate();
+        upload_text(c, c.slot[S_TEXT], seq, n);
+        ScanResult r;
+        strict_scan_device(c, c.slot[S_TEXT].as<uint8_t>(), n, min_unit, max_unit, min_copies, r);
+        *nhits = (int64_t)r.hits.size();
+        auto *out = (bwtmi_hit *)std::malloc(std::max<size_t>(1, r.hits.size()) * sizeof(bwtmi_hit));
+        if (!out) fail(BWTMI_E_NOMEM, "malloc");
+        if (!r.hits.empty()) std::memcpy(out, r.hits.data(), r.hits.size() * sizeof(bwtmi_hit));
+        *hits = out;
+    });
+}
+
+// ------------------------------------------------------------ index
+int bwtmi_index_build(bwtmi_ctx *ctx, const uint8_t *text, int64_t n, int32_t sa_sample, int32_t occ_sample,
+                      uint32_t flags, bwtmi_index **out) {
+    return guard([&] {
+        CHECK_ARG(ctx && out && (text || n == 0) && n >= 0 && sa_sample > 0 && occ_sample > 0, "bad argument");
+        *out = nullptr;
+        Ctx &c = ctx->c;
+        c.activate();
+        upload_text(c, c.slot[S_TEXT], text, n);
+        auto *idx = new bwtmi_index();
+        idx->ctx = ctx;
+        try {
+            idx->d = index_build_device(c, c.slot[S_TEXT].as<uint8_t>(), n, sa_sample, occ_sample, flags);
+        } catch (...) {
+            delete idx;
+            throw;
+        }
+        *out = idx;
+    });
+}
+
+int bwtmi_index_free(bwtmi_index *idx) {
+    return guard([&] {
+        if (!idx) return;
+        idx->ctx->c.activate();
+        index_free(idx->d);
+        delete idx;
+    });
+}
+
+int64_t bwtmi_index_size(const bwtmi_index *idx) { return idx ? index_n(idx->d) : -1; }
+int64_t bwtmi_index_occ_len(const bwtmi_index *idx) { return idx ? index_occ_len(idx->d) : -1; }
+int64_t bwtmi_index_sampled_len(const bwtmi_index *idx) { return idx ? index_sampled_len(idx->d) : -1; }
+int64_t bwtmi_index_kmer_count(const bwtmi_index *idx) { return idx ? index_kmer_count(idx->d) : -1; }
+
+int bwtmi_index_get_sa(const bwtmi_index *idx, int32_t *sa) {
+    return guard([&] { CHECK_ARG(idx && sa, "null"); index_get_sa(idx->ctx->c, idx->d, sa); });
+}
+int bwtmi_index_get_bwt(const bwtmi_index *idx, uint8_t *bwt) {
+    return guard([&] { CHECK_ARG(idx && bwt, "null"); index_get_bwt(idx->ctx->c, idx->d, bwt); });
+}
+int bwtmi_index_get_counts(const bwtmi_index *idx, int64_t *totals, int64_t *C) {
+    return guard([&] { CHECK_ARG(idx && totals && C, "null"); index_get_counts(idx->d, totals, C); });
+}
+int bwtmi_index_get_occ(const bwtmi_index *idx, uint8_t code, int32_t *cp) {
+    return guard([&] { CHECK_ARG(idx && cp, "null"); index_get_occ(idx->ctx->c, idx->d, code, cp); });
+}
+int bwtmi_index_get_sampled(const bwtmi_index *idx, int32_t *vals) {
+    return guard([&] { CHECK_ARG(idx && vals, "null"); index_get_sampled(idx->ctx->c, idx->d, vals); });
+}
+int bwtmi_index_get_kmer(const bwtmi_index *idx, int64_t *offsets, int32_t *positions) {
+    return guard([&] {
+        CHECK_ARG(idx && offsets && positions, "null");
+        index_get_kmer(idx->ctx->c, idx->d, offsets, positions);
+    });
+}
+int bwtmi_index_lcp(bwtmi_ctx *ctx, bwtmi_index *idx, int32_t *lcp) {
+    return guard([&] {
+        CHECK_ARG(ctx && idx && lcp, "null");
+        ctx->c.activate();
+        index_lcp(ctx->c, idx->d, lcp);
+    });
+}
+int bwtmi_backward_search_batch(bwtmi_ctx *ctx, bwtmi_index *idx, const uint8_t *pats, const int64_t *off,
+                                int64_t npat, int64_t *sp_ep) {
+    return guard([&] {
+        CHECK_ARG(ctx && idx && off && sp_ep && npat >= 0, "bad argument");
+        ctx->c.activate();
+        index_backward_search(ctx->c, idx->d, pats, off, npat, sp_ep);
+    });
+}
+
+// ------------------------------------------------------------ job
+int bwtmi_job_create(const bwtmi_params *params, bwtmi_job **out) {
+    return guard([&] {
+        CHECK_ARG(params && out, "null argument");
+        auto *j = new bwtmi_job();
+        j->j.params = *params;
+        if (j->j.params.sa_sample <= 0) j->j.params.sa_sample = 32;
+        *out = j;
+    });
+}
+
+int bwtmi_job_free(bwtmi_job *job) {
+    return guard([&] {
+        if (!job) return;
+        if (job->dev.device >= 0) (void)hipSetDevice(job->dev.device);
+        for (auto &d : job->dev.seqs) d.buf.release();
+        delete job;
+    });
+}
+
+int bwtmi_job_add_contig(bwtmi_job *job, const char *name, const uint8_t *full, int64_t full_len,
+                         int64_t trim_left, int64_t trim_right, int32_t *contig_id) {
+    return guard([&] {
+        CHECK_ARG(job && name && (full || full_len == 0) && full_len >= 0, "bad argument");
+        CHECK_ARG(trim_left >= 0 && trim_right >= 0 && trim_left + trim_right <= full_len, "bad trim");
+        Contig c;
+        c.name = name;
+        c.full.assign((const char *)full, (size_t)full_len);
+        c.trim_left = trim_left;
+        c.trim_right = trim_right;
+        job->j.contigs.push_back(std::move(c));
+        if (contig_id) *contig_id = (int32_t)job->j.contigs.size() - 1;
+    });
+}
+
+int bwtmi_job_load_fasta(bwtmi_job *job, const char *path, int32_t flank_trim) {
+    return guard([&] {
+        CHECK_ARG(job && path, "null argument");
+        load_fasta(job->j, path, flank_trim);
+    });
+}
+
+int32_t bwtmi_job_contig_count(const bwtmi_job *job) { return job ? (int32_t)job->j.contigs.size() : -1; }
+
+int64_t bwtmi_job_contig_info(const bwtmi_job *job, int32_t id, char *name, int64_t cap, int64_t *full_len,
+                              int64_t *trim_left, int64_t *trim_right) {
+    if (!job || id < 0 || id >= (int32_t)job->j.contigs.size()) return -1;
+    const Contig &c = job->j.contigs[(size_t)id];
+    if (name && cap > 0) {
+        const size_t k = std::min<size_t>((size_t)cap - 1, c.name.size());
+        std::memcpy(name, c.name.data(), k);
+        name[k] = 0;
+    }
+    if (full_len) *full_len = (int64_t)c.full.size();
+    if (trim_left) *trim_left = c.trim_left;
+    if (trim_right) *trim_right = c.trim_right;
+    return (int64_t)c.name.size();
+}
+
+int bwtmi_job_contig_seq(const bwtmi_job *job, int32_t id, uint8_t *dst) {
+    return guard([&] {
+        CHECK_ARG(job && dst && id >= 0 && id < (int32_t)job->j.contigs.size(), "bad argument");
+        const Contig &c = job->j.contigs[(size_t)id];
+        std::memcpy(dst, c.full.data(), c.full.size());
+    });
+}
+
+static void job_upload(bwtmi_ctx *ctx, bwtmi_job *job) {
+    Ctx &c = ctx->c;
+    c.activate();
+    JobDev &d = job->dev;
+    if (d.device >= 0 && d.device != c.device) {
+        for (auto &s : d.seqs) s.buf.release();
+        d.seqs.clear();
+    }
+    d.device = c.device;
+    d.seqs.resize(job->j.contigs.size());
+    for (size_t i = 0; i < job->j.contigs.size(); ++i) {
+        const Contig &ct = job->j.contigs[i];
+        DevContig &dc = d.seqs[i];
+        if (dc.n == ct.trimmed_len()) continue;
+        upload_text(c, dc.buf, (const uint8_t *)ct.trimmed(), ct.trimmed_len());
+        dc.n = ct.trimmed_len();
+    }
+    HIPCHECK(hipStreamSynchronize(c.stream));
+}
+
+int bwtmi_job_upload(bwtmi_ctx *ctx, bwtmi_job *job) {
+    return guard([&] {
+        CHECK_ARG(ctx && job, "null argument");
+        job_upload(ctx, job);
+    });
+}
+
+int bwtmi_job_reset(bwtmi_job *job) {
+    return guard([&] {
+        CHECK_ARG(job, "null argument");
+        job->j.raw.clear();
+        job->j.final_recs.clear();
+        job->j.postprocessed = false;
+    });
+}
+
+int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
+    return guard([&] {
+        CHECK_ARG(ctx && job, "null argument");
+        auto t0 = std::chrono::steady_clock::now();
+        job_upload(ctx, job);
+        Job &J = job->j;
+        Ctx &c = ctx->c;
+        J.raw.assign(J.contigs.size(), {});
+        J.final_recs.clear();
+        J.postprocessed = false;
+        const bwtmi_params &P = J.params;
+        double idx_ms = 0;
+        for (size_t i = 0; i < J.contigs.size(); ++i) {
+            const Contig &ct = J.contigs[i];
+            const int64_t len = ct.trimmed_len();
+            if (P.build_index) {   // BWTCore(seq + '$') of the worker (bwt.py:3053-3054)
+                auto ti = std::chrono::steady_clock::now();
+                DevContig &dc = job->dev.seqs[i];
+                c.slot[S_MISC3].ensure((size_t)len + 1 + 128);
+                HIPCHECK(hipMemcpyAsync(c.slot[S_MISC3].p, dc.buf.p, (size_t)len, hipMemcpyDeviceToDevice, c.stream));
+                HIPCHECK(hipMemsetAsync(c.slot[S_MISC3].as<uint8_t>() + len, '$', 1, c.stream));
+                HIPCHECK(hipMemsetAsync(c.slot[S_MISC3].as<uint8_t>() + len + 1, 0, 127, c.stream));
+                DeviceIndex *di = index_build_device(c, c.slot[S_MISC3].as<uint8_t>(), len + 1, P.sa_sample, 128,
+                                                     0u);
+                index_free(di);   // the worker never consumes it
+                idx_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ti).count();
+            }
+            if (!P.tier2) continue;                                  // bwt.py:3068
+            if (len > 50000000 && !P.show_progress) continue;        // bwt.py:3070
+            if (P.min_copies <= 0) continue;                         // worker raises -> [] (bwt.py:3137)
+            const int64_t U = std::max<int64_t>(P.max_unit_len, std::min<int64_t>(len / P.min_copies, 1000));
+            ScanResult r;
+            strict_scan_device(c, job->dev.seqs[i].buf.as<uint8_t>(), len, 1, (int32_t)std::min<int64_t>(U, INT32_MAX),
+                               P.min_copies, r);
+            strict_hits_to_records(J, (int32_t)i, r.hits.data(), (int64_t)r.hits.size(), J.raw[i]);
+        }
+        J.stage_ms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        J.stage_ms[1] = idx_ms;
+    });
+}
+
+int bwtmi_job_add_hits(bwtmi_job *job, int32_t contig_id, const bwtmi_hit *hits, int64_t n) {
+    return guard([&] {
+        CHECK_ARG(job && (hits || n == 0) && n >= 0, "bad argument");
+        Job &J = job->j;
+        CHECK_ARG(contig_id >= 0 && contig_id < (int32_t)J.contigs.size(), "bad contig id");
+        if (J.raw.size() < J.contigs.size()) J.raw.resize(J.contigs.size());
+        strict_hits_to_records(J, contig_id, hits, n, J.raw[(size_t)contig_id]);
+    });
+}
+
+int64_t bwtmi_job_raw_count(const bwtmi_job *job) {
+    if (!job) return -1;
+    int64_t n = 0;
+    for (auto &v : job->j.raw) n += (int64_t)v.size();
+    return n;
+}
+
+int bwtmi_job_postprocess(bwtmi_job *job) {
+    return guard([&] {
+        CHECK_ARG(job, "null argument");
+        postprocess(job->j);
+    });
+}
+
+int64_t bwtmi_job_count(const bwtmi_job *job) { return job ? (int64_t)job->j.final_recs.size() : -1; }
+
+int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len) {
+    return guard([&] {
+        CHECK_ARG(job && out && len, "null argument");
+        std::string s = render(job->j, fmt);
+        char *p = (char *)std::malloc(s.size() + 1);
+        if (!p) fail(BWTMI_E_NOMEM, "malloc");
+        std::memcpy(p, s.data(), s.size());
+        p[s.size()] = 0;
+        *out = p;
+        *len = (int64_t)s.size();
+    });
+}
+
+int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path) {
+    return guard([&] {
+        CHECK_ARG(job && path, "null argument");
+        std::string s = render(job->j, fmt);
+        FILE *f = std::fopen(path, "wb");
+        if (!f) fail(BWTMI_E_IO, "cannot open %s for writing", path);
+        const size_t w = std::fwrite(s.data(), 1, s.size(), f);
+        std::fclose(f);
+        if (w != s.size()) fail(BWTMI_E_IO, "short write to %s", path);
+    });
+}
+
+int bwtmi_job_get_records(bwtmi_job *job, int64_t *ints9, double *dbls3) {
+    return guard([&] {
+        CHECK_ARG(job && ints9 && dbls3, "null argument");
+        size_t k = 0;
+        for (const Rec &r : job->j.final_recs) {
+            int64_t *I = ints9 + 9 * k;
+            double *D = dbls3 + 3 * k;
+            I[0] = r.start; I[1] = r.end; I[2] = r.length; I[3] = r.tier; I[4] = r.n_eval; I[5] = r.max_mm;
+            I[6] = (int64_t)r.motif.size(); I[7] = (int64_t)r.motif.size(); I[8] = r.chrom;
+            D[0] = r.copies; D[1] = r.mismatch_rate; D[2] = r.confidence;
+            ++k;
+        }
+    });
+}
+
+int64_t bwtmi_job_get_string(bwtmi_job *job, int64_t i, int which, char *buf, int64_t cap) {
+    if (!job || i < 0 || i >= (int64_t)job->j.final_recs.size()) return -1;
+    const Rec &r = job->j.final_recs[(size_t)i];
+    std::string s;
+    switch (which) {
+        case 0: case 1: s = r.motif; break;
+        case 2: s = r.variations; break;
+        case 3: {
+            if (r.act_kind != ACT_NONE) {
+                const Contig &c = job->j.contigs[(size_t)r.chrom];
+                const char *p = (r.act_kind == ACT_FULL ? c.full.data() : c.trimmed()) + r.act_off;
+                s.assign(p, (size_t)r.act_len);
+            }
+            break;
+        }
+        case 4: s.assign(1, r.strand); break;
+        default: return -1;
+    }
+    if (buf && cap > 0) std::memcpy(buf, s.data(), std::min<size_t>((size_t)cap, s.size()));
+    return (int64_t)s.size();
+}
+
+// record wire format for the multi-GPU gather: POD header + strings
+struct WireRec {
+    int32_t chrom, tier;
+    int64_t start, end, length, max_mm, n_eval, score, act_off, act_len;
+    double copies, confidence, mismatch_rate, pmatch, pindel;
+    int8_t act_kind, strand, is_compound, kmer_stats;
+    int32_t motif_len, var_len;
+};
+
+int bwtmi_job_export(bwtmi_job *job, uint8_t **buf, int64_t *len) {
+    return guard([&] {
+        CHECK_ARG(job && buf && len, "null argument");
+        std::string s;
+        const int64_t n = (int64_t)job->j.final_recs.size();
+        s.append((const char *)&n, sizeof n);
+        for (const Rec &r : job->j.final_recs) {
+            WireRec w{};
+            w.chrom = r.chrom; w.tier = r.tier; w.start = r.start; w.end = r.end; w.length = r.length;
+            w.max_mm = r.max_mm; w.n_eval = r.n_eval; w.score = r.score; w.act_off = r.act_off; w.act_len = r.act_len;
+            w.copies = r.copies; w.confidence = r.confidence; w.mismatch_rate = r.mismatch_rate;
+            w.pmatch = r.pmatch; w.pindel = r.pindel; w.act_kind = r.act_kind; w.strand = r.strand;
+            w.is_compound = r.is_compound; w.kmer_stats = r.kmer_stats;
+            w.motif_len = (int32_t)r.motif.size(); w.var_len = (int32_t)r.variations.size();
+            s.append((const char *)&w, sizeof w);
+            s.append(r.motif);
+            s.append(r.variations);
+        }
+        auto *p = (uint8_t *)std::malloc(s.size());
+        if (!p) fail(BWTMI_E_NOMEM, "malloc");
+        std::memcpy(p, s.data(), s.size());
+        *buf = p;
+        *len = (int64_t)s.size();
+    });
+}
+
+int bwtmi_job_import(bwtmi_job *job, const uint8_t *buf, int64_t len) {
+    return guard([&] {
+        CHECK_ARG(job && buf && len >= 8, "bad argument");
+        int64_t n;
+        std::memcpy(&n, buf, 8);
+        int64_t o = 8;
+        for (int64_t k = 0; k < n; ++k) {
+            CHECK_ARG(o + (int64_t)sizeof(WireRec) <= len, "truncated record buffer");
+            WireRec w;
+            std::memcpy(&w, buf + o, sizeof w);
+            o += sizeof w;
+            CHECK_ARG(o + w.motif_len + w.var_len <= len, "truncated record strings");
+            CHECK_ARG(w.chrom >= 0 && w.chrom < (int32_t)job->j.contigs.size(), "record for unknown contig");
+            Rec r;
+            r.chrom = w.chrom; r.tier = w.tier; r.start = w.start; r.end = w.end; r.length = w.length;
+            r.max_mm = w.max_mm; r.n_eval = w.n_eval; r.score = w.score; r.act_off = w.act_off; r.act_len = w.act_len;
+            r.copies = w.copies; r.confidence = w.confidence; r.mismatch_rate = w.mismatch_rate;
+            r.pmatch = w.pmatch; r.pindel = w.pindel; r.act_kind = w.act_kind; r.strand = (char)w.strand;
+            r.is_compound = w.is_compound; r.kmer_stats = w.kmer_stats;
+            r.motif.assign((const char *)buf + o, (size_t)w.motif_len);
+            o += w.motif_len;
+            r.variations.assign((const char *)buf + o, (size_t)w.var_len);
+            o += w.var_len;
+            job->j.final_recs.push_back(std::move(r));
+        }
+        job->j.postprocessed = true;
+    });
+}
+
+int bwtmi_job_stage_ms(const bwtmi_job *job, double *out8) {
+    return guard([&] {
+        CHECK_ARG(job && out8, "null argument");
+        for (int i = 0; i < 8; ++i) out8[i] = job->j.stage_ms[i];
+    });
+}
+
+int bwtmi_align_region(const char *seq, int64_t seq_len, int64_t start, int64_t end, const char *tmpl,
+                       int64_t tmpl_len, double frac, int64_t max_indel, int64_t min_copies, int64_t *ints8,
+                       double *mismatch_rate, char *consensus, char **variations, int64_t **copy_len,
+                       int64_t **copy_err) {
+    int found = 0;
+    int rc = guard([&] {
+        CHECK_ARG((seq || seq_len == 0) && (tmpl || tmpl_len == 0) && ints8 && mismatch_rate && consensus &&
+                      variations && copy_len && copy_err, "null argument");
+        *variations = nullptr;
+        *copy_len = *copy_err = nullptr;
+        AlignSummary s;
+        std::string t(tmpl ? tmpl : "", (size_t)tmpl_len);
+        if (!align_repeat_region(seq, seq_len, start, end, t, min_copies, s, frac, max_indel)) return;
+        found = 1;
+        ints8[0] = s.copies; ints8[1] = s.motif_len; ints8[2] = s.consumed; ints8[3] = s.max_errors;
+        ints8[4] = s.tot_ins; ints8[5] = s.tot_del; ints8[6] = ints8[7] = 0;
+        *mismatch_rate = s.mismatch_rate;
+        std::memcpy(consensus, s.consensus.data(), s.consensus.size());
+        char *v = (char *)std::malloc(s.variations.size() + 1);
+        std::memcpy(v, s.variations.data(), s.variations.size());
+        v[s.variations.size()] = 0;
+        *variations = v;
+        auto *cl = (int64_t *)std::malloc(std::max<size_t>(1, s.copy_len.size()) * 8);
+        auto *ce = (int64_t *)std::malloc(std::max<size_t>(1, s.copy_err.size()) * 8);
+        for (size_t i = 0; i < s.copy_len.size(); ++i) { cl[i] = s.copy_len[i]; ce[i] = s.copy_err[i]; }
+        *copy_len = cl;
+        *copy_err = ce;
+    });
+    return rc ? rc : found;
+}
+
+}  // extern "C"

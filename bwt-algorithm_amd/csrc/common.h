@@ -1,0 +1,114 @@
+// common.h -- internal declarations shared by the libbwtmi translation units.
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/bwtmi.h"
+
+namespace bwtmi {
+
+// ---------------------------------------------------------------- errors
+void set_error(const char *fmt, ...);
+struct Error {
+    int code;
+};
+[[noreturn]] void fail(int code, const char *fmt, ...);
+
+// ---------------------------------------------------------------- contigs
+struct Contig {
+    std::string name;
+    std::string full;      // untrimmed, upper-cased (bwt.py:3739)
+    int64_t trim_left = 0;  // trim_offsets[name] (bwt.py:3733)
+    int64_t trim_right = 0;
+    int32_t unit = 0;       // fold unit (contigs with equal natural sort key)
+    const char *trimmed() const { return full.data() + trim_left; }
+    int64_t trimmed_len() const { return (int64_t)full.size() - trim_left - trim_right; }
+};
+
+// natural sort key (bwt.py:22-36) and its comparison
+struct NatPart {
+    bool digit;
+    std::string text;  // digits with leading zeros stripped, or lower-cased text
+};
+std::vector<NatPart> natural_key(const std::string &s);
+int natural_cmp(const std::vector<NatPart> &a, const std::vector<NatPart> &b);
+
+// ---------------------------------------------------------------- records
+// Field-for-field counterpart of TandemRepeat (bwt.py:429-452) as it occurs
+// on the CLI path.  On that path consensus_motif == motif for every record
+// (strict hits bwt.py:1981, recomputes 3602, compound pieces 4077/4086), so
+// one string carries both.
+enum ActKind : int8_t { ACT_NONE = 0, ACT_TRIMMED = 1, ACT_FULL = 2 };
+
+struct Rec {
+    int32_t chrom = 0;
+    int32_t tier = 2;
+    int64_t start = 0, end = 0, length = 0;
+    std::string motif;
+    double copies = 0.0;
+    double confidence = 1.0;
+    double mismatch_rate = 0.0;
+    int64_t max_mm = 0;
+    int64_t n_eval = 0;
+    char strand = '+';
+    double pmatch = 0.0, pindel = 0.0;
+    int64_t score = 0;
+    int8_t act_kind = ACT_NONE;  // actual_sequence = slice of trimmed/full contig
+    int64_t act_off = 0, act_len = 0;
+    std::string variations;      // ';'-joined; empty == None
+    int32_t partner = -1;        // compound partner index in the owning pool, -1 = none
+    bool is_compound = false;
+    bool kmer_stats = false;     // compound-stage pieces: score 100.0, zero composition,
+                                 // entropy 1.5 (bwt.py:3980-3987, 4074-4091)
+};
+
+// motif utilities (MotifUtils, bwt.py:675-1381)
+std::string min_rotation(const std::string &s);
+void canonical_stranded(const std::string &s, std::string &canon, char &strand);
+int64_t smallest_period(const char *s, int64_t n);
+double entropy_of(const char *s, int64_t n);
+void composition_of(const char *s, int64_t n, double out[4]);
+int64_t trf_score(int64_t length, double mm);
+
+struct AlignSummary {
+    std::vector<int64_t> copy_len, copy_err;  // per copy: consumed bases, errors
+    std::string consensus;
+    int64_t motif_len = 0, copies = 0, consumed = 0, max_errors = 0, tot_ins = 0, tot_del = 0;
+    double mismatch_rate = 0.0;
+    std::string variations;  // ';'-joined
+    bool any_variation = false;
+};
+// MotifUtils.align_repeat_region (bwt.py:998-1102), max_indel=None, frac=0.1
+bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_t end,
+                         const std::string &tmpl, int64_t min_copies, AlignSummary &out,
+                         double frac = 0.1, int64_t max_indel_arg = -1);
+
+// ---------------------------------------------------------------- job
+struct Job {
+    bwtmi_params params{};
+    std::vector<Contig> contigs;
+    std::vector<std::vector<NatPart>> natkeys;
+    int32_t nunits = 0;
+    std::vector<int32_t> unit_rank;                  // unit id -> rank by natural key
+    std::vector<std::vector<Rec>> raw;               // per contig, worker output order
+    std::vector<Rec> final_recs;                     // after bwt.py:3940-3944
+    bool postprocessed = false;
+    double stage_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    void assign_units();
+};
+
+// post.cpp
+void postprocess(Job &job);
+void strict_hits_to_records(const Job &job, int32_t contig, const bwtmi_hit *hits, int64_t n,
+                            std::vector<Rec> &out);
+// render.cpp
+std::string render(Job &job, int fmt);
+// fasta.cpp
+void load_fasta(Job &job, const char *path, int32_t flank_trim);
+
+int host_threads(const bwtmi_params &p);
+
+}  // namespace bwtmi

@@ -1,0 +1,123 @@
+// device.h -- HIP context, device buffers and the device-primitive entry points.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+namespace bwtmi {
+
+#define HIPCHECK(expr)                                                                  \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess)                                                           \
+            ::bwtmi::fail(BWTMI_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                          __FILE__, __LINE__);                                          \
+    } while (0)
+
+// growable device allocation
+struct DBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    void ensure(size_t n) {
+        if (n <= bytes) return;
+        if (p) {
+            HIPCHECK(hipDeviceSynchronize());  // queued kernels may still use the old block
+            HIPCHECK(hipFree(p));
+        }
+        size_t cap = n + n / 8 + 256;
+        HIPCHECK(hipMalloc(&p, cap));
+        bytes = cap;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+struct HBuf {  // pinned host staging
+    void *p = nullptr;
+    size_t bytes = 0;
+    void ensure(size_t n) {
+        if (n <= bytes) return;
+        if (p) HIPCHECK(hipHostFree(p));
+        size_t cap = n + n / 8 + 256;
+        HIPCHECK(hipHostMalloc(&p, cap, hipHostMallocDefault));
+        bytes = cap;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+enum Slot {
+    S_TEXT = 0, S_PACK, S_CAND_K, S_CAND_V, S_CAND_K2, S_CAND_V2, S_FLAG, S_SCAN, S_HITS, S_COUNTS,
+    S_SORT_TMP0, S_SORT_TMP1, S_SORT_HIST, S_SCAN_TMP, S_MISC0, S_MISC1, S_MISC2, S_MISC3,
+    S_IDX0, S_IDX1, S_IDX2, S_IDX3, S_IDX4, S_IDX5, S_IDX6, S_IDX7, S_NSLOTS
+};
+
+struct KernelTimer {
+    hipEvent_t a = nullptr, b = nullptr;
+    double total_ms = 0;
+    int launches = 0;
+};
+
+struct Ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DBuf slot[S_NSLOTS];
+    HBuf host[4];
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_total_ms = 0, last_dom_ms = 0;
+    int last_dom_launches = 0;
+    std::string dom_name;
+    bool timing = true;
+    void activate() const { HIPCHECK(hipSetDevice(device)); }
+};
+
+// ----- primitives (radix.hip)
+template <class T>
+void exclusive_scan(Ctx &c, const T *in, T *out, int64_t n);   // out may alias in
+void radix_sort_pairs(Ctx &c, uint64_t *keys, uint64_t *vals, int64_t n, int bit0, int bit1);
+void radix_sort_pairs32(Ctx &c, uint64_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1);
+
+// ----- strict scan (strict_scan.hip)
+struct ScanResult {
+    std::vector<bwtmi_hit> hits;
+    double kernel_ms = 0;
+    int64_t candidates = 0;
+};
+// d_text: device copy of the trimmed contig (n bytes, padded by >= 64 bytes)
+void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
+                        int32_t min_copies, ScanResult &out);
+
+// ----- index (index.hip)
+struct DeviceIndex;
+// d_text: device text incl. sentinel, n bytes (padded by >= 64 bytes)
+DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t sa_sample,
+                                int32_t occ_sample, uint32_t flags);
+void index_free(DeviceIndex *);
+int64_t index_n(const DeviceIndex *);
+int64_t index_occ_len(const DeviceIndex *);
+int64_t index_sampled_len(const DeviceIndex *);
+int64_t index_kmer_count(const DeviceIndex *);
+void index_get_sa(Ctx &c, const DeviceIndex *, int32_t *out);
+void index_get_bwt(Ctx &c, const DeviceIndex *, uint8_t *out);
+void index_get_counts(const DeviceIndex *, int64_t *totals, int64_t *C);
+void index_get_occ(Ctx &c, const DeviceIndex *, uint8_t code, int32_t *out);
+void index_get_sampled(Ctx &c, const DeviceIndex *, int32_t *out);
+void index_get_kmer(Ctx &c, const DeviceIndex *, int64_t *offsets, int32_t *pos);
+void index_lcp(Ctx &c, DeviceIndex *, int32_t *out);
+void index_backward_search(Ctx &c, DeviceIndex *, const uint8_t *pats, const int64_t *off, int64_t npat,
+                           int64_t *sp_ep);
+
+}  // namespace bwtmi

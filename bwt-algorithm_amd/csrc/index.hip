@@ -1,0 +1,599 @@
+// index.hip -- FM-index construction on gfx950 (replaces BWTCore.__init__,
+// bwt.py:106-136) plus the library queries built on it.
+//
+// Suffix array (bwt.py:212-264).  The reference sorts suffixes of seq+'$' by
+// byte value with "end of text" smallest; '$' unique makes the order total.
+// Here: prefix doubling over radix sorts.
+//   round 0  key = k symbols of b bits (b = bits for sigma+1 codes, code 0 =
+//            past the end, k = 64/b; ACGT$ -> 21 symbols), one 64-bit radix sort
+//   round r  only suffixes in groups of size >= 2 survive; each gets the key
+//            (group start, rank[i+h] + 1) -- sorted with one radix sort whose
+//            digit range covers exactly those bits -- and its group is split;
+//            singletons are dropped (h doubles each round)
+// BWT/C/Occ/sampled SA are single streaming kernels; the 8-mer hash is a
+// stable 16-bit radix sort of (window code, position) pairs; LCP is chunked
+// Kasai; backward search runs one pattern per lane.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "device.h"
+
+namespace bwtmi {
+
+struct DeviceIndex {
+    int64_t n = 0;
+    int32_t sa_sample = 32, occ_sample = 128;
+    int sigma = 0;
+    uint8_t code_of[256];        // byte -> occ row (valid when totals > 0)
+    int64_t totals[256], C[256];
+    DBuf text;                   // copy of the text (n + pad)
+    DBuf sa;                     // int32[n]
+    DBuf bwt;                    // uint8[n + pad]
+    DBuf occ;                    // int32[sigma][occ_len]
+    DBuf sampled;                // int32[ceil(n/s)]
+    DBuf kmer_off;               // int64[65537]
+    DBuf kmer_pos;               // int32[count]
+    int64_t kmer_count = 0;
+    bool has_kmer = false;
+    int64_t occ_len = 0, sampled_len = 0;
+};
+
+namespace {
+
+__global__ void k_hist_bytes(const uint8_t *__restrict__ t, int64_t n, unsigned long long *__restrict__ h) {
+    __shared__ unsigned int lh[256];
+    lh[threadIdx.x] = 0;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&lh[t[i]], 1u);
+    __syncthreads();
+    if (lh[threadIdx.x]) atomicAdd(&h[threadIdx.x], (unsigned long long)lh[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void k_init_keys(const uint8_t *__restrict__ t, int64_t n,
+                                                   const uint8_t *__restrict__ code, int b, int k,
+                                                   uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    __shared__ uint8_t cm[256];
+    cm[threadIdx.x] = code[threadIdx.x];
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t key = 0;
+    for (int q = 0; q < k; ++q) {
+        const uint64_t c = (i + q < n) ? cm[t[i + q]] : 0u;
+        key = (key << b) | c;
+    }
+    keys[i] = key;
+    vals[i] = (uint32_t)i;
+}
+
+// head flag of sorted position r (key differs from r-1)
+__global__ __launch_bounds__(256) void k_heads(const uint64_t *__restrict__ keys, int64_t m, uint32_t *__restrict__ head) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    head[r] = (r == 0 || keys[r] != keys[r - 1]) ? 1u : 0u;
+}
+
+// after round 0: SA = vals; rank[SA[r]] = start of r's group; flag[r] = group size >= 2
+__global__ __launch_bounds__(256) void k_rank0(const uint32_t *__restrict__ head, const uint32_t *__restrict__ gid,
+                                               const uint32_t *__restrict__ sa, int64_t m,
+                                               uint32_t *__restrict__ gstart, uint32_t *__restrict__ rank,
+                                               uint32_t *__restrict__ flag, int pass) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    if (pass == 0) {
+        if (head[r]) gstart[gid[r]] = (uint32_t)r;
+        return;
+    }
+    const uint32_t g = gid[r];
+    rank[sa[r]] = gstart[g];
+    const bool single = head[r] && (r + 1 == m || head[r + 1]);
+    flag[r] = single ? 0u : 1u;
+}
+
+// compaction of flagged indices (ascending)
+__global__ __launch_bounds__(256) void k_compact_idx(const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
+                                                     int64_t m, uint32_t *__restrict__ out, const uint32_t *__restrict__ src) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m || !flag[r]) return;
+    out[pos[r]] = src ? src[r] : (uint32_t)r;
+}
+
+// keys for the surviving suffixes: (group start << nb) | (rank[i+h] + 1 or 0)
+__global__ __launch_bounds__(256) void k_round_keys(const uint32_t *__restrict__ U, int64_t m, const uint32_t *__restrict__ sa,
+                                                    const uint32_t *__restrict__ rank, int64_t n, int64_t h, int nb,
+                                                    uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= m) return;
+    const uint32_t i = sa[U[u]];
+    const uint64_t g = rank[i];
+    const uint64_t r2 = ((int64_t)i + h < n) ? (uint64_t)rank[i + h] + 1u : 0u;
+    keys[u] = (g << nb) | r2;
+    vals[u] = i;
+}
+
+// write back: SA[U[u]] = vals[u]; group starts at heads
+__global__ __launch_bounds__(256) void k_round_apply(const uint32_t *__restrict__ U, int64_t m, const uint32_t *__restrict__ vals,
+                                                     const uint32_t *__restrict__ head, const uint32_t *__restrict__ gid,
+                                                     uint32_t *__restrict__ sa, uint32_t *__restrict__ gstart, int pass,
+                                                     uint32_t *__restrict__ rank, uint32_t *__restrict__ flag) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= m) return;
+    if (pass == 0) {
+        sa[U[u]] = vals[u];
+        if (head[u]) gstart[gid[u]] = U[u];
+        return;
+    }
+    rank[vals[u]] = gstart[gid[u]];
+    const bool single = head[u] && (u + 1 == m || head[u + 1]);
+    flag[u] = single ? 0u : 1u;
+}
+
+__global__ void k_gid(const uint32_t *__restrict__ head_scan_excl, const uint32_t *__restrict__ head, int64_t m,
+                      uint32_t *__restrict__ gid) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    gid[r] = head_scan_excl[r] + head[r] - 1u;
+}
+
+__global__ __launch_bounds__(256) void k_bwt(const uint8_t *__restrict__ t, const uint32_t *__restrict__ sa, int64_t n,
+                                             uint8_t *__restrict__ bwt) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const int64_t p = (int64_t)sa[r] - 1;
+    bwt[r] = t[p < 0 ? p + n : p];
+}
+
+// per 128-byte block counts of each present code: one wave per block (occ_sample = 128)
+__global__ __launch_bounds__(256) void k_occ_blocks(const uint8_t *__restrict__ bwt, int64_t n, int64_t nblk, int blk,
+                                                    const uint8_t *__restrict__ present, int sigma,
+                                                    uint32_t *__restrict__ cnt /* [sigma][nblk+1] */) {
+    const int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (wv >= nblk) return;
+    const int64_t base = wv * blk;
+    for (int c = 0; c < sigma; ++c) {
+        const uint8_t code = present[c];
+        uint32_t s = 0;
+        for (int o = lane; o < blk; o += 64) {
+            const int64_t i = base + o;
+            s += (i < n && bwt[i] == code) ? 1u : 0u;
+        }
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+        if (lane == 0) cnt[(int64_t)c * (nblk + 1) + wv] = s;
+    }
+}
+
+__global__ void k_sample(const uint32_t *__restrict__ sa, int64_t n, int32_t s, int32_t *__restrict__ out, int64_t m) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    out[j] = (int32_t)sa[j * s];
+}
+
+// ---- 8-mer hash (bwt.py:138-171)
+__device__ __forceinline__ int kbits(uint8_t ch) {
+    if (ch >= 'a' && ch <= 'z') ch = (uint8_t)(ch - 32);
+    switch (ch) {
+        case 'A': return 0;
+        case 'C': return 1;
+        case 'G': return 2;
+        case 'T': return 3;
+        case 'N': return 0;
+        default: return -1;
+    }
+}
+
+__global__ void k_kvalid(const uint8_t *__restrict__ t, int64_t n, uint32_t *__restrict__ v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = kbits(t[i]) >= 0 ? 1u : 0u;
+}
+
+__global__ void k_kcompact(const uint8_t *__restrict__ t, int64_t n, const uint32_t *__restrict__ vpos,
+                           uint8_t *__restrict__ V) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int b = kbits(t[i]);
+    if (b >= 0) V[vpos[i]] = (uint8_t)b;
+}
+
+// entries in position order: [first window at 0 if all k leading chars valid]
+// then every valid i >= k -> (window of the last k valid codes, i-k+1)
+__global__ void k_kentries(const uint8_t *__restrict__ t, int64_t n, int k, const uint32_t *__restrict__ vpos,
+                           const uint8_t *__restrict__ V, int first, uint64_t *__restrict__ keys,
+                           uint32_t *__restrict__ vals, uint32_t vbase_k) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (i == k - 1 && first) {
+        uint64_t w = 0;
+        for (int q = 0; q < k; ++q) w = (w << 2) | V[q];
+        keys[0] = w;
+        vals[0] = 0;
+    }
+    if (i < k || kbits(t[i]) < 0) return;
+    const int64_t v = vpos[i];
+    uint64_t w = 0;
+    for (int q = k - 1; q >= 0; --q) {
+        const int64_t x = v - q;
+        w = (w << 2) | (x >= 0 ? V[x] : 0u);
+    }
+    const int64_t e = (int64_t)first + (v - vbase_k);
+    keys[e] = w;
+    vals[e] = (uint32_t)(i - k + 1);
+}
+
+__global__ void k_khist(const uint64_t *__restrict__ keys, int64_t m, uint32_t *__restrict__ h) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) atomicAdd(&h[keys[i]], 1u);
+}
+
+// ---- LCP: chunked Kasai (exact while the only rank-0 suffix is the last one)
+__global__ void k_isa(const uint32_t *__restrict__ sa, int64_t n, uint32_t *__restrict__ isa) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n) isa[sa[r]] = (uint32_t)r;
+}
+
+__global__ void k_kasai(const uint8_t *__restrict__ t, const uint32_t *__restrict__ sa, const uint32_t *__restrict__ isa,
+                        int64_t n, int64_t chunk, int32_t *__restrict__ lcp) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i0 = c * chunk;
+    if (i0 >= n) return;
+    const int64_t i1 = i0 + chunk < n ? i0 + chunk : n;
+    int64_t h = 0;
+    for (int64_t i = i0; i < i1; ++i) {
+        const int64_t r = isa[i];
+        if (r > 0) {
+            const int64_t j = sa[r - 1];
+            while (i + h < n && j + h < n && t[i + h] == t[j + h]) ++h;
+            lcp[r] = (int32_t)h;
+            if (h > 0) --h;
+        }
+    }
+}
+
+__global__ void k_kasai_serial(const uint8_t *__restrict__ t, const uint32_t *__restrict__ sa,
+                               const uint32_t *__restrict__ isa, int64_t n, int32_t *__restrict__ lcp) {
+    if (blockIdx.x || threadIdx.x) return;
+    int64_t h = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t r = isa[i];
+        if (r > 0) {
+            const int64_t j = sa[r - 1];
+            while (i + h < n && j + h < n && t[i + h] == t[j + h]) ++h;
+            lcp[r] = (int32_t)h;
+            if (h > 0) --h;
+        }
+    }
+}
+
+// ---- backward search (bwt.py:335-389), one pattern per lane
+struct FMView {
+    const uint8_t *bwt;
+    const int32_t *occ;
+    const int64_t *C;
+    const int64_t *tot;
+    const uint8_t *row;
+    int64_t n, olen;
+    int32_t k;
+};
+
+__device__ int64_t d_rank(const FMView &f, uint8_t c, int64_t pos) {
+    if (pos <= 0) return 0;
+    if (pos > f.n) pos = f.n;
+    const int64_t ci = pos / f.k, cpos = ci * f.k;
+    int64_t base = f.occ[(int64_t)f.row[c] * f.olen + ci];
+    for (int64_t i = cpos; i < pos; ++i) base += f.bwt[i] == c;
+    return base;
+}
+
+__global__ void k_bsearch(FMView f, const uint8_t *__restrict__ pats, const int64_t *__restrict__ off, int64_t np,
+                          int64_t *__restrict__ out) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= np) return;
+    const int64_t a = off[p], b = off[p + 1];
+    int64_t sp = -1, ep = -1;
+    if (b == a) {
+        sp = 0;
+        ep = f.n - 1;
+    } else {
+        uint8_t c = pats[b - 1];
+        if (f.tot[c] > 0) {
+            sp = f.C[c];
+            ep = sp + f.tot[c] - 1;
+            for (int64_t i = b - 2; i >= a; --i) {
+                c = pats[i];
+                if (f.tot[c] == 0) { sp = ep = -1; break; }
+                sp = f.C[c] + d_rank(f, c, sp);
+                ep = f.C[c] + d_rank(f, c, ep + 1) - 1;
+                if (sp > ep) { sp = ep = -1; break; }
+            }
+        }
+    }
+    out[2 * p] = sp;
+    out[2 * p + 1] = ep;
+}
+
+inline unsigned blocks(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+
+}  // namespace
+
+DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t sa_sample, int32_t occ_sample,
+                                uint32_t flags) {
+    auto *ix = new DeviceIndex();
+    hipStream_t st = c.stream;
+    ix->n = n;
+    ix->sa_sample = sa_sample;
+    ix->occ_sample = occ_sample;
+    ix->text.ensure((size_t)n + 128);
+    HIPCHECK(hipMemsetAsync(ix->text.p, 0, (size_t)n + 128, st));
+    if (n) HIPCHECK(hipMemcpyAsync(ix->text.p, d_text, (size_t)n, hipMemcpyDeviceToDevice, st));
+    const uint8_t *T = ix->text.as<uint8_t>();
+    // histogram -> alphabet, totals, C (bwt.py:129-134, 276-286)
+    c.slot[S_COUNTS].ensure(256 * 8);
+    HIPCHECK(hipMemsetAsync(c.slot[S_COUNTS].p, 0, 256 * 8, st));
+    if (n) hipLaunchKernelGGL(k_hist_bytes, dim3(1024), dim3(256), 0, st, T, n, c.slot[S_COUNTS].as<unsigned long long>());
+    unsigned long long h[256];
+    HIPCHECK(hipMemcpyAsync(h, c.slot[S_COUNTS].p, sizeof h, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    int64_t cum = 0;
+    uint8_t code[256] = {0}, present[256] = {0};
+    int sigma = 0;
+    std::memset(ix->code_of, 0, sizeof ix->code_of);
+    for (int b = 0; b < 256; ++b) {
+        ix->totals[b] = (int64_t)h[b];
+        ix->C[b] = cum;
+        cum += (int64_t)h[b];
+        if (h[b]) {
+            present[sigma] = (uint8_t)b;
+            ix->code_of[b] = (uint8_t)sigma;
+            code[b] = (uint8_t)(++sigma);   // 0 = past the end
+        }
+    }
+    ix->sigma = sigma;
+    ix->sa.ensure((size_t)std::max<int64_t>(n, 1) * 4);
+    if (n == 0) return ix;
+
+    // ------------------------------------------------------------ suffix array
+    int b = 1;
+    while ((1 << b) < sigma + 1) ++b;
+    const int k = 64 / b;
+    c.slot[S_IDX0].ensure((size_t)n * 8);    // keys
+    c.slot[S_IDX1].ensure((size_t)n * 4);    // vals
+    c.slot[S_IDX2].ensure((size_t)n * 4);    // rank
+    c.slot[S_IDX3].ensure((size_t)(n + 1) * 4);  // head
+    c.slot[S_IDX4].ensure((size_t)(n + 1) * 4);  // scan / gid
+    c.slot[S_IDX5].ensure((size_t)(n + 1) * 4);  // gstart
+    c.slot[S_IDX6].ensure((size_t)(n + 1) * 4);  // flag
+    c.slot[S_IDX7].ensure((size_t)(n + 1) * 4);  // U (surviving SA slots)
+    c.slot[S_MISC2].ensure((size_t)(n + 1) * 4); // next U
+    c.slot[S_MISC3].ensure(256);
+    uint64_t *keys = c.slot[S_IDX0].as<uint64_t>();
+    uint32_t *vals = c.slot[S_IDX1].as<uint32_t>();
+    uint32_t *rank = c.slot[S_IDX2].as<uint32_t>();
+    uint32_t *head = c.slot[S_IDX3].as<uint32_t>();
+    uint32_t *gid = c.slot[S_IDX4].as<uint32_t>();
+    uint32_t *gstart = c.slot[S_IDX5].as<uint32_t>();
+    uint32_t *flag = c.slot[S_IDX6].as<uint32_t>();
+    uint32_t *U = c.slot[S_IDX7].as<uint32_t>();
+    uint32_t *U2 = c.slot[S_MISC2].as<uint32_t>();
+    uint32_t *SA = ix->sa.as<uint32_t>();
+    HIPCHECK(hipMemcpyAsync(c.slot[S_MISC3].p, code, 256, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_init_keys, dim3(blocks(n)), dim3(256), 0, st, T, n, c.slot[S_MISC3].as<uint8_t>(), b, k, keys,
+                       vals);
+    radix_sort_pairs32(c, keys, vals, n, 0, ((b * k + 7) / 8) * 8);
+    HIPCHECK(hipMemcpyAsync(SA, vals, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
+    auto group_ids = [&](int64_t m) {   // head -> gid (group index), uses flag as scratch
+        exclusive_scan<uint32_t>(c, head, flag, m);
+        hipLaunchKernelGGL(k_gid, dim3(blocks(m)), dim3(256), 0, st, flag, head, m, gid);
+    };
+    hipLaunchKernelGGL(k_heads, dim3(blocks(n)), dim3(256), 0, st, keys, n, head);
+    group_ids(n);
+    hipLaunchKernelGGL(k_rank0, dim3(blocks(n)), dim3(256), 0, st, head, gid, SA, n, gstart, rank, flag, 0);
+    hipLaunchKernelGGL(k_rank0, dim3(blocks(n)), dim3(256), 0, st, head, gid, SA, n, gstart, rank, flag, 1);
+    // U = SA slots in groups of size >= 2
+    auto compact = [&](int64_t m, const uint32_t *src, uint32_t *dst) -> int64_t {
+        exclusive_scan<uint32_t>(c, flag, head, m);   // head reused as positions
+        uint32_t lastp = 0, lastf = 0;
+        HIPCHECK(hipMemcpyAsync(&lastp, head + m - 1, 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(&lastf, flag + m - 1, 4, hipMemcpyDeviceToHost, st));
+        hipLaunchKernelGGL(k_compact_idx, dim3(blocks(m)), dim3(256), 0, st, flag, head, m, dst, src);
+        HIPCHECK(hipStreamSynchronize(st));
+        return (int64_t)lastp + lastf;
+    };
+    int64_t m = compact(n, nullptr, U);
+    int nb = 1;
+    while ((1ll << nb) <= n) ++nb;   // rank + 1 <= n fits in nb bits
+    int64_t hlen = k;
+    while (m > 0) {
+        hipLaunchKernelGGL(k_round_keys, dim3(blocks(m)), dim3(256), 0, st, U, m, SA, rank, n, hlen, nb, keys, vals);
+        radix_sort_pairs32(c, keys, vals, m, 0, ((2 * nb + 7) / 8) * 8);
+        hipLaunchKernelGGL(k_heads, dim3(blocks(m)), dim3(256), 0, st, keys, m, head);
+        group_ids(m);
+        hipLaunchKernelGGL(k_round_apply, dim3(blocks(m)), dim3(256), 0, st, U, m, vals, head, gid, SA, gstart, 0,
+                           rank, flag);
+        hipLaunchKernelGGL(k_round_apply, dim3(blocks(m)), dim3(256), 0, st, U, m, vals, head, gid, SA, gstart, 1,
+                           rank, flag);
+        m = compact(m, U, U2);
+        std::swap(U, U2);
+        hlen *= 2;
+        if (hlen > 4 * n + 64) fail(BWTMI_E_STATE, "suffix array doubling did not converge");
+    }
+    HIPCHECK(hipGetLastError());
+
+    // ------------------------------------------------------------ BWT, Occ, sampled SA
+    ix->bwt.ensure((size_t)n + 128);
+    HIPCHECK(hipMemsetAsync(ix->bwt.p, 0, (size_t)n + 128, st));
+    hipLaunchKernelGGL(k_bwt, dim3(blocks(n)), dim3(256), 0, st, T, SA, n, ix->bwt.as<uint8_t>());
+    const int64_t nblk = (n + occ_sample - 1) / occ_sample;
+    ix->occ_len = 1 + n / occ_sample + (n % occ_sample != 0);   // == nblk + 1
+    ix->occ.ensure((size_t)sigma * (nblk + 1) * 4);
+    HIPCHECK(hipMemsetAsync(ix->occ.p, 0, (size_t)sigma * (nblk + 1) * 4, st));
+    HIPCHECK(hipMemcpyAsync(c.slot[S_MISC3].p, present, 256, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_occ_blocks, dim3(blocks(nblk * 64)), dim3(256), 0, st, ix->bwt.as<uint8_t>(), n, nblk,
+                       occ_sample, c.slot[S_MISC3].as<uint8_t>(), sigma, ix->occ.as<uint32_t>());
+    for (int cc = 0; cc < sigma; ++cc) {
+        uint32_t *row = ix->occ.as<uint32_t>() + (int64_t)cc * (nblk + 1);
+        exclusive_scan<uint32_t>(c, row, row, nblk + 1);
+    }
+    ix->sampled_len = (n + sa_sample - 1) / sa_sample;
+    ix->sampled.ensure((size_t)ix->sampled_len * 4 + 4);
+    hipLaunchKernelGGL(k_sample, dim3(blocks(ix->sampled_len)), dim3(256), 0, st, SA, n, sa_sample,
+                       ix->sampled.as<int32_t>(), ix->sampled_len);
+
+    // ------------------------------------------------------------ 8-mer hash
+    const int K = 8;
+    if (!(flags & BWTMI_INDEX_NO_KMER) && n >= K) {
+        ix->has_kmer = true;
+        hipLaunchKernelGGL(k_kvalid, dim3(blocks(n)), dim3(256), 0, st, T, n, flag);
+        exclusive_scan<uint32_t>(c, flag, head, n);   // head = vpos
+        uint32_t vk = 0, vkf = 0, vlast = 0, vlastf = 0;
+        HIPCHECK(hipMemcpyAsync(&vk, head + K - 1, 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(&vkf, flag + K - 1, 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(&vlast, head + n - 1, 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(&vlastf, flag + n - 1, 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        const int64_t nvalid = (int64_t)vlast + vlastf;
+        const int64_t valid_first = (int64_t)vk + vkf;   // valid among the first K chars
+        const int first = valid_first == K ? 1 : 0;
+        const int64_t nent = first + (nvalid - valid_first);
+        uint8_t *V = (uint8_t *)gid;   // reuse: nvalid bytes <= 4n
+        hipLaunchKernelGGL(k_kcompact, dim3(blocks(n)), dim3(256), 0, st, T, n, head, V);
+        ix->kmer_pos.ensure((size_t)std::max<int64_t>(nent, 1) * 4);
+        if (nent > 0) {
+            hipLaunchKernelGGL(k_kentries, dim3(blocks(n)), dim3(256), 0, st, T, n, K, head, V, first, keys,
+                               ix->kmer_pos.as<uint32_t>(), (uint32_t)valid_first);
+            radix_sort_pairs32(c, keys, ix->kmer_pos.as<uint32_t>(), nent, 0, 16);
+        }
+        ix->kmer_off.ensure((size_t)(65537) * 8);
+        c.slot[S_MISC0].ensure(65537 * 8);
+        uint32_t *kh = c.slot[S_MISC0].as<uint32_t>();
+        HIPCHECK(hipMemsetAsync(kh, 0, 65537 * 4, st));
+        if (nent > 0) hipLaunchKernelGGL(k_khist, dim3(blocks(nent)), dim3(256), 0, st, keys, nent, kh);
+        std::vector<uint32_t> hh(65537);
+        HIPCHECK(hipMemcpyAsync(hh.data(), kh, 65537 * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        std::vector<int64_t> offs(65537);
+        int64_t s = 0;
+        for (int q = 0; q < 65536; ++q) { offs[q] = s; s += hh[q]; }
+        offs[65536] = s;
+        HIPCHECK(hipMemcpyAsync(ix->kmer_off.p, offs.data(), 65537 * 8, hipMemcpyHostToDevice, st));
+        ix->kmer_count = nent;
+    }
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(st));
+    return ix;
+}
+
+void index_free(DeviceIndex *ix) {
+    if (!ix) return;
+    (void)hipDeviceSynchronize();
+    ix->text.release();
+    ix->sa.release();
+    ix->bwt.release();
+    ix->occ.release();
+    ix->sampled.release();
+    ix->kmer_off.release();
+    ix->kmer_pos.release();
+    delete ix;
+}
+
+int64_t index_n(const DeviceIndex *ix) { return ix->n; }
+int64_t index_occ_len(const DeviceIndex *ix) { return ix->n ? ix->occ_len : 0; }
+int64_t index_sampled_len(const DeviceIndex *ix) { return ix->sampled_len; }
+int64_t index_kmer_count(const DeviceIndex *ix) { return ix->kmer_count; }
+
+void index_get_sa(Ctx &c, const DeviceIndex *ix, int32_t *out) {
+    if (ix->n) HIPCHECK(hipMemcpy(out, ix->sa.p, (size_t)ix->n * 4, hipMemcpyDeviceToHost));
+}
+void index_get_bwt(Ctx &c, const DeviceIndex *ix, uint8_t *out) {
+    if (ix->n) HIPCHECK(hipMemcpy(out, ix->bwt.p, (size_t)ix->n, hipMemcpyDeviceToHost));
+}
+void index_get_counts(const DeviceIndex *ix, int64_t *totals, int64_t *C) {
+    std::memcpy(totals, ix->totals, sizeof ix->totals);
+    std::memcpy(C, ix->C, sizeof ix->C);
+}
+void index_get_occ(Ctx &c, const DeviceIndex *ix, uint8_t code, int32_t *out) {
+    const int64_t len = index_occ_len(ix);
+    if (!len) return;
+    if (!ix->totals[code]) {   // absent alphabet codes read as zeros (bwt.py:318-325)
+        std::memset(out, 0, (size_t)len * 4);
+        return;
+    }
+    HIPCHECK(hipMemcpy(out, ix->occ.as<int32_t>() + (int64_t)ix->code_of[code] * len, (size_t)len * 4,
+                       hipMemcpyDeviceToHost));
+}
+void index_get_sampled(Ctx &c, const DeviceIndex *ix, int32_t *out) {
+    if (ix->sampled_len) HIPCHECK(hipMemcpy(out, ix->sampled.p, (size_t)ix->sampled_len * 4, hipMemcpyDeviceToHost));
+}
+void index_get_kmer(Ctx &c, const DeviceIndex *ix, int64_t *offsets, int32_t *pos) {
+    if (!ix->has_kmer) {
+        std::memset(offsets, 0, 65537 * 8);
+        return;
+    }
+    HIPCHECK(hipMemcpy(offsets, ix->kmer_off.p, 65537 * 8, hipMemcpyDeviceToHost));
+    if (ix->kmer_count) HIPCHECK(hipMemcpy(pos, ix->kmer_pos.p, (size_t)ix->kmer_count * 4, hipMemcpyDeviceToHost));
+}
+
+void index_lcp(Ctx &c, DeviceIndex *ix, int32_t *out) {
+    const int64_t n = ix->n;
+    if (!n) return;
+    hipStream_t st = c.stream;
+    c.slot[S_MISC0].ensure((size_t)n * 4);
+    c.slot[S_MISC1].ensure((size_t)n * 4);
+    uint32_t *isa = c.slot[S_MISC0].as<uint32_t>();
+    int32_t *lcp = c.slot[S_MISC1].as<int32_t>();
+    HIPCHECK(hipMemsetAsync(lcp, 0, (size_t)n * 4, st));
+    hipLaunchKernelGGL(k_isa, dim3(blocks(n)), dim3(256), 0, st, ix->sa.as<uint32_t>(), n, isa);
+    uint32_t sa0 = 0;
+    HIPCHECK(hipMemcpyAsync(&sa0, ix->sa.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if ((int64_t)sa0 == n - 1) {
+        const int64_t chunk = 64;
+        const int64_t nch = (n + chunk - 1) / chunk;
+        hipLaunchKernelGGL(k_kasai, dim3(blocks(nch)), dim3(256), 0, st, ix->text.as<uint8_t>(),
+                           ix->sa.as<uint32_t>(), isa, n, chunk, lcp);
+    } else {
+        // the smallest suffix is not the last one (no unique final sentinel):
+        // Kasai's h then carries over the skipped rank-0 step, so replay it serially
+        hipLaunchKernelGGL(k_kasai_serial, dim3(1), dim3(64), 0, st, ix->text.as<uint8_t>(), ix->sa.as<uint32_t>(),
+                           isa, n, lcp);
+    }
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(out, lcp, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+}
+
+void index_backward_search(Ctx &c, DeviceIndex *ix, const uint8_t *pats, const int64_t *off, int64_t npat,
+                           int64_t *sp_ep) {
+    if (npat <= 0) return;
+    hipStream_t st = c.stream;
+    const int64_t plen = off[npat];
+    c.slot[S_MISC0].ensure((size_t)plen + 8);
+    c.slot[S_MISC1].ensure((size_t)(npat + 1) * 8);
+    c.slot[S_MISC2].ensure((size_t)npat * 16);
+    c.slot[S_MISC3].ensure(256 * 8 * 2 + 256);
+    if (plen) HIPCHECK(hipMemcpyAsync(c.slot[S_MISC0].p, pats, (size_t)plen, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemcpyAsync(c.slot[S_MISC1].p, off, (size_t)(npat + 1) * 8, hipMemcpyHostToDevice, st));
+    int64_t *tabs = c.slot[S_MISC3].as<int64_t>();
+    HIPCHECK(hipMemcpyAsync(tabs, ix->C, 256 * 8, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemcpyAsync(tabs + 256, ix->totals, 256 * 8, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemcpyAsync(tabs + 512, ix->code_of, 256, hipMemcpyHostToDevice, st));
+    FMView f;
+    f.bwt = ix->bwt.as<uint8_t>();
+    f.occ = ix->occ.as<int32_t>();
+    f.C = tabs;
+    f.tot = tabs + 256;
+    f.row = (const uint8_t *)(tabs + 512);
+    f.n = ix->n;
+    f.olen = index_occ_len(ix);
+    f.k = ix->occ_sample;
+    hipLaunchKernelGGL(k_bsearch, dim3(blocks(npat)), dim3(256), 0, st, f, c.slot[S_MISC0].as<uint8_t>(),
+                       c.slot[S_MISC1].as<int64_t>(), npat, c.slot[S_MISC2].as<int64_t>());
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(sp_ep, c.slot[S_MISC2].p, (size_t)npat * 16, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+}
+
+}  // namespace bwtmi

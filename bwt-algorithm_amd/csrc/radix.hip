@@ -1,0 +1,231 @@
+// radix.hip -- hand-written device primitives for gfx950: exclusive scan and a
+// stable LSD radix sort (8-bit digits) over 64-bit keys with 32/64-bit values.
+//
+// Radix pass = three launches:
+//   hist    : one workgroup per 4096-key tile, LDS histogram -> counts[d][tile]
+//   scan    : exclusive scan of counts (digit-major) -> global offsets
+//   scatter : each of the 4 waves owns 1024 consecutive keys of the tile; it
+//             ranks keys of equal digit with 8 ballots (wave64 match-any) in
+//             index order, so the pass is stable; per-wave digit bases come
+//             from the scanned offsets + the preceding waves' histograms.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "device.h"
+
+namespace bwtmi {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kItems = 16;
+constexpr int kTile = kBlock * kItems;  // 4096
+constexpr int kWaves = kBlock / 64;
+
+// ------------------------------------------------------------------ scan
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_chunk_sums(const T *__restrict__ in, T *__restrict__ sums, int64_t n) {
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    T s = 0;
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
+        if (idx < n) s += in[idx];
+    }
+    __shared__ T red[kBlock];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = kBlock / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) sums[blockIdx.x] = red[0];
+}
+
+template <class T>
+__device__ inline T wave_incl_scan(T v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        T u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    return v;
+}
+
+// exclusive scan of one chunk, adding offs[blockIdx.x] (exclusive chunk prefix)
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_chunk_scan(const T *__restrict__ in, T *__restrict__ out,
+                                                       const T *__restrict__ offs, int64_t n) {
+    __shared__ T buf[kTile];
+    __shared__ T wsum[kWaves];
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
+        buf[i * kBlock + threadIdx.x] = idx < n ? in[idx] : (T)0;
+    }
+    __syncthreads();
+    T loc[kItems];
+    T s = 0;
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        loc[i] = s;
+        s += buf[threadIdx.x * kItems + i];
+    }
+    const T inc = wave_incl_scan<T>(s);
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    T wpre = 0;
+    for (int w = 0; w < wv; ++w) wpre += wsum[w];
+    const T excl = inc - s + wpre + (offs ? offs[blockIdx.x] : (T)0);
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) buf[threadIdx.x * kItems + i] = loc[i] + excl;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
+        if (idx < n) out[idx] = buf[i * kBlock + threadIdx.x];
+    }
+}
+
+// ------------------------------------------------------------------ radix
+__global__ __launch_bounds__(kBlock) void k_hist(const uint64_t *__restrict__ keys, uint32_t *__restrict__ counts,
+                                                 int64_t n, int shift, int64_t ntiles) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
+        if (idx < n) atomicAdd(&h[(keys[idx] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    counts[(int64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+template <class V>
+__global__ __launch_bounds__(kBlock) void k_scatter(const uint64_t *__restrict__ kin, const V *__restrict__ vin,
+                                                    uint64_t *__restrict__ kout, V *__restrict__ vout,
+                                                    const uint32_t *__restrict__ offs, int64_t n, int shift,
+                                                    int64_t ntiles) {
+    __shared__ uint32_t whist[kWaves][256];
+    __shared__ uint32_t woff[kWaves][256];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int w = 0; w < kWaves; ++w) whist[w][threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t wbase = (int64_t)blockIdx.x * kTile + (int64_t)wv * (kItems * 64);
+    uint64_t k[kItems];
+    V v[kItems];
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        const int64_t idx = wbase + i * 64 + lane;
+        if (idx < n) {
+            k[i] = kin[idx];
+            if (vin) v[i] = vin[idx];
+            atomicAdd(&whist[wv][(k[i] >> shift) & 255u], 1u);
+        }
+    }
+    __syncthreads();
+    {
+        uint32_t b = offs[(int64_t)threadIdx.x * ntiles + blockIdx.x];
+        for (int w = 0; w < kWaves; ++w) {
+            woff[w][threadIdx.x] = b;
+            b += whist[w][threadIdx.x];
+        }
+    }
+    __syncthreads();
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        const int64_t idx = wbase + i * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t d = valid ? (uint32_t)((k[i] >> shift) & 255u) : 0u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bt = 0; bt < 8; ++bt) {
+            const bool bit = (d >> bt) & 1u;
+            const uint64_t bal = __ballot(bit);
+            peers &= bit ? bal : ~bal;
+        }
+        uint32_t pos = 0;
+        if (valid) pos = woff[wv][d] + (uint32_t)__popcll(peers & lt);
+        __builtin_amdgcn_wave_barrier();
+        if (valid && (peers & lt) == 0) woff[wv][d] += (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        if (valid) {
+            kout[pos] = k[i];
+            if (vout) vout[pos] = v[i];
+        }
+    }
+}
+
+template <class V>
+void radix_sort_impl(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int bit1) {
+    if (n <= 1) return;
+    const int64_t ntiles = (n + kTile - 1) / kTile;
+    c.slot[S_SORT_TMP0].ensure((size_t)n * sizeof(uint64_t));
+    if (vals) c.slot[S_SORT_TMP1].ensure((size_t)n * sizeof(V));
+    c.slot[S_SORT_HIST].ensure((size_t)ntiles * 256 * sizeof(uint32_t));
+    uint64_t *ka = keys, *kb = c.slot[S_SORT_TMP0].as<uint64_t>();
+    V *va = vals, *vb = vals ? c.slot[S_SORT_TMP1].as<V>() : nullptr;
+    uint32_t *cnt = c.slot[S_SORT_HIST].as<uint32_t>();
+    int passes = 0;
+    for (int sh = bit0; sh < bit1; sh += 8) {
+        hipLaunchKernelGGL(k_hist, dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream, ka, cnt, n, sh, ntiles);
+        exclusive_scan<uint32_t>(c, cnt, cnt, ntiles * 256);
+        hipLaunchKernelGGL(k_scatter<V>, dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream, ka, va, kb, vb, cnt, n,
+                           sh, ntiles);
+        std::swap(ka, kb);
+        std::swap(va, vb);
+        ++passes;
+    }
+    HIPCHECK(hipGetLastError());
+    if (passes & 1) {
+        HIPCHECK(hipMemcpyAsync(keys, ka, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToDevice, c.stream));
+        if (vals) HIPCHECK(hipMemcpyAsync(vals, va, (size_t)n * sizeof(V), hipMemcpyDeviceToDevice, c.stream));
+    }
+}
+
+}  // namespace
+
+template <class T>
+static void scan_rec(Ctx &c, const T *in, T *out, int64_t n, T *tmp) {
+    const int64_t nch = (n + kTile - 1) / kTile;
+    if (nch == 1) {
+        hipLaunchKernelGGL(k_chunk_scan<T>, dim3(1), dim3(kBlock), 0, c.stream, in, out, (const T *)nullptr, n);
+        return;
+    }
+    T *sums = tmp;
+    hipLaunchKernelGGL(k_chunk_sums<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, sums, n);
+    scan_rec<T>(c, sums, sums, nch, tmp + nch);
+    hipLaunchKernelGGL(k_chunk_scan<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, out, (const T *)sums, n);
+}
+
+template <class T>
+void exclusive_scan(Ctx &c, const T *in, T *out, int64_t n) {
+    if (n <= 0) return;
+    int64_t need = 0;
+    for (int64_t m = n; m > kTile;) {
+        m = (m + kTile - 1) / kTile;
+        need += m;
+    }
+    c.slot[S_SCAN_TMP].ensure((size_t)(need + 1) * sizeof(T));
+    scan_rec<T>(c, in, out, n, c.slot[S_SCAN_TMP].as<T>());
+    HIPCHECK(hipGetLastError());
+}
+
+template void exclusive_scan<uint32_t>(Ctx &, const uint32_t *, uint32_t *, int64_t);
+template void exclusive_scan<uint64_t>(Ctx &, const uint64_t *, uint64_t *, int64_t);
+template void exclusive_scan<int64_t>(Ctx &, const int64_t *, int64_t *, int64_t);
+
+void radix_sort_pairs(Ctx &c, uint64_t *keys, uint64_t *vals, int64_t n, int bit0, int bit1) {
+    radix_sort_impl<uint64_t>(c, keys, vals, n, bit0, bit1);
+}
+void radix_sort_pairs32(Ctx &c, uint64_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1) {
+    radix_sort_impl<uint32_t>(c, keys, vals, n, bit0, bit1);
+}
+
+}  // namespace bwtmi

@@ -1,0 +1,422 @@
+// render.cpp -- compound detection and the five output writers
+// (TandemRepeatFinder.save_results bwt.py:4141-4198, _detect_compound_repeats
+// 3995-4139, _simple_kmer_scan 3956-3993, TandemRepeat.to_* 454-641).
+// Python's "{x:.Nf}" and C's "%.Nf" both print the exact binary value rounded
+// half-to-even, so numeric columns are byte-identical.
+#include <algorithm>
+#include <chrono>
+#include <cinttypes>
+#include <cmath>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+namespace bwtmi {
+namespace {
+
+struct View {
+    const char *p = nullptr;
+    int64_t n = 0;
+    bool empty() const { return n <= 0; }
+};
+
+View act_of(const Job &job, const Rec &r) {
+    View v;
+    if (r.act_kind == ACT_NONE) return v;
+    const Contig &c = job.contigs[(size_t)r.chrom];
+    v.p = (r.act_kind == ACT_FULL ? c.full.data() : c.trimmed()) + r.act_off;
+    v.n = r.act_len;
+    return v;
+}
+
+Rec kmer_piece(int32_t chrom, int64_t start, int64_t end, const std::string &motif, int64_t copies,
+               int32_t tier, int8_t kind, int64_t off, int64_t len) {
+    Rec r;
+    r.chrom = chrom;
+    r.start = start;
+    r.end = end;
+    r.length = end - start;
+    r.motif = motif;
+    r.copies = (double)copies;
+    r.tier = tier;
+    r.confidence = 1.0;
+    r.mismatch_rate = 0.0;
+    r.max_mm = 0;
+    r.n_eval = copies;
+    r.strand = '+';
+    r.pmatch = 100.0;
+    r.pindel = 0.0;
+    r.score = 100;
+    r.kmer_stats = true;
+    r.act_kind = kind;
+    r.act_off = off;
+    r.act_len = len;
+    return r;
+}
+
+// _simple_kmer_scan(chrom, start, end, k=3, use_full_seq=True)
+void kmer_scan(const Job &job, int32_t chrom, int64_t start, int64_t end, std::vector<Rec> &out) {
+    const std::string &seq = job.contigs[(size_t)chrom].full;
+    const int64_t L = (int64_t)seq.size();
+    const int64_t k = 3;
+    if (seq.empty() || start >= end || start < 0 || end > L) return;
+    const char *reg = seq.data() + start;
+    const int64_t rl = end - start;
+    int64_t i = 0;
+    while (i < rl - k) {
+        int64_t c = 1, j = i + k;
+        while (j + k <= rl && std::memcmp(reg + j, reg + i, (size_t)k) == 0) {
+            ++c;
+            j += k;
+        }
+        if (c >= 5) {
+            out.push_back(kmer_piece(chrom, start + i, start + j, std::string(reg + i, (size_t)k), c, 1,
+                                     ACT_FULL, start + i, j - i));
+            i = j;
+        } else {
+            ++i;
+        }
+    }
+}
+
+struct Compound {
+    std::vector<Rec> result;
+    std::vector<Rec> partners;
+};
+
+// _detect_compound_repeats (bwt.py:3995-4139) over the final records
+Compound detect_compounds(const Job &job, const std::vector<Rec> &recs) {
+    Compound out;
+    std::vector<int32_t> chrom_order;
+    std::vector<std::vector<Rec>> by(job.contigs.size());
+    for (const Rec &r : recs) {
+        if (by[(size_t)r.chrom].empty()) chrom_order.push_back(r.chrom);
+        by[(size_t)r.chrom].push_back(r);
+    }
+    for (int32_t ch : chrom_order) {
+        const std::string &full = job.contigs[(size_t)ch].full;
+        if (full.empty()) continue;
+        std::vector<Rec> &lst = by[(size_t)ch];
+        const size_t n0 = lst.size();
+        for (size_t q = 0; q < n0; ++q) {
+            const Rec r = lst[q];
+            if (!r.motif.empty() && r.motif.size() == 3) {
+                const int64_t a = r.end, b = std::min<int64_t>((int64_t)full.size(), r.end + 50);
+                if (a < b) {
+                    std::vector<Rec> kr;
+                    kmer_scan(job, ch, a, b, kr);
+                    for (auto &x : kr)
+                        if (x.motif != r.motif) lst.push_back(std::move(x));
+                }
+            }
+        }
+    }
+    for (int32_t ch : chrom_order) {
+        std::vector<Rec> &rs = by[(size_t)ch];
+        std::stable_sort(rs.begin(), rs.end(), [](const Rec &a, const Rec &b) { return a.start < b.start; });
+        struct Long { int64_t s, e; };
+        std::vector<Long> longs;
+        for (auto &r : rs)
+            if (r.motif.size() > 10) longs.push_back({r.start, r.end});
+        const Contig &ctg = job.contigs[(size_t)ch];
+        const int64_t TL = ctg.trimmed_len();
+        const char *tseq = ctg.trimmed();
+        size_t i = 0;
+        while (i < rs.size()) {
+            Rec &cur = rs[i];
+            if (cur.motif.size() == 3 && cur.copies >= 10 && TL > 0) {
+                // repeat_seq = sequences[chrom][cur.start:cur.end] (trimmed sequence, restored
+                // coordinates -- bwt.py:4045-4047)
+                const int64_t a = std::min(std::max<int64_t>(cur.start, 0), TL);
+                const int64_t b = std::max(a, std::min(std::max<int64_t>(cur.end, 0), TL));
+                const char *rsq = tseq + a;
+                const int64_t rl = b - a;
+                const int64_t k = 3;
+                for (int64_t sp = k; sp < rl - k; sp += k) {
+                    const int64_t l1 = std::min<int64_t>(k, rl), l2 = std::min<int64_t>(k, rl - sp);
+                    if (l1 == l2 && std::memcmp(rsq, rsq + sp, (size_t)l1) == 0) continue;
+                    int64_t c1 = 0;
+                    for (int64_t j = 0; j < sp; j += k) {
+                        const int64_t lj = std::min<int64_t>(k, rl - j);
+                        if (lj == l1 && std::memcmp(rsq + j, rsq, (size_t)l1) == 0) ++c1;
+                        else break;
+                    }
+                    int64_t c2 = 0;
+                    for (int64_t j = sp; j < rl; j += k) {
+                        const int64_t lj = std::min<int64_t>(k, rl - j);
+                        if (lj == l2 && std::memcmp(rsq + j, rsq + sp, (size_t)l2) == 0) ++c2;
+                        else break;
+                    }
+                    if (c1 >= 5 && c2 >= 5 && (double)(c1 * l1 + c2 * l2) >= (double)rl * 0.9) {
+                        const int64_t e1 = cur.start + c1 * l1;
+                        // actual = repeat_seq[:c1*l1], repeat_seq[c1*l1 : c1*l1 + c2*l2]
+                        const int64_t x1 = std::min(c1 * l1, rl);
+                        const int64_t y0 = std::min(c1 * l1, rl), y1 = std::max(y0, std::min(c1 * l1 + c2 * l2, rl));
+                        Rec r1 = kmer_piece(ch, cur.start, e1, std::string(rsq, (size_t)l1), c1, cur.tier,
+                                            ACT_TRIMMED, a, x1);
+                        Rec r2 = kmer_piece(ch, e1, e1 + c2 * l2, std::string(rsq + sp, (size_t)l2), c2,
+                                            cur.tier, ACT_TRIMMED, a + y0, y1 - y0);
+                        r1.is_compound = true;
+                        r1.partner = (int32_t)out.partners.size();
+                        out.partners.push_back(std::move(r2));
+                        out.result.push_back(std::move(r1));
+                        ++i;
+                    }
+                }
+            }
+            if (i + 1 < rs.size()) {
+                const Rec &nx = rs[i + 1];
+                const int64_t gap = nx.start - cur.end;
+                if (gap <= 5 && cur.motif.size() <= 4 && nx.motif.size() <= 4 && cur.motif != nx.motif &&
+                    cur.copies >= 5 && nx.copies >= 5) {
+                    const int64_t cs = cur.start, ce = nx.end;
+                    bool covered = false;
+                    for (auto &lm : longs) {
+                        const int64_t ov = std::max<int64_t>(0, std::min(ce, lm.e) - std::max(cs, lm.s));
+                        if ((double)ov / (double)(ce - cs) >= 0.8) { covered = true; break; }
+                    }
+                    if (!covered) {
+                        Rec c = cur;
+                        c.is_compound = true;
+                        c.partner = (int32_t)out.partners.size();
+                        out.partners.push_back(nx);
+                        out.result.push_back(std::move(c));
+                        i += 2;
+                        continue;
+                    }
+                }
+            }
+            out.result.push_back(cur);
+            ++i;
+        }
+    }
+    return out;
+}
+
+// ---------------------------------------------------------------- formatting
+struct Out {
+    std::string s;
+    void put(const char *p, int64_t n) { s.append(p, (size_t)n); }
+    void put(const std::string &x) { s.append(x); }
+    void put(View v) { if (v.n > 0) s.append(v.p, (size_t)v.n); }
+    void c(char ch) { s.push_back(ch); }
+    void f(const char *fmt, double x) {
+        char b[64];
+        int n = snprintf(b, sizeof b, fmt, x);
+        s.append(b, (size_t)n);
+    }
+    void i(int64_t x) {
+        char b[32];
+        int n = snprintf(b, sizeof b, "%" PRId64, x);
+        s.append(b, (size_t)n);
+    }
+    void rep(const std::string &m, int64_t times) {
+        for (int64_t k = 0; k < times; ++k) s.append(m);
+    }
+};
+
+inline int64_t py_round(double x) { return (int64_t)std::nearbyint(x); }
+
+void comp_entropy(const Rec &r, double comp[4], double &ent) {
+    if (r.kmer_stats) {
+        comp[0] = comp[1] = comp[2] = comp[3] = 0.0;
+        ent = 1.5;
+        return;
+    }
+    composition_of(r.motif.data(), (int64_t)r.motif.size(), comp);
+    ent = entropy_of(r.motif.data(), (int64_t)r.motif.size());
+}
+
+void row_strfinder(Out &o, const Job &job, const Rec &r, const Rec *partner) {
+    const Contig &c = job.contigs[(size_t)r.chrom];
+    const std::string &full = c.full;
+    const int64_t FL = (int64_t)full.size();
+    View fl, fr;
+    if (!full.empty()) {   // full[max(0,start-30):start], full[end:end+30]
+        int64_t a = std::min(std::max<int64_t>(0, r.start - 30), FL), b = std::min(std::max<int64_t>(r.start, 0), FL);
+        if (b > a) { fl.p = full.data() + a; fl.n = b - a; }
+        a = std::min(std::max<int64_t>(r.end, 0), FL);
+        b = std::min(std::max<int64_t>(r.end + 30, 0), FL);
+        if (b > a) { fr.p = full.data() + a; fr.n = b - a; }
+    }
+    const bool flanks = !fl.empty() || !fr.empty();
+    o.put("STR_");
+    o.put(c.name);
+    o.c('\t');
+    if (partner) {
+        const Rec &p = *partner;
+        const int64_t k1 = py_round(r.copies), k2 = py_round(p.copies);
+        std::string core;
+        View a1 = act_of(job, r), a2 = act_of(job, p);
+        if (!a1.empty()) core.append(a1.p, (size_t)a1.n);
+        else for (int64_t k = 0; k < k1; ++k) core += r.motif;
+        if (!a2.empty()) core.append(a2.p, (size_t)a2.n);
+        else for (int64_t k = 0; k < k2; ++k) core += p.motif;
+        o.put(c.name); o.c(':'); o.i(r.start + 1); o.c('-'); o.i(p.end); o.c('\t');
+        o.c('['); o.put(r.motif); o.put("]n+["); o.put(p.motif); o.put("]n\t");
+        o.i((int64_t)r.motif.size()); o.c('['); o.put(r.motif); o.c(']'); o.i(k1); o.c(';');
+        o.i((int64_t)p.motif.size()); o.c('['); o.put(p.motif); o.c(']'); o.i(k2); o.put(",0\t");
+        o.i(k1); o.c('/'); o.i(k2); o.c('\t');
+        o.put(core); o.put("\t100%\t-\t");
+        o.i(k1); o.c(':'); o.i(k2); o.c('\t'); o.i(k1 + k2); o.c('\t');
+        if (flanks) { o.put(fl); o.put(core); o.put(fr); } else o.put(core);
+        o.put("\t-\n");
+        return;
+    }
+    const std::string &cons = r.motif;
+    const int64_t ml = (int64_t)cons.size();
+    const int64_t cc = (int64_t)std::floor(r.copies + 1e-6);
+    o.put(c.name); o.c(':'); o.i(r.start + 1); o.c('-'); o.i(r.end); o.c('\t');
+    o.c('['); o.put(cons); o.put("]n\t");
+    o.i(ml); o.c('['); o.put(cons); o.c(']'); o.i(cc); o.c(','); o.i((r.end - r.start) - ml * cc); o.c('\t');
+    if (std::fabs(r.copies - std::nearbyint(r.copies)) < 1e-6) {
+        o.i(py_round(r.copies));
+    } else {
+        char b[64];
+        snprintf(b, sizeof b, "%.2f", r.copies);
+        std::string g(b);
+        while (!g.empty() && g.back() == '0') g.pop_back();
+        while (!g.empty() && g.back() == '.') g.pop_back();
+        o.put(g);
+    }
+    o.c('\t');
+    std::string core_full;
+    View av = act_of(job, r);
+    if (!av.empty()) core_full.assign(av.p, (size_t)av.n);
+    else for (int64_t k = 0; k < (int64_t)r.copies; ++k) core_full += cons;
+    if ((int64_t)core_full.size() > 150) {
+        o.put(core_full.data(), 70);
+        o.put("... (x"); o.i(cc); o.c(')');
+    } else {
+        o.put(core_full);
+    }
+    o.c('\t');
+    o.f("%.0f", r.pmatch);
+    o.put("%\t-\t");
+    o.i(cc); o.c(':'); o.i(r.n_eval); o.c('\t'); o.i(r.n_eval); o.c('\t');
+    const int64_t tot = (flanks ? fl.n + fr.n : 0) + (int64_t)core_full.size();
+    if (tot > 500) {
+        std::string fc;
+        if (flanks) { fc.append(fl.p ? fl.p : "", (size_t)fl.n); fc += core_full; fc.append(fr.p ? fr.p : "", (size_t)fr.n); }
+        else fc = core_full;
+        o.put(fc.data(), 250);
+        o.put("...");
+        o.put(fc.data() + fc.size() - 200, 200);
+    } else {
+        if (flanks) { o.put(fl); o.put(core_full); o.put(fr); } else o.put(core_full);
+    }
+    o.c('\t');
+    if (!r.variations.empty()) o.put(r.variations); else o.c('-');
+    o.c('\n');
+}
+
+const char *kVcfHeader =
+    "##fileformat=VCFv4.2\n"
+    "##INFO=<ID=MOTIF,Number=1,Type=String,Description=\"Original seed motif\">\n"
+    "##INFO=<ID=CONS_MOTIF,Number=1,Type=String,Description=\"Consensus motif from all copies\">\n"
+    "##INFO=<ID=COPIES,Number=1,Type=Float,Description=\"Number of copies\">\n"
+    "##INFO=<ID=TIER,Number=1,Type=Integer,Description=\"Detection tier (1=short, 2=medium/long, 3=very long)\">\n"
+    "##INFO=<ID=CONF,Number=1,Type=Float,Description=\"Confidence score\">\n"
+    "##INFO=<ID=MM_RATE,Number=1,Type=Float,Description=\"Overall mismatch rate across all copies\">\n"
+    "##INFO=<ID=MAX_MM_PER_COPY,Number=1,Type=Integer,Description=\"Maximum mismatches in any single copy\">\n"
+    "##INFO=<ID=N_COPIES_EVAL,Number=1,Type=Integer,Description=\"Number of copies evaluated for consensus\">\n"
+    "##INFO=<ID=STRAND,Number=1,Type=String,Description=\"Strand of canonical motif (+/-)\">\n"
+    "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\n";
+
+}  // namespace
+
+std::string render(Job &job, int fmt) {
+    auto t0 = std::chrono::steady_clock::now();
+    job.assign_units();
+    Compound comp;
+    const std::vector<Rec> *rows = &job.final_recs;
+    if (fmt == BWTMI_FMT_STRFINDER) {
+        comp = detect_compounds(job, job.final_recs);
+        rows = &comp.result;
+    }
+    std::vector<uint32_t> order(rows->size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = (uint32_t)i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        const Rec &x = (*rows)[a], &y = (*rows)[b];
+        const int32_t ux = job.contigs[(size_t)x.chrom].unit, uy = job.contigs[(size_t)y.chrom].unit;
+        if (ux != uy) return ux < uy;
+        if (x.start != y.start) return x.start < y.start;
+        return x.end < y.end;
+    });
+    Out o;
+    o.s.reserve(order.size() * 160 + 1024);
+    double cp[4], ent;
+    switch (fmt) {
+        case BWTMI_FMT_BED:
+            o.put("# Tandem Repeats (BED format with imperfect repeat support)\n");
+            o.put("# chrom\tstart\tend\tconsensus_motif\tcopies\ttier\tmismatch_rate\tstrand\n");
+            for (uint32_t k : order) {
+                const Rec &r = (*rows)[k];
+                o.put(job.contigs[(size_t)r.chrom].name); o.c('\t'); o.i(r.start); o.c('\t'); o.i(r.end); o.c('\t');
+                o.put(r.motif); o.c('\t'); o.f("%.1f", r.copies); o.c('\t'); o.i(r.tier); o.c('\t');
+                o.f("%.3f", r.mismatch_rate); o.c('\t'); o.c(r.strand); o.c('\n');
+            }
+            break;
+        case BWTMI_FMT_VCF: {
+            o.put(kVcfHeader);
+            int64_t idx = 0;
+            for (uint32_t k : order) {
+                const Rec &r = (*rows)[k];
+                o.put(job.contigs[(size_t)r.chrom].name); o.c('\t'); o.i(r.start + 1); o.put("\tTR"); o.i(idx++);
+                o.put("\t.\t<TR>\t.\tPASS\tMOTIF="); o.put(r.motif); o.put(";CONS_MOTIF="); o.put(r.motif);
+                o.put(";COPIES="); o.f("%.1f", r.copies); o.put(";TIER="); o.i(r.tier);
+                o.put(";CONF="); o.f("%.2f", r.confidence); o.put(";MM_RATE="); o.f("%.3f", r.mismatch_rate);
+                o.put(";MAX_MM_PER_COPY="); o.i(r.max_mm); o.put(";N_COPIES_EVAL="); o.i(r.n_eval);
+                o.put(";STRAND="); o.c(r.strand); o.c('\n');
+            }
+            break;
+        }
+        case BWTMI_FMT_TRF_TABLE:
+            o.put("# Tandem Repeats Finder Compatible Table Format\n");
+            o.put("# Indices\tPeriod\tCopyNumber\tConsensusSize\tPercentMatches\tPercentIndels\t");
+            o.put("Score\tA\tC\tG\tT\tEntropy\n");
+            for (uint32_t k : order) {
+                const Rec &r = (*rows)[k];
+                comp_entropy(r, cp, ent);
+                const int64_t ml = (int64_t)r.motif.size();
+                o.i(r.start); o.put("--"); o.i(r.end); o.c('\t'); o.i(ml); o.c('\t'); o.f("%.1f", r.copies);
+                o.c('\t'); o.i(ml); o.c('\t'); o.f("%.0f", r.pmatch); o.c('\t'); o.f("%.0f", r.pindel); o.c('\t');
+                o.i(r.score); o.c('\t'); o.f("%.0f", cp[0]); o.c('\t'); o.f("%.0f", cp[1]); o.c('\t');
+                o.f("%.0f", cp[2]); o.c('\t'); o.f("%.0f", cp[3]); o.c('\t'); o.f("%.2f", ent); o.c('\n');
+            }
+            break;
+        case BWTMI_FMT_TRF_DAT:
+            for (uint32_t k : order) {
+                const Rec &r = (*rows)[k];
+                comp_entropy(r, cp, ent);
+                const int64_t ml = (int64_t)r.motif.size();
+                o.i(r.start); o.c(' '); o.i(r.end); o.c(' '); o.i(ml); o.c(' '); o.f("%.1f", r.copies); o.c(' ');
+                o.i(ml); o.c(' '); o.f("%.0f", r.pmatch); o.c(' '); o.f("%.0f", r.pindel); o.c(' ');
+                o.i(r.score); o.c(' '); o.f("%.0f", cp[0]); o.c(' '); o.f("%.0f", cp[1]); o.c(' ');
+                o.f("%.0f", cp[2]); o.c(' '); o.f("%.0f", cp[3]); o.c(' '); o.f("%.2f", ent); o.c(' ');
+                o.put(r.motif); o.c(' ');
+                View av = act_of(job, r);
+                if (!av.empty()) o.put(av); else o.rep(r.motif, (int64_t)r.copies);
+                o.c('\n');
+            }
+            break;
+        case BWTMI_FMT_STRFINDER:
+            o.put("STR_marker\tSTR_position\tSTR_motif\tSTR_genotype_structure\tSTR_genotype\t");
+            o.put("STR_core_seq\tAllele_coverage\tAlleles_ratio\tReads_Distribution(consensused)\t");
+            o.put("STR_depth\tFull_seq\tVariations\n");
+            for (uint32_t k : order) {
+                const Rec &r = (*rows)[k];
+                const Rec *p = (r.is_compound && r.partner >= 0) ? &comp.partners[(size_t)r.partner] : nullptr;
+                row_strfinder(o, job, r, p);
+            }
+            break;
+        default:
+            fail(BWTMI_E_ARG, "unknown output format %d", fmt);
+    }
+    job.stage_ms[6] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return std::move(o.s);
+}
+
+}  // namespace bwtmi

@@ -1,0 +1,473 @@
+// strict_scan.hip -- exact adjacent-copy tandem scan on gfx950.
+//
+// Replaces Tier2LCPFinder.find_long_unit_repeats_strict (bwt.py:1891-2001)
+// with max_mismatch = 0.  For one unit length L the reference's while-loop is
+// equivalent to a run formulation:
+//   M_L[j] = (t[j] == t[j+L]), j < n-L; for each maximal 1-run [s,e) in
+//   position order, i = max(s, carry); if e - i >= (min_copies-1)*L emit
+//   count = 1 + (e-i)/L and set carry = i + count*L.
+// Kernel pipeline (one launch each, all on the ctx stream):
+//   k_pack       bytes -> B-bit codes (B = 2/4/8 from the contig's alphabet),
+//                64-bit words, coalesced
+//   k_runs       grid (word tiles x L chunks): every lane owns 32 positions of
+//                one L; equality masks by XOR of packed windows, neighbour
+//                masks by wave shuffles; emits the maximal runs long enough
+//                to hold min_copies copies (candidates)
+//   radix sort   candidates by (L desc, s asc) -- the reference order
+//   k_resolve    chains of candidates closer than L (where carry can act) are
+//                walked by their head lane; all others resolve independently
+//   scan+compact hits in candidate order
+//   k_period     smallest divisor period of the first unit per hit
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <vector>
+
+#include "device.h"
+
+namespace bwtmi {
+namespace {
+
+constexpr uint32_t FULL = 0xFFFFFFFFu;
+
+// ------------------------------------------------------------------ pack
+template <int B>
+__global__ __launch_bounds__(256) void k_pack(const uint8_t *__restrict__ text, int64_t n,
+                                              const uint8_t *__restrict__ code, uint64_t *__restrict__ P,
+                                              int64_t nwords) {
+    constexpr int S = 64 / B;
+    __shared__ uint8_t cmap[256];
+    cmap[threadIdx.x] = code[threadIdx.x];
+    __syncthreads();
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwords) return;
+    const int64_t j0 = w * S;
+    uint64_t x = 0;
+    if (j0 + S <= n) {
+        // aligned vector loads of S bytes
+        uint64_t lo = 0;
+#pragma unroll
+        for (int q = 0; q < S / 8; ++q) {
+            const uint64_t v = *reinterpret_cast<const uint64_t *>(text + j0 + 8 * q);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) lo |= (uint64_t)cmap[(v >> (8 * b)) & 255u] << ((8 * q + b) * B);
+        }
+        x = lo;
+    } else {
+        for (int k = 0; k < S; ++k)
+            if (j0 + k < n) x |= (uint64_t)cmap[text[j0 + k]] << (k * B);
+    }
+    P[w] = x;
+}
+
+// 64-bit window of symbols j .. j+S-1
+template <int B>
+__device__ __forceinline__ uint64_t window(const uint64_t *__restrict__ P, int64_t j) {
+    constexpr int S = 64 / B;
+    const int64_t q = j / S;
+    const int r = (int)(j - q * S) * B;
+    const uint64_t lo = P[q];
+    if (r == 0) return lo;
+    return (lo >> r) | (P[q + 1] << (64 - r));
+}
+
+// per-symbol equality of two windows -> dense mask of S bits
+template <int B>
+__device__ __forceinline__ uint32_t eqbits(uint64_t a, uint64_t b) {
+    uint64_t x = a ^ b;
+    if constexpr (B == 2) {
+        x = ~(x | (x >> 1)) & 0x5555555555555555ull;
+        x = (x | (x >> 1)) & 0x3333333333333333ull;
+        x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+        x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+        x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+        x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+        return (uint32_t)x;
+    } else if constexpr (B == 4) {
+        x = ~(x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x1111111111111111ull;
+        x = (x | (x >> 3)) & 0x0303030303030303ull;
+        x = (x | (x >> 6)) & 0x000F000F000F000Full;
+        x = (x | (x >> 12)) & 0x000000FF000000FFull;
+        x = (x | (x >> 24)) & 0x000000000000FFFFull;
+        return (uint32_t)x;
+    } else {
+        uint64_t t = (x & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full;
+        t = ~(t | x | 0x7F7F7F7F7F7F7F7Full);  // 0x80 in every zero byte
+        x = (t >> 7) & 0x0101010101010101ull;
+        x = (x | (x >> 7)) & 0x0003000300030003ull;
+        x = (x | (x >> 14)) & 0x0000000F0000000Full;
+        x = (x | (x >> 28)) & 0xFFull;
+        return (uint32_t)x;
+    }
+}
+
+// M_L for positions 32w .. 32w+31 (bit k <-> position 32w+k)
+template <int B>
+__device__ __forceinline__ uint32_t eq32(const uint64_t *__restrict__ P, int64_t w, int64_t L, int64_t n) {
+    constexpr int S = 64 / B;
+    const int64_t j0 = w * 32;
+    const int64_t lim = n - L - j0;  // positions j0+k valid iff k < lim
+    if (w < 0 || lim <= 0) return 0u;
+    uint32_t m = 0;
+#pragma unroll
+    for (int h = 0; h < 32 / S; ++h) {
+        const int64_t j = j0 + h * S;
+        m |= eqbits<B>(P[j / S], window<B>(P, j + L)) << (h * S);
+    }
+    if (lim < 32) m &= (1u << lim) - 1u;
+    return m;
+}
+
+struct CandOut {
+    uint64_t *keys;
+    uint64_t *vals;
+    unsigned long long *count;
+    int64_t cap;
+    int32_t umax;
+};
+
+__device__ __forceinline__ void emit(const CandOut &o, int64_t L, int64_t s, int64_t e) {
+    const unsigned long long idx = atomicAdd(o.count, 1ull);
+    if ((int64_t)idx < o.cap) {
+        o.keys[idx] = ((uint64_t)(o.umax - L) << 40) | (uint64_t)s;
+        o.vals[idx] = (uint64_t)e;
+    }
+}
+
+// grid.x: tiles of 256 words (8192 positions); grid.y: chunks of LCH unit lengths
+template <int B, int LCH>
+__global__ __launch_bounds__(256) void k_runs(const uint64_t *__restrict__ P, int64_t n, int64_t nwords32,
+                                              int32_t lmin, int32_t lmax, int64_t mc, CandOut out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t l0 = lmax - (int64_t)blockIdx.y * LCH;
+    for (int li = 0; li < LCH; ++li) {
+        const int64_t L = l0 - li;
+        if (L < lmin) break;                                     // uniform across the block
+        if ((int64_t)blockIdx.x * 256 * 32 >= n - L) break;      // whole tile past n-L
+        const int64_t K = (mc - 1) * L;
+        const uint32_t M = eq32<B>(P, w, L, n);
+        // neighbour masks: lanes 0 / 63 compute the word outside the wave
+        uint32_t X = 0;
+        if (lane == 0 || lane == 63) X = eq32<B>(P, lane == 0 ? w - 1 : w + 1, L, n);
+        uint32_t Mp = (uint32_t)__shfl_up((int)M, 1, 64);
+        uint32_t Mn = (uint32_t)__shfl_down((int)M, 1, 64);
+        if (lane == 0) Mp = X;
+        if (lane == 63) Mn = X;
+        if (w >= nwords32) continue;
+        const int64_t j0 = w * 32;
+        if (M == FULL) {
+            if (Mp != FULL) {  // first full word of a streak: the run contains >= 1 aligned word
+                const int64_t s = j0 - (int64_t)__clz(~Mp);
+                int64_t q = w + 1;
+                uint32_t Mq = Mn;
+                while (Mq == FULL) {
+                    ++q;
+                    Mq = eq32<B>(P, q, L, n);
+                }
+                const int64_t e = q * 32 + (int64_t)__ffs(~Mq) - 1;
+                if (e - s >= K) emit(out, L, s, e);
+            }
+        } else if (K <= 62 && M != 0u) {
+            // runs that start in this word and contain no full aligned word
+            uint32_t starts = M & ~((M << 1) | (Mp >> 31));
+            while (starts) {
+                const int k = __ffs(starts) - 1;
+                starts &= starts - 1;
+                const uint32_t r = M >> k;
+                const int len_in = __ffs(~r) - 1;  // ~r has its top k bits set
+                int64_t e;
+                if (k + len_in < 32) {
+                    e = j0 + k + len_in;
+                } else {
+                    if (Mn == FULL) continue;     // joins a streak owned by word w+1
+                    e = j0 + 32 + (int64_t)__ffs(~Mn) - 1;
+                }
+                const int64_t s = j0 + k;
+                if (e - s >= K) emit(out, L, s, e);
+            }
+        }
+    }
+}
+
+// min_copies == 1: every position starts a hit; one lane walks one L.  Row
+// `row` (L = lmax - row) owns hits[off[row] ..), at most n/L + 1 of them.
+__global__ void k_mc1(const uint8_t *__restrict__ t, int64_t n, int32_t lmin, int32_t lmax,
+                      const int64_t *__restrict__ off, bwtmi_hit *__restrict__ hits, int64_t *__restrict__ nper) {
+    const int64_t L = lmax - (int64_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (L < lmin) return;
+    const int64_t row = lmax - L;
+    int64_t i = 0, k = 0;
+    while (i + L <= n) {
+        int64_t c = 1;
+        while (i + (c + 1) * L <= n) {
+            bool eq = true;
+            for (int64_t x = 0; x < L && eq; ++x) eq = t[i + (c - 1) * L + x] == t[i + c * L + x];
+            if (!eq) break;
+            ++c;
+        }
+        bwtmi_hit h;
+        h.start = i;
+        h.end = i + c * L;
+        h.unit_len = (int32_t)L;
+        h.prim_len = 0;
+        h.copies = c;
+        hits[off[row] + k] = h;
+        ++k;
+        i += c * L;
+    }
+    nper[row] = k;
+}
+
+// ---------------------------------------------------------- resolution
+__global__ __launch_bounds__(256) void k_resolve(const uint64_t *__restrict__ keys, const uint64_t *__restrict__ vals,
+                                                 int64_t nc, int32_t umax, int64_t mc,
+                                                 int64_t *__restrict__ hit_i, int64_t *__restrict__ hit_c,
+                                                 uint32_t *__restrict__ flag) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nc) return;
+    const uint64_t mask40 = (1ull << 40) - 1;
+    auto Lof = [&](int64_t j) { return (int64_t)umax - (int64_t)(keys[j] >> 40); };
+    const int64_t L = Lof(k);
+    const int64_t s = (int64_t)(keys[k] & mask40);
+    const bool head = (k == 0) || Lof(k - 1) != L || s >= (int64_t)vals[k - 1] + L;
+    if (!head) return;
+    const int64_t K = (mc - 1) * L;
+    int64_t carry = 0;
+    for (int64_t j = k; j < nc; ++j) {
+        const int64_t sj = (int64_t)(keys[j] & mask40);
+        if (j > k && (Lof(j) != L || sj >= (int64_t)vals[j - 1] + L)) break;
+        const int64_t e = (int64_t)vals[j];
+        const int64_t i = sj > carry ? sj : carry;
+        if (e - i >= K) {
+            const int64_t cnt = 1 + (e - i) / L;
+            hit_i[j] = i;
+            hit_c[j] = cnt;
+            flag[j] = 1;
+            carry = i + cnt * L;
+        } else {
+            flag[j] = 0;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_compact(const uint64_t *__restrict__ keys, int64_t nc, int32_t umax,
+                                                 const int64_t *__restrict__ hit_i, const int64_t *__restrict__ hit_c,
+                                                 const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
+                                                 bwtmi_hit *__restrict__ hits) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nc || !flag[k]) return;
+    const int64_t L = (int64_t)umax - (int64_t)(keys[k] >> 40);
+    bwtmi_hit h;
+    h.start = hit_i[k];
+    h.end = hit_i[k] + hit_c[k] * L;
+    h.unit_len = (int32_t)L;
+    h.prim_len = 0;
+    h.copies = hit_c[k];
+    hits[pos[k]] = h;
+}
+
+// smallest_period_str of text[i : i+L] (bwt.py:1125-1133), then
+// count = length // p when p < L (bwt.py:1957-1961)
+__global__ __launch_bounds__(256) void k_period(const uint8_t *__restrict__ t, bwtmi_hit *__restrict__ hits, int64_t nh) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nh) return;
+    bwtmi_hit h = hits[k];
+    const int64_t L = h.unit_len;
+    const uint8_t *s = t + h.start;
+    int64_t p = L;
+    for (int64_t d = 1; d < L; ++d) {
+        if (L % d) continue;
+        int64_t x = d;
+        while (x < L && s[x] == s[x - d]) ++x;
+        if (x == L) { p = d; break; }
+    }
+    h.prim_len = (int32_t)p;
+    if (p < L) h.copies = (h.end - h.start) / p;
+    hits[k] = h;
+}
+
+__global__ void k_hist256(const uint8_t *__restrict__ t, int64_t n, unsigned long long *__restrict__ h) {
+    __shared__ unsigned int lh[256];
+    lh[threadIdx.x] = 0;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&lh[t[i]], 1u);
+    __syncthreads();
+    if (lh[threadIdx.x]) atomicAdd(&h[threadIdx.x], (unsigned long long)lh[threadIdx.x]);
+}
+
+template <int B>
+void launch_runs(Ctx &c, const uint64_t *P, int64_t n, int32_t lmin, int32_t lmax, int64_t mc, CandOut out) {
+    constexpr int LCH = 8;
+    const int64_t nwords32 = (n + 31) / 32;
+    const int64_t tiles = (nwords32 + 255) / 256;
+    const int64_t chunks = ((int64_t)lmax - lmin + LCH) / LCH;
+    hipLaunchKernelGGL((k_runs<B, LCH>), dim3((unsigned)tiles, (unsigned)chunks), dim3(256), 0, c.stream, P, n,
+                       nwords32, lmin, lmax, mc, out);
+}
+
+}  // namespace
+
+void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
+                        int32_t min_copies, ScanResult &res) {
+    res.hits.clear();
+    res.candidates = 0;
+    res.kernel_ms = 0;
+    if (min_copies <= 0) fail(BWTMI_E_ARG, "min_copies must be positive");
+    // bwt.py:1920-1921
+    const int64_t maxL = std::min<int64_t>(max_unit, n / min_copies);
+    if (n <= 0 || maxL < min_unit || maxL < 1) return;
+    const int32_t lmin = std::max<int32_t>(1, min_unit), lmax = (int32_t)maxL;
+    hipStream_t st = c.stream;
+    if (c.timing) HIPCHECK(hipEventRecord(c.ev0, st));
+
+    if (min_copies == 1) {   // degenerate but reachable from --min-copies 1
+        const int64_t nL = lmax - lmin + 1;
+        std::vector<int64_t> off((size_t)nL + 1, 0);
+        for (int64_t row = 0; row < nL; ++row) off[(size_t)row + 1] = off[(size_t)row] + n / (lmax - row) + 1;
+        const int64_t tot = off[(size_t)nL];
+        c.slot[S_MISC0].ensure((size_t)(nL + 1) * sizeof(int64_t));
+        c.slot[S_MISC1].ensure((size_t)tot * sizeof(bwtmi_hit));
+        c.slot[S_MISC2].ensure((size_t)nL * sizeof(int64_t));
+        HIPCHECK(hipMemcpyAsync(c.slot[S_MISC0].p, off.data(), off.size() * 8, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_mc1, dim3((unsigned)((nL + 63) / 64)), dim3(64), 0, st, d_text, n, lmin, lmax,
+                           c.slot[S_MISC0].as<int64_t>(), c.slot[S_MISC1].as<bwtmi_hit>(),
+                           c.slot[S_MISC2].as<int64_t>());
+        HIPCHECK(hipGetLastError());
+        std::vector<int64_t> np((size_t)nL);
+        HIPCHECK(hipMemcpyAsync(np.data(), c.slot[S_MISC2].p, np.size() * 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        int64_t nh = 0;
+        for (auto v : np) nh += v;
+        c.slot[S_HITS].ensure((size_t)std::max<int64_t>(nh, 1) * sizeof(bwtmi_hit));
+        int64_t w = 0;
+        for (int64_t row = 0; row < nL; ++row) {   // rows are already in (L desc, start asc) order
+            if (np[(size_t)row])
+                HIPCHECK(hipMemcpyAsync(c.slot[S_HITS].as<bwtmi_hit>() + w,
+                                        c.slot[S_MISC1].as<bwtmi_hit>() + off[(size_t)row],
+                                        (size_t)np[(size_t)row] * sizeof(bwtmi_hit), hipMemcpyDeviceToDevice, st));
+            w += np[(size_t)row];
+        }
+        if (nh > 0)
+            hipLaunchKernelGGL(k_period, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st, d_text,
+                               c.slot[S_HITS].as<bwtmi_hit>(), nh);
+        HIPCHECK(hipGetLastError());
+        res.hits.resize((size_t)nh);
+        if (nh > 0)
+            HIPCHECK(hipMemcpyAsync(res.hits.data(), c.slot[S_HITS].p, (size_t)nh * sizeof(bwtmi_hit),
+                                    hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        return;
+    }
+
+    // 1. alphabet -> code width
+    c.slot[S_COUNTS].ensure(256 * sizeof(unsigned long long));
+    HIPCHECK(hipMemsetAsync(c.slot[S_COUNTS].p, 0, 256 * sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_hist256, dim3(1024), dim3(256), 0, st, d_text, n, c.slot[S_COUNTS].as<unsigned long long>());
+    unsigned long long hist[256];
+    HIPCHECK(hipMemcpyAsync(hist, c.slot[S_COUNTS].p, sizeof hist, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    uint8_t code[256] = {0};
+    int sigma = 0;
+    for (int b = 0; b < 256; ++b)
+        if (hist[b]) code[b] = (uint8_t)sigma++;
+    const int B = sigma <= 4 ? 2 : (sigma <= 16 ? 4 : 8);
+    const int S = 64 / B;
+    const int64_t nwords = (n + S - 1) / S + 8;
+    c.slot[S_PACK].ensure((size_t)nwords * sizeof(uint64_t) + 256);
+    uint8_t *d_code = c.slot[S_PACK].as<uint8_t>() + nwords * sizeof(uint64_t);
+    HIPCHECK(hipMemcpyAsync(d_code, code, 256, hipMemcpyHostToDevice, st));
+    uint64_t *P = c.slot[S_PACK].as<uint64_t>();
+    HIPCHECK(hipMemsetAsync(P, 0, (size_t)nwords * sizeof(uint64_t), st));
+    const unsigned pgrid = (unsigned)((nwords + 255) / 256);
+    if (B == 2) hipLaunchKernelGGL(k_pack<2>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
+    else if (B == 4) hipLaunchKernelGGL(k_pack<4>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
+    else hipLaunchKernelGGL(k_pack<8>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
+    HIPCHECK(hipGetLastError());
+
+    // 2. candidate runs
+    int64_t cap = std::max<int64_t>(1 << 16, n / 8);
+    unsigned long long ncand = 0;
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        c.slot[S_CAND_K].ensure((size_t)cap * sizeof(uint64_t));
+        c.slot[S_CAND_V].ensure((size_t)cap * sizeof(uint64_t));
+        c.slot[S_MISC3].ensure(sizeof(unsigned long long));
+        HIPCHECK(hipMemsetAsync(c.slot[S_MISC3].p, 0, sizeof(unsigned long long), st));
+        CandOut co{c.slot[S_CAND_K].as<uint64_t>(), c.slot[S_CAND_V].as<uint64_t>(),
+                   c.slot[S_MISC3].as<unsigned long long>(), cap, lmax};
+        hipEvent_t ka = nullptr, kb = nullptr;
+        if (c.timing) {
+            HIPCHECK(hipEventCreate(&ka));
+            HIPCHECK(hipEventCreate(&kb));
+            HIPCHECK(hipEventRecord(ka, st));
+        }
+        if (B == 2) launch_runs<2>(c, P, n, lmin, lmax, min_copies, co);
+        else if (B == 4) launch_runs<4>(c, P, n, lmin, lmax, min_copies, co);
+        else launch_runs<8>(c, P, n, lmin, lmax, min_copies, co);
+        HIPCHECK(hipGetLastError());
+        if (c.timing) HIPCHECK(hipEventRecord(kb, st));
+        HIPCHECK(hipMemcpyAsync(&ncand, c.slot[S_MISC3].p, sizeof ncand, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        if (c.timing) {
+            float ms = 0;
+            HIPCHECK(hipEventElapsedTime(&ms, ka, kb));
+            c.last_dom_ms = ms;
+            c.last_dom_launches = 1;
+            c.dom_name = "k_runs";
+            res.kernel_ms = ms;
+            (void)hipEventDestroy(ka);
+            (void)hipEventDestroy(kb);
+        }
+        if ((int64_t)ncand <= cap) break;
+        cap = (int64_t)ncand + (int64_t)ncand / 4 + 1024;
+    }
+    const int64_t nc = (int64_t)ncand;
+    res.candidates = nc;
+    if (nc == 0) return;
+
+    // 3. order candidates as the reference emits them: L desc, start asc
+    int hb = 0;
+    while ((1ll << hb) <= (int64_t)lmax) ++hb;
+    radix_sort_pairs(c, c.slot[S_CAND_K].as<uint64_t>(), c.slot[S_CAND_V].as<uint64_t>(), nc, 0,
+                     ((40 + hb + 7) / 8) * 8);
+
+    // 4. carry resolution + compaction
+    c.slot[S_MISC0].ensure((size_t)nc * sizeof(int64_t));
+    c.slot[S_MISC1].ensure((size_t)nc * sizeof(int64_t));
+    c.slot[S_FLAG].ensure((size_t)nc * sizeof(uint32_t));
+    c.slot[S_SCAN].ensure((size_t)(nc + 1) * sizeof(uint32_t));
+    const unsigned g = (unsigned)((nc + 255) / 256);
+    hipLaunchKernelGGL(k_resolve, dim3(g), dim3(256), 0, st, c.slot[S_CAND_K].as<uint64_t>(),
+                       c.slot[S_CAND_V].as<uint64_t>(), nc, lmax, (int64_t)min_copies, c.slot[S_MISC0].as<int64_t>(),
+                       c.slot[S_MISC1].as<int64_t>(), c.slot[S_FLAG].as<uint32_t>());
+    HIPCHECK(hipMemsetAsync(c.slot[S_SCAN].as<uint32_t>() + nc, 0, sizeof(uint32_t), st));
+    exclusive_scan<uint32_t>(c, c.slot[S_FLAG].as<uint32_t>(), c.slot[S_SCAN].as<uint32_t>(), nc);
+    uint32_t last_pos = 0, last_flag = 0;
+    HIPCHECK(hipMemcpyAsync(&last_pos, c.slot[S_SCAN].as<uint32_t>() + nc - 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(&last_flag, c.slot[S_FLAG].as<uint32_t>() + nc - 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    const int64_t nh = (int64_t)last_pos + last_flag;
+    c.slot[S_HITS].ensure((size_t)std::max<int64_t>(nh, 1) * sizeof(bwtmi_hit));
+    hipLaunchKernelGGL(k_compact, dim3(g), dim3(256), 0, st, c.slot[S_CAND_K].as<uint64_t>(), nc, lmax,
+                       c.slot[S_MISC0].as<int64_t>(), c.slot[S_MISC1].as<int64_t>(), c.slot[S_FLAG].as<uint32_t>(),
+                       c.slot[S_SCAN].as<uint32_t>(), c.slot[S_HITS].as<bwtmi_hit>());
+    if (nh > 0)
+        hipLaunchKernelGGL(k_period, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st, d_text,
+                           c.slot[S_HITS].as<bwtmi_hit>(), nh);
+    HIPCHECK(hipGetLastError());
+    if (c.timing) HIPCHECK(hipEventRecord(c.ev1, st));
+    res.hits.resize((size_t)nh);
+    if (nh > 0)
+        HIPCHECK(hipMemcpyAsync(res.hits.data(), c.slot[S_HITS].p, (size_t)nh * sizeof(bwtmi_hit),
+                                hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if (c.timing) {
+        float ms = 0;
+        HIPCHECK(hipEventElapsedTime(&ms, c.ev0, c.ev1));
+        c.last_total_ms = ms;
+    }
+}
+
+}  // namespace bwtmi

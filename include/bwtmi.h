@@ -1,0 +1,192 @@
+/*
+ * bwtmi.h -- C ABI of libbwtmi.so, the MI355X-native (gfx950) BWT/FM-index and
+ * tandem-repeat engine behind the `bwt.py` drop-in surface.
+ *
+ * The reference (wyim-pgl/bwt-algorithm, bwt.py) is pure Python and has no
+ * FFI; its "interface" is the Python names listed below.  Each entry point
+ * here replaces the body of one of those names; the Python host
+ * (bwt-algorithm_amd/bwtmi) keeps the names and binds these symbols with
+ * ctypes.
+ *
+ * Conventions
+ *   - every function returns 0 on success, a negative BWTMI_E* code on error;
+ *     bwtmi_last_error() returns the thread-local message of the last error.
+ *   - inputs are caller-owned and only borrowed for the duration of a call;
+ *     outputs allocated by the library are released with bwtmi_free() or the
+ *     matching *_free().
+ *   - one bwtmi_ctx per device; calls on one ctx are serialised by the caller.
+ *     HIP is not fork-safe: never fork() after bwtmi_open().
+ *   - there is no CPU fallback: without a usable gfx950 device bwtmi_open()
+ *     fails with BWTMI_E_NODEVICE.
+ */
+#ifndef BWTMI_H
+#define BWTMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BWTMI_OK 0
+#define BWTMI_E_ARG (-1)
+#define BWTMI_E_NODEVICE (-2)
+#define BWTMI_E_HIP (-3)
+#define BWTMI_E_NOMEM (-4)
+#define BWTMI_E_STATE (-5)
+#define BWTMI_E_IO (-6)
+
+typedef struct bwtmi_ctx bwtmi_ctx;
+typedef struct bwtmi_index bwtmi_index;
+typedef struct bwtmi_job bwtmi_job;
+
+/* ------------------------------------------------------------ context */
+const char *bwtmi_last_error(void);
+const char *bwtmi_version(void);
+int bwtmi_device_count(int *count);
+int bwtmi_open(int device, bwtmi_ctx **out);
+int bwtmi_close(bwtmi_ctx *ctx);
+void bwtmi_free(void *p);
+/* time (ms) of the kernels of the last call on ctx, measured with HIP events
+ * on the ctx stream: [0]=total device, [1]=dominant kernel, [2]=its launches */
+int bwtmi_last_timing(bwtmi_ctx *ctx, double *out3);
+
+/* ------------------------------------------------------------ strict scan
+ * Replaces Tier2LCPFinder.find_long_unit_repeats_strict (bwt.py:1891-2001),
+ * as called by _process_chromosome_worker (bwt.py:3103-3106).
+ * seq: ASCII bases of one (trimmed) contig; a single trailing '$' is ignored
+ * (bwt.py:1915-1916).  Hits come out in the reference's emission order
+ * (unit_len descending, start ascending).  prim_len = smallest_period_str of
+ * the first unit (bwt.py:1956); copies = count after primitive reduction
+ * (bwt.py:1957-1961).  max_mismatch must be 0 (the CLI value). */
+typedef struct {
+    int64_t start;
+    int64_t end;
+    int32_t unit_len;
+    int32_t prim_len;
+    int64_t copies;
+} bwtmi_hit;
+
+int bwtmi_strict_scan(bwtmi_ctx *ctx, const uint8_t *seq, int64_t n, int32_t min_unit,
+                      int32_t max_unit, int32_t max_mismatch, int32_t min_copies,
+                      bwtmi_hit **hits, int64_t *nhits);
+
+/* ------------------------------------------------------------ FM index
+ * Replaces BWTCore.__init__ (bwt.py:106-136): suffix array (212-264), BWT
+ * (266-274), C table (276-286), Occ checkpoints (288-326), sampled SA
+ * (328-333) and the 8-mer hash (138-171).  text includes the sentinel, exactly
+ * as the reference receives it (seq + '$'). */
+#define BWTMI_INDEX_NO_KMER 1u
+
+int bwtmi_index_build(bwtmi_ctx *ctx, const uint8_t *text, int64_t n, int32_t sa_sample,
+                      int32_t occ_sample, uint32_t flags, bwtmi_index **out);
+int bwtmi_index_free(bwtmi_index *idx);
+int64_t bwtmi_index_size(const bwtmi_index *idx);
+int bwtmi_index_get_sa(const bwtmi_index *idx, int32_t *sa /* n */);
+int bwtmi_index_get_bwt(const bwtmi_index *idx, uint8_t *bwt /* n */);
+/* totals[256] and cumulative C[256] over byte values (absent bytes: total 0) */
+int bwtmi_index_get_counts(const bwtmi_index *idx, int64_t *totals, int64_t *C);
+/* checkpoints of one byte code; length = 1 + n/occ + (n%occ != 0) */
+int64_t bwtmi_index_occ_len(const bwtmi_index *idx);
+int bwtmi_index_get_occ(const bwtmi_index *idx, uint8_t code, int32_t *cp);
+/* sampled SA (bwt.py:328-333): values SA[i] for i = 0, s, 2s, ... */
+int64_t bwtmi_index_sampled_len(const bwtmi_index *idx);
+int bwtmi_index_get_sampled(const bwtmi_index *idx, int32_t *vals);
+/* 8-mer hash as CSR: offsets[65537], positions[offsets[65536]] */
+int64_t bwtmi_index_kmer_count(const bwtmi_index *idx);
+int bwtmi_index_get_kmer(const bwtmi_index *idx, int64_t *offsets, int32_t *positions);
+/* Kasai LCP over the index text (bwt.py:56-95, 2108-2116), int32[n] */
+int bwtmi_index_lcp(bwtmi_ctx *ctx, bwtmi_index *idx, int32_t *lcp);
+/* BWTCore.backward_search (bwt.py:359-389) for npat patterns packed in pats,
+ * pattern p = pats[off[p] .. off[p+1]).  Writes sp_ep[2p], sp_ep[2p+1]
+ * (inclusive interval, or -1,-1). */
+int bwtmi_backward_search_batch(bwtmi_ctx *ctx, bwtmi_index *idx, const uint8_t *pats,
+                                const int64_t *off, int64_t npat, int64_t *sp_ep);
+
+/* ------------------------------------------------------------ repeat job
+ * Replaces the per-contig worker result handling and the post-processing of
+ * TandemRepeatFinder (bwt.py:3040-3141, 3402-3944) and save_results with
+ * compound detection and the five writers (bwt.py:454-641, 3995-4198). */
+typedef struct {
+    int32_t min_copies;     /* --min-copies (default 3) */
+    int32_t max_unit_len;   /* --max-unit-len (default 120) */
+    int32_t show_progress;  /* --progress: lifts the >50 Mbp Tier-2 gate (bwt.py:3070) */
+    int32_t tier2;          /* 0 when --tier1 (bwt.py:4257-4259) */
+    int32_t threads;        /* host threads for post-processing (0 = auto) */
+    int32_t build_index;    /* also build the FM index per contig in bwtmi_job_scan, as the
+                               reference worker does (bwt.py:3053-3054); 0 = skip */
+    int32_t sa_sample;      /* --sa-sample (default 32) */
+    int32_t reserved;
+} bwtmi_params;
+
+#define BWTMI_FMT_STRFINDER 0
+#define BWTMI_FMT_BED 1
+#define BWTMI_FMT_VCF 2
+#define BWTMI_FMT_TRF_TABLE 3
+#define BWTMI_FMT_TRF_DAT 4
+
+int bwtmi_job_create(const bwtmi_params *params, bwtmi_job **out);
+int bwtmi_job_free(bwtmi_job *job);
+/* register a contig: name, the full (untrimmed, upper-cased) sequence and the
+ * trim offset; the analysed sequence is full[trim : full_len - trim_right]. */
+int bwtmi_job_add_contig(bwtmi_job *job, const char *name, const uint8_t *full, int64_t full_len,
+                         int64_t trim_left, int64_t trim_right, int32_t *contig_id);
+/* run the worker on every registered contig on ctx's device (strict scan,
+ * gates, Rule-1 filter) -- equivalent to find_tandem_repeats(_parallel) up to
+ * all_repeats (bwt.py:3792-3822, 3850-3915) */
+int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job);
+/* copy every contig to device memory now (bwtmi_job_scan does it on first use);
+ * later scans reuse the resident copies */
+int bwtmi_job_upload(bwtmi_ctx *ctx, bwtmi_job *job);
+/* drop raw / final records so the job can be scanned again */
+int bwtmi_job_reset(bwtmi_job *job);
+/* alternatively feed raw hits computed elsewhere (one contig at a time) */
+int bwtmi_job_add_hits(bwtmi_job *job, int32_t contig_id, const bwtmi_hit *hits, int64_t n);
+int64_t bwtmi_job_raw_count(const bwtmi_job *job);
+/* nested suppression .. final filter (bwt.py:3926-3944) */
+int bwtmi_job_postprocess(bwtmi_job *job);
+int64_t bwtmi_job_count(const bwtmi_job *job);
+/* render a format into a malloc'd buffer (free with bwtmi_free) or a file */
+int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len);
+int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path);
+/* final records as rows of int64: start, end, length, tier, n_copies_eval,
+ * max_mm, motif_len, cons_len, chrom_id and doubles: copies, mismatch_rate,
+ * confidence (for tests / the Python record view) */
+int bwtmi_job_get_records(bwtmi_job *job, int64_t *ints9, double *dbls3);
+/* strings of record i: which = 0 motif, 1 consensus, 2 variations(';'-joined),
+ * 3 actual_sequence, 4 strand; returns length, copies up to cap bytes */
+int64_t bwtmi_job_get_string(bwtmi_job *job, int64_t i, int which, char *buf, int64_t cap);
+/* serialise final records for a gather to another rank; import appends them */
+int bwtmi_job_export(bwtmi_job *job, uint8_t **buf, int64_t *len);
+int bwtmi_job_import(bwtmi_job *job, const uint8_t *buf, int64_t len);
+/* per-stage wall times (ms) of the last scan/postprocess/render calls */
+int bwtmi_job_stage_ms(const bwtmi_job *job, double *out8);
+
+/* ------------------------------------------------------------ helpers
+ * MotifUtils.align_repeat_region (bwt.py:998-1102) -- the banded per-copy
+ * alignment used by merge/refine; exposed for the Python MotifUtils mirror.
+ * max_indel < 0 means None.  Returns 1 with a summary, 0 for None.
+ * ints8: copies, motif_len, consumed, max_errors, tot_ins, tot_del, 0, 0;
+ * mismatch_rate; consensus (motif_len bytes) and variations (';'-joined,
+ * malloc'd, free with bwtmi_free); copy_len/copy_err (malloc'd int64[copies]). */
+int bwtmi_align_region(const char *seq, int64_t seq_len, int64_t start, int64_t end, const char *tmpl,
+                       int64_t tmpl_len, double frac, int64_t max_indel, int64_t min_copies,
+                       int64_t *ints8, double *mismatch_rate, char *consensus, char **variations,
+                       int64_t **copy_len, int64_t **copy_err);
+
+/* ------------------------------------------------------------ FASTA
+ * TandemRepeatFinder.load_reference (bwt.py:3713-3756) natively: strip,
+ * '>' headers (name = first whitespace token), upper-case sequence lines,
+ * blank lines skipped, duplicate names overwrite in place.  Registers every
+ * contig in job (trim = flank_trim if len > 2*flank_trim). */
+int bwtmi_job_load_fasta(bwtmi_job *job, const char *path, int32_t flank_trim);
+int32_t bwtmi_job_contig_count(const bwtmi_job *job);
+int64_t bwtmi_job_contig_info(const bwtmi_job *job, int32_t id, char *name, int64_t cap,
+                              int64_t *full_len, int64_t *trim_left, int64_t *trim_right);
+int bwtmi_job_contig_seq(const bwtmi_job *job, int32_t id, uint8_t *dst /* full_len */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BWTMI_H */

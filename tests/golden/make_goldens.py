@@ -1,0 +1,380 @@
+#!/usr/bin/env python3
+"""Generate the committed golden vectors from the REFERENCE itself.
+
+Runs only in the build container, where /root/reference (wyim-pgl/bwt-algorithm
+@ 2025-11-14, pure Python) is importable; the GPU box never sees it.  Nothing
+here is product code.  Outputs land in tests/golden/ as small data files:
+
+  fixtures      reference CLI (`bwt.py IN.fa --jobs -1 ...`) on the reference's
+                own FASTA fixtures + crafted edge files + seeded small synthetic
+                contigs -> expected output files (*.out) and expected_cli.json
+  rawhits       Tier2LCPFinder.find_long_unit_repeats_strict raw hit lists
+  index         BWTCore arrays (SA, BWT, C, Occ, sampled SA, 8-mer hash),
+                Kasai LCP, backward_search / locate / get_kmer_positions
+  motif         MotifUtils known answers
+  hybrid        reference post-processing with the strict scan (and the
+                O(k^2) nested-suppression loop) swapped for the oracle's
+                restatements -> full-size output SHA-256; the
+                swap is validated against the pure reference on every fixture
+                by `fixtures --check-hybrid`.
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import hashlib
+import io
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "bwt-algorithm_amd"))
+
+FIXTURE_FASTAS = ["synthetic_test.fa", "test.fa", "test1.fa", "test2.fa", "test_all_12.fa",
+                  "test_long_motif.fa", "test_repeat.fa", "test_seq1.fa", "test_simple.fasta",
+                  "test_synthetic.fasta"]
+FORMATS = ["strfinder", "bed", "vcf", "trf_table", "trf_dat"]
+
+
+def ref_module():
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import bwt as ref  # noqa: E402  (the reference, build container only)
+    return ref
+
+
+def sha(path):
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def run_ref_cli(ref, args, cwd):
+    old = os.getcwd(), sys.argv
+    try:
+        os.chdir(cwd)
+        sys.argv = ["bwt.py"] + list(args)
+        with contextlib.redirect_stdout(io.StringIO()):
+            ref.main()
+    finally:
+        os.chdir(old[0])
+        sys.argv = old[1]
+
+
+# --------------------------------------------------------------------- inputs
+EDGE_FA = """>chr10 some description
+ACGTTGCAAGTCAGTCAGTCAGTCGGATCCNNNNNNNNNNNNNNNNNNNNACGTAGCTAGCTACGATCG
+acgtacgtacgtacgtTTAGGCATCGATCGAaaaaaaaaaaGCGCGCGCATCRYRYRYRYRYRYGATTACA
+
+GATCGATCGTAGCTAGCTAGGGCCCAGCAGCAGCAGCAGCAGCAGCAGCAGCAGCAGCAGCTGCTGCTGCTG
+CTGCTGCTGACGATCGATTTTTTTTTTTTTTGACTAGCATCGATCGATTAGACAGACAGACAGACAGACAGA
+>chr2
+GGATCCGATCGATGCATCGATCGGCATGCATCGATCGGGAAGGAAGGAAGGAAGGAAGGAAGGCTAGCTAGCAT
+CGATCGATGCATGCAACACACACACACACACATGTGTGTGTGTGTGTATCGATCGATCGGCTAGCTAGCTAGG
+ATCGATCGTACGATCGTAGCTAGCATGCATCAGCAGCAGCAGCAGCAGCAGCAGCAGCAGCAGCAGTTGTTGTT
+GTTGTTGTTGATCGATCGTACGTAGCTAGCTAGCATCGATGCATCGACTGCATGCAAAAAAAAAAAAAAAAACG
+>Chr1
+ACGTACGTTTTTTTTTGGGGGGGGATATATATATATCGCGCG
+>chr3
+TGCATGCAGGTCAGTCAGTCAGTCAGTCAGTCAGTCAGTCGGTCAGTCAGTTAGTCAGTCAGTCAGTCCATCAT
+GCATCGATCGATCGGCTAGCTAGCTAGCTCATCATCATCATCATCATCATCATCATCATCATCATCATCTGCTG
+CTGCTGCTGCTGCTGCTGAGAGAGAGAGAGAGAGCGATCGATTGCATGCACCGCCGCCGCCGCCGATCGATCGA
+"""
+
+
+def write_inputs(dst):
+    from bwtmi import synth
+    os.makedirs(dst, exist_ok=True)
+    for fa in FIXTURE_FASTAS:
+        shutil.copy(os.path.join(REF, fa), os.path.join(dst, fa))
+    with open(os.path.join(dst, "edge_mixed.fa"), "w") as f:
+        f.write(EDGE_FA)
+    synth.write_fasta(os.path.join(dst, "synth_small.fa"), [3000, 2200], 0.0, first_index=101)
+    synth.write_fasta(os.path.join(dst, "synth_imperfect.fa"), [3000, 2600], 0.05, first_index=201)
+    synth.write_fasta(os.path.join(dst, "synth_imperfect2.fa"), [4000], 0.02, first_index=301)
+
+
+CLI_CASES = []   # (name, input, args)
+for fa in FIXTURE_FASTAS:
+    CLI_CASES.append((f"{fa}.strfinder", fa, []))
+for fmt in FORMATS[1:]:
+    CLI_CASES.append((f"synthetic_test.fa.{fmt}", "synthetic_test.fa", ["--format", fmt]))
+CLI_CASES += [
+    ("synthetic_test.fa.tier1", "synthetic_test.fa", ["--tier1", "--max-motif-len", "6"]),
+    ("synthetic_test.fa.nomm", "synthetic_test.fa", ["--no-mismatches"]),
+    ("test2.fa.mc4", "test2.fa", ["--min-copies", "4"]),
+    ("edge_mixed.fa.strfinder", "edge_mixed.fa", []),
+    ("edge_mixed.fa.bed", "edge_mixed.fa", ["--format", "bed"]),
+    ("edge_mixed.fa.trim0", "edge_mixed.fa", ["--flank-trim", "0"]),
+    ("edge_mixed.fa.trim7.vcf", "edge_mixed.fa", ["--flank-trim", "7", "--format", "vcf"]),
+    ("synth_small.fa.strfinder", "synth_small.fa", []),
+    ("synth_small.fa.mc2", "synth_small.fa", ["--min-copies", "2"]),
+    ("synth_small.fa.mc5.bed", "synth_small.fa", ["--min-copies", "5", "--format", "bed"]),
+    ("synth_imperfect.fa.strfinder", "synth_imperfect.fa", []),
+    ("synth_imperfect.fa.trf_table", "synth_imperfect.fa", ["--format", "trf_table"]),
+    ("synth_imperfect.fa.trf_dat", "synth_imperfect.fa", ["--format", "trf_dat"]),
+    ("synth_imperfect.fa.vcf", "synth_imperfect.fa", ["--format", "vcf"]),
+    ("synth_imperfect2.fa.strfinder", "synth_imperfect2.fa", []),
+    ("synth_imperfect2.fa.bed", "synth_imperfect2.fa", ["--format", "bed"]),
+    ("test_all_12.fa.trf_table", "test_all_12.fa", ["--format", "trf_table"]),
+    ("test2.fa.vcf", "test2.fa", ["--format", "vcf"]),
+]
+
+
+# --------------------------------------------------------------- hybrid swap
+class _StubCore:
+    """Index stand-in for the hybrid oracle: the CLI path consumes only
+    text_arr from BWTCore (bwt.py:1910); every other array is built and
+    discarded, so the hybrid skips the build."""
+
+    def __init__(self, text, sa_sample_rate=32, occ_sample_rate=128):
+        self.text = text
+        self.n = len(text)
+        self.text_arr = np.frombuffer(text.encode("utf-8"), dtype=np.uint8)
+
+    def clear(self):
+        self.text_arr = np.array([], dtype=np.uint8)
+
+
+def install_hybrid(ref, stub_index=True, restate_nested=True):
+    import oracle
+    from oracle import post
+
+    def fast_strict(self, chromosome, min_unit_len=20, max_unit_len=120, max_mismatch=2,
+                    min_copies=3):
+        t = self.bwt.text_arr
+        hits = oracle.strict_scan(t, min_unit_len, max_unit_len, max_mismatch, min_copies)
+        out = []
+        for s, e, L, p, c in hits.tolist():
+            motif = bytes(t[s:s + p]).decode("ascii", errors="replace")
+            pm, pi, sc, comp, ent, act = ref.MotifUtils.calculate_trf_statistics(t, s, e, motif, c, 0.0)
+            out.append(ref.TandemRepeat(
+                chrom=chromosome, start=s, end=e, motif=motif, copies=float(c), length=e - s,
+                tier=2, confidence=0.95, consensus_motif=motif, mismatch_rate=0.0,
+                max_mismatches_per_copy=0 if pm >= 99.9 else max_mismatch, n_copies_evaluated=c,
+                strand="+", percent_matches=pm, percent_indels=pi, score=sc, composition=comp,
+                entropy=ent, actual_sequence=act, variations=None))
+        return out
+
+    ref.Tier2LCPFinder.find_long_unit_repeats_strict = fast_strict
+    if stub_index:
+        ref.BWTCore = _StubCore
+    if restate_nested:
+        def nested(self, repeats, overlap_threshold=0.5):
+            return post.Pipeline({}, {}, {}).suppress_nested(repeats, overlap_threshold)
+        ref.TandemRepeatFinder._suppress_nested_short_calls = nested
+
+
+# ------------------------------------------------------------------ commands
+def cmd_fixtures(a):
+    ref = ref_module()
+    inp = os.path.join(HERE, "inputs")
+    write_inputs(inp)
+    out_dir = os.path.join(HERE, "cli")
+    os.makedirs(out_dir, exist_ok=True)
+    manifest = {}
+    work = tempfile.mkdtemp()
+    for name, fa, args in CLI_CASES:
+        t0 = time.time()
+        dst = os.path.join(out_dir, name + ".out")
+        shutil.copy(os.path.join(inp, fa), os.path.join(work, fa))
+        run_ref_cli(ref, [fa, "-o", "out.tab", "--jobs", "-1"] + args, work)
+        shutil.copy(os.path.join(work, "out.tab"), dst)
+        manifest[name] = dict(input=fa, args=args, sha256=sha(dst))
+        print(f"{name}: {time.time() - t0:.1f}s {manifest[name]['sha256'][:12]}", flush=True)
+    with open(os.path.join(HERE, "expected_cli.json"), "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+    if a.check_hybrid:
+        install_hybrid(ref, stub_index=True, restate_nested=True)
+        bad = 0
+        for name, fa, args in CLI_CASES:
+            run_ref_cli(ref, [fa, "-o", "hy.tab", "--jobs", "-1"] + args, work)
+            ok = sha(os.path.join(work, "hy.tab")) == manifest[name]["sha256"]
+            bad += not ok
+            print(f"hybrid {name}: {'OK' if ok else 'MISMATCH'}", flush=True)
+        if bad:
+            raise SystemExit(f"hybrid oracle disagrees with reference on {bad} case(s)")
+
+
+def _contigs_of(ref, path, flank=30):
+    f = ref.TandemRepeatFinder(path, flank_trim=flank)
+    return f.load_reference()
+
+
+def cmd_rawhits(a):
+    ref = ref_module()
+    inp = os.path.join(HERE, "inputs")
+    res = {}
+    for fa in ["synthetic_test.fa", "test.fa", "test2.fa", "test_all_12.fa", "test_long_motif.fa",
+               "edge_mixed.fa", "synth_small.fa", "synth_imperfect.fa"]:
+        seqs = _contigs_of(ref, os.path.join(inp, fa))
+        for chrom, seq in seqs.items():
+            core = ref.BWTCore(seq + "$", 32)
+            for mc in ([3, 2, 4] if fa == "synth_small.fa" else [3]):
+                U = max(120, min(len(seq) // mc, 1000))
+                t2 = ref.Tier2LCPFinder(core, min_period=1)
+                hits = t2.find_long_unit_repeats_strict(chrom, min_unit_len=1, max_unit_len=U,
+                                                        max_mismatch=0, min_copies=mc)
+                res[f"{fa}|{chrom}|mc{mc}"] = dict(
+                    seq=seq, U=U, min_copies=mc,
+                    hits=[[h.start, h.end, h.motif, int(h.copies)] for h in hits])
+            print(fa, chrom, len(seq), flush=True)
+    # a mismatch-tolerant call of the same function (library use, bwt.py:1941)
+    seqs = _contigs_of(ref, os.path.join(inp, "synth_imperfect.fa"))
+    chrom, seq = next(iter(seqs.items()))
+    core = ref.BWTCore(seq + "$", 32)
+    hits = ref.Tier2LCPFinder(core).find_long_unit_repeats_strict(chrom, 4, 40, 2, 3)
+    res["synth_imperfect.fa|mm2"] = dict(seq=seq, U=40, min_unit=4, max_mismatch=2, min_copies=3,
+                                         hits=[[h.start, h.end, h.motif, int(h.copies)] for h in hits])
+    with open(os.path.join(HERE, "rawhits.json"), "w") as f:
+        json.dump(res, f)
+
+
+def cmd_index(a):
+    ref = ref_module()
+    from bwtmi import synth
+    inp = os.path.join(HERE, "inputs")
+    texts = {}
+    for fa in ["test2.fa", "edge_mixed.fa"]:
+        for chrom, seq in _contigs_of(ref, os.path.join(inp, fa)).items():
+            texts[f"{fa}|{chrom}"] = seq
+    texts["synth10k"] = synth.generate_contig(10000, 7).decode()
+    texts["lower_mixed"] = "acgtNNACGTacgtRYKMacgtacgtTTTTTTTTtttt$$ACGT"[:40]
+    texts["tiny"] = "A"
+    texts["empty"] = ""
+    rng = np.random.default_rng(5)
+    pats = ["", "A", "C", "G", "T", "N", "$", "X", "AC", "ACG", "ACGT", "TTTT", "GATC",
+            "CAGCAG", "NNNN", "acgt", "AAAAAAAAA"]
+    for k in range(1, 11):
+        for _ in range(4):
+            pats.append("".join(rng.choice(list("ACGT"), k)))
+    arrays = {}
+    meta = {}
+    for name, seq in texts.items():
+        text = seq + "$"
+        core = ref.BWTCore(text, 32)
+        key = name.replace("|", "__").replace(".", "_")
+        arrays[key + "__text"] = np.frombuffer(text.encode(), dtype=np.uint8)
+        arrays[key + "__sa"] = np.asarray(core.suffix_array, dtype=np.int32)
+        arrays[key + "__bwt"] = np.asarray(core.bwt_arr, dtype=np.uint8)
+        arrays[key + "__lcp"] = np.asarray(ref.Tier2LCPFinder(core)._compute_lcp_array(), dtype=np.int32)
+        occ = {str(c): v.tolist() for c, v in core.occ_checkpoints.items()}
+        kh = {str(c): v for c, v in core.kmer_hash.items()}
+        bs = {p: list(core.backward_search(p)) for p in pats}
+        loc = {p: core.locate_positions(p) for p in pats if p}
+        kp = {p: core.get_kmer_positions(p) for p in ["ACGT", "A", "CAG", "GATCGATC", "AC", "TTTTTTTT"]}
+        meta[key] = dict(name=name, C={str(ord(c)): v for c, v in core.char_counts.items()},
+                         totals={str(ord(c)): v for c, v in core.char_totals.items()},
+                         occ=occ, sampled={str(k): int(v) for k, v in core.sampled_sa.items()},
+                         kmer_hash=kh, backward=bs, locate=loc, kmer_positions=kp)
+    np.savez_compressed(os.path.join(HERE, "index_arrays.npz"), **arrays)
+    with open(os.path.join(HERE, "index_meta.json"), "w") as f:
+        json.dump(meta, f)
+
+
+def cmd_motif(a):
+    ref = ref_module()
+    M = ref.MotifUtils
+    words = ["ATCG", "CGAT", "AAAA", "ATAT", "GCGGCG", "TGCTGATCGTAGCTAGCTGA", "CAG", "A", "",
+             "NNAC", "ACGTN", "TTAGGG", "GATCGATC", "RYRY"]
+    out = dict(
+        canonical={w: M.get_canonical_motif(w) for w in words},
+        stranded={w: list(M.get_canonical_motif_stranded(w)) for w in words},
+        revcomp={w: M.reverse_complement(w) for w in words},
+        entropy={w: float(M.calculate_entropy(w)) for w in words},
+        primitive={w: M.is_primitive_motif(w) for w in words},
+        period={w: M.smallest_period_str(w) for w in words},
+        hamming=[[s1, s2, M.hamming_distance(s1, s2)] for s1, s2 in
+                 [("ATCG", "ATGG"), ("ATCG", "GGGG"), ("AAAA", "TTTT"), ("AC", "ACG")]],
+        edit=[[s1, s2, M.edit_distance(s1, s2)] for s1, s2 in
+              [("ACGT", "AGT"), ("", "AC"), ("CAGCAG", "CAGAG"), ("ATCG", "TACG")]],
+        consensus=[[seqs, list(M.build_consensus_motif(seqs))] for seqs in
+                   [["ATCG", "ATCG", "ATGG"], ["AAA", "AAT", "ATT"], ["CG"]]],
+        composition={w: M.calculate_composition(w) for w in words},
+        score=[[l, mm, M.calculate_trf_score("A", 3, mm, l)] for l, mm in
+               [(10, 0.0), (35, 0.1), (100, 0.333), (7, 0.9)]],
+        enumerate={k: len(list(M.enumerate_motifs(k))) for k in range(1, 7)},
+    )
+    aligns = []
+    cases = [("ACGTTACGTACGTAACGTACGT", 0, 22, "ACGT"),
+             ("CAGCAGCAGCAAGCAGCAGTCAGCAG", 0, 26, "CAG"),
+             ("TCATCGGTCATCGGTCATCGGTCATCGGTCAACGGTCATCGGGTCATCGG", 0, 50, "TCATCGG"),
+             ("AAAAAAAAAA", 0, 10, "AA"), ("GATTACA", 2, 1, "TTA")]
+    for seq, s, e, m in cases:
+        for mc in (1, 3):
+            r = M.align_repeat_region(seq, s, e, m, min_copies=mc)
+            aligns.append([seq, s, e, m, mc, None if r is None else dict(
+                consensus=r.consensus, copies=r.copies, consumed=r.consumed_length,
+                mismatch_rate=r.mismatch_rate, max_err=r.max_errors_per_copy,
+                variations=r.variations, ins=r.total_insertions, dele=r.total_deletions)])
+    out["align"] = aligns
+    with open(os.path.join(HERE, "motif_known.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+def cmd_hybrid(a):
+    """Full-size golden via the validated hybrid oracle."""
+    ref = ref_module()
+    from bwtmi import synth
+    install_hybrid(ref, stub_index=True, restate_nested=True)
+    work = a.work or tempfile.mkdtemp()
+    fa = os.path.join(work, f"{a.name}.fa")
+    cfg = synth.CONFIGS.get(a.config) if a.config else None
+    lengths = cfg["lengths"] if cfg else [int(x) for x in a.lengths.split(",")]
+    sub = cfg["sub_rate"] if cfg else a.sub_rate
+    t0 = time.time()
+    fa_sha = synth.write_fasta(fa, lengths, sub)
+    args = [os.path.basename(fa), "-o", "out.tab", "--jobs", str(a.jobs)] + a.extra.split()
+    run_ref_cli(ref, args, work)
+    outp = os.path.join(work, "out.tab")
+    with open(outp, "rb") as f:
+        data = f.read()
+    rec = dict(config=a.config, lengths=lengths, sub_rate=sub, args=a.extra.split(),
+               fasta_sha256=fa_sha, out_sha256=hashlib.sha256(data).hexdigest(),
+               out_rows=data.count(b"\n") - 1, seconds=round(time.time() - t0, 1))
+    if a.keep_rows:
+        lines = data.decode().splitlines()
+        step = max(1, (len(lines) - 1) // a.keep_rows)
+        rec["sample"] = {str(i): lines[i] for i in range(1, len(lines), step)}
+    if a.save_out:
+        shutil.copy(outp, os.path.join(HERE, "cli", f"{a.name}.out"))
+    path = os.path.join(HERE, "expected_large.json")
+    allr = json.load(open(path)) if os.path.exists(path) else {}
+    allr[a.name] = rec
+    with open(path, "w") as f:
+        json.dump(allr, f, indent=1, sort_keys=True)
+    print(json.dumps({k: v for k, v in rec.items() if k != "sample"}))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    sp = ap.add_subparsers(dest="cmd", required=True)
+    p = sp.add_parser("fixtures"); p.add_argument("--check-hybrid", action="store_true")
+    sp.add_parser("rawhits")
+    sp.add_parser("index")
+    sp.add_parser("motif")
+    p = sp.add_parser("hybrid")
+    p.add_argument("name")
+    p.add_argument("--config")
+    p.add_argument("--lengths", default="100000")
+    p.add_argument("--sub-rate", type=float, default=0.0)
+    p.add_argument("--extra", default="")
+    p.add_argument("--jobs", type=int, default=-1)
+    p.add_argument("--work")
+    p.add_argument("--keep-rows", type=int, default=0)
+    p.add_argument("--save-out", action="store_true")
+    a = ap.parse_args()
+    dict(fixtures=cmd_fixtures, rawhits=cmd_rawhits, index=cmd_index, motif=cmd_motif,
+         hybrid=cmd_hybrid)[a.cmd](a)
+
+
+if __name__ == "__main__":
+    main()
