@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: Mbp/s indexed+scanned (Tier 1+2) on 100 Mbp
+synthetic contigs, 1/2/4/8 GPUs (BASELINE.json `metric`).
+
+Workload (with --progress so the reference's >50 Mbp Tier-2
+gate does not turn the run into a header-only no-op): one 100,000,000 bp
+synthetic contig per rank (seeded generator bwtmi/synth.py, contig k+1 on
+rank k), default parameters (min_copies 3, max_unit_len 120 -> U = 1000).
+Contigs are the sharding unit (one per GPU, weak scaling).
+
+One step = one pass of the whole path over the resident contig(s):
+  device FM index (SA, BWT, C, Occ, sampled SA, 8-mer hash)  [bwt.py:3053-3054]
+  device strict adjacency scan + hit download                [bwt.py:3103-3106]
+  native post-processing to the final records                [bwt.py:3928-3944]
+  RCCL all-gather of the final records to rank 0 (N > 1)
+  rank 0: compound detection + STRfinder rendering in memory [bwt.py:4141-4198]
+Inputs are resident in HBM before timing starts (uploaded during warmup).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "bwt-algorithm_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+CONTIG_BP = 100_000_000
+FLANK = 30
+
+
+def cpu_baseline(sample_bp: int):
+    """Oracle port (C index + C strict scan + Python post-processing, 1 thread)
+    on the first `sample_bp` bases of the rank-0 contig."""
+    import oracle
+    from oracle import post
+    from bwtmi import synth
+    seq = synth.generate_contig(sample_bp, 1, 0.0)
+    t0 = time.perf_counter()
+    trimmed = seq[FLANK:len(seq) - FLANK]
+    oracle.Index(trimmed + b"$")
+    U = max(120, min(len(trimmed) // 3, 1000))
+    hits = oracle.strict_scan(trimmed, 1, U, 0, 3, threads=1)
+    s = trimmed.decode()
+    p = post.Pipeline({"contig1": s}, {"contig1": seq.decode()}, {"contig1": FLANK}, 3)
+    recs = p.run(post.worker_records("contig1", s, hits))
+    post.render(p, recs, "strfinder")
+    dt = time.perf_counter() - t0
+    return dict(value=round(sample_bp / 1e6 / dt, 5), unit="Mbp/s", cores=1, kind="port",
+                sample=f"first {sample_bp:,} bp of contig1 (C3 workload): oracle index + strict scan "
+                       f"+ post-processing + STRfinder render, 1 thread, {dt:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--contig-bp", type=int, default=CONTIG_BP)
+    ap.add_argument("--cpu-sample-bp", type=int, default=1_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-index", action="store_true", help="skip the FM index (scan-only step)")
+    ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    td = None
+    if world > 1:
+        import torch
+        from bwtmi import dist
+        td = dist.init()                      # RCCL (nccl backend) over xGMI
+
+    from bwtmi import _lib, dist, synth
+    from bwtmi.records import Job
+
+    ctx = _lib.ctx(local)
+    # every rank registers every contig (ids match across ranks); rank 0 needs
+    # all sequences to render, other ranks only their own
+    job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True,
+              build_index=not a.no_index, sa_sample=32)
+    for k in range(world):
+        own = (k == rank) or rank == 0
+        seq = synth.generate_contig(a.contig_bp, k + 1, 0.0) if own else b""
+        trim = FLANK if len(seq) > 2 * FLANK else 0
+        job.add_contig(f"contig{k + 1}", seq, trim, trim)
+    job.select([rank])
+    job.upload(ctx)
+
+    def step():
+        job.reset()
+        job.select([rank])
+        job.scan(ctx)
+        job.postprocess()
+        if world > 1:
+            blobs = dist.gather_bytes(td, job.export(), torch.device("cuda", local))
+            job.reset()
+            if rank == 0:
+                for b in blobs:
+                    job.import_records(b)
+        if rank == 0:
+            return job.render("strfinder")
+        return b""
+
+    def sync():
+        if world > 1:
+            torch.cuda.synchronize()
+            td.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        step()
+    _lib.kernel_stats(ctx, enable=True, reset=True)
+    sync()
+    t0 = time.perf_counter()
+    out = b""
+    for _ in range(a.steps):
+        out = step()
+    sync()
+    elapsed = time.perf_counter() - t0
+    kstats = _lib.kernel_stats(ctx, enable=False, reset=True)
+    stages = job.stage_ms()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local))
+        td.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if a.stages:
+        print(json.dumps(dict(rank=rank, stage_ms=stages, kernels=kstats)), file=sys.stderr)
+    if rank != 0:
+        if td is not None:
+            td.barrier()
+        return 0
+
+    ms_step = elapsed / a.steps * 1000.0
+    total_bp = world * a.contig_bp
+    value = total_bp / 1e6 / (elapsed / a.steps)
+    # dominant kernel = largest total device time in the timed steps
+    dom = max(kstats.items(), key=lambda kv: kv[1][0]) if kstats else None
+    roofline = None
+    if dom:
+        name, (kms, launches, kbytes) = dom
+        achieved = kbytes / (kms / 1e3) / 1e9 if kms > 0 else 0.0
+        roofline = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / HBM_PEAK_GBS, 5), traffic=None, kernel=name,
+                        avg_launch_ms=round(kms / launches, 4), launches_per_step=launches / a.steps)
+    cpu = None if a.no_cpu_baseline else cpu_baseline(a.cpu_sample_bp)
+    line = {
+        "metric": "Mbp/s indexed+scanned (Tier1+2) on 100 Mbp synthetic FASTA, 1/2/4/8 GPU",
+        "value": round(value, 3), "unit": "Mbp/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded splitmix64 generator, bwtmi/synth.py)",
+        "config": {"workload": "C3: one 100 Mbp synthetic contig per GPU, Tier1+2 defaults with "
+                               "--progress (ungated), FM index + strict scan + post-processing + "
+                               "STRfinder render", "contig_bp": a.contig_bp, "contigs": world,
+                   "parallelism": f"contig-shard x{world}", "index": not a.no_index},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "rows": out.count(b"\n") - 1 if out else 0,
+        "stage_ms_last_step": {"scan+index": round(stages[0], 2), "index": round(stages[1], 2),
+                               "nested": round(stages[2], 2), "dedup": round(stages[3], 2),
+                               "merge": round(stages[4], 2), "refine..filter": round(stages[5], 2),
+                               "render": round(stages[6], 2)},
+        "kernels_ms_per_step": {k: round(v[0] / a.steps, 3) for k, v in sorted(kstats.items())},
+    }
+    print(json.dumps(line))
+    if td is not None:
+        td.barrier()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

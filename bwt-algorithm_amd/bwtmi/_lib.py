@@ -46,6 +46,7 @@ _SIGS = {
     "bwtmi_close": (C.c_int, [_P]),
     "bwtmi_free": (None, [_P]),
     "bwtmi_last_timing": (C.c_int, [_P, C.POINTER(C.c_double)]),
+    "bwtmi_kernel_stats": (C.c_int, [_P, C.c_int, C.c_int, C.c_char_p, C.c_int64]),
     "bwtmi_strict_scan": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                     C.POINTER(C.POINTER(Hit)), C.POINTER(C.c_int64)]),
     "bwtmi_index_build": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_uint32, C.POINTER(_P)]),
@@ -69,6 +70,8 @@ _SIGS = {
     "bwtmi_job_scan": (C.c_int, [_P, _P]),
     "bwtmi_job_upload": (C.c_int, [_P, _P]),
     "bwtmi_job_reset": (C.c_int, [_P]),
+    "bwtmi_job_set_params": (C.c_int, [_P, C.POINTER(Params)]),
+    "bwtmi_job_select": (C.c_int, [_P, _P, C.c_int32]),
     "bwtmi_job_add_hits": (C.c_int, [_P, C.c_int32, _P, C.c_int64]),
     "bwtmi_job_raw_count": (C.c_int64, [_P]),
     "bwtmi_job_postprocess": (C.c_int, [_P]),
@@ -146,6 +149,17 @@ def _close_all():
     for h in list(_ctxs.values()):
         _lib.bwtmi_close(h)
     _ctxs.clear()
+
+
+def kernel_stats(h, enable: bool = True, reset: bool = True) -> dict:
+    """{kernel: (total_ms, launches, algorithmic_bytes)} from HIP events on the ctx stream."""
+    buf = C.create_string_buffer(1 << 16)
+    check(lib().bwtmi_kernel_stats(h, int(enable), int(reset), buf, len(buf)))
+    out = {}
+    for line in buf.value.decode().splitlines():
+        name, ms, n, b = line.split()
+        out[name] = (float(ms), int(n), float(b))
+    return out
 
 
 def last_timing(h) -> tuple:

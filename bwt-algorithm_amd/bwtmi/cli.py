@@ -1,0 +1,97 @@
+"""`bwt.py` command line (bwt.py:4201-4370): same positional argument, the
+same 16 options and defaults, the same output files."""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+from .finder import TandemRepeatFinder
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(
+        description="Advanced BWT-based Tandem Repeat Finder with Imperfect Repeat Support "
+                    "(MI355X-native engine)",
+        formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("reference", help="Reference genome FASTA file")
+    p.add_argument("-o", "--output", default="repeat.tab", help="Output file (default: repeat.tab)")
+    p.add_argument("--format", choices=["bed", "vcf", "trf_table", "trf_dat", "strfinder"],
+                   default="strfinder", help="Output format (default: strfinder)")
+    p.add_argument("--tier1", action="store_true", help="Enable tier 1 only (short repeats, 1-9bp)")
+    p.add_argument("--tier3", action="store_true", help="Enable tier 3 (very long repeats, kb+)")
+    p.add_argument("--long-reads", help="Long reads file for tier 3")
+    p.add_argument("--sa-sample", type=int, default=32, help="Suffix array sampling rate (default: 32)")
+    p.add_argument("--progress", action="store_true", help="Show progress bars where applicable")
+    p.add_argument("--jobs", type=int, default=4,
+                   help="Parallel workers (default: 4, 0=all, -1=sequential); results are identical")
+    p.add_argument("--no-mismatches", action="store_true",
+                   help="Disable mismatch tolerance (exact matches only)")
+    p.add_argument("--max-motif-len", type=int, default=9, help="Maximum motif length for tier 1 (default: 9)")
+    p.add_argument("--min-period", type=int, default=10, help="Minimum period for tier 2 (default: 10)")
+    p.add_argument("--max-period", type=int, default=1000, help="Maximum period for tier 2 (default: 1000)")
+    p.add_argument("--max-unit-len", type=int, default=120,
+                   help="Maximum unit length for tier 2 long repeat detection (default: 120)")
+    p.add_argument("--min-copies", type=int, default=3, help="Minimum number of copies required (default: 3)")
+    p.add_argument("--min-entropy", type=float, default=1.0,
+                   help="Minimum Shannon entropy to avoid low-complexity (default: 1.0)")
+    p.add_argument("--flank-trim", type=int, default=30,
+                   help="Trim N bp from each end before analysis (default: 30, use 0 to disable)")
+    return p
+
+
+def _read_long_reads(path: str):
+    reads, cur = [], ""
+    with open(path) as f:
+        for line in f:
+            line = line.strip()
+            if line.startswith(">") or line.startswith("@"):
+                if cur:
+                    reads.append(cur)
+                    cur = ""
+            elif not line.startswith("+"):
+                cur += line.upper()
+    if cur:
+        reads.append(cur)
+    return reads
+
+
+def main(argv=None) -> int:
+    a = build_parser().parse_args(argv)
+    tier2 = not a.tier1                                   # bwt.py:4257-4262
+    tiers = "Tier 1 (short repeats)" if a.tier1 else "Tier 1 + Tier 2 (short + medium repeats)"
+    if a.tier3:
+        tiers += " + Tier 3 (very long repeats)"
+    print("BWT-based Tandem Repeat Finder")
+    print("=" * 60)
+    print(f"Reference:    {a.reference}")
+    print(f"Output:       {a.output} ({a.format} format)")
+    print(f"Tiers:        {tiers}")
+    print(f"Engine:       libbwtmi on MI355X (gfx950)")
+    print()
+    finder = TandemRepeatFinder(a.reference, a.sa_sample, show_progress=a.progress,
+                                allow_mismatches=not a.no_mismatches, max_motif_length=a.max_motif_len,
+                                min_period=a.min_period, max_period=a.max_period,
+                                min_copies=a.min_copies, min_entropy=a.min_entropy,
+                                flank_trim=a.flank_trim, max_unit_len=a.max_unit_len)
+    sequences = finder.load_reference()
+    if os.environ.get("BWTMI_SKIP_INDEX", "0") != "1":
+        finder.build_indices(sequences)
+    long_reads = _read_long_reads(a.long_reads) if (a.long_reads and a.tier3) else []
+    if a.jobs != -1:
+        repeats = finder.find_tandem_repeats_parallel(True, tier2, a.tier3, long_reads or None, None)
+    else:
+        repeats = finder.find_tandem_repeats(True, tier2, a.tier3, long_reads or None)
+    from . import dist
+    if dist.is_distributed() and dist._torch_dist().get_rank() != 0:
+        return 0
+    finder.save_results(repeats, a.output, a.format)
+    print()
+    print("=" * 60)
+    print(f"Completed! Found {len(repeats)} total tandem repeats.")
+    print(f"Results saved to {a.output}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,127 @@
+"""TandemRepeatFinder -- the reference's orchestrator (bwt.py:3144-4198) with
+the same constructor, methods and results, running on one MI355X device per
+process.
+
+  load_reference      native FASTA loader (bwt.py:3713-3756)
+  build_indices       device FM index per contig (bwt.py:3758-3790)
+  find_tandem_repeats / find_tandem_repeats_parallel
+                      device strict scan per contig + native post-processing
+                      (bwt.py:3792-3954); with torch.distributed initialised
+                      the contigs are sharded over ranks (bwtmi.dist)
+  save_results        native writers incl. compound detection (bwt.py:4141-4198)
+"""
+from __future__ import annotations
+
+import sys
+import time
+from typing import Dict, List, Optional
+
+from . import _lib
+from .core import BWTCore
+from .records import Job, RepeatList, TandemRepeat
+
+
+class TandemRepeatFinder:
+    def __init__(self, reference_file: str, sa_sample_rate: int = 32, show_progress: bool = False,
+                 allow_mismatches: bool = True, max_motif_length: int = 9, min_period: int = 10,
+                 max_period: int = 1000, min_copies: int = 3, min_entropy: float = 1.0,
+                 flank_trim: int = 30, max_unit_len: int = 120, device: Optional[int] = None,
+                 threads: int = 0):
+        self.reference_file = reference_file
+        self.sa_sample_rate = sa_sample_rate
+        self.bwt_cores: Dict[str, BWTCore] = {}
+        self.sequences: Dict[str, str] = {}
+        self.show_progress = show_progress
+        self.allow_mismatches = allow_mismatches      # no effect on results (bwt.py:3105)
+        self.max_motif_length = max_motif_length
+        self.min_period = min_period
+        self.max_period = max_period
+        self.min_copies = min_copies
+        self.min_entropy = min_entropy
+        self.flank_trim = max(0, flank_trim)
+        self.max_unit_len = max_unit_len
+        self.trim_offsets: Dict[str, int] = {}
+        self.full_sequences: Dict[str, str] = {}
+        self.device = device
+        self.threads = threads
+        self.job: Optional[Job] = None
+
+    # ------------------------------------------------------------------ input
+    def _new_job(self, tier2: bool = True) -> Job:
+        return Job(min_copies=self.min_copies, max_unit_len=self.max_unit_len,
+                   show_progress=self.show_progress, tier2=tier2, threads=self.threads,
+                   build_index=False, sa_sample=self.sa_sample_rate)
+
+    def load_reference(self) -> Dict[str, str]:
+        job = self._new_job()
+        job.load_fasta(self.reference_file, self.flank_trim)
+        self.job = job
+        seqs: Dict[str, str] = {}
+        self.full_sequences = {}
+        self.trim_offsets = {}
+        for i in range(job.contig_count()):
+            name, fl, tl, tr = job.contig_info(i)
+            full = job.contig_seq(i).decode("latin-1")
+            self.full_sequences[name] = full
+            self.trim_offsets[name] = tl
+            seqs[name] = full[tl:fl - tr]
+        self.sequences = seqs
+        return seqs
+
+    def build_indices(self, sequences: Dict[str, str]):
+        """One device FM index per contig over seq + '$' (bwt.py:3758-3790)."""
+        print("Building BWT indices...")
+        t0 = time.time()
+        items = list(sequences.items())
+        for i, (chrom, seq) in enumerate(items, 1):
+            pct = (i - 1) / len(items) * 100
+            print(f"\r  {pct:5.1f}% Building index for {chrom} ({len(seq):,} bp)", end="", flush=True)
+            self.bwt_cores[chrom] = BWTCore(seq + "$", self.sa_sample_rate, device=self.device)
+        print(f"\r  100.0% BWT indices built for {len(items)} chromosome(s) - {time.time() - t0:.1f}s     ")
+        print()
+
+    # ------------------------------------------------------------------ search
+    def _run(self, enable_tier2: bool, enable_tier3: bool, long_reads) -> RepeatList:
+        if enable_tier3 and long_reads:
+            raise NotImplementedError("Tier 3 long-read anchoring is not built yet (SURVEY.md §8(f) #3)")
+        if self.job is None:
+            self.load_reference()
+        job = self.job
+        job.reset()
+        if self.min_copies == 0 and enable_tier2:
+            # the reference worker raises ZeroDivisionError and returns [] (bwt.py:3095, 3137-3141)
+            for name in job.names:
+                print(f"ERROR processing chromosome {name}: integer division or modulo by zero")
+        job.set_tier2(enable_tier2)
+        from . import dist
+        if dist.is_distributed():
+            return dist.run_sharded(self, job)
+        job.scan(_lib.ctx(self.device))
+        job.postprocess()
+        return job.records()
+
+    def find_tandem_repeats(self, enable_tier1: bool = True, enable_tier2: bool = True,
+                            enable_tier3: bool = False, long_reads: Optional[List[str]] = None) -> RepeatList:
+        res = self._run(enable_tier2, enable_tier3, long_reads)
+        print(f"Analysis complete! Found {len(res)} total repeats.")
+        return res
+
+    def find_tandem_repeats_parallel(self, enable_tier1: bool = True, enable_tier2: bool = True,
+                                     enable_tier3: bool = False, long_reads: Optional[List[str]] = None,
+                                     n_jobs: Optional[int] = None) -> RepeatList:
+        res = self._run(enable_tier2, enable_tier3, long_reads)
+        print(f"Analysis complete! Found {len(res)} unique repeats.")
+        return res
+
+    # ------------------------------------------------------------------ output
+    def save_results(self, repeats, output_file: str, format_type: str = "bed"):
+        if format_type not in _lib.FMT:
+            raise ValueError(f"unknown format {format_type}")
+        if isinstance(repeats, RepeatList):
+            repeats.job.write(format_type, output_file)
+            return
+        if not repeats:
+            empty = self._new_job()
+            empty.write(format_type, output_file)
+            return
+        raise TypeError("save_results renders the records returned by find_tandem_repeats*")

@@ -150,6 +150,23 @@ class Job:
     def reset(self) -> None:
         check(lib().bwtmi_job_reset(self.h))
 
+    def set_tier2(self, on: bool) -> None:
+        self.params.tier2 = int(bool(on))
+        check(lib().bwtmi_job_set_params(self.h, C.byref(self.params)))
+
+    def set_build_index(self, on: bool) -> None:
+        self.params.build_index = int(bool(on))
+        check(lib().bwtmi_job_set_params(self.h, C.byref(self.params)))
+
+    def select(self, ids) -> None:
+        """Scan only these contig ids (this rank's shard); None = all."""
+        if ids is None:
+            check(lib().bwtmi_job_select(self.h, None, -1))
+            return
+        arr = np.asarray(list(ids), dtype=np.int32)
+        buf = arr if arr.size else np.zeros(1, dtype=np.int32)
+        check(lib().bwtmi_job_select(self.h, buf.ctypes.data_as(C.c_void_p), int(arr.size)))
+
     def add_hits(self, cid: int, hits: np.ndarray) -> None:
         """hits: int64[k,5] rows (start, end, unit_len, prim_len, copies)."""
         hits = np.asarray(hits, dtype=np.int64).reshape(-1, 5)

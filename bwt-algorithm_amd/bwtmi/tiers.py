@@ -1,0 +1,119 @@
+"""Detector classes of the reference (bwt.py:1387-3036).
+
+Tier2LCPFinder.find_long_unit_repeats_strict -- the detector that decides the
+CLI's repeat.tab -- runs on the device (libbwtmi strict scan); the LCP array
+comes from the device index.  The library-only finders that the CLI never
+calls are listed in SURVEY.md §8(f) as the next rows to build; until then
+they raise NotImplementedError instead of silently returning something else.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Set, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import Hit, check, lib
+from .motif import MotifUtils
+from .records import TandemRepeat
+
+
+def strict_scan_hits(text_arr: np.ndarray, min_unit: int, max_unit: int, min_copies: int,
+                     device: Optional[int] = None) -> np.ndarray:
+    """Device strict scan -> int64[k, 5] rows (start, end, unit_len, prim_len, copies)."""
+    t = np.ascontiguousarray(text_arr, dtype=np.uint8)
+    buf = t if t.size else np.zeros(1, dtype=np.uint8)
+    out = C.POINTER(Hit)()
+    n = C.c_int64()
+    check(lib().bwtmi_strict_scan(_lib.ctx(device), buf.ctypes.data_as(C.c_void_p), t.size, min_unit,
+                                  max_unit, 0, min_copies, C.byref(out), C.byref(n)))
+    try:
+        if n.value == 0:
+            return np.zeros((0, 5), dtype=np.int64)
+        raw = np.ctypeslib.as_array(C.cast(out, C.POINTER(C.c_int64)), shape=(n.value * 4,))
+        rec = raw.reshape(n.value, 4).copy()
+    finally:
+        lib().bwtmi_free(out)
+    res = np.empty((n.value, 5), dtype=np.int64)
+    res[:, 0] = rec[:, 0]
+    res[:, 1] = rec[:, 1]
+    res[:, 2] = rec[:, 2] & 0xFFFFFFFF
+    res[:, 3] = rec[:, 2] >> 32
+    res[:, 4] = rec[:, 3]
+    return res
+
+
+class Tier1STRFinder:
+    """bwt.py:1387-1862 -- library-only sliding-window finder (never reached by
+    the CLI: `--tier1` disables Tier 2 and the worker ignores Tier 1)."""
+
+    def __init__(self, text_arr: np.ndarray, max_motif_length: int = 9, show_progress: bool = False):
+        self.text_arr = text_arr
+        self.max_motif_length = max_motif_length
+        self.min_copies = 3
+        self.min_array_length = 6
+        self.min_entropy = 1.0
+        self.show_progress = show_progress
+
+    def find_strs(self, chromosome: str) -> List[TandemRepeat]:
+        raise NotImplementedError("Tier1STRFinder.find_strs: SURVEY.md §8(f) next #2 (not built yet)")
+
+
+class Tier2LCPFinder:
+    def __init__(self, bwt_core, min_period: int = 1, max_period: int = 1000, max_short_motif: int = 9,
+                 allow_mismatches: bool = True, show_progress: bool = False):
+        self.bwt = bwt_core
+        self.min_period = min_period
+        self.max_period = max_period
+        self.max_short_motif = max_short_motif
+        self.min_copies = 3
+        self.min_array_length = 6
+        self.min_entropy = 1.0
+        self.allow_mismatches = allow_mismatches
+        self.show_progress = show_progress
+        self.period_step = 1
+
+    def find_long_unit_repeats_strict(self, chromosome: str, min_unit_len: int = 20,
+                                      max_unit_len: int = 120, max_mismatch: int = 2,
+                                      min_copies: int = 3) -> List[TandemRepeat]:
+        """bwt.py:1891-2001 on the device (records built as bwt.py:1952-1993)."""
+        if max_mismatch != 0:
+            raise NotImplementedError("strict scan with max_mismatch > 0 is not built yet "
+                                      "(the CLI path uses max_mismatch=0, bwt.py:3105)")
+        t = self.bwt.text_arr
+        hits = strict_scan_hits(t, min_unit_len, max_unit_len, min_copies)
+        out = []
+        for s, e, L, p, c in hits.tolist():
+            motif = bytes(t[s:s + p]).decode("ascii", errors="replace")
+            pm, pi, sc, comp, ent, act = MotifUtils.calculate_trf_statistics(t, s, e, motif, c, 0.0)
+            out.append(TandemRepeat(
+                chrom=chromosome, start=s, end=e, motif=motif, copies=float(c), length=e - s, tier=2,
+                confidence=0.95, consensus_motif=motif, mismatch_rate=0.0,
+                max_mismatches_per_copy=0 if pm >= 99.9 else max_mismatch, n_copies_evaluated=c,
+                strand="+", percent_matches=pm, percent_indels=pi, score=sc, composition=comp,
+                entropy=ent, actual_sequence=act, variations=None))
+        return out
+
+    def _compute_lcp_array(self) -> np.ndarray:
+        """bwt.py:2108-2116 (Kasai) -- device LCP."""
+        if self.bwt.n == 0:
+            return np.zeros(0, dtype=np.int32)
+        return self.bwt.lcp_array()
+
+    def find_short_imperfect_repeats(self, chromosome: str, tier1_seen: Set[Tuple[int, int]]):
+        raise NotImplementedError("find_short_imperfect_repeats: FM seed-and-extend kernels are "
+                                  "the next §8 row (not built yet)")
+
+    def find_long_repeats(self, chromosome: str, tier1_seen=None):
+        raise NotImplementedError("find_long_repeats: out of scope (wall-clock-dependent results, "
+                                  "bwt.py:2236-2257)")
+
+
+class Tier3LongReadFinder:
+    def __init__(self, bwt_core, show_progress: bool = False):
+        self.bwt = bwt_core
+        self.show_progress = show_progress
+
+    def find_very_long_repeats(self, long_reads: List[str], chromosome: str):
+        raise NotImplementedError("Tier 3 long-read anchoring: SURVEY.md §8(f) next #3 (not built yet)")

@@ -1,6 +1,7 @@
 // api.cpp -- the extern "C" boundary of libbwtmi.so (include/bwtmi.h).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -141,6 +142,27 @@ int bwtmi_last_timing(bwtmi_ctx *ctx, double *out3) {
         out3[0] = ctx->c.last_total_ms;
         out3[1] = ctx->c.last_dom_ms;
         out3[2] = ctx->c.last_dom_launches;
+    });
+}
+
+int bwtmi_kernel_stats(bwtmi_ctx *ctx, int enable, int reset, char *out, int64_t cap) {
+    return guard([&] {
+        CHECK_ARG(ctx, "null ctx");
+        Ctx &c = ctx->c;
+        std::string s;
+        char line[160];
+        for (auto &k : c.kstats) {
+            snprintf(line, sizeof line, "%s %.6f %lld %.0f\n", k.first.c_str(), k.second.ms,
+                     (long long)k.second.launches, k.second.bytes);
+            s += line;
+        }
+        if (out && cap > 0) {
+            const size_t m = std::min<size_t>((size_t)cap - 1, s.size());
+            std::memcpy(out, s.data(), m);
+            out[m] = 0;
+        }
+        if (reset) c.kstats.clear();
+        c.ktiming = enable != 0;
     });
 }
 
@@ -347,6 +369,28 @@ int bwtmi_job_reset(bwtmi_job *job) {
     });
 }
 
+int bwtmi_job_set_params(bwtmi_job *job, const bwtmi_params *params) {
+    return guard([&] {
+        CHECK_ARG(job && params, "null argument");
+        job->j.params = *params;
+        if (job->j.params.sa_sample <= 0) job->j.params.sa_sample = 32;
+    });
+}
+
+int bwtmi_job_select(bwtmi_job *job, const int32_t *ids, int32_t n) {
+    return guard([&] {
+        CHECK_ARG(job && (ids || n <= 0), "bad argument");
+        Job &J = job->j;
+        J.selected.clear();
+        if (n < 0) return;
+        J.selected.assign(J.contigs.size(), 0);
+        for (int32_t k = 0; k < n; ++k) {
+            CHECK_ARG(ids[k] >= 0 && ids[k] < (int32_t)J.contigs.size(), "bad contig id");
+            J.selected[(size_t)ids[k]] = 1;
+        }
+    });
+}
+
 int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
     return guard([&] {
         CHECK_ARG(ctx && job, "null argument");
@@ -362,6 +406,7 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
         for (size_t i = 0; i < J.contigs.size(); ++i) {
             const Contig &ct = J.contigs[i];
             const int64_t len = ct.trimmed_len();
+            if (!J.selected.empty() && !J.selected[i]) continue;   // another rank's shard
             if (P.build_index) {   // BWTCore(seq + '$') of the worker (bwt.py:3053-3054)
                 auto ti = std::chrono::steady_clock::now();
                 DevContig &dc = job->dev.seqs[i];
@@ -536,7 +581,17 @@ int bwtmi_job_import(bwtmi_job *job, const uint8_t *buf, int64_t len) {
             o += w.var_len;
             job->j.final_recs.push_back(std::move(r));
         }
-        job->j.postprocessed = true;
+        // keep the reference's global order (natural chrom, start, end); every
+        // unit arrives whole from one rank, already in order
+        Job &J = job->j;
+        J.assign_units();
+        std::stable_sort(J.final_recs.begin(), J.final_recs.end(), [&](const Rec &a, const Rec &b) {
+            const int32_t ua = J.contigs[(size_t)a.chrom].unit, ub = J.contigs[(size_t)b.chrom].unit;
+            if (ua != ub) return ua < ub;
+            if (a.start != b.start) return a.start < b.start;
+            return a.end < b.end;
+        });
+        J.postprocessed = true;
     });
 }
 

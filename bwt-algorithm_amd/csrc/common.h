@@ -95,6 +95,7 @@ struct Job {
     std::vector<int32_t> unit_rank;                  // unit id -> rank by natural key
     std::vector<std::vector<Rec>> raw;               // per contig, worker output order
     std::vector<Rec> final_recs;                     // after bwt.py:3940-3944
+    std::vector<uint8_t> selected;                   // scan only these contigs (empty = all)
     bool postprocessed = false;
     double stage_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     void assign_units();

@@ -71,9 +71,55 @@ struct KernelTimer {
     int launches = 0;
 };
 
+struct KStat {
+    double ms = 0;
+    int64_t launches = 0;
+    double bytes = 0;   // algorithmic bytes (compulsory reads + writes) of those launches
+};
+
 struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // per-kernel HIP-event timing (on the ctx stream), enabled by bwtmi_kernel_stats
+    bool ktiming = false;
+    struct Pend {
+        std::string name;
+        hipEvent_t a, b;
+        double bytes;
+    };
+    std::vector<Pend> pending;
+    std::vector<std::pair<std::string, KStat>> kstats;
+    void kbegin(const char *name, double alg_bytes = 0) {
+        if (!ktiming) return;
+        hipEvent_t a, b;
+        HIPCHECK(hipEventCreate(&a));
+        HIPCHECK(hipEventCreate(&b));
+        HIPCHECK(hipEventRecord(a, stream));
+        pending.push_back({name, a, b, alg_bytes});
+    }
+    void kend() {
+        if (!ktiming || pending.empty()) return;
+        HIPCHECK(hipEventRecord(pending.back().b, stream));
+    }
+    void kresolve() {   // after a stream sync
+        for (auto &p : pending) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, p.a, p.b) != hipSuccess) ms = 0;
+            bool found = false;
+            for (auto &k : kstats)
+                if (k.first == p.name) {
+                    k.second.ms += ms;
+                    ++k.second.launches;
+                    k.second.bytes += p.bytes;
+                    found = true;
+                    break;
+                }
+            if (!found) kstats.push_back({p.name, KStat{ms, 1, p.bytes}});
+            (void)hipEventDestroy(p.a);
+            (void)hipEventDestroy(p.b);
+        }
+        pending.clear();
+    }
     DBuf slot[S_NSLOTS];
     HBuf host[4];
     hipEvent_t ev0 = nullptr, ev1 = nullptr;

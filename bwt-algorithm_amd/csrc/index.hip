@@ -380,8 +380,10 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     uint32_t *U2 = c.slot[S_MISC2].as<uint32_t>();
     uint32_t *SA = ix->sa.as<uint32_t>();
     HIPCHECK(hipMemcpyAsync(c.slot[S_MISC3].p, code, 256, hipMemcpyHostToDevice, st));
+    c.kbegin("sa_init_keys", (double)n * (1.0 + 12.0));   // text in, (key, value) out
     hipLaunchKernelGGL(k_init_keys, dim3(blocks(n)), dim3(256), 0, st, T, n, c.slot[S_MISC3].as<uint8_t>(), b, k, keys,
                        vals);
+    c.kend();
     radix_sort_pairs32(c, keys, vals, n, 0, ((b * k + 7) / 8) * 8);
     HIPCHECK(hipMemcpyAsync(SA, vals, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
     auto group_ids = [&](int64_t m) {   // head -> gid (group index), uses flag as scratch
@@ -425,14 +427,18 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     // ------------------------------------------------------------ BWT, Occ, sampled SA
     ix->bwt.ensure((size_t)n + 128);
     HIPCHECK(hipMemsetAsync(ix->bwt.p, 0, (size_t)n + 128, st));
+    c.kbegin("bwt_gather", (double)n * (4.0 + 1.0 + 1.0));   // SA in, text gather, BWT out
     hipLaunchKernelGGL(k_bwt, dim3(blocks(n)), dim3(256), 0, st, T, SA, n, ix->bwt.as<uint8_t>());
+    c.kend();
     const int64_t nblk = (n + occ_sample - 1) / occ_sample;
     ix->occ_len = 1 + n / occ_sample + (n % occ_sample != 0);   // == nblk + 1
     ix->occ.ensure((size_t)sigma * (nblk + 1) * 4);
     HIPCHECK(hipMemsetAsync(ix->occ.p, 0, (size_t)sigma * (nblk + 1) * 4, st));
     HIPCHECK(hipMemcpyAsync(c.slot[S_MISC3].p, present, 256, hipMemcpyHostToDevice, st));
+    c.kbegin("occ_blocks", (double)n + (double)sigma * (double)(nblk + 1) * 4.0);
     hipLaunchKernelGGL(k_occ_blocks, dim3(blocks(nblk * 64)), dim3(256), 0, st, ix->bwt.as<uint8_t>(), n, nblk,
                        occ_sample, c.slot[S_MISC3].as<uint8_t>(), sigma, ix->occ.as<uint32_t>());
+    c.kend();
     for (int cc = 0; cc < sigma; ++cc) {
         uint32_t *row = ix->occ.as<uint32_t>() + (int64_t)cc * (nblk + 1);
         exclusive_scan<uint32_t>(c, row, row, nblk + 1);
@@ -483,6 +489,7 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     }
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipStreamSynchronize(st));
+    c.kresolve();
     return ix;
 }
 

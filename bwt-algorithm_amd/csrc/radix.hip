@@ -174,10 +174,16 @@ void radix_sort_impl(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int b
     uint32_t *cnt = c.slot[S_SORT_HIST].as<uint32_t>();
     int passes = 0;
     for (int sh = bit0; sh < bit1; sh += 8) {
+        c.kbegin("radix_hist", (double)n * 8.0);                       // read keys once
         hipLaunchKernelGGL(k_hist, dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream, ka, cnt, n, sh, ntiles);
+        c.kend();
         exclusive_scan<uint32_t>(c, cnt, cnt, ntiles * 256);
+        // read (key, value) once, write it once
+        c.kbegin(sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16",
+                 (double)n * 2.0 * (8.0 + (vals ? (double)sizeof(V) : 0.0)));
         hipLaunchKernelGGL(k_scatter<V>, dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream, ka, va, kb, vb, cnt, n,
                            sh, ntiles);
+        c.kend();
         std::swap(ka, kb);
         std::swap(va, vb);
         ++passes;

@@ -403,9 +403,12 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
             HIPCHECK(hipEventCreate(&kb));
             HIPCHECK(hipEventRecord(ka, st));
         }
+        // compulsory traffic: the packed text once (0.25 B/base at 2 bits)
+        c.kbegin("k_runs", (double)n * (double)B / 8.0);
         if (B == 2) launch_runs<2>(c, P, n, lmin, lmax, min_copies, co);
         else if (B == 4) launch_runs<4>(c, P, n, lmin, lmax, min_copies, co);
         else launch_runs<8>(c, P, n, lmin, lmax, min_copies, co);
+        c.kend();
         HIPCHECK(hipGetLastError());
         if (c.timing) HIPCHECK(hipEventRecord(kb, st));
         HIPCHECK(hipMemcpyAsync(&ncand, c.slot[S_MISC3].p, sizeof ncand, hipMemcpyDeviceToHost, st));
@@ -463,6 +466,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
         HIPCHECK(hipMemcpyAsync(res.hits.data(), c.slot[S_HITS].p, (size_t)nh * sizeof(bwtmi_hit),
                                 hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
+    c.kresolve();
     if (c.timing) {
         float ms = 0;
         HIPCHECK(hipEventElapsedTime(&ms, c.ev0, c.ev1));

@@ -52,6 +52,11 @@ void bwtmi_free(void *p);
  * on the ctx stream: [0]=total device, [1]=dominant kernel, [2]=its launches */
 int bwtmi_last_timing(bwtmi_ctx *ctx, double *out3);
 
+/* per-kernel HIP-event timing on the ctx stream: enable=1 starts collecting,
+ * the call writes "name ms launches\n" lines of everything collected so far
+ * into out (cap bytes, NUL-terminated) and resets when reset=1 */
+int bwtmi_kernel_stats(bwtmi_ctx *ctx, int enable, int reset, char *out, int64_t cap);
+
 /* ------------------------------------------------------------ strict scan
  * Replaces Tier2LCPFinder.find_long_unit_repeats_strict (bwt.py:1891-2001),
  * as called by _process_chromosome_worker (bwt.py:3103-3106).
@@ -141,6 +146,9 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job);
 int bwtmi_job_upload(bwtmi_ctx *ctx, bwtmi_job *job);
 /* drop raw / final records so the job can be scanned again */
 int bwtmi_job_reset(bwtmi_job *job);
+int bwtmi_job_set_params(bwtmi_job *job, const bwtmi_params *params);
+/* restrict bwtmi_job_scan to the listed contigs (this rank's shard); n < 0 = all */
+int bwtmi_job_select(bwtmi_job *job, const int32_t *ids, int32_t n);
 /* alternatively feed raw hits computed elsewhere (one contig at a time) */
 int bwtmi_job_add_hits(bwtmi_job *job, int32_t contig_id, const bwtmi_hit *hits, int64_t n);
 int64_t bwtmi_job_raw_count(const bwtmi_job *job);

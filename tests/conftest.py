@@ -1,0 +1,38 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "bwt-algorithm_amd")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+for p in (REPO, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) device; runs the HIP path")
+    config.addinivalue_line("markers", "slow: large-input property tests")
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return GOLDEN
+
+
+@pytest.fixture(scope="session")
+def built_lib():
+    """libbwtmi.so built in-tree (the GPU box receives the prebuilt file)."""
+    so = os.path.join(PKG, "libbwtmi.so")
+    if not os.path.exists(so):
+        import subprocess
+        subprocess.run(["make", "-s", "-j8", "-C", PKG], check=True)
+    from bwtmi import _lib
+    return _lib.lib()
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx(built_lib):
+    from bwtmi import _lib
+    return _lib.ctx(0)     # raises (fails the test) when no gfx950 device is present

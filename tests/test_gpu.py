@@ -1,0 +1,262 @@
+"""Parity of the HIP path (through the C ABI) with the reference goldens and
+with the CPU oracle.  Integer/byte work: every comparison is exact."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from oracle import post
+
+pytestmark = pytest.mark.gpu
+
+
+def _rng_text(n, alphabet, seed):
+    r = np.random.default_rng(seed)
+    a = np.frombuffer(alphabet, dtype=np.uint8)
+    return a[r.integers(0, len(a), n)].tobytes()
+
+
+def _planted(n, seed, alphabet=b"ACGT", max_unit=200, density=0.3):
+    """Random text with planted perfect arrays of many unit lengths."""
+    r = np.random.default_rng(seed)
+    t = bytearray(_rng_text(n, alphabet, seed))
+    pos = 0
+    while pos < n:
+        pos += int(r.integers(20, 400))
+        L = int(r.choice([1, 2, 3, 4, 5, 6, 7, 12, 31, 32, 33, 63, 64, 65, 100, max_unit]))
+        c = int(r.integers(2, 9))
+        unit = _rng_text(L, alphabet, int(r.integers(1 << 30)))
+        arr = (unit * c)[: max(0, n - pos)]
+        t[pos:pos + len(arr)] = arr
+        pos += len(arr)
+    return bytes(t)
+
+
+def _gpu_hits(seq, min_unit, max_unit, mc):
+    from bwtmi.tiers import strict_scan_hits
+    return strict_scan_hits(np.frombuffer(seq, dtype=np.uint8), min_unit, max_unit, mc)
+
+
+def _same(seq, min_unit, max_unit, mc):
+    g = _gpu_hits(seq, min_unit, max_unit, mc)
+    o = oracle.strict_scan(seq, min_unit, max_unit, 0, mc)
+    assert g.shape == o.shape, (len(seq), max_unit, mc, g.shape, o.shape)
+    assert (g == o).all(), (len(seq), max_unit, mc)
+    return len(g)
+
+
+# ------------------------------------------------------------------ strict scan
+def test_strict_scan_reference_raw_hits(gpu_ctx, golden_dir):
+    with open(os.path.join(golden_dir, "rawhits.json")) as f:
+        raw = json.load(f)
+    for key, case in raw.items():
+        if case.get("max_mismatch", 0):
+            continue
+        seq = case["seq"].encode()
+        h = _gpu_hits(seq, 1, case["U"], case["min_copies"])
+        got = [[int(s), int(e), seq[s:s + p].decode(), int(c)] for s, e, L, p, c in h.tolist()]
+        assert got == case["hits"], key
+
+
+@pytest.mark.parametrize("n,alpha,seed", [
+    (1, b"ACGT", 1), (2, b"A", 1), (7, b"AC", 2), (64, b"A", 3), (200, b"AT", 4), (1000, b"ACGT", 5),
+    (5000, b"ACGT", 6), (5000, b"ACGTN", 7), (4000, b"ACGTNRYKM", 8), (3000, bytes(range(65, 90)), 9),
+    (20000, b"ACGT", 10), (100000, b"ACGT", 11)])
+def test_strict_scan_random_vs_oracle(gpu_ctx, n, alpha, seed):
+    seq = _planted(n, seed, alpha) if n > 100 else _rng_text(n, alpha, seed)
+    for mc in (2, 3, 4, 5):
+        U = max(120, min(n // mc, 1000))
+        _same(seq, 1, U, mc)
+    _same(seq, 3, 40, 3)
+
+
+def test_strict_scan_long_runs_and_streaks(gpu_ctx):
+    # homopolymers and long periodic arrays: runs spanning many 32-position words
+    parts = [b"A" * 5000, b"ACGT" * 700, b"G" * 33, b"CA" * 1000, _rng_text(997, b"ACGT", 3) * 4,
+             b"T" * 64, b"ACG" * 22, b"N" * 300]
+    seq = b"".join(parts)
+    for mc in (2, 3, 6):
+        _same(seq, 1, 1000, mc)
+
+
+def test_strict_scan_min_copies_one(gpu_ctx):
+    seq = _planted(600, 21)
+    _same(seq, 1, 200, 1)
+
+
+def test_strict_scan_synthetic_1mbp_vs_oracle(gpu_ctx):
+    from bwtmi import synth
+    for sub in (0.0, 0.02):
+        seq = synth.generate_contig(1_000_000, 40, sub)
+        assert _same(seq, 1, 1000, 3) > 1000
+
+
+# ------------------------------------------------------------------ CLI end to end
+def _cli(args):
+    d = dict(fmt="strfinder", mc=3, trim=30, tier2=True)
+    for i, x in enumerate(args):
+        if x == "--format":
+            d["fmt"] = args[i + 1]
+        elif x == "--min-copies":
+            d["mc"] = int(args[i + 1])
+        elif x == "--flank-trim":
+            d["trim"] = int(args[i + 1])
+        elif x == "--tier1":
+            d["tier2"] = False
+    return d
+
+
+def test_cli_outputs_match_reference_goldens(gpu_ctx, golden_dir, tmp_path):
+    from bwtmi import TandemRepeatFinder
+    with open(os.path.join(golden_dir, "expected_cli.json")) as f:
+        man = json.load(f)
+    for name, m in sorted(man.items()):
+        d = _cli(m["args"])
+        f = TandemRepeatFinder(os.path.join(golden_dir, "inputs", m["input"]), min_copies=d["mc"],
+                               flank_trim=d["trim"])
+        f.load_reference()
+        reps = f.find_tandem_repeats_parallel(True, d["tier2"], False, None)
+        out = tmp_path / f"{name}.out"
+        f.save_results(reps, str(out), d["fmt"])
+        assert hashlib.sha256(out.read_bytes()).hexdigest() == m["sha256"], name
+
+
+def test_cli_entry_point(gpu_ctx, golden_dir, tmp_path):
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    bwt = os.path.join(here, "..", "bwt-algorithm_amd", "bwt.py")
+    out = tmp_path / "repeat.tab"
+    subprocess.run([sys.executable, bwt, os.path.join(golden_dir, "inputs", "test.fa"), "-o", str(out),
+                    "--jobs", "0"], check=True, capture_output=True)
+    with open(os.path.join(golden_dir, "expected_cli.json")) as f:
+        want = json.load(f)["test.fa.strfinder"]["sha256"]
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == want
+
+
+def test_reference_unittest_on_device(gpu_ctx, golden_dir):
+    """The reference's tests/test_repeat_outputs.py, through the device path."""
+    from bwtmi import TandemRepeatFinder
+    f = TandemRepeatFinder(os.path.join(golden_dir, "inputs", "test2.fa"), show_progress=False,
+                           max_motif_length=12)
+    f.build_indices(f.load_reference())
+    reps = f.find_tandem_repeats(enable_tier1=True, enable_tier2=True, enable_tier3=False)
+    by = {}
+    for r in reps:
+        by.setdefault(r.chrom, []).append(r)
+    (r1,) = by["test1_PERFECT_7mer_5copies"]
+    assert (r1.start, r1.end, r1.motif, r1.variations) == (30, 65, "TCATCGG", None)
+    (r4,) = by["test4_INTERRUPTED_7mer_11copies"]
+    assert set(r4.variations) == {"6:5:C>A", "10:6:G>A", "11:0:ins(G)"}
+    motifs = {r.motif for r in by["test6_NESTED_long20_short4"]}
+    assert {"TGCTGATCGTAGCTAGCTGA", "TGCT"} <= motifs and "CTGA" not in motifs
+    (r12,) = by["test12_LONG_IMPERFECT_indel"]
+    assert any(v.startswith("9:10:del(") for v in r12.variations)
+
+
+def test_pipeline_seeded_imperfect_vs_oracle(gpu_ctx, tmp_path):
+    from bwtmi import TandemRepeatFinder, synth
+    fa = str(tmp_path / "imp.fa")
+    synth.write_fasta(fa, [60000, 25000], 0.03, first_index=900)
+    for fmt in ("strfinder", "vcf", "trf_table"):
+        f = TandemRepeatFinder(fa)
+        f.load_reference()
+        reps = f.find_tandem_repeats_parallel()
+        out = tmp_path / "o.tab"
+        f.save_results(reps, str(out), fmt)
+        assert out.read_text() == post.run_file(fa, fmt), fmt
+
+
+# ------------------------------------------------------------------ FM index
+def _check_index(text: bytes, golden=None):
+    from bwtmi import BWTCore
+    core = BWTCore(text.decode("latin-1"))
+    ref = oracle.Index(text) if golden is None else None
+    sa = core.suffix_array
+    if golden is not None:
+        assert (sa == golden["sa"]).all() and (core.bwt_arr == golden["bwt"]).all()
+        assert (core.lcp_array() == golden["lcp"]).all()
+        return core
+    assert (sa == ref.sa).all()
+    assert (core.bwt_arr == ref.bwt).all()
+    for c in ref.alphabet():
+        assert (core.occ_checkpoints[c] == ref.occ[c, :len(core.occ_checkpoints[c])]).all()
+        assert core.char_counts[chr(c)] == ref.C[c] and core.char_totals[chr(c)] == ref.totals[c]
+    assert core.sampled_sa == ref.sampled_sa
+    off, pos = core.kmer_csr()
+    assert (off == ref.kmer_offsets).all() and (pos == ref.kmer_pos).all()
+    assert (core.lcp_array() == ref.lcp()).all()
+    return core
+
+
+def test_index_matches_reference_goldens(gpu_ctx, golden_dir):
+    arrs = np.load(os.path.join(golden_dir, "index_arrays.npz"))
+    with open(os.path.join(golden_dir, "index_meta.json")) as f:
+        meta = json.load(f)
+    from bwtmi import BWTCore
+    for key, m in meta.items():
+        text = arrs[key + "__text"].tobytes()
+        core = _check_index(text, dict(sa=arrs[key + "__sa"], bwt=arrs[key + "__bwt"],
+                                       lcp=arrs[key + "__lcp"]))
+        for c, v in m["occ"].items():
+            assert core.occ_checkpoints[int(c)].tolist() == v, key
+        assert {str(k): v for k, v in core.sampled_sa.items()} == m["sampled"], key
+        assert {str(k): v for k, v in core.kmer_hash.items()} == m["kmer_hash"], key
+        for p, iv in m["backward"].items():
+            assert list(core.backward_search(p)) == iv, (key, p)
+        for p, pos in m["locate"].items():
+            assert core.locate_positions(p) == pos, (key, p)
+        for p, pos in m["kmer_positions"].items():
+            assert core.get_kmer_positions(p) == pos, (key, p)
+
+
+@pytest.mark.parametrize("n,alpha,seed", [(2, b"A", 1), (100, b"ACGT", 2), (5000, b"ACGT", 3),
+                                          (3000, b"ACGTN", 4), (2000, b"acgtNRY$", 5),
+                                          (200000, b"ACGT", 6)])
+def test_index_vs_oracle(gpu_ctx, n, alpha, seed):
+    body = _planted(n, seed, alpha) if n > 200 else _rng_text(n, alpha, seed)
+    _check_index(body + b"$")
+
+
+def test_index_repetitive_text(gpu_ctx):
+    _check_index(b"A" * 3000 + b"$")
+    _check_index((b"ACGTTGCA" * 500) + b"$")
+    _check_index(b"CA" * 2000 + b"C" + b"$")
+
+
+def test_backward_search_all_short_motifs(gpu_ctx):
+    from bwtmi import BWTCore, MotifUtils, synth
+    text = synth.generate_contig(50000, 77) + b"$"
+    core = BWTCore(text.decode())
+    ref = oracle.Index(text)
+    pats = [m for k in range(1, 7) for m in MotifUtils.enumerate_motifs(k)]
+    pats += ["ACGTACGTAC", "N", "", "TTTTTTTTTT", "GATTACA"]
+    got = core.backward_search_batch(pats)
+    for p, (sp, ep) in zip(pats, got.tolist()):
+        assert (sp, ep) == ref.backward_search(p.encode()), p
+
+
+def test_index_12mbp_properties(gpu_ctx):
+    """C4-size contig: SA is a permutation, adjacent suffixes ascend, BWT/occ consistent."""
+    from bwtmi import BWTCore, synth
+    text = synth.generate_contig(12_500_000, 3) + b"$"
+    core = BWTCore(text.decode())
+    sa = core.suffix_array.astype(np.int64)
+    n = len(text)
+    assert np.array_equal(np.sort(sa), np.arange(n))
+    assert sa[0] == n - 1
+    r = np.random.default_rng(0)
+    t = np.frombuffer(text, dtype=np.uint8)
+    for k in r.integers(1, n, 3000).tolist():
+        a, b = sa[k - 1], sa[k]
+        assert text[a:a + 4000] <= text[b:b + 4000], k
+    bwt = core.bwt_arr
+    assert (bwt == t[(sa - 1) % n]).all()
+    occ = core.occ_checkpoints
+    for c in (65, 67, 71, 84):
+        assert occ[c][-1] == int((t == c).sum())
+    off, pos = core.kmer_csr()
+    assert off[-1] == n - 8
