@@ -34,7 +34,7 @@ class Params(C.Structure):
 
 
 _lib = None
-_lock = threading.Lock()
+_lock = threading.RLock()    # ctx() -> lib() re-enters
 
 # name -> (restype, argtypes)
 _P = C.c_void_p

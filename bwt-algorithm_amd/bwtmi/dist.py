@@ -23,13 +23,13 @@ def _torch_dist():
 
 
 def is_distributed() -> bool:
-    try:
-        td = _torch_dist()
-    except Exception:
-        return False
-    if td.is_available() and td.is_initialized():
-        return td.get_world_size() > 1
-    return int(os.environ.get("WORLD_SIZE", "1")) > 1
+    """True under a multi-rank launch.  Never imports torch itself: the
+    single-GPU path stays torch-free (a cold torch import costs minutes)."""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return True
+    import sys
+    td = sys.modules.get("torch.distributed")
+    return bool(td is not None and td.is_available() and td.is_initialized() and td.get_world_size() > 1)
 
 
 def init(backend: Optional[str] = None):
