@@ -3,6 +3,7 @@
 // library is built with -ffp-contract=off so no FMA changes a rounding.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -14,26 +15,31 @@ namespace bwtmi {
 // Least rotation (Booth).  MotifUtils.get_canonical_motif takes the min over
 // all rotations (bwt.py:679-685); the least rotation string is unique, so any
 // exact algorithm yields the same string.
-std::string min_rotation(const std::string &s) {
-    const int64_t n = (int64_t)s.size();
-    if (n <= 1) return s;
-    std::vector<int64_t> f(2 * n, -1);
+static int64_t least_rotation(const char *s, int64_t n, std::vector<int64_t> &f) {
+    if (n <= 1) return 0;
+    f.assign((size_t)(2 * n), -1);
     int64_t k = 0;
-    auto at = [&](int64_t i) { return (unsigned char)s[(size_t)(i % n)]; };
+    auto at = [&](int64_t i) { return (unsigned char)s[i < n ? i : i - n]; };
     for (int64_t j = 1; j < 2 * n; ++j) {
-        unsigned char sj = at(j);
-        int64_t i = f[j - k - 1];
+        const unsigned char sj = at(j);
+        int64_t i = f[(size_t)(j - k - 1)];
         while (i != -1 && sj != at(k + i + 1)) {
             if (sj < at(k + i + 1)) k = j - i - 1;
-            i = f[i];
+            i = f[(size_t)i];
         }
         if (sj != at(k + i + 1)) {  // i == -1
             if (sj < at(k)) k = j;
-            f[j - k] = -1;
+            f[(size_t)(j - k)] = -1;
         } else {
-            f[j - k] = i + 1;
+            f[(size_t)(j - k)] = i + 1;
         }
     }
+    return k % n;
+}
+
+std::string min_rotation(const std::string &s) {
+    thread_local std::vector<int64_t> f;
+    const int64_t k = least_rotation(s.data(), (int64_t)s.size(), f);
     return s.substr((size_t)k) + s.substr(0, (size_t)k);
 }
 
@@ -47,22 +53,34 @@ static inline char comp_base(char c) {       // bwt.py:688-691
     }
 }
 
+// compare rotation a of x with rotation b of y (equal lengths n)
+static inline int rot_cmp(const char *x, int64_t a, const char *y, int64_t b, int64_t n) {
+    for (int64_t t = 0; t < n; ++t) {
+        const unsigned char p = (unsigned char)x[(a + t) % n], q = (unsigned char)y[(b + t) % n];
+        if (p != q) return p < q ? -1 : 1;
+    }
+    return 0;
+}
+
 void canonical_stranded(const std::string &s, std::string &canon, char &strand) {  // 694-716
-    if (s.empty()) {
-        canon = s;
+    const int64_t n = (int64_t)s.size();
+    if (n == 0) {
+        canon.clear();
         strand = '+';
         return;
     }
-    std::string rc(s.rbegin(), s.rend());
-    for (auto &c : rc) c = comp_base(c);
-    std::string f = min_rotation(s), r = min_rotation(rc);
-    if (f <= r) {
-        canon.swap(f);
-        strand = '+';
-    } else {
-        canon.swap(r);
-        strand = '-';
-    }
+    thread_local std::vector<int64_t> f;
+    thread_local std::string rc;
+    rc.resize((size_t)n);
+    for (int64_t i = 0; i < n; ++i) rc[(size_t)i] = comp_base(s[(size_t)(n - 1 - i)]);
+    const int64_t kf = least_rotation(s.data(), n, f);
+    const int64_t kr = least_rotation(rc.data(), n, f);
+    const bool fwd = rot_cmp(s.data(), kf, rc.data(), kr, n) <= 0;
+    const std::string &src = fwd ? s : rc;
+    const int64_t k = fwd ? kf : kr;
+    canon.resize((size_t)n);
+    for (int64_t t = 0; t < n; ++t) canon[(size_t)t] = src[(size_t)((k + t) % n)];
+    strand = fwd ? '+' : '-';
 }
 
 int64_t smallest_period(const char *s, int64_t n) {   // bwt.py:1125-1133
@@ -123,34 +141,45 @@ int64_t trf_score(int64_t length, double mm) {      // bwt.py:1313-1333
 }
 
 // ------------------------------------------------------------------------
-// MotifUtils._align_unit_to_window (bwt.py:829-983), banded storage.
-// Cells outside the computed band read as the reference's `inf`; row 0 and
-// column 0 hold the reference's initialisation.  Ties keep sub > del > ins.
+// MotifUtils._align_unit_to_window (bwt.py:829-983) and align_repeat_region
+// (998-1102).  Banded storage: row i keeps columns i-band..i+band; cells
+// outside the computed band read as the reference's `inf`, row 0 / column 0
+// hold its initialisation.  Ties keep sub > del > ins.  All scratch is
+// thread-local and reused: no allocation per copy.
 // ------------------------------------------------------------------------
 namespace {
 
-struct Op {
-    char kind;      // 's' sub, 'i' ins, 'd' del
-    int64_t pos;
-    char ref, alt;  // sub
-    std::string ins;
-    int64_t len = 0;
-};
-
-struct UnitResult {
-    int64_t consumed = 0;
-    int64_t n_sub = 0, n_ins = 0, n_del = 0;
-    std::vector<Op> ops;
-    std::vector<std::pair<int64_t, char>> observed;
-};
-
-struct DPBuf {
+struct Scratch {
     std::vector<int32_t> cost;
     std::vector<char> ptr;
+    std::vector<char> cref, cqry;              // aligned columns (reversed)
+    std::vector<int64_t> obs_idx;              // observed bases of the current copy
+    std::vector<char> obs_base;
+    std::string ops;                           // formatted ops of the current copy ("" parts)
+    std::vector<uint32_t> op_end;              // piece boundaries in ops
+    // per-position Counter in insertion order: up to 8 inline entries, overflow vector
+    std::vector<char> pc_c;
+    std::vector<int64_t> pc_n;
+    std::vector<uint8_t> pc_k;
+    std::vector<std::vector<std::pair<char, int64_t>>> pc_over;
 };
 
-bool align_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_t max_indel,
-                int64_t tol, DPBuf &buf, UnitResult &res) {
+constexpr int KIN = 8;
+
+struct UnitOut {
+    int64_t consumed = 0, n_sub = 0, n_ins = 0, n_del = 0;
+};
+
+inline void put_num(std::string &s, int64_t v) {
+    char b[24];
+    int n = snprintf(b, sizeof b, "%lld", (long long)v);
+    s.append(b, (size_t)n);
+}
+
+// ops of one copy are formatted with a placeholder-free prefix; the copy index
+// is prepended when the copy is accepted (ops hold "pos:..." pieces)
+bool align_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_t max_indel, int64_t tol,
+                Scratch &S, UnitOut &res) {
     if (m == 0 || n == 0) return false;
     max_indel = std::max<int64_t>(0, max_indel);
     tol = std::max<int64_t>(0, tol);
@@ -159,29 +188,36 @@ bool align_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_
     if (lower > upper) return false;
     const int64_t INF = m + n + 10;
     const int64_t band = max_indel + 2;
-    const int64_t W = 2 * band + 1;  // row i stores columns i-band .. i+band
-    buf.cost.assign((size_t)((m + 1) * W), (int32_t)INF);
-    buf.ptr.assign((size_t)((m + 1) * W), 0);
-    auto inb = [&](int64_t i, int64_t j) { return j >= i - band && j <= i + band; };
+    const int64_t W = 2 * band + 1;
+    const size_t cells = (size_t)((m + 1) * W);
+    if (S.cost.size() < cells) {
+        S.cost.resize(cells);
+        S.ptr.resize(cells);
+    }
+    int32_t *cost = S.cost.data();
+    char *ptr = S.ptr.data();
+    std::fill(cost, cost + cells, (int32_t)INF);
     auto get = [&](int64_t i, int64_t j) -> int64_t {
-        if (i == 0) return j;        // dp[0][j] = j (j <= n)
-        if (j == 0) return i;        // dp[i][0] = i
-        if (!inb(i, j)) return INF;
-        return buf.cost[(size_t)(i * W + (j - i + band))];
+        if (i == 0) return j;
+        if (j == 0) return i;
+        if (j < i - band || j > i + band) return INF;
+        return cost[i * W + (j - i + band)];
     };
     for (int64_t i = 1; i <= m; ++i) {
         const int64_t jmin = std::max<int64_t>(1, i - band), jmax = std::min<int64_t>(n, i + band);
         const char mi = motif[i - 1];
+        int32_t *row = cost + i * W + band - i;   // row[j]
+        char *prow = ptr + i * W + band - i;
         for (int64_t j = jmin; j <= jmax; ++j) {
             const bool eq = mi == win[j - 1];
             int64_t best = get(i - 1, j - 1) + (eq ? 0 : 1);
             char op = eq ? 'M' : 'S';
             const int64_t dc = get(i - 1, j) + 1;
             if (dc < best) { best = dc; op = 'D'; }
-            const int64_t ic = get(i, j - 1) + 1;
+            const int64_t ic = (j - 1 == 0) ? i + 1 : (j - 1 >= jmin ? row[j - 1] + 1 : INF + 1);
             if (ic < best) { best = ic; op = 'I'; }
-            buf.cost[(size_t)(i * W + (j - i + band))] = (int32_t)best;
-            buf.ptr[(size_t)(i * W + (j - i + band))] = op;
+            row[j] = (int32_t)best;
+            prow[j] = op;
         }
     }
     int64_t bj = -1, bc = INF;
@@ -190,102 +226,129 @@ bool align_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_
         if (c < bc) { bc = c; bj = j; }
     }
     if (bj <= 0 || bc >= INF) return false;
-    auto ptr = [&](int64_t i, int64_t j) -> char {
-        if (i == 0 && j == 0) return 0;
-        if (i == 0) return 'I';
-        if (j == 0) return 'D';
-        if (!inb(i, j)) return 0;
-        return buf.ptr[(size_t)(i * W + (j - i + band))];
-    };
-    // traceback into aligned columns (ref, query); '-' = gap
-    std::vector<std::pair<char, char>> cols;
-    cols.reserve((size_t)(m + n));
+    // traceback (columns collected in reverse)
+    S.cref.clear();
+    S.cqry.clear();
     int64_t i = m, j = bj;
     while (i > 0 || j > 0) {
-        const char op = ptr(i, j);
-        if (op == 'M' || op == 'S') { cols.push_back({motif[i - 1], win[j - 1]}); --i; --j; }
-        else if (op == 'D') { cols.push_back({motif[i - 1], '-'}); --i; }
-        else if (op == 'I') { cols.push_back({'-', win[j - 1]}); --j; }
+        char op;
+        if (i == 0) op = 'I';
+        else if (j == 0) op = 'D';
+        else if (j < i - band || j > i + band) op = 0;
+        else op = ptr[i * W + (j - i + band)];
+        if (op == 'M' || op == 'S') { S.cref.push_back(motif[i - 1]); S.cqry.push_back(win[j - 1]); --i; --j; }
+        else if (op == 'D') { S.cref.push_back(motif[i - 1]); S.cqry.push_back('-'); --i; }
+        else if (op == 'I') { S.cref.push_back('-'); S.cqry.push_back(win[j - 1]); --j; }
         else break;
     }
-    std::reverse(cols.begin(), cols.end());
-    res.ops.clear();
-    res.observed.clear();
+    S.obs_idx.clear();
+    S.obs_base.clear();
+    S.ops.clear();
+    S.op_end.clear();
     res.n_sub = res.n_ins = res.n_del = 0;
     int64_t ref = 0;
-    std::string ins_buf;
+    size_t ins_from = 0;
+    bool ins_open = false;
     int64_t ins_at = 0, del_len = 0, del_at = 0;
-    for (auto &rq : cols) {
-        const char r = rq.first, q = rq.second;
+    std::string &o = S.ops;
+    auto flush_ins = [&](size_t upto) {   // columns ins_from..upto-1 (forward order) are insertions
+        o.push_back(':');
+        put_num(o, ins_at);
+        o.append(":ins(");
+        for (size_t q = ins_from; q < upto; ++q) o.push_back(S.cqry[S.cqry.size() - 1 - q]);
+        o.push_back(')');
+        S.op_end.push_back((uint32_t)o.size());
+        res.n_ins += (int64_t)(upto - ins_from);
+    };
+    auto flush_del = [&]() {
+        o.push_back(':');
+        put_num(o, del_at);
+        o.append(":del(");
+        put_num(o, del_len);
+        o.push_back(')');
+        S.op_end.push_back((uint32_t)o.size());
+        res.n_del += del_len;
+    };
+    const size_t ncols = S.cref.size();
+    for (size_t q = 0; q < ncols; ++q) {
+        const char r = S.cref[ncols - 1 - q], qq = S.cqry[ncols - 1 - q];
         if (r == '-') {
-            if (ins_buf.empty()) ins_at = ref;
-            ins_buf.push_back(q);
+            if (!ins_open) { ins_at = ref; ins_from = q; ins_open = true; }
             continue;
         }
-        if (!ins_buf.empty()) {
-            Op o; o.kind = 'i'; o.pos = ins_at; o.ins = ins_buf;
-            res.n_ins += (int64_t)ins_buf.size();
-            res.ops.push_back(std::move(o));
-            ins_buf.clear();
-            ins_at = 0;
-        }
+        if (ins_open) { flush_ins(q); ins_open = false; ins_at = 0; }
         ++ref;
-        if (q == '-') {
+        if (qq == '-') {
             if (del_len == 0) del_at = ref;
             ++del_len;
             continue;
         }
-        if (del_len) {
-            Op o; o.kind = 'd'; o.pos = del_at; o.len = del_len;
-            res.n_del += del_len;
-            res.ops.push_back(std::move(o));
-            del_len = 0;
-        }
-        res.observed.push_back({ref - 1, q});
-        if (r != q) {
-            Op o; o.kind = 's'; o.pos = ref; o.ref = r; o.alt = q;
-            res.ops.push_back(std::move(o));
+        if (del_len) { flush_del(); del_len = 0; }
+        S.obs_idx.push_back(ref - 1);
+        S.obs_base.push_back(qq);
+        if (r != qq) {
+            o.push_back(':');
+            put_num(o, ref);
+            o.push_back(':');
+            o.push_back(r);
+            o.push_back('>');
+            o.push_back(qq);
+            S.op_end.push_back((uint32_t)o.size());
             ++res.n_sub;
         }
     }
-    if (!ins_buf.empty()) {
-        Op o; o.kind = 'i'; o.pos = ins_at; o.ins = ins_buf;
-        res.n_ins += (int64_t)ins_buf.size();
-        res.ops.push_back(std::move(o));
-    }
-    if (del_len) {
-        Op o; o.kind = 'd'; o.pos = del_at; o.len = del_len;
-        res.n_del += del_len;
-        res.ops.push_back(std::move(o));
-    }
+    if (ins_open) flush_ins(ncols);
+    if (del_len) flush_del();
     if (res.n_sub > tol) return false;
     if (res.n_ins > max_indel || res.n_del > max_indel) return false;
     res.consumed = bj;
     return true;
 }
 
-// per-position Counter with insertion order (most_common(1) = first max)
-struct PosCount {
-    std::vector<std::pair<char, int64_t>> v;
-    void add(char b) {
-        for (auto &p : v)
-            if (p.first == b) { ++p.second; return; }
-        v.push_back({b, 1});
-    }
-    bool empty() const { return v.empty(); }
-    char top() const {
-        char b = v[0].first;
-        int64_t c = v[0].second;
-        for (size_t k = 1; k < v.size(); ++k)
-            if (v[k].second > c) { c = v[k].second; b = v[k].first; }
-        return b;
-    }
-};
+inline void pc_reset(Scratch &S, int64_t m) {
+    S.pc_c.assign((size_t)(m * KIN), 0);
+    S.pc_n.assign((size_t)(m * KIN), 0);
+    S.pc_k.assign((size_t)m, 0);
+    if ((int64_t)S.pc_over.size() < m) S.pc_over.resize((size_t)m);
+    for (int64_t p = 0; p < m; ++p) S.pc_over[(size_t)p].clear();
+}
 
-void consensus_from(const std::vector<PosCount> &pc, const std::string &fallback, std::string &out) {
-    out.resize(pc.size());
-    for (size_t i = 0; i < pc.size(); ++i)
-        out[i] = !pc[i].empty() ? pc[i].top() : (i < fallback.size() ? fallback[i] : 'N');
+inline void pc_add(Scratch &S, int64_t p, char b) {
+    char *c = &S.pc_c[(size_t)(p * KIN)];
+    int64_t *n = &S.pc_n[(size_t)(p * KIN)];
+    const int k = S.pc_k[(size_t)p];
+    for (int t = 0; t < k; ++t)
+        if (c[t] == b) { ++n[t]; return; }
+    auto &ov = S.pc_over[(size_t)p];
+    for (auto &e : ov)
+        if (e.first == b) { ++e.second; return; }
+    if (k < KIN) { c[k] = b; n[k] = 1; S.pc_k[(size_t)p] = (uint8_t)(k + 1); }
+    else ov.push_back({b, 1});
+}
+
+// Counter.most_common(1): first maximal entry in insertion order
+inline bool pc_top(const Scratch &S, int64_t p, char &out) {
+    const int k = S.pc_k[(size_t)p];
+    if (k == 0) return false;
+    const char *c = &S.pc_c[(size_t)(p * KIN)];
+    const int64_t *n = &S.pc_n[(size_t)(p * KIN)];
+    char b = c[0];
+    int64_t best = n[0];
+    for (int t = 1; t < k; ++t)
+        if (n[t] > best) { best = n[t]; b = c[t]; }
+    for (auto &e : S.pc_over[(size_t)p])
+        if (e.second > best) { best = e.second; b = e.first; }
+    out = b;
+    return true;
+}
+
+void consensus_from(const Scratch &S, int64_t m, const std::string &fallback, std::string &out) {
+    out.resize((size_t)m);
+    for (int64_t i = 0; i < m; ++i) {
+        char b;
+        if (pc_top(S, i, b)) out[(size_t)i] = b;
+        else out[(size_t)i] = (size_t)i < fallback.size() ? fallback[(size_t)i] : 'N';
+    }
 }
 
 }  // namespace
@@ -300,41 +363,53 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
     const int64_t tol = std::max<int64_t>(1, (int64_t)std::floor((double)m * frac));
     const int64_t max_indel = max_indel_arg < 0 ? std::max<int64_t>(1, std::min<int64_t>(10, m >= 4 ? m / 2 : 1))
                                                 : max_indel_arg;
-    std::vector<PosCount> pc((size_t)m);
+    thread_local Scratch S;
+    pc_reset(S, m);
     out.copy_len.clear();
-    std::vector<std::vector<Op>> ops_by_copy;
-    std::vector<int64_t> errs;
+    out.copy_err.clear();
+    out.variations.clear();
+    out.any_variation = false;
     int64_t tot_ins = 0, tot_del = 0;
-    std::string cur = tmpl, next;
+    thread_local std::string cur, nxt;
+    cur = tmpl;
     int64_t pos = start;
     const int64_t limit = std::min<int64_t>(
         seq_len, std::max<int64_t>(end, start + m * min_copies) + std::max<int64_t>(m * 3, max_indel * 4));
-    thread_local DPBuf buf;
-    UnitResult res;
+    UnitOut res;
+    int64_t copies = 0;
     while (pos < limit) {
         const int64_t wend = std::min<int64_t>(seq_len, pos + m + max_indel);
         const int64_t wlen = wend - pos;
         if (wlen < m - max_indel) break;
-        if (!align_unit(cur.data(), m, seq + pos, wlen, max_indel, tol, buf, res) || res.consumed == 0)
-            break;
-        ops_by_copy.push_back(res.ops);
-        errs.push_back(res.n_sub + res.n_ins + res.n_del);
+        if (!align_unit(cur.data(), m, seq + pos, wlen, max_indel, tol, S, res) || res.consumed == 0) break;
+        ++copies;
+        // variation pieces "copy:pos:..." in op order (bwt.py:1073-1088)
+        uint32_t from = 0;
+        for (uint32_t e : S.op_end) {
+            if (out.any_variation) out.variations.push_back(';');
+            put_num(out.variations, copies);
+            out.variations.append(S.ops, from, e - from);
+            out.any_variation = true;
+            from = e;
+        }
+        out.copy_err.push_back(res.n_sub + res.n_ins + res.n_del);
         out.copy_len.push_back(res.consumed);
         tot_ins += res.n_ins;
         tot_del += res.n_del;
-        for (auto &ob : res.observed)
-            if (ob.first >= 0 && ob.first < m) pc[(size_t)ob.first].add(ob.second);
+        for (size_t q = 0; q < S.obs_idx.size(); ++q) {
+            const int64_t idx = S.obs_idx[q];
+            if (idx >= 0 && idx < m) pc_add(S, idx, S.obs_base[q]);
+        }
         pos += res.consumed;
-        consensus_from(pc, cur, next);
-        cur.swap(next);
+        consensus_from(S, m, cur, nxt);
+        cur.swap(nxt);
     }
-    const int64_t copies = (int64_t)errs.size();
     if (copies < min_copies) return false;
     const int64_t consumed = pos - start;
     if (consumed <= 0) return false;
-    consensus_from(pc, cur, out.consensus);
+    consensus_from(S, m, cur, out.consensus);
     int64_t tot = 0, mx = 0;
-    for (auto e : errs) { tot += e; mx = std::max(mx, e); }
+    for (auto e : out.copy_err) { tot += e; mx = std::max(mx, e); }
     const int64_t denom = copies * m;
     out.motif_len = m;
     out.copies = copies;
@@ -343,31 +418,6 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
     out.max_errors = mx;
     out.tot_ins = tot_ins;
     out.tot_del = tot_del;
-    out.copy_err = errs;
-    out.variations.clear();
-    out.any_variation = false;
-    char tmp[64];
-    for (size_t k = 0; k < ops_by_copy.size(); ++k) {
-        const long long idx = (long long)k + 1;
-        for (auto &o : ops_by_copy[k]) {
-            std::string piece;
-            if (o.kind == 's') {
-                snprintf(tmp, sizeof tmp, "%lld:%lld:", idx, (long long)o.pos);
-                piece = std::string(tmp) + o.ref + ">" + o.alt;
-            } else if (o.kind == 'i') {
-                if (o.ins.empty()) continue;
-                snprintf(tmp, sizeof tmp, "%lld:%lld:ins(", idx, (long long)o.pos);
-                piece = std::string(tmp) + o.ins + ")";
-            } else {
-                if (o.len <= 0) continue;
-                snprintf(tmp, sizeof tmp, "%lld:%lld:del(%lld)", idx, (long long)o.pos, (long long)o.len);
-                piece = tmp;
-            }
-            if (out.any_variation) out.variations.push_back(';');
-            out.variations += piece;
-            out.any_variation = true;
-        }
-    }
     return true;
 }
 

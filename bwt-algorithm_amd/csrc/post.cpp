@@ -4,8 +4,11 @@
 // Work is organised per "fold unit": the contigs whose natural sort keys are
 // equal (normally exactly one contig).  Every stage of the reference either
 // groups by chromosome or folds over the globally sorted list with a
-// same-chromosome test, so units are independent and run on separate host
-// threads; inside a unit the reference's sequential order is kept.
+// same-chromosome test, so units are independent.  Inside a unit every stage
+// is either data-parallel (record construction, nested-suppression queries,
+// refine, restore) or a fold that is parallelised speculatively and then
+// repaired to the exact sequential result (merge), so the output is the
+// reference's regardless of the thread count.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -13,7 +16,6 @@
 #include <functional>
 #include <string>
 #include <thread>
-#include <unordered_map>
 #include <vector>
 
 #include "common.h"
@@ -25,6 +27,43 @@ int host_threads(const bwtmi_params &p) {
     unsigned hc = std::thread::hardware_concurrency();
     int t = hc ? (int)hc : 4;
     return std::min(t, 16);
+}
+
+// fn(begin, end) over [0, n) in `nt` contiguous chunks
+template <class F>
+static void parallel_for(int64_t n, int nt, F &&fn) {
+    if (n <= 0) return;
+    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, (n + 1023) / 1024));
+    if (nt <= 1) {
+        fn((int64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve((size_t)nt);
+    for (int t = 0; t < nt; ++t) {
+        const int64_t a = n * t / nt, b = n * (t + 1) / nt;
+        th.emplace_back([&fn, a, b] { fn(a, b); });
+    }
+    for (auto &x : th) x.join();
+}
+
+// dynamic scheduling over items (uneven costs)
+template <class F>
+static void parallel_items(int64_t n, int nt, F &&fn) {
+    if (n <= 0) return;
+    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n));
+    std::atomic<int64_t> next{0};
+    auto work = [&] {
+        for (;;) {
+            const int64_t k = next.fetch_add(1);
+            if (k >= n) break;
+            fn(k);
+        }
+    };
+    if (nt == 1) { work(); return; }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back(work);
+    for (auto &x : th) x.join();
 }
 
 // ------------------------------------------------------------ natural key
@@ -57,10 +96,8 @@ int natural_cmp(const std::vector<NatPart> &a, const std::vector<NatPart> &b) {
     for (size_t i = 0; i < n; ++i) {
         const NatPart &x = a[i], &y = b[i];
         if (x.digit != y.digit) return x.digit ? -1 : 1;  // (0, int) < (1, str)
-        if (x.digit) {
-            if (x.text.size() != y.text.size()) return x.text.size() < y.text.size() ? -1 : 1;
-        }
-        int c = x.text.compare(y.text);
+        if (x.digit && x.text.size() != y.text.size()) return x.text.size() < y.text.size() ? -1 : 1;
+        const int c = x.text.compare(y.text);
         if (c) return c < 0 ? -1 : 1;
     }
     if (a.size() != b.size()) return a.size() < b.size() ? -1 : 1;
@@ -72,9 +109,8 @@ void Job::assign_units() {
     for (auto &c : contigs) natkeys.push_back(natural_key(c.name));
     std::vector<int32_t> order(contigs.size());
     for (size_t i = 0; i < order.size(); ++i) order[i] = (int32_t)i;
-    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
-        return natural_cmp(natkeys[a], natkeys[b]) < 0;
-    });
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int32_t a, int32_t b) { return natural_cmp(natkeys[a], natkeys[b]) < 0; });
     nunits = 0;
     unit_rank.clear();
     for (size_t k = 0; k < order.size(); ++k) {
@@ -95,37 +131,76 @@ void strict_hits_to_records(const Job &job, int32_t contig, const bwtmi_hit *hit
                             std::vector<Rec> &out) {
     const Contig &c = job.contigs[(size_t)contig];
     const char *t = c.trimmed();
-    out.reserve(out.size() + (size_t)n);
-    for (int64_t k = 0; k < n; ++k) {
-        const bwtmi_hit &h = hits[k];
-        Rec r;
-        r.chrom = contig;
-        r.tier = 2;
-        r.start = h.start;
-        r.end = h.end;
-        r.length = h.end - h.start;
-        r.motif.assign(t + h.start, (size_t)h.prim_len);
-        r.copies = (double)h.copies;
-        r.confidence = 0.95;
-        r.mismatch_rate = 0.0;
-        r.max_mm = 0;
-        r.n_eval = h.copies;
-        r.strand = '+';
-        r.pmatch = (1.0 - 0.0) * 100.0;
-        r.pindel = 0.0;
-        r.score = trf_score(r.length, 0.0);
-        r.act_kind = ACT_TRIMMED;
-        r.act_off = h.start;
-        r.act_len = h.end - h.start;
-        out.push_back(std::move(r));
-    }
+    const size_t base = out.size();
+    out.resize(base + (size_t)n);
+    parallel_for(n, host_threads(job.params), [&](int64_t a, int64_t b) {
+        for (int64_t k = a; k < b; ++k) {
+            const bwtmi_hit &h = hits[k];
+            Rec &r = out[base + (size_t)k];
+            r.chrom = contig;
+            r.tier = 2;
+            r.start = h.start;
+            r.end = h.end;
+            r.length = h.end - h.start;
+            r.motif.assign(t + h.start, (size_t)h.prim_len);
+            r.copies = (double)h.copies;
+            r.confidence = 0.95;
+            r.mismatch_rate = 0.0;
+            r.max_mm = 0;
+            r.n_eval = h.copies;
+            r.strand = '+';
+            r.pmatch = (1.0 - 0.0) * 100.0;
+            r.pindel = 0.0;
+            r.score = trf_score(r.length, 0.0);
+            r.act_kind = ACT_TRIMMED;
+            r.act_off = h.start;
+            r.act_len = h.end - h.start;
+        }
+    });
 }
 
 namespace {
 
-inline bool key_less(const Rec &a, const Rec &b) {   // (natural(chrom), start, end) in a unit
-    if (a.start != b.start) return a.start < b.start;
-    return a.end < b.end;
+// stable sort of records by (start, end): sort compact keys, then permute
+void sort_by_pos(std::vector<Rec> &v, int nt) {
+    const size_t n = v.size();
+    if (n < 2) return;
+    bool sorted = true;
+    for (size_t i = 1; i < n && sorted; ++i)
+        sorted = v[i - 1].start < v[i].start || (v[i - 1].start == v[i].start && v[i - 1].end <= v[i].end);
+    if (sorted) return;
+    struct K { int64_t s, e; uint32_t i; };
+    std::vector<K> k(n);
+    for (size_t i = 0; i < n; ++i) k[i] = {v[i].start, v[i].end, (uint32_t)i};
+    auto lt = [](const K &a, const K &b) {
+        if (a.s != b.s) return a.s < b.s;
+        if (a.e != b.e) return a.e < b.e;
+        return a.i < b.i;
+    };
+    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, n / 65536 + 1));
+    if (T == 1) {
+        std::sort(k.begin(), k.end(), lt);
+    } else {
+        std::vector<size_t> cut(T + 1);
+        for (int t = 0; t <= T; ++t) cut[t] = n * (size_t)t / (size_t)T;
+        parallel_for(T, T, [&](int64_t a, int64_t b) {
+            for (int64_t t = a; t < b; ++t) std::sort(k.begin() + cut[t], k.begin() + cut[t + 1], lt);
+        });
+        for (int w = 1; w < T; w *= 2) {    // pairwise merges, each level in parallel
+            std::vector<std::pair<size_t, std::pair<size_t, size_t>>> jobs;
+            for (int t = 0; t + w < T; t += 2 * w)
+                jobs.push_back({cut[t], {cut[t + w], cut[std::min(T, t + 2 * w)]}});
+            parallel_items((int64_t)jobs.size(), nt, [&](int64_t q) {
+                auto &j = jobs[(size_t)q];
+                std::inplace_merge(k.begin() + j.first, k.begin() + j.second.first, k.begin() + j.second.second, lt);
+            });
+        }
+    }
+    std::vector<Rec> out(n);
+    parallel_for((int64_t)n, nt, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) out[(size_t)i] = std::move(v[k[(size_t)i].i]);
+    });
+    v.swap(out);
 }
 
 // ---------------------------------------------------- nested suppression
@@ -133,66 +208,68 @@ inline bool key_less(const Rec &a, const Rec &b) {   // (natural(chrom), start, 
 // longer motif; the stable sort by (mismatch_rate > 0, -len(motif)) places
 // every such span of its class (and the whole perfect class) before it, and
 // repeats of equal motif length never test each other.  So each (class,
-// length) group is screened against the spans kept so far and appended as a
-// whole.  Kept spans live in a bucket grid for the overlap queries; the
+// length) group is screened -- in parallel, against a frozen grid of the
+// spans kept so far -- and its survivors are appended as a whole.  The
 // predicate is the reference's, division for division.
-std::vector<Rec> suppress_nested_chrom(std::vector<Rec> &rs, double thr) {
+std::vector<Rec> suppress_nested_chrom(std::vector<Rec> &rs, double thr, int nt) {
     const size_t n = rs.size();
-    std::vector<uint32_t> order(n);
-    for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-        const bool ia = rs[a].mismatch_rate > 0, ib = rs[b].mismatch_rate > 0;
-        if (ia != ib) return !ia;
-        return rs[a].motif.size() > rs[b].motif.size();
-    });
+    // stable counting sort by (class, motif length desc)
+    size_t maxlen = 0;
+    for (auto &r : rs) maxlen = std::max(maxlen, r.motif.size());
+    const size_t nb = 2 * (maxlen + 1);
+    auto bucket = [&](const Rec &r) { return (r.mismatch_rate > 0 ? (maxlen + 1) : 0) + (maxlen - r.motif.size()); };
+    std::vector<uint32_t> cnt(nb + 1, 0), order(n);
+    for (auto &r : rs) ++cnt[bucket(r) + 1];
+    for (size_t b = 0; b < nb; ++b) cnt[b + 1] += cnt[b];
+    std::vector<uint32_t> groups(cnt.begin(), cnt.end());
+    for (size_t i = 0; i < n; ++i) order[cnt[bucket(rs[i])]++] = (uint32_t)i;
+
     int64_t maxpos = 1;
     for (auto &r : rs) maxpos = std::max(maxpos, r.end + 1);
-    const int64_t B = 2048;
-    struct Span { int64_t s, e; int64_t M; };
+    const int64_t B = 256;
+    struct Span { int64_t s, e, M; };
     std::vector<std::vector<Span>> grid((size_t)(maxpos / B + 2));
     std::vector<uint8_t> keep(n, 0);
     std::vector<Rec> kept;
     kept.reserve(n);
-    size_t g = 0;
-    while (g < n) {
-        const bool cls = rs[order[g]].mismatch_rate > 0;
-        const size_t len = rs[order[g]].motif.size();
-        size_t h = g;
-        while (h < n && (rs[order[h]].mismatch_rate > 0) == cls && rs[order[h]].motif.size() == len) ++h;
-        for (size_t k = g; k < h; ++k) {
-            const Rec &r = rs[order[k]];
-            const int64_t a = r.start, b = r.end, m = (int64_t)r.motif.size();
-            const int64_t rl = b - a;
-            bool nested = false;
-            if (b > a) {
-                const int64_t b0 = std::max<int64_t>(0, a) / B, b1 = std::max<int64_t>(0, b - 1) / B;
-                for (int64_t bk = b0; bk <= b1 && !nested && bk < (int64_t)grid.size(); ++bk) {
-                    for (const Span &sp : grid[(size_t)bk]) {
-                        if (sp.M <= m) continue;
-                        const int64_t ov = std::max<int64_t>(0, std::min(b, sp.e) - std::max(a, sp.s));
-                        if (ov == 0) continue;
-                        const double ratio = (double)sp.M / (double)m;
-                        const double frac = (double)ov / (double)rl;
-                        if (m == 1 && sp.M > 1 && frac >= 0.8) { nested = true; break; }
-                        const double t = ratio >= 10 ? 0.1 : (ratio >= 5 ? 0.3 : thr);
-                        if (frac >= t) { nested = true; break; }
+    for (size_t g = 0; g < nb; ++g) {
+        const size_t g0 = groups[g], g1 = groups[g + 1];
+        if (g0 == g1) continue;
+        parallel_for((int64_t)(g1 - g0), nt, [&](int64_t a, int64_t b) {
+            for (int64_t q = a; q < b; ++q) {
+                const Rec &r = rs[order[g0 + (size_t)q]];
+                const int64_t s0 = r.start, e0 = r.end, m = (int64_t)r.motif.size();
+                const int64_t rl = e0 - s0;
+                bool nested = false;
+                if (e0 > s0) {
+                    const int64_t b0 = std::max<int64_t>(0, s0) / B, b1 = std::max<int64_t>(0, e0 - 1) / B;
+                    for (int64_t bk = b0; bk <= b1 && !nested && bk < (int64_t)grid.size(); ++bk) {
+                        for (const Span &sp : grid[(size_t)bk]) {
+                            if (sp.M <= m) continue;
+                            const int64_t ov = std::max<int64_t>(0, std::min(e0, sp.e) - std::max(s0, sp.s));
+                            if (ov == 0) continue;
+                            const double ratio = (double)sp.M / (double)m;
+                            const double frac = (double)ov / (double)rl;
+                            if (m == 1 && sp.M > 1 && frac >= 0.8) { nested = true; break; }
+                            const double t = ratio >= 10 ? 0.1 : (ratio >= 5 ? 0.3 : thr);
+                            if (frac >= t) { nested = true; break; }
+                        }
                     }
                 }
+                keep[order[g0 + (size_t)q]] = !nested;
             }
-            keep[order[k]] = !nested;
-        }
-        for (size_t k = g; k < h; ++k) {
-            const uint32_t idx = order[k];
+        });
+        for (size_t q = g0; q < g1; ++q) {
+            const uint32_t idx = order[q];
             if (!keep[idx]) continue;
             Rec &r = rs[idx];
             if (r.end > r.start) {
-                Span sp{r.start, r.end, (int64_t)r.motif.size()};
+                const Span sp{r.start, r.end, (int64_t)r.motif.size()};
                 const int64_t b0 = std::max<int64_t>(0, r.start) / B, b1 = std::max<int64_t>(0, r.end - 1) / B;
                 for (int64_t bk = b0; bk <= b1 && bk < (int64_t)grid.size(); ++bk) grid[(size_t)bk].push_back(sp);
             }
             kept.push_back(std::move(r));
         }
-        g = h;
     }
     return kept;
 }
@@ -222,40 +299,37 @@ Rec recompute(const UnitCtx &u, int32_t chrom, int64_t start, int64_t end, int64
         tmpl = slice(a, a + m);
     }
     if (tmpl.empty()) tmpl.assign((size_t)m, 'N');
-    AlignSummary s;
+    thread_local AlignSummary s;
     bool ok = align_repeat_region(seq, L, start, end, tmpl, std::max<int64_t>(1, u.min_copies), s);
     if (!ok) ok = align_repeat_region(seq, L, start, end, tmpl, 1, s);
     Rec r;
     r.chrom = chrom;
     r.tier = tier;
     r.start = start;
-    int64_t consumed, cint;
-    std::string cons;
+    int64_t consumed, cint, maxe;
     double mm, pind;
-    int64_t maxe;
     if (!ok) {
         consumed = std::min(L - start, std::max(m, end - start));
         cint = std::max<int64_t>(1, consumed / m);
-        cons = tmpl;  // never empty here
+        r.motif = tmpl;  // never empty here
         mm = 0.0;
         maxe = 0;
         pind = 0.0;
-        r.variations.clear();
     } else {
         consumed = s.consumed;
         cint = s.copies;
-        cons = s.consensus.empty() ? tmpl : s.consensus;
+        r.motif = s.consensus.empty() ? tmpl : s.consensus;
         mm = s.mismatch_rate;
         const int64_t tb = s.copies * s.motif_len;
         const double ir = tb > 0 ? (double)(s.tot_ins + s.tot_del) / (double)tb : 0.0;
         pind = ir * 100.0;
         maxe = s.max_errors;
-        r.variations = s.any_variation ? s.variations : std::string();
+        if (s.any_variation) r.variations = s.variations;
     }
     // actual_sequence = sequence[start:start+consumed]
     const int64_t a0 = std::min(start, L), a1 = std::max(a0, std::min(start + consumed, L));
     const int64_t tl = a1 - a0;
-    const int64_t mle = cons.empty() ? m : (int64_t)cons.size();
+    const int64_t mle = r.motif.empty() ? m : (int64_t)r.motif.size();
     double cf = (double)cint;
     if (tl > 0 && mle > 0) {
         const double fr = (double)tl / (double)mle;
@@ -264,14 +338,13 @@ Rec recompute(const UnitCtx &u, int32_t chrom, int64_t start, int64_t end, int64
     }
     r.end = start + tl;
     r.length = tl;
-    r.motif = cons;
     r.copies = cf;
     r.confidence = std::max(0.3, 1.0 - mm);
     r.mismatch_rate = mm;
     r.max_mm = maxe;
     r.n_eval = std::max<int64_t>(1, cint);
-    std::string canon;
-    canonical_stranded(cons, canon, r.strand);
+    thread_local std::string canon;
+    canonical_stranded(r.motif, canon, r.strand);
     r.pmatch = std::max(0.0, 100.0 - mm * 100.0);
     r.pindel = pind;
     r.score = trf_score(tl, mm);
@@ -281,32 +354,120 @@ Rec recompute(const UnitCtx &u, int32_t chrom, int64_t start, int64_t end, int64
     return r;
 }
 
-// canonical of a motif with a tiny cache (adjacent pairs re-ask for the same r1)
-struct CanonCache {
-    std::string key, val;
-    const std::string &get(const std::string &m) {
-        if (m != key || val.empty()) {
-            char st;
-            canonical_stranded(m, val, st);
-            key = m;
-        }
-        return val;
-    }
+std::string canon_of(const std::string &m) {
+    std::string c;
+    char st;
+    canonical_stranded(m, c, st);
+    return c;
+}
+
+// ------------------------------------------------------------ merge fold
+// bwt.py:3222-3289.  cur/nxt fold over the sorted list.  should_merge needs
+// a recompute only for same-canonical neighbours within min_len+1; when it
+// accepts and len(cur.motif) == min_len the merge recompute has identical
+// arguments, so that result is reused.
+struct MergeState {
+    Rec cur;
+    std::string canon;
 };
 
-// bwt.py:3240-3281
-bool should_merge(const UnitCtx &u, const Rec &r1, const Rec &r2, CanonCache &c1, CanonCache &c2) {
+// returns true and fills `merged` when cur and nx merge
+bool try_merge(const UnitCtx &u, const Rec &r1, const std::string &c1, const Rec &r2, const std::string &c2,
+               Rec &merged) {
     if (r1.chrom != r2.chrom) return false;
     if (r1.motif.empty() || r2.motif.empty()) return false;
     const int64_t ml = (int64_t)std::min(r1.motif.size(), r2.motif.size());
-    const int64_t gap = std::max<int64_t>(0, r2.start - r1.end);
-    if (gap > ml + 1) return false;   // cheap test first: the result is a conjunction
-    if (c1.get(r1.motif) != c2.get(r2.motif)) return false;
-    const Rec mg = recompute(u, r1.chrom, std::min(r1.start, r2.start), std::max(r1.end, r2.end),
-                             std::max<int64_t>(1, ml), std::min(r1.tier, r2.tier));
+    if (std::max<int64_t>(0, r2.start - r1.end) > ml + 1) return false;   // cheap test first
+    if (c1 != c2) return false;
+    const int64_t s = std::min(r1.start, r2.start), e = std::max(r1.end, r2.end);
+    const int32_t tier = std::min(r1.tier, r2.tier);
+    Rec mg = recompute(u, r1.chrom, s, e, std::max<int64_t>(1, ml), tier);
     if (mg.copies < (double)u.min_copies) return false;
     const double base = std::max(std::max(r1.mismatch_rate, r2.mismatch_rate), 0.01);
-    return mg.mismatch_rate <= base + 0.2;
+    if (!(mg.mismatch_rate <= base + 0.2)) return false;
+    const int64_t m1 = (int64_t)r1.motif.size();     // _merge_repeats uses len(r1.consensus_motif)
+    if (m1 == std::max<int64_t>(1, ml)) merged = std::move(mg);
+    else merged = recompute(u, r1.chrom, s, e, m1, tier);
+    return true;
+}
+
+struct SpecOut {
+    std::vector<Rec> emitted;           // records emitted by the speculative run
+    std::vector<int64_t> emit_step;     // index i at which each was emitted
+    Rec pending;
+    std::string pending_canon;
+};
+
+// speculative run over [b, e): starts with cur = R[b] as if fresh at b
+void spec_run(const UnitCtx &u, std::vector<Rec> &R, const std::vector<std::string> &canon, int64_t b, int64_t e,
+              std::vector<uint8_t> &fresh, SpecOut &o) {
+    Rec cur = R[(size_t)b];
+    std::string cc = canon[(size_t)b];
+    fresh[(size_t)b] = 1;
+    Rec mg;
+    for (int64_t i = b + 1; i < e; ++i) {
+        if (try_merge(u, cur, cc, R[(size_t)i], canon[(size_t)i], mg)) {
+            cur = std::move(mg);
+            cc = canon_of(cur.motif);
+            fresh[(size_t)i] = 0;
+        } else {
+            o.emitted.push_back(std::move(cur));
+            o.emit_step.push_back(i);
+            cur = R[(size_t)i];
+            cc = canon[(size_t)i];
+            fresh[(size_t)i] = 1;
+        }
+    }
+    o.pending = std::move(cur);
+    o.pending_canon = std::move(cc);
+}
+
+std::vector<Rec> merge_fold(const UnitCtx &u, std::vector<Rec> &R, int nt) {
+    const int64_t n = (int64_t)R.size();
+    if (n == 0) return {};
+    std::vector<std::string> canon((size_t)n);
+    parallel_for(n, nt, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) canon[(size_t)i] = canon_of(R[(size_t)i].motif);
+    });
+    const int64_t K = std::max<int64_t>(1, std::min<int64_t>(nt * 8, n / 2048 + 1));
+    std::vector<int64_t> cut((size_t)K + 1);
+    for (int64_t k = 0; k <= K; ++k) cut[(size_t)k] = n * k / K;
+    std::vector<uint8_t> fresh((size_t)n, 0);
+    std::vector<SpecOut> spec((size_t)K);
+    parallel_items(K, nt, [&](int64_t k) { spec_run(u, R, canon, cut[(size_t)k], cut[(size_t)k + 1], fresh, spec[(size_t)k]); });
+    // repair: chunk 0 is exact; later chunks are valid once the true run is
+    // fresh at an index where the speculative run was fresh too
+    std::vector<Rec> out;
+    out.reserve((size_t)n);
+    for (auto &r : spec[0].emitted) out.push_back(std::move(r));
+    Rec cur = std::move(spec[0].pending);
+    std::string cc = std::move(spec[0].pending_canon);
+    Rec mg;
+    for (int64_t k = 1; k < K; ++k) {
+        const int64_t b = cut[(size_t)k], e = cut[(size_t)k + 1];
+        SpecOut &sp = spec[(size_t)k];
+        int64_t i = b;
+        int64_t sync = -1;
+        for (; i < e; ++i) {
+            if (try_merge(u, cur, cc, R[(size_t)i], canon[(size_t)i], mg)) {
+                cur = std::move(mg);
+                cc = canon_of(cur.motif);
+            } else {
+                out.push_back(std::move(cur));
+                cur = R[(size_t)i];
+                cc = canon[(size_t)i];
+                if (fresh[(size_t)i]) { sync = i; break; }
+            }
+        }
+        if (sync < 0) continue;   // never re-synchronised: `cur` carries into chunk k+1
+        // identical from `sync` on: take the speculative emissions after it
+        for (size_t q = 0; q < sp.emitted.size(); ++q)
+            if (sp.emit_step[q] > sync) out.push_back(std::move(sp.emitted[q]));
+        cur = std::move(sp.pending);
+        cc = std::move(sp.pending_canon);
+    }
+    out.push_back(std::move(cur));
+    return out;
 }
 
 // bwt.py:3327-3354
@@ -318,11 +479,7 @@ bool should_collapse(const Rec &r1, const Rec &r2) {
     if (sh <= 0) return false;
     const double f = (double)ov / (double)sh;
     if (f < 0.8) return false;
-    std::string a, b;
-    char st;
-    canonical_stranded(r1.motif, a, st);
-    canonical_stranded(r2.motif, b, st);
-    if (a == b) return true;
+    if (canon_of(r1.motif) == canon_of(r2.motif)) return true;
     if ((r1.motif.size() == 1 || r2.motif.size() == 1) && f >= 0.95) return true;
     if (r1.motif.size() == r2.motif.size() && f >= 0.9)
         return std::fabs(r1.mismatch_rate - r2.mismatch_rate) >= 0.2;
@@ -351,24 +508,40 @@ bool prefer_first(const Rec &r1, const Rec &r2) {
     return true;
 }
 
-struct DedupKey {
-    int32_t chrom;
-    int64_t s, e;
-    const std::string *m;
-    bool operator==(const DedupKey &o) const {
-        return chrom == o.chrom && s == o.s && e == o.e && *m == *o.m;
+// bwt.py:3189-3220.  After the (start, end) sort, equal keys (chrom, start,
+// end, motif) sit inside runs of equal (start, end); the first occurrence
+// keeps its position and takes the preferred content.
+void dedup_sorted(std::vector<Rec> &recs) {
+    std::vector<Rec> d;
+    d.reserve(recs.size());
+    size_t i = 0;
+    const size_t n = recs.size();
+    while (i < n) {
+        size_t j = i + 1;
+        while (j < n && recs[j].start == recs[i].start && recs[j].end == recs[i].end) ++j;
+        const size_t first_out = d.size();
+        for (size_t q = i; q < j; ++q) {
+            Rec &r = recs[q];
+            size_t hit = SIZE_MAX;
+            for (size_t x = first_out; x < d.size(); ++x)
+                if (d[x].chrom == r.chrom && d[x].motif == r.motif) { hit = x; break; }
+            if (hit == SIZE_MAX) { d.push_back(std::move(r)); continue; }
+            const Rec &ex = d[hit];
+            bool repl = false;
+            if (r.confidence > ex.confidence) repl = true;
+            else if (r.confidence == ex.confidence) {
+                if (r.mismatch_rate < ex.mismatch_rate) repl = true;
+                else if (r.mismatch_rate == ex.mismatch_rate && r.tier < ex.tier) repl = true;
+            }
+            if (repl) d[hit] = std::move(r);
+        }
+        i = j;
     }
-};
-struct DedupHash {
-    size_t operator()(const DedupKey &k) const {
-        size_t h = std::hash<std::string>()(*k.m);
-        h ^= (size_t)k.s * 0x9E3779B97F4A7C15ull + ((size_t)k.e << 7) + (size_t)k.chrom;
-        return h;
-    }
-};
+    recs.swap(d);
+}
 
-void process_unit(const Job &job, const std::vector<int32_t> &chroms,
-                  std::vector<std::vector<Rec>> &raw, std::vector<Rec> &out, double *ms) {
+void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vector<std::vector<Rec>> &raw,
+                  std::vector<Rec> &out, double *ms, int nt) {
     using clk = std::chrono::steady_clock;
     auto t0 = clk::now();
     UnitCtx u{&job, job.params.min_copies};
@@ -376,77 +549,31 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms,
     //    chromosome order, stable-sorted by (start, end).
     std::vector<Rec> recs;
     for (int32_t c : chroms) {
-        std::vector<Rec> kept = suppress_nested_chrom(raw[(size_t)c], 0.5);
+        std::vector<Rec> kept = suppress_nested_chrom(raw[(size_t)c], 0.5, nt);
         if (recs.empty()) recs.swap(kept);
         else for (auto &r : kept) recs.push_back(std::move(r));
         std::vector<Rec>().swap(raw[(size_t)c]);
     }
-    std::stable_sort(recs.begin(), recs.end(), key_less);
+    sort_by_pos(recs, nt);
     auto t1 = clk::now();
     // 2. dedup (bwt.py:3189-3220)
-    {
-        std::vector<Rec> d;
-        d.reserve(recs.size());
-        std::unordered_map<DedupKey, size_t, DedupHash> pos;
-        pos.reserve(recs.size() * 2);
-        // keys point into `recs`; replaced records keep their slot
-        std::vector<size_t> src;
-        src.reserve(recs.size());
-        for (size_t i = 0; i < recs.size(); ++i) {
-            const Rec &r = recs[i];
-            DedupKey k{r.chrom, r.start, r.end, &r.motif};
-            auto it = pos.find(k);
-            if (it == pos.end()) {
-                pos.emplace(k, src.size());
-                src.push_back(i);
-                continue;
-            }
-            const Rec &ex = recs[src[it->second]];
-            bool repl = false;
-            if (r.confidence > ex.confidence) repl = true;
-            else if (r.confidence == ex.confidence) {
-                if (r.mismatch_rate < ex.mismatch_rate) repl = true;
-                else if (r.mismatch_rate == ex.mismatch_rate && r.tier < ex.tier) repl = true;
-            }
-            if (repl) src[it->second] = i;
-        }
-        for (size_t i : src) d.push_back(std::move(recs[i]));
-        recs.swap(d);
-        std::stable_sort(recs.begin(), recs.end(), key_less);
-    }
+    dedup_sorted(recs);
     auto t2 = clk::now();
-    // 3. merge adjacent (bwt.py:3222-3289) -- sequential fold
-    if (!recs.empty()) {
-        std::vector<Rec> merged;
-        merged.reserve(recs.size());
-        Rec cur = std::move(recs[0]);
-        CanonCache cc, cn;
-        for (size_t i = 1; i < recs.size(); ++i) {
-            Rec &nx = recs[i];
-            if (should_merge(u, cur, nx, cc, cn)) {
-                cur = recompute(u, cur.chrom, std::min(cur.start, nx.start), std::max(cur.end, nx.end),
-                                (int64_t)cur.motif.size(), std::min(cur.tier, nx.tier));
-            } else {
-                merged.push_back(std::move(cur));
-                cur = std::move(nx);
-                std::swap(cc, cn);
-            }
-        }
-        merged.push_back(std::move(cur));
-        recs.swap(merged);
-    }
+    // 3. merge adjacent (bwt.py:3222-3289)
+    recs = merge_fold(u, recs, nt);
     auto t3 = clk::now();
     // 4. refine (bwt.py:3291-3314)
-    for (auto &r : recs) {
-        if (r.mismatch_rate == 0.0) continue;
+    parallel_items((int64_t)recs.size(), nt, [&](int64_t k) {
+        Rec &r = recs[(size_t)k];
+        if (r.mismatch_rate == 0.0) return;
         int64_t m = (int64_t)r.motif.size();
         if (m <= 0) {
             const int64_t rc = (int64_t)std::nearbyint(r.copies);
             m = std::max<int64_t>(1, r.length / std::max<int64_t>(1, rc ? rc : 1));
         }
         r = recompute(u, r.chrom, r.start, r.end, m, r.tier);
-    }
-    std::stable_sort(recs.begin(), recs.end(), key_less);
+    });
+    sort_by_pos(recs, nt);
     // 5. restore coordinates (bwt.py:3316-3325)
     for (auto &r : recs) {
         const Contig &c = job.contigs[(size_t)r.chrom];
@@ -462,7 +589,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms,
         }
     }
     // 6. collapse (bwt.py:3499-3513)
-    std::stable_sort(recs.begin(), recs.end(), key_less);
+    sort_by_pos(recs, nt);
     {
         std::vector<Rec> col;
         col.reserve(recs.size());
@@ -497,20 +624,17 @@ void postprocess(Job &job) {
     if (job.raw.size() < job.contigs.size()) job.raw.resize(job.contigs.size());
     std::vector<std::vector<Rec>> res((size_t)job.nunits);
     std::vector<double> ms((size_t)job.nunits * 4, 0.0);
-    std::atomic<int32_t> next{0};
-    const int nt = std::max(1, std::min(host_threads(job.params), job.nunits));
-    auto worker = [&]() {
-        for (;;) {
-            const int32_t k = next.fetch_add(1);
-            if (k >= job.nunits) break;
-            process_unit(job, units[(size_t)k], job.raw, res[(size_t)k], &ms[(size_t)k * 4]);
-        }
-    };
-    if (nt == 1) worker();
-    else {
-        std::vector<std::thread> th;
-        for (int i = 0; i < nt; ++i) th.emplace_back(worker);
-        for (auto &t : th) t.join();
+    const int T = host_threads(job.params);
+    // many small units: one thread per unit; few large units: all threads inside each
+    int64_t busy = 0;
+    for (auto &v : job.raw) busy += v.empty() ? 0 : 1;
+    if (busy >= T) {
+        parallel_items(job.nunits, T, [&](int64_t k) {
+            process_unit(job, units[(size_t)k], job.raw, res[(size_t)k], &ms[(size_t)k * 4], 1);
+        });
+    } else {
+        for (int32_t k = 0; k < job.nunits; ++k)
+            process_unit(job, units[(size_t)k], job.raw, res[(size_t)k], &ms[(size_t)k * 4], T);
     }
     job.final_recs.clear();
     for (auto &v : res)
