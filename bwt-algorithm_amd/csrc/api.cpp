@@ -363,7 +363,7 @@ int bwtmi_job_upload(bwtmi_ctx *ctx, bwtmi_job *job) {
 int bwtmi_job_reset(bwtmi_job *job) {
     return guard([&] {
         CHECK_ARG(job, "null argument");
-        job->j.raw.clear();
+        job->j.hits.clear();
         job->j.final_recs.clear();
         job->j.postprocessed = false;
     });
@@ -398,7 +398,7 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
         job_upload(ctx, job);
         Job &J = job->j;
         Ctx &c = ctx->c;
-        J.raw.assign(J.contigs.size(), {});
+        J.hits.assign(J.contigs.size(), {});
         J.final_recs.clear();
         J.postprocessed = false;
         const bwtmi_params &P = J.params;
@@ -426,7 +426,7 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
             ScanResult r;
             strict_scan_device(c, job->dev.seqs[i].buf.as<uint8_t>(), len, 1, (int32_t)std::min<int64_t>(U, INT32_MAX),
                                P.min_copies, r);
-            strict_hits_to_records(J, (int32_t)i, r.hits.data(), (int64_t)r.hits.size(), J.raw[i]);
+            J.hits[i].swap(r.hits);   // Rule 1 (bwt.py:3118-3130) never fires on strict hits
         }
         J.stage_ms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         J.stage_ms[1] = idx_ms;
@@ -438,15 +438,15 @@ int bwtmi_job_add_hits(bwtmi_job *job, int32_t contig_id, const bwtmi_hit *hits,
         CHECK_ARG(job && (hits || n == 0) && n >= 0, "bad argument");
         Job &J = job->j;
         CHECK_ARG(contig_id >= 0 && contig_id < (int32_t)J.contigs.size(), "bad contig id");
-        if (J.raw.size() < J.contigs.size()) J.raw.resize(J.contigs.size());
-        strict_hits_to_records(J, contig_id, hits, n, J.raw[(size_t)contig_id]);
+        if (J.hits.size() < J.contigs.size()) J.hits.resize(J.contigs.size());
+        J.hits[(size_t)contig_id].insert(J.hits[(size_t)contig_id].end(), hits, hits + n);
     });
 }
 
 int64_t bwtmi_job_raw_count(const bwtmi_job *job) {
     if (!job) return -1;
     int64_t n = 0;
-    for (auto &v : job->j.raw) n += (int64_t)v.size();
+    for (auto &v : job->j.hits) n += (int64_t)v.size();
     return n;
 }
 

@@ -93,7 +93,7 @@ struct Job {
     std::vector<std::vector<NatPart>> natkeys;
     int32_t nunits = 0;
     std::vector<int32_t> unit_rank;                  // unit id -> rank by natural key
-    std::vector<std::vector<Rec>> raw;               // per contig, worker output order
+    std::vector<std::vector<bwtmi_hit>> hits;        // per contig raw strict hits, worker order
     std::vector<Rec> final_recs;                     // after bwt.py:3940-3944
     std::vector<uint8_t> selected;                   // scan only these contigs (empty = all)
     bool postprocessed = false;
@@ -103,8 +103,6 @@ struct Job {
 
 // post.cpp
 void postprocess(Job &job);
-void strict_hits_to_records(const Job &job, int32_t contig, const bwtmi_hit *hits, int64_t n,
-                            std::vector<Rec> &out);
 // render.cpp
 std::string render(Job &job, int fmt);
 // fasta.cpp
