@@ -364,6 +364,8 @@ int bwtmi_job_reset(bwtmi_job *job) {
     return guard([&] {
         CHECK_ARG(job, "null argument");
         job->j.hits.clear();
+        job->j.screened.clear();
+        job->j.raw_n.clear();
         job->j.final_recs.clear();
         job->j.postprocessed = false;
     });
@@ -399,6 +401,11 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
         Job &J = job->j;
         Ctx &c = ctx->c;
         J.hits.assign(J.contigs.size(), {});
+        J.screened.assign(J.contigs.size(), 0);
+        J.raw_n.assign(J.contigs.size(), 0);
+        // nested suppression + sort + dedup on the device (BWTMI_HOST_SCREEN=1: on the host)
+        const char *hs = std::getenv("BWTMI_HOST_SCREEN");
+        const bool screen = !(hs && *hs == '1');
         J.final_recs.clear();
         J.postprocessed = false;
         const bwtmi_params &P = J.params;
@@ -410,11 +417,13 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
             if (P.build_index) {   // BWTCore(seq + '$') of the worker (bwt.py:3053-3054)
                 auto ti = std::chrono::steady_clock::now();
                 DevContig &dc = job->dev.seqs[i];
-                c.slot[S_MISC3].ensure((size_t)len + 1 + 128);
-                HIPCHECK(hipMemcpyAsync(c.slot[S_MISC3].p, dc.buf.p, (size_t)len, hipMemcpyDeviceToDevice, c.stream));
-                HIPCHECK(hipMemsetAsync(c.slot[S_MISC3].as<uint8_t>() + len, '$', 1, c.stream));
-                HIPCHECK(hipMemsetAsync(c.slot[S_MISC3].as<uint8_t>() + len + 1, 0, 127, c.stream));
-                DeviceIndex *di = index_build_device(c, c.slot[S_MISC3].as<uint8_t>(), len + 1, P.sa_sample, 128,
+                // (S_CAND_K2 is free until the scan; index_build_device uses the MISC/IDX slots)
+                DBuf &tb = c.slot[S_CAND_K2];
+                tb.ensure((size_t)len + 1 + 128);
+                HIPCHECK(hipMemcpyAsync(tb.p, dc.buf.p, (size_t)len, hipMemcpyDeviceToDevice, c.stream));
+                HIPCHECK(hipMemsetAsync(tb.as<uint8_t>() + len, '$', 1, c.stream));
+                HIPCHECK(hipMemsetAsync(tb.as<uint8_t>() + len + 1, 0, 127, c.stream));
+                DeviceIndex *di = index_build_device(c, tb.as<uint8_t>(), len + 1, P.sa_sample, 128,
                                                      0u);
                 index_free(di);   // the worker never consumes it
                 idx_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ti).count();
@@ -425,8 +434,10 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
             const int64_t U = std::max<int64_t>(P.max_unit_len, std::min<int64_t>(len / P.min_copies, 1000));
             ScanResult r;
             strict_scan_device(c, job->dev.seqs[i].buf.as<uint8_t>(), len, 1, (int32_t)std::min<int64_t>(U, INT32_MAX),
-                               P.min_copies, r);
+                               P.min_copies, r, screen);
             J.hits[i].swap(r.hits);   // Rule 1 (bwt.py:3118-3130) never fires on strict hits
+            J.screened[i] = r.screened ? 1 : 0;
+            J.raw_n[i] = r.raw;
         }
         J.stage_ms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         J.stage_ms[1] = idx_ms;
@@ -439,14 +450,19 @@ int bwtmi_job_add_hits(bwtmi_job *job, int32_t contig_id, const bwtmi_hit *hits,
         Job &J = job->j;
         CHECK_ARG(contig_id >= 0 && contig_id < (int32_t)J.contigs.size(), "bad contig id");
         if (J.hits.size() < J.contigs.size()) J.hits.resize(J.contigs.size());
+        if (J.screened.size() < J.contigs.size()) J.screened.resize(J.contigs.size(), 0);
+        if (J.raw_n.size() < J.contigs.size()) J.raw_n.resize(J.contigs.size(), 0);
+        CHECK_ARG(!J.screened[(size_t)contig_id] || n == 0,
+                  "contig holds device-screened hits; reset the job before adding raw hits");
         J.hits[(size_t)contig_id].insert(J.hits[(size_t)contig_id].end(), hits, hits + n);
+        J.raw_n[(size_t)contig_id] += n;
     });
 }
 
 int64_t bwtmi_job_raw_count(const bwtmi_job *job) {
     if (!job) return -1;
     int64_t n = 0;
-    for (auto &v : job->j.hits) n += (int64_t)v.size();
+    for (auto v : job->j.raw_n) n += v;
     return n;
 }
 

@@ -93,7 +93,10 @@ struct Job {
     std::vector<std::vector<NatPart>> natkeys;
     int32_t nunits = 0;
     std::vector<int32_t> unit_rank;                  // unit id -> rank by natural key
-    std::vector<std::vector<bwtmi_hit>> hits;        // per contig raw strict hits, worker order
+    std::vector<std::vector<bwtmi_hit>> hits;        // per contig strict hits: raw (worker order), or
+    std::vector<uint8_t> screened;                   // screened[c]: nested-suppressed, sorted by
+                                                     // (start, end, m desc, worker order) and deduped
+    std::vector<int64_t> raw_n;                      // raw strict hits per contig
     std::vector<Rec> final_recs;                     // after bwt.py:3940-3944
     std::vector<uint8_t> selected;                   // scan only these contigs (empty = all)
     bool postprocessed = false;

@@ -88,6 +88,7 @@ struct Ctx {
         double bytes;
     };
     std::vector<Pend> pending;
+    std::vector<size_t> open;   // kbegin/kend nest (a stage timer around primitive timers)
     std::vector<std::pair<std::string, KStat>> kstats;
     void kbegin(const char *name, double alg_bytes = 0) {
         if (!ktiming) return;
@@ -95,16 +96,21 @@ struct Ctx {
         HIPCHECK(hipEventCreate(&a));
         HIPCHECK(hipEventCreate(&b));
         HIPCHECK(hipEventRecord(a, stream));
+        open.push_back(pending.size());
         pending.push_back({name, a, b, alg_bytes});
     }
     void kend() {
-        if (!ktiming || pending.empty()) return;
-        HIPCHECK(hipEventRecord(pending.back().b, stream));
+        if (!ktiming || open.empty()) return;
+        HIPCHECK(hipEventRecord(pending[open.back()].b, stream));
+        open.pop_back();
     }
     void kresolve() {   // after a stream sync
         for (auto &p : pending) {
             float ms = 0;
-            if (hipEventElapsedTime(&ms, p.a, p.b) != hipSuccess) ms = 0;
+            if (hipEventElapsedTime(&ms, p.a, p.b) != hipSuccess) {
+                ms = 0;
+                (void)hipGetLastError();   // do not leave a sticky error for the next check
+            }
             bool found = false;
             for (auto &k : kstats)
                 if (k.first == p.name) {
@@ -119,6 +125,7 @@ struct Ctx {
             (void)hipEventDestroy(p.b);
         }
         pending.clear();
+        open.clear();
     }
     DBuf slot[S_NSLOTS];
     HBuf host[4];
@@ -138,13 +145,21 @@ void radix_sort_pairs32(Ctx &c, uint64_t *keys, uint32_t *vals, int64_t n, int b
 
 // ----- strict scan (strict_scan.hip)
 struct ScanResult {
-    std::vector<bwtmi_hit> hits;
+    std::vector<bwtmi_hit> hits;   // raw hits in worker order, or screened hits (see below)
     double kernel_ms = 0;
     int64_t candidates = 0;
+    int64_t raw = 0;               // raw strict hits found
+    bool screened = false;
 };
-// d_text: device copy of the trimmed contig (n bytes, padded by >= 64 bytes)
+// d_text: device copy of the trimmed contig (n bytes, padded by >= 64 bytes).
+// screen: also run nested suppression + (start, end) sort + dedup on the
+// device (nested.hip) and return only the survivors, in that order.
 void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
-                        int32_t min_copies, ScanResult &out);
+                        int32_t min_copies, ScanResult &out, bool screen = false);
+
+// ----- nested suppression / sort / dedup of one contig's strict hits (nested.hip)
+void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
+                        std::vector<bwtmi_hit> &out);
 
 // ----- index (index.hip)
 struct DeviceIndex;

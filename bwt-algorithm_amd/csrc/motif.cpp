@@ -186,43 +186,45 @@ bool align_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_
     const int64_t lower = std::max<int64_t>(0, m - max_indel);
     const int64_t upper = std::min<int64_t>(n, m + max_indel);
     if (lower > upper) return false;
-    const int64_t INF = m + n + 10;
+    // Every in-band cell is finite (<= i + j), so the reference's `inf` only
+    // has to lose every comparison: two rolling rows indexed by column, with
+    // the out-of-band neighbours (left of jmin, right of the previous row's
+    // jmax) set to INF, make the recurrence branch-free.
+    const int32_t INF = (int32_t)(m + n + 10);
     const int64_t band = max_indel + 2;
     const int64_t W = 2 * band + 1;
     const size_t cells = (size_t)((m + 1) * W);
-    if (S.cost.size() < cells) {
-        S.cost.resize(cells);
-        S.ptr.resize(cells);
-    }
-    int32_t *cost = S.cost.data();
+    if (S.ptr.size() < cells) S.ptr.resize(cells);
+    if (S.cost.size() < (size_t)(2 * (n + 2))) S.cost.resize((size_t)(2 * (n + 2)));
     char *ptr = S.ptr.data();
-    std::fill(cost, cost + cells, (int32_t)INF);
-    auto get = [&](int64_t i, int64_t j) -> int64_t {
-        if (i == 0) return j;
-        if (j == 0) return i;
-        if (j < i - band || j > i + band) return INF;
-        return cost[i * W + (j - i + band)];
-    };
+    int32_t *prev = S.cost.data(), *cur = prev + (n + 2);
+    for (int64_t j = 0; j <= n; ++j) prev[j] = (int32_t)j;   // row 0
+    prev[n + 1] = INF;
+    int64_t pjmax = n;                                        // row 0 spans every column
     for (int64_t i = 1; i <= m; ++i) {
         const int64_t jmin = std::max<int64_t>(1, i - band), jmax = std::min<int64_t>(n, i + band);
         const char mi = motif[i - 1];
-        int32_t *row = cost + i * W + band - i;   // row[j]
         char *prow = ptr + i * W + band - i;
+        if (pjmax + 1 <= n) prev[pjmax + 1] = INF;            // (i-1, i-1+band+1) is out of band
+        cur[jmin - 1] = jmin - 1 == 0 ? (int32_t)i : INF;
         for (int64_t j = jmin; j <= jmax; ++j) {
             const bool eq = mi == win[j - 1];
-            int64_t best = get(i - 1, j - 1) + (eq ? 0 : 1);
+            int32_t best = prev[j - 1] + (eq ? 0 : 1);
             char op = eq ? 'M' : 'S';
-            const int64_t dc = get(i - 1, j) + 1;
+            const int32_t dc = prev[j] + 1;
             if (dc < best) { best = dc; op = 'D'; }
-            const int64_t ic = (j - 1 == 0) ? i + 1 : (j - 1 >= jmin ? row[j - 1] + 1 : INF + 1);
+            const int32_t ic = cur[j - 1] + 1;
             if (ic < best) { best = ic; op = 'I'; }
-            row[j] = (int32_t)best;
+            cur[j] = best;
             prow[j] = op;
         }
+        pjmax = jmax;
+        std::swap(prev, cur);
     }
+    // prev = row m over [max(1, m-band), min(n, m+band)]; column 0 reads m
     int64_t bj = -1, bc = INF;
     for (int64_t j = lower; j <= upper; ++j) {
-        const int64_t c = get(m, j);
+        const int64_t c = j == 0 ? m : prev[j];
         if (c < bc) { bc = c; bj = j; }
     }
     if (bj <= 0 || bc >= INF) return false;
@@ -381,6 +383,17 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
         const int64_t wend = std::min<int64_t>(seq_len, pos + m + max_indel);
         const int64_t wlen = wend - pos;
         if (wlen < m - max_indel) break;
+        if (wlen >= m && std::memcmp(cur.data(), seq + pos, (size_t)m) == 0) {
+            // exact copy: the DP's unique zero is (m, m) on the all-'M' diagonal,
+            // so no ops, consumed m, every base observed; each cur[p] is already
+            // its position's first maximal count, so the consensus is unchanged
+            ++copies;
+            out.copy_err.push_back(0);
+            out.copy_len.push_back(m);
+            for (int64_t p = 0; p < m; ++p) pc_add(S, p, cur[(size_t)p]);
+            pos += m;
+            continue;
+        }
         if (!align_unit(cur.data(), m, seq + pos, wlen, max_indel, tol, S, res) || res.consumed == 0) break;
         ++copies;
         // variation pieces "copy:pos:..." in op order (bwt.py:1073-1088)

@@ -1,0 +1,308 @@
+// nested.hip -- nested-repeat suppression, position sort and dedup of one
+// contig's strict hits, on the device where the scan left them.
+//
+// Replaces, for strict hits (mismatch_rate 0, one class), the worker-side
+// _filter_nested_repeats (bwt.py:3402-3497), the (start, end) sort that
+// follows it and _deduplicate_repeats (bwt.py:3189-3220):
+//
+//   * a hit r (start s0, end e0, primitive motif length m) is suppressed when
+//     a KEPT hit of strictly longer motif M overlaps it by ov with
+//     ov / (e0 - s0) >= t(M / m) (t = 0.1 / 0.3 / 0.5, or 0.8 when m == 1);
+//     hits are decided in descending m, so the kept set a query sees is
+//     exactly the reference's;
+//   * the survivors, stable-sorted by (start, end), keep the reference's tie
+//     order (m desc, then worker order), i.e. the total order
+//     (start, end, m desc, hit index);
+//   * dedup keys (start, end, motif) of strict hits reduce to (start, end, m)
+//     (the motif is text[start, start + m)); equal keys are adjacent in that
+//     order and share the nested decision, and every field dedup compares
+//     (confidence 0.95, mismatch 0, tier 2) ties, so the first one stays.
+//
+// Kernels: two stable LSD radix sorts give the position order P (by
+// (len, m desc) then start) and the level order G (by m desc); the position
+// arrays S/E/M and an inclusive prefix max of E (PME) are gathered once.  One
+// launch per distinct m (descending) decides that level: each thread binary
+// searches the last span starting before e0 and walks P backwards until PME
+// drops to s0 -- every span that can overlap r lies in that window.  A final
+// flag/scan/compact pass writes the kept, deduplicated hits in P order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "device.h"
+
+namespace bwtmi {
+namespace {
+
+constexpr int kB = 256;
+constexpr int kTile = 4096;
+
+inline unsigned blocks(int64_t n) { return (unsigned)((n + kB - 1) / kB); }
+inline int bits_for(uint64_t v) {
+    int b = 0;
+    while (b < 64 && (v >> b) != 0) ++b;
+    return b;
+}
+
+__global__ void k_maxlen(const bwtmi_hit *__restrict__ H, int64_t n, unsigned long long *__restrict__ out) {
+    __shared__ unsigned long long red[kB];
+    unsigned long long v = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB)
+        v = max(v, (unsigned long long)(H[i].end - H[i].start));
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = kB / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMax(out, red[0]);
+}
+
+// position sort, stage 1 key: (len << mb) | (lmax - m); group key: lmax - m
+__global__ void k_keys(const bwtmi_hit *__restrict__ H, int64_t n, int mb, int64_t lmax, uint64_t *__restrict__ kpos,
+                       uint32_t *__restrict__ vpos, uint64_t *__restrict__ kgrp, uint32_t *__restrict__ vgrp) {
+    const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (i >= n) return;
+    const bwtmi_hit h = H[i];
+    const uint64_t g = (uint64_t)(lmax - h.prim_len);
+    kpos[i] = ((uint64_t)(h.end - h.start) << mb) | g;
+    vpos[i] = (uint32_t)i;
+    kgrp[i] = g;
+    vgrp[i] = (uint32_t)i;
+}
+
+// stage 2 key: start of the hit now at rank k
+__global__ void k_keys_start(const bwtmi_hit *__restrict__ H, int64_t n, const uint32_t *__restrict__ vpos,
+                             uint64_t *__restrict__ kpos) {
+    const int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (k >= n) return;
+    kpos[k] = (uint64_t)H[vpos[k]].start;
+}
+
+__global__ void k_gather(const bwtmi_hit *__restrict__ H, int64_t n, const uint32_t *__restrict__ vpos,
+                         int64_t *__restrict__ S, int64_t *__restrict__ E, int32_t *__restrict__ M,
+                         uint32_t *__restrict__ rank_of, uint8_t *__restrict__ kept) {
+    const int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t idx = vpos[k];
+    const bwtmi_hit h = H[idx];
+    S[k] = h.start;
+    E[k] = h.end;
+    M[k] = h.prim_len;
+    rank_of[idx] = (uint32_t)k;
+    kept[k] = 0;
+}
+
+// level boundaries: first[g] = first position of group key g in the G order
+__global__ void k_bounds(const uint64_t *__restrict__ kgrp, int64_t n, int64_t *__restrict__ first) {
+    const int64_t j = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (j >= n) return;
+    if (j == 0 || kgrp[j] != kgrp[j - 1]) first[kgrp[j]] = j;
+}
+
+// ---- inclusive prefix max (int64), tiles of 4096
+__global__ __launch_bounds__(kB) void k_tile_max(const int64_t *__restrict__ in, int64_t *__restrict__ out, int64_t n) {
+    __shared__ int64_t red[kB];
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    int64_t v = INT64_MIN;
+    for (int i = 0; i < kTile / kB; ++i) {
+        const int64_t idx = base + (int64_t)i * kB + threadIdx.x;
+        if (idx < n) v = max(v, in[idx]);
+    }
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = kB / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
+// inclusive max scan of one tile, seeded with the inclusive max of all
+// earlier tiles (pre[blockIdx.x - 1])
+__global__ __launch_bounds__(kB) void k_tile_scan_max(const int64_t *__restrict__ in, int64_t *__restrict__ out,
+                                                      const int64_t *__restrict__ pre, int64_t n) {
+    constexpr int kI = kTile / kB;   // 16 consecutive items per thread
+    __shared__ int64_t part[kB];
+    const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kI;
+    int64_t loc[kI];
+    int64_t run = INT64_MIN;
+#pragma unroll
+    for (int i = 0; i < kI; ++i) {
+        const int64_t idx = base + i;
+        run = max(run, idx < n ? in[idx] : INT64_MIN);
+        loc[i] = run;
+    }
+    part[threadIdx.x] = run;
+    __syncthreads();
+    // Hillis-Steele over the 256 thread totals
+    for (int o = 1; o < kB; o <<= 1) {
+        const int64_t u = (int)threadIdx.x >= o ? part[threadIdx.x - o] : INT64_MIN;
+        __syncthreads();
+        part[threadIdx.x] = max(part[threadIdx.x], u);
+        __syncthreads();
+    }
+    int64_t seed = threadIdx.x > 0 ? part[threadIdx.x - 1] : INT64_MIN;
+    if (pre && blockIdx.x > 0) seed = max(seed, pre[blockIdx.x - 1]);
+#pragma unroll
+    for (int i = 0; i < kI; ++i) {
+        const int64_t idx = base + i;
+        if (idx < n) out[idx] = max(loc[i], seed);
+    }
+}
+
+void prefix_max(Ctx &c, const int64_t *in, int64_t *out, int64_t n, int64_t *tmp) {
+    const int64_t nt = (n + kTile - 1) / kTile;
+    if (nt == 1) {
+        hipLaunchKernelGGL(k_tile_scan_max, dim3(1), dim3(kB), 0, c.stream, in, out, (const int64_t *)nullptr, n);
+        return;
+    }
+    int64_t *tm = tmp;
+    hipLaunchKernelGGL(k_tile_max, dim3((unsigned)nt), dim3(kB), 0, c.stream, in, tm, n);
+    prefix_max(c, tm, tm, nt, tmp + nt);   // inclusive max over tiles
+    hipLaunchKernelGGL(k_tile_scan_max, dim3((unsigned)nt), dim3(kB), 0, c.stream, in, out, (const int64_t *)tm, n);
+}
+
+// one level (all hits of one primitive length m): nested test against the
+// kept spans of longer motif (bwt.py:3460-3490), predicate division for division
+__global__ __launch_bounds__(kB) void k_level(const uint32_t *__restrict__ lvl, int64_t cnt,
+                                              const bwtmi_hit *__restrict__ H, const uint32_t *__restrict__ rank_of,
+                                              const int64_t *__restrict__ S, const int64_t *__restrict__ E,
+                                              const int32_t *__restrict__ M, const int64_t *__restrict__ PME,
+                                              uint8_t *__restrict__ kept, int64_t n, double thr) {
+    const int64_t t = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (t >= cnt) return;
+    const uint32_t idx = lvl[t];
+    const bwtmi_hit h = H[idx];
+    const int64_t s0 = h.start, e0 = h.end, m = h.prim_len, rl = e0 - s0;
+    bool nested = false;
+    if (rl > 0) {
+        int64_t lo = 0, hi = n;   // first rank with S >= e0
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (S[mid] < e0) lo = mid + 1;
+            else hi = mid;
+        }
+        for (int64_t k = lo - 1; k >= 0 && PME[k] > s0; --k) {
+            const int64_t Mk = M[k];
+            if (Mk <= m || !kept[k]) continue;   // same-level entries are being written now: never read
+            const int64_t ov = min(e0, E[k]) - max(s0, S[k]);
+            if (ov <= 0) continue;
+            const double ratio = (double)Mk / (double)m;
+            const double frac = (double)ov / (double)rl;
+            if (m == 1 && Mk > 1 && frac >= 0.8) { nested = true; break; }
+            const double th = ratio >= 10 ? 0.1 : (ratio >= 5 ? 0.3 : thr);
+            if (frac >= th) { nested = true; break; }
+        }
+    }
+    kept[rank_of[idx]] = nested ? 0 : 1;
+}
+
+__global__ void k_final_flags(const int64_t *__restrict__ S, const int64_t *__restrict__ E,
+                              const int32_t *__restrict__ M, const uint8_t *__restrict__ kept, int64_t n,
+                              uint32_t *__restrict__ flag) {
+    const int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (k >= n) return;
+    bool f = kept[k] != 0;
+    if (f && k > 0 && S[k - 1] == S[k] && E[k - 1] == E[k] && M[k - 1] == M[k]) f = false;
+    flag[k] = f ? 1u : 0u;
+}
+
+__global__ void k_final_compact(const bwtmi_hit *__restrict__ H, const uint32_t *__restrict__ vpos,
+                                const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos, int64_t n,
+                                bwtmi_hit *__restrict__ out) {
+    const int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (k >= n || !flag[k]) return;
+    out[pos[k]] = H[vpos[k]];
+}
+
+}  // namespace
+
+void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
+                        std::vector<bwtmi_hit> &out) {
+    out.clear();
+    if (n <= 0) return;
+    if (n >= (int64_t)UINT32_MAX) fail(BWTMI_E_ARG, "too many strict hits for one contig (%lld)", (long long)n);
+    hipStream_t st = c.stream;
+    c.slot[S_CAND_K].ensure((size_t)n * 8);
+    c.slot[S_CAND_V].ensure((size_t)n * 4);
+    c.slot[S_CAND_K2].ensure((size_t)n * 8);
+    c.slot[S_CAND_V2].ensure((size_t)n * 4);
+    c.slot[S_MISC0].ensure((size_t)n * 8);
+    c.slot[S_MISC1].ensure((size_t)n * 8);
+    c.slot[S_IDX0].ensure((size_t)n * 8);
+    c.slot[S_IDX1].ensure((size_t)n * 4);
+    c.slot[S_IDX2].ensure((size_t)n * 4);
+    c.slot[S_IDX3].ensure((size_t)n + 64);
+    c.slot[S_IDX4].ensure((size_t)n * sizeof(bwtmi_hit));
+    c.slot[S_IDX5].ensure((size_t)(n / kTile + 64) * 2 * 8);
+    c.slot[S_FLAG].ensure((size_t)(n + 1) * 4);
+    c.slot[S_SCAN].ensure((size_t)(n + 1) * 4);
+    c.slot[S_COUNTS].ensure((size_t)(lmax + 2) * 8);
+    uint64_t *kpos = c.slot[S_CAND_K].as<uint64_t>(), *kgrp = c.slot[S_CAND_K2].as<uint64_t>();
+    uint32_t *vpos = c.slot[S_CAND_V].as<uint32_t>(), *vgrp = c.slot[S_CAND_V2].as<uint32_t>();
+    int64_t *S = c.slot[S_MISC0].as<int64_t>(), *E = c.slot[S_MISC1].as<int64_t>();
+    int64_t *PME = c.slot[S_IDX0].as<int64_t>();
+    int32_t *M = c.slot[S_IDX1].as<int32_t>();
+    uint32_t *rank_of = c.slot[S_IDX2].as<uint32_t>();
+    uint8_t *kept = c.slot[S_IDX3].as<uint8_t>();
+    bwtmi_hit *dout = c.slot[S_IDX4].as<bwtmi_hit>();
+    uint32_t *flag = c.slot[S_FLAG].as<uint32_t>(), *pos = c.slot[S_SCAN].as<uint32_t>();
+    unsigned long long *d_max = c.slot[S_COUNTS].as<unsigned long long>();
+
+    // longest span -> key widths
+    HIPCHECK(hipMemsetAsync(d_max, 0, 8, st));
+    hipLaunchKernelGGL(k_maxlen, dim3((unsigned)std::min<int64_t>(1024, blocks(n))), dim3(kB), 0, st, d_hits, n, d_max);
+    unsigned long long maxlen = 0;
+    HIPCHECK(hipMemcpyAsync(&maxlen, d_max, 8, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    const int mb = std::max(1, bits_for((uint64_t)lmax));
+    const int lb = std::max(1, bits_for(maxlen));
+    if (lb + mb > 64) fail(BWTMI_E_ARG, "span too long for the screen keys");
+    auto round8 = [](int b) { return ((b + 7) / 8) * 8; };
+
+    c.kbegin("screen_sort", 0.0);
+    hipLaunchKernelGGL(k_keys, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, mb, (int64_t)lmax, kpos, vpos, kgrp, vgrp);
+    radix_sort_pairs32(c, kpos, vpos, n, 0, round8(lb + mb));
+    hipLaunchKernelGGL(k_keys_start, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, kpos);
+    radix_sort_pairs32(c, kpos, vpos, n, 0, round8(std::max(1, bits_for((uint64_t)text_len))));   // start < text_len
+    radix_sort_pairs32(c, kgrp, vgrp, n, 0, round8(mb));
+    hipLaunchKernelGGL(k_gather, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, S, E, M, rank_of, kept);
+    prefix_max(c, E, PME, n, c.slot[S_IDX5].as<int64_t>());
+    int64_t *first = reinterpret_cast<int64_t *>(d_max);
+    HIPCHECK(hipMemsetAsync(first, 0xff, (size_t)(lmax + 2) * 8, st));
+    hipLaunchKernelGGL(k_bounds, dim3(blocks(n)), dim3(kB), 0, st, kgrp, n, first);
+    c.kend();
+    std::vector<int64_t> fh((size_t)lmax + 2);
+    HIPCHECK(hipMemcpyAsync(fh.data(), first, fh.size() * 8, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(st));
+
+    // levels in descending m (ascending group key)
+    c.kbegin("screen_levels", 0.0);
+    std::vector<std::pair<int64_t, int64_t>> lv;   // (first, group key)
+    for (int64_t g = 0; g <= lmax; ++g)
+        if (fh[(size_t)g] >= 0) lv.push_back({fh[(size_t)g], g});
+    for (size_t q = 0; q < lv.size(); ++q) {
+        const int64_t a = lv[q].first, b = q + 1 < lv.size() ? lv[q + 1].first : n;
+        hipLaunchKernelGGL(k_level, dim3(blocks(b - a)), dim3(kB), 0, st, vgrp + a, b - a, d_hits, rank_of, S, E, M,
+                           PME, kept, n, 0.5);
+    }
+    c.kend();
+    c.kbegin("screen_compact", 0.0);
+    hipLaunchKernelGGL(k_final_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, kept, n, flag);
+    HIPCHECK(hipMemsetAsync(flag + n, 0, 4, st));
+    exclusive_scan<uint32_t>(c, flag, pos, n + 1);
+    hipLaunchKernelGGL(k_final_compact, dim3(blocks(n)), dim3(kB), 0, st, d_hits, vpos, flag, pos, n, dout);
+    c.kend();
+    HIPCHECK(hipGetLastError());
+    uint32_t nk = 0;
+    HIPCHECK(hipMemcpyAsync(&nk, pos + n, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    out.resize(nk);
+    if (nk) HIPCHECK(hipMemcpyAsync(out.data(), dout, (size_t)nk * sizeof(bwtmi_hit), hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+}
+
+}  // namespace bwtmi

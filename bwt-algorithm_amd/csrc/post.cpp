@@ -153,6 +153,18 @@ struct Item {
     int32_t chrom, mlen, tier, pad;
 };
 
+// vector storage without value-initialisation: large item arrays are written
+// once in parallel, so the first touch happens in the filling threads
+template <class T>
+struct NoInit : std::allocator<T> {
+    template <class U> struct rebind { using other = NoInit<U>; };
+    NoInit() = default;
+    template <class U> NoInit(const NoInit<U> &) noexcept {}
+    template <class U> void construct(U *p) noexcept { ::new ((void *)p) U; }
+    template <class U, class... A> void construct(U *p, A &&...a) { ::new ((void *)p) U(std::forward<A>(a)...); }
+};
+using ItemVec = std::vector<Item, NoInit<Item>>;
+
 struct Pools {                  // per-worker arenas of Extras (pointer-stable)
     std::vector<std::unique_ptr<std::deque<Extra>>> p;
     explicit Pools(int n) { for (int i = 0; i < n; ++i) p.emplace_back(new std::deque<Extra>()); }
@@ -183,7 +195,7 @@ std::string canon_of(std::string_view m) {
 }
 
 // stable sort of items by (start, end)
-void sort_by_pos(std::vector<Item> &v, int nt) {
+void sort_by_pos(ItemVec &v, int nt) {
     const size_t n = v.size();
     if (n < 2) return;
     bool sorted = true;
@@ -220,7 +232,7 @@ void sort_by_pos(std::vector<Item> &v, int nt) {
 // length) group is screened -- in parallel, against a frozen grid of the
 // spans kept so far -- and its survivors are appended as a whole.  The
 // predicate is the reference's, division for division.
-std::vector<Item> suppress_nested(const std::vector<Item> &rs, double thr, int nt) {
+ItemVec suppress_nested(const ItemVec &rs, double thr, int nt) {
     const size_t n = rs.size();
     int32_t maxlen = 0;
     for (auto &r : rs) maxlen = std::max(maxlen, r.mlen);
@@ -240,7 +252,7 @@ std::vector<Item> suppress_nested(const std::vector<Item> &rs, double thr, int n
     struct Span { int64_t s, e, M; };
     std::vector<std::vector<Span>> grid((size_t)(maxpos / B + 2));
     std::vector<uint8_t> keep(n, 0);
-    std::vector<Item> kept;
+    ItemVec kept;
     kept.reserve(n);
     for (size_t g = 0; g < nb; ++g) {
         const size_t g0 = groups[g], g1 = groups[g + 1];
@@ -287,19 +299,23 @@ std::vector<Item> suppress_nested(const std::vector<Item> &rs, double thr, int n
 
 // optional counters (BWTMI_STATS=1): recompute calls / time, merge accepts
 std::atomic<int64_t> g_recomputes{0}, g_recompute_ns{0}, g_merges{0};
+std::atomic<int64_t> g_hist_n[8][8], g_hist_ns[8][8];   // [log4 motif len][log4 region len]
+inline int lg4(int64_t v) { int k = 0; while (v >= 4 && k < 7) { v >>= 2; ++k; } return k; }
 
 // bwt.py:3515-3614 (on the trimmed sequence, before coordinate restore)
 Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t start, int64_t end,
                int64_t motif_len, int32_t tier) {
     struct Tick {
+        int a, b;
         std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
         ~Tick() {
+            const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t).count();
             g_recomputes.fetch_add(1, std::memory_order_relaxed);
-            g_recompute_ns.fetch_add(
-                std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t).count(),
-                std::memory_order_relaxed);
+            g_recompute_ns.fetch_add(ns, std::memory_order_relaxed);
+            g_hist_n[a][b].fetch_add(1, std::memory_order_relaxed);
+            g_hist_ns[a][b].fetch_add(ns, std::memory_order_relaxed);
         }
-    } tick;
+    } tick{lg4(motif_len), lg4(end - start)};
     const Contig &c = u.job->contigs[(size_t)chrom];
     const char *seq = c.trimmed();
     const int64_t L = c.trimmed_len();
@@ -398,14 +414,14 @@ bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, const std:
 }
 
 struct SpecOut {
-    std::vector<Item> emitted;          // records emitted by the speculative run
+    ItemVec emitted;          // records emitted by the speculative run
     std::vector<int64_t> emit_step;     // index i at which each was emitted
     Item pending;
     std::string pending_canon;
 };
 
 // speculative run over [b, e): starts with cur = R[b] as if fresh at b
-void spec_run(const UnitCtx &u, Pools &pools, int w, const std::vector<Item> &R,
+void spec_run(const UnitCtx &u, Pools &pools, int w, const ItemVec &R,
               const std::vector<std::string> &canon, int64_t b, int64_t e, std::vector<uint8_t> &fresh, SpecOut &o) {
     Item cur = R[(size_t)b];
     std::string cc = canon[(size_t)b];
@@ -428,7 +444,7 @@ void spec_run(const UnitCtx &u, Pools &pools, int w, const std::vector<Item> &R,
     o.pending_canon = std::move(cc);
 }
 
-std::vector<Item> merge_fold(const UnitCtx &u, Pools &pools, const std::vector<Item> &R, int nt) {
+ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
     const int64_t n = (int64_t)R.size();
     if (n == 0) return {};
     std::vector<std::string> canon((size_t)n);
@@ -452,7 +468,7 @@ std::vector<Item> merge_fold(const UnitCtx &u, Pools &pools, const std::vector<I
     // repair: chunk 0 is exact; a later chunk's speculative results hold from
     // the first index where the true run restarts (non-merge) at an index
     // where the speculative run restarted too
-    std::vector<Item> out;
+    ItemVec out;
     out.reserve((size_t)n);
     for (auto &r : spec[0].emitted) out.push_back(r);
     Item cur = spec[0].pending;
@@ -523,8 +539,8 @@ bool prefer_first(const UnitCtx &u, const Item &r1, const Item &r2) {
 // bwt.py:3189-3220.  After the (start, end) sort, equal keys (chrom, start,
 // end, motif) sit inside runs of equal (start, end); the first occurrence
 // keeps its position and takes the preferred content.
-void dedup_sorted(const UnitCtx &u, std::vector<Item> &recs) {
-    std::vector<Item> d;
+void dedup_sorted(const UnitCtx &u, ItemVec &recs) {
+    ItemVec d;
     d.reserve(recs.size());
     size_t i = 0;
     const size_t n = recs.size();
@@ -608,10 +624,15 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     Pools pools(std::max(1, nt));
     // 1. nested suppression per chromosome (bwt.py:3928), concatenated in
     //    chromosome order, stable-sorted by (start, end).
-    std::vector<Item> recs;
+    //    Hits the device already screened (nested.hip) arrive kept, sorted and
+    //    deduplicated per chromosome; a one-chromosome unit then skips 1-2.
+    ItemVec recs;
+    bool presorted = chroms.size() == 1;
     for (int32_t c : chroms) {
         auto &h = raw[(size_t)c];
-        std::vector<Item> items(h.size());
+        const bool scr = (size_t)c < job.screened.size() && job.screened[(size_t)c];
+        presorted = presorted && scr;
+        ItemVec items(h.size());
         parallel_for((int64_t)h.size(), nt, [&](int64_t a, int64_t b) {
             for (int64_t k = a; k < b; ++k) {
                 const bwtmi_hit &x = h[(size_t)k];
@@ -619,13 +640,14 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
             }
         });
         std::vector<bwtmi_hit>().swap(h);
-        std::vector<Item> kept = suppress_nested(items, 0.5, nt);
-        recs.insert(recs.end(), kept.begin(), kept.end());
+        if (!scr) items = suppress_nested(items, 0.5, nt);
+        if (recs.empty()) recs.swap(items);
+        else recs.insert(recs.end(), items.begin(), items.end());
     }
-    sort_by_pos(recs, nt);
+    if (!presorted) sort_by_pos(recs, nt);
     auto t1 = clk::now();
     // 2. dedup (bwt.py:3189-3220)
-    dedup_sorted(u, recs);
+    if (!presorted) dedup_sorted(u, recs);
     auto t2 = clk::now();
     // 3. merge adjacent (bwt.py:3222-3289)
     recs = merge_fold(u, pools, recs, nt);
@@ -651,7 +673,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     // 6. collapse (bwt.py:3499-3513)
     sort_by_pos(recs, nt);
     {
-        std::vector<Item> col;
+        ItemVec col;
         col.reserve(recs.size());
         for (auto &r : recs) {
             if (!col.empty() && should_collapse(u, col.back(), r)) {
@@ -712,6 +734,12 @@ void postprocess(Job &job) {
         std::fprintf(stderr, "[bwtmi] recomputes=%lld (%.1f ms thread-summed) merges=%lld final=%zu\n",
                      (long long)g_recomputes.exchange(0), g_recompute_ns.exchange(0) / 1e6,
                      (long long)g_merges.exchange(0), job.final_recs.size());
+    if (const char *e = std::getenv("BWTMI_STATS"); e && *e == '1')
+        for (int a = 0; a < 8; ++a)
+            for (int b = 0; b < 8; ++b)
+                if (int64_t c = g_hist_n[a][b].exchange(0))
+                    std::fprintf(stderr, "  m~4^%d len~4^%d: n=%lld %.1f ms (%.2f us)\n", a, b, (long long)c,
+                                 g_hist_ns[a][b].load() / 1e6, g_hist_ns[a][b].exchange(0) / 1e3 / (double)c);
     job.postprocessed = true;
 }
 

@@ -311,10 +311,12 @@ void launch_runs(Ctx &c, const uint64_t *P, int64_t n, int32_t lmin, int32_t lma
 }  // namespace
 
 void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
-                        int32_t min_copies, ScanResult &res) {
+                        int32_t min_copies, ScanResult &res, bool screen) {
     res.hits.clear();
     res.candidates = 0;
     res.kernel_ms = 0;
+    res.raw = 0;
+    res.screened = screen;
     if (min_copies <= 0) fail(BWTMI_E_ARG, "min_copies must be positive");
     // bwt.py:1920-1921
     const int64_t maxL = std::min<int64_t>(max_unit, n / min_copies);
@@ -354,6 +356,12 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
             hipLaunchKernelGGL(k_period, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st, d_text,
                                c.slot[S_HITS].as<bwtmi_hit>(), nh);
         HIPCHECK(hipGetLastError());
+        res.raw = nh;
+        if (screen) {
+            screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.hits);
+            c.kresolve();
+            return;
+        }
         res.hits.resize((size_t)nh);
         if (nh > 0)
             HIPCHECK(hipMemcpyAsync(res.hits.data(), c.slot[S_HITS].p, (size_t)nh * sizeof(bwtmi_hit),
@@ -460,11 +468,17 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
         hipLaunchKernelGGL(k_period, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st, d_text,
                            c.slot[S_HITS].as<bwtmi_hit>(), nh);
     HIPCHECK(hipGetLastError());
-    if (c.timing) HIPCHECK(hipEventRecord(c.ev1, st));
-    res.hits.resize((size_t)nh);
-    if (nh > 0)
-        HIPCHECK(hipMemcpyAsync(res.hits.data(), c.slot[S_HITS].p, (size_t)nh * sizeof(bwtmi_hit),
-                                hipMemcpyDeviceToHost, st));
+    res.raw = nh;
+    if (screen) {
+        screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.hits);
+        if (c.timing) HIPCHECK(hipEventRecord(c.ev1, st));
+    } else {
+        if (c.timing) HIPCHECK(hipEventRecord(c.ev1, st));
+        res.hits.resize((size_t)nh);
+        if (nh > 0)
+            HIPCHECK(hipMemcpyAsync(res.hits.data(), c.slot[S_HITS].p, (size_t)nh * sizeof(bwtmi_hit),
+                                    hipMemcpyDeviceToHost, st));
+    }
     HIPCHECK(hipStreamSynchronize(st));
     c.kresolve();
     if (c.timing) {

@@ -170,6 +170,49 @@ def test_pipeline_seeded_imperfect_vs_oracle(gpu_ctx, tmp_path):
         assert out.read_text() == post.run_file(fa, fmt), fmt
 
 
+def _job_output(contigs, screen: bool, mc=3, fmt="strfinder"):
+    """Scan + post-process + render through the job API; screen selects the
+    device (nested.hip) or the host nested/sort/dedup stage."""
+    from bwtmi import _lib
+    from bwtmi.records import Job
+    old = os.environ.get("BWTMI_HOST_SCREEN")
+    os.environ["BWTMI_HOST_SCREEN"] = "0" if screen else "1"
+    try:
+        j = Job(min_copies=mc, show_progress=True)
+        for name, seq in contigs:
+            j.add_contig(name, seq, 30 if len(seq) > 60 else 0, 30 if len(seq) > 60 else 0)
+        j.scan(_lib.ctx())
+        raw = j.raw_count()
+        j.postprocess()
+        return raw, j.render(fmt)
+    finally:
+        if old is None:
+            os.environ.pop("BWTMI_HOST_SCREEN", None)
+        else:
+            os.environ["BWTMI_HOST_SCREEN"] = old
+
+
+@pytest.mark.parametrize("case", ["planted", "synthetic", "imperfect", "same_unit", "tiny"])
+def test_device_screen_matches_host(gpu_ctx, case):
+    """nested suppression + sort + dedup on the device == the host restatement."""
+    from bwtmi import synth
+    if case == "planted":
+        contigs = [("p1", _planted(300_000, 5, max_unit=400, density=0.5)), ("p2", _planted(50_000, 6))]
+    elif case == "synthetic":
+        contigs = [("contig1", synth.generate_contig(2_000_000, 1, 0.0))]
+    elif case == "imperfect":
+        contigs = [("c7", synth.generate_contig(1_000_000, 7, 0.02))]
+    elif case == "same_unit":   # equal natural keys -> one fold unit over two contigs
+        contigs = [("chr01", _planted(40_000, 8)), ("CHR1", _planted(40_000, 9)), ("chr2", _planted(9_000, 10))]
+    else:
+        contigs = [("a", b"ACACACACAC"), ("b", b"A" * 7), ("c", b"")]
+    for fmt in ("strfinder", "bed"):
+        rd, d = _job_output(contigs, True, fmt=fmt)
+        rh, h = _job_output(contigs, False, fmt=fmt)
+        assert rd == rh
+        assert d == h, (case, fmt)
+
+
 # ------------------------------------------------------------------ FM index
 def _check_index(text: bytes, golden=None):
     from bwtmi import BWTCore
