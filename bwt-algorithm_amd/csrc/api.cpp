@@ -478,25 +478,32 @@ int64_t bwtmi_job_count(const bwtmi_job *job) { return job ? (int64_t)job->j.fin
 int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len) {
     return guard([&] {
         CHECK_ARG(job && out && len, "null argument");
-        std::string s = render(job->j, fmt);
-        char *p = (char *)std::malloc(s.size() + 1);
+        const std::vector<std::string> parts = render_parts(job->j, fmt);
+        size_t tot = 0;
+        for (auto &s : parts) tot += s.size();
+        char *p = (char *)std::malloc(tot + 1);
         if (!p) fail(BWTMI_E_NOMEM, "malloc");
-        std::memcpy(p, s.data(), s.size());
-        p[s.size()] = 0;
+        size_t at = 0;
+        for (auto &s : parts) {
+            std::memcpy(p + at, s.data(), s.size());
+            at += s.size();
+        }
+        p[tot] = 0;
         *out = p;
-        *len = (int64_t)s.size();
+        *len = (int64_t)tot;
     });
 }
 
 int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path) {
     return guard([&] {
         CHECK_ARG(job && path, "null argument");
-        std::string s = render(job->j, fmt);
+        const std::vector<std::string> parts = render_parts(job->j, fmt);
         FILE *f = std::fopen(path, "wb");
         if (!f) fail(BWTMI_E_IO, "cannot open %s for writing", path);
-        const size_t w = std::fwrite(s.data(), 1, s.size(), f);
-        std::fclose(f);
-        if (w != s.size()) fail(BWTMI_E_IO, "short write to %s", path);
+        bool ok = true;
+        for (auto &s : parts) ok = ok && std::fwrite(s.data(), 1, s.size(), f) == s.size();
+        ok = (std::fclose(f) == 0) && ok;
+        if (!ok) fail(BWTMI_E_IO, "short write to %s", path);
     });
 }
 

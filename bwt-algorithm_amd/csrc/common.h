@@ -3,6 +3,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -106,11 +107,14 @@ struct Job {
 
 // post.cpp
 void postprocess(Job &job);
-// render.cpp
+// render.cpp: the output as consecutive parts (formatted in parallel)
+std::vector<std::string> render_parts(Job &job, int fmt);
 std::string render(Job &job, int fmt);
 // fasta.cpp
 void load_fasta(Job &job, const char *path, int32_t flank_trim);
 
 int host_threads(const bwtmi_params &p);
+// fn(task) for task in [0, n) on up to nt threads (dynamic scheduling)
+void run_tasks(int64_t n, int nt, const std::function<void(int64_t)> &fn);
 
 }  // namespace bwtmi

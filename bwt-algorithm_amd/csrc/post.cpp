@@ -78,6 +78,10 @@ static void parallel_items(int64_t n, int nt, F &&fn) {
     for (auto &x : th) x.join();
 }
 
+void run_tasks(int64_t n, int nt, const std::function<void(int64_t)> &fn) {
+    parallel_items(n, nt, [&](int64_t k, int) { fn(k); });
+}
+
 // ------------------------------------------------------------ natural key
 std::vector<NatPart> natural_key(const std::string &s) {      // bwt.py:22-36
     std::vector<NatPart> out;
@@ -198,10 +202,23 @@ std::string canon_of(std::string_view m) {
 void sort_by_pos(ItemVec &v, int nt) {
     const size_t n = v.size();
     if (n < 2) return;
-    bool sorted = true;
-    for (size_t i = 1; i < n && sorted; ++i)
-        sorted = v[i - 1].start < v[i].start || (v[i - 1].start == v[i].start && v[i - 1].end <= v[i].end);
-    if (sorted) return;
+    bool sorted = true, by_start = true;
+    for (size_t i = 1; i < n && by_start; ++i) {
+        by_start = v[i - 1].start <= v[i].start;
+        sorted = sorted && (v[i - 1].start < v[i].start || v[i - 1].end <= v[i].end);
+    }
+    if (sorted && by_start) return;
+    if (by_start) {   // the usual case after merge/refine: only equal-start runs need ordering by end
+        size_t i = 0;
+        while (i < n) {
+            size_t j = i + 1;
+            while (j < n && v[j].start == v[i].start) ++j;
+            if (j - i > 1)
+                std::stable_sort(v.begin() + i, v.begin() + j, [](const Item &a, const Item &b) { return a.end < b.end; });
+            i = j;
+        }
+        return;
+    }
     auto lt = [](const Item &a, const Item &b) {
         if (a.start != b.start) return a.start < b.start;
         return a.end < b.end;
@@ -393,14 +410,32 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
 // bwt.py:3222-3289.  should_merge needs a recompute only for same-canonical
 // neighbours within min_len + 1; when it accepts and len(cur.motif) equals the
 // min_len it used, _merge_repeats' recompute has identical arguments and that
-// result is reused.
-bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, const std::string &c1, const Item &r2,
-               const std::string &c2, Item &merged) {
+// result is reused.  Canonical motifs are computed lazily: most neighbours
+// fail the distance test first.
+struct Canon {
+    std::string s;
+    bool ok = false;
+};
+
+inline const std::string &canon_get(const UnitCtx &u, const Item &it, Canon &c) {
+    if (!c.ok) {
+        thread_local std::string tmp;
+        const std::string_view mv = motif_of(u, it);
+        tmp.assign(mv.data(), mv.size());
+        char st;
+        canonical_stranded(tmp, c.s, st);
+        c.ok = true;
+    }
+    return c.s;
+}
+
+bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, Canon &c1, const Item &r2, Canon &c2,
+               Item &merged) {
     if (r1.chrom != r2.chrom) return false;
     if (r1.mlen == 0 || r2.mlen == 0) return false;
     const int64_t ml = std::min(r1.mlen, r2.mlen);
     if (std::max<int64_t>(0, r2.start - r1.end) > ml + 1) return false;   // cheap test first
-    if (c1 != c2) return false;
+    if (canon_get(u, r1, c1) != canon_get(u, r2, c2)) return false;
     const int64_t s = std::min(r1.start, r2.start), e = std::max(r1.end, r2.end);
     const int32_t tier = std::min(r1.tier, r2.tier);
     Item mg = recompute(u, pools, w, r1.chrom, s, e, std::max<int64_t>(1, ml), tier);
@@ -414,29 +449,30 @@ bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, const std:
 }
 
 struct SpecOut {
-    ItemVec emitted;          // records emitted by the speculative run
-    std::vector<int64_t> emit_step;     // index i at which each was emitted
+    ItemVec emitted;                 // records emitted by the speculative run
+    std::vector<int64_t> emit_step;  // index i at which each was emitted
     Item pending;
-    std::string pending_canon;
+    Canon pending_canon;
 };
 
 // speculative run over [b, e): starts with cur = R[b] as if fresh at b
-void spec_run(const UnitCtx &u, Pools &pools, int w, const ItemVec &R,
-              const std::vector<std::string> &canon, int64_t b, int64_t e, std::vector<uint8_t> &fresh, SpecOut &o) {
+void spec_run(const UnitCtx &u, Pools &pools, int w, const ItemVec &R, int64_t b, int64_t e,
+              std::vector<uint8_t> &fresh, SpecOut &o) {
     Item cur = R[(size_t)b];
-    std::string cc = canon[(size_t)b];
+    Canon cc;
     fresh[(size_t)b] = 1;
     Item mg;
     for (int64_t i = b + 1; i < e; ++i) {
-        if (try_merge(u, pools, w, cur, cc, R[(size_t)i], canon[(size_t)i], mg)) {
+        Canon ci;
+        if (try_merge(u, pools, w, cur, cc, R[(size_t)i], ci, mg)) {
             cur = mg;
-            cc = canon_of(motif_of(u, cur));
+            cc.ok = false;
             fresh[(size_t)i] = 0;
         } else {
             o.emitted.push_back(cur);
             o.emit_step.push_back(i);
             cur = R[(size_t)i];
-            cc = canon[(size_t)i];
+            std::swap(cc, ci);
             fresh[(size_t)i] = 1;
         }
     }
@@ -447,51 +483,45 @@ void spec_run(const UnitCtx &u, Pools &pools, int w, const ItemVec &R,
 ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
     const int64_t n = (int64_t)R.size();
     if (n == 0) return {};
-    std::vector<std::string> canon((size_t)n);
-    parallel_for(n, nt, [&](int64_t a, int64_t b) {
-        std::string s, c;
-        char st;
-        for (int64_t i = a; i < b; ++i) {
-            const std::string_view mv = motif_of(u, R[(size_t)i]);
-            s.assign(mv.data(), mv.size());
-            canonical_stranded(s, canon[(size_t)i], st);
-        }
-    });
     const int64_t K = std::max<int64_t>(1, std::min<int64_t>((int64_t)nt * 8, n / 2048 + 1));
     std::vector<int64_t> cut((size_t)K + 1);
     for (int64_t k = 0; k <= K; ++k) cut[(size_t)k] = n * k / K;
     std::vector<uint8_t> fresh((size_t)n, 0);
     std::vector<SpecOut> spec((size_t)K);
     parallel_items(K, nt, [&](int64_t k, int w) {
-        spec_run(u, pools, w, R, canon, cut[(size_t)k], cut[(size_t)k + 1], fresh, spec[(size_t)k]);
+        spec_run(u, pools, w, R, cut[(size_t)k], cut[(size_t)k + 1], fresh, spec[(size_t)k]);
     });
     // repair: chunk 0 is exact; a later chunk's speculative results hold from
     // the first index where the true run restarts (non-merge) at an index
     // where the speculative run restarted too
+    std::vector<size_t> base((size_t)K + 1, 0);
+    for (int64_t k = 0; k < K; ++k) base[(size_t)k + 1] = base[(size_t)k] + spec[(size_t)k].emitted.size();
     ItemVec out;
-    out.reserve((size_t)n);
-    for (auto &r : spec[0].emitted) out.push_back(r);
+    out.reserve(base[(size_t)K] + (size_t)K + 1);
+    out.insert(out.end(), spec[0].emitted.begin(), spec[0].emitted.end());
     Item cur = spec[0].pending;
-    std::string cc = std::move(spec[0].pending_canon);
+    Canon cc = std::move(spec[0].pending_canon);
     Item mg;
     for (int64_t k = 1; k < K; ++k) {
         const int64_t b = cut[(size_t)k], e = cut[(size_t)k + 1];
         SpecOut &sp = spec[(size_t)k];
         int64_t sync = -1;
         for (int64_t i = b; i < e; ++i) {
-            if (try_merge(u, pools, 0, cur, cc, R[(size_t)i], canon[(size_t)i], mg)) {
+            Canon ci;
+            if (try_merge(u, pools, 0, cur, cc, R[(size_t)i], ci, mg)) {
                 cur = mg;
-                cc = canon_of(motif_of(u, cur));
+                cc.ok = false;
             } else {
                 out.push_back(cur);
                 cur = R[(size_t)i];
-                cc = canon[(size_t)i];
+                std::swap(cc, ci);
                 if (fresh[(size_t)i]) { sync = i; break; }
             }
         }
         if (sync < 0) continue;   // never re-synchronised: `cur` carries into chunk k+1
-        for (size_t q = 0; q < sp.emitted.size(); ++q)
-            if (sp.emit_step[q] > sync) out.push_back(sp.emitted[q]);
+        size_t q = 0;
+        while (q < sp.emitted.size() && sp.emit_step[q] <= sync) ++q;
+        out.insert(out.end(), sp.emitted.begin() + (std::ptrdiff_t)q, sp.emitted.end());
         cur = sp.pending;
         cc = std::move(sp.pending_canon);
     }
@@ -653,9 +683,11 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     recs = merge_fold(u, pools, recs, nt);
     auto t3 = clk::now();
     // 4. refine (bwt.py:3291-3314): only recomputed records can carry mismatches
-    parallel_items((int64_t)recs.size(), nt, [&](int64_t k, int w) {
-        Item &r = recs[(size_t)k];
-        if (mm_of(r) == 0.0) return;
+    std::vector<uint32_t> imperfect;
+    for (size_t k = 0; k < recs.size(); ++k)
+        if (recs[k].x && recs[k].x->mm != 0.0) imperfect.push_back((uint32_t)k);
+    parallel_items((int64_t)imperfect.size(), nt, [&](int64_t q, int w) {
+        Item &r = recs[imperfect[(size_t)q]];
         int64_t m = r.mlen;
         if (m <= 0) {
             const int64_t rc = (int64_t)std::nearbyint(copies_of(r));
@@ -663,7 +695,9 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
         }
         r = recompute(u, pools, w, r.chrom, r.start, r.end, m, r.tier);
     });
+    auto r1 = clk::now();
     sort_by_pos(recs, nt);
+    auto r2 = clk::now();
     // 5. restore coordinates (bwt.py:3316-3325); actual_sequence is the frame slice
     for (auto &r : recs) {
         const int64_t off = job.contigs[(size_t)r.chrom].trim_left;
@@ -672,28 +706,33 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     }
     // 6. collapse (bwt.py:3499-3513)
     sort_by_pos(recs, nt);
-    {
-        ItemVec col;
-        col.reserve(recs.size());
-        for (auto &r : recs) {
-            if (!col.empty() && should_collapse(u, col.back(), r)) {
-                if (!prefer_first(u, col.back(), r)) col.back() = r;
-            } else {
-                col.push_back(r);
-            }
+    auto r3 = clk::now();
+    const size_t n_before_collapse = recs.size();
+    std::vector<uint32_t> col;   // collapsed list as indices into recs (the slot takes the preferred record)
+    col.reserve(recs.size());
+    for (size_t k = 0; k < recs.size(); ++k) {
+        if (!col.empty() && should_collapse(u, recs[col.back()], recs[k])) {
+            if (!prefer_first(u, recs[col.back()], recs[k])) col.back() = (uint32_t)k;
+        } else {
+            col.push_back((uint32_t)k);
         }
-        recs.swap(col);
     }
+    auto r4 = clk::now();
     // 7. final filter (bwt.py:3940-3944)
     std::vector<uint32_t> keep;
-    for (size_t i = 0; i < recs.size(); ++i)
+    for (uint32_t i : col)
         if (copies_of(recs[i]) >= (double)job.params.min_copies && recs[i].end - recs[i].start >= 6)
-            keep.push_back((uint32_t)i);
+            keep.push_back(i);
     out.resize(keep.size());
     parallel_for((int64_t)keep.size(), nt, [&](int64_t a, int64_t b) {
         for (int64_t q = a; q < b; ++q) out[(size_t)q] = materialize(u, recs[keep[(size_t)q]]);
     });
     auto t4 = clk::now();
+    if (std::getenv("BWTMI_STATS")) {
+        auto d = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "  merge %.1f (-> %zu) refine %.1f sort %.1f restore+sort %.1f collapse %.1f (%zu -> %zu) filter+mat %.1f ms\n",
+                     d(t2, t3), n_before_collapse, d(t3, r1), d(r1, r2), d(r2, r3), d(r3, r4), n_before_collapse, col.size(), d(r4, t4));
+    }
     if (ms) {
         ms[0] += std::chrono::duration<double, std::milli>(t1 - t0).count();
         ms[1] += std::chrono::duration<double, std::milli>(t2 - t1).count();

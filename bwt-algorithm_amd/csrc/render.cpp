@@ -7,7 +7,10 @@
 #include <chrono>
 #include <cinttypes>
 #include <cmath>
+#include <charconv>
 #include <cstdio>
+#include <cstring>
+#include <deque>
 #include <string>
 #include <vector>
 
@@ -81,56 +84,65 @@ void kmer_scan(const Job &job, int32_t chrom, int64_t start, int64_t end, std::v
     }
 }
 
-struct Compound {
-    std::vector<Rec> result;
-    std::vector<Rec> partners;
+// one output row of the STRfinder writer: a final record or a compound piece,
+// with its compound partner (bwt.py:4126-4130)
+struct Row {
+    const Rec *r;
+    const Rec *partner;   // nullptr unless is_compound
 };
 
-// _detect_compound_repeats (bwt.py:3995-4139) over the final records
-Compound detect_compounds(const Job &job, const std::vector<Rec> &recs) {
-    Compound out;
+struct Compound {
+    std::deque<Rec> pool;   // records created here (k-mer scan and split pieces), pointer-stable
+    std::vector<Row> rows;
+};
+
+// _detect_compound_repeats (bwt.py:3995-4139) over the final records; works on
+// pointers, so the final records are never copied
+void detect_compounds(const Job &job, const std::vector<Rec> &recs, Compound &out) {
     std::vector<int32_t> chrom_order;
-    std::vector<std::vector<Rec>> by(job.contigs.size());
+    std::vector<std::vector<const Rec *>> by(job.contigs.size());
     for (const Rec &r : recs) {
         if (by[(size_t)r.chrom].empty()) chrom_order.push_back(r.chrom);
-        by[(size_t)r.chrom].push_back(r);
+        by[(size_t)r.chrom].push_back(&r);
     }
     for (int32_t ch : chrom_order) {
         const std::string &full = job.contigs[(size_t)ch].full;
         if (full.empty()) continue;
-        std::vector<Rec> &lst = by[(size_t)ch];
+        std::vector<const Rec *> &lst = by[(size_t)ch];
         const size_t n0 = lst.size();
+        std::vector<Rec> kr;
         for (size_t q = 0; q < n0; ++q) {
-            const Rec r = lst[q];
-            if (!r.motif.empty() && r.motif.size() == 3) {
-                const int64_t a = r.end, b = std::min<int64_t>((int64_t)full.size(), r.end + 50);
-                if (a < b) {
-                    std::vector<Rec> kr;
-                    kmer_scan(job, ch, a, b, kr);
-                    for (auto &x : kr)
-                        if (x.motif != r.motif) lst.push_back(std::move(x));
+            const Rec *r = lst[q];
+            if (r->motif.size() != 3) continue;
+            const int64_t a = r->end, b = std::min<int64_t>((int64_t)full.size(), r->end + 50);
+            if (a >= b) continue;
+            kr.clear();
+            kmer_scan(job, ch, a, b, kr);
+            for (auto &x : kr)
+                if (x.motif != r->motif) {
+                    out.pool.push_back(std::move(x));
+                    lst.push_back(&out.pool.back());
                 }
-            }
         }
     }
     for (int32_t ch : chrom_order) {
-        std::vector<Rec> &rs = by[(size_t)ch];
-        std::stable_sort(rs.begin(), rs.end(), [](const Rec &a, const Rec &b) { return a.start < b.start; });
+        std::vector<const Rec *> &rs = by[(size_t)ch];
+        std::stable_sort(rs.begin(), rs.end(), [](const Rec *a, const Rec *b) { return a->start < b->start; });
         struct Long { int64_t s, e; };
         std::vector<Long> longs;
-        for (auto &r : rs)
-            if (r.motif.size() > 10) longs.push_back({r.start, r.end});
+        for (auto *r : rs)
+            if (r->motif.size() > 10) longs.push_back({r->start, r->end});
         const Contig &ctg = job.contigs[(size_t)ch];
         const int64_t TL = ctg.trimmed_len();
         const char *tseq = ctg.trimmed();
         size_t i = 0;
         while (i < rs.size()) {
-            Rec &cur = rs[i];
-            if (cur.motif.size() == 3 && cur.copies >= 10 && TL > 0) {
+            const Rec *cur = rs[i];
+            if (cur->motif.size() == 3 && cur->copies >= 10 && TL > 0) {
                 // repeat_seq = sequences[chrom][cur.start:cur.end] (trimmed sequence, restored
                 // coordinates -- bwt.py:4045-4047)
-                const int64_t a = std::min(std::max<int64_t>(cur.start, 0), TL);
-                const int64_t b = std::max(a, std::min(std::max<int64_t>(cur.end, 0), TL));
+                const int64_t a = std::min(std::max<int64_t>(cur->start, 0), TL);
+                const int64_t b = std::max(a, std::min(std::max<int64_t>(cur->end, 0), TL));
                 const char *rsq = tseq + a;
                 const int64_t rl = b - a;
                 const int64_t k = 3;
@@ -150,49 +162,43 @@ Compound detect_compounds(const Job &job, const std::vector<Rec> &recs) {
                         else break;
                     }
                     if (c1 >= 5 && c2 >= 5 && (double)(c1 * l1 + c2 * l2) >= (double)rl * 0.9) {
-                        const int64_t e1 = cur.start + c1 * l1;
+                        const int64_t e1 = cur->start + c1 * l1;
                         // actual = repeat_seq[:c1*l1], repeat_seq[c1*l1 : c1*l1 + c2*l2]
                         const int64_t x1 = std::min(c1 * l1, rl);
                         const int64_t y0 = std::min(c1 * l1, rl), y1 = std::max(y0, std::min(c1 * l1 + c2 * l2, rl));
-                        Rec r1 = kmer_piece(ch, cur.start, e1, std::string(rsq, (size_t)l1), c1, cur.tier,
-                                            ACT_TRIMMED, a, x1);
-                        Rec r2 = kmer_piece(ch, e1, e1 + c2 * l2, std::string(rsq + sp, (size_t)l2), c2,
-                                            cur.tier, ACT_TRIMMED, a + y0, y1 - y0);
-                        r1.is_compound = true;
-                        r1.partner = (int32_t)out.partners.size();
-                        out.partners.push_back(std::move(r2));
-                        out.result.push_back(std::move(r1));
-                        ++i;
+                        out.pool.push_back(kmer_piece(ch, cur->start, e1, std::string(rsq, (size_t)l1), c1, cur->tier,
+                                                      ACT_TRIMMED, a, x1));
+                        Rec *r1 = &out.pool.back();
+                        out.pool.push_back(kmer_piece(ch, e1, e1 + c2 * l2, std::string(rsq + sp, (size_t)l2), c2,
+                                                      cur->tier, ACT_TRIMMED, a + y0, y1 - y0));
+                        r1->is_compound = true;
+                        out.rows.push_back({r1, &out.pool.back()});
+                        ++i;   // the reference advances i inside the split loop (bwt.py:4083)
                     }
                 }
             }
             if (i + 1 < rs.size()) {
-                const Rec &nx = rs[i + 1];
-                const int64_t gap = nx.start - cur.end;
-                if (gap <= 5 && cur.motif.size() <= 4 && nx.motif.size() <= 4 && cur.motif != nx.motif &&
-                    cur.copies >= 5 && nx.copies >= 5) {
-                    const int64_t cs = cur.start, ce = nx.end;
+                const Rec *nx = rs[i + 1];
+                const int64_t gap = nx->start - cur->end;
+                if (gap <= 5 && cur->motif.size() <= 4 && nx->motif.size() <= 4 && cur->motif != nx->motif &&
+                    cur->copies >= 5 && nx->copies >= 5) {
+                    const int64_t cs = cur->start, ce = nx->end;
                     bool covered = false;
                     for (auto &lm : longs) {
                         const int64_t ov = std::max<int64_t>(0, std::min(ce, lm.e) - std::max(cs, lm.s));
                         if ((double)ov / (double)(ce - cs) >= 0.8) { covered = true; break; }
                     }
                     if (!covered) {
-                        Rec c = cur;
-                        c.is_compound = true;
-                        c.partner = (int32_t)out.partners.size();
-                        out.partners.push_back(nx);
-                        out.result.push_back(std::move(c));
+                        out.rows.push_back({cur, nx});
                         i += 2;
                         continue;
                     }
                 }
             }
-            out.result.push_back(cur);
+            out.rows.push_back({cur, nullptr});
             ++i;
         }
     }
-    return out;
 }
 
 // ---------------------------------------------------------------- formatting
@@ -202,15 +208,15 @@ struct Out {
     void put(const std::string &x) { s.append(x); }
     void put(View v) { if (v.n > 0) s.append(v.p, (size_t)v.n); }
     void c(char ch) { s.push_back(ch); }
-    void f(const char *fmt, double x) {
+    void f(const char *fmt, double x) {   // printf keeps Python's exact-value rounding
         char b[64];
         int n = snprintf(b, sizeof b, fmt, x);
         s.append(b, (size_t)n);
     }
     void i(int64_t x) {
-        char b[32];
-        int n = snprintf(b, sizeof b, "%" PRId64, x);
-        s.append(b, (size_t)n);
+        char b[24];
+        auto r = std::to_chars(b, b + sizeof b, x);
+        s.append(b, (size_t)(r.ptr - b));
     }
     void rep(const std::string &m, int64_t times) {
         for (int64_t k = 0; k < times; ++k) s.append(m);
@@ -327,96 +333,115 @@ const char *kVcfHeader =
 
 }  // namespace
 
-std::string render(Job &job, int fmt) {
+// Rows are formatted in parallel, in chunks of consecutive rows; each chunk is
+// one part of the output, so concatenating the parts gives the file.
+std::vector<std::string> render_parts(Job &job, int fmt) {
     auto t0 = std::chrono::steady_clock::now();
     job.assign_units();
     Compound comp;
-    const std::vector<Rec> *rows = &job.final_recs;
+    std::vector<Row> rows;
     if (fmt == BWTMI_FMT_STRFINDER) {
-        comp = detect_compounds(job, job.final_recs);
-        rows = &comp.result;
+        detect_compounds(job, job.final_recs, comp);
+        rows.swap(comp.rows);
+    } else {
+        rows.reserve(job.final_recs.size());
+        for (const Rec &r : job.final_recs) rows.push_back({&r, nullptr});
     }
-    std::vector<uint32_t> order(rows->size());
-    for (size_t i = 0; i < order.size(); ++i) order[i] = (uint32_t)i;
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-        const Rec &x = (*rows)[a], &y = (*rows)[b];
+    // sorted(all_repeats, key=lambda r: (natural_sort_key(r.chrom), r.start, r.end)) (bwt.py:4150)
+    std::stable_sort(rows.begin(), rows.end(), [&](const Row &a, const Row &b) {
+        const Rec &x = *a.r, &y = *b.r;
         const int32_t ux = job.contigs[(size_t)x.chrom].unit, uy = job.contigs[(size_t)y.chrom].unit;
         if (ux != uy) return ux < uy;
         if (x.start != y.start) return x.start < y.start;
         return x.end < y.end;
     });
-    Out o;
-    o.s.reserve(order.size() * 160 + 1024);
-    double cp[4], ent;
+    std::string head;
     switch (fmt) {
         case BWTMI_FMT_BED:
-            o.put("# Tandem Repeats (BED format with imperfect repeat support)\n");
-            o.put("# chrom\tstart\tend\tconsensus_motif\tcopies\ttier\tmismatch_rate\tstrand\n");
-            for (uint32_t k : order) {
-                const Rec &r = (*rows)[k];
-                o.put(job.contigs[(size_t)r.chrom].name); o.c('\t'); o.i(r.start); o.c('\t'); o.i(r.end); o.c('\t');
-                o.put(r.motif); o.c('\t'); o.f("%.1f", r.copies); o.c('\t'); o.i(r.tier); o.c('\t');
-                o.f("%.3f", r.mismatch_rate); o.c('\t'); o.c(r.strand); o.c('\n');
-            }
+            head = "# Tandem Repeats (BED format with imperfect repeat support)\n"
+                   "# chrom\tstart\tend\tconsensus_motif\tcopies\ttier\tmismatch_rate\tstrand\n";
             break;
-        case BWTMI_FMT_VCF: {
-            o.put(kVcfHeader);
-            int64_t idx = 0;
-            for (uint32_t k : order) {
-                const Rec &r = (*rows)[k];
-                o.put(job.contigs[(size_t)r.chrom].name); o.c('\t'); o.i(r.start + 1); o.put("\tTR"); o.i(idx++);
-                o.put("\t.\t<TR>\t.\tPASS\tMOTIF="); o.put(r.motif); o.put(";CONS_MOTIF="); o.put(r.motif);
-                o.put(";COPIES="); o.f("%.1f", r.copies); o.put(";TIER="); o.i(r.tier);
-                o.put(";CONF="); o.f("%.2f", r.confidence); o.put(";MM_RATE="); o.f("%.3f", r.mismatch_rate);
-                o.put(";MAX_MM_PER_COPY="); o.i(r.max_mm); o.put(";N_COPIES_EVAL="); o.i(r.n_eval);
-                o.put(";STRAND="); o.c(r.strand); o.c('\n');
-            }
-            break;
-        }
+        case BWTMI_FMT_VCF: head = kVcfHeader; break;
         case BWTMI_FMT_TRF_TABLE:
-            o.put("# Tandem Repeats Finder Compatible Table Format\n");
-            o.put("# Indices\tPeriod\tCopyNumber\tConsensusSize\tPercentMatches\tPercentIndels\t");
-            o.put("Score\tA\tC\tG\tT\tEntropy\n");
-            for (uint32_t k : order) {
-                const Rec &r = (*rows)[k];
-                comp_entropy(r, cp, ent);
-                const int64_t ml = (int64_t)r.motif.size();
-                o.i(r.start); o.put("--"); o.i(r.end); o.c('\t'); o.i(ml); o.c('\t'); o.f("%.1f", r.copies);
-                o.c('\t'); o.i(ml); o.c('\t'); o.f("%.0f", r.pmatch); o.c('\t'); o.f("%.0f", r.pindel); o.c('\t');
-                o.i(r.score); o.c('\t'); o.f("%.0f", cp[0]); o.c('\t'); o.f("%.0f", cp[1]); o.c('\t');
-                o.f("%.0f", cp[2]); o.c('\t'); o.f("%.0f", cp[3]); o.c('\t'); o.f("%.2f", ent); o.c('\n');
-            }
+            head = "# Tandem Repeats Finder Compatible Table Format\n"
+                   "# Indices\tPeriod\tCopyNumber\tConsensusSize\tPercentMatches\tPercentIndels\t"
+                   "Score\tA\tC\tG\tT\tEntropy\n";
             break;
-        case BWTMI_FMT_TRF_DAT:
-            for (uint32_t k : order) {
-                const Rec &r = (*rows)[k];
-                comp_entropy(r, cp, ent);
-                const int64_t ml = (int64_t)r.motif.size();
-                o.i(r.start); o.c(' '); o.i(r.end); o.c(' '); o.i(ml); o.c(' '); o.f("%.1f", r.copies); o.c(' ');
-                o.i(ml); o.c(' '); o.f("%.0f", r.pmatch); o.c(' '); o.f("%.0f", r.pindel); o.c(' ');
-                o.i(r.score); o.c(' '); o.f("%.0f", cp[0]); o.c(' '); o.f("%.0f", cp[1]); o.c(' ');
-                o.f("%.0f", cp[2]); o.c(' '); o.f("%.0f", cp[3]); o.c(' '); o.f("%.2f", ent); o.c(' ');
-                o.put(r.motif); o.c(' ');
-                View av = act_of(job, r);
-                if (!av.empty()) o.put(av); else o.rep(r.motif, (int64_t)r.copies);
-                o.c('\n');
-            }
-            break;
+        case BWTMI_FMT_TRF_DAT: break;
         case BWTMI_FMT_STRFINDER:
-            o.put("STR_marker\tSTR_position\tSTR_motif\tSTR_genotype_structure\tSTR_genotype\t");
-            o.put("STR_core_seq\tAllele_coverage\tAlleles_ratio\tReads_Distribution(consensused)\t");
-            o.put("STR_depth\tFull_seq\tVariations\n");
-            for (uint32_t k : order) {
-                const Rec &r = (*rows)[k];
-                const Rec *p = (r.is_compound && r.partner >= 0) ? &comp.partners[(size_t)r.partner] : nullptr;
-                row_strfinder(o, job, r, p);
-            }
+            head = "STR_marker\tSTR_position\tSTR_motif\tSTR_genotype_structure\tSTR_genotype\t"
+                   "STR_core_seq\tAllele_coverage\tAlleles_ratio\tReads_Distribution(consensused)\t"
+                   "STR_depth\tFull_seq\tVariations\n";
             break;
         default:
             fail(BWTMI_E_ARG, "unknown output format %d", fmt);
     }
+    const int64_t n = (int64_t)rows.size();
+    const int64_t CH = 8192;
+    const int64_t nch = (n + CH - 1) / CH;
+    std::vector<std::string> parts((size_t)nch + 1);
+    parts[0] = std::move(head);
+    run_tasks(nch, host_threads(job.params), [&](int64_t ck) {
+        Out o;
+        const int64_t a = ck * CH, b = std::min(n, a + CH);
+        o.s.reserve((size_t)(b - a) * 192);
+        double cp[4], ent;
+        for (int64_t k = a; k < b; ++k) {
+            const Rec &r = *rows[(size_t)k].r;
+            switch (fmt) {
+                case BWTMI_FMT_BED:
+                    o.put(job.contigs[(size_t)r.chrom].name); o.c('\t'); o.i(r.start); o.c('\t'); o.i(r.end);
+                    o.c('\t'); o.put(r.motif); o.c('\t'); o.f("%.1f", r.copies); o.c('\t'); o.i(r.tier); o.c('\t');
+                    o.f("%.3f", r.mismatch_rate); o.c('\t'); o.c(r.strand); o.c('\n');
+                    break;
+                case BWTMI_FMT_VCF:
+                    o.put(job.contigs[(size_t)r.chrom].name); o.c('\t'); o.i(r.start + 1); o.put("\tTR"); o.i(k);
+                    o.put("\t.\t<TR>\t.\tPASS\tMOTIF="); o.put(r.motif); o.put(";CONS_MOTIF="); o.put(r.motif);
+                    o.put(";COPIES="); o.f("%.1f", r.copies); o.put(";TIER="); o.i(r.tier);
+                    o.put(";CONF="); o.f("%.2f", r.confidence); o.put(";MM_RATE="); o.f("%.3f", r.mismatch_rate);
+                    o.put(";MAX_MM_PER_COPY="); o.i(r.max_mm); o.put(";N_COPIES_EVAL="); o.i(r.n_eval);
+                    o.put(";STRAND="); o.c(r.strand); o.c('\n');
+                    break;
+                case BWTMI_FMT_TRF_TABLE: {
+                    comp_entropy(r, cp, ent);
+                    const int64_t ml = (int64_t)r.motif.size();
+                    o.i(r.start); o.put("--"); o.i(r.end); o.c('\t'); o.i(ml); o.c('\t'); o.f("%.1f", r.copies);
+                    o.c('\t'); o.i(ml); o.c('\t'); o.f("%.0f", r.pmatch); o.c('\t'); o.f("%.0f", r.pindel); o.c('\t');
+                    o.i(r.score); o.c('\t'); o.f("%.0f", cp[0]); o.c('\t'); o.f("%.0f", cp[1]); o.c('\t');
+                    o.f("%.0f", cp[2]); o.c('\t'); o.f("%.0f", cp[3]); o.c('\t'); o.f("%.2f", ent); o.c('\n');
+                    break;
+                }
+                case BWTMI_FMT_TRF_DAT: {
+                    comp_entropy(r, cp, ent);
+                    const int64_t ml = (int64_t)r.motif.size();
+                    o.i(r.start); o.c(' '); o.i(r.end); o.c(' '); o.i(ml); o.c(' '); o.f("%.1f", r.copies); o.c(' ');
+                    o.i(ml); o.c(' '); o.f("%.0f", r.pmatch); o.c(' '); o.f("%.0f", r.pindel); o.c(' ');
+                    o.i(r.score); o.c(' '); o.f("%.0f", cp[0]); o.c(' '); o.f("%.0f", cp[1]); o.c(' ');
+                    o.f("%.0f", cp[2]); o.c(' '); o.f("%.0f", cp[3]); o.c(' '); o.f("%.2f", ent); o.c(' ');
+                    o.put(r.motif); o.c(' ');
+                    View av = act_of(job, r);
+                    if (!av.empty()) o.put(av); else o.rep(r.motif, (int64_t)r.copies);
+                    o.c('\n');
+                    break;
+                }
+                default:   // STRfinder
+                    row_strfinder(o, job, r, rows[(size_t)k].partner);
+            }
+        }
+        parts[(size_t)ck + 1] = std::move(o.s);
+    });
     job.stage_ms[6] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return std::move(o.s);
+    return parts;
+}
+
+std::string render(Job &job, int fmt) {
+    std::vector<std::string> parts = render_parts(job, fmt);
+    size_t tot = 0;
+    for (auto &p : parts) tot += p.size();
+    std::string s;
+    s.reserve(tot);
+    for (auto &p : parts) s.append(p);
+    return s;
 }
 
 }  // namespace bwtmi
