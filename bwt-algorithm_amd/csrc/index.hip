@@ -224,9 +224,14 @@ __global__ void k_kentries(const uint8_t *__restrict__ t, int64_t n, int k, cons
     vals[e] = (uint32_t)(i - k + 1);
 }
 
-__global__ void k_khist(const uint64_t *__restrict__ keys, int64_t m, uint32_t *__restrict__ h) {
+// CSR offsets from the sorted k-mer codes: boundary i (between keys[i-1] and
+// keys[i]) owns the codes (keys[i-1], keys[i]]; every code is written once
+__global__ void k_kbounds(const uint64_t *__restrict__ keys, int64_t m, int64_t *__restrict__ off) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < m) atomicAdd(&h[keys[i]], 1u);
+    if (i > m) return;
+    const int64_t prev = i == 0 ? -1 : (int64_t)keys[i - 1];
+    const int64_t cur = i == m ? 65536 : (int64_t)keys[i];
+    for (int64_t code = prev + 1; code <= cur; ++code) off[code] = i;
 }
 
 // ---- LCP: chunked Kasai (exact while the only rank-0 suffix is the last one)
@@ -473,18 +478,8 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
             radix_sort_pairs32(c, keys, ix->kmer_pos.as<uint32_t>(), nent, 0, 16);
         }
         ix->kmer_off.ensure((size_t)(65537) * 8);
-        c.slot[S_MISC0].ensure(65537 * 8);
-        uint32_t *kh = c.slot[S_MISC0].as<uint32_t>();
-        HIPCHECK(hipMemsetAsync(kh, 0, 65537 * 4, st));
-        if (nent > 0) hipLaunchKernelGGL(k_khist, dim3(blocks(nent)), dim3(256), 0, st, keys, nent, kh);
-        std::vector<uint32_t> hh(65537);
-        HIPCHECK(hipMemcpyAsync(hh.data(), kh, 65537 * 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipStreamSynchronize(st));
-        std::vector<int64_t> offs(65537);
-        int64_t s = 0;
-        for (int q = 0; q < 65536; ++q) { offs[q] = s; s += hh[q]; }
-        offs[65536] = s;
-        HIPCHECK(hipMemcpyAsync(ix->kmer_off.p, offs.data(), 65537 * 8, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_kbounds, dim3(blocks(nent + 1)), dim3(256), 0, st, keys, nent,
+                           ix->kmer_off.as<int64_t>());
         ix->kmer_count = nent;
     }
     HIPCHECK(hipGetLastError());

@@ -488,17 +488,24 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
     for (int64_t k = 0; k <= K; ++k) cut[(size_t)k] = n * k / K;
     std::vector<uint8_t> fresh((size_t)n, 0);
     std::vector<SpecOut> spec((size_t)K);
+    auto ts0 = std::chrono::steady_clock::now();
     parallel_items(K, nt, [&](int64_t k, int w) {
         spec_run(u, pools, w, R, cut[(size_t)k], cut[(size_t)k + 1], fresh, spec[(size_t)k]);
     });
+    auto ts1 = std::chrono::steady_clock::now();
+    if (std::getenv("BWTMI_STATS"))
+        std::fprintf(stderr, "  merge spec %.1f ms (K=%lld)\n",
+                     std::chrono::duration<double, std::milli>(ts1 - ts0).count(), (long long)K);
     // repair: chunk 0 is exact; a later chunk's speculative results hold from
     // the first index where the true run restarts (non-merge) at an index
     // where the speculative run restarted too
-    std::vector<size_t> base((size_t)K + 1, 0);
-    for (int64_t k = 0; k < K; ++k) base[(size_t)k + 1] = base[(size_t)k] + spec[(size_t)k].emitted.size();
-    ItemVec out;
-    out.reserve(base[(size_t)K] + (size_t)K + 1);
-    out.insert(out.end(), spec[0].emitted.begin(), spec[0].emitted.end());
+    // The serial part only walks each chunk up to its sync point; the output
+    // is then assembled in parallel: chunk k contributes rep[k] (records the
+    // true run emitted before syncing) and spec[k].emitted[from[k]..].
+    std::vector<ItemVec> rep((size_t)K);
+    std::vector<size_t> from((size_t)K, 0);
+    std::vector<uint8_t> synced((size_t)K, 0);
+    synced[0] = 1;
     Item cur = spec[0].pending;
     Canon cc = std::move(spec[0].pending_canon);
     Item mg;
@@ -512,7 +519,7 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
                 cur = mg;
                 cc.ok = false;
             } else {
-                out.push_back(cur);
+                rep[(size_t)k].push_back(cur);
                 cur = R[(size_t)i];
                 std::swap(cc, ci);
                 if (fresh[(size_t)i]) { sync = i; break; }
@@ -521,11 +528,27 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
         if (sync < 0) continue;   // never re-synchronised: `cur` carries into chunk k+1
         size_t q = 0;
         while (q < sp.emitted.size() && sp.emit_step[q] <= sync) ++q;
-        out.insert(out.end(), sp.emitted.begin() + (std::ptrdiff_t)q, sp.emitted.end());
+        from[(size_t)k] = q;
+        synced[(size_t)k] = 1;
         cur = sp.pending;
         cc = std::move(sp.pending_canon);
     }
-    out.push_back(cur);
+    std::vector<size_t> at((size_t)K + 1, 0);
+    for (int64_t k = 0; k < K; ++k) {
+        const SpecOut &sp = spec[(size_t)k];
+        at[(size_t)k + 1] = at[(size_t)k] + rep[(size_t)k].size() +
+                            (synced[(size_t)k] ? sp.emitted.size() - from[(size_t)k] : 0);
+    }
+    ItemVec out(at[(size_t)K] + 1);
+    parallel_items(K, nt, [&](int64_t k, int) {
+        const SpecOut &sp = spec[(size_t)k];
+        Item *dst = out.data() + at[(size_t)k];
+        const ItemVec &rp = rep[(size_t)k];
+        std::copy(rp.begin(), rp.end(), dst);
+        if (synced[(size_t)k])
+            std::copy(sp.emitted.begin() + (std::ptrdiff_t)from[(size_t)k], sp.emitted.end(), dst + rp.size());
+    });
+    out[at[(size_t)K]] = cur;
     return out;
 }
 

@@ -32,89 +32,59 @@ namespace {
 constexpr uint32_t FULL = 0xFFFFFFFFu;
 
 // ------------------------------------------------------------------ pack
+// Bit-plane layout: word w (positions 32w .. 32w+31) is B uint32 planes,
+// plane p holding bit p of each position's code (bit k <-> position 32w+k).
+// The equality mask of two windows is then ~OR_p(a_p ^ b_p): no bit
+// compaction, and an unaligned window is one v_alignbit per plane.
 template <int B>
 __global__ __launch_bounds__(256) void k_pack(const uint8_t *__restrict__ text, int64_t n,
-                                              const uint8_t *__restrict__ code, uint64_t *__restrict__ P,
+                                              const uint8_t *__restrict__ code, uint32_t *__restrict__ P,
                                               int64_t nwords) {
-    constexpr int S = 64 / B;
     __shared__ uint8_t cmap[256];
     cmap[threadIdx.x] = code[threadIdx.x];
     __syncthreads();
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= nwords) return;
-    const int64_t j0 = w * S;
-    uint64_t x = 0;
-    if (j0 + S <= n) {
-        // aligned vector loads of S bytes
-        uint64_t lo = 0;
+    const int64_t j0 = w * 32;
+    uint32_t pl[B];
 #pragma unroll
-        for (int q = 0; q < S / 8; ++q) {
+    for (int p = 0; p < B; ++p) pl[p] = 0;
+    if (j0 + 32 <= n) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
             const uint64_t v = *reinterpret_cast<const uint64_t *>(text + j0 + 8 * q);
 #pragma unroll
-            for (int b = 0; b < 8; ++b) lo |= (uint64_t)cmap[(v >> (8 * b)) & 255u] << ((8 * q + b) * B);
+            for (int b = 0; b < 8; ++b) {
+                const uint32_t cd = cmap[(v >> (8 * b)) & 255u];
+#pragma unroll
+                for (int p = 0; p < B; ++p) pl[p] |= ((cd >> p) & 1u) << (8 * q + b);
+            }
         }
-        x = lo;
     } else {
-        for (int k = 0; k < S; ++k)
-            if (j0 + k < n) x |= (uint64_t)cmap[text[j0 + k]] << (k * B);
+        for (int k = 0; k < 32; ++k)
+            if (j0 + k < n) {
+                const uint32_t cd = cmap[text[j0 + k]];
+#pragma unroll
+                for (int p = 0; p < B; ++p) pl[p] |= ((cd >> p) & 1u) << k;
+            }
     }
-    P[w] = x;
+#pragma unroll
+    for (int p = 0; p < B; ++p) P[w * B + p] = pl[p];
 }
 
-// 64-bit window of symbols j .. j+S-1
+// M_L for positions 32w .. 32w+31 (bit k <-> position 32w+k), from global planes
 template <int B>
-__device__ __forceinline__ uint64_t window(const uint64_t *__restrict__ P, int64_t j) {
-    constexpr int S = 64 / B;
-    const int64_t q = j / S;
-    const int r = (int)(j - q * S) * B;
-    const uint64_t lo = P[q];
-    if (r == 0) return lo;
-    return (lo >> r) | (P[q + 1] << (64 - r));
-}
-
-// per-symbol equality of two windows -> dense mask of S bits
-template <int B>
-__device__ __forceinline__ uint32_t eqbits(uint64_t a, uint64_t b) {
-    uint64_t x = a ^ b;
-    if constexpr (B == 2) {
-        x = ~(x | (x >> 1)) & 0x5555555555555555ull;
-        x = (x | (x >> 1)) & 0x3333333333333333ull;
-        x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
-        x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
-        x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
-        x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
-        return (uint32_t)x;
-    } else if constexpr (B == 4) {
-        x = ~(x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x1111111111111111ull;
-        x = (x | (x >> 3)) & 0x0303030303030303ull;
-        x = (x | (x >> 6)) & 0x000F000F000F000Full;
-        x = (x | (x >> 12)) & 0x000000FF000000FFull;
-        x = (x | (x >> 24)) & 0x000000000000FFFFull;
-        return (uint32_t)x;
-    } else {
-        uint64_t t = (x & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full;
-        t = ~(t | x | 0x7F7F7F7F7F7F7F7Full);  // 0x80 in every zero byte
-        x = (t >> 7) & 0x0101010101010101ull;
-        x = (x | (x >> 7)) & 0x0003000300030003ull;
-        x = (x | (x >> 14)) & 0x0000000F0000000Full;
-        x = (x | (x >> 28)) & 0xFFull;
-        return (uint32_t)x;
-    }
-}
-
-// M_L for positions 32w .. 32w+31 (bit k <-> position 32w+k)
-template <int B>
-__device__ __forceinline__ uint32_t eq32(const uint64_t *__restrict__ P, int64_t w, int64_t L, int64_t n) {
-    constexpr int S = 64 / B;
+__device__ __forceinline__ uint32_t eq32(const uint32_t *__restrict__ P, int64_t w, int64_t L, int64_t n) {
     const int64_t j0 = w * 32;
     const int64_t lim = n - L - j0;  // positions j0+k valid iff k < lim
     if (w < 0 || lim <= 0) return 0u;
-    uint32_t m = 0;
+    const int64_t q = w + (L >> 5);
+    const uint32_t r = (uint32_t)(L & 31);
+    uint32_t x = 0;
 #pragma unroll
-    for (int h = 0; h < 32 / S; ++h) {
-        const int64_t j = j0 + h * S;
-        m |= eqbits<B>(P[j / S], window<B>(P, j + L)) << (h * S);
-    }
+    for (int p = 0; p < B; ++p)
+        x |= P[w * B + p] ^ __builtin_amdgcn_alignbit(P[(q + 1) * B + p], P[q * B + p], r);
+    uint32_t m = ~x;
     if (lim < 32) m &= (1u << lim) - 1u;
     return m;
 }
@@ -135,30 +105,56 @@ __device__ __forceinline__ void emit(const CandOut &o, int64_t L, int64_t s, int
     }
 }
 
-// grid.x: tiles of 256 words (8192 positions); grid.y: chunks of LCH unit lengths
-template <int B, int LCH>
-__global__ __launch_bounds__(256) void k_runs(const uint64_t *__restrict__ P, int64_t n, int64_t nwords32,
+constexpr int kOwn = 62;   // words owned per wave: lanes 1..62; lanes 0 and 63 only feed neighbours
+
+// grid.x: tiles of 4 waves x 62 words; grid.y: group g of unit lengths
+// L in [32g, 32g+31].  All L of a group read the same two words q = w+g,
+// q+1, so a lane loads its planes once and derives every M_L in registers.
+template <int B>
+__global__ __launch_bounds__(256) void k_runs(const uint32_t *__restrict__ P, int64_t n, int64_t nwords32,
                                               int32_t lmin, int32_t lmax, int64_t mc, CandOut out) {
     const int lane = threadIdx.x & 63;
-    const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t l0 = lmax - (int64_t)blockIdx.y * LCH;
-    for (int li = 0; li < LCH; ++li) {
-        const int64_t L = l0 - li;
-        if (L < lmin) break;                                     // uniform across the block
-        if ((int64_t)blockIdx.x * 256 * 32 >= n - L) break;      // whole tile past n-L
+    const int64_t wave_base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kOwn;
+    const int64_t w = wave_base - 1 + lane;
+    const bool owned = lane >= 1 && lane <= kOwn && w < nwords32;
+    const int64_t g = (int64_t)blockIdx.y + (lmin >> 5);
+    const int64_t j0 = w * 32;
+    const int64_t tile_j0 = (int64_t)blockIdx.x * 4 * kOwn * 32;
+    uint32_t a[B], lo[B], hi[B];
+    const bool inb = w >= 0 && w < nwords32;
+    // words past the text (the planes are zero-padded by 8 words) only feed
+    // positions that the `lim` mask below discards
+    const bool lok = inb && w + g + 1 < nwords32 + 8;
+#pragma unroll
+    for (int p = 0; p < B; ++p) {
+        a[p] = inb ? P[w * B + p] : 0u;
+        lo[p] = lok ? P[(w + g) * B + p] : 0u;
+        hi[p] = lok ? P[(w + g + 1) * B + p] : 0u;
+    }
+    for (int r = 0; r < 32; ++r) {
+        const int64_t L = g * 32 + r;
+        if (L < lmin) continue;
+        if (L > lmax || tile_j0 >= n - L) break;        // uniform across the block
+        uint32_t x = 0;
+#pragma unroll
+        for (int p = 0; p < B; ++p) x |= a[p] ^ __builtin_amdgcn_alignbit(hi[p], lo[p], (uint32_t)r);
+        uint32_t M = ~x;
+        const int64_t lim = n - L - j0;
+        if (!inb || lim <= 0) M = 0u;
+        else if (lim < 32) M &= (1u << lim) - 1u;
         const int64_t K = (mc - 1) * L;
-        const uint32_t M = eq32<B>(P, w, L, n);
-        // neighbour masks: lanes 0 / 63 compute the word outside the wave
-        uint32_t X = 0;
-        if (lane == 0 || lane == 63) X = eq32<B>(P, lane == 0 ? w - 1 : w + 1, L, n);
-        uint32_t Mp = (uint32_t)__shfl_up((int)M, 1, 64);
-        uint32_t Mn = (uint32_t)__shfl_down((int)M, 1, 64);
-        if (lane == 0) Mp = X;
-        if (lane == 63) Mn = X;
-        if (w >= nwords32) continue;
-        const int64_t j0 = w * 32;
+        if (K > 62) {
+            // a qualifying run is >= 64 long, so it contains a full aligned
+            // word: only the first full word of a streak can own it
+            if (!__any(M == FULL)) continue;
+        } else if (!__any(M != 0u)) {
+            continue;
+        }
+        const uint32_t Mp = (uint32_t)__shfl_up((int)M, 1, 64);
+        const uint32_t Mn = (uint32_t)__shfl_down((int)M, 1, 64);
+        if (!owned) continue;
         if (M == FULL) {
-            if (Mp != FULL) {  // first full word of a streak: the run contains >= 1 aligned word
+            if (Mp != FULL) {   // first full word of a streak
                 const int64_t s = j0 - (int64_t)__clz(~Mp);
                 int64_t q = w + 1;
                 uint32_t Mq = Mn;
@@ -170,13 +166,22 @@ __global__ __launch_bounds__(256) void k_runs(const uint64_t *__restrict__ P, in
                 if (e - s >= K) emit(out, L, s, e);
             }
         } else if (K <= 62 && M != 0u) {
-            // runs that start in this word and contain no full aligned word
+            // runs that start in this word and contain no full aligned word;
+            // only starts with K ones ahead (within M:Mn) can qualify
             uint32_t starts = M & ~((M << 1) | (Mp >> 31));
+            const uint64_t V = (uint64_t)M | ((uint64_t)Mn << 32);
+            uint64_t A = V;
+            for (int64_t have = 1; have < K;) {
+                const int64_t s = have < K - have ? have : K - have;
+                A &= A >> s;
+                have += s;
+            }
+            starts &= (uint32_t)A;
             while (starts) {
                 const int k = __ffs(starts) - 1;
                 starts &= starts - 1;
-                const uint32_t r = M >> k;
-                const int len_in = __ffs(~r) - 1;  // ~r has its top k bits set
+                const uint32_t rr = M >> k;
+                const int len_in = __ffs(~rr) - 1;  // ~rr has its top k bits set
                 int64_t e;
                 if (k + len_in < 32) {
                     e = j0 + k + len_in;
@@ -299,13 +304,12 @@ __global__ void k_hist256(const uint8_t *__restrict__ t, int64_t n, unsigned lon
 }
 
 template <int B>
-void launch_runs(Ctx &c, const uint64_t *P, int64_t n, int32_t lmin, int32_t lmax, int64_t mc, CandOut out) {
-    constexpr int LCH = 8;
+void launch_runs(Ctx &c, const uint32_t *P, int64_t n, int32_t lmin, int32_t lmax, int64_t mc, CandOut out) {
     const int64_t nwords32 = (n + 31) / 32;
-    const int64_t tiles = (nwords32 + 255) / 256;
-    const int64_t chunks = ((int64_t)lmax - lmin + LCH) / LCH;
-    hipLaunchKernelGGL((k_runs<B, LCH>), dim3((unsigned)tiles, (unsigned)chunks), dim3(256), 0, c.stream, P, n,
-                       nwords32, lmin, lmax, mc, out);
+    const int64_t tiles = (nwords32 + 4 * kOwn - 1) / (4 * kOwn);
+    const int64_t groups = (int64_t)(lmax >> 5) - (int64_t)(lmin >> 5) + 1;
+    hipLaunchKernelGGL((k_runs<B>), dim3((unsigned)tiles, (unsigned)groups), dim3(256), 0, c.stream, P, n, nwords32,
+                       lmin, lmax, mc, out);
 }
 
 }  // namespace
@@ -381,16 +385,16 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     int sigma = 0;
     for (int b = 0; b < 256; ++b)
         if (hist[b]) code[b] = (uint8_t)sigma++;
-    const int B = sigma <= 4 ? 2 : (sigma <= 16 ? 4 : 8);
-    const int S = 64 / B;
-    const int64_t nwords = (n + S - 1) / S + 8;
-    c.slot[S_PACK].ensure((size_t)nwords * sizeof(uint64_t) + 256);
-    uint8_t *d_code = c.slot[S_PACK].as<uint8_t>() + nwords * sizeof(uint64_t);
+    const int B = sigma <= 2 ? 1 : (sigma <= 4 ? 2 : (sigma <= 16 ? 4 : 8));
+    const int64_t nwords = (n + 31) / 32 + 8;   // + padding read by the window of the last words
+    c.slot[S_PACK].ensure((size_t)nwords * B * sizeof(uint32_t) + 256);
+    uint8_t *d_code = c.slot[S_PACK].as<uint8_t>() + nwords * B * sizeof(uint32_t);
     HIPCHECK(hipMemcpyAsync(d_code, code, 256, hipMemcpyHostToDevice, st));
-    uint64_t *P = c.slot[S_PACK].as<uint64_t>();
-    HIPCHECK(hipMemsetAsync(P, 0, (size_t)nwords * sizeof(uint64_t), st));
+    uint32_t *P = c.slot[S_PACK].as<uint32_t>();
+    HIPCHECK(hipMemsetAsync(P, 0, (size_t)nwords * B * sizeof(uint32_t), st));
     const unsigned pgrid = (unsigned)((nwords + 255) / 256);
-    if (B == 2) hipLaunchKernelGGL(k_pack<2>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
+    if (B == 1) hipLaunchKernelGGL(k_pack<1>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
+    else if (B == 2) hipLaunchKernelGGL(k_pack<2>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
     else if (B == 4) hipLaunchKernelGGL(k_pack<4>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
     else hipLaunchKernelGGL(k_pack<8>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
     HIPCHECK(hipGetLastError());
@@ -413,7 +417,8 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
         }
         // compulsory traffic: the packed text once (0.25 B/base at 2 bits)
         c.kbegin("k_runs", (double)n * (double)B / 8.0);
-        if (B == 2) launch_runs<2>(c, P, n, lmin, lmax, min_copies, co);
+        if (B == 1) launch_runs<1>(c, P, n, lmin, lmax, min_copies, co);
+        else if (B == 2) launch_runs<2>(c, P, n, lmin, lmax, min_copies, co);
         else if (B == 4) launch_runs<4>(c, P, n, lmin, lmax, min_copies, co);
         else launch_runs<8>(c, P, n, lmin, lmax, min_copies, co);
         c.kend();
