@@ -28,6 +28,11 @@ for _p in (REPO, os.path.join(REPO, "bwt-algorithm_amd")):
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PMC_SUMMARY = os.path.join(REPO, "profiles", "pmc_traffic.json")
+# bench kernel-timer names -> kernel names in the rocprofv3 summaries
+KERNEL_OF = {"radix_scatter_kv12": "k_scatter<u32>", "radix_scatter_kv16": "k_scatter<u64>",
+             "radix_hist": "k_hist", "k_runs": "k_runs", "screen_levels": "k_level",
+             "bwt_gather": "k_bwt", "occ_blocks": "k_occ_blocks", "sa_init_keys": "k_init_keys"}
 CONTIG_BP = 100_000_000
 FLANK = 30
 
@@ -64,6 +69,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-index", action="store_true", help="skip the FM index (scan-only step)")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
+    ap.add_argument("--pmc-summary", default=PMC_SUMMARY,
+                    help="tools/pmc_traffic.py output giving HBM bytes per launch (roofline.traffic)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -89,7 +96,9 @@ def main():
         trim = FLANK if len(seq) > 2 * FLANK else 0
         job.add_contig(f"contig{k + 1}", seq, trim, trim)
     job.select([rank])
-    job.upload(ctx)
+    t_up = time.perf_counter()
+    job.upload(ctx)                           # host -> HBM once; outside the timed region
+    upload_ms = (time.perf_counter() - t_up) * 1000.0
 
     def step():
         job.reset()
@@ -144,9 +153,16 @@ def main():
     if dom:
         name, (kms, launches, kbytes) = dom
         achieved = kbytes / (kms / 1e3) / 1e9 if kms > 0 else 0.0
+        traffic = None
+        if a.pmc_summary and os.path.exists(a.pmc_summary):
+            with open(a.pmc_summary) as f:
+                pk = json.load(f).get("kernels", {}).get(KERNEL_OF.get(name, name))
+            if pk:
+                traffic = pk["hbm_bytes_per_launch"]
         roofline = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(achieved / HBM_PEAK_GBS, 5), traffic=None, kernel=name,
-                        avg_launch_ms=round(kms / launches, 4), launches_per_step=launches / a.steps)
+                        frac=round(achieved / HBM_PEAK_GBS, 5), traffic=traffic, kernel=name,
+                        alg_bytes_per_launch=round(kbytes / launches), avg_launch_ms=round(kms / launches, 4),
+                        launches_per_step=launches / a.steps)
     cpu = None if a.no_cpu_baseline else cpu_baseline(a.cpu_sample_bp)
     line = {
         "metric": "Mbp/s indexed+scanned (Tier1+2) on 100 Mbp synthetic FASTA, 1/2/4/8 GPU",
@@ -166,6 +182,8 @@ def main():
                                "merge": round(stages[4], 2), "refine..filter": round(stages[5], 2),
                                "render": round(stages[6], 2)},
         "kernels_ms_per_step": {k: round(v[0] / a.steps, 3) for k, v in sorted(kstats.items())},
+        "h2d_upload_ms": round(upload_ms, 2),
+        "value_incl_upload": round(total_bp / 1e6 / (elapsed / a.steps + upload_ms / 1e3), 3),
     }
     print(json.dumps(line))
     if td is not None:
