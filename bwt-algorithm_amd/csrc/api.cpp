@@ -7,6 +7,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <new>
 #include <string>
 #include <vector>
@@ -127,6 +130,7 @@ int bwtmi_close(bwtmi_ctx *ctx) {
         if (!ctx) return;
         ctx->c.activate();
         (void)hipStreamSynchronize(ctx->c.stream);
+        if (ctx->c.scratch_index) index_free(ctx->c.scratch_index);
         for (auto &s : ctx->c.slot) s.release();
         for (auto &h : ctx->c.host) h.release();
         (void)hipEventDestroy(ctx->c.ev0);
@@ -423,9 +427,9 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
                 HIPCHECK(hipMemcpyAsync(tb.p, dc.buf.p, (size_t)len, hipMemcpyDeviceToDevice, c.stream));
                 HIPCHECK(hipMemsetAsync(tb.as<uint8_t>() + len, '$', 1, c.stream));
                 HIPCHECK(hipMemsetAsync(tb.as<uint8_t>() + len + 1, 0, 127, c.stream));
-                DeviceIndex *di = index_build_device(c, tb.as<uint8_t>(), len + 1, P.sa_sample, 128,
-                                                     0u);
-                index_free(di);   // the worker never consumes it
+                // the worker never consumes it; its buffers are kept for the next build
+                c.scratch_index = index_build_device(c, tb.as<uint8_t>(), len + 1, P.sa_sample, 128, 0u,
+                                                     c.scratch_index);
                 idx_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ti).count();
             }
             if (!P.tier2) continue;                                  // bwt.py:3068
@@ -479,15 +483,14 @@ int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len) {
     return guard([&] {
         CHECK_ARG(job && out && len, "null argument");
         const std::vector<std::string> parts = render_parts(job->j, fmt);
-        size_t tot = 0;
-        for (auto &s : parts) tot += s.size();
+        std::vector<size_t> at(parts.size() + 1, 0);
+        for (size_t k = 0; k < parts.size(); ++k) at[k + 1] = at[k] + parts[k].size();
+        const size_t tot = at.back();
         char *p = (char *)std::malloc(tot + 1);
         if (!p) fail(BWTMI_E_NOMEM, "malloc");
-        size_t at = 0;
-        for (auto &s : parts) {
-            std::memcpy(p + at, s.data(), s.size());
-            at += s.size();
-        }
+        run_tasks((int64_t)parts.size(), host_threads(job->j.params), [&](int64_t k) {
+            std::memcpy(p + at[(size_t)k], parts[(size_t)k].data(), parts[(size_t)k].size());
+        });
         p[tot] = 0;
         *out = p;
         *len = (int64_t)tot;
@@ -498,12 +501,24 @@ int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path) {
     return guard([&] {
         CHECK_ARG(job && path, "null argument");
         const std::vector<std::string> parts = render_parts(job->j, fmt);
-        FILE *f = std::fopen(path, "wb");
-        if (!f) fail(BWTMI_E_IO, "cannot open %s for writing", path);
-        bool ok = true;
-        for (auto &s : parts) ok = ok && std::fwrite(s.data(), 1, s.size(), f) == s.size();
-        ok = (std::fclose(f) == 0) && ok;
-        if (!ok) fail(BWTMI_E_IO, "short write to %s", path);
+        std::vector<size_t> at(parts.size() + 1, 0);
+        for (size_t k = 0; k < parts.size(); ++k) at[k + 1] = at[k] + parts[k].size();
+        const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        if (fd < 0) fail(BWTMI_E_IO, "cannot open %s for writing", path);
+        // parts land at their final offsets in parallel (page-cache copies)
+        std::vector<uint8_t> ok(parts.size(), 1);
+        run_tasks((int64_t)parts.size(), host_threads(job->j.params), [&](int64_t k) {
+            const std::string &s = parts[(size_t)k];
+            size_t done = 0;
+            while (done < s.size()) {
+                const ssize_t w = ::pwrite(fd, s.data() + done, s.size() - done, (off_t)(at[(size_t)k] + done));
+                if (w <= 0) { ok[(size_t)k] = 0; return; }
+                done += (size_t)w;
+            }
+        });
+        bool good = ::close(fd) == 0;
+        for (auto v : ok) good = good && v;
+        if (!good) fail(BWTMI_E_IO, "short write to %s", path);
     });
 }
 

@@ -18,6 +18,18 @@ struct Error {
 };
 [[noreturn]] void fail(int code, const char *fmt, ...);
 
+// vector storage without value-initialisation: large arrays that are written
+// once (device downloads, parallel fills) skip a serial zero fill
+template <class T>
+struct NoInit : std::allocator<T> {
+    template <class U> struct rebind { using other = NoInit<U>; };
+    NoInit() = default;
+    template <class U> NoInit(const NoInit<U> &) noexcept {}
+    template <class U> void construct(U *p) noexcept { ::new ((void *)p) U; }
+    template <class U, class... A> void construct(U *p, A &&...a) { ::new ((void *)p) U(std::forward<A>(a)...); }
+};
+using HitVec = std::vector<bwtmi_hit, NoInit<bwtmi_hit>>;
+
 // ---------------------------------------------------------------- contigs
 struct Contig {
     std::string name;
@@ -94,7 +106,7 @@ struct Job {
     std::vector<std::vector<NatPart>> natkeys;
     int32_t nunits = 0;
     std::vector<int32_t> unit_rank;                  // unit id -> rank by natural key
-    std::vector<std::vector<bwtmi_hit>> hits;        // per contig strict hits: raw (worker order), or
+    std::vector<HitVec> hits;                        // per contig strict hits: raw (worker order), or
     std::vector<uint8_t> screened;                   // screened[c]: nested-suppressed, sorted by
                                                      // (start, end, m desc, worker order) and deduped
     std::vector<int64_t> raw_n;                      // raw strict hits per contig

@@ -129,6 +129,7 @@ struct Ctx {
     }
     DBuf slot[S_NSLOTS];
     HBuf host[4];
+    struct DeviceIndex *scratch_index = nullptr;   // reused by the worker-path index builds
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_total_ms = 0, last_dom_ms = 0;
     int last_dom_launches = 0;
@@ -145,7 +146,7 @@ void radix_sort_pairs32(Ctx &c, uint64_t *keys, uint32_t *vals, int64_t n, int b
 
 // ----- strict scan (strict_scan.hip)
 struct ScanResult {
-    std::vector<bwtmi_hit> hits;   // raw hits in worker order, or screened hits (see below)
+    HitVec hits;                   // raw hits in worker order, or screened hits (see below)
     double kernel_ms = 0;
     int64_t candidates = 0;
     int64_t raw = 0;               // raw strict hits found
@@ -159,13 +160,13 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
 
 // ----- nested suppression / sort / dedup of one contig's strict hits (nested.hip)
 void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
-                        std::vector<bwtmi_hit> &out);
+                        HitVec &out);
 
 // ----- index (index.hip)
 struct DeviceIndex;
 // d_text: device text incl. sentinel, n bytes (padded by >= 64 bytes)
 DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t sa_sample,
-                                int32_t occ_sample, uint32_t flags);
+                                int32_t occ_sample, uint32_t flags, DeviceIndex *reuse = nullptr);
 void index_free(DeviceIndex *);
 int64_t index_n(const DeviceIndex *);
 int64_t index_occ_len(const DeviceIndex *);

@@ -325,8 +325,10 @@ inline unsigned blocks(int64_t n, int b = 256) { return (unsigned)((n + b - 1) /
 }  // namespace
 
 DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t sa_sample, int32_t occ_sample,
-                                uint32_t flags) {
-    auto *ix = new DeviceIndex();
+                                uint32_t flags, DeviceIndex *reuse) {
+    auto *ix = reuse ? reuse : new DeviceIndex();   // reuse: keep the buffers of an earlier build
+    ix->has_kmer = false;
+    ix->kmer_count = 0;
     hipStream_t st = c.stream;
     ix->n = n;
     ix->sa_sample = sa_sample;

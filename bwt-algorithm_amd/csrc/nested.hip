@@ -220,7 +220,7 @@ __global__ void k_final_compact(const bwtmi_hit *__restrict__ H, const uint32_t 
 }  // namespace
 
 void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
-                        std::vector<bwtmi_hit> &out) {
+                        HitVec &out) {
     out.clear();
     if (n <= 0) return;
     if (n >= (int64_t)UINT32_MAX) fail(BWTMI_E_ARG, "too many strict hits for one contig (%lld)", (long long)n);

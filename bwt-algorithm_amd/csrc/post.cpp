@@ -141,9 +141,9 @@ void Job::assign_units() {
 namespace {
 
 // fields of a record produced by _recompute_repeat (bwt.py:3593-3614)
-struct Extra {
-    std::string motif;          // == consensus_motif
-    std::string variations;     // ';'-joined, empty == None
+struct Extra {                  // trivially destructible: strings live in the Pools arena
+    std::string_view motif;     // == consensus_motif
+    std::string_view variations;  // ';'-joined, empty == None
     double copies = 0, confidence = 0, mm = 0, pmatch = 0, pindel = 0;
     int64_t max_mm = 0, n_eval = 0, score = 0;
     char strand = '+';
@@ -159,22 +159,43 @@ struct Item {
 
 // vector storage without value-initialisation: large item arrays are written
 // once in parallel, so the first touch happens in the filling threads
-template <class T>
-struct NoInit : std::allocator<T> {
-    template <class U> struct rebind { using other = NoInit<U>; };
-    NoInit() = default;
-    template <class U> NoInit(const NoInit<U> &) noexcept {}
-    template <class U> void construct(U *p) noexcept { ::new ((void *)p) U; }
-    template <class U, class... A> void construct(U *p, A &&...a) { ::new ((void *)p) U(std::forward<A>(a)...); }
-};
 using ItemVec = std::vector<Item, NoInit<Item>>;
 
-struct Pools {                  // per-worker arenas of Extras (pointer-stable)
-    std::vector<std::unique_ptr<std::deque<Extra>>> p;
-    explicit Pools(int n) { for (int i = 0; i < n; ++i) p.emplace_back(new std::deque<Extra>()); }
-    Extra *add(int w, Extra &&e) {
-        p[(size_t)w]->push_back(std::move(e));
-        return &p[(size_t)w]->back();
+// per-worker bump arenas for Extras and their strings (pointer-stable; freed
+// as a handful of blocks)
+struct Pools {
+    struct Arena {
+        std::vector<std::unique_ptr<Extra[]>> xb;
+        size_t xn = 0;                                   // used in the last Extra block
+        std::vector<std::unique_ptr<char[]>> cb;
+        size_t cn = 0, ccap = 0;                         // used / size of the last char block
+    };
+    static constexpr size_t XB = 4096, CB = 1 << 20;
+    std::vector<Arena> a;
+    explicit Pools(int n) : a((size_t)n) {}
+    std::string_view str(Arena &A, std::string_view s) {
+        if (s.empty()) return {};
+        if (A.cb.empty() || A.cn + s.size() > A.ccap) {
+            A.ccap = std::max(CB, s.size());
+            A.cb.emplace_back(new char[A.ccap]);
+            A.cn = 0;
+        }
+        char *d = A.cb.back().get() + A.cn;
+        std::memcpy(d, s.data(), s.size());
+        A.cn += s.size();
+        return std::string_view(d, s.size());
+    }
+    Extra *add(int w, const Extra &e, std::string_view motif, std::string_view variations) {
+        Arena &A = a[(size_t)w];
+        if (A.xb.empty() || A.xn == XB) {
+            A.xb.emplace_back(new Extra[XB]);
+            A.xn = 0;
+        }
+        Extra *x = &A.xb.back()[A.xn++];
+        *x = e;
+        x->motif = str(A, motif);
+        x->variations = str(A, variations);
+        return x;
     }
 };
 
@@ -316,16 +337,19 @@ ItemVec suppress_nested(const ItemVec &rs, double thr, int nt) {
 
 // optional counters (BWTMI_STATS=1): recompute calls / time, merge accepts
 std::atomic<int64_t> g_recomputes{0}, g_recompute_ns{0}, g_merges{0};
+const bool g_stats = [] { const char *e = std::getenv("BWTMI_STATS"); return e && *e == '1'; }();
 std::atomic<int64_t> g_hist_n[8][8], g_hist_ns[8][8];   // [log4 motif len][log4 region len]
 inline int lg4(int64_t v) { int k = 0; while (v >= 4 && k < 7) { v >>= 2; ++k; } return k; }
 
 // bwt.py:3515-3614 (on the trimmed sequence, before coordinate restore)
 Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t start, int64_t end,
                int64_t motif_len, int32_t tier) {
-    struct Tick {
+    struct Tick {   // BWTMI_STATS=1 only
         int a, b;
-        std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+        std::chrono::steady_clock::time_point t;
+        Tick(int a_, int b_) : a(a_), b(b_) { if (g_stats) t = std::chrono::steady_clock::now(); }
         ~Tick() {
+            if (!g_stats) return;
             const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t).count();
             g_recomputes.fetch_add(1, std::memory_order_relaxed);
             g_recompute_ns.fetch_add(ns, std::memory_order_relaxed);
@@ -357,28 +381,29 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     Extra x;
     int64_t consumed, cint;
     double mm, pind;
+    const std::string *motif_s = &tmpl;   // never empty
+    std::string_view var_s;
     if (!ok) {
         consumed = std::min(L - start, std::max(m, end - start));
         cint = std::max<int64_t>(1, consumed / m);
-        x.motif = tmpl;  // never empty here
         mm = 0.0;
         x.max_mm = 0;
         pind = 0.0;
     } else {
         consumed = s.consumed;
         cint = s.copies;
-        x.motif = s.consensus.empty() ? tmpl : s.consensus;
+        if (!s.consensus.empty()) motif_s = &s.consensus;
         mm = s.mismatch_rate;
         const int64_t tb = s.copies * s.motif_len;
         const double ir = tb > 0 ? (double)(s.tot_ins + s.tot_del) / (double)tb : 0.0;
         pind = ir * 100.0;
         x.max_mm = s.max_errors;
-        if (s.any_variation) x.variations = s.variations;
+        if (s.any_variation) var_s = s.variations;
     }
     // actual_sequence = sequence[start:start+consumed]
     const int64_t a0 = std::min(start, L), a1 = std::max(a0, std::min(start + consumed, L));
     const int64_t tl = a1 - a0;
-    const int64_t mle = x.motif.empty() ? m : (int64_t)x.motif.size();
+    const int64_t mle = (int64_t)motif_s->size();
     double cf = (double)cint;
     if (tl > 0 && mle > 0) {
         const double fr = (double)tl / (double)mle;
@@ -390,7 +415,7 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     x.mm = mm;
     x.n_eval = std::max<int64_t>(1, cint);
     thread_local std::string canon;
-    canonical_stranded(x.motif, canon, x.strand);
+    canonical_stranded(*motif_s, canon, x.strand);
     x.pmatch = std::max(0.0, 100.0 - mm * 100.0);
     x.pindel = pind;
     x.score = trf_score(tl, mm);
@@ -400,9 +425,9 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     it.count = 0;
     it.moff = 0;
     it.chrom = chrom;
-    it.mlen = (int32_t)x.motif.size();
+    it.mlen = (int32_t)motif_s->size();
     it.tier = tier;
-    it.x = pools.add(w, std::move(x));
+    it.x = pools.add(w, x, *motif_s, var_s);
     return it;
 }
 
@@ -669,7 +694,7 @@ Rec materialize(const UnitCtx &u, const Item &it) {
     return r;
 }
 
-void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vector<std::vector<bwtmi_hit>> &raw,
+void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vector<HitVec> &raw,
                   std::vector<Rec> &out, double *ms, int nt) {
     using clk = std::chrono::steady_clock;
     auto t0 = clk::now();
@@ -692,7 +717,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
                 items[(size_t)k] = Item{x.start, x.end, x.copies, x.start, nullptr, c, x.prim_len, 2, 0};
             }
         });
-        std::vector<bwtmi_hit>().swap(h);
+        HitVec().swap(h);
         if (!scr) items = suppress_nested(items, 0.5, nt);
         if (recs.empty()) recs.swap(items);
         else recs.insert(recs.end(), items.begin(), items.end());
@@ -782,12 +807,24 @@ void postprocess(Job &job) {
             process_unit(job, units[(size_t)k], job.hits, res[(size_t)k], &ms[(size_t)k * 4], 1);
         });
     } else {
-        for (int32_t k = 0; k < job.nunits; ++k)
+        for (int32_t k = 0; k < job.nunits; ++k) {
+            auto a = std::chrono::steady_clock::now();
             process_unit(job, units[(size_t)k], job.hits, res[(size_t)k], &ms[(size_t)k * 4], T);
+            if (g_stats)
+                std::fprintf(stderr, "  unit %d: %.1f ms total\n", k,
+                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count());
+        }
     }
     job.final_recs.clear();
-    for (auto &v : res)
-        for (auto &r : v) job.final_recs.push_back(std::move(r));
+    if (job.nunits == 1) {
+        job.final_recs.swap(res[0]);
+    } else {
+        size_t tot = 0;
+        for (auto &v : res) tot += v.size();
+        job.final_recs.reserve(tot);
+        for (auto &v : res)
+            for (auto &r : v) job.final_recs.push_back(std::move(r));
+    }
     for (int s = 0; s < 4; ++s) {
         job.stage_ms[2 + s] = 0;
         for (int32_t k = 0; k < job.nunits; ++k) job.stage_ms[2 + s] += ms[(size_t)k * 4 + s];

@@ -25,3 +25,6 @@ st = j.stage_ms()
 print(f"postprocess {tp:.2f}s  nested {st[2]:.0f} dedup {st[3]:.0f} merge {st[4]:.0f} rest {st[5]:.0f} ms; final {j.count()}")
 t = time.time(); out = j.render("strfinder"); nl = out.count(b"\n") - 1; print(f"render {time.time()-t:.2f}s rows {nl}")
 import hashlib; print("sha", hashlib.sha256(out).hexdigest()[:16])
+st = j.stage_ms()
+print(f"render stage {st[6]:.0f} ms")
+t = time.time(); j.reset(); print(f"reset {1000*(time.time()-t):.0f} ms")
