@@ -201,12 +201,17 @@ bool align_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_
     for (int64_t j = 0; j <= n; ++j) prev[j] = (int32_t)j;   // row 0
     prev[n + 1] = INF;
     int64_t pjmax = n;                                        // row 0 spans every column
+    // costs never decrease along a path, so once a whole row exceeds
+    // tol + 2*max_indel every alignment has n_sub > tol or an indel count
+    // > max_indel, and the copy is rejected below anyway
+    const int32_t reject = (int32_t)(tol + 2 * max_indel);
     for (int64_t i = 1; i <= m; ++i) {
         const int64_t jmin = std::max<int64_t>(1, i - band), jmax = std::min<int64_t>(n, i + band);
         const char mi = motif[i - 1];
         char *prow = ptr + i * W + band - i;
         if (pjmax + 1 <= n) prev[pjmax + 1] = INF;            // (i-1, i-1+band+1) is out of band
         cur[jmin - 1] = jmin - 1 == 0 ? (int32_t)i : INF;
+        int32_t rowmin = INF;
         for (int64_t j = jmin; j <= jmax; ++j) {
             const bool eq = mi == win[j - 1];
             int32_t best = prev[j - 1] + (eq ? 0 : 1);
@@ -217,7 +222,9 @@ bool align_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_
             if (ic < best) { best = ic; op = 'I'; }
             cur[j] = best;
             prow[j] = op;
+            rowmin = std::min(rowmin, best);
         }
+        if (rowmin > reject && (jmin > 1 || i > reject)) return false;
         pjmax = jmax;
         std::swap(prev, cur);
     }

@@ -20,6 +20,8 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
@@ -41,6 +43,91 @@ int host_threads(const bwtmi_params &p) {
     return std::min(t, 16);
 }
 
+// Persistent worker pool: parallel regions reuse the same threads (and their
+// thread-local DP scratch) instead of spawning per call.  The caller takes
+// part as worker 0; a region started from inside a worker runs inline.
+namespace {
+class Pool {
+public:
+    static Pool &get() {
+        static Pool p;
+        return p;
+    }
+    // f(w) for w in [0, nt)
+    void run(int nt, const std::function<void(int)> &f) {
+        if (nt <= 1 || in_worker) {
+            for (int w = 0; w < nt; ++w) f(w);
+            return;
+        }
+        std::unique_lock<std::mutex> region(region_mu);   // one region at a time
+        grow(nt - 1);
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            job = &f;
+            want = nt - 1;
+            pending = nt - 1;
+            ++gen;
+        }
+        cv.notify_all();
+        in_worker = true;
+        f(0);
+        in_worker = false;
+        std::unique_lock<std::mutex> lk(mu);
+        done.wait(lk, [&] { return pending == 0; });
+        job = nullptr;
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+            ++gen;
+        }
+        cv.notify_all();
+        for (auto &t : th) t.join();
+    }
+
+private:
+    void grow(int n) {
+        while ((int)th.size() < n) {
+            const int id = (int)th.size();
+            th.emplace_back([this, id] { loop(id); });
+        }
+    }
+    void loop(int id) {
+        in_worker = true;
+        int64_t seen = 0;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            seen = gen;   // a worker created for the current region still takes part in it
+            if (job && id < want) seen = gen - 1;
+        }
+        for (;;) {
+            const std::function<void(int)> *f;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || gen != seen; });
+                if (stop) return;
+                seen = gen;
+                if (id >= want) continue;
+                f = job;
+            }
+            (*f)(id + 1);
+            std::lock_guard<std::mutex> lk(mu);
+            if (--pending == 0) done.notify_one();
+        }
+    }
+    std::vector<std::thread> th;
+    std::mutex mu, region_mu;
+    std::condition_variable cv, done;
+    const std::function<void(int)> *job = nullptr;
+    int want = 0, pending = 0;
+    int64_t gen = 0;
+    bool stop = false;
+    static thread_local bool in_worker;
+};
+thread_local bool Pool::in_worker = false;
+}  // namespace
+
 // fn(begin, end) over [0, n) in contiguous chunks
 template <class F>
 static void parallel_for(int64_t n, int nt, F &&fn) {
@@ -50,13 +137,7 @@ static void parallel_for(int64_t n, int nt, F &&fn) {
         fn((int64_t)0, n);
         return;
     }
-    std::vector<std::thread> th;
-    th.reserve((size_t)nt);
-    for (int t = 0; t < nt; ++t) {
-        const int64_t a = n * t / nt, b = n * (t + 1) / nt;
-        th.emplace_back([&fn, a, b] { fn(a, b); });
-    }
-    for (auto &x : th) x.join();
+    Pool::get().run(nt, [&](int t) { fn(n * t / nt, n * (t + 1) / nt); });
 }
 
 // dynamic scheduling: fn(item, worker)
@@ -67,15 +148,13 @@ static void parallel_items(int64_t n, int nt, F &&fn) {
     std::atomic<int64_t> next{0};
     auto work = [&](int w) {
         for (;;) {
-            const int64_t k = next.fetch_add(1);
+            const int64_t k = next.fetch_add(1, std::memory_order_relaxed);
             if (k >= n) break;
             fn(k, w);
         }
     };
     if (nt == 1) { work(0); return; }
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
-    for (auto &x : th) x.join();
+    Pool::get().run(nt, work);
 }
 
 void run_tasks(int64_t n, int nt, const std::function<void(int64_t)> &fn) {
@@ -212,13 +291,6 @@ inline double copies_of(const Item &it) { return it.x ? it.x->copies : (double)i
 inline double mm_of(const Item &it) { return it.x ? it.x->mm : 0.0; }
 inline double conf_of(const Item &it) { return it.x ? it.x->confidence : 0.95; }
 
-std::string canon_of(std::string_view m) {
-    std::string c, s(m);
-    char st;
-    canonical_stranded(s, c, st);
-    return c;
-}
-
 // stable sort of items by (start, end)
 void sort_by_pos(ItemVec &v, int nt) {
     const size_t n = v.size();
@@ -336,7 +408,7 @@ ItemVec suppress_nested(const ItemVec &rs, double thr, int nt) {
 }
 
 // optional counters (BWTMI_STATS=1): recompute calls / time, merge accepts
-std::atomic<int64_t> g_recomputes{0}, g_recompute_ns{0}, g_merges{0};
+std::atomic<int64_t> g_recomputes{0}, g_recompute_ns{0}, g_merges{0}, g_canons{0};
 const bool g_stats = [] { const char *e = std::getenv("BWTMI_STATS"); return e && *e == '1'; }();
 std::atomic<int64_t> g_hist_n[8][8], g_hist_ns[8][8];   // [log4 motif len][log4 region len]
 inline int lg4(int64_t v) { int k = 0; while (v >= 4 && k < 7) { v >>= 2; ++k; } return k; }
@@ -444,6 +516,7 @@ struct Canon {
 
 inline const std::string &canon_get(const UnitCtx &u, const Item &it, Canon &c) {
     if (!c.ok) {
+        if (g_stats) g_canons.fetch_add(1, std::memory_order_relaxed);
         thread_local std::string tmp;
         const std::string_view mv = motif_of(u, it);
         tmp.assign(mv.data(), mv.size());
@@ -454,13 +527,51 @@ inline const std::string &canon_get(const UnitCtx &u, const Item &it, Canon &c) 
     return c.s;
 }
 
+inline char comp_of(char c) {   // bwt.py:688-691
+    switch (c) {
+        case 'A': return 'T';
+        case 'T': return 'A';
+        case 'C': return 'G';
+        case 'G': return 'C';
+        default: return c;
+    }
+}
+
+// get_canonical_motif_stranded(m1)[0] == ...(m2)[0] (bwt.py:694-716): the
+// canonical form is the least string over the rotations of m and of its
+// reverse complement, a set that is the same for every member, so equality
+// holds iff m2 is a rotation of m1 or of rc(m1).  Motifs up to 8 bytes are
+// compared as packed words; longer ones through the canonical strings.
+inline bool same_canonical(const UnitCtx &u, const Item &r1, Canon &c1, const Item &r2, Canon &c2) {
+    const std::string_view a = motif_of(u, r1), b = motif_of(u, r2);
+    if (a.size() != b.size()) return false;
+    const size_t m = a.size();
+    if (m == 0) return true;
+    if (m > 8) return canon_get(u, r1, c1) == canon_get(u, r2, c2);
+    uint64_t x = 0, r = 0, y = 0;
+    for (size_t i = 0; i < m; ++i) {
+        x = (x << 8) | (uint8_t)a[i];
+        r = (r << 8) | (uint8_t)comp_of(a[m - 1 - i]);
+        y = (y << 8) | (uint8_t)b[i];
+    }
+    const unsigned bits = (unsigned)(8 * m);
+    const uint64_t mask = bits == 64 ? ~0ull : ((1ull << bits) - 1);
+    for (size_t k = 0; k < m; ++k) {
+        const unsigned s = (unsigned)(8 * k);
+        const uint64_t rx = s ? (((x << s) | (x >> (bits - s))) & mask) : x;
+        const uint64_t rr = s ? (((r << s) | (r >> (bits - s))) & mask) : r;
+        if (rx == y || rr == y) return true;
+    }
+    return false;
+}
+
 bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, Canon &c1, const Item &r2, Canon &c2,
                Item &merged) {
     if (r1.chrom != r2.chrom) return false;
     if (r1.mlen == 0 || r2.mlen == 0) return false;
     const int64_t ml = std::min(r1.mlen, r2.mlen);
     if (std::max<int64_t>(0, r2.start - r1.end) > ml + 1) return false;   // cheap test first
-    if (canon_get(u, r1, c1) != canon_get(u, r2, c2)) return false;
+    if (!same_canonical(u, r1, c1, r2, c2)) return false;
     const int64_t s = std::min(r1.start, r2.start), e = std::max(r1.end, r2.end);
     const int32_t tier = std::min(r1.tier, r2.tier);
     Item mg = recompute(u, pools, w, r1.chrom, s, e, std::max<int64_t>(1, ml), tier);
@@ -487,6 +598,8 @@ void spec_run(const UnitCtx &u, Pools &pools, int w, const ItemVec &R, int64_t b
     Canon cc;
     fresh[(size_t)b] = 1;
     Item mg;
+    o.emitted.reserve((size_t)(e - b));
+    o.emit_step.reserve((size_t)(e - b));
     for (int64_t i = b + 1; i < e; ++i) {
         Canon ci;
         if (try_merge(u, pools, w, cur, cc, R[(size_t)i], ci, mg)) {
@@ -514,13 +627,19 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
     std::vector<uint8_t> fresh((size_t)n, 0);
     std::vector<SpecOut> spec((size_t)K);
     auto ts0 = std::chrono::steady_clock::now();
+    std::vector<double> cms(g_stats ? (size_t)K : 0);
     parallel_items(K, nt, [&](int64_t k, int w) {
+        auto a = std::chrono::steady_clock::now();
         spec_run(u, pools, w, R, cut[(size_t)k], cut[(size_t)k + 1], fresh, spec[(size_t)k]);
+        if (g_stats) cms[(size_t)k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
     });
     auto ts1 = std::chrono::steady_clock::now();
-    if (std::getenv("BWTMI_STATS"))
-        std::fprintf(stderr, "  merge spec %.1f ms (K=%lld)\n",
-                     std::chrono::duration<double, std::milli>(ts1 - ts0).count(), (long long)K);
+    if (g_stats) {
+        double sum = 0, mx = 0;
+        for (double v : cms) { sum += v; mx = std::max(mx, v); }
+        std::fprintf(stderr, "  merge spec %.1f ms (K=%lld, chunk sum %.1f max %.1f ms)\n",
+                     std::chrono::duration<double, std::milli>(ts1 - ts0).count(), (long long)K, sum, mx);
+    }
     // repair: chunk 0 is exact; a later chunk's speculative results hold from
     // the first index where the true run restarts (non-merge) at an index
     // where the speculative run restarted too
@@ -586,7 +705,10 @@ bool should_collapse(const UnitCtx &u, const Item &r1, const Item &r2) {
     if (sh <= 0) return false;
     const double f = (double)ov / (double)sh;
     if (f < 0.8) return false;
-    if (canon_of(motif_of(u, r1)) == canon_of(motif_of(u, r2))) return true;
+    {
+        Canon c1, c2;
+        if (same_canonical(u, r1, c1, r2, c2)) return true;
+    }
     if ((r1.mlen == 1 || r2.mlen == 1) && f >= 0.95) return true;
     if (r1.mlen == r2.mlen && f >= 0.9) return std::fabs(mm_of(r1) - mm_of(r2)) >= 0.2;
     return false;
@@ -830,9 +952,9 @@ void postprocess(Job &job) {
         for (int32_t k = 0; k < job.nunits; ++k) job.stage_ms[2 + s] += ms[(size_t)k * 4 + s];
     }
     if (const char *e = std::getenv("BWTMI_STATS"); e && *e == '1')
-        std::fprintf(stderr, "[bwtmi] recomputes=%lld (%.1f ms thread-summed) merges=%lld final=%zu\n",
+        std::fprintf(stderr, "[bwtmi] recomputes=%lld (%.1f ms thread-summed) merges=%lld canons=%lld final=%zu\n",
                      (long long)g_recomputes.exchange(0), g_recompute_ns.exchange(0) / 1e6,
-                     (long long)g_merges.exchange(0), job.final_recs.size());
+                     (long long)g_merges.exchange(0), (long long)g_canons.exchange(0), job.final_recs.size());
     if (const char *e = std::getenv("BWTMI_STATS"); e && *e == '1')
         for (int a = 0; a < 8; ++a)
             for (int b = 0; b < 8; ++b)
