@@ -15,32 +15,40 @@ namespace bwtmi {
 // Least rotation (Booth).  MotifUtils.get_canonical_motif takes the min over
 // all rotations (bwt.py:679-685); the least rotation string is unique, so any
 // exact algorithm yields the same string.
-static int64_t least_rotation(const char *s, int64_t n, std::vector<int64_t> &f) {
+// ss = s + s (2n bytes)
+static int64_t least_rotation(const unsigned char *ss, int64_t n, std::vector<int32_t> &f) {
     if (n <= 1) return 0;
+    if (n <= 16) {   // short motifs: direct comparison of the n rotations
+        int64_t k = 0;
+        for (int64_t j = 1; j < n; ++j)
+            if (std::memcmp(ss + j, ss + k, (size_t)n) < 0) k = j;
+        return k;
+    }
     f.assign((size_t)(2 * n), -1);
     int64_t k = 0;
-    auto at = [&](int64_t i) { return (unsigned char)s[i < n ? i : i - n]; };
     for (int64_t j = 1; j < 2 * n; ++j) {
-        const unsigned char sj = at(j);
+        const unsigned char sj = ss[j];
         int64_t i = f[(size_t)(j - k - 1)];
-        while (i != -1 && sj != at(k + i + 1)) {
-            if (sj < at(k + i + 1)) k = j - i - 1;
+        while (i != -1 && sj != ss[k + i + 1]) {
+            if (sj < ss[k + i + 1]) k = j - i - 1;
             i = f[(size_t)i];
         }
-        if (sj != at(k + i + 1)) {  // i == -1
-            if (sj < at(k)) k = j;
+        if (sj != ss[k + i + 1]) {  // i == -1
+            if (sj < ss[k]) k = j;
             f[(size_t)(j - k)] = -1;
         } else {
-            f[(size_t)(j - k)] = i + 1;
+            f[(size_t)(j - k)] = (int32_t)(i + 1);
         }
     }
     return k % n;
 }
 
 std::string min_rotation(const std::string &s) {
-    thread_local std::vector<int64_t> f;
-    const int64_t k = least_rotation(s.data(), (int64_t)s.size(), f);
-    return s.substr((size_t)k) + s.substr(0, (size_t)k);
+    thread_local std::vector<int32_t> f;
+    thread_local std::string ss;
+    ss.assign(s).append(s);
+    const int64_t k = least_rotation((const unsigned char *)ss.data(), (int64_t)s.size(), f);
+    return ss.substr((size_t)k, s.size());
 }
 
 static inline char comp_base(char c) {       // bwt.py:688-691
@@ -53,15 +61,6 @@ static inline char comp_base(char c) {       // bwt.py:688-691
     }
 }
 
-// compare rotation a of x with rotation b of y (equal lengths n)
-static inline int rot_cmp(const char *x, int64_t a, const char *y, int64_t b, int64_t n) {
-    for (int64_t t = 0; t < n; ++t) {
-        const unsigned char p = (unsigned char)x[(a + t) % n], q = (unsigned char)y[(b + t) % n];
-        if (p != q) return p < q ? -1 : 1;
-    }
-    return 0;
-}
-
 void canonical_stranded(const std::string &s, std::string &canon, char &strand) {  // 694-716
     const int64_t n = (int64_t)s.size();
     if (n == 0) {
@@ -69,17 +68,18 @@ void canonical_stranded(const std::string &s, std::string &canon, char &strand) 
         strand = '+';
         return;
     }
-    thread_local std::vector<int64_t> f;
-    thread_local std::string rc;
-    rc.resize((size_t)n);
-    for (int64_t i = 0; i < n; ++i) rc[(size_t)i] = comp_base(s[(size_t)(n - 1 - i)]);
-    const int64_t kf = least_rotation(s.data(), n, f);
-    const int64_t kr = least_rotation(rc.data(), n, f);
-    const bool fwd = rot_cmp(s.data(), kf, rc.data(), kr, n) <= 0;
-    const std::string &src = fwd ? s : rc;
-    const int64_t k = fwd ? kf : kr;
-    canon.resize((size_t)n);
-    for (int64_t t = 0; t < n; ++t) canon[(size_t)t] = src[(size_t)((k + t) % n)];
+    thread_local std::vector<int32_t> f;
+    thread_local std::string ss, rr;   // s+s and rc+rc: every rotation is a plain slice
+    ss.resize((size_t)(2 * n));
+    rr.resize((size_t)(2 * n));
+    for (int64_t i = 0; i < n; ++i) {
+        ss[(size_t)i] = ss[(size_t)(i + n)] = s[(size_t)i];
+        rr[(size_t)i] = rr[(size_t)(i + n)] = comp_base(s[(size_t)(n - 1 - i)]);
+    }
+    const int64_t kf = least_rotation((const unsigned char *)ss.data(), n, f);
+    const int64_t kr = least_rotation((const unsigned char *)rr.data(), n, f);
+    const bool fwd = std::memcmp(ss.data() + kf, rr.data() + kr, (size_t)n) <= 0;
+    canon.assign((fwd ? ss.data() + kf : rr.data() + kr), (size_t)n);
     strand = fwd ? '+' : '-';
 }
 
@@ -322,17 +322,17 @@ inline void pc_reset(Scratch &S, int64_t m) {
     for (int64_t p = 0; p < m; ++p) S.pc_over[(size_t)p].clear();
 }
 
-inline void pc_add(Scratch &S, int64_t p, char b) {
+inline void pc_add(Scratch &S, int64_t p, char b, int64_t cnt = 1) {
     char *c = &S.pc_c[(size_t)(p * KIN)];
     int64_t *n = &S.pc_n[(size_t)(p * KIN)];
     const int k = S.pc_k[(size_t)p];
     for (int t = 0; t < k; ++t)
-        if (c[t] == b) { ++n[t]; return; }
+        if (c[t] == b) { n[t] += cnt; return; }
     auto &ov = S.pc_over[(size_t)p];
     for (auto &e : ov)
-        if (e.first == b) { ++e.second; return; }
-    if (k < KIN) { c[k] = b; n[k] = 1; S.pc_k[(size_t)p] = (uint8_t)(k + 1); }
-    else ov.push_back({b, 1});
+        if (e.first == b) { e.second += cnt; return; }
+    if (k < KIN) { c[k] = b; n[k] = cnt; S.pc_k[(size_t)p] = (uint8_t)(k + 1); }
+    else ov.push_back({b, cnt});
 }
 
 // Counter.most_common(1): first maximal entry in insertion order
@@ -386,6 +386,14 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
         seq_len, std::max<int64_t>(end, start + m * min_copies) + std::max<int64_t>(m * 3, max_indel * 4));
     UnitOut res;
     int64_t copies = 0;
+    // exact copies observe cur[p] at every p; they are counted in bulk before
+    // the next count update or read, which keeps first-insertion order
+    int64_t pend = 0;
+    auto flush = [&]() {
+        if (!pend) return;
+        for (int64_t p = 0; p < m; ++p) pc_add(S, p, cur[(size_t)p], pend);
+        pend = 0;
+    };
     while (pos < limit) {
         const int64_t wend = std::min<int64_t>(seq_len, pos + m + max_indel);
         const int64_t wlen = wend - pos;
@@ -397,11 +405,12 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
             ++copies;
             out.copy_err.push_back(0);
             out.copy_len.push_back(m);
-            for (int64_t p = 0; p < m; ++p) pc_add(S, p, cur[(size_t)p]);
+            ++pend;
             pos += m;
             continue;
         }
         if (!align_unit(cur.data(), m, seq + pos, wlen, max_indel, tol, S, res) || res.consumed == 0) break;
+        flush();
         ++copies;
         // variation pieces "copy:pos:..." in op order (bwt.py:1073-1088)
         uint32_t from = 0;
@@ -427,6 +436,7 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
     if (copies < min_copies) return false;
     const int64_t consumed = pos - start;
     if (consumed <= 0) return false;
+    flush();
     consensus_from(S, m, cur, out.consensus);
     int64_t tot = 0, mx = 0;
     for (auto e : out.copy_err) { tot += e; mx = std::max(mx, e); }

@@ -213,6 +213,30 @@ def test_device_screen_matches_host(gpu_ctx, case):
         assert d == h, (case, fmt)
 
 
+def test_full_size_goldens(gpu_ctx, golden_dir, tmp_path):
+    """BASELINE configs at full size (C2 1 Mbp --tier1, C4 8x12.5 Mbp, C3 100 Mbp
+    --progress when generated) against repeat.tab hashes of the reference
+    pipeline (tests/golden/make_goldens.py hybrid; strict scan and nested
+    suppression restated, everything else the reference's own code)."""
+    from bwtmi import TandemRepeatFinder, synth
+    with open(os.path.join(golden_dir, "expected_large.json")) as f:
+        man = json.load(f)
+    for name, g in sorted(man.items()):
+        fa = str(tmp_path / f"{name}.fa")
+        assert synth.write_fasta(fa, g["lengths"], g["sub_rate"]) == g["fasta_sha256"], name
+        args = g["args"]
+        mml = int(args[args.index("--max-motif-len") + 1]) if "--max-motif-len" in args else 9
+        f = TandemRepeatFinder(fa, show_progress="--progress" in args, max_motif_length=mml)
+        f.load_reference()
+        reps = f.find_tandem_repeats_parallel(True, "--tier1" not in args, False, None)
+        out = tmp_path / f"{name}.tab"
+        f.save_results(reps, str(out), "strfinder")
+        data = out.read_bytes()
+        assert data.count(b"\n") - 1 == g["out_rows"], name
+        assert hashlib.sha256(data).hexdigest() == g["out_sha256"], name
+        os.unlink(fa)
+
+
 # ------------------------------------------------------------------ FM index
 def _check_index(text: bytes, golden=None):
     from bwtmi import BWTCore
