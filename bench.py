@@ -12,9 +12,10 @@ One step = one pass of the whole path over the resident contig(s):
   device FM index (SA, BWT, C, Occ, sampled SA, 8-mer hash)  [bwt.py:3053-3054]
   device strict adjacency scan + hit download                [bwt.py:3103-3106]
   native post-processing to the final records                [bwt.py:3928-3944]
-  RCCL all-gather of the final records to rank 0 (N > 1)
-  rank 0: compound detection + STRfinder repeat.tab written  [bwt.py:4141-4198]
-          to $TMPDIR (sha256 and row count reported)
+  compound detection + STRfinder rows of the rank's own contig,
+  written into one repeat.tab at offsets from an RCCL
+  all-reduce of per-contig sizes (N > 1)                   [bwt.py:4141-4198]
+  (sha256 and row count of the file are reported)
 Inputs are resident in HBM before timing starts (uploaded during warmup).
 """
 import argparse
@@ -89,20 +90,20 @@ def main():
     from bwtmi.records import Job
 
     ctx = _lib.ctx(local)
-    # every rank registers every contig (ids match across ranks); rank 0 needs
-    # all sequences to render, other ranks only their own
+    # every rank registers every contig (fold-unit ids match across ranks) but
+    # holds only its own sequence: rows are rendered and written by their owner
     job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True,
               build_index=not a.no_index, sa_sample=32)
     for k in range(world):
-        own = (k == rank) or rank == 0
-        seq = synth.generate_contig(a.contig_bp, k + 1, 0.0) if own else b""
+        seq = synth.generate_contig(a.contig_bp, k + 1, 0.0) if k == rank else b""
         trim = FLANK if len(seq) > 2 * FLANK else 0
         job.add_contig(f"contig{k + 1}", seq, trim, trim)
     job.select([rank])
     t_up = time.perf_counter()
     job.upload(ctx)                           # host -> HBM once; outside the timed region
     upload_ms = (time.perf_counter() - t_up) * 1000.0
-    out_path = os.path.join(tempfile.gettempdir(), f"bwtmi_bench_rank{rank}.tab")
+    out_path = os.path.join(tempfile.gettempdir(), f"bwtmi_bench_{os.environ.get('MASTER_PORT', 'single')}.tab")
+    dev = torch.device("cuda", local) if world > 1 else None
 
     def step():
         job.reset()
@@ -110,12 +111,10 @@ def main():
         job.scan(ctx)
         job.postprocess()
         if world > 1:
-            blobs = dist.gather_bytes(td, job.export(), torch.device("cuda", local))
-            job.reset()
-            if rank == 0:
-                for b in blobs:
-                    job.import_records(b)
-        if rank == 0:
+            # each rank writes its own contig's rows at offsets from two
+            # all-reduces of per-unit sizes (RCCL); no record leaves its GPU
+            dist.write_sharded(td, job, "strfinder", out_path, dev)
+        else:
             job.write("strfinder", out_path)     # repeat.tab, as the CLI writes it
         return out_path
 

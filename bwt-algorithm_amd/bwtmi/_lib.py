@@ -78,6 +78,10 @@ _SIGS = {
     "bwtmi_job_count": (C.c_int64, [_P]),
     "bwtmi_job_render": (C.c_int, [_P, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
     "bwtmi_job_write": (C.c_int, [_P, C.c_int, C.c_char_p]),
+    "bwtmi_job_unit_count": (C.c_int32, [_P]),
+    "bwtmi_job_unit_rows": (C.c_int, [_P, _P]),
+    "bwtmi_job_render_units": (C.c_int, [_P, C.c_int, _P, _P]),
+    "bwtmi_job_write_units": (C.c_int, [_P, C.c_char_p, _P, C.c_int]),
     "bwtmi_job_get_records": (C.c_int, [_P, _P, _P]),
     "bwtmi_job_get_string": (C.c_int64, [_P, C.c_int64, C.c_int, _P, C.c_int64]),
     "bwtmi_job_export": (C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),

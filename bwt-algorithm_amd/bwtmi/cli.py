@@ -75,6 +75,18 @@ def main(argv=None) -> int:
                                 min_copies=a.min_copies, min_entropy=a.min_entropy,
                                 flank_trim=a.flank_trim, max_unit_len=a.max_unit_len)
     sequences = finder.load_reference()
+    from . import dist
+    if dist.is_distributed() and not a.tier3:
+        # one process per GPU: shard fold units, each rank writes its own rows
+        if a.format not in ("bed", "vcf", "trf_table", "trf_dat", "strfinder"):
+            raise SystemExit(f"unknown format {a.format}")
+        n = finder.find_and_write_sharded(tier2, a.output, a.format)
+        if dist._torch_dist().get_rank() == 0:
+            print()
+            print("=" * 60)
+            print(f"Completed! Found {n} total tandem repeats.")
+            print(f"Results saved to {a.output}")
+        return 0
     if os.environ.get("BWTMI_SKIP_INDEX", "0") != "1":
         finder.build_indices(sequences)
     long_reads = _read_long_reads(a.long_reads) if (a.long_reads and a.tier3) else []
@@ -82,7 +94,6 @@ def main(argv=None) -> int:
         repeats = finder.find_tandem_repeats_parallel(True, tier2, a.tier3, long_reads or None, None)
     else:
         repeats = finder.find_tandem_repeats(True, tier2, a.tier3, long_reads or None)
-    from . import dist
     if dist.is_distributed() and dist._torch_dist().get_rank() != 0:
         return 0
     finder.save_results(repeats, a.output, a.format)

@@ -91,6 +91,39 @@ def gather_bytes(td, blob: bytes, device) -> List[bytes]:
     return [bytes(p[:s].cpu().numpy().tobytes()) for p, s in zip(parts, sizes)]
 
 
+def _allreduce_sum(td, arr, device):
+    import numpy as np
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int64)).to(device)
+    td.all_reduce(t, op=td.ReduceOp.SUM)
+    return t.cpu().numpy()
+
+
+def write_sharded(td, job, fmt: str, path: str, device="cpu") -> int:
+    """Write the output file from every rank's own fold units, without moving
+    records between ranks.  The file is the units' rows in unit (natural-key)
+    order (bwt.py:4147-4150) and each unit lives on exactly one rank, so two
+    all-reduces of per-unit counts (rows for VCF ids, then bytes) give every
+    rank its byte offsets; rank 0 sizes the file and writes the header.
+    Returns the file size."""
+    import numpy as np
+    rank = td.get_rank()
+    rows = _allreduce_sum(td, job.unit_rows(), device)
+    row_base = np.concatenate([[0], np.cumsum(rows)[:-1]]).astype(np.int64)
+    local = job.render_units(fmt, row_base)
+    sizes = _allreduce_sum(td, local[1:], device)
+    header = int(local[0])
+    offsets = np.concatenate([[0, header], header + np.cumsum(sizes)[:-1]]).astype(np.int64)
+    total = header + int(sizes.sum())
+    if rank == 0:
+        with open(path, "wb") as f:
+            f.truncate(total)
+    td.barrier()
+    job.write_units(path, offsets, write_header=(rank == 0))
+    td.barrier()
+    return total
+
+
 def run_sharded(finder, job, scan_fn: Optional[Callable] = None):
     """Shard `job`'s contigs over the ranks; returns rank 0's RepeatList (other
     ranks get an empty one).  `scan_fn(job, ids)` overrides the device scan

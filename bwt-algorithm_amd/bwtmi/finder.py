@@ -100,6 +100,34 @@ class TandemRepeatFinder:
         job.postprocess()
         return job.records()
 
+    def find_and_write_sharded(self, enable_tier2: bool, output_file: str, format_type: str) -> int:
+        """Multi-GPU CLI path: every rank scans and post-processes its own fold
+        units and writes them into `output_file` at offsets from an exchange of
+        per-unit sizes (bwtmi.dist.write_sharded) -- records never leave their
+        rank.  Returns the total number of records (all ranks)."""
+        import numpy as np
+        from . import dist
+        if self.job is None:
+            self.load_reference()
+        job = self.job
+        job.reset()
+        job.set_tier2(enable_tier2)
+        td = dist.init()
+        rank, world = td.get_rank(), td.get_world_size()
+        infos = [job.contig_info(i) for i in range(job.contig_count())]
+        shard = dist.assign(dist.natural_units([x[0] for x in infos]), [x[1] - x[2] - x[3] for x in infos],
+                            world)[rank]
+        job.select(shard)
+        job.scan(_lib.ctx(self.device))
+        job.postprocess()
+        device = "cpu"
+        if td.get_backend() == "nccl":
+            import torch
+            device = torch.device("cuda", torch.cuda.current_device())
+        total = int(dist._allreduce_sum(td, np.array([job.count()], dtype=np.int64), device)[0])
+        dist.write_sharded(td, job, format_type, output_file, device)
+        return total
+
     def find_tandem_repeats(self, enable_tier1: bool = True, enable_tier2: bool = True,
                             enable_tier3: bool = False, long_reads: Optional[List[str]] = None) -> RepeatList:
         res = self._run(enable_tier2, enable_tier3, long_reads)

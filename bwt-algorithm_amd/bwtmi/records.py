@@ -195,6 +195,29 @@ class Job:
     def write(self, fmt: str, path: str) -> None:
         check(lib().bwtmi_job_write(self.h, _lib.FMT[fmt], path.encode()))
 
+    # ---- sharded output (bwtmi.dist.write_sharded)
+    def unit_count(self) -> int:
+        return lib().bwtmi_job_unit_count(self.h)
+
+    def unit_rows(self) -> np.ndarray:
+        out = np.zeros(self.unit_count(), dtype=np.int64)
+        check(lib().bwtmi_job_unit_rows(self.h, out.ctypes.data))
+        return out
+
+    def render_units(self, fmt: str, row_base: Optional[np.ndarray] = None) -> np.ndarray:
+        """Format the local fold units; returns [header bytes, bytes of unit 0, ...]."""
+        out = np.zeros(self.unit_count() + 1, dtype=np.int64)
+        rb = None
+        if row_base is not None:
+            row_base = np.ascontiguousarray(row_base, dtype=np.int64)
+            rb = row_base.ctypes.data
+        check(lib().bwtmi_job_render_units(self.h, _lib.FMT[fmt], rb, out.ctypes.data))
+        return out
+
+    def write_units(self, path: str, offsets: np.ndarray, write_header: bool) -> None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        check(lib().bwtmi_job_write_units(self.h, path.encode(), offsets.ctypes.data, int(write_header)))
+
     def export(self) -> bytes:
         p, n = C.c_void_p(), C.c_int64()
         check(lib().bwtmi_job_export(self.h, C.byref(p), C.byref(n)))

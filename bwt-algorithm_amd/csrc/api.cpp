@@ -67,6 +67,26 @@ struct JobDev {
     std::vector<DevContig> seqs;
 };
 
+// parts[k] lands at byte offset at[k] of `path`, in parallel (page-cache copies)
+static void pwrite_parts(const char *path, bool truncate, const std::vector<std::string> &parts,
+                         const std::vector<size_t> &at, int threads) {
+    const int fd = ::open(path, O_WRONLY | O_CREAT | (truncate ? O_TRUNC : 0), 0644);
+    if (fd < 0) fail(BWTMI_E_IO, "cannot open %s for writing", path);
+    std::vector<uint8_t> ok(parts.size(), 1);
+    run_tasks((int64_t)parts.size(), threads, [&](int64_t k) {
+        const std::string &s = parts[(size_t)k];
+        size_t done = 0;
+        while (done < s.size()) {
+            const ssize_t w = ::pwrite(fd, s.data() + done, s.size() - done, (off_t)(at[(size_t)k] + done));
+            if (w <= 0) { ok[(size_t)k] = 0; return; }
+            done += (size_t)w;
+        }
+    });
+    bool good = ::close(fd) == 0;
+    for (auto v : ok) good = good && v;
+    if (!good) fail(BWTMI_E_IO, "short write to %s", path);
+}
+
 }  // namespace bwtmi
 
 using namespace bwtmi;
@@ -350,6 +370,7 @@ static void job_upload(bwtmi_ctx *ctx, bwtmi_job *job) {
     for (size_t i = 0; i < job->j.contigs.size(); ++i) {
         const Contig &ct = job->j.contigs[i];
         DevContig &dc = d.seqs[i];
+        if (!job->j.selected.empty() && !job->j.selected[i]) continue;   // another rank's shard
         if (dc.n == ct.trimmed_len()) continue;
         upload_text(c, dc.buf, (const uint8_t *)ct.trimmed(), ct.trimmed_len());
         dc.n = ct.trimmed_len();
@@ -503,22 +524,58 @@ int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path) {
         const std::vector<std::string> parts = render_parts(job->j, fmt);
         std::vector<size_t> at(parts.size() + 1, 0);
         for (size_t k = 0; k < parts.size(); ++k) at[k + 1] = at[k] + parts[k].size();
-        const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
-        if (fd < 0) fail(BWTMI_E_IO, "cannot open %s for writing", path);
-        // parts land at their final offsets in parallel (page-cache copies)
-        std::vector<uint8_t> ok(parts.size(), 1);
-        run_tasks((int64_t)parts.size(), host_threads(job->j.params), [&](int64_t k) {
-            const std::string &s = parts[(size_t)k];
-            size_t done = 0;
-            while (done < s.size()) {
-                const ssize_t w = ::pwrite(fd, s.data() + done, s.size() - done, (off_t)(at[(size_t)k] + done));
-                if (w <= 0) { ok[(size_t)k] = 0; return; }
-                done += (size_t)w;
-            }
-        });
-        bool good = ::close(fd) == 0;
-        for (auto v : ok) good = good && v;
-        if (!good) fail(BWTMI_E_IO, "short write to %s", path);
+        pwrite_parts(path, true, parts, at, host_threads(job->j.params));
+    });
+}
+
+int32_t bwtmi_job_unit_count(bwtmi_job *job) {
+    if (!job) return -1;
+    job->j.assign_units();
+    return job->j.nunits;
+}
+
+int bwtmi_job_unit_rows(bwtmi_job *job, int64_t *unit_rows) {
+    return guard([&] {
+        CHECK_ARG(job && unit_rows, "null argument");
+        Job &J = job->j;
+        J.assign_units();
+        for (int32_t u = 0; u < J.nunits; ++u) unit_rows[u] = 0;
+        for (const Rec &r : J.final_recs) ++unit_rows[J.contigs[(size_t)r.chrom].unit];
+    });
+}
+
+int bwtmi_job_render_units(bwtmi_job *job, int fmt, const int64_t *row_base, int64_t *bytes) {
+    return guard([&] {
+        CHECK_ARG(job && bytes, "null argument");
+        Job &J = job->j;
+        render_rows(J, fmt, row_base, J.rendered);
+        for (int32_t u = 0; u <= J.nunits; ++u) bytes[u] = 0;
+        bytes[0] = (int64_t)J.rendered.header.size();
+        for (size_t k = 0; k < J.rendered.parts.size(); ++k)
+            bytes[1 + J.rendered.part_unit[k]] += (int64_t)J.rendered.parts[k].size();
+    });
+}
+
+int bwtmi_job_write_units(bwtmi_job *job, const char *path, const int64_t *offsets, int write_header) {
+    return guard([&] {
+        CHECK_ARG(job && path && offsets, "null argument");
+        Job &J = job->j;
+        Rendered &R = J.rendered;
+        std::vector<std::string> parts;
+        std::vector<size_t> at;
+        std::vector<int64_t> fill((size_t)J.nunits, 0);
+        if (write_header && !R.header.empty()) {
+            parts.push_back(std::move(R.header));
+            at.push_back((size_t)offsets[0]);
+        }
+        for (size_t k = 0; k < R.parts.size(); ++k) {
+            const int32_t u = R.part_unit[k];
+            at.push_back((size_t)(offsets[1 + u] + fill[(size_t)u]));
+            fill[(size_t)u] += (int64_t)R.parts[k].size();
+            parts.push_back(std::move(R.parts[k]));
+        }
+        R = Rendered();
+        pwrite_parts(path, false, parts, at, host_threads(J.params));
     });
 }
 

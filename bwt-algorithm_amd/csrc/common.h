@@ -100,6 +100,13 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
                          double frac = 0.1, int64_t max_indel_arg = -1);
 
 // ---------------------------------------------------------------- job
+// formatted output: header + parts of consecutive rows, each inside one fold unit
+struct Rendered {
+    std::string header;
+    std::vector<std::string> parts;
+    std::vector<int32_t> part_unit;
+};
+
 struct Job {
     bwtmi_params params{};
     std::vector<Contig> contigs;
@@ -113,13 +120,16 @@ struct Job {
     std::vector<Rec> final_recs;                     // after bwt.py:3940-3944
     std::vector<uint8_t> selected;                   // scan only these contigs (empty = all)
     bool postprocessed = false;
+    Rendered rendered;                               // last bwtmi_job_render_units result
     double stage_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     void assign_units();
 };
 
 // post.cpp
 void postprocess(Job &job);
-// render.cpp: the output as consecutive parts (formatted in parallel)
+// render.cpp: the output as consecutive parts (formatted in parallel).
+// row_base (per fold unit, may be null): global VCF row id of the unit's first row.
+void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out);
 std::vector<std::string> render_parts(Job &job, int fmt);
 std::string render(Job &job, int fmt);
 // fasta.cpp

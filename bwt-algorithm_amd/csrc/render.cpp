@@ -335,7 +335,7 @@ const char *kVcfHeader =
 
 // Rows are formatted in parallel, in chunks of consecutive rows; each chunk is
 // one part of the output, so concatenating the parts gives the file.
-std::vector<std::string> render_parts(Job &job, int fmt) {
+void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out) {
     auto t0 = std::chrono::steady_clock::now();
     job.assign_units();
     Compound comp;
@@ -376,18 +376,35 @@ std::vector<std::string> render_parts(Job &job, int fmt) {
         default:
             fail(BWTMI_E_ARG, "unknown output format %d", fmt);
     }
+    // chunks of <= CH consecutive rows that never span two fold units; VCF row
+    // ids are row_base[unit] + rank within the unit (global index when the
+    // caller renders only its own shard), else the local index
     const int64_t n = (int64_t)rows.size();
     const int64_t CH = 8192;
-    const int64_t nch = (n + CH - 1) / CH;
-    std::vector<std::string> parts((size_t)nch + 1);
-    parts[0] = std::move(head);
-    run_tasks(nch, host_threads(job.params), [&](int64_t ck) {
+    auto unit_of = [&](int64_t k) { return job.contigs[(size_t)rows[(size_t)k].r->chrom].unit; };
+    struct Chunk { int64_t a, b, id0; int32_t unit; };
+    std::vector<Chunk> chunks;
+    for (int64_t a = 0; a < n;) {
+        const int32_t un = unit_of(a);
+        int64_t e = a;
+        while (e < n && unit_of(e) == un) ++e;
+        const int64_t base = row_base ? row_base[un] : a;
+        for (int64_t c = a; c < e; c += CH) chunks.push_back({c, std::min(e, c + CH), base + (c - a), un});
+        a = e;
+    }
+    out.header = std::move(head);
+    out.parts.assign(chunks.size(), std::string());
+    out.part_unit.resize(chunks.size());
+    for (size_t q = 0; q < chunks.size(); ++q) out.part_unit[q] = chunks[q].unit;
+    run_tasks((int64_t)chunks.size(), host_threads(job.params), [&](int64_t ck) {
         Out o;
-        const int64_t a = ck * CH, b = std::min(n, a + CH);
+        const Chunk &C = chunks[(size_t)ck];
+        const int64_t a = C.a, b = C.b;
         o.s.reserve((size_t)(b - a) * 192);
         double cp[4], ent;
         for (int64_t k = a; k < b; ++k) {
             const Rec &r = *rows[(size_t)k].r;
+            const int64_t row_id = C.id0 + (k - a);
             switch (fmt) {
                 case BWTMI_FMT_BED:
                     o.put(job.contigs[(size_t)r.chrom].name); o.c('\t'); o.i(r.start); o.c('\t'); o.i(r.end);
@@ -395,7 +412,7 @@ std::vector<std::string> render_parts(Job &job, int fmt) {
                     o.f("%.3f", r.mismatch_rate); o.c('\t'); o.c(r.strand); o.c('\n');
                     break;
                 case BWTMI_FMT_VCF:
-                    o.put(job.contigs[(size_t)r.chrom].name); o.c('\t'); o.i(r.start + 1); o.put("\tTR"); o.i(k);
+                    o.put(job.contigs[(size_t)r.chrom].name); o.c('\t'); o.i(r.start + 1); o.put("\tTR"); o.i(row_id);
                     o.put("\t.\t<TR>\t.\tPASS\tMOTIF="); o.put(r.motif); o.put(";CONS_MOTIF="); o.put(r.motif);
                     o.put(";COPIES="); o.f("%.1f", r.copies); o.put(";TIER="); o.i(r.tier);
                     o.put(";CONF="); o.f("%.2f", r.confidence); o.put(";MM_RATE="); o.f("%.3f", r.mismatch_rate);
@@ -428,9 +445,18 @@ std::vector<std::string> render_parts(Job &job, int fmt) {
                     row_strfinder(o, job, r, rows[(size_t)k].partner);
             }
         }
-        parts[(size_t)ck + 1] = std::move(o.s);
+        out.parts[(size_t)ck] = std::move(o.s);
     });
     job.stage_ms[6] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+std::vector<std::string> render_parts(Job &job, int fmt) {
+    Rendered r;
+    render_rows(job, fmt, nullptr, r);
+    std::vector<std::string> parts;
+    parts.reserve(r.parts.size() + 1);
+    parts.push_back(std::move(r.header));
+    for (auto &p : r.parts) parts.push_back(std::move(p));
     return parts;
 }
 

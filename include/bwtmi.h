@@ -158,6 +158,23 @@ int64_t bwtmi_job_count(const bwtmi_job *job);
 /* render a format into a malloc'd buffer (free with bwtmi_free) or a file */
 int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len);
 int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path);
+/* Sharded output (one process per GPU, each owning whole fold units = contigs
+ * with equal natural sort keys, bwt.py:22-36): the file is the concatenation,
+ * in unit order, of every unit's rows (bwt.py:4147-4150), so each rank writes
+ * its own units at offsets from an exchange of sizes -- no record gather.
+ *   unit_count              number of fold units (same on every rank)
+ *   unit_rows[u]            local final records of unit u (VCF row ids)
+ *   render_units            format the local units; bytes[0] = header size,
+ *                           bytes[1 + u] = size of unit u (0 if not local);
+ *                           row_base[u] = global VCF id of unit u's first row
+ *                           (NULL: local numbering)
+ *   write_units             pwrite the rendered units into `path` (opened
+ *                           without truncation) at offsets[1 + u]; the header
+ *                           at offsets[0] when write_header */
+int32_t bwtmi_job_unit_count(bwtmi_job *job);
+int bwtmi_job_unit_rows(bwtmi_job *job, int64_t *unit_rows);
+int bwtmi_job_render_units(bwtmi_job *job, int fmt, const int64_t *row_base, int64_t *bytes);
+int bwtmi_job_write_units(bwtmi_job *job, const char *path, const int64_t *offsets, int write_header);
 /* final records as rows of int64: start, end, length, tier, n_copies_eval,
  * max_mm, motif_len, cons_len, chrom_id and doubles: copies, mismatch_rate,
  * confidence (for tests / the Python record view) */
