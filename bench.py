@@ -63,6 +63,25 @@ def cpu_baseline(sample_bp: int):
                        f"+ post-processing + STRfinder render, 1 thread, {dt:.1f} s")
 
 
+def fm_all_motifs(seq: bytes, reps: int = 5):
+    """FM backward search over every canonical primitive ACGT motif of length
+    1..10 (bwt.py:1369-1381 + 359-389; 145,338 patterns) on a device index of
+    the rank's contig; outside the timed steps."""
+    from bwtmi import BWTCore, MotifUtils
+    core = BWTCore((seq[FLANK:len(seq) - FLANK] + b"$").decode("latin-1"))
+    pats = [m for k in range(1, 11) for m in MotifUtils.enumerate_motifs(k)]
+    blob, off = BWTCore.pack_patterns(pats)
+    res = core.backward_search_packed(blob, off)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        core.backward_search_packed(blob, off)
+    dt = (time.perf_counter() - t0) / reps
+    found = int((res[:, 0] >= 0).sum())
+    core.clear()
+    return dict(patterns=len(pats), found=found, ms=round(dt * 1e3, 3),
+                mpatterns_per_s=round(len(pats) / dt / 1e6, 2))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -72,6 +91,7 @@ def main():
     ap.add_argument("--cpu-sample-bp", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-index", action="store_true", help="skip the FM index (scan-only step)")
+    ap.add_argument("--no-fm", action="store_true", help="skip the all-motif FM search report")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--pmc-summary", default=PMC_SUMMARY,
                     help="tools/pmc_traffic.py output giving HBM bytes per launch (roofline.traffic)")
@@ -94,10 +114,13 @@ def main():
     # holds only its own sequence: rows are rendered and written by their owner
     job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True,
               build_index=not a.no_index, sa_sample=32)
+    own_seq = b""
     for k in range(world):
         seq = synth.generate_contig(a.contig_bp, k + 1, 0.0) if k == rank else b""
         trim = FLANK if len(seq) > 2 * FLANK else 0
         job.add_contig(f"contig{k + 1}", seq, trim, trim)
+        if k == rank:
+            own_seq = seq
     job.select([rank])
     t_up = time.perf_counter()
     job.upload(ctx)                           # host -> HBM once; outside the timed region
@@ -170,6 +193,7 @@ def main():
                         alg_bytes_per_launch=round(kbytes / launches), avg_launch_ms=round(kms / launches, 4),
                         launches_per_step=launches / a.steps)
     cpu = None if a.no_cpu_baseline else cpu_baseline(a.cpu_sample_bp)
+    fm = None if a.no_fm else fm_all_motifs(own_seq)
     line = {
         "metric": "Mbp/s indexed+scanned (Tier1+2) on 100 Mbp synthetic FASTA, 1/2/4/8 GPU",
         "value": round(value, 3), "unit": "Mbp/s", "n_gpus": world, "steps": a.steps,
@@ -190,6 +214,7 @@ def main():
                                "render": round(stages[6], 2)},
         "kernels_ms_per_step": {k: round(v[0] / a.steps, 3) for k, v in sorted(kstats.items())},
         "h2d_upload_ms": round(upload_ms, 2),
+        "fm_all_motifs_1_10": fm,
         "value_incl_upload": round(total_bp / 1e6 / (elapsed / a.steps + upload_ms / 1e3), 3),
     }
     print(json.dumps(line))

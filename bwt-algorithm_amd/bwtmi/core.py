@@ -150,17 +150,26 @@ class BWTCore:
             base += int(np.count_nonzero(self.bwt_arr[ci * k:pos] == code))
         return base
 
-    def backward_search_batch(self, patterns: Sequence[str]) -> np.ndarray:
-        """Device batch of BWTCore.backward_search: int64[len(patterns), 2]."""
+    @staticmethod
+    def pack_patterns(patterns: Sequence[str]) -> Tuple[np.ndarray, np.ndarray]:
+        """(concatenated bytes, offsets[n + 1]) for backward_search_packed."""
         enc = [p.encode("utf-8") for p in patterns]
         off = np.zeros(len(enc) + 1, dtype=np.int64)
         off[1:] = np.cumsum([len(e) for e in enc]) if enc else 0
         blob = np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8)
-        out = np.zeros((max(len(enc), 1), 2), dtype=np.int64)
+        return blob, off
+
+    def backward_search_packed(self, blob: np.ndarray, off: np.ndarray) -> np.ndarray:
+        npat = off.size - 1
+        out = np.zeros((max(npat, 1), 2), dtype=np.int64)
         check(lib().bwtmi_backward_search_batch(self._ctx, self._h, blob.ctypes.data_as(C.c_void_p),
-                                                off.ctypes.data_as(C.c_void_p), len(enc),
+                                                off.ctypes.data_as(C.c_void_p), npat,
                                                 out.ctypes.data_as(C.c_void_p)))
-        return out[:len(enc)]
+        return out[:npat]
+
+    def backward_search_batch(self, patterns: Sequence[str]) -> np.ndarray:
+        """Device batch of BWTCore.backward_search: int64[len(patterns), 2]."""
+        return self.backward_search_packed(*self.pack_patterns(patterns))
 
     def backward_search(self, pattern: str) -> Tuple[int, int]:
         if not pattern:

@@ -244,6 +244,27 @@ class MotifUtils:
 
     @staticmethod
     def enumerate_motifs(k: int, alphabet: str = "ACGT") -> Iterator[str]:
+        """bwt.py:1369-1381: canonical (least rotation) primitive strings of
+        length k in itertools.product order.  Vectorised for k >= 1 over a
+        duplicate-free alphabet: a string is its own least rotation iff no
+        rotation is smaller, and primitive iff no non-trivial rotation equals
+        it (motif[:p] * (k // p) == motif <=> rotation by p is the identity)."""
+        a = len(alphabet)
+        if k >= 1 and a >= 1 and len(set(alphabet)) == a and a ** k <= 1 << 22:
+            rank = np.argsort(np.argsort([ord(c) for c in alphabet]))   # string order of each symbol
+            idx = np.arange(a ** k, dtype=np.int64)
+            digits = np.stack([(idx // a ** (k - 1 - j)) % a for j in range(k)], axis=1)
+            w = np.array([a ** (k - 1 - j) for j in range(k)], dtype=np.int64)
+            r = rank[digits]
+            val = r @ w
+            keep = np.ones(idx.size, dtype=bool)
+            for s in range(1, k):
+                rot = np.roll(r, -s, axis=1) @ w
+                keep &= rot > val          # smaller rotation -> not canonical; equal -> not primitive
+            chars = np.array(list(alphabet))
+            for row in digits[keep]:
+                yield "".join(chars[row])
+            return
         for tup in product(alphabet, repeat=k):
             s = "".join(tup)
             if MotifUtils.get_canonical_motif(s) == s and MotifUtils.is_primitive_motif(s):

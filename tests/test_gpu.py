@@ -306,6 +306,21 @@ def test_backward_search_all_short_motifs(gpu_ctx):
         assert (sp, ep) == ref.backward_search(p.encode()), p
 
 
+def test_backward_search_all_motifs_1_to_10(gpu_ctx):
+    """The north_star's FM query set: every canonical primitive ACGT motif of
+    length 1..10 (MotifUtils.enumerate_motifs, bwt.py:1369-1381; 145,338
+    patterns) on a 1 Mbp contig, interval for interval against the oracle."""
+    from bwtmi import BWTCore, MotifUtils, synth
+    text = synth.generate_contig(1_000_000, 5) + b"$"
+    core = BWTCore(text.decode())
+    ref = oracle.Index(text)
+    pats = [m for k in range(1, 11) for m in MotifUtils.enumerate_motifs(k)]
+    assert len(pats) == 145338
+    got = core.backward_search_batch(pats)
+    for p, (sp, ep) in zip(pats, got.tolist()):
+        assert (sp, ep) == ref.backward_search(p.encode()), p
+
+
 def test_index_12mbp_properties(gpu_ctx):
     """C4-size contig: SA is a permutation, adjacent suffixes ascend, BWT/occ consistent."""
     from bwtmi import BWTCore, synth

@@ -124,6 +124,23 @@ def test_record_view_matches_reference_unittest(golden_dir, built_lib):
     assert any(v.startswith("9:10:del(") for v in r12.variations)
 
 
+def test_enumerate_motifs_vectorised_matches_definition(built_lib):
+    """bwt.py:1369-1381 restated literally (product order, canonical & primitive)
+    vs the vectorised enumeration; 145,338 motifs for k = 1..10."""
+    from itertools import product
+    from bwtmi import MotifUtils as M
+
+    def literal(k, alphabet="ACGT"):
+        for tup in product(alphabet, repeat=k):
+            s = "".join(tup)
+            if min(s[i:] + s[:i] for i in range(len(s))) == s and M.is_primitive_motif(s):
+                yield s
+    for k in range(1, 7):
+        assert list(M.enumerate_motifs(k)) == list(literal(k)), k
+    assert list(M.enumerate_motifs(5, "TGCAN")) == list(literal(5, "TGCAN"))
+    assert sum(1 for k in range(1, 11) for _ in M.enumerate_motifs(k)) == 145338
+
+
 def test_motifutils_mirror_matches_reference(golden_dir, built_lib):
     from bwtmi import MotifUtils as M
     with open(os.path.join(golden_dir, "motif_known.json")) as f:
