@@ -33,6 +33,12 @@ class Params(C.Structure):
                 ("build_index", C.c_int32), ("sa_sample", C.c_int32), ("reserved", C.c_int32)]
 
 
+class LibParams(C.Structure):
+    _fields_ = [("min_period", C.c_int32), ("max_period", C.c_int32), ("max_short_motif", C.c_int32),
+                ("min_copies", C.c_int32), ("min_array_length", C.c_int32), ("allow_mismatches", C.c_int32),
+                ("min_entropy", C.c_double)]
+
+
 _lib = None
 _lock = threading.RLock()    # ctx() -> lib() re-enters
 
@@ -63,6 +69,9 @@ _SIGS = {
     "bwtmi_index_get_kmer": (C.c_int, [_P, _P, _P]),
     "bwtmi_index_lcp": (C.c_int, [_P, _P, _P]),
     "bwtmi_backward_search_batch": (C.c_int, [_P, _P, _P, _P, C.c_int64, _P]),
+    "bwtmi_index_lcp_plateaus": (C.c_int, [_P, _P, C.POINTER(LibParams), C.POINTER(C.c_void_p),
+                                           C.POINTER(C.c_int64)]),
+    "bwtmi_index_short_imperfect": (C.c_int, [_P, _P, C.POINTER(LibParams), _P, C.c_int64, _P, C.c_int32]),
     "bwtmi_job_create": (C.c_int, [C.POINTER(Params), C.POINTER(_P)]),
     "bwtmi_job_free": (C.c_int, [_P]),
     "bwtmi_job_add_contig": (C.c_int, [_P, C.c_char_p, _P, C.c_int64, C.c_int64, C.c_int64,

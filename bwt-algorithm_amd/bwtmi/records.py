@@ -90,8 +90,8 @@ def _entropy(s: str) -> float:
     e = 0.0
     for c in seen.values():
         p = c / len(s)
-        e -= p * math.log2(p)
-    return e
+        e -= p * np.log2(p)            # MotifUtils.calculate_entropy uses np.log2 (bwt.py:730-745)
+    return float(e)
 
 
 class Job:

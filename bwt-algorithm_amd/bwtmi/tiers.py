@@ -101,9 +101,49 @@ class Tier2LCPFinder:
             return np.zeros(0, dtype=np.int32)
         return self.bwt.lcp_array()
 
-    def find_short_imperfect_repeats(self, chromosome: str, tier1_seen: Set[Tuple[int, int]]):
-        raise NotImplementedError("find_short_imperfect_repeats: FM seed-and-extend kernels are "
-                                  "the next §8 row (not built yet)")
+    def _params(self) -> "_lib.LibParams":
+        return _lib.LibParams(self.min_period, self.max_period, self.max_short_motif, self.min_copies,
+                              self.min_array_length, int(bool(self.allow_mismatches)), float(self.min_entropy))
+
+    def find_short_imperfect_repeats(self, chromosome: str, tier1_seen: Set[Tuple[int, int]]) -> List[TandemRepeat]:
+        """bwt.py:2027-2095: k-mer-table / FM seeds for every canonical motif of
+        length min_period..9, Hamming seed-and-extend with majority-vote
+        consensus (device extension table, library.hip), records as bwt.py:2653-2691."""
+        from .records import Job
+        t = np.ascontiguousarray(self.bwt.text_arr, dtype=np.uint8)
+        if t.size > 1_000_000:                                   # bwt.py:2048-2051
+            if self.show_progress:
+                print(f"  [{chromosome}] Tier 2 short imperfect repeats: SKIPPED (>{t.size:,} bp, too expensive)")
+            return []
+        job = Job()
+        job.add_contig(chromosome, t.tobytes(), 0, 0)
+        seen = np.array(sorted(tier1_seen or ()), dtype=np.int64).reshape(-1)
+        buf = seen if seen.size else np.zeros(2, dtype=np.int64)
+        p = self._params()
+        check(lib().bwtmi_index_short_imperfect(self.bwt._ctx, self.bwt._h, C.byref(p), buf.ctypes.data,
+                                                seen.size // 2, job.h, 0))
+        return list(job.records())
+
+    def _detect_lcp_plateaus(self, lcp_array: np.ndarray, chromosome: str) -> List[TandemRepeat]:
+        """bwt.py:2118-2145 with _analyze_sa_interval_for_tandems (2500-2549) on the
+        device.  The LCP used is this finder's own Kasai array (what
+        _compute_lcp_array() returns), recomputed on the device."""
+        out = C.c_void_p()
+        n = C.c_int64()
+        p = self._params()
+        check(lib().bwtmi_index_lcp_plateaus(self.bwt._ctx, self.bwt._h, C.byref(p), C.byref(out), C.byref(n)))
+        try:
+            trip = (np.ctypeslib.as_array(C.cast(out, C.POINTER(C.c_int64)), shape=(n.value * 3,)).copy()
+                    if n.value else np.zeros(0, dtype=np.int64))
+        finally:
+            lib().bwtmi_free(out)
+        t = self.bwt.text_arr
+        res = []
+        for s, c, per in trip.reshape(-1, 3).tolist():
+            res.append(TandemRepeat(chrom=chromosome, start=s, end=s + c * per,
+                                    motif=bytes(t[s:s + per]).decode("ascii"), copies=c, length=c * per,
+                                    tier=2, confidence=0.9))
+        return res
 
     def find_long_repeats(self, chromosome: str, tier1_seen=None):
         raise NotImplementedError("find_long_repeats: out of scope (wall-clock-dependent results, "

@@ -290,6 +290,51 @@ int bwtmi_backward_search_batch(bwtmi_ctx *ctx, bwtmi_index *idx, const uint8_t 
     });
 }
 
+static LibParams lib_params(const bwtmi_lib_params *p) {
+    LibParams q;
+    if (p) {
+        q.min_period = p->min_period;
+        q.max_period = p->max_period;
+        q.max_short_motif = p->max_short_motif;
+        q.min_copies = p->min_copies;
+        q.min_array_length = p->min_array_length;
+        q.allow_mismatches = p->allow_mismatches;
+        q.min_entropy = p->min_entropy;
+    }
+    return q;
+}
+
+int bwtmi_index_lcp_plateaus(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_lib_params *p, int64_t **out,
+                             int64_t *n) {
+    return guard([&] {
+        CHECK_ARG(ctx && idx && out && n, "null argument");
+        *out = nullptr;
+        *n = 0;
+        ctx->c.activate();
+        std::vector<int64_t> v;
+        lcp_plateaus_device(ctx->c, idx->d, lib_params(p), v);
+        auto *o = (int64_t *)std::malloc(std::max<size_t>(1, v.size()) * sizeof(int64_t));
+        if (!o) fail(BWTMI_E_NOMEM, "malloc");
+        if (!v.empty()) std::memcpy(o, v.data(), v.size() * sizeof(int64_t));
+        *out = o;
+        *n = (int64_t)(v.size() / 3);
+    });
+}
+
+int bwtmi_index_short_imperfect(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_lib_params *p, const int64_t *seen,
+                                int64_t nseen, bwtmi_job *job, int32_t contig_id) {
+    return guard([&] {
+        CHECK_ARG(ctx && idx && job && (seen || nseen == 0) && nseen >= 0, "bad argument");
+        CHECK_ARG(contig_id >= 0 && contig_id < (int32_t)job->j.contigs.size(), "bad contig id");
+        CHECK_ARG((int64_t)job->j.contigs[(size_t)contig_id].full.size() == index_n(idx->d),
+                  "the job contig must hold the index text");
+        ctx->c.activate();
+        std::vector<int64_t> sp(seen, seen + 2 * nseen);
+        short_imperfect_device(ctx->c, idx->d, lib_params(p), sp, contig_id, job->j.final_recs);
+        job->j.postprocessed = true;
+    });
+}
+
 // ------------------------------------------------------------ job
 int bwtmi_job_create(const bwtmi_params *params, bwtmi_job **out) {
     return guard([&] {

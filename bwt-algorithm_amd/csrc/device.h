@@ -179,6 +179,23 @@ void index_get_occ(Ctx &c, const DeviceIndex *, uint8_t code, int32_t *out);
 void index_get_sampled(Ctx &c, const DeviceIndex *, int32_t *out);
 void index_get_kmer(Ctx &c, const DeviceIndex *, int64_t *offsets, int32_t *pos);
 void index_lcp(Ctx &c, DeviceIndex *, int32_t *out);
+const int32_t *index_lcp_device(Ctx &c, DeviceIndex *);   // in the S_MISC1 slot
+const uint8_t *index_text_device(const DeviceIndex *);
+const uint32_t *index_sa_device(const DeviceIndex *);
+void index_get_text(Ctx &c, const DeviceIndex *, uint8_t *out);
+
+// ----- library finders off the CLI path (library.hip)
+struct LibParams {
+    int32_t min_period = 1, max_period = 1000, max_short_motif = 9, min_copies = 3;
+    int32_t min_array_length = 6, allow_mismatches = 1;
+    double min_entropy = 1.0;
+};
+// Tier2LCPFinder._detect_lcp_plateaus (bwt.py:2118-2145, 2500-2560): (start, copies, period) in order
+void lcp_plateaus_device(Ctx &c, DeviceIndex *ix, const LibParams &p, std::vector<int64_t> &out);
+// Tier2LCPFinder.find_short_imperfect_repeats (bwt.py:2027-2095, 2562-2825); records appended
+// to `out` with chrom = `chrom`; `seen` = (start, end) pairs already found (tier1_seen)
+void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const std::vector<int64_t> &seen,
+                            int32_t chrom, std::vector<Rec> &out);
 void index_backward_search(Ctx &c, DeviceIndex *, const uint8_t *pats, const int64_t *off, int64_t npat,
                            int64_t *sp_ep);
 

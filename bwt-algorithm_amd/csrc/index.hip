@@ -540,9 +540,27 @@ void index_get_kmer(Ctx &c, const DeviceIndex *ix, int64_t *offsets, int32_t *po
     if (ix->kmer_count) HIPCHECK(hipMemcpy(pos, ix->kmer_pos.p, (size_t)ix->kmer_count * 4, hipMemcpyDeviceToHost));
 }
 
+const uint8_t *index_text_device(const DeviceIndex *ix) { return ix->text.as<uint8_t>(); }
+const uint32_t *index_sa_device(const DeviceIndex *ix) { return ix->sa.as<uint32_t>(); }
+
+void index_get_text(Ctx &c, const DeviceIndex *ix, uint8_t *out) {
+    if (!ix->n) return;
+    HIPCHECK(hipMemcpyAsync(out, ix->text.p, (size_t)ix->n, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+}
+
 void index_lcp(Ctx &c, DeviceIndex *ix, int32_t *out) {
     const int64_t n = ix->n;
     if (!n) return;
+    const int32_t *lcp = index_lcp_device(c, ix);
+    HIPCHECK(hipMemcpyAsync(out, lcp, (size_t)n * 4, hipMemcpyDeviceToHost, c.stream));
+    HIPCHECK(hipStreamSynchronize(c.stream));
+}
+
+// Kasai LCP left in the S_MISC1 slot (valid until that slot is reused)
+const int32_t *index_lcp_device(Ctx &c, DeviceIndex *ix) {
+    const int64_t n = ix->n;
+    if (!n) return nullptr;
     hipStream_t st = c.stream;
     c.slot[S_MISC0].ensure((size_t)n * 4);
     c.slot[S_MISC1].ensure((size_t)n * 4);
@@ -565,8 +583,7 @@ void index_lcp(Ctx &c, DeviceIndex *ix, int32_t *out) {
                            isa, n, lcp);
     }
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipMemcpyAsync(out, lcp, (size_t)n * 4, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
+    return lcp;
 }
 
 void index_backward_search(Ctx &c, DeviceIndex *ix, const uint8_t *pats, const int64_t *off, int64_t npat,

@@ -1,0 +1,568 @@
+// library.hip -- the reference's library finders that are not on the CLI path
+// (SURVEY.md §8(a) A2-9 and A2-10), over a device FM index.
+//
+// LCP plateaus (Tier2LCPFinder._detect_lcp_plateaus, bwt.py:2118-2145, with
+// _analyze_sa_interval_for_tandems 2500-2549 and _validate_periodicity_arr
+// 2551-2560): device Kasai LCP -> run flags at thr = max(min_period,
+// min(max_period, max LCP, 20)) -> one stable radix sort of (run, SA value)
+// keys gives every run's sorted positions in run order -> one thread per
+// position counts its arithmetic progression of step thr and validates the
+// periodicity of text[p, p + copies*thr) -> compaction in that order.
+//
+// Short imperfect repeats (Tier2LCPFinder.find_short_imperfect_repeats,
+// bwt.py:2027-2095 -> _find_tandems_fm_with_mismatches 2562-2695 ->
+// _extend_tandem_fm 2697-2805).  The extension of a candidate depends only on
+// (candidate start, unit length): k_extend computes it for EVERY start and
+// every unit length 1..9 at once (inputs are <= 1 Mbp), keeping per-column
+// symbol counts so each added copy costs O(unit) instead of re-voting all
+// copies (majority vote = np.unique + argmax: smallest byte among the most
+// frequent; Hamming total and transversions follow from the counts).  The
+// order-dependent part -- seeds from the k-mer table / FM locate per motif in
+// enumerate_motifs order, the seen-region test, best-shift choice, primitive
+// reduction (whose motif_len persists for later seeds, as in the reference),
+// maximality, match-rate filter, variations -- runs on the host over that table.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "device.h"
+
+namespace bwtmi {
+namespace {
+
+constexpr int kB = 256;
+constexpr int kMaxUnit = 9;   // enumerate_motifs range ends at 9 (bwt.py:2052)
+constexpr int kD = 6;         // distinct symbols tracked per column before a host recompute
+
+inline unsigned blocks(int64_t n) { return (unsigned)((n + kB - 1) / kB); }
+
+// ------------------------------------------------------------- LCP plateaus
+__global__ void k_max_i32(const int32_t *__restrict__ a, int64_t n, int *__restrict__ out) {
+    int v = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) v = max(v, a[i]);
+    __shared__ int red[kB];
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = kB / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMax(out, red[0]);
+}
+
+__global__ void k_plateau_flags(const int32_t *__restrict__ lcp, int64_t n, int32_t thr, uint32_t *__restrict__ inrun,
+                                uint32_t *__restrict__ head) {
+    const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (i >= n) return;
+    const bool in = lcp[i] >= thr;
+    inrun[i] = in ? 1u : 0u;
+    head[i] = (in && (i == 0 || lcp[i - 1] < thr)) ? 1u : 0u;
+}
+
+__global__ void k_plateau_keys(const uint32_t *__restrict__ sa, const uint32_t *__restrict__ inrun,
+                               const uint32_t *__restrict__ head, const uint32_t *__restrict__ hscan,
+                               const uint32_t *__restrict__ cpos, int64_t n, uint64_t *__restrict__ keys) {
+    const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (i >= n || !inrun[i]) return;
+    const uint64_t run = (uint64_t)(hscan[i] + head[i] - 1);
+    keys[cpos[i]] = (run << 32) | (uint64_t)sa[i];
+}
+
+// one sorted position of one run: progression length and periodicity test
+__global__ void k_plateau_eval(const uint64_t *__restrict__ keys, int64_t m, const uint8_t *__restrict__ t, int64_t n,
+                               int64_t thr, int64_t mc, uint32_t *__restrict__ flag, int64_t *__restrict__ copies) {
+    const int64_t a = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (a >= m) return;
+    const uint64_t run = keys[a] >> 32;
+    const int64_t sp = (int64_t)(keys[a] & 0xffffffffull);
+    int64_t c = 1;
+    for (int64_t b = a + 1; b < m && (keys[b] >> 32) == run && (int64_t)(keys[b] & 0xffffffffull) == sp + c * thr; ++b)
+        ++c;
+    bool ok = false;
+    if (c >= mc && sp + thr <= n) {
+        const int64_t len = min(c * thr, n - sp);   // text[sp : sp + copies*thr]
+        if (len >= 2 * thr) {
+            int64_t match = 0;
+            for (int64_t q = 0; q < len; ++q) match += t[sp + q] == t[sp + q % thr];
+            ok = (double)match / (double)len >= 0.8;
+        }
+    }
+    flag[a] = ok ? 1u : 0u;
+    copies[a] = c;
+}
+
+__global__ void k_plateau_out(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ flag,
+                              const uint32_t *__restrict__ pos, const int64_t *__restrict__ copies, int64_t m,
+                              int64_t thr, int64_t *__restrict__ out) {
+    const int64_t a = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (a >= m || !flag[a]) return;
+    int64_t *o = out + 3 * (int64_t)pos[a];
+    o[0] = (int64_t)(keys[a] & 0xffffffffull);
+    o[1] = copies[a];
+    o[2] = thr;
+}
+
+// --------------------------------------------------------- seed extension
+__device__ __host__ inline bool transversion(uint8_t a, uint8_t b) {   // count_transversions_array, 781-800
+    if (a == b) return false;
+    const uint8_t x = (a >= 65 && a <= 84) ? a : (uint8_t)'N', y = (b >= 65 && b <= 84) ? b : (uint8_t)'N';
+    if (x == y) return false;   // is_transition(c, c) is True
+    if ((x == 'A' && y == 'G') || (x == 'G' && y == 'A') || (x == 'C' && y == 'T') || (x == 'T' && y == 'C'))
+        return false;
+    return true;
+}
+
+__device__ __host__ inline int64_t max_mm_for_array(int64_t L, int64_t copies) {   // bwt.py:2003-2025
+    const int64_t total = L * copies;
+    if (L == 1) return 0;
+    if (L <= 6) return max((int64_t)1, (int64_t)ceil(0.05 * (double)total));
+    return max((int64_t)1, (int64_t)ceil(0.08 * (double)total));
+}
+
+struct ColHist {
+    uint8_t sym[kMaxUnit][kD];
+    int32_t cnt[kMaxUnit][kD];
+    uint8_t nd[kMaxUnit];
+};
+
+__device__ inline bool hist_add(ColHist &h, const uint8_t *cp, int L, int32_t d) {
+    for (int p = 0; p < L; ++p) {
+        const uint8_t b = cp[p];
+        int k = 0;
+        while (k < h.nd[p] && h.sym[p][k] != b) ++k;
+        if (k == h.nd[p]) {
+            if (k == kD) return false;
+            h.sym[p][k] = b;
+            h.cnt[p][k] = 0;
+            ++h.nd[p];
+        }
+        h.cnt[p][k] += d;
+    }
+    return true;
+}
+
+// total mismatches and transversions of every copy against the majority consensus
+__device__ inline void hist_eval(const ColHist &h, int L, int64_t tc, int64_t &mm, int64_t &tv) {
+    mm = 0;
+    tv = 0;
+    for (int p = 0; p < L; ++p) {
+        int32_t best = 0;
+        uint8_t cons = 0;
+        for (int k = 0; k < h.nd[p]; ++k) {
+            const int32_t v = h.cnt[p][k];
+            if (v > best || (v == best && v > 0 && h.sym[p][k] < cons)) { best = v; cons = h.sym[p][k]; }
+        }
+        mm += tc - best;
+        for (int k = 0; k < h.nd[p]; ++k)
+            if (h.cnt[p][k] > 0 && transversion(h.sym[p][k], cons)) tv += h.cnt[p][k];
+    }
+}
+
+__device__ inline bool homopolymer(const uint8_t *cp, int L) {
+    for (int p = 1; p < L; ++p)
+        if (cp[p] != cp[0]) return false;
+    return true;
+}
+
+// _extend_tandem_fm(text, cs, text[cs:cs+L], L) for all cs and L = 1..Lmax
+__global__ void k_extend(const uint8_t *__restrict__ t, int64_t n, int Lmax, int32_t *__restrict__ es,
+                         int32_t *__restrict__ ee, int32_t *__restrict__ ec, uint8_t *__restrict__ ovf) {
+    const int64_t tid = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (tid >= (int64_t)Lmax * n) return;
+    const int L = (int)(tid / n) + 1;
+    const int64_t cs = tid % n;
+    ovf[tid] = 0;
+    if (cs + L > n) {
+        es[tid] = -1;
+        return;
+    }
+    ColHist h;
+    for (int p = 0; p < L; ++p) h.nd[p] = 0;
+    int64_t start = cs, end = cs + L, copies = 1;
+    bool ok = hist_add(h, t + cs, L, 1);
+    while (ok && end + L <= n) {
+        const uint8_t *nx = t + end;
+        if (L > 1 && homopolymer(nx, L)) break;
+        if (!(ok = hist_add(h, nx, L, 1))) break;
+        int64_t mm, tv;
+        hist_eval(h, L, copies + 1, mm, tv);
+        if (mm <= max_mm_for_array(L, copies + 1) && tv == 0) {
+            ++copies;
+            end += L;
+        } else {
+            hist_add(h, nx, L, -1);
+            break;
+        }
+    }
+    while (ok && start - L >= 0) {
+        const uint8_t *pv = t + start - L;
+        if (L > 1 && homopolymer(pv, L)) break;
+        if (!(ok = hist_add(h, pv, L, 1))) break;
+        int64_t mm, tv;
+        hist_eval(h, L, copies + 1, mm, tv);
+        if (mm <= max_mm_for_array(L, copies + 1) && tv == 0) {
+            ++copies;
+            start -= L;
+        } else {
+            hist_add(h, pv, L, -1);
+            break;
+        }
+    }
+    es[tid] = (int32_t)start;
+    ee[tid] = (int32_t)end;
+    ec[tid] = (int32_t)copies;
+    ovf[tid] = ok ? 0 : 1;
+}
+
+// --------------------------------------------------- host-side exact helpers
+// majority vote of n_copies copies from `start` (np.unique + argmax)
+static void majority(const uint8_t *t, int64_t n, int64_t start, int64_t L, int64_t n_copies, std::string &cons,
+                     int64_t &used) {
+    cons.assign((size_t)L, '\0');
+    used = 0;
+    while (used < n_copies && start + (used + 1) * L <= n) ++used;
+    for (int64_t p = 0; p < L; ++p) {
+        int32_t cnt[256] = {0};
+        for (int64_t i = 0; i < used; ++i) ++cnt[t[start + i * L + p]];
+        int best = -1, bv = 0;
+        for (int b = 0; b < 256; ++b)
+            if (cnt[b] > bv) { bv = cnt[b]; best = b; }
+        cons[(size_t)p] = (char)(best < 0 ? 0 : best);
+    }
+}
+
+// scalar _extend_tandem_fm for a column with more than kD symbols
+static void extend_host(const uint8_t *t, int64_t n, int64_t cs, int64_t L, int64_t &s, int64_t &e, int64_t &c) {
+    s = cs;
+    e = cs + L;
+    c = 1;
+    std::string cons;
+    int64_t used;
+    auto score = [&](int64_t from, int64_t tc, int64_t &mm, int64_t &tv) {
+        majority(t, n, from, L, tc, cons, used);
+        mm = tv = 0;
+        for (int64_t i = 0; i < tc; ++i) {
+            const int64_t a = from + i * L;
+            if (a + L > n) continue;
+            for (int64_t p = 0; p < L; ++p) {
+                const uint8_t x = t[a + p], y = (uint8_t)cons[(size_t)p];
+                if (x != y) {
+                    ++mm;
+                    if (transversion(x, y)) ++tv;
+                }
+            }
+        }
+    };
+    auto homo = [&](int64_t a) {
+        for (int64_t p = 1; p < L; ++p)
+            if (t[a + p] != t[a]) return false;
+        return true;
+    };
+    while (e + L <= n) {
+        if (L > 1 && homo(e)) break;
+        int64_t mm, tv;
+        score(s, c + 1, mm, tv);
+        if (mm <= max_mm_for_array(L, c + 1) && tv == 0) { ++c; e += L; }
+        else break;
+    }
+    while (s - L >= 0) {
+        if (L > 1 && homo(s - L)) break;
+        int64_t mm, tv;
+        score(s - L, c + 1, mm, tv);
+        if (mm <= max_mm_for_array(L, c + 1) && tv == 0) { ++c; s -= L; }
+        else break;
+    }
+}
+
+// build_consensus_motif_array (bwt.py:1208-1256)
+static bool consensus_array(const uint8_t *t, int64_t n, int64_t start, int64_t L, int64_t n_copies, std::string &cons,
+                            double &mm_rate, int64_t &max_mm) {
+    if (n_copies == 0 || L == 0) return false;
+    int64_t used;
+    majority(t, n, start, L, n_copies, cons, used);
+    if (used == 0) return false;
+    int64_t tot = 0;
+    max_mm = 0;
+    for (int64_t i = 0; i < used; ++i) {
+        int64_t h = 0;
+        for (int64_t p = 0; p < L; ++p) h += t[start + i * L + p] != (uint8_t)cons[(size_t)p];
+        tot += h;
+        max_mm = std::max(max_mm, h);
+    }
+    mm_rate = (double)tot / (double)(used * L);
+    return true;
+}
+
+// canonical (least rotation, forward only) primitive ACGT strings of length k, product order
+static void enumerate_motifs(int k, std::vector<std::string> &out) {
+    out.clear();
+    static const char A[4] = {'A', 'C', 'G', 'T'};
+    const int64_t total = (int64_t)1 << (2 * k);
+    std::string s((size_t)k, 'A');
+    for (int64_t code = 0; code < total; ++code) {
+        for (int j = 0; j < k; ++j) s[(size_t)j] = A[(code >> (2 * (k - 1 - j))) & 3];
+        bool keep = true;
+        for (int r = 1; r < k && keep; ++r) {
+            int cmp = 0;
+            for (int q = 0; q < k && !cmp; ++q) {
+                const char x = s[(size_t)((q + r) % k)], y = s[(size_t)q];
+                cmp = x < y ? -1 : (x > y ? 1 : 0);
+            }
+            keep = cmp > 0;   // a smaller rotation: not canonical; an equal one: not primitive
+        }
+        if (keep) out.push_back(s);
+    }
+}
+
+inline char comp_base(char c) {
+    switch (c) {
+        case 'A': return 'T';
+        case 'T': return 'A';
+        case 'C': return 'G';
+        case 'G': return 'C';
+        default: return c;
+    }
+}
+
+}  // namespace
+
+void lcp_plateaus_device(Ctx &c, DeviceIndex *ix, const LibParams &p, std::vector<int64_t> &out) {
+    out.clear();
+    const int64_t n = index_n(ix);
+    if (n == 0) return;
+    hipStream_t st = c.stream;
+    const int32_t *lcp = index_lcp_device(c, ix);
+    c.slot[S_COUNTS].ensure(64);
+    int *d_max = c.slot[S_COUNTS].as<int>();
+    HIPCHECK(hipMemsetAsync(d_max, 0, 4, st));
+    hipLaunchKernelGGL(k_max_i32, dim3((unsigned)std::min<int64_t>(1024, blocks(n))), dim3(kB), 0, st, lcp, n, d_max);
+    int lmax = 0;
+    HIPCHECK(hipMemcpyAsync(&lmax, d_max, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if (lmax < p.min_period) return;
+    const int64_t thr = std::max<int64_t>(p.min_period, std::min<int64_t>(std::min<int64_t>(p.max_period, lmax), 20));
+    c.slot[S_IDX1].ensure((size_t)(n + 1) * 4);
+    c.slot[S_IDX2].ensure((size_t)(n + 1) * 4);
+    c.slot[S_IDX3].ensure((size_t)(n + 1) * 4);
+    c.slot[S_IDX4].ensure((size_t)(n + 1) * 4);
+    uint32_t *inrun = c.slot[S_IDX1].as<uint32_t>(), *head = c.slot[S_IDX2].as<uint32_t>();
+    uint32_t *hscan = c.slot[S_IDX3].as<uint32_t>(), *cpos = c.slot[S_IDX4].as<uint32_t>();
+    hipLaunchKernelGGL(k_plateau_flags, dim3(blocks(n)), dim3(kB), 0, st, lcp, n, (int32_t)thr, inrun, head);
+    HIPCHECK(hipMemsetAsync(inrun + n, 0, 4, st));
+    HIPCHECK(hipMemsetAsync(head + n, 0, 4, st));
+    exclusive_scan<uint32_t>(c, head, hscan, n + 1);
+    exclusive_scan<uint32_t>(c, inrun, cpos, n + 1);
+    uint32_t m32 = 0, runs = 0;
+    HIPCHECK(hipMemcpyAsync(&m32, cpos + n, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(&runs, hscan + n, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    const int64_t m = m32;
+    if (m == 0) return;
+    c.slot[S_IDX0].ensure((size_t)m * 8);
+    c.slot[S_IDX5].ensure((size_t)m * 8);
+    c.slot[S_IDX6].ensure((size_t)(m + 1) * 4);
+    c.slot[S_IDX7].ensure((size_t)(m + 1) * 4);
+    uint64_t *keys = c.slot[S_IDX0].as<uint64_t>();
+    int64_t *copies = c.slot[S_IDX5].as<int64_t>();
+    uint32_t *flag = c.slot[S_IDX6].as<uint32_t>(), *pos = c.slot[S_IDX7].as<uint32_t>();
+    hipLaunchKernelGGL(k_plateau_keys, dim3(blocks(n)), dim3(kB), 0, st, index_sa_device(ix), inrun, head, hscan, cpos,
+                       n, keys);
+    int rb = 0;
+    while (rb < 32 && ((uint64_t)runs >> rb)) ++rb;
+    radix_sort_pairs32(c, keys, nullptr, m, 0, ((32 + rb + 7) / 8) * 8);
+    hipLaunchKernelGGL(k_plateau_eval, dim3(blocks(m)), dim3(kB), 0, st, keys, m, index_text_device(ix), n, thr,
+                       (int64_t)p.min_copies, flag, copies);
+    HIPCHECK(hipMemsetAsync(flag + m, 0, 4, st));
+    exclusive_scan<uint32_t>(c, flag, pos, m + 1);
+    uint32_t k32 = 0;
+    HIPCHECK(hipMemcpyAsync(&k32, pos + m, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if (k32 == 0) return;
+    c.slot[S_MISC2].ensure((size_t)k32 * 24);
+    hipLaunchKernelGGL(k_plateau_out, dim3(blocks(m)), dim3(kB), 0, st, keys, flag, pos, copies, m, thr,
+                       c.slot[S_MISC2].as<int64_t>());
+    HIPCHECK(hipGetLastError());
+    out.resize((size_t)k32 * 3);
+    HIPCHECK(hipMemcpyAsync(out.data(), c.slot[S_MISC2].p, (size_t)k32 * 24, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+}
+
+void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const std::vector<int64_t> &seen_pairs,
+                            int32_t chrom, std::vector<Rec> &out) {
+    const int64_t n = index_n(ix);
+    if (n > 1000000 || n == 0) return;                    // bwt.py:2048
+    const int kmin = std::max(1, p.min_period), kend = std::min(p.max_short_motif + 1, 10);
+    hipStream_t st = c.stream;
+    std::vector<uint8_t> text((size_t)n);
+    index_get_text(c, ix, text.data());
+    const uint8_t *t = text.data();
+
+    // extension table for every start and unit length 1..9
+    const int Lmax = kMaxUnit;
+    const int64_t tot = (int64_t)Lmax * n;
+    c.slot[S_IDX0].ensure((size_t)tot * 4);
+    c.slot[S_IDX1].ensure((size_t)tot * 4);
+    c.slot[S_IDX2].ensure((size_t)tot * 4);
+    c.slot[S_IDX3].ensure((size_t)tot);
+    hipLaunchKernelGGL(k_extend, dim3(blocks(tot)), dim3(kB), 0, st, index_text_device(ix), n, Lmax,
+                       c.slot[S_IDX0].as<int32_t>(), c.slot[S_IDX1].as<int32_t>(), c.slot[S_IDX2].as<int32_t>(),
+                       c.slot[S_IDX3].as<uint8_t>());
+    HIPCHECK(hipGetLastError());
+    std::vector<int32_t> es((size_t)tot), ee((size_t)tot), ec((size_t)tot);
+    std::vector<uint8_t> ovf((size_t)tot);
+    HIPCHECK(hipMemcpyAsync(es.data(), c.slot[S_IDX0].p, (size_t)tot * 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(ee.data(), c.slot[S_IDX1].p, (size_t)tot * 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(ec.data(), c.slot[S_IDX2].p, (size_t)tot * 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(ovf.data(), c.slot[S_IDX3].p, (size_t)tot, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    for (int64_t q = 0; q < tot; ++q)
+        if (ovf[(size_t)q]) {
+            int64_t s, e, cc;
+            extend_host(t, n, q % n, q / n + 1, s, e, cc);
+            es[(size_t)q] = (int32_t)s;
+            ee[(size_t)q] = (int32_t)e;
+            ec[(size_t)q] = (int32_t)cc;
+        }
+
+    // seeds: k-mer table (with the reference's short-k lookup, bwt.py:173-193) or FM locate
+    std::vector<int64_t> koff;
+    std::vector<int32_t> kpos;
+    const int64_t kcount = index_kmer_count(ix);
+    if (kcount > 0) {
+        koff.resize(65537);
+        kpos.resize((size_t)kcount);
+        index_get_kmer(c, ix, koff.data(), kpos.data());
+    }
+    std::vector<std::vector<std::string>> motifs(10);
+    std::vector<std::string> pats;            // patterns that go through locate
+    for (int k = kmin; k < kend; ++k) {
+        enumerate_motifs(k, motifs[(size_t)k]);
+        if (k <= 8 && kcount > 0) continue;
+        for (auto &m : motifs[(size_t)k]) {
+            if (entropy_of(m.data(), k) < p.min_entropy) continue;
+            std::string rc(m.rbegin(), m.rend());
+            for (auto &ch : rc) ch = comp_base(ch);
+            for (int r = 0; r < k; ++r) {
+                pats.push_back(m.substr((size_t)r) + m.substr(0, (size_t)r));
+                pats.push_back(rc.substr((size_t)r) + rc.substr(0, (size_t)r));
+            }
+        }
+    }
+    std::vector<int64_t> spep;
+    std::vector<int32_t> sa;
+    size_t pat_at = 0;
+    if (!pats.empty()) {
+        std::vector<int64_t> off(pats.size() + 1, 0);
+        std::string blob;
+        for (size_t q = 0; q < pats.size(); ++q) {
+            blob += pats[q];
+            off[q + 1] = (int64_t)blob.size();
+        }
+        spep.resize(pats.size() * 2);
+        index_backward_search(c, ix, (const uint8_t *)blob.data(), off.data(), (int64_t)pats.size(), spep.data());
+        sa.resize((size_t)n);
+        index_get_sa(c, ix, sa.data());
+    }
+
+    std::vector<uint8_t> seen((size_t)n + 1, 0);
+    for (size_t q = 0; q + 1 < seen_pairs.size(); q += 2)
+        for (int64_t x = std::max<int64_t>(0, seen_pairs[q]); x < std::min<int64_t>(n, seen_pairs[q + 1]); ++x)
+            seen[(size_t)x] = 1;
+    const std::string seq((const char *)t, (size_t)n);
+    std::vector<int64_t> positions;
+    AlignSummary summ;
+    for (int k = kmin; k < kend; ++k) {
+        for (auto &m : motifs[(size_t)k]) {
+            if (entropy_of(m.data(), k) < p.min_entropy) continue;   // bwt.py:2058-2060
+            positions.clear();
+            const bool use_hash = k <= 8 && kcount > 0;
+            std::string rc(m.rbegin(), m.rend());
+            for (auto &ch : rc) ch = comp_base(ch);
+            if (use_hash) {
+                for (int r = 0; r < k; ++r)
+                    for (const std::string &rot : {m.substr((size_t)r) + m.substr(0, (size_t)r),
+                                                   rc.substr((size_t)r) + rc.substr(0, (size_t)r)}) {
+                        int64_t w = 0;
+                        for (char ch : rot) w = (w << 2) | (ch == 'C' ? 1 : ch == 'G' ? 2 : ch == 'T' ? 3 : 0);
+                        for (int64_t q = koff[(size_t)w]; q < koff[(size_t)w + 1]; ++q) positions.push_back(kpos[(size_t)q]);
+                    }
+            } else {
+                for (int r = 0; r < 2 * k; ++r, ++pat_at) {
+                    const int64_t sp = spep[2 * pat_at], ep = spep[2 * pat_at + 1];
+                    if (sp < 0) continue;
+                    for (int64_t q = sp; q <= ep; ++q) positions.push_back(sa[(size_t)q]);
+                }
+            }
+            std::sort(positions.begin(), positions.end());
+            positions.erase(std::unique(positions.begin(), positions.end()), positions.end());
+            if ((int64_t)positions.size() < p.min_copies || !p.allow_mismatches) continue;
+            // _find_tandems_fm_with_mismatches (bwt.py:2562-2695)
+            int64_t motif_len = k;
+            for (int64_t seed : positions) {
+                if (seen[(size_t)seed]) continue;
+                if (seed + motif_len > n) continue;
+                int64_t bs = -1, be = -1, bc = 0;
+                const int64_t shifts = std::min<int64_t>(motif_len, seed + 1);
+                for (int64_t sh = 0; sh < shifts; ++sh) {
+                    const int64_t cs = seed - sh;
+                    if (cs < 0 || cs + motif_len > n || seen[(size_t)cs]) continue;
+                    const size_t q = (size_t)((motif_len - 1) * n + cs);
+                    const int64_t s = es[q], e = ee[q], cc = ec[q];
+                    if (!(s <= seed && seed < e)) continue;
+                    if (cc > bc || (cc == bc && (bs < 0 || s < bs))) { bs = s; be = e; bc = cc; }
+                }
+                if (bs < 0) continue;
+                int64_t start = bs, end = be, copies = bc;
+                if (!(copies >= p.min_copies && end - start >= p.min_array_length)) continue;
+                std::string cons;
+                double mm = 0;
+                int64_t maxmm = 0;
+                if (!consensus_array(t, n, start, motif_len, copies, cons, mm, maxmm)) continue;
+                const int64_t prim = smallest_period(cons.data(), (int64_t)cons.size());
+                if (prim < (int64_t)cons.size()) {
+                    motif_len = prim;                    // persists for the later seeds (as in the reference)
+                    copies = std::max<int64_t>(1, (end - start) / motif_len);
+                    end = start + copies * motif_len;
+                    if (!consensus_array(t, n, start, motif_len, copies, cons, mm, maxmm)) continue;
+                }
+                std::string canon;
+                char strand = '+';
+                canonical_stranded(cons, canon, strand);
+                if (start > 0 && t[start - 1] == (uint8_t)cons[(size_t)motif_len - 1]) continue;   // _is_maximal_fm
+                if (end < n && t[end] == (uint8_t)cons[0]) continue;
+                const double pm = (1.0 - mm) * 100.0;
+                if (pm < (motif_len <= 6 ? 90.0 : 85.0)) continue;
+                Rec r;
+                r.chrom = chrom;
+                r.tier = 2;
+                r.start = start;
+                r.end = end;
+                r.length = end - start;
+                r.motif = cons;
+                r.copies = (double)copies;
+                r.confidence = std::max(0.5, 1.0 - mm);
+                r.mismatch_rate = mm;
+                r.max_mm = maxmm;
+                r.n_eval = copies;
+                r.strand = strand;
+                r.pmatch = pm;
+                r.pindel = 0.0;
+                r.score = trf_score(end - start, mm);
+                r.act_kind = ACT_FULL;
+                r.act_off = std::min(start, n);
+                r.act_len = std::max<int64_t>(0, std::min(end, n) - r.act_off);
+                // summarize_variations_array -> align_repeat_region(min_copies=1) (bwt.py:1259-1287)
+                if (align_repeat_region(seq.data(), n, start, end, cons, 1, summ) && summ.any_variation)
+                    r.variations = summ.variations;
+                out.push_back(std::move(r));
+                for (int64_t x = start; x < std::min(end, n); ++x) seen[(size_t)x] = 1;
+            }
+        }
+    }
+}
+
+}  // namespace bwtmi

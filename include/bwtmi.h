@@ -103,6 +103,25 @@ int64_t bwtmi_index_kmer_count(const bwtmi_index *idx);
 int bwtmi_index_get_kmer(const bwtmi_index *idx, int64_t *offsets, int32_t *positions);
 /* Kasai LCP over the index text (bwt.py:56-95, 2108-2116), int32[n] */
 int bwtmi_index_lcp(bwtmi_ctx *ctx, bwtmi_index *idx, int32_t *lcp);
+/* Library finders of Tier2LCPFinder over an index (not on the CLI path). */
+typedef struct {
+    int32_t min_period;        /* Tier2LCPFinder(min_period=1, max_period=1000, max_short_motif=9) */
+    int32_t max_period;
+    int32_t max_short_motif;
+    int32_t min_copies;        /* self.min_copies = 3 (bwt.py:1880) */
+    int32_t min_array_length;  /* 6 (bwt.py:1881) */
+    int32_t allow_mismatches;
+    double min_entropy;        /* 1.0 (bwt.py:1882) */
+} bwtmi_lib_params;
+/* _detect_lcp_plateaus over the index's Kasai LCP (bwt.py:2118-2145, 2500-2560):
+ * *out = (start, copies, period) triples in the reference's order (free with bwtmi_free) */
+int bwtmi_index_lcp_plateaus(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_lib_params *p, int64_t **out,
+                             int64_t *n);
+/* find_short_imperfect_repeats(chromosome, tier1_seen) (bwt.py:2027-2095, 2562-2825): the
+ * records are appended to job's final records with contig contig_id, whose sequence must be
+ * the index text; seen = nseen (start, end) pairs (tier1_seen) */
+int bwtmi_index_short_imperfect(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_lib_params *p,
+                                const int64_t *seen, int64_t nseen, bwtmi_job *job, int32_t contig_id);
 /* BWTCore.backward_search (bwt.py:359-389) for npat patterns packed in pats,
  * pattern p = pats[off[p] .. off[p+1]).  Writes sp_ep[2p], sp_ep[2p+1]
  * (inclusive interval, or -1,-1). */

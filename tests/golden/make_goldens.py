@@ -12,6 +12,8 @@ here is product code.  Outputs land in tests/golden/ as small data files:
   index         BWTCore arrays (SA, BWT, C, Occ, sampled SA, 8-mer hash),
                 Kasai LCP, backward_search / locate / get_kmer_positions
   motif         MotifUtils known answers
+  library       library finders off the CLI path: short imperfect repeats
+                (FM seeds + Hamming seed-and-extend), LCP plateaus, Tier 1
   hybrid        reference post-processing with the strict scan (and the
                 O(k^2) nested-suppression loop) swapped for the oracle's
                 restatements -> full-size output SHA-256; the
@@ -320,6 +322,78 @@ def cmd_motif(a):
         json.dump(out, f, indent=1)
 
 
+def _rec_json(r):
+    import dataclasses
+    d = dataclasses.asdict(r)
+    for k, v in list(d.items()):
+        if isinstance(v, np.generic):
+            d[k] = v.item()
+    return d
+
+
+def _crafted_short(seed: int, n_segments: int = 30) -> bytes:
+    """Random spacers + short imperfect arrays (units 2-9 bp, 3-13 copies,
+    transition-only substitutions at 4 %), most preceded by 'A' * (8 - k): the
+    reference's k-mer lookup for k < 8 returns positions of that padded
+    8-mer, so these arrays actually get seeded."""
+    r = np.random.default_rng(seed)
+    B = b"ACGT"
+    trans = {ord("A"): ord("G"), ord("G"): ord("A"), ord("C"): ord("T"), ord("T"): ord("C")}
+    out = bytearray()
+    for _ in range(n_segments):
+        out += bytes(B[i] for i in r.integers(0, 4, int(r.integers(10, 60))))
+        k = int(r.choice([2, 3, 4, 5, 6, 7, 8, 9]))
+        if r.random() < 0.6 and k < 8:
+            out += b"A" * (8 - k)
+        unit = bytes(B[i] for i in r.integers(0, 4, k))
+        arr = bytearray(unit * int(r.integers(3, 14)))
+        for q in range(len(arr)):
+            if r.random() < 0.04:
+                arr[q] = trans[arr[q]]
+        out += arr
+    return bytes(out)
+
+
+def cmd_library(a):
+    """Library finders that are not on the CLI path (SURVEY.md §8(a) A2-9, A2-10,
+    §8(f) #2): Tier2LCPFinder.find_short_imperfect_repeats (FM seeds + Hamming
+    seed-and-extend + majority vote), Tier2LCPFinder._detect_lcp_plateaus over
+    the Kasai LCP, Tier1STRFinder.find_strs -> library.json."""
+    ref = ref_module()
+    from bwtmi import synth
+    cases = {}
+    for name, n, idx, sub in [("imp3k", 3000, 501, 0.03), ("imp10k", 10000, 502, 0.03),
+                              ("imp2k_dense", 2000, 504, 0.05)]:
+        cases[name] = synth.generate_contig(n, idx, sub).decode()
+    for seed in (1, 2, 3):
+        cases[f"craft{seed}"] = _crafted_short(seed).decode()
+    with open(os.path.join(HERE, "inputs", "test2.fa")) as f:
+        cur = None
+        for line in f:
+            line = line.strip()
+            if line.startswith(">"):
+                cur = "test2_" + line[1:].split()[0]
+                cases[cur] = ""
+            elif cur:
+                cases[cur] += line.upper()
+    out = {}
+    for name, seq in cases.items():
+        t0 = time.time()
+        core = ref.BWTCore(seq + "$", 32)
+        f = ref.Tier2LCPFinder(core)
+        with contextlib.redirect_stdout(io.StringIO()):
+            short = f.find_short_imperfect_repeats(name, set())
+            lcp = f._compute_lcp_array()
+            plate = f._detect_lcp_plateaus(lcp, name)
+            t1 = ref.Tier1STRFinder(core.text_arr, 9, False).find_strs(name)
+        out[name] = dict(seq=seq, short_imperfect=[_rec_json(r) for r in short],
+                         lcp_plateaus=[_rec_json(r) for r in plate], tier1=[_rec_json(r) for r in t1],
+                         seconds=round(time.time() - t0, 1))
+        print(name, len(seq), len(short), len(plate), len(t1), out[name]["seconds"], flush=True)
+    with open(os.path.join(HERE, "library.json"), "w") as f:
+        json.dump(out, f, indent=0)
+
+
 def cmd_hybrid(a):
     """Full-size golden via the validated hybrid oracle."""
     ref = ref_module()
@@ -361,6 +435,7 @@ def main():
     sp.add_parser("rawhits")
     sp.add_parser("index")
     sp.add_parser("motif")
+    sp.add_parser("library")
     p = sp.add_parser("hybrid")
     p.add_argument("name")
     p.add_argument("--config")
@@ -373,7 +448,7 @@ def main():
     p.add_argument("--save-out", action="store_true")
     a = ap.parse_args()
     dict(fixtures=cmd_fixtures, rawhits=cmd_rawhits, index=cmd_index, motif=cmd_motif,
-         hybrid=cmd_hybrid)[a.cmd](a)
+         hybrid=cmd_hybrid, library=cmd_library)[a.cmd](a)
 
 
 if __name__ == "__main__":
