@@ -220,7 +220,8 @@ def short_imperfect(chrom: str, t: bytes, idx, min_period: int = 1, max_short_mo
     n = len(t)
     if n > 1_000_000:
         return out
-    _EXT_CACHE.clear()
+    _EXT_CACHE.clear()       # both caches are keyed by id(t): never reuse them across calls
+    _OCC.clear()
     seen = np.zeros(n + 1, dtype=bool)
     for s, e in tier1_seen:                        # `any(start <= p < end ...)` as a bitmap
         seen[max(0, s):max(0, min(n, e))] = True
