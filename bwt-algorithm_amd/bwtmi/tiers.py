@@ -57,7 +57,15 @@ class Tier1STRFinder:
         self.show_progress = show_progress
 
     def find_strs(self, chromosome: str) -> List[TandemRepeat]:
-        raise NotImplementedError("Tier1STRFinder.find_strs: SURVEY.md §8(f) next #2 (not built yet)")
+        """bwt.py:1426-1538: perfect 1-9 bp arrays, longest unit first, with the
+        reference's seen-mask and position step; stop positions are decided on
+        the device per unit length (library.hip), the walk itself on the host."""
+        from .records import Job
+        t = np.ascontiguousarray(self.text_arr, dtype=np.uint8)
+        job = Job()
+        job.add_contig(chromosome, t.tobytes(), 0, 0)
+        check(lib().bwtmi_job_tier1(_lib.ctx(), job.h, 0, int(self.max_motif_length)))
+        return list(job.records())
 
 
 class Tier2LCPFinder:

@@ -335,6 +335,21 @@ int bwtmi_index_short_imperfect(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_li
     });
 }
 
+int bwtmi_job_tier1(bwtmi_ctx *ctx, bwtmi_job *job, int32_t contig_id, int32_t max_motif_length) {
+    return guard([&] {
+        CHECK_ARG(ctx && job, "null argument");
+        CHECK_ARG(contig_id >= 0 && contig_id < (int32_t)job->j.contigs.size(), "bad contig id");
+        Ctx &c = ctx->c;
+        c.activate();
+        const std::string &full = job->j.contigs[(size_t)contig_id].full;
+        const int64_t n = (int64_t)full.size();
+        upload_text(c, c.slot[S_TEXT], (const uint8_t *)full.data(), n);
+        tier1_device(c, c.slot[S_TEXT].as<uint8_t>(), (const uint8_t *)full.data(), n, max_motif_length, contig_id,
+                     job->j.final_recs);
+        job->j.postprocessed = true;
+    });
+}
+
 // ------------------------------------------------------------ job
 int bwtmi_job_create(const bwtmi_params *params, bwtmi_job **out) {
     return guard([&] {

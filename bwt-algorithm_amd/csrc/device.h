@@ -196,6 +196,9 @@ void lcp_plateaus_device(Ctx &c, DeviceIndex *ix, const LibParams &p, std::vecto
 // to `out` with chrom = `chrom`; `seen` = (start, end) pairs already found (tier1_seen)
 void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const std::vector<int64_t> &seen,
                             int32_t chrom, std::vector<Rec> &out);
+// Tier1STRFinder.find_strs (bwt.py:1426-1538) over text t (host) / d_text (device copy, n bytes)
+void tier1_device(Ctx &c, const uint8_t *d_text, const uint8_t *t, int64_t n, int32_t max_motif_length,
+                  int32_t chrom, std::vector<Rec> &out);
 void index_backward_search(Ctx &c, DeviceIndex *, const uint8_t *pats, const int64_t *off, int64_t npat,
                            int64_t *sp_ep);
 

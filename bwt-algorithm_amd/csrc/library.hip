@@ -218,6 +218,59 @@ __global__ void k_extend(const uint8_t *__restrict__ t, int64_t n, int Lmax, int
     ovf[tid] = ok ? 0 : 1;
 }
 
+// -------------------------------------------------------------- Tier 1
+// Tier1STRFinder._find_simple_tandems_kmer (bwt.py:1426-1532), one unit length:
+// does the walk STOP at q (record a repeat) if it visits q?  Depends only on q
+// and the positions marked by longer units.  Copies are counted up to the
+// point where both length tests are settled (3 copies, and >= 10 bp when the
+// motif's entropy is < 1; the closest entropy to 1.0 among motifs <= 9 bp is
+// 0.009 away, so the device log2 cannot flip that test).
+__global__ void k_t1_flags(const uint8_t *__restrict__ t, int64_t n, int L, const uint8_t *__restrict__ seen,
+                           uint32_t *__restrict__ flag) {
+    const int64_t q = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (q >= n) return;
+    flag[q] = 0;
+    if (q >= n - L || seen[q]) return;                     // while i < n - motif_len; seen_mask[i]
+    uint8_t cnt[4] = {0, 0, 0, 0};
+    for (int p = 0; p < L; ++p) {
+        const uint8_t c = t[q + p];
+        const int b = c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : -1;
+        if (b < 0) return;                                 // motif with N / non-ACGT
+        ++cnt[b];
+    }
+    const int cap = max(3, (10 + L - 1) / L);
+    int copies = 1;
+    for (int64_t cp = q + L; copies < cap && cp + L <= n; cp += L) {
+        bool eq = true;
+        for (int p = 0; p < L && eq; ++p) eq = t[cp + p] == t[q + p];
+        if (!eq) break;
+        ++copies;
+    }
+    if (copies < 3) return;
+    const int length = copies * L;                         // exact unless capped (then >= 10)
+    double ent = 0.0;
+    for (int b = 0; b < 4; ++b)
+        if (cnt[b]) {
+            const double pr = (double)cnt[b] / (double)L;
+            ent -= pr * log2(pr);
+        }
+    if (ent < 1.0 && length < 10) return;
+    if (length < 6) return;
+    flag[q] = 1;
+}
+
+__global__ void k_t1_compact(const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos, int64_t n,
+                             int64_t *__restrict__ out) {
+    const int64_t q = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (q < n && flag[q]) out[pos[q]] = q;
+}
+
+__global__ void k_t1_mark(const int64_t *__restrict__ ranges, int64_t nr, uint8_t *__restrict__ seen) {
+    const int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (r >= nr) return;
+    for (int64_t x = ranges[2 * r]; x < ranges[2 * r + 1]; ++x) seen[x] = 1;
+}
+
 // --------------------------------------------------- host-side exact helpers
 // majority vote of n_copies copies from `start` (np.unique + argmax)
 static void majority(const uint8_t *t, int64_t n, int64_t start, int64_t L, int64_t n_copies, std::string &cons,
@@ -389,6 +442,77 @@ void lcp_plateaus_device(Ctx &c, DeviceIndex *ix, const LibParams &p, std::vecto
     out.resize((size_t)k32 * 3);
     HIPCHECK(hipMemcpyAsync(out.data(), c.slot[S_MISC2].p, (size_t)k32 * 24, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
+}
+
+void tier1_device(Ctx &c, const uint8_t *d_text, const uint8_t *t, int64_t n, int32_t max_motif_length,
+                  int32_t chrom, std::vector<Rec> &out) {
+    if (n <= 0) return;
+    hipStream_t st = c.stream;
+    const int64_t step = n > 10000000 ? 50 : (n > 5000000 ? 20 : 1);   // bwt.py:1440-1447
+    c.slot[S_MISC0].ensure((size_t)n + 64);
+    c.slot[S_MISC1].ensure((size_t)(n + 1) * 4);
+    c.slot[S_MISC2].ensure((size_t)(n + 1) * 4);
+    uint8_t *seen = c.slot[S_MISC0].as<uint8_t>();
+    uint32_t *flag = c.slot[S_MISC1].as<uint32_t>(), *pos = c.slot[S_MISC2].as<uint32_t>();
+    HIPCHECK(hipMemsetAsync(seen, 0, (size_t)n, st));
+    std::vector<int64_t> cand, ranges;
+    for (int L = std::min(max_motif_length, 9); L >= 1; --L) {   // longest unit first (bwt.py:1451)
+        hipLaunchKernelGGL(k_t1_flags, dim3(blocks(n)), dim3(kB), 0, st, d_text, n, L, seen, flag);
+        HIPCHECK(hipMemsetAsync(flag + n, 0, 4, st));
+        exclusive_scan<uint32_t>(c, flag, pos, n + 1);
+        uint32_t m = 0;
+        HIPCHECK(hipMemcpyAsync(&m, pos + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        if (m == 0) continue;
+        c.slot[S_MISC3].ensure((size_t)m * 8);
+        hipLaunchKernelGGL(k_t1_compact, dim3(blocks(n)), dim3(kB), 0, st, flag, pos, n, c.slot[S_MISC3].as<int64_t>());
+        HIPCHECK(hipGetLastError());
+        cand.resize(m);
+        HIPCHECK(hipMemcpyAsync(cand.data(), c.slot[S_MISC3].p, (size_t)m * 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        // the walk visits ptr, ptr + step, ... and stops at the first stopping position
+        ranges.clear();
+        int64_t ptr = 0;
+        for (int64_t q : cand) {
+            if (q < ptr || (q - ptr) % step) continue;
+            int64_t copies = 1, cp = q + L;
+            while (cp + L <= n && std::memcmp(t + cp, t + q, (size_t)L) == 0) {
+                ++copies;
+                cp += L;
+            }
+            const int64_t end = q + copies * L;
+            Rec r;
+            r.chrom = chrom;
+            r.tier = 1;
+            r.start = q;
+            r.end = end;
+            r.length = end - q;
+            r.motif.assign((const char *)t + q, (size_t)L);
+            r.copies = (double)copies;
+            r.confidence = 1.0;
+            r.mismatch_rate = 0.0;
+            r.max_mm = 0;
+            r.n_eval = copies;
+            r.strand = '+';
+            r.pmatch = 100.0;
+            r.pindel = 0.0;
+            r.score = trf_score(end - q, 0.0);
+            r.act_kind = ACT_FULL;
+            r.act_off = q;
+            r.act_len = end - q;
+            out.push_back(std::move(r));
+            ranges.push_back(q);
+            ranges.push_back(end);
+            ptr = end;
+        }
+        if (ranges.empty()) continue;
+        const int64_t nr = (int64_t)ranges.size() / 2;
+        c.slot[S_MISC3].ensure(ranges.size() * 8);
+        HIPCHECK(hipMemcpyAsync(c.slot[S_MISC3].p, ranges.data(), ranges.size() * 8, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_t1_mark, dim3(blocks(nr)), dim3(kB), 0, st, c.slot[S_MISC3].as<int64_t>(), nr, seen);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipStreamSynchronize(st));
+    }
 }
 
 void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const std::vector<int64_t> &seen_pairs,

@@ -122,6 +122,9 @@ int bwtmi_index_lcp_plateaus(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_lib_p
  * the index text; seen = nseen (start, end) pairs (tier1_seen) */
 int bwtmi_index_short_imperfect(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_lib_params *p,
                                 const int64_t *seen, int64_t nseen, bwtmi_job *job, int32_t contig_id);
+/* Tier1STRFinder(text_arr, max_motif_length).find_strs (bwt.py:1426-1538) over the full
+ * sequence of the job's contig contig_id; records appended to the job's final records */
+int bwtmi_job_tier1(bwtmi_ctx *ctx, bwtmi_job *job, int32_t contig_id, int32_t max_motif_length);
 /* BWTCore.backward_search (bwt.py:359-389) for npat patterns packed in pats,
  * pattern p = pats[off[p] .. off[p+1]).  Writes sp_ep[2p], sp_ep[2p+1]
  * (inclusive interval, or -1,-1). */

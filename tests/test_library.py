@@ -115,6 +115,28 @@ def test_device_short_imperfect_vs_oracle(gpu_ctx, seed):
 
 
 @pytest.mark.gpu
+def test_device_tier1_matches_reference(gpu_ctx, lib_golden):
+    from bwtmi.tiers import Tier1STRFinder
+    for name, case in lib_golden.items():
+        t = np.frombuffer(case["seq"].encode() + b"$", dtype=np.uint8)
+        got = _as_dicts(Tier1STRFinder(t, 9).find_strs(name))
+        _cmp(got, case["tier1"], DEV_FIELDS)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,mml", [(300_000, 9), (6_000_000, 9), (11_000_000, 6)])
+def test_device_tier1_vs_oracle(gpu_ctx, n, mml):
+    """Position step 1 / 20 / 50 regimes (n > 5 and > 10 Mbp, bwt.py:1440-1447)."""
+    from bwtmi import synth
+    from bwtmi.tiers import Tier1STRFinder
+    seq = synth.generate_contig(n, 900 + mml, 0.01)
+    want = olib.tier1_find_strs("c", seq, mml)
+    got = _as_dicts(Tier1STRFinder(np.frombuffer(seq, dtype=np.uint8), mml).find_strs("c"))
+    assert len(want) > 0
+    _cmp(got, want, DEV_FIELDS)
+
+
+@pytest.mark.gpu
 def test_device_lcp_plateaus_vs_oracle_100kbp(gpu_ctx):
     from bwtmi import synth
     seq = synth.generate_contig(100_000, 77, 0.01)
