@@ -128,17 +128,25 @@ def main():
     out_path = os.path.join(tempfile.gettempdir(), f"bwtmi_bench_{os.environ.get('MASTER_PORT', 'single')}.tab")
     dev = torch.device("cuda", local) if world > 1 else None
 
+    calls = {}
+
+    def timed(name, fn, *args):
+        t = time.perf_counter()
+        r = fn(*args)
+        calls[name] = calls.get(name, 0.0) + (time.perf_counter() - t) * 1e3
+        return r
+
     def step():
-        job.reset()
+        timed("reset", job.reset)
         job.select([rank])
-        job.scan(ctx)
-        job.postprocess()
+        timed("scan", job.scan, ctx)
+        timed("postprocess", job.postprocess)
         if world > 1:
             # each rank writes its own contig's rows at offsets from two
             # all-reduces of per-unit sizes (RCCL); no record leaves its GPU
-            dist.write_sharded(td, job, "strfinder", out_path, dev)
+            timed("write", dist.write_sharded, td, job, "strfinder", out_path, dev)
         else:
-            job.write("strfinder", out_path)     # repeat.tab, as the CLI writes it
+            timed("write", job.write, "strfinder", out_path)     # repeat.tab, as the CLI writes it
         return out_path
 
     def sync():
@@ -149,6 +157,7 @@ def main():
 
     for _ in range(a.warmup):
         step()
+    calls.clear()
     _lib.kernel_stats(ctx, enable=True, reset=True)
     sync()
     t0 = time.perf_counter()
@@ -215,6 +224,7 @@ def main():
         "kernels_ms_per_step": {k: round(v[0] / a.steps, 3) for k, v in sorted(kstats.items())},
         "h2d_upload_ms": round(upload_ms, 2),
         "fm_all_motifs_1_10": fm,
+        "calls_ms_per_step": {k: round(v / a.steps, 2) for k, v in calls.items()},
         "value_incl_upload": round(total_bp / 1e6 / (elapsed / a.steps + upload_ms / 1e3), 3),
     }
     print(json.dumps(line))
