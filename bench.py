@@ -147,6 +147,7 @@ def main():
             timed("write", dist.write_sharded, td, job, "strfinder", out_path, dev)
         else:
             timed("write", job.write, "strfinder", out_path)     # repeat.tab, as the CLI writes it
+        timed("index_wait", job.wait, ctx)    # the FM index build ran behind the host work
         return out_path
 
     def sync():

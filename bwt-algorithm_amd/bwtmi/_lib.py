@@ -78,6 +78,7 @@ _SIGS = {
     "bwtmi_job_add_contig": (C.c_int, [_P, C.c_char_p, _P, C.c_int64, C.c_int64, C.c_int64,
                                        C.POINTER(C.c_int32)]),
     "bwtmi_job_scan": (C.c_int, [_P, _P]),
+    "bwtmi_job_wait": (C.c_int, [_P, _P]),
     "bwtmi_job_upload": (C.c_int, [_P, _P]),
     "bwtmi_job_reset": (C.c_int, [_P]),
     "bwtmi_job_set_params": (C.c_int, [_P, C.POINTER(Params)]),

@@ -140,6 +140,8 @@ def run_sharded(finder, job, scan_fn: Optional[Callable] = None):
     else:
         job.scan(_lib.ctx(int(os.environ.get("LOCAL_RANK", "0"))))
     job.postprocess()
+    if scan_fn is None:
+        job.wait(_lib.ctx(int(os.environ.get("LOCAL_RANK", "0"))))
     blob = job.export()
     device = torch.device("cuda", torch.cuda.current_device()) if td.get_backend() == "nccl" else "cpu"
     blobs = gather_bytes(td, blob, device)

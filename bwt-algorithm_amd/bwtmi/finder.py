@@ -98,6 +98,7 @@ class TandemRepeatFinder:
             return dist.run_sharded(self, job)
         job.scan(_lib.ctx(self.device))
         job.postprocess()
+        job.wait(_lib.ctx(self.device))     # the worker's FM index build ran behind post-processing
         return job.records()
 
     def find_and_write_sharded(self, enable_tier2: bool, output_file: str, format_type: str) -> int:
@@ -126,6 +127,7 @@ class TandemRepeatFinder:
             device = torch.device("cuda", torch.cuda.current_device())
         total = int(dist._allreduce_sum(td, np.array([job.count()], dtype=np.int64), device)[0])
         dist.write_sharded(td, job, format_type, output_file, device)
+        job.wait(_lib.ctx(self.device))
         return total
 
     def find_tandem_repeats(self, enable_tier1: bool = True, enable_tier2: bool = True,

@@ -147,6 +147,10 @@ class Job:
     def scan(self, dev_ctx) -> None:
         check(lib().bwtmi_job_scan(dev_ctx, self.h))
 
+    def wait(self, dev_ctx) -> None:
+        """Join the background FM index builds started by scan()."""
+        check(lib().bwtmi_job_wait(dev_ctx, self.h))
+
     def reset(self) -> None:
         check(lib().bwtmi_job_reset(self.h))
 

@@ -65,7 +65,15 @@ struct DevContig {
 struct JobDev {
     int device = -1;
     std::vector<DevContig> seqs;
+    Ctx *bg_ctx = nullptr;   // context whose background work reads these buffers (cleared by its join)
 };
+
+// every entry point that touches a context: join its background work, select the device
+static Ctx &use(Ctx &c) {
+    ctx_wait(c);
+    c.activate();
+    return c;
+}
 
 // parts[k] lands at byte offset at[k] of `path`, in parallel (page-cache copies)
 static void pwrite_parts(const char *path, bool truncate, const std::vector<std::string> &parts,
@@ -148,6 +156,7 @@ int bwtmi_open(int device, bwtmi_ctx **out) {
 int bwtmi_close(bwtmi_ctx *ctx) {
     return guard([&] {
         if (!ctx) return;
+        ctx_join(ctx->c);   // a background error dies with the context
         ctx->c.activate();
         (void)hipStreamSynchronize(ctx->c.stream);
         if (ctx->c.scratch_index) index_free(ctx->c.scratch_index);
@@ -163,6 +172,7 @@ int bwtmi_close(bwtmi_ctx *ctx) {
 int bwtmi_last_timing(bwtmi_ctx *ctx, double *out3) {
     return guard([&] {
         CHECK_ARG(ctx && out3, "null argument");
+        ctx_wait(ctx->c);
         out3[0] = ctx->c.last_total_ms;
         out3[1] = ctx->c.last_dom_ms;
         out3[2] = ctx->c.last_dom_launches;
@@ -173,6 +183,7 @@ int bwtmi_kernel_stats(bwtmi_ctx *ctx, int enable, int reset, char *out, int64_t
     return guard([&] {
         CHECK_ARG(ctx, "null ctx");
         Ctx &c = ctx->c;
+        ctx_wait(c);
         std::string s;
         char line[160];
         for (auto &k : c.kstats) {
@@ -206,7 +217,7 @@ int bwtmi_strict_scan(bwtmi_ctx *ctx, const uint8_t *seq, int64_t n, int32_t min
         *nhits = 0;
         if (n > 0 && seq[n - 1] == '$') --n;   // bwt.py:1915-1916
         Ctx &c = ctx->c;
-        c.activate();
+        use(c);
         upload_text(c, c.slot[S_TEXT], seq, n);
         ScanResult r;
         strict_scan_device(c, c.slot[S_TEXT].as<uint8_t>(), n, min_unit, max_unit, min_copies, r);
@@ -225,7 +236,7 @@ int bwtmi_index_build(bwtmi_ctx *ctx, const uint8_t *text, int64_t n, int32_t sa
         CHECK_ARG(ctx && out && (text || n == 0) && n >= 0 && sa_sample > 0 && occ_sample > 0, "bad argument");
         *out = nullptr;
         Ctx &c = ctx->c;
-        c.activate();
+        use(c);
         upload_text(c, c.slot[S_TEXT], text, n);
         auto *idx = new bwtmi_index();
         idx->ctx = ctx;
@@ -242,7 +253,7 @@ int bwtmi_index_build(bwtmi_ctx *ctx, const uint8_t *text, int64_t n, int32_t sa
 int bwtmi_index_free(bwtmi_index *idx) {
     return guard([&] {
         if (!idx) return;
-        idx->ctx->c.activate();
+        use(idx->ctx->c);
         index_free(idx->d);
         delete idx;
     });
@@ -254,30 +265,30 @@ int64_t bwtmi_index_sampled_len(const bwtmi_index *idx) { return idx ? index_sam
 int64_t bwtmi_index_kmer_count(const bwtmi_index *idx) { return idx ? index_kmer_count(idx->d) : -1; }
 
 int bwtmi_index_get_sa(const bwtmi_index *idx, int32_t *sa) {
-    return guard([&] { CHECK_ARG(idx && sa, "null"); index_get_sa(idx->ctx->c, idx->d, sa); });
+    return guard([&] { CHECK_ARG(idx && sa, "null"); index_get_sa(use(idx->ctx->c), idx->d, sa); });
 }
 int bwtmi_index_get_bwt(const bwtmi_index *idx, uint8_t *bwt) {
-    return guard([&] { CHECK_ARG(idx && bwt, "null"); index_get_bwt(idx->ctx->c, idx->d, bwt); });
+    return guard([&] { CHECK_ARG(idx && bwt, "null"); index_get_bwt(use(idx->ctx->c), idx->d, bwt); });
 }
 int bwtmi_index_get_counts(const bwtmi_index *idx, int64_t *totals, int64_t *C) {
     return guard([&] { CHECK_ARG(idx && totals && C, "null"); index_get_counts(idx->d, totals, C); });
 }
 int bwtmi_index_get_occ(const bwtmi_index *idx, uint8_t code, int32_t *cp) {
-    return guard([&] { CHECK_ARG(idx && cp, "null"); index_get_occ(idx->ctx->c, idx->d, code, cp); });
+    return guard([&] { CHECK_ARG(idx && cp, "null"); index_get_occ(use(idx->ctx->c), idx->d, code, cp); });
 }
 int bwtmi_index_get_sampled(const bwtmi_index *idx, int32_t *vals) {
-    return guard([&] { CHECK_ARG(idx && vals, "null"); index_get_sampled(idx->ctx->c, idx->d, vals); });
+    return guard([&] { CHECK_ARG(idx && vals, "null"); index_get_sampled(use(idx->ctx->c), idx->d, vals); });
 }
 int bwtmi_index_get_kmer(const bwtmi_index *idx, int64_t *offsets, int32_t *positions) {
     return guard([&] {
         CHECK_ARG(idx && offsets && positions, "null");
-        index_get_kmer(idx->ctx->c, idx->d, offsets, positions);
+        index_get_kmer(use(idx->ctx->c), idx->d, offsets, positions);
     });
 }
 int bwtmi_index_lcp(bwtmi_ctx *ctx, bwtmi_index *idx, int32_t *lcp) {
     return guard([&] {
         CHECK_ARG(ctx && idx && lcp, "null");
-        ctx->c.activate();
+        use(ctx->c);
         index_lcp(ctx->c, idx->d, lcp);
     });
 }
@@ -285,7 +296,7 @@ int bwtmi_backward_search_batch(bwtmi_ctx *ctx, bwtmi_index *idx, const uint8_t 
                                 int64_t npat, int64_t *sp_ep) {
     return guard([&] {
         CHECK_ARG(ctx && idx && off && sp_ep && npat >= 0, "bad argument");
-        ctx->c.activate();
+        use(ctx->c);
         index_backward_search(ctx->c, idx->d, pats, off, npat, sp_ep);
     });
 }
@@ -310,7 +321,7 @@ int bwtmi_index_lcp_plateaus(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_lib_p
         CHECK_ARG(ctx && idx && out && n, "null argument");
         *out = nullptr;
         *n = 0;
-        ctx->c.activate();
+        use(ctx->c);
         std::vector<int64_t> v;
         lcp_plateaus_device(ctx->c, idx->d, lib_params(p), v);
         auto *o = (int64_t *)std::malloc(std::max<size_t>(1, v.size()) * sizeof(int64_t));
@@ -328,7 +339,7 @@ int bwtmi_index_short_imperfect(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_li
         CHECK_ARG(contig_id >= 0 && contig_id < (int32_t)job->j.contigs.size(), "bad contig id");
         CHECK_ARG((int64_t)job->j.contigs[(size_t)contig_id].full.size() == index_n(idx->d),
                   "the job contig must hold the index text");
-        ctx->c.activate();
+        use(ctx->c);
         std::vector<int64_t> sp(seen, seen + 2 * nseen);
         short_imperfect_device(ctx->c, idx->d, lib_params(p), sp, contig_id, job->j.final_recs);
         job->j.postprocessed = true;
@@ -340,7 +351,7 @@ int bwtmi_job_tier1(bwtmi_ctx *ctx, bwtmi_job *job, int32_t contig_id, int32_t m
         CHECK_ARG(ctx && job, "null argument");
         CHECK_ARG(contig_id >= 0 && contig_id < (int32_t)job->j.contigs.size(), "bad contig id");
         Ctx &c = ctx->c;
-        c.activate();
+        use(c);
         const std::string &full = job->j.contigs[(size_t)contig_id].full;
         const int64_t n = (int64_t)full.size();
         upload_text(c, c.slot[S_TEXT], (const uint8_t *)full.data(), n);
@@ -364,6 +375,7 @@ int bwtmi_job_create(const bwtmi_params *params, bwtmi_job **out) {
 int bwtmi_job_free(bwtmi_job *job) {
     return guard([&] {
         if (!job) return;
+        if (job->dev.bg_ctx) ctx_join(*job->dev.bg_ctx);   // its error stays for the ctx's next call
         if (job->dev.device >= 0) (void)hipSetDevice(job->dev.device);
         for (auto &d : job->dev.seqs) d.buf.release();
         delete job;
@@ -419,7 +431,8 @@ int bwtmi_job_contig_seq(const bwtmi_job *job, int32_t id, uint8_t *dst) {
 
 static void job_upload(bwtmi_ctx *ctx, bwtmi_job *job) {
     Ctx &c = ctx->c;
-    c.activate();
+    if (job->dev.bg_ctx && job->dev.bg_ctx != &c) ctx_wait(*job->dev.bg_ctx);
+    use(c);
     JobDev &d = job->dev;
     if (d.device >= 0 && d.device != c.device) {
         for (auto &s : d.seqs) s.buf.release();
@@ -494,25 +507,12 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
         J.final_recs.clear();
         J.postprocessed = false;
         const bwtmi_params &P = J.params;
-        double idx_ms = 0;
+        std::vector<std::pair<const uint8_t *, int64_t>> to_index;
         for (size_t i = 0; i < J.contigs.size(); ++i) {
             const Contig &ct = J.contigs[i];
             const int64_t len = ct.trimmed_len();
             if (!J.selected.empty() && !J.selected[i]) continue;   // another rank's shard
-            if (P.build_index) {   // BWTCore(seq + '$') of the worker (bwt.py:3053-3054)
-                auto ti = std::chrono::steady_clock::now();
-                DevContig &dc = job->dev.seqs[i];
-                // (S_CAND_K2 is free until the scan; index_build_device uses the MISC/IDX slots)
-                DBuf &tb = c.slot[S_CAND_K2];
-                tb.ensure((size_t)len + 1 + 128);
-                HIPCHECK(hipMemcpyAsync(tb.p, dc.buf.p, (size_t)len, hipMemcpyDeviceToDevice, c.stream));
-                HIPCHECK(hipMemsetAsync(tb.as<uint8_t>() + len, '$', 1, c.stream));
-                HIPCHECK(hipMemsetAsync(tb.as<uint8_t>() + len + 1, 0, 127, c.stream));
-                // the worker never consumes it; its buffers are kept for the next build
-                c.scratch_index = index_build_device(c, tb.as<uint8_t>(), len + 1, P.sa_sample, 128, 0u,
-                                                     c.scratch_index);
-                idx_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ti).count();
-            }
+            if (P.build_index) to_index.push_back({job->dev.seqs[i].buf.as<uint8_t>(), len});
             if (!P.tier2) continue;                                  // bwt.py:3068
             if (len > 50000000 && !P.show_progress) continue;        // bwt.py:3070
             if (P.min_copies <= 0) continue;                         // worker raises -> [] (bwt.py:3137)
@@ -525,7 +525,53 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
             J.raw_n[i] = r.raw;
         }
         J.stage_ms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        J.stage_ms[1] = idx_ms;
+        J.stage_ms[1] = 0;
+        if (to_index.empty()) return;
+        // BWTCore(seq + '$') of the worker (bwt.py:3053-3054). The worker never consumes
+        // it, so the builds run on a background thread behind the host
+        // post-processing; every later use of this ctx (or of this job's device
+        // buffers) joins them first. The scratch index keeps its buffers between builds.
+        const int32_t sa_sample = P.sa_sample;
+        c.bg_ms = 0;
+        job->dev.bg_ctx = &c;
+        c.bg_link = &job->dev.bg_ctx;
+        c.bg = std::thread([&c, sa_sample, to_index] {
+            auto ti = std::chrono::steady_clock::now();
+            try {
+                c.activate();
+                for (const auto &tx : to_index) {
+                    const int64_t len = tx.second;
+                    // (S_CAND_K2 is free after the scan; index_build_device uses the MISC/IDX slots)
+                    DBuf &tb = c.slot[S_CAND_K2];
+                    tb.ensure((size_t)len + 1 + 128);
+                    HIPCHECK(hipMemcpyAsync(tb.p, tx.first, (size_t)len, hipMemcpyDeviceToDevice, c.stream));
+                    HIPCHECK(hipMemsetAsync(tb.as<uint8_t>() + len, '$', 1, c.stream));
+                    HIPCHECK(hipMemsetAsync(tb.as<uint8_t>() + len + 1, 0, 127, c.stream));
+                    c.scratch_index = index_build_device(c, tb.as<uint8_t>(), len + 1, sa_sample, 128, 0u,
+                                                         c.scratch_index);
+                }
+                HIPCHECK(hipStreamSynchronize(c.stream));
+            } catch (const Error &e) {
+                c.bg_code = e.code;
+                c.bg_err = "background index build: " + g_err;
+            } catch (const std::bad_alloc &) {
+                c.bg_code = BWTMI_E_NOMEM;
+                c.bg_err = "background index build: out of host memory";
+            } catch (const std::exception &e) {
+                c.bg_code = BWTMI_E_STATE;
+                c.bg_err = std::string("background index build: ") + e.what();
+            }
+            c.bg_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ti).count();
+        });
+    });
+}
+
+int bwtmi_job_wait(bwtmi_ctx *ctx, bwtmi_job *job) {
+    return guard([&] {
+        CHECK_ARG(ctx && job, "null argument");
+        const bool ran = ctx->c.bg.joinable();
+        ctx_wait(ctx->c);
+        if (ran) job->j.stage_ms[1] = ctx->c.bg_ms;
     });
 }
 

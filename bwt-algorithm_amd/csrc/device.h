@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -130,6 +131,13 @@ struct Ctx {
     DBuf slot[S_NSLOTS];
     HBuf host[4];
     struct DeviceIndex *scratch_index = nullptr;   // reused by the worker-path index builds
+    // device work that runs behind host work (the worker-path index builds):
+    // every entry point that uses this context joins it first (ctx_wait)
+    std::thread bg;
+    int bg_code = 0;
+    std::string bg_err;
+    double bg_ms = 0;                 // wall time of the last background index builds
+    Ctx **bg_link = nullptr;          // the job field naming this ctx while bg reads its buffers
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_total_ms = 0, last_dom_ms = 0;
     int last_dom_launches = 0;
@@ -137,6 +145,21 @@ struct Ctx {
     bool timing = true;
     void activate() const { HIPCHECK(hipSetDevice(device)); }
 };
+
+// join the context's background device work; rethrows its error
+inline void ctx_join(Ctx &c) {
+    if (c.bg.joinable()) c.bg.join();
+    if (c.bg_link) *c.bg_link = nullptr;
+    c.bg_link = nullptr;
+}
+inline void ctx_wait(Ctx &c) {
+    ctx_join(c);
+    if (c.bg_code) {
+        const int code = c.bg_code;
+        c.bg_code = 0;
+        fail(code, "%s", c.bg_err.c_str());
+    }
+}
 
 // ----- primitives (radix.hip)
 template <class T>

@@ -163,6 +163,10 @@ int bwtmi_job_add_contig(bwtmi_job *job, const char *name, const uint8_t *full, 
  * gates, Rule-1 filter) -- equivalent to find_tandem_repeats(_parallel) up to
  * all_repeats (bwt.py:3792-3822, 3850-3915) */
 int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job);
+/* the FM index builds of bwtmi_job_scan (build_index) run on the device behind
+ * the host post-processing; this joins them (every other call on ctx, and
+ * bwtmi_job_free, joins them too) and returns their error, if any */
+int bwtmi_job_wait(bwtmi_ctx *ctx, bwtmi_job *job);
 /* copy every contig to device memory now (bwtmi_job_scan does it on first use);
  * later scans reuse the resident copies */
 int bwtmi_job_upload(bwtmi_ctx *ctx, bwtmi_job *job);
