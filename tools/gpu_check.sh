@@ -7,8 +7,9 @@ TAG=${1:-run}; shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -x -q "$@" > "$OUT/pytest_gpu.log" 2>&1 || { echo PYTEST_FAIL; tail -30 "$OUT/pytest_gpu.log"; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > "$OUT/pytest_gpu.log" 2>&1 || { echo PYTEST_FAIL; tail -30 "$OUT/pytest_gpu.log"; exit 1; }
 tail -2 "$OUT/pytest_gpu.log"
+timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { echo SMOKE_FAIL; tail -20 "$OUT/smoke.log"; exit 1; }
 timeout -k 10 600 python bench.py --steps 3 --warmup 1 --stages > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo BENCH_FAIL; tail -20 "$OUT/bench.err"; exit 1; }
 cat "$OUT/bench.json"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/bench_prof.json" 2> "$OUT/prof_stderr.log" || { echo PROF_FAIL; exit 1; }
