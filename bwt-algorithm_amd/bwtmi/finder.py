@@ -81,13 +81,13 @@ class TandemRepeatFinder:
         print()
 
     # ------------------------------------------------------------------ search
-    def _run(self, enable_tier2: bool, enable_tier3: bool, long_reads) -> RepeatList:
-        if enable_tier3 and long_reads:
-            raise NotImplementedError("Tier 3 long-read anchoring is not built yet (SURVEY.md §8(f) #3)")
+    def _run(self, enable_tier2: bool, enable_tier3: bool, long_reads, parallel: bool = True) -> RepeatList:
         if self.job is None:
             self.load_reference()
         job = self.job
         job.reset()
+        if parallel and enable_tier3 and long_reads:
+            self._tier3(job, long_reads)
         if self.min_copies == 0 and enable_tier2:
             # the reference worker raises ZeroDivisionError and returns [] (bwt.py:3095, 3137-3141)
             for name in job.names:
@@ -100,6 +100,18 @@ class TandemRepeatFinder:
         job.postprocess()
         job.wait(_lib.ctx(self.device))     # the worker's FM index build ran behind post-processing
         return job.records()
+
+    def _tier3(self, job, long_reads) -> None:
+        """Tier 3 (bwt.py:3917-3924, parallel mode only): every built index
+        anchors the long reads; the records join that contig's strict hits
+        ahead of nested suppression (bwtmi_index_tier3 as_input=1)."""
+        from .tiers import Tier3LongReadFinder
+        print("\nTier 3 processing (serial)...")
+        ids = {name: i for i, name in enumerate(job.names)}   # load_reference: the last duplicate wins
+        for chrom, core in self.bwt_cores.items():
+            if chrom not in ids:
+                raise KeyError(f"Tier 3: index {chrom!r} has no loaded sequence")
+            Tier3LongReadFinder(core, show_progress=self.show_progress)._run(long_reads, job, ids[chrom], True)
 
     def find_and_write_sharded(self, enable_tier2: bool, output_file: str, format_type: str) -> int:
         """Multi-GPU CLI path: every rank scans and post-processes its own fold
@@ -132,7 +144,7 @@ class TandemRepeatFinder:
 
     def find_tandem_repeats(self, enable_tier1: bool = True, enable_tier2: bool = True,
                             enable_tier3: bool = False, long_reads: Optional[List[str]] = None) -> RepeatList:
-        res = self._run(enable_tier2, enable_tier3, long_reads)
+        res = self._run(enable_tier2, enable_tier3, long_reads, parallel=False)   # no Tier 3 (bwt.py:3792-3848)
         print(f"Analysis complete! Found {len(res)} total repeats.")
         return res
 

@@ -261,7 +261,7 @@ class RepeatList(Sequence):
         n = job.count()
         self._n = n
         self._ints = np.zeros((max(n, 1), 9), dtype=np.int64)
-        self._dbls = np.zeros((max(n, 1), 3), dtype=np.float64)
+        self._dbls = np.zeros((max(n, 1), 5), dtype=np.float64)
         if n:
             check(lib().bwtmi_job_get_records(job.h, self._ints.ctypes.data_as(C.c_void_p),
                                               self._dbls.ctypes.data_as(C.c_void_p)))
@@ -279,17 +279,23 @@ class RepeatList(Sequence):
             raise IndexError(i)
         r = self._cache.get(i)
         if r is None:
-            s, e, ln, tier, neval, maxmm, _, _, chrom = self._ints[i].tolist()
-            copies, mm, conf = self._dbls[i].tolist()
+            s, e, ln, tier, neval, maxmm, score, flags, chrom = self._ints[i].tolist()
+            copies, mm, conf, pmatch, pindel = self._dbls[i].tolist()
             motif = self.job._string(i, 0)
             var = self.job._string(i, 2)
+            act = self.job._string(i, 3)
+            if flags & 1:      # a bare consolidated Tier 3 call (bwt.py:3021-3030)
+                cons, comp, ent = None, None, 0.0
+            elif flags & 2:    # compound-stage k-mer piece (bwt.py:3980-3987)
+                cons, comp, ent = motif, {"A": 0, "C": 0, "G": 0, "T": 0}, 1.5
+            else:
+                cons, comp, ent = motif, _composition(motif), _entropy(motif)
             r = TandemRepeat(chrom=self.job.names[chrom], start=s, end=e, motif=motif, copies=copies,
-                             length=ln, tier=tier, confidence=conf, consensus_motif=motif,
+                             length=ln, tier=tier, confidence=conf, consensus_motif=cons,
                              mismatch_rate=mm, max_mismatches_per_copy=maxmm,
                              n_copies_evaluated=neval, strand=self.job._string(i, 4),
-                             percent_matches=max(0.0, 100.0 - mm * 100.0),
-                             composition=_composition(motif), entropy=_entropy(motif),
-                             actual_sequence=self.job._string(i, 3),
+                             percent_matches=pmatch, percent_indels=pindel, score=score,
+                             composition=comp, entropy=ent, actual_sequence=act if act else None,
                              variations=var.split(";") if var else None)
             self._cache[i] = r
         return r

@@ -158,10 +158,38 @@ class Tier2LCPFinder:
                                   "bwt.py:2236-2257)")
 
 
+def pack_reads(long_reads) -> Tuple[np.ndarray, np.ndarray]:
+    """Reads (str or bytes) back to back + int64 offsets[n + 1]."""
+    bs = [r if isinstance(r, (bytes, bytearray)) else r.encode("latin-1", errors="replace") for r in long_reads]
+    off = np.zeros(len(bs) + 1, dtype=np.int64)
+    if bs:
+        off[1:] = np.cumsum([len(b) for b in bs])
+    blob = np.frombuffer(b"".join(bs), dtype=np.uint8) if off[-1] else np.zeros(1, dtype=np.uint8)
+    return np.ascontiguousarray(blob), off
+
+
 class Tier3LongReadFinder:
+    """bwt.py:2828-3036 -- long-read anchoring.  The window periodicity scan
+    (500-byte windows every 100 bytes, periods 10..165) and the anchor lookups
+    (backward search + SA of the 50-byte anchors) run on the device over the
+    core's index; records are built and consolidated natively (library.hip)."""
+
     def __init__(self, bwt_core, show_progress: bool = False):
         self.bwt = bwt_core
+        self.min_read_length = 1000  # bwt.py:2833
+        self.min_span_length = 100   # bwt.py:2834 (unused by the reference too)
         self.show_progress = show_progress
 
-    def find_very_long_repeats(self, long_reads: List[str], chromosome: str):
-        raise NotImplementedError("Tier 3 long-read anchoring: SURVEY.md §8(f) next #3 (not built yet)")
+    def _run(self, long_reads, job, contig_id: int, as_input: bool) -> None:
+        blob, off = pack_reads(long_reads)
+        check(lib().bwtmi_index_tier3(self.bwt._ctx, self.bwt._h, blob.ctypes.data_as(C.c_void_p),
+                                      off.ctypes.data_as(C.c_void_p), len(off) - 1, job.h, contig_id,
+                                      int(as_input)))
+
+    def find_very_long_repeats(self, long_reads: List[str], chromosome: str) -> List[TandemRepeat]:
+        from .records import Job
+        t = np.ascontiguousarray(self.bwt.text_arr, dtype=np.uint8)
+        job = Job()
+        job.add_contig(chromosome, t.tobytes(), 0, 0)
+        self._run(long_reads, job, 0, False)
+        return list(job.records())

@@ -346,6 +346,30 @@ int bwtmi_index_short_imperfect(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_li
     });
 }
 
+int bwtmi_index_tier3(bwtmi_ctx *ctx, bwtmi_index *idx, const uint8_t *reads, const int64_t *read_off,
+                      int64_t nreads, bwtmi_job *job, int32_t contig_id, int32_t as_input) {
+    return guard([&] {
+        CHECK_ARG(ctx && idx && job && nreads >= 0 && (read_off || nreads == 0), "bad argument");
+        CHECK_ARG(contig_id >= 0 && contig_id < (int32_t)job->j.contigs.size(), "bad contig id");
+        if (nreads > 0) {
+            CHECK_ARG(read_off[0] == 0 && (reads || read_off[nreads] == 0), "bad read offsets");
+            for (int64_t r = 0; r < nreads; ++r) CHECK_ARG(read_off[r + 1] >= read_off[r], "bad read offsets");
+        }
+        use(ctx->c);
+        std::vector<Rec> recs;
+        tier3_device(ctx->c, idx->d, reads, read_off, nreads, contig_id, recs);
+        Job &J = job->j;
+        if (as_input) {
+            if (J.t3.size() < J.contigs.size()) J.t3.resize(J.contigs.size());
+            auto &dst = J.t3[(size_t)contig_id];
+            for (auto &r : recs) dst.push_back(std::move(r));
+        } else {
+            for (auto &r : recs) J.final_recs.push_back(std::move(r));
+            J.postprocessed = true;
+        }
+    });
+}
+
 int bwtmi_job_tier1(bwtmi_ctx *ctx, bwtmi_job *job, int32_t contig_id, int32_t max_motif_length) {
     return guard([&] {
         CHECK_ARG(ctx && job, "null argument");
@@ -465,6 +489,7 @@ int bwtmi_job_reset(bwtmi_job *job) {
         job->j.screened.clear();
         job->j.raw_n.clear();
         job->j.final_recs.clear();
+        job->j.t3.clear();
         job->j.postprocessed = false;
     });
 }
@@ -517,9 +542,11 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
             if (len > 50000000 && !P.show_progress) continue;        // bwt.py:3070
             if (P.min_copies <= 0) continue;                         // worker raises -> [] (bwt.py:3137)
             const int64_t U = std::max<int64_t>(P.max_unit_len, std::min<int64_t>(len / P.min_copies, 1000));
+            // a contig with Tier 3 records is screened on the host, together with them
+            const bool t3 = i < J.t3.size() && !J.t3[i].empty();
             ScanResult r;
             strict_scan_device(c, job->dev.seqs[i].buf.as<uint8_t>(), len, 1, (int32_t)std::min<int64_t>(U, INT32_MAX),
-                               P.min_copies, r, screen);
+                               P.min_copies, r, screen && !t3);
             J.hits[i].swap(r.hits);   // Rule 1 (bwt.py:3118-3130) never fires on strict hits
             J.screened[i] = r.screened ? 1 : 0;
             J.raw_n[i] = r.raw;
@@ -685,16 +712,16 @@ int bwtmi_job_write_units(bwtmi_job *job, const char *path, const int64_t *offse
     });
 }
 
-int bwtmi_job_get_records(bwtmi_job *job, int64_t *ints9, double *dbls3) {
+int bwtmi_job_get_records(bwtmi_job *job, int64_t *ints9, double *dbls5) {
     return guard([&] {
-        CHECK_ARG(job && ints9 && dbls3, "null argument");
+        CHECK_ARG(job && ints9 && dbls5, "null argument");
         size_t k = 0;
         for (const Rec &r : job->j.final_recs) {
             int64_t *I = ints9 + 9 * k;
-            double *D = dbls3 + 3 * k;
+            double *D = dbls5 + 5 * k;
             I[0] = r.start; I[1] = r.end; I[2] = r.length; I[3] = r.tier; I[4] = r.n_eval; I[5] = r.max_mm;
-            I[6] = (int64_t)r.motif.size(); I[7] = (int64_t)r.motif.size(); I[8] = r.chrom;
-            D[0] = r.copies; D[1] = r.mismatch_rate; D[2] = r.confidence;
+            I[6] = r.score; I[7] = (r.stats_none ? 1 : 0) | (r.kmer_stats ? 2 : 0); I[8] = r.chrom;
+            D[0] = r.copies; D[1] = r.mismatch_rate; D[2] = r.confidence; D[3] = r.pmatch; D[4] = r.pindel;
             ++k;
         }
     });
@@ -727,7 +754,7 @@ struct WireRec {
     int32_t chrom, tier;
     int64_t start, end, length, max_mm, n_eval, score, act_off, act_len;
     double copies, confidence, mismatch_rate, pmatch, pindel;
-    int8_t act_kind, strand, is_compound, kmer_stats;
+    int8_t act_kind, strand, is_compound, kmer_stats, stats_none;
     int32_t motif_len, var_len;
 };
 
@@ -743,7 +770,7 @@ int bwtmi_job_export(bwtmi_job *job, uint8_t **buf, int64_t *len) {
             w.max_mm = r.max_mm; w.n_eval = r.n_eval; w.score = r.score; w.act_off = r.act_off; w.act_len = r.act_len;
             w.copies = r.copies; w.confidence = r.confidence; w.mismatch_rate = r.mismatch_rate;
             w.pmatch = r.pmatch; w.pindel = r.pindel; w.act_kind = r.act_kind; w.strand = r.strand;
-            w.is_compound = r.is_compound; w.kmer_stats = r.kmer_stats;
+            w.is_compound = r.is_compound; w.kmer_stats = r.kmer_stats; w.stats_none = r.stats_none;
             w.motif_len = (int32_t)r.motif.size(); w.var_len = (int32_t)r.variations.size();
             s.append((const char *)&w, sizeof w);
             s.append(r.motif);
@@ -775,7 +802,7 @@ int bwtmi_job_import(bwtmi_job *job, const uint8_t *buf, int64_t len) {
             r.max_mm = w.max_mm; r.n_eval = w.n_eval; r.score = w.score; r.act_off = w.act_off; r.act_len = w.act_len;
             r.copies = w.copies; r.confidence = w.confidence; r.mismatch_rate = w.mismatch_rate;
             r.pmatch = w.pmatch; r.pindel = w.pindel; r.act_kind = w.act_kind; r.strand = (char)w.strand;
-            r.is_compound = w.is_compound; r.kmer_stats = w.kmer_stats;
+            r.is_compound = w.is_compound; r.kmer_stats = w.kmer_stats; r.stats_none = w.stats_none;
             r.motif.assign((const char *)buf + o, (size_t)w.motif_len);
             o += w.motif_len;
             r.variations.assign((const char *)buf + o, (size_t)w.var_len);

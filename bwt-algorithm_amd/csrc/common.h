@@ -76,6 +76,8 @@ struct Rec {
     bool is_compound = false;
     bool kmer_stats = false;     // compound-stage pieces: score 100.0, zero composition,
                                  // entropy 1.5 (bwt.py:3980-3987, 4074-4091)
+    bool stats_none = false;     // composition None, entropy 0.0: records built without
+                                 // statistics (consolidated Tier 3 calls, bwt.py:3021-3030)
 };
 
 // motif utilities (MotifUtils, bwt.py:675-1381)
@@ -118,6 +120,8 @@ struct Job {
                                                      // (start, end, m desc, worker order) and deduped
     std::vector<int64_t> raw_n;                      // raw strict hits per contig
     std::vector<Rec> final_recs;                     // after bwt.py:3940-3944
+    std::vector<std::vector<Rec>> t3;                // per contig: Tier 3 records (bwt.py:3918-3924), joined
+                                                     // after the contig's strict hits before nested suppression
     std::vector<uint8_t> selected;                   // scan only these contigs (empty = all)
     bool postprocessed = false;
     Rendered rendered;                               // last bwtmi_job_render_units result

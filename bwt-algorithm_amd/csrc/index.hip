@@ -586,6 +586,30 @@ const int32_t *index_lcp_device(Ctx &c, DeviceIndex *ix) {
     return lcp;
 }
 
+namespace {
+__global__ void k_sa_rows(const uint32_t *__restrict__ sa, const int64_t *__restrict__ rows, int64_t k,
+                          int64_t *__restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < k) out[j] = (int64_t)sa[rows[j]];
+}
+}  // namespace
+
+// SA[rows[j]] for k rows (host arrays; every row < n)
+void index_sa_rows(Ctx &c, const DeviceIndex *ix, const int64_t *rows, int64_t k, int64_t *out) {
+    if (k <= 0) return;
+    for (int64_t j = 0; j < k; ++j)
+        if (rows[j] < 0 || rows[j] >= ix->n) fail(BWTMI_E_ARG, "SA row %lld out of range", (long long)rows[j]);
+    hipStream_t st = c.stream;
+    c.slot[S_MISC0].ensure((size_t)k * 8);
+    c.slot[S_MISC1].ensure((size_t)k * 8);
+    HIPCHECK(hipMemcpyAsync(c.slot[S_MISC0].p, rows, (size_t)k * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_sa_rows, dim3(blocks(k)), dim3(256), 0, st, ix->sa.as<uint32_t>(),
+                       c.slot[S_MISC0].as<int64_t>(), k, c.slot[S_MISC1].as<int64_t>());
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(out, c.slot[S_MISC1].p, (size_t)k * 8, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+}
+
 void index_backward_search(Ctx &c, DeviceIndex *ix, const uint8_t *pats, const int64_t *off, int64_t npat,
                            int64_t *sp_ep) {
     if (npat <= 0) return;

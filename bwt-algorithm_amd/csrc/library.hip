@@ -271,6 +271,50 @@ __global__ void k_t1_mark(const int64_t *__restrict__ ranges, int64_t nr, uint8_
     for (int64_t x = ranges[2 * r]; x < ranges[2 * r + 1]; ++x) seen[x] = 1;
 }
 
+// ------------------------------------------------------------- Tier 3
+// Tier3LongReadFinder._detect_repetitive_structure (bwt.py:2948-2984) for one
+// 500-byte window per wave: for period p = 10..165 the score is
+// #{i < 500 : w[i] == w[i % p]} / 500 (_score_periodicity: motif = w[:p], so
+// every position counts); the first period with the highest score > 0.7 wins.
+// Scores share the denominator, so "higher score" is "more matches"; the
+// 0.7 test is done on the double quotient, as in the reference.
+constexpr int kT3Win = 500, kT3Pmin = 10, kT3Pend = kT3Win / 3;   // range(10, len // 3)
+
+__global__ __launch_bounds__(256) void k_t3_windows(const uint8_t *__restrict__ reads, const int64_t *__restrict__ wpos,
+                                                    int64_t nwin, int32_t *__restrict__ best) {
+    __shared__ uint8_t win[4][512];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * 4 + wv;
+    const bool live = w < nwin;
+    uint8_t c[8];
+    if (live) {
+        const uint8_t *src = reads + wpos[w];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = lane + 64 * k;
+            c[k] = i < kT3Win ? src[i] : 0;
+            if (i < kT3Win) win[wv][i] = c[k];
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    int bp = 0, bm = 0;
+    for (int p = kT3Pmin; p < kT3Pend; ++p) {
+        int m = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = lane + 64 * k;
+            const bool eq = i < kT3Win && c[k] == win[wv][i % p];
+            m += __popcll(__ballot(eq));
+        }
+        if (m > bm && (double)m / (double)kT3Win > 0.7) {
+            bm = m;
+            bp = p;
+        }
+    }
+    if (lane == 0) best[w] = bp ? (bp << 16) | bm : 0;
+}
+
 // --------------------------------------------------- host-side exact helpers
 // majority vote of n_copies copies from `start` (np.unique + argmax)
 static void majority(const uint8_t *t, int64_t n, int64_t start, int64_t L, int64_t n_copies, std::string &cons,
@@ -687,6 +731,153 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
             }
         }
     }
+}
+
+
+// Tier3LongReadFinder.find_very_long_repeats (bwt.py:2837-2850): every read of
+// >= 1000 bytes, windows of 500 every 100 bytes (2852-2946).  The periodicity
+// scan runs on the device (k_t3_windows); the anchors of repetitive windows
+// (read[start-50:start], mapped only when located exactly once,
+// _map_read_to_reference 2986-3001) go through the device backward search and
+// SA; records are built and consolidated (3003-3036) on the host, in read and
+// window order.
+void tier3_device(Ctx &c, DeviceIndex *ix, const uint8_t *reads, const int64_t *read_off, int64_t nreads,
+                  int32_t chrom, std::vector<Rec> &out) {
+    const int64_t n = index_n(ix);
+    std::vector<int64_t> wpos;   // window starts (offsets into reads)
+    std::vector<int64_t> wread;  // read of each window
+    for (int64_t r = 0; r < nreads; ++r) {
+        const int64_t a = read_off[r], len = read_off[r + 1] - read_off[r];
+        if (len < 1000) continue;                                     // min_read_length (2833, 2842)
+        for (int64_t s = 0; s < len - kT3Win; s += 100) {             // range(0, len - 500, 100)
+            wpos.push_back(a + s);
+            wread.push_back(r);
+        }
+    }
+    const int64_t nwin = (int64_t)wpos.size();
+    if (nwin == 0 || n == 0) return;
+    hipStream_t st = c.stream;
+    const int64_t rbytes = read_off[nreads];
+    c.slot[S_IDX0].ensure((size_t)rbytes + 64);
+    c.slot[S_IDX1].ensure((size_t)nwin * 8);
+    c.slot[S_IDX2].ensure((size_t)nwin * 4);
+    HIPCHECK(hipMemcpyAsync(c.slot[S_IDX0].p, reads, (size_t)rbytes, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemcpyAsync(c.slot[S_IDX1].p, wpos.data(), (size_t)nwin * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_t3_windows, dim3((unsigned)((nwin + 3) / 4)), dim3(256), 0, st, c.slot[S_IDX0].as<uint8_t>(),
+                       c.slot[S_IDX1].as<int64_t>(), nwin, c.slot[S_IDX2].as<int32_t>());
+    HIPCHECK(hipGetLastError());
+    std::vector<int32_t> best((size_t)nwin);
+    HIPCHECK(hipMemcpyAsync(best.data(), c.slot[S_IDX2].p, (size_t)nwin * 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+
+    // anchors of the repetitive windows: read[max(0, s-50):s], used when >= 20 bytes
+    std::vector<int64_t> cand;        // window ids with an anchor
+    std::vector<uint8_t> pats;
+    std::vector<int64_t> poff(1, 0);
+    for (int64_t w = 0; w < nwin; ++w) {
+        if (!best[(size_t)w]) continue;
+        const int64_t s = wpos[(size_t)w] - read_off[wread[(size_t)w]];
+        const int64_t as = std::max<int64_t>(0, s - 50);
+        if (s - as < 20) continue;
+        cand.push_back(w);
+        pats.insert(pats.end(), reads + read_off[wread[(size_t)w]] + as, reads + wpos[(size_t)w]);
+        poff.push_back((int64_t)pats.size());
+    }
+    const int64_t na = (int64_t)cand.size();
+    if (na == 0) return;
+    std::vector<int64_t> spep((size_t)na * 2);
+    index_backward_search(c, ix, pats.data(), poff.data(), na, spep.data());
+    std::vector<int64_t> rows, hitw;
+    for (int64_t q = 0; q < na; ++q)
+        if (spep[2 * q] >= 0 && spep[2 * q] == spep[2 * q + 1]) {   // len(positions) == 1
+            rows.push_back(spep[2 * q]);
+            hitw.push_back(q);
+        }
+    if (rows.empty()) return;
+    std::vector<int64_t> pos(rows.size());
+    index_sa_rows(c, ix, rows.data(), (int64_t)rows.size(), pos.data());
+    std::vector<uint8_t> text((size_t)n);
+    index_get_text(c, ix, text.data());
+    const uint8_t *t = text.data();
+    const int64_t max_len = (n > 0 && t[n - 1] == '$') ? n - 1 : n;   // 2877-2880
+    std::vector<Rec> recs;
+    AlignSummary summ;
+    for (size_t h = 0; h < rows.size(); ++h) {
+        const int64_t q = hitw[h], w = cand[(size_t)q];
+        const int64_t s = wpos[(size_t)w] - read_off[wread[(size_t)w]];
+        const int64_t as = std::max<int64_t>(0, s - 50);
+        const int64_t ref_start = pos[h] + (s - as);
+        const int64_t p = best[(size_t)w] >> 16, matches = best[(size_t)w] & 0xFFFF;
+        int64_t motif_len = p;
+        if (ref_start >= max_len) continue;
+        const int64_t avail = std::max<int64_t>((max_len - ref_start) / motif_len, 0);
+        if (avail == 0) continue;
+        const int64_t copies_int = std::max<int64_t>(1, std::min<int64_t>(kT3Win / p, avail));
+        const int64_t ref_end = ref_start + motif_len * copies_int;
+        std::string cons((const char *)reads + wpos[(size_t)w], (size_t)p);   // motif = window[:p]
+        double mm = 0.0;
+        int64_t maxmm = 0;
+        Rec r;
+        r.pmatch = 100.0;
+        r.score = 0;
+        std::string cc;
+        if (consensus_array(t, n, ref_start, motif_len, copies_int, cc, mm, maxmm)) {
+            cons = cc;
+            motif_len = (int64_t)cons.size();
+        }
+        // calculate_trf_statistics (1336-1366): ref_end <= max_len always holds here
+        r.pmatch = (1.0 - mm) * 100.0;
+        r.pindel = 0.0;
+        r.score = trf_score(ref_end - ref_start, mm);
+        std::string canon;
+        canonical_stranded(cons, canon, r.strand);
+        // summarize_variations_array over the index text (incl. '$'), min_copies = 1 (1259-1287)
+        if (align_repeat_region((const char *)t, n, ref_start, std::min(ref_end, n), cons, 1, summ) &&
+            summ.any_variation)
+            r.variations = summ.variations;
+        r.chrom = chrom;
+        r.tier = 3;
+        r.start = ref_start;
+        r.end = ref_end;
+        r.length = ref_end - ref_start;
+        r.motif = cons;
+        r.copies = (double)copies_int;
+        r.confidence = (double)matches / (double)kT3Win;
+        r.mismatch_rate = mm;
+        r.max_mm = maxmm;
+        r.n_eval = copies_int;
+        r.act_kind = ACT_FULL;   // actual_sequence = text_arr[ref_start:ref_end] (1345-1346)
+        r.act_off = ref_start;
+        r.act_len = ref_end - ref_start;
+        recs.push_back(std::move(r));
+    }
+    // _consolidate_repeat_calls (3003-3036): stable sort by (start, end), then a
+    // fold merging overlapping calls with equal motifs into bare records
+    std::stable_sort(recs.begin(), recs.end(), [](const Rec &a, const Rec &b) {
+        return a.start != b.start ? a.start < b.start : a.end < b.end;
+    });
+    if (recs.empty()) return;
+    Rec cur = recs[0];
+    for (size_t k = 1; k < recs.size(); ++k) {
+        const Rec &r = recs[k];
+        if (r.start <= cur.end && r.motif == cur.motif) {
+            Rec m;
+            m.chrom = cur.chrom;
+            m.start = std::min(cur.start, r.start);
+            m.end = std::max(cur.end, r.end);
+            m.motif = cur.motif;
+            m.copies = (cur.copies + r.copies) / 2;
+            m.length = m.end - m.start;
+            m.tier = cur.tier;
+            m.confidence = std::min(cur.confidence, r.confidence);
+            m.stats_none = true;   // composition None, entropy 0.0, the other fields at their defaults
+            cur = std::move(m);
+        } else {
+            out.push_back(std::move(cur));
+            cur = r;
+        }
+    }
+    out.push_back(std::move(cur));
 }
 
 }  // namespace bwtmi

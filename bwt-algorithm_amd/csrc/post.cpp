@@ -226,6 +226,7 @@ struct Extra {                  // trivially destructible: strings live in the P
     double copies = 0, confidence = 0, mm = 0, pmatch = 0, pindel = 0;
     int64_t max_mm = 0, n_eval = 0, score = 0;
     char strand = '+';
+    bool stats_none = false;    // Rec::stats_none
 };
 
 struct Item {
@@ -771,6 +772,29 @@ void dedup_sorted(const UnitCtx &u, ItemVec &recs) {
     recs.swap(d);
 }
 
+// an input record that is not a strict hit (Tier 3): every field carried in an Extra
+Item item_of_rec(Pools &pools, const Rec &r) {
+    Extra x;
+    x.copies = r.copies;
+    x.confidence = r.confidence;
+    x.mm = r.mismatch_rate;
+    x.pmatch = r.pmatch;
+    x.pindel = r.pindel;
+    x.max_mm = r.max_mm;
+    x.n_eval = r.n_eval;
+    x.score = r.score;
+    x.strand = r.strand;
+    x.stats_none = r.stats_none;
+    Item it{};
+    it.start = r.start;
+    it.end = r.end;
+    it.chrom = r.chrom;
+    it.mlen = (int32_t)r.motif.size();
+    it.tier = r.tier;
+    it.x = pools.add(0, x, r.motif, r.variations);
+    return it;
+}
+
 // final Rec of an item (after restore): strict fields per bwt.py:1972-1993
 Rec materialize(const UnitCtx &u, const Item &it) {
     Rec r;
@@ -793,6 +817,7 @@ Rec materialize(const UnitCtx &u, const Item &it) {
         r.pindel = x.pindel;
         r.score = x.score;
         r.variations = x.variations;
+        r.stats_none = x.stats_none;
     } else {
         r.motif.assign(c.trimmed() + it.moff, (size_t)it.mlen);
         r.copies = (double)it.count;
@@ -840,6 +865,12 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
             }
         });
         HitVec().swap(h);
+        // Tier 3 records of this chromosome come after all worker records (bwt.py:3918-3924)
+        const bool mine = job.selected.empty() || ((size_t)c < job.selected.size() && job.selected[(size_t)c]);
+        if (mine && (size_t)c < job.t3.size() && !job.t3[(size_t)c].empty()) {
+            if (scr) fail(BWTMI_E_STATE, "contig %d holds device-screened hits and Tier 3 records", (int)c);
+            for (const Rec &r : job.t3[(size_t)c]) items.push_back(item_of_rec(pools, r));
+        }
         if (!scr) items = suppress_nested(items, 0.5, nt);
         if (recs.empty()) recs.swap(items);
         else recs.insert(recs.end(), items.begin(), items.end());

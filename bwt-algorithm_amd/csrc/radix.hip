@@ -6,8 +6,9 @@
 //   scan    : exclusive scan of counts (digit-major) -> global offsets
 //   scatter : each of the 4 waves owns 1024 consecutive keys of the tile; it
 //             ranks keys of equal digit with 8 ballots (wave64 match-any) in
-//             index order, so the pass is stable; per-wave digit bases come
-//             from the scanned offsets + the preceding waves' histograms.
+//             index order, so the pass is stable; the tile is reordered by
+//             digit in LDS and streamed out in that order, so each digit's
+//             run of the tile is one contiguous, coalesced write.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -106,43 +107,42 @@ __global__ __launch_bounds__(kBlock) void k_hist(const uint64_t *__restrict__ ke
     counts[(int64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
+// Scatter of one tile, staged through LDS so that the global writes are
+// coalesced: every key is ranked inside the tile (stable: wave order, then
+// item order, then lane order), written to LDS at its tile-sorted slot, and the
+// tile is then streamed out in slot order -- consecutive lanes write
+// consecutive addresses inside each digit's run.
 template <class V>
 __global__ __launch_bounds__(kBlock) void k_scatter(const uint64_t *__restrict__ kin, const V *__restrict__ vin,
                                                     uint64_t *__restrict__ kout, V *__restrict__ vout,
                                                     const uint32_t *__restrict__ offs, int64_t n, int shift,
                                                     int64_t ntiles) {
-    __shared__ uint32_t whist[kWaves][256];
-    __shared__ uint32_t woff[kWaves][256];
+    __shared__ uint32_t wcnt[kWaves][256];   // per-wave digit counts, then per-wave digit bases
+    __shared__ uint32_t gdelta[256];         // global position of tile slot j = gdelta[digit] + j
+    __shared__ uint32_t dsum[kWaves];
+    __shared__ uint64_t ks[kTile];
+    __shared__ V vs[kTile];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int w = 0; w < kWaves; ++w) whist[w][threadIdx.x] = 0;
+    for (int w = 0; w < kWaves; ++w) wcnt[w][threadIdx.x] = 0;
     __syncthreads();
-    const int64_t wbase = (int64_t)blockIdx.x * kTile + (int64_t)wv * (kItems * 64);
+    const int64_t tbase = (int64_t)blockIdx.x * kTile;
+    const int64_t wbase = tbase + (int64_t)wv * (kItems * 64);
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint64_t k[kItems];
     V v[kItems];
-#pragma unroll
-    for (int i = 0; i < kItems; ++i) {
-        const int64_t idx = wbase + i * 64 + lane;
-        if (idx < n) {
-            k[i] = kin[idx];
-            if (vin) v[i] = vin[idx];
-            atomicAdd(&whist[wv][(k[i] >> shift) & 255u], 1u);
-        }
-    }
-    __syncthreads();
-    {
-        uint32_t b = offs[(int64_t)threadIdx.x * ntiles + blockIdx.x];
-        for (int w = 0; w < kWaves; ++w) {
-            woff[w][threadIdx.x] = b;
-            b += whist[w][threadIdx.x];
-        }
-    }
-    __syncthreads();
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t r[kItems];   // rank among the wave's earlier keys of the same digit
 #pragma unroll
     for (int i = 0; i < kItems; ++i) {
         const int64_t idx = wbase + i * 64 + lane;
         const bool valid = idx < n;
-        const uint32_t d = valid ? (uint32_t)((k[i] >> shift) & 255u) : 0u;
+        k[i] = valid ? kin[idx] : 0ull;
+        if (vin) v[i] = valid ? vin[idx] : (V)0;
+    }
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        const int64_t idx = wbase + i * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t d = (uint32_t)((k[i] >> shift) & 255u);
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int bt = 0; bt < 8; ++bt) {
@@ -150,14 +150,57 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const uint64_t *__restrict__
             const uint64_t bal = __ballot(bit);
             peers &= bit ? bal : ~bal;
         }
-        uint32_t pos = 0;
-        if (valid) pos = woff[wv][d] + (uint32_t)__popcll(peers & lt);
+        const uint32_t before = (uint32_t)__popcll(peers & lt);
+        r[i] = valid ? wcnt[wv][d] + before : 0u;
         __builtin_amdgcn_wave_barrier();
-        if (valid && (peers & lt) == 0) woff[wv][d] += (uint32_t)__popcll(peers);
+        if (valid && before == 0) wcnt[wv][d] += (uint32_t)__popcll(peers);
         __builtin_amdgcn_wave_barrier();
-        if (valid) {
-            kout[pos] = k[i];
-            if (vout) vout[pos] = v[i];
+    }
+    __syncthreads();
+    // thread t owns digit t: tile count, exclusive scan over digits, per-wave bases
+    const int dg = threadIdx.x;
+    uint32_t cnt[kWaves], tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+        cnt[w] = wcnt[w][dg];
+        tot += cnt[w];
+    }
+    const uint32_t inc = wave_incl_scan<uint32_t>(tot);
+    if (lane == 63) dsum[wv] = inc;
+    __syncthreads();
+    uint32_t toff = inc - tot;
+    for (int w = 0; w < wv; ++w) toff += dsum[w];
+    gdelta[dg] = offs[(int64_t)dg * ntiles + blockIdx.x] - toff;
+    {
+        uint32_t b = toff;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            wcnt[w][dg] = b;
+            b += cnt[w];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        const int64_t idx = wbase + i * 64 + lane;
+        if (idx < n) {
+            const uint32_t d = (uint32_t)((k[i] >> shift) & 255u);
+            const uint32_t slot = wcnt[wv][d] + r[i];
+            ks[slot] = k[i];
+            if (vin) vs[slot] = v[i];
+        }
+    }
+    __syncthreads();
+    const int64_t rem = n - tbase;
+    const int cntt = rem < kTile ? (int)rem : kTile;
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        const int j = i * kBlock + threadIdx.x;
+        if (j < cntt) {
+            const uint64_t key = ks[j];
+            const uint32_t pos = gdelta[(key >> shift) & 255u] + (uint32_t)j;
+            kout[pos] = key;
+            if (vout) vout[pos] = vs[j];
         }
     }
 }

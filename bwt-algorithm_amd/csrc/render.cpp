@@ -231,6 +231,11 @@ void comp_entropy(const Rec &r, double comp[4], double &ent) {
         ent = 1.5;
         return;
     }
+    if (r.stats_none) {   // to_trf_table/to_trf_dat: composition or 25 % each (bwt.py:485, 505)
+        comp[0] = comp[1] = comp[2] = comp[3] = 25.0;
+        ent = 0.0;
+        return;
+    }
     composition_of(r.motif.data(), (int64_t)r.motif.size(), comp);
     ent = entropy_of(r.motif.data(), (int64_t)r.motif.size());
 }

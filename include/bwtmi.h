@@ -125,6 +125,15 @@ int bwtmi_index_short_imperfect(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_li
 /* Tier1STRFinder(text_arr, max_motif_length).find_strs (bwt.py:1426-1538) over the full
  * sequence of the job's contig contig_id; records appended to the job's final records */
 int bwtmi_job_tier1(bwtmi_ctx *ctx, bwtmi_job *job, int32_t contig_id, int32_t max_motif_length);
+/* Tier3LongReadFinder(bwt_core).find_very_long_repeats(long_reads, chromosome) (bwt.py:2837-3036)
+ * over the index (built over seq + '$'): reads = the reads' bytes back to back, read_off[nreads + 1]
+ * their offsets (read_off[0] = 0).  The consolidated records get contig contig_id and go
+ *   as_input = 0: to the job's final records (the library call's return value);
+ *   as_input = 1: to the job's Tier 3 input of that contig, which bwtmi_job_postprocess joins after
+ *                 the contig's strict hits before nested suppression (find_tandem_repeats_parallel,
+ *                 bwt.py:3917-3924); call after bwtmi_job_reset and before bwtmi_job_scan. */
+int bwtmi_index_tier3(bwtmi_ctx *ctx, bwtmi_index *idx, const uint8_t *reads, const int64_t *read_off,
+                      int64_t nreads, bwtmi_job *job, int32_t contig_id, int32_t as_input);
 /* BWTCore.backward_search (bwt.py:359-389) for npat patterns packed in pats,
  * pattern p = pats[off[p] .. off[p+1]).  Writes sp_ep[2p], sp_ep[2p+1]
  * (inclusive interval, or -1,-1). */
@@ -202,9 +211,10 @@ int bwtmi_job_unit_rows(bwtmi_job *job, int64_t *unit_rows);
 int bwtmi_job_render_units(bwtmi_job *job, int fmt, const int64_t *row_base, int64_t *bytes);
 int bwtmi_job_write_units(bwtmi_job *job, const char *path, const int64_t *offsets, int write_header);
 /* final records as rows of int64: start, end, length, tier, n_copies_eval,
- * max_mm, motif_len, cons_len, chrom_id and doubles: copies, mismatch_rate,
- * confidence (for tests / the Python record view) */
-int bwtmi_job_get_records(bwtmi_job *job, int64_t *ints9, double *dbls3);
+ * max_mm, score, flags (1: composition None / entropy 0.0, 2: k-mer scan piece),
+ * chrom_id and doubles: copies, mismatch_rate, confidence, percent_matches,
+ * percent_indels (for tests / the Python record view) */
+int bwtmi_job_get_records(bwtmi_job *job, int64_t *ints9, double *dbls5);
 /* strings of record i: which = 0 motif, 1 consensus, 2 variations(';'-joined),
  * 3 actual_sequence, 4 strand; returns length, copies up to cap bytes */
 int64_t bwtmi_job_get_string(bwtmi_job *job, int64_t i, int which, char *buf, int64_t cap);

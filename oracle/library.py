@@ -12,6 +12,11 @@ Reference: /root/reference/bwt.py (wyim-pgl/bwt-algorithm @ 2025-11-14).
                     -> _analyze_sa_interval_for_tandems (2500-2549),
                     _validate_periodicity_arr (2551-2560)   (A2-9)
   tier1_find_strs   Tier1STRFinder.find_strs (1426-1538)    (§8(f) #2)
+  tier3             Tier3LongReadFinder.find_very_long_repeats (2837-3036):
+                    500-byte windows every 100 bytes of each read >= 1000,
+                    self-periodicity 10..165, unique 50-byte anchor -> FM
+                    locate, consensus/statistics/variations, consolidation
+                    (§8(f) #3)
 
 Records are dicts with the reference TandemRepeat field names (bwt.py:429-452).
 """
@@ -379,4 +384,100 @@ def tier1_find_strs(chrom: str, t: bytes, max_motif_length: int = 9, min_copies:
                     i = end
                     continue
             i += step
+    return out
+
+
+# ------------------------------------------------------------------ Tier 3
+def _t3_structure(window: bytes):
+    """_detect_repetitive_structure + _score_periodicity (bwt.py:2948-2984):
+    the first period 10 <= p < len // 3 with the highest score > 0.7, where
+    score = #{i : w[i] == w[i % p]} / len(w) (motif = w[:p] covers every i)."""
+    if len(window) < 50:
+        return None
+    w = np.frombuffer(window, dtype=np.uint8)
+    idx = np.arange(len(w))
+    best_p, best_copies, best_score = None, 0, 0
+    for p in range(10, len(w) // 3):
+        score = int(np.count_nonzero(w == w[idx % p])) / len(w)
+        if score > best_score and score > 0.7:
+            best_score, best_p, best_copies = score, p, len(w) // p
+    if best_p and best_copies >= 3:
+        return window[:best_p], best_copies, best_score
+    return None
+
+
+def _t3_map(idx, read: bytes, position: int) -> int:   # _map_read_to_reference, bwt.py:2986-3001
+    anchor_start = max(0, position - 50)
+    anchor = read[anchor_start:position]
+    if len(anchor) >= 20:
+        sp, ep = idx.backward_search(anchor)
+        if sp != -1 and ep == sp:
+            return int(idx.sa[sp]) + (position - anchor_start)
+    return -1
+
+
+def tier3(text: bytes, reads: List[bytes], chromosome: str, idx=None) -> List[Dict]:
+    """Tier3LongReadFinder(BWTCore(text)).find_very_long_repeats(reads, chromosome)
+    (bwt.py:2837-2850 -> _analyze_read_for_repeats 2852-2946 ->
+    _consolidate_repeat_calls 3003-3036).  text includes the sentinel."""
+    from . import Index
+    idx = idx if idx is not None else Index(text)
+    max_len = len(text) - 1 if text and text[-1] == 36 else len(text)   # 2877-2880
+    seq = text.decode("ascii", errors="replace")
+    reps: List[Dict] = []
+    for read in reads:
+        if len(read) < 1000:                                               # 2842
+            continue
+        for start in range(0, len(read) - 500, 100):                       # 2857-2861
+            info = _t3_structure(read[start:start + 500])
+            if not info:
+                continue
+            motif, copies, confidence = info
+            ref_start = _t3_map(idx, read, start)
+            if ref_start < 0:
+                continue
+            motif_len = len(motif)
+            if ref_start >= max_len:
+                continue
+            avail = max((max_len - ref_start) // motif_len, 0)
+            if avail == 0:
+                continue
+            copies_int = max(1, min(int(round(copies)), avail))
+            ref_end = ref_start + motif_len * copies_int
+            cons = motif.decode("ascii", errors="replace")
+            mm, max_mm = 0.0, 0
+            pm, pi, score = 100.0, 0.0, 0
+            comp, ent = post.composition(cons), entropy(cons)
+            actual = (cons * copies_int)[:max(ref_end - ref_start, 0)]
+            if motif_len > 0 and ref_end > ref_start:
+                carr, mm, max_mm = consensus_array(text, ref_start, motif_len, copies_int)
+                if carr:
+                    cons = carr.decode("ascii", errors="replace")
+                    motif_len = len(cons)
+                if ref_end <= max_len:
+                    pm, pi, score, comp, ent, actual = trf_statistics(text, ref_start, ref_end, cons, copies_int, mm)
+            _, strand = post.canonical_stranded(cons)
+            var = None                                                     # summarize_variations_array (1259-1287)
+            if len(text) and motif_len > 0:
+                s0, e0 = max(0, ref_start), min(len(seq), ref_end if ref_end > ref_start else len(seq))
+                if e0 > s0:
+                    summ = post.align_region(seq, s0, e0, cons, 0.1, None, 1)
+                    if summ and summ["variations"]:
+                        var = summ["variations"]
+            reps.append(_rec(chromosome, ref_start, ref_end, cons, float(copies_int), ref_end - ref_start, 3,
+                             confidence, cons, mm, max_mm, copies_int, strand, pm, pi, score, comp, ent,
+                             actual, var))
+    if not reps:
+        return reps
+    reps.sort(key=lambda r: (post.natural_key(r["chrom"]), r["start"], r["end"]))
+    out, cur = [], reps[0]
+    for r in reps[1:]:
+        if r["chrom"] == cur["chrom"] and r["start"] <= cur["end"] and r["motif"] == cur["motif"]:
+            s, e = min(cur["start"], r["start"]), max(cur["end"], r["end"])
+            cur = _rec(cur["chrom"], s, e, cur["motif"], (cur["copies"] + r["copies"]) / 2, e - s, cur["tier"],
+                       min(cur["confidence"], r["confidence"]))
+        else:
+            out.append(cur)
+            cur = r
+    out.append(cur)
     return out

@@ -825,11 +825,32 @@ def load_fasta(path: str, flank_trim: int = 30):
     return seqs, full, offs
 
 
+def read_long_reads(path: str) -> List[str]:
+    """The CLI's FASTA/FASTQ long-read reader (bwt.py:4312-4328): '>'/'@' lines
+    start a read, '+' lines are skipped, every other line (FASTQ quality
+    lines included) is upper-cased and appended."""
+    reads: List[str] = []
+    seq = ""
+    with open(path, "r") as f:
+        for line in f:
+            line = line.strip()
+            if line.startswith(">") or line.startswith("@"):
+                if seq:
+                    reads.append(seq)
+                    seq = ""
+            elif not line.startswith("+"):
+                seq += line.upper()
+        if seq:
+            reads.append(seq)
+    return reads
+
+
 def run_file(path: str, fmt: str = "strfinder", min_copies: int = 3, max_unit_len: int = 120,
              flank_trim: int = 30, tier2: bool = True, show_progress: bool = False,
-             strict_scan=None) -> str:
+             strict_scan=None, long_reads: Optional[List[str]] = None) -> str:
     """Whole CLI path (bwt.py:4293-4361) with `strict_scan(seq_bytes, U, min_copies)`
-    supplying raw hits (defaults to the C oracle)."""
+    supplying raw hits (defaults to the C oracle).  long_reads: Tier 3 in
+    parallel mode (bwt.py:3917-3924), after all worker records."""
     if strict_scan is None:
         from oracle import strict_scan as _ss
 
@@ -846,4 +867,9 @@ def run_file(path: str, fmt: str = "strfinder", min_copies: int = 3, max_unit_le
         U = max(max_unit_len, min(len(s) // min_copies, 1000))
         hits = strict_scan(s.encode("utf-8"), U, min_copies)
         raw.extend(worker_records(chrom, s, hits))
+    if long_reads:
+        from . import library
+        rb = [x.encode("latin-1", errors="replace") for x in long_reads]
+        for chrom, s in seqs.items():
+            raw.extend(Rec(**d) for d in library.tier3((s + "$").encode("utf-8"), rb, chrom))
     return render(p, p.run(raw), fmt)

@@ -14,6 +14,9 @@ here is product code.  Outputs land in tests/golden/ as small data files:
   motif         MotifUtils known answers
   library       library finders off the CLI path: short imperfect repeats
                 (FM seeds + Hamming seed-and-extend), LCP plateaus, Tier 1
+  tier3         Tier3LongReadFinder on seeded contigs + long reads (library
+                call) and the CLI with --tier3 --long-reads (FASTA and FASTQ
+                reads, four formats, parallel and sequential modes)
   hybrid        reference post-processing with the strict scan (and the
                 O(k^2) nested-suppression loop) swapped for the oracle's
                 restatements -> full-size output SHA-256; the
@@ -394,6 +397,108 @@ def cmd_library(a):
         json.dump(out, f, indent=0)
 
 
+def _tier3_inputs():
+    """Seeded contigs with long-period arrays (10-160 bp units, some with 2 %
+    substitutions, one 3 bp array, one array at a contig's end) and long reads
+    sampled over them (1 % noise on some), plus random, short and lower-case
+    reads.  Returns ({name: seq}, [reads as str])."""
+    r = np.random.default_rng(7)
+    B = "ACGT"
+
+    def rnd(n):
+        return "".join(B[i] for i in r.integers(0, 4, n))
+
+    def array(unit, copies, sub):
+        s = list(unit * copies)
+        for q in range(len(s)):
+            if r.random() < sub:
+                s[q] = B[(B.index(s[q]) + int(r.integers(1, 4))) % 4]
+        return "".join(s)
+
+    plan = {"chrT1": [(12, 70, 0.0), (40, 25, 0.02), (77, 12, 0.0), (3, 300, 0.0), (160, 6, 0.0)],
+            "chrT2": [(25, 40, 0.0), (120, 8, 0.02), (33, 30, 0.0)],
+            "chrT10": [(50, 20, 0.0), (18, 50, 0.0)]}
+    contigs, spans = {}, []
+    for name, arrs in plan.items():
+        seq = rnd(400)
+        for (u, c, sub) in arrs:
+            a0 = len(seq)
+            seq += array(rnd(u), c, sub)
+            spans.append((name, a0, len(seq)))
+            seq += rnd(int(r.integers(300, 900)))
+        if name == "chrT10":          # an array running to the contig's end
+            a0 = len(seq)
+            seq += array(rnd(45), 14, 0.0)
+            spans.append((name, a0, len(seq)))
+        contigs[name] = seq
+    reads = []
+    for (name, a0, a1) in spans:
+        seq = contigs[name]
+        for _ in range(2):
+            s0 = max(0, a0 - int(r.integers(60, 420)))
+            ln = int(r.integers(1000, 2600))
+            rd = list(seq[s0:s0 + ln])
+            if r.random() < 0.3:
+                for q in range(len(rd)):
+                    if r.random() < 0.01:
+                        rd[q] = B[(B.index(rd[q]) + 1) % 4]
+            reads.append("".join(rd))
+    reads.append(rnd(1500))                                 # no repeat
+    reads.append(contigs["chrT1"][350:1200])                # < 1000: skipped
+    reads.append(contigs["chrT2"][300:1900].lower())        # lower case (the CLI upper-cases)
+    reads.append(contigs["chrT1"][:1400] + contigs["chrT2"][400:1500])   # chimeric
+    return contigs, reads
+
+
+def cmd_tier3(a):
+    """Tier 3 long-read anchoring: the library call on each
+    contig (trimmed as the CLI does, + '$') and CLI runs -> tier3.json, inputs
+    tier3.fa / tier3_reads.fa / tier3_reads.fq."""
+    ref = ref_module()
+    contigs, reads = _tier3_inputs()
+    inp = os.path.join(HERE, "inputs")
+    with open(os.path.join(inp, "tier3.fa"), "w") as f:
+        for name, seq in contigs.items():
+            f.write(f">{name}\n")
+            for i in range(0, len(seq), 60):
+                f.write(seq[i:i + 60] + "\n")
+    with open(os.path.join(inp, "tier3_reads.fa"), "w") as f:
+        for i, rd in enumerate(reads):
+            f.write(f">read{i}\n")
+            for q in range(0, len(rd), 70):
+                f.write(rd[q:q + 70] + "\n")
+    with open(os.path.join(inp, "tier3_reads.fq"), "w") as f:
+        for i, rd in enumerate(reads[:8]):
+            f.write(f"@read{i}\n{rd}\n+\n{'I' * len(rd)}\n")
+    out = {"library": {}, "cli": {}}
+    for name, seq in contigs.items():
+        trimmed = seq[30:-30]
+        core = ref.BWTCore(trimmed + "$", 32)
+        t0 = time.time()
+        recs = ref.Tier3LongReadFinder(core).find_very_long_repeats(reads, name)
+        out["library"][name] = dict(records=[_rec_json(x) for x in recs], seconds=round(time.time() - t0, 1))
+        print(name, len(seq), len(recs), out["library"][name]["seconds"], flush=True)
+    work = tempfile.mkdtemp()
+    for fn in ("tier3.fa", "tier3_reads.fa", "tier3_reads.fq"):
+        shutil.copy(os.path.join(inp, fn), os.path.join(work, fn))
+    cases = [("fa.strfinder", ["--long-reads", "tier3_reads.fa", "--jobs", "2"]),
+             ("fa.bed", ["--long-reads", "tier3_reads.fa", "--jobs", "2", "--format", "bed"]),
+             ("fa.vcf", ["--long-reads", "tier3_reads.fa", "--jobs", "2", "--format", "vcf"]),
+             ("fa.trf_dat", ["--long-reads", "tier3_reads.fa", "--jobs", "2", "--format", "trf_dat"]),
+             ("fq.strfinder", ["--long-reads", "tier3_reads.fq", "--jobs", "2"]),
+             ("fa.sequential", ["--long-reads", "tier3_reads.fa", "--jobs", "-1"])]
+    for tag, extra in cases:
+        t0 = time.time()
+        run_ref_cli(ref, ["tier3.fa", "--tier3", "-o", "out.tab"] + extra, work)
+        with open(os.path.join(work, "out.tab"), "rb") as f:
+            data = f.read()
+        out["cli"][tag] = dict(args=["--tier3"] + extra, sha256=hashlib.sha256(data).hexdigest(),
+                               text=data.decode(), seconds=round(time.time() - t0, 1))
+        print(tag, out["cli"][tag]["sha256"][:16], data.count(b"\n"), out["cli"][tag]["seconds"], flush=True)
+    with open(os.path.join(HERE, "tier3.json"), "w") as f:
+        json.dump(out, f, indent=0)
+
+
 def cmd_hybrid(a):
     """Full-size golden via the validated hybrid oracle."""
     ref = ref_module()
@@ -436,6 +541,7 @@ def main():
     sp.add_parser("index")
     sp.add_parser("motif")
     sp.add_parser("library")
+    sp.add_parser("tier3")
     p = sp.add_parser("hybrid")
     p.add_argument("name")
     p.add_argument("--config")
@@ -448,7 +554,7 @@ def main():
     p.add_argument("--save-out", action="store_true")
     a = ap.parse_args()
     dict(fixtures=cmd_fixtures, rawhits=cmd_rawhits, index=cmd_index, motif=cmd_motif,
-         hybrid=cmd_hybrid, library=cmd_library)[a.cmd](a)
+         hybrid=cmd_hybrid, library=cmd_library, tier3=cmd_tier3)[a.cmd](a)
 
 
 if __name__ == "__main__":
