@@ -73,6 +73,7 @@ _SIGS = {
                                            C.POINTER(C.c_int64)]),
     "bwtmi_index_short_imperfect": (C.c_int, [_P, _P, C.POINTER(LibParams), _P, C.c_int64, _P, C.c_int32]),
     "bwtmi_job_tier1": (C.c_int, [_P, _P, C.c_int32, C.c_int32]),
+    "bwtmi_index_long_repeats": (C.c_int, [_P, _P, C.POINTER(LibParams), _P, C.c_int64, _P, C.c_int32]),
     "bwtmi_index_tier3": (C.c_int, [_P, _P, _P, _P, C.c_int64, _P, C.c_int32, C.c_int32]),
     "bwtmi_job_create": (C.c_int, [C.POINTER(Params), C.POINTER(_P)]),
     "bwtmi_job_free": (C.c_int, [_P]),

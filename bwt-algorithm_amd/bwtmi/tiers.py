@@ -3,8 +3,8 @@
 Tier2LCPFinder.find_long_unit_repeats_strict -- the detector that decides the
 CLI's repeat.tab -- runs on the device (libbwtmi strict scan); the LCP array
 comes from the device index.  The library-only finders that the CLI never
-calls are listed in SURVEY.md §8(f) as the next rows to build; until then
-they raise NotImplementedError instead of silently returning something else.
+calls run over the device index
+as well (library.hip).
 """
 from __future__ import annotations
 
@@ -153,9 +153,24 @@ class Tier2LCPFinder:
                                     tier=2, confidence=0.9))
         return res
 
-    def find_long_repeats(self, chromosome: str, tier1_seen=None):
-        raise NotImplementedError("find_long_repeats: out of scope (wall-clock-dependent results, "
-                                  "bwt.py:2236-2257)")
+    def find_long_repeats(self, chromosome: str, tier1_seen: Optional[Set[Tuple[int, int]]] = None):
+        """bwt.py:2097-2106 -> _find_repeats_simple (2177-2390): one walk per
+        period over the positions, first extensions (_extend_with_mismatches,
+        2392-2498) evaluated on the device in look-ahead batches (library.hip).
+        The reference's 30 s wall-clock stop (2238-2257) is not reproduced."""
+        return self._find_repeats_simple(chromosome, tier1_seen or set())
+
+    def _find_repeats_simple(self, chromosome: str, tier1_seen: Set[Tuple[int, int]]) -> List[TandemRepeat]:
+        from .records import Job
+        t = np.ascontiguousarray(self.bwt.text_arr, dtype=np.uint8)
+        job = Job()
+        job.add_contig(chromosome, t.tobytes(), 0, 0)
+        seen = np.array(sorted(tier1_seen or ()), dtype=np.int64).reshape(-1)
+        buf = seen if seen.size else np.zeros(2, dtype=np.int64)
+        p = self._params()
+        check(lib().bwtmi_index_long_repeats(self.bwt._ctx, self.bwt._h, C.byref(p), buf.ctypes.data,
+                                             seen.size // 2, job.h, 0))
+        return list(job.records())
 
 
 def pack_reads(long_reads) -> Tuple[np.ndarray, np.ndarray]:

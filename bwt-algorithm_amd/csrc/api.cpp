@@ -370,6 +370,19 @@ int bwtmi_index_tier3(bwtmi_ctx *ctx, bwtmi_index *idx, const uint8_t *reads, co
     });
 }
 
+int bwtmi_index_long_repeats(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_lib_params *p, const int64_t *seen,
+                             int64_t nseen, bwtmi_job *job, int32_t contig_id) {
+    return guard([&] {
+        CHECK_ARG(ctx && idx && job && (seen || nseen == 0) && nseen >= 0, "bad argument");
+        CHECK_ARG(contig_id >= 0 && contig_id < (int32_t)job->j.contigs.size(), "bad contig id");
+        CHECK_ARG(p->min_copies >= 0 && p->min_array_length >= 0, "bad parameters");
+        use(ctx->c);
+        std::vector<int64_t> sp(seen, seen + 2 * nseen);
+        simple_scan_device(ctx->c, idx->d, lib_params(p), sp, contig_id, job->j.final_recs);
+        job->j.postprocessed = true;
+    });
+}
+
 int bwtmi_job_tier1(bwtmi_ctx *ctx, bwtmi_job *job, int32_t contig_id, int32_t max_motif_length) {
     return guard([&] {
         CHECK_ARG(ctx && job, "null argument");

@@ -225,6 +225,9 @@ void tier1_device(Ctx &c, const uint8_t *d_text, const uint8_t *t, int64_t n, in
 void index_backward_search(Ctx &c, DeviceIndex *, const uint8_t *pats, const int64_t *off, int64_t npat,
                            int64_t *sp_ep);
 void index_sa_rows(Ctx &c, const DeviceIndex *, const int64_t *rows, int64_t k, int64_t *out);
+// Tier2LCPFinder.find_long_repeats -> _find_repeats_simple (bwt.py:2097-2106, 2177-2498)
+void simple_scan_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const std::vector<int64_t> &seen_pairs,
+                        int32_t chrom, std::vector<Rec> &out);
 // Tier3LongReadFinder.find_very_long_repeats (bwt.py:2837-3036) of `reads` (concatenated,
 // read_off[nreads + 1]) against the index; consolidated records with chrom = `chrom`
 void tier3_device(Ctx &c, DeviceIndex *ix, const uint8_t *reads, const int64_t *read_off, int64_t nreads,

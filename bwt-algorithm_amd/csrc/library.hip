@@ -24,6 +24,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <set>
+#include <tuple>
+#include <unordered_map>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -313,6 +317,157 @@ __global__ __launch_bounds__(256) void k_t3_windows(const uint8_t *__restrict__ 
         }
     }
     if (lane == 0) best[w] = bp ? (bp << 16) | bm : 0;
+}
+
+// --------------------------------------------------- simple period scan
+// Tier2LCPFinder._extend_with_mismatches (bwt.py:2392-2498) for a batch of
+// (start, period) candidates, one wave per candidate, lane l owning motif
+// columns l, l + 64, l + 128, l + 192 (period <= 256).  Each column keeps up
+// to kSimSyms (symbol, count) pairs, so adding or retracting a copy is O(1)
+// per column; the array's mismatches against the majority consensus are
+// sum over columns of (copies - max count), reduced across the wave.  The
+// majority symbol is the smallest byte among the most frequent (np.unique +
+// argmax).  A column needing more symbols marks the candidate for the host.
+constexpr int kSimCols = 4, kSimSyms = 6, kSimMaxP = 64 * kSimCols;
+
+__device__ __forceinline__ int64_t max_mm_for_array_dev(int64_t L, int64_t c) {   // bwt.py:2003-2025
+    const int64_t tot = L * c;
+    if (L == 1) return 0;
+    const double f = L <= 6 ? 0.05 : 0.08;
+    const int64_t m = (int64_t)ceil(f * (double)tot);
+    return m > 1 ? m : 1;
+}
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+struct SimCol {
+    uint8_t s[kSimSyms];
+    uint32_t c[kSimSyms];
+    int nd;
+};
+
+__device__ __forceinline__ void simcol_add(SimCol &k, uint8_t b, int d, bool &ovf) {
+#pragma unroll
+    for (int q = 0; q < kSimSyms; ++q)
+        if (q < k.nd && k.s[q] == b) { k.c[q] += d; return; }
+    if (k.nd < kSimSyms) {
+#pragma unroll
+        for (int q = 0; q < kSimSyms; ++q)
+            if (q == k.nd) { k.s[q] = b; k.c[q] = (uint32_t)d; }
+        ++k.nd;
+    } else {
+        ovf = true;
+    }
+}
+// max count and the smallest symbol holding it
+__device__ __forceinline__ void simcol_major(const SimCol &k, uint32_t &mx, uint8_t &sym) {
+    mx = 0;
+    sym = 255;
+#pragma unroll
+    for (int q = 0; q < kSimSyms; ++q)
+        if (q < k.nd && (k.c[q] > mx || (k.c[q] == mx && k.c[q] > 0 && k.s[q] < sym))) { mx = k.c[q]; sym = k.s[q]; }
+}
+
+// out[5*j] = (array_start, array_end, copies, full_start, full_end); ovf[j] = 1: redo on the host
+__global__ __launch_bounds__(256) void k_simple_extend(const uint8_t *__restrict__ t, int64_t n,
+                                                       const int64_t *__restrict__ cand, int64_t ncand,
+                                                       int64_t *__restrict__ out, uint8_t *__restrict__ ovf_out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= ncand) return;   // wave-uniform
+    const int64_t s0 = cand[2 * j];
+    const int64_t pw = cand[2 * j + 1];
+    const int64_t p = pw & 0xFFFF;
+    const bool allow = (pw >> 16) & 1;
+    SimCol col[kSimCols];
+    uint8_t cons[kSimCols];
+    bool ovf = false;
+#pragma unroll
+    for (int k = 0; k < kSimCols; ++k) {
+        const int64_t c = lane + 64 * k;
+        col[k].nd = 0;
+        cons[k] = 0;
+        if (c < p) {
+            cons[k] = t[s0 + c];
+            simcol_add(col[k], cons[k], 1, ovf);
+        }
+    }
+    int64_t start = s0, end = s0 + p, copies = 1;
+    // extend right, then left, by whole copies (bwt.py:2417-2475)
+    for (int dir = 0; dir < 2; ++dir) {
+        for (;;) {
+            const int64_t at = dir == 0 ? end : start - p;
+            if (dir == 0 ? (end + p > n) : (start - p < 0)) break;
+            const int64_t tc = copies + 1;
+            int mm = 0;
+#pragma unroll
+            for (int k = 0; k < kSimCols; ++k) {
+                const int64_t c = lane + 64 * k;
+                if (c < p) {
+                    simcol_add(col[k], t[at + c], 1, ovf);
+                    uint32_t mx;
+                    uint8_t sy;
+                    simcol_major(col[k], mx, sy);
+                    mm += (int)(tc - mx);
+                }
+            }
+            const int64_t tot = wave_sum_i(mm);
+            const int64_t lim = allow ? max_mm_for_array_dev(p, tc) : 0;
+            if (tot <= lim) {
+                copies = tc;
+                if (dir == 0) end += p;
+                else start -= p;
+#pragma unroll
+                for (int k = 0; k < kSimCols; ++k) {
+                    const int64_t c = lane + 64 * k;
+                    if (c < p) {
+                        uint32_t mx;
+                        uint8_t sy;
+                        simcol_major(col[k], mx, sy);
+                        cons[k] = sy;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < kSimCols; ++k) {
+                    const int64_t c = lane + 64 * k;
+                    if (c < p) simcol_add(col[k], t[at + c], -1, ovf);
+                }
+                break;
+            }
+        }
+    }
+    // partial copies, exact matches only (bwt.py:2480-2496): first failing offset
+    int pr = (int)p, pl = (int)p;
+#pragma unroll
+    for (int k = 0; k < kSimCols; ++k) {
+        const int64_t c = lane + 64 * k;
+        if (c < p) {
+            if (!(end + c < n && t[end + c] == cons[k])) pr = min(pr, (int)c);
+            const int64_t kk = p - 1 - c;                       // left offset whose consensus column is c
+            if (!(start - kk - 1 >= 0 && t[start - kk - 1] == cons[k])) pl = min(pl, (int)kk);
+        }
+    }
+    pr = wave_min_i(pr);
+    pl = wave_min_i(pl);
+    const int any_ovf = wave_sum_i(ovf ? 1 : 0);
+    if (lane == 0) {
+        out[5 * j] = start - pl;
+        out[5 * j + 1] = end + pr;
+        out[5 * j + 2] = copies;
+        out[5 * j + 3] = start;
+        out[5 * j + 4] = end;
+        ovf_out[j] = any_ovf ? 1 : 0;
+    }
 }
 
 // --------------------------------------------------- host-side exact helpers
@@ -878,6 +1033,288 @@ void tier3_device(Ctx &c, DeviceIndex *ix, const uint8_t *reads, const int64_t *
         }
     }
     out.push_back(std::move(cur));
+}
+
+
+// ------------------------------------------------- simple period scan (host)
+namespace {
+struct SimRes {
+    int64_t as, ae, copies, fs, fe;
+};
+
+inline int64_t max_mm_for_array_host(int64_t L, int64_t c) {
+    const int64_t tot = L * c;
+    if (L == 1) return 0;
+    const double f = L <= 6 ? 0.05 : 0.08;
+    return std::max<int64_t>(1, (int64_t)std::ceil(f * (double)tot));
+}
+
+// _extend_with_mismatches (bwt.py:2392-2498), exact, any alphabet
+SimRes simple_extend_host(const uint8_t *t, int64_t n, int64_t s0, int64_t p, bool allow) {
+    std::vector<std::array<uint32_t, 256>> cnt((size_t)p);
+    for (auto &a : cnt) a.fill(0);
+    std::string cons((const char *)t + s0, (size_t)p);
+    for (int64_t c = 0; c < p; ++c) ++cnt[(size_t)c][t[s0 + c]];
+    int64_t start = s0, end = s0 + p, copies = 1;
+    auto major = [&](int64_t c, uint32_t &mx) {
+        mx = 0;
+        int sym = 0;
+        for (int b = 0; b < 256; ++b)
+            if (cnt[(size_t)c][(size_t)b] > mx) { mx = cnt[(size_t)c][(size_t)b]; sym = b; }
+        return (char)sym;
+    };
+    for (int dir = 0; dir < 2; ++dir) {
+        for (;;) {
+            if (dir == 0 ? (end + p > n) : (start - p < 0)) break;
+            const int64_t at = dir == 0 ? end : start - p;
+            const int64_t tc = copies + 1;
+            int64_t mm = 0;
+            for (int64_t c = 0; c < p; ++c) {
+                ++cnt[(size_t)c][t[at + c]];
+                uint32_t mx;
+                major(c, mx);
+                mm += tc - mx;
+            }
+            if (mm <= (allow ? max_mm_for_array_host(p, tc) : 0)) {
+                copies = tc;
+                if (dir == 0) end += p;
+                else start -= p;
+                uint32_t mx;
+                for (int64_t c = 0; c < p; ++c) cons[(size_t)c] = major(c, mx);
+            } else {
+                for (int64_t c = 0; c < p; ++c) --cnt[(size_t)c][t[at + c]];
+                break;
+            }
+        }
+    }
+    int64_t pr = 0, pl = 0;
+    while (pr < p && end + pr < n && t[end + pr] == (uint8_t)cons[(size_t)pr]) ++pr;
+    while (pl < p && start - pl - 1 >= 0 && t[start - pl - 1] == (uint8_t)cons[(size_t)(p - 1 - pl)]) ++pl;
+    return SimRes{start - pl, end + pr, copies, start, end};
+}
+
+struct SimWalk {
+    int64_t p = 0, i = 0, iters = 0;
+    bool done = false;
+    std::vector<int64_t> accepts;   // positions i whose first extension was accepted, in walk order
+    std::vector<int64_t> acc_iter;  // iteration number (1-based, within the walk) of each
+};
+}  // namespace
+
+// Tier2LCPFinder.find_long_repeats -> _find_repeats_simple (bwt.py:2097-2106,
+// 2177-2390).  Walks (one per period) are independent: a step's outcome depends
+// only on (position, period), and the seen-key set only decides which records
+// are kept.  So every walk is simulated on the host, and the first extensions it
+// needs (the costly part) are evaluated on the device in rounds of look-ahead
+// batches -- the next kLook positions of the walk that pass the cheap tests
+// (Tier 1 mask, '$'/'N', entropy), as if nothing were accepted before them.  The
+// walks are then replayed in period order under the reference's global
+// iteration cap (100,000) to build the records.  The reference also stops after
+// 30 s of wall time (2238-2257); that machine-dependent stop is not reproduced.
+void simple_scan_device(Ctx &c, DeviceIndex *ix, const LibParams &P, const std::vector<int64_t> &seen_pairs,
+                        int32_t chrom, std::vector<Rec> &out) {
+    const int64_t nt = index_n(ix);
+    if (nt == 0) return;
+    std::vector<uint8_t> text((size_t)nt);
+    index_get_text(c, ix, text.data());
+    const uint8_t *t = text.data();
+    int64_t n = nt;
+    if (t[n - 1] == '$') --n;
+    int64_t max_p = std::min<int64_t>(P.max_period, std::max<int64_t>(1, n / 2));
+    if (n > 100000) max_p = std::min<int64_t>(max_p, 30);
+    else if (n > 10000) max_p = std::min<int64_t>(max_p, 50);
+    else if (n > 1000) max_p = std::min<int64_t>(max_p, 100);
+    else max_p = std::min<int64_t>(max_p, 200);
+    const int64_t min_p = std::min<int64_t>(P.min_period, max_p);
+    int64_t step, pstep;
+    if (n > 10000000) { step = 500; pstep = 20; }
+    else if (n > 5000000) { step = 200; pstep = 10; }
+    else if (n > 1000000) { step = 100; pstep = 5; }
+    else if (n > 100000) { step = 50; pstep = 2; }
+    else if (n > 10000) { step = 20; pstep = 1; }
+    else { step = 10; pstep = 1; }
+    constexpr int64_t kMaxIter = 100000;
+    std::vector<uint8_t> mask((size_t)std::max<int64_t>(n, 1), 0);
+    for (size_t q = 0; q + 1 < seen_pairs.size(); q += 2)
+        for (int64_t x = std::max<int64_t>(0, seen_pairs[q]); x < std::min(seen_pairs[q + 1], n); ++x) mask[(size_t)x] = 1;
+    std::vector<SimWalk> walks;
+    for (int64_t p = min_p; p <= max_p; p += pstep) {
+        SimWalk w;
+        w.p = p;
+        walks.push_back(w);
+    }
+    // cheap tests of position i for period p: true = the first extension is needed
+    auto needs_ext = [&](int64_t i, int64_t p) {
+        if (i < n && mask[(size_t)i]) return false;
+        for (int64_t q = 0; q < p; ++q)
+            if (t[i + q] == '$' || t[i + q] == 'N') return false;
+        return !(entropy_of((const char *)t + i, p) < P.min_entropy);
+    };
+    const bool allow_all = P.allow_mismatches != 0;
+    std::vector<std::unordered_map<int64_t, SimRes>> ext(walks.size());
+    constexpr int kLook = 512;   // look-ahead positions per walk and round
+    hipStream_t st = c.stream;
+    for (;;) {
+        // advance every walk until it needs an unknown extension; collect look-ahead requests
+        std::vector<int64_t> req;        // (i, p | allow << 16)
+        std::vector<int32_t> req_w;
+        int64_t lower = 0;               // iterations the earlier walks (period order) take at least
+        for (size_t wi = 0; wi < walks.size(); ++wi) {
+            SimWalk &w = walks[wi];
+            const int64_t p = w.p;
+            const bool allow = allow_all && p <= 64;
+            while (!w.done) {
+                if (w.i + 2 * p > n) { w.done = true; break; }
+                if (lower + w.iters + 1 > kMaxIter) { w.done = true; break; }   // beyond the global cap
+                const int64_t i = w.i;
+                if (!needs_ext(i, p)) { ++w.iters; w.i += step; continue; }
+                auto it = ext[wi].find(i);
+                if (it == ext[wi].end() && p > kSimMaxP) {            // wider than a wave's columns
+                    ext[wi][i] = simple_extend_host(t, n, i, p, allow);
+                    it = ext[wi].find(i);
+                }
+                if (it == ext[wi].end()) {
+                    for (int64_t q = 0, j = i; q < kLook && j + 2 * p <= n; j += step) {
+                        if (!needs_ext(j, p) || ext[wi].count(j)) continue;
+                        req.push_back(j);
+                        req.push_back(p | (allow ? (1 << 16) : 0));
+                        req_w.push_back((int32_t)wi);
+                        ++q;
+                    }
+                    break;
+                }
+                ++w.iters;
+                const SimRes &r = it->second;
+                const int64_t alen = r.ae - r.as;
+                bool acc = false;
+                if (alen >= P.min_array_length) {
+                    const int64_t part = std::max<int64_t>(0, alen - r.copies * p);
+                    const double pf = (double)part / (double)p;
+                    const int64_t eff = r.copies + (pf >= 0.75 ? 1 : 0);
+                    acc = r.copies >= P.min_copies || eff >= P.min_copies;
+                }
+                if (!acc) { w.i += step; continue; }
+                w.accepts.push_back(i);
+                w.acc_iter.push_back(w.iters);
+                // the walk resumes at the (second-extension) array end, decided on the host
+                const int64_t fs = r.fs;
+                const int64_t prim = smallest_period((const char *)t + fs, p);
+                const int64_t pe = prim < p ? prim : p;
+                const SimRes r2 = simple_extend_host(t, n, fs, pe, allow_all && pe <= 64);
+                int64_t ae = r2.ae;
+                const int64_t alen2 = r2.ae - r2.as;
+                const int64_t part2 = std::max<int64_t>(0, alen2 - r2.copies * pe);
+                const double pf2 = (double)part2 / (double)pe;
+                const int64_t eff2 = r2.copies + (pf2 >= 0.75 ? 1 : 0);
+                if (r2.copies < P.min_copies && eff2 < P.min_copies) { w.i += step; continue; }
+                std::string cons;
+                double mm = 0;
+                int64_t maxmm = 0;
+                if (!consensus_array(t, nt, r2.fs, pe, r2.copies, cons, mm, maxmm)) { w.i += step; continue; }
+                const int64_t pl = smallest_period(cons.data(), (int64_t)cons.size());
+                if (pl < (int64_t)cons.size()) {
+                    const int64_t cf = std::max<int64_t>(1, (r2.ae - r2.as) / pl);
+                    ae = r2.as + cf * pl;
+                    if (!consensus_array(t, nt, r2.as, pl, cf, cons, mm, maxmm)) { w.i += step; continue; }
+                }
+                w.i = ae;
+            }
+            lower += w.iters;
+        }
+        if (req.empty()) {
+            for (auto &w : walks)
+                if (!w.done) fail(BWTMI_E_STATE, "simple scan: walk of period %lld stalled", (long long)w.p);
+            break;
+        }
+        // device batch
+        const int64_t nr = (int64_t)req_w.size();
+        c.slot[S_IDX0].ensure((size_t)nt + 64);
+        c.slot[S_IDX1].ensure((size_t)nr * 16);
+        c.slot[S_IDX2].ensure((size_t)nr * 40);
+        c.slot[S_IDX3].ensure((size_t)nr);
+        HIPCHECK(hipMemcpyAsync(c.slot[S_IDX0].p, t, (size_t)nt, hipMemcpyHostToDevice, st));
+        HIPCHECK(hipMemcpyAsync(c.slot[S_IDX1].p, req.data(), (size_t)nr * 16, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_simple_extend, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, st,
+                           c.slot[S_IDX0].as<uint8_t>(), n, c.slot[S_IDX1].as<int64_t>(), nr,
+                           c.slot[S_IDX2].as<int64_t>(), c.slot[S_IDX3].as<uint8_t>());
+        HIPCHECK(hipGetLastError());
+        std::vector<int64_t> res((size_t)nr * 5);
+        std::vector<uint8_t> ovf((size_t)nr);
+        HIPCHECK(hipMemcpyAsync(res.data(), c.slot[S_IDX2].p, (size_t)nr * 40, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(ovf.data(), c.slot[S_IDX3].p, (size_t)nr, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        for (int64_t q = 0; q < nr; ++q) {
+            const int64_t i = req[(size_t)(2 * q)], pw = req[(size_t)(2 * q + 1)];
+            SimRes r;
+            if (ovf[(size_t)q])
+                r = simple_extend_host(t, n, i, pw & 0xFFFF, (pw >> 16) & 1);
+            else
+                r = SimRes{res[(size_t)(5 * q)], res[(size_t)(5 * q + 1)], res[(size_t)(5 * q + 2)],
+                           res[(size_t)(5 * q + 3)], res[(size_t)(5 * q + 4)]};
+            ext[(size_t)req_w[(size_t)q]][i] = r;
+        }
+    }
+    // replay in period order under the global cap: records of the accepted positions
+    std::set<std::tuple<int64_t, int64_t, std::string>> seen;
+    const std::string seq((const char *)t, (size_t)nt);
+    AlignSummary summ;
+    int64_t cum = 0;
+    for (size_t wi = 0; wi < walks.size(); ++wi) {
+        const SimWalk &w = walks[wi];
+        const int64_t p = w.p;
+        for (size_t a = 0; a < w.accepts.size(); ++a) {
+            if (cum + w.acc_iter[a] > kMaxIter) break;
+            const SimRes &r = ext[wi].at(w.accepts[a]);
+            const int64_t prim = smallest_period((const char *)t + r.fs, p);
+            int64_t pe = prim < p ? prim : p;
+            const SimRes r2 = simple_extend_host(t, n, r.fs, pe, allow_all && pe <= 64);
+            int64_t as = r2.as, ae = r2.ae, cf = r2.copies;
+            const int64_t alen2 = ae - as;
+            const int64_t part2 = std::max<int64_t>(0, alen2 - cf * pe);
+            const double pf2 = (double)part2 / (double)pe;
+            const int64_t eff2 = cf + (pf2 >= 0.75 ? 1 : 0);
+            if (cf < P.min_copies && eff2 < P.min_copies) continue;
+            std::string cons;
+            double mm = 0;
+            int64_t maxmm = 0;
+            if (!consensus_array(t, nt, r2.fs, pe, cf, cons, mm, maxmm)) continue;
+            const int64_t pl = smallest_period(cons.data(), (int64_t)cons.size());
+            if (pl < (int64_t)cons.size()) {
+                pe = pl;
+                cf = std::max<int64_t>(1, (ae - as) / pe);
+                ae = as + cf * pe;
+                if (!consensus_array(t, nt, as, pe, cf, cons, mm, maxmm)) continue;
+            }
+            std::string canon;
+            char strand = '+';
+            canonical_stranded(cons, canon, strand);
+            if (!seen.insert(std::make_tuple(as, ae, canon)).second) continue;
+            Rec rec;
+            rec.chrom = chrom;
+            rec.tier = 2;
+            rec.start = as;
+            rec.end = ae;
+            rec.length = ae - as;
+            rec.motif = cons;
+            rec.copies = (double)cf;
+            rec.confidence = std::max(0.5, 0.95 - mm);
+            rec.mismatch_rate = mm;
+            rec.max_mm = maxmm;
+            rec.n_eval = cf;
+            rec.strand = strand;
+            rec.pmatch = (1.0 - mm) * 100.0;
+            rec.pindel = 0.0;
+            rec.score = trf_score(ae - as, mm);
+            rec.act_kind = ACT_FULL;
+            rec.act_off = as;
+            rec.act_len = ae - as;
+            if (ae > as && align_repeat_region(seq.data(), nt, as, ae, cons, 1, summ) && summ.any_variation)
+                rec.variations = summ.variations;
+            out.push_back(std::move(rec));
+        }
+        cum += w.iters;
+        if (cum >= kMaxIter) break;
+    }
 }
 
 }  // namespace bwtmi

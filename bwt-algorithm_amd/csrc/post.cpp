@@ -296,21 +296,40 @@ inline double conf_of(const Item &it) { return it.x ? it.x->confidence : 0.95; }
 void sort_by_pos(ItemVec &v, int nt) {
     const size_t n = v.size();
     if (n < 2) return;
+    // order checks in parallel chunks (each chunk also checks the pair across its left edge)
+    const int C = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt * 4, n / 32768 + 1));
+    std::vector<uint8_t> c_sorted((size_t)C, 1), c_start((size_t)C, 1);
+    parallel_items(C, nt, [&](int64_t t, int) {
+        const size_t a = std::max<size_t>(1, n * (size_t)t / (size_t)C), b = n * (size_t)(t + 1) / (size_t)C;
+        bool so = true, bs = true;
+        for (size_t i = a; i < b && bs; ++i) {
+            bs = v[i - 1].start <= v[i].start;
+            so = so && (v[i - 1].start < v[i].start || v[i - 1].end <= v[i].end);
+        }
+        c_sorted[(size_t)t] = so;
+        c_start[(size_t)t] = bs;
+    });
     bool sorted = true, by_start = true;
-    for (size_t i = 1; i < n && by_start; ++i) {
-        by_start = v[i - 1].start <= v[i].start;
-        sorted = sorted && (v[i - 1].start < v[i].start || v[i - 1].end <= v[i].end);
+    for (int t = 0; t < C; ++t) {
+        sorted = sorted && c_sorted[(size_t)t];
+        by_start = by_start && c_start[(size_t)t];
     }
     if (sorted && by_start) return;
     if (by_start) {   // the usual case after merge/refine: only equal-start runs need ordering by end
-        size_t i = 0;
-        while (i < n) {
-            size_t j = i + 1;
-            while (j < n && v[j].start == v[i].start) ++j;
-            if (j - i > 1)
-                std::stable_sort(v.begin() + i, v.begin() + j, [](const Item &a, const Item &b) { return a.end < b.end; });
-            i = j;
-        }
+        // chunk t orders the runs that begin inside it
+        parallel_items(C, nt, [&](int64_t t, int) {
+            size_t i = n * (size_t)t / (size_t)C;
+            const size_t b = n * (size_t)(t + 1) / (size_t)C;
+            while (i > 0 && i < b && v[i - 1].start == v[i].start) ++i;
+            while (i < b) {
+                size_t j = i + 1;
+                while (j < n && v[j].start == v[i].start) ++j;
+                if (j - i > 1)
+                    std::stable_sort(v.begin() + (std::ptrdiff_t)i, v.begin() + (std::ptrdiff_t)j,
+                                     [](const Item &x, const Item &y) { return x.end < y.end; });
+                i = j;
+            }
+        });
         return;
     }
     auto lt = [](const Item &a, const Item &b) {
@@ -409,7 +428,7 @@ ItemVec suppress_nested(const ItemVec &rs, double thr, int nt) {
 }
 
 // optional counters (BWTMI_STATS=1): recompute calls / time, merge accepts
-std::atomic<int64_t> g_recomputes{0}, g_recompute_ns{0}, g_merges{0}, g_canons{0};
+std::atomic<int64_t> g_recomputes{0}, g_recompute_ns{0}, g_merges{0}, g_canons{0}, g_tests{0}, g_same{0};
 const bool g_stats = [] { const char *e = std::getenv("BWTMI_STATS"); return e && *e == '1'; }();
 std::atomic<int64_t> g_hist_n[8][8], g_hist_ns[8][8];   // [log4 motif len][log4 region len]
 inline int lg4(int64_t v) { int k = 0; while (v >= 4 && k < 7) { v >>= 2; ++k; } return k; }
@@ -572,14 +591,16 @@ bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, Canon &c1,
     if (r1.mlen == 0 || r2.mlen == 0) return false;
     const int64_t ml = std::min(r1.mlen, r2.mlen);
     if (std::max<int64_t>(0, r2.start - r1.end) > ml + 1) return false;   // cheap test first
+    if (g_stats) g_tests.fetch_add(1, std::memory_order_relaxed);
     if (!same_canonical(u, r1, c1, r2, c2)) return false;
+    if (g_stats) g_same.fetch_add(1, std::memory_order_relaxed);
     const int64_t s = std::min(r1.start, r2.start), e = std::max(r1.end, r2.end);
     const int32_t tier = std::min(r1.tier, r2.tier);
     Item mg = recompute(u, pools, w, r1.chrom, s, e, std::max<int64_t>(1, ml), tier);
     if (mg.x->copies < (double)u.min_copies) return false;
     const double base = std::max(std::max(mm_of(r1), mm_of(r2)), 0.01);
     if (!(mg.x->mm <= base + 0.2)) return false;
-    g_merges.fetch_add(1, std::memory_order_relaxed);
+    if (g_stats) g_merges.fetch_add(1, std::memory_order_relaxed);
     if ((int64_t)r1.mlen == std::max<int64_t>(1, ml)) merged = mg;   // len(r1.consensus_motif)
     else merged = recompute(u, pools, w, r1.chrom, s, e, r1.mlen, tier);
     return true;
@@ -884,33 +905,44 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     recs = merge_fold(u, pools, recs, nt);
     auto t3 = clk::now();
     // 4. refine (bwt.py:3291-3314): only recomputed records can carry mismatches
-    std::vector<uint32_t> imperfect;
-    for (size_t k = 0; k < recs.size(); ++k)
-        if (recs[k].x && recs[k].x->mm != 0.0) imperfect.push_back((uint32_t)k);
-    parallel_items((int64_t)imperfect.size(), nt, [&](int64_t q, int w) {
-        Item &r = recs[imperfect[(size_t)q]];
-        int64_t m = r.mlen;
-        if (m <= 0) {
-            const int64_t rc = (int64_t)std::nearbyint(copies_of(r));
-            m = std::max<int64_t>(1, (r.end - r.start) / std::max<int64_t>(1, rc ? rc : 1));
-        }
-        r = recompute(u, pools, w, r.chrom, r.start, r.end, m, r.tier);
-    });
+    //    (dynamic chunks: recomputes cluster along the contig)
+    {
+        const int64_t nr = (int64_t)recs.size(), CH = 4096;
+        parallel_items((nr + CH - 1) / CH, nt, [&](int64_t ch, int w) {
+            const int64_t a = ch * CH, b = std::min(nr, a + CH);
+            for (int64_t k = a; k < b; ++k) {
+                Item &r = recs[(size_t)k];
+                if (!r.x || r.x->mm == 0.0) continue;
+                int64_t m = r.mlen;
+                if (m <= 0) {
+                    const int64_t rc = (int64_t)std::nearbyint(copies_of(r));
+                    m = std::max<int64_t>(1, (r.end - r.start) / std::max<int64_t>(1, rc ? rc : 1));
+                }
+                r = recompute(u, pools, w, r.chrom, r.start, r.end, m, r.tier);
+            }
+        });
+    }
     auto r1 = clk::now();
     sort_by_pos(recs, nt);
     auto r2 = clk::now();
-    // 5. restore coordinates (bwt.py:3316-3325); actual_sequence is the frame slice
-    for (auto &r : recs) {
-        const int64_t off = job.contigs[(size_t)r.chrom].trim_left;
-        r.start += off;
-        r.end += off;
-    }
+    // 5. restore coordinates (bwt.py:3316-3325); actual_sequence is the frame slice.
+    //    With one trim offset for the whole unit the (start, end) order is unchanged.
+    bool one_offset = true;
+    for (int32_t c : chroms) one_offset = one_offset && job.contigs[(size_t)c].trim_left == job.contigs[(size_t)chroms[0]].trim_left;
+    parallel_for((int64_t)recs.size(), nt, [&](int64_t a, int64_t b) {
+        for (int64_t k = a; k < b; ++k) {
+            Item &r = recs[(size_t)k];
+            const int64_t off = job.contigs[(size_t)r.chrom].trim_left;
+            r.start += off;
+            r.end += off;
+        }
+    });
     // 6. collapse (bwt.py:3499-3513)
-    sort_by_pos(recs, nt);
+    if (!one_offset) sort_by_pos(recs, nt);
     auto r3 = clk::now();
     const size_t n_before_collapse = recs.size();
     std::vector<uint32_t> col;   // collapsed list as indices into recs (the slot takes the preferred record)
-    col.reserve(recs.size());
+    col.reserve(recs.size() / 4 + 16);
     for (size_t k = 0; k < recs.size(); ++k) {
         if (!col.empty() && should_collapse(u, recs[col.back()], recs[k])) {
             if (!prefer_first(u, recs[col.back()], recs[k])) col.back() = (uint32_t)k;
@@ -919,14 +951,23 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
         }
     }
     auto r4 = clk::now();
-    // 7. final filter (bwt.py:3940-3944)
-    std::vector<uint32_t> keep;
-    for (uint32_t i : col)
-        if (copies_of(recs[i]) >= (double)job.params.min_copies && recs[i].end - recs[i].start >= 6)
-            keep.push_back(i);
-    out.resize(keep.size());
-    parallel_for((int64_t)keep.size(), nt, [&](int64_t a, int64_t b) {
-        for (int64_t q = a; q < b; ++q) out[(size_t)q] = materialize(u, recs[keep[(size_t)q]]);
+    // 7. final filter (bwt.py:3940-3944), counted and materialised in parallel chunks
+    const double mc = (double)job.params.min_copies;
+    auto pass = [&](uint32_t i) { return copies_of(recs[i]) >= mc && recs[i].end - recs[i].start >= 6; };
+    const int64_t ncol = (int64_t)col.size();
+    const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nt, ncol / 16384 + 1));
+    std::vector<int64_t> cnt((size_t)T + 1, 0);
+    parallel_items(T, T, [&](int64_t t, int) {
+        int64_t c = 0;
+        for (int64_t q = ncol * t / T; q < ncol * (t + 1) / T; ++q) c += pass(col[(size_t)q]);
+        cnt[(size_t)t + 1] = c;
+    });
+    for (int t = 0; t < T; ++t) cnt[(size_t)t + 1] += cnt[(size_t)t];
+    out.resize((size_t)cnt[(size_t)T]);
+    parallel_items(T, T, [&](int64_t t, int) {
+        int64_t o = cnt[(size_t)t];
+        for (int64_t q = ncol * t / T; q < ncol * (t + 1) / T; ++q)
+            if (pass(col[(size_t)q])) out[(size_t)o++] = materialize(u, recs[col[(size_t)q]]);
     });
     auto t4 = clk::now();
     if (std::getenv("BWTMI_STATS")) {
@@ -986,6 +1027,9 @@ void postprocess(Job &job) {
         std::fprintf(stderr, "[bwtmi] recomputes=%lld (%.1f ms thread-summed) merges=%lld canons=%lld final=%zu\n",
                      (long long)g_recomputes.exchange(0), g_recompute_ns.exchange(0) / 1e6,
                      (long long)g_merges.exchange(0), (long long)g_canons.exchange(0), job.final_recs.size());
+    if (const char *e = std::getenv("BWTMI_STATS"); e && *e == '1')
+        std::fprintf(stderr, "[bwtmi] merge tests past the gap test=%lld, same canonical=%lld\n",
+                     (long long)g_tests.exchange(0), (long long)g_same.exchange(0));
     if (const char *e = std::getenv("BWTMI_STATS"); e && *e == '1')
         for (int a = 0; a < 8; ++a)
             for (int b = 0; b < 8; ++b)

@@ -122,6 +122,12 @@ int bwtmi_index_lcp_plateaus(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_lib_p
  * the index text; seen = nseen (start, end) pairs (tier1_seen) */
 int bwtmi_index_short_imperfect(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_lib_params *p,
                                 const int64_t *seen, int64_t nseen, bwtmi_job *job, int32_t contig_id);
+/* find_long_repeats(chromosome, tier1_seen) -> _find_repeats_simple (bwt.py:2097-2106,
+ * 2177-2498): adaptive period/position scan with majority-vote extension; records appended to
+ * job's final records with contig contig_id (the reference's extra 30 s wall-clock stop,
+ * bwt.py:2238-2257, is not reproduced; its 100,000-iteration cap is) */
+int bwtmi_index_long_repeats(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_lib_params *p,
+                             const int64_t *seen, int64_t nseen, bwtmi_job *job, int32_t contig_id);
 /* Tier1STRFinder(text_arr, max_motif_length).find_strs (bwt.py:1426-1538) over the full
  * sequence of the job's contig contig_id; records appended to the job's final records */
 int bwtmi_job_tier1(bwtmi_ctx *ctx, bwtmi_job *job, int32_t contig_id, int32_t max_motif_length);

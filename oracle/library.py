@@ -12,6 +12,11 @@ Reference: /root/reference/bwt.py (wyim-pgl/bwt-algorithm @ 2025-11-14).
                     -> _analyze_sa_interval_for_tandems (2500-2549),
                     _validate_periodicity_arr (2551-2560)   (A2-9)
   tier1_find_strs   Tier1STRFinder.find_strs (1426-1538)    (§8(f) #2)
+  find_repeats_simple  Tier2LCPFinder.find_long_repeats -> _find_repeats_simple
+                    (2097-2106, 2177-2390) with _extend_with_mismatches
+                    (2392-2498): adaptive period/position scan with
+                    majority-vote extension (§8(f) #4; the reference's 30 s
+                    wall-clock stop is not restated)
   tier3             Tier3LongReadFinder.find_very_long_repeats (2837-3036):
                     500-byte windows every 100 bytes of each read >= 1000,
                     self-periodicity 10..165, unique 50-byte anchor -> FM
@@ -481,3 +486,191 @@ def tier3(text: bytes, reads: List[bytes], chromosome: str, idx=None) -> List[Di
             cur = r
     out.append(cur)
     return out
+
+
+# ------------------------------------------------- simple period scan
+def _smallest_period_kmp(a: bytes) -> int:          # _smallest_period_codes, bwt.py:2161-2175
+    n = len(a)
+    if n == 0:
+        return 0
+    pi = [0] * n
+    j = 0
+    for i in range(1, n):
+        while j > 0 and a[i] != a[j]:
+            j = pi[j - 1]
+        if a[i] == a[j]:
+            j += 1
+        pi[i] = j
+    p = n - pi[-1]
+    return p if p != 0 and n % p == 0 else n
+
+
+def _majority_full(cps: List[bytes], L: int) -> bytes:
+    out = bytearray(L)
+    for pos in range(L):
+        cnt = Counter(c[pos] for c in cps if pos < len(c))
+        if cnt:
+            best = max(cnt.values())
+            out[pos] = min(b for b, v in cnt.items() if v == best)
+    return bytes(out)
+
+
+def extend_with_mismatches(t: bytes, start_pos: int, period: int, n: int, allow: bool):
+    """_extend_with_mismatches (bwt.py:2392-2498) -> (array_start, array_end,
+    copies, full_start, full_end)."""
+    motif = t[start_pos:start_pos + period]
+    start, end, copies = start_pos, start_pos + period, 1
+    consensus = motif
+
+    def total_mm(s, e, cons):
+        tot = 0
+        for i in range((e - s) // period):
+            a = s + i * period
+            if a + period <= n:
+                tot += sum(1 for x, y in zip(t[a:a + period], cons) if x != y)
+        return tot
+
+    while end + period <= n:
+        tc = copies + 1
+        cps = [t[start + i * period:start + i * period + period] for i in range(tc)
+               if start + i * period + period <= n]
+        cons = _majority_full(cps, period)
+        mx = max_mismatches_for_array(period, tc) if allow else 0
+        if total_mm(start, end + period, cons) <= mx:
+            copies, end, consensus = tc, end + period, cons
+        else:
+            break
+    while start - period >= 0:
+        tc = copies + 1
+        ts = start - period
+        cps = [t[ts + i * period:ts + i * period + period] for i in range(tc) if ts + i * period + period <= n]
+        cons = _majority_full(cps, period)
+        mx = max_mismatches_for_array(period, tc) if allow else 0
+        if total_mm(ts, end, cons) <= mx:
+            copies, start, consensus = tc, ts, cons
+        else:
+            break
+    fs, fe = start, end
+    pr = 0
+    while pr < period and fe + pr < n:
+        if t[fe + pr] != consensus[pr % period]:
+            break
+        pr += 1
+    pl = 0
+    while pl < period and fs - pl - 1 >= 0:
+        if t[fs - pl - 1] != consensus[period - 1 - (pl % period)]:
+            break
+        pl += 1
+    return fs - pl, fe + pr, copies, fs, fe
+
+
+def find_repeats_simple(chromosome: str, text: bytes, tier1_seen=(), min_period: int = 1,
+                        max_period: int = 1000, allow_mismatches: bool = True, min_entropy: float = 1.0,
+                        min_copies: int = 3, min_array_length: int = 6, max_iterations: int = 100_000):
+    """Tier2LCPFinder._find_repeats_simple (bwt.py:2177-2390) behind
+    find_long_repeats (2097-2106).  The reference also stops after 30 s of
+    wall time (2238-2257), which makes its output machine-dependent; this
+    restatement (like the device path) never times out -- it is the
+    reference's result whenever the reference finishes within its limit."""
+    n = len(text)
+    if n > 0 and text[n - 1] == 36:
+        n -= 1
+    max_p = min(max_period, max(1, n // 2))
+    if n > 100_000:
+        max_p = min(max_p, 30)
+    elif n > 10_000:
+        max_p = min(max_p, 50)
+    elif n > 1_000:
+        max_p = min(max_p, 100)
+    else:
+        max_p = min(max_p, 200)
+    min_p = min(min_period, max_p)
+    mask = bytearray(n)
+    for s, e in tier1_seen:
+        for x in range(max(0, s), min(e, n)):
+            mask[x] = 1
+    if n > 10_000_000:
+        step, pstep = 500, 20
+    elif n > 5_000_000:
+        step, pstep = 200, 10
+    elif n > 1_000_000:
+        step, pstep = 100, 5
+    elif n > 100_000:
+        step, pstep = 50, 2
+    elif n > 10_000:
+        step, pstep = 20, 1
+    else:
+        step, pstep = 10, 1
+    results, seen = [], set()
+    it = 0
+    for p in range(min_p, max_p + 1, pstep):
+        i = 0
+        while i + 2 * p <= n:
+            it += 1
+            if it > max_iterations:
+                return results
+            if i < n and mask[i]:
+                i += step
+                continue
+            mv = text[i:i + p]
+            if 36 in mv or 78 in mv:
+                i += step
+                continue
+            if entropy(mv.decode("ascii", errors="replace")) < min_entropy:
+                i += step
+                continue
+            a_s, a_e, cf, fs, fe = extend_with_mismatches(text, i, p, n, allow_mismatches and p <= 64)
+            alen = a_e - a_s
+            if alen < min_array_length:
+                i += step
+                continue
+            part = max(0, alen - cf * p)
+            pf = part / p if p > 0 else 0.0
+            eff_i = cf + (1 if pf >= 0.75 else 0)
+            if cf >= min_copies or eff_i >= min_copies:
+                mv = text[fs:fs + p]
+                prim = _smallest_period_kmp(mv)
+                pe = prim if prim < p else p
+                a_s, a_e, cf, fs, fe = extend_with_mismatches(text, fs, pe, n, allow_mismatches and pe <= 64)
+                alen = a_e - a_s
+                part = max(0, alen - cf * pe)
+                pf = part / pe if pe > 0 else 0.0
+                eff_i = cf + (1 if pf >= 0.75 else 0)
+                eff_f = cf + pf
+                if cf < min_copies and eff_i < min_copies:
+                    i += step
+                    continue
+                carr, mm, mxm = consensus_array(text, fs, pe, cf)
+                if not carr:
+                    i += step
+                    continue
+                cons = carr.decode("ascii", errors="replace")
+                pl = post.smallest_period(cons)
+                if pl < len(cons):
+                    pe = pl
+                    cf = max(1, (a_e - a_s) // pe)
+                    a_e = a_s + cf * pe
+                    carr, mm, mxm = consensus_array(text, a_s, pe, cf)
+                    if not carr:
+                        i += step
+                        continue
+                    cons = carr.decode("ascii", errors="replace")
+                canon, strand = post.canonical_stranded(cons)
+                key = (a_s, a_e, canon)
+                if key not in seen:
+                    seen.add(key)
+                    conf = max(0.5, 0.95 - mm)
+                    pm, pi, sc, comp, ent, act = trf_statistics(text, a_s, a_e, cons, eff_f, mm)
+                    var = None
+                    seq = text.decode("ascii", errors="replace")
+                    s0, e0 = max(0, a_s), min(len(seq), a_e if a_e > a_s else len(seq))
+                    if e0 > s0 and pe > 0:
+                        summ = post.align_region(seq, s0, e0, cons, 0.1, None, 1)
+                        if summ and summ["variations"]:
+                            var = summ["variations"]
+                    results.append(_rec(chromosome, a_s, a_e, cons, float(cf), a_e - a_s, 2, conf, cons, mm, mxm,
+                                        cf, strand, pm, pi, sc, comp, ent, act, var))
+                i = a_e
+            else:
+                i += step
+    return results

@@ -17,6 +17,9 @@ here is product code.  Outputs land in tests/golden/ as small data files:
   tier3         Tier3LongReadFinder on seeded contigs + long reads (library
                 call) and the CLI with --tier3 --long-reads (FASTA and FASTQ
                 reads, four formats, parallel and sequential modes)
+  simple        Tier2LCPFinder.find_long_repeats (_find_repeats_simple) on
+                small seeded / crafted / edge contigs (each well inside the
+                reference's 30 s wall-clock stop)
   hybrid        reference post-processing with the strict scan (and the
                 O(k^2) nested-suppression loop) swapped for the oracle's
                 restatements -> full-size output SHA-256; the
@@ -499,6 +502,51 @@ def cmd_tier3(a):
         json.dump(out, f, indent=0)
 
 
+def cmd_simple(a):
+    """Tier2LCPFinder.find_long_repeats -> _find_repeats_simple (SURVEY.md §8(f)
+    #4) -> simple.json.  The reference stops after 30 s of wall time
+    (bwt.py:2238-2257); every case here finishes well inside it (the time is
+    recorded), so the stop never fired and the output is deterministic."""
+    ref = ref_module()
+    from bwtmi import synth
+    contigs, _ = _tier3_inputs()
+    cases = {
+        "imp1500": (synth.generate_contig(1500, 601, 0.03).decode(), {}),
+        "imp1200_nomm": (synth.generate_contig(1200, 604, 0.03).decode(), dict(allow_mismatches=False)),
+        "imp900": (synth.generate_contig(900, 602, 0.02).decode(), {}),
+        "long_t2_p20": (contigs["chrT2"][:1100], dict(min_period=20, max_period=60)),
+        "long_t1_p10": (contigs["chrT1"][:1200], dict(min_period=10, max_period=45)),
+        "imp11k_p40": (synth.generate_contig(11000, 603, 0.02).decode(), dict(min_period=40)),
+    }
+    with open(os.path.join(HERE, "inputs", "edge_mixed.fa")) as f:
+        cur = None
+        for line in f:
+            line = line.strip()
+            if line.startswith(">"):
+                cur = "edge_" + line[1:].split()[0]
+                cases[cur] = ("", {})
+            elif cur:
+                cases[cur] = (cases[cur][0] + line, {})
+    out = {}
+    for name, (seq, kw) in cases.items():
+        core = ref.BWTCore(seq + "$", 32)
+        f = ref.Tier2LCPFinder(core, **kw)
+        seen = set()
+        if name == "imp1500":   # with a Tier 1 mask, as the library's callers pass it
+            with contextlib.redirect_stdout(io.StringIO()):
+                seen = {(r.start, r.end) for r in ref.Tier1STRFinder(core.text_arr, 9, False).find_strs(name)}
+        t0 = time.time()
+        with contextlib.redirect_stdout(io.StringIO()):
+            recs = f.find_long_repeats(name, seen)
+        dt = time.time() - t0
+        assert dt < 29.5, f"{name}: {dt:.1f} s -- the reference's 30 s stop may have fired"
+        out[name] = dict(seq=seq, params=kw, tier1_seen=sorted(seen), records=[_rec_json(r) for r in recs],
+                         seconds=round(dt, 1))
+        print(name, len(seq), len(recs), round(dt, 1), flush=True)
+    with open(os.path.join(HERE, "simple.json"), "w") as f:
+        json.dump(out, f, indent=0)
+
+
 def cmd_hybrid(a):
     """Full-size golden via the validated hybrid oracle."""
     ref = ref_module()
@@ -542,6 +590,7 @@ def main():
     sp.add_parser("motif")
     sp.add_parser("library")
     sp.add_parser("tier3")
+    sp.add_parser("simple")
     p = sp.add_parser("hybrid")
     p.add_argument("name")
     p.add_argument("--config")
@@ -554,7 +603,7 @@ def main():
     p.add_argument("--save-out", action="store_true")
     a = ap.parse_args()
     dict(fixtures=cmd_fixtures, rawhits=cmd_rawhits, index=cmd_index, motif=cmd_motif,
-         hybrid=cmd_hybrid, library=cmd_library, tier3=cmd_tier3)[a.cmd](a)
+         hybrid=cmd_hybrid, library=cmd_library, tier3=cmd_tier3, simple=cmd_simple)[a.cmd](a)
 
 
 if __name__ == "__main__":
