@@ -116,7 +116,9 @@ def write_sharded(td, job, fmt: str, path: str, device="cpu") -> int:
     offsets = np.concatenate([[0, header], header + np.cumsum(sizes)[:-1]]).astype(np.int64)
     total = header + int(sizes.sum())
     if rank == 0:
-        with open(path, "wb") as f:
+        # sized in place: every byte of [0, total) is written below, so an
+        # existing file is overwritten (reusing its page-cache pages) and cut
+        with open(path, "r+b" if os.path.isfile(path) else "wb") as f:
             f.truncate(total)
     td.barrier()
     job.write_units(path, offsets, write_header=(rank == 0))

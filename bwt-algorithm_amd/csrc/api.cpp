@@ -75,14 +75,17 @@ static Ctx &use(Ctx &c) {
     return c;
 }
 
-// parts[k] lands at byte offset at[k] of `path`, in parallel (page-cache copies)
-static void pwrite_parts(const char *path, bool truncate, const std::vector<std::string> &parts,
+// parts[k] lands at byte offset at[k] of `path`, in parallel (page-cache copies).
+// `whole`: the parts are the whole file -- it is overwritten in place and cut to
+// at.back() bytes afterwards (the content is that of open(path, 'w') + write;
+// rewriting a file of the same size reuses its page-cache pages).
+static void pwrite_parts(const char *path, bool whole, const std::vector<Text> &parts,
                          const std::vector<size_t> &at, int threads) {
-    const int fd = ::open(path, O_WRONLY | O_CREAT | (truncate ? O_TRUNC : 0), 0644);
+    const int fd = ::open(path, O_WRONLY | O_CREAT, 0644);
     if (fd < 0) fail(BWTMI_E_IO, "cannot open %s for writing", path);
     std::vector<uint8_t> ok(parts.size(), 1);
     run_tasks((int64_t)parts.size(), threads, [&](int64_t k) {
-        const std::string &s = parts[(size_t)k];
+        const Text &s = parts[(size_t)k];
         size_t done = 0;
         while (done < s.size()) {
             const ssize_t w = ::pwrite(fd, s.data() + done, s.size() - done, (off_t)(at[(size_t)k] + done));
@@ -90,7 +93,8 @@ static void pwrite_parts(const char *path, bool truncate, const std::vector<std:
             done += (size_t)w;
         }
     });
-    bool good = ::close(fd) == 0;
+    bool good = !whole || ::ftruncate(fd, (off_t)at.back()) == 0;
+    good = (::close(fd) == 0) && good;
     for (auto v : ok) good = good && v;
     if (!good) fail(BWTMI_E_IO, "short write to %s", path);
 }
@@ -356,7 +360,7 @@ int bwtmi_index_tier3(bwtmi_ctx *ctx, bwtmi_index *idx, const uint8_t *reads, co
             for (int64_t r = 0; r < nreads; ++r) CHECK_ARG(read_off[r + 1] >= read_off[r], "bad read offsets");
         }
         use(ctx->c);
-        std::vector<Rec> recs;
+        RecVec recs;
         tier3_device(ctx->c, idx->d, reads, read_off, nreads, contig_id, recs);
         Job &J = job->j;
         if (as_input) {
@@ -649,7 +653,7 @@ int64_t bwtmi_job_count(const bwtmi_job *job) { return job ? (int64_t)job->j.fin
 int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len) {
     return guard([&] {
         CHECK_ARG(job && out && len, "null argument");
-        const std::vector<std::string> parts = render_parts(job->j, fmt);
+        const std::vector<Text> parts = render_parts(job->j, fmt);
         std::vector<size_t> at(parts.size() + 1, 0);
         for (size_t k = 0; k < parts.size(); ++k) at[k + 1] = at[k] + parts[k].size();
         const size_t tot = at.back();
@@ -667,7 +671,7 @@ int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len) {
 int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path) {
     return guard([&] {
         CHECK_ARG(job && path, "null argument");
-        const std::vector<std::string> parts = render_parts(job->j, fmt);
+        const std::vector<Text> parts = render_parts(job->j, fmt);
         std::vector<size_t> at(parts.size() + 1, 0);
         for (size_t k = 0; k < parts.size(); ++k) at[k + 1] = at[k] + parts[k].size();
         pwrite_parts(path, true, parts, at, host_threads(job->j.params));
@@ -707,11 +711,11 @@ int bwtmi_job_write_units(bwtmi_job *job, const char *path, const int64_t *offse
         CHECK_ARG(job && path && offsets, "null argument");
         Job &J = job->j;
         Rendered &R = J.rendered;
-        std::vector<std::string> parts;
+        std::vector<Text> parts;
         std::vector<size_t> at;
         std::vector<int64_t> fill((size_t)J.nunits, 0);
         if (write_header && !R.header.empty()) {
-            parts.push_back(std::move(R.header));
+            parts.emplace_back(R.header.data(), R.header.size());
             at.push_back((size_t)offsets[0]);
         }
         for (size_t k = 0; k < R.parts.size(); ++k) {

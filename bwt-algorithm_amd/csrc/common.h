@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "../../include/bwtmi.h"
+#include "mem.h"
 
 namespace bwtmi {
 
@@ -18,16 +19,12 @@ struct Error {
 };
 [[noreturn]] void fail(int code, const char *fmt, ...);
 
-// vector storage without value-initialisation: large arrays that are written
-// once (device downloads, parallel fills) skip a serial zero fill
+// vector storage without value-initialisation, large arrays from the cached
+// huge-page blocks of mem.h: arrays that are written once (device downloads,
+// parallel fills) skip a serial zero fill and, from the second step on, the
+// page faults
 template <class T>
-struct NoInit : std::allocator<T> {
-    template <class U> struct rebind { using other = NoInit<U>; };
-    NoInit() = default;
-    template <class U> NoInit(const NoInit<U> &) noexcept {}
-    template <class U> void construct(U *p) noexcept { ::new ((void *)p) U; }
-    template <class U, class... A> void construct(U *p, A &&...a) { ::new ((void *)p) U(std::forward<A>(a)...); }
-};
+using NoInit = BigAlloc<T>;
 using HitVec = std::vector<bwtmi_hit, NoInit<bwtmi_hit>>;
 
 // ---------------------------------------------------------------- contigs
@@ -80,6 +77,8 @@ struct Rec {
                                  // statistics (consolidated Tier 3 calls, bwt.py:3021-3030)
 };
 
+using RecVec = std::vector<Rec, BigAlloc<Rec>>;
+
 // motif utilities (MotifUtils, bwt.py:675-1381)
 std::string min_rotation(const std::string &s);
 void canonical_stranded(const std::string &s, std::string &canon, char &strand);
@@ -102,10 +101,13 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
                          double frac = 0.1, int64_t max_indel_arg = -1);
 
 // ---------------------------------------------------------------- job
+// formatted text in cached huge-page blocks (mem.h)
+using Text = std::basic_string<char, std::char_traits<char>, BigAlloc<char>>;
+
 // formatted output: header + parts of consecutive rows, each inside one fold unit
 struct Rendered {
     std::string header;
-    std::vector<std::string> parts;
+    std::vector<Text> parts;
     std::vector<int32_t> part_unit;
 };
 
@@ -119,8 +121,8 @@ struct Job {
     std::vector<uint8_t> screened;                   // screened[c]: nested-suppressed, sorted by
                                                      // (start, end, m desc, worker order) and deduped
     std::vector<int64_t> raw_n;                      // raw strict hits per contig
-    std::vector<Rec> final_recs;                     // after bwt.py:3940-3944
-    std::vector<std::vector<Rec>> t3;                // per contig: Tier 3 records (bwt.py:3918-3924), joined
+    RecVec final_recs;                               // after bwt.py:3940-3944
+    std::vector<RecVec> t3;                          // per contig: Tier 3 records (bwt.py:3918-3924), joined
                                                      // after the contig's strict hits before nested suppression
     std::vector<uint8_t> selected;                   // scan only these contigs (empty = all)
     bool postprocessed = false;
@@ -134,7 +136,7 @@ void postprocess(Job &job);
 // render.cpp: the output as consecutive parts (formatted in parallel).
 // row_base (per fold unit, may be null): global VCF row id of the unit's first row.
 void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out);
-std::vector<std::string> render_parts(Job &job, int fmt);
+std::vector<Text> render_parts(Job &job, int fmt);
 std::string render(Job &job, int fmt);
 // fasta.cpp
 void load_fasta(Job &job, const char *path, int32_t flank_trim);

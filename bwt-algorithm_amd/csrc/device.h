@@ -218,19 +218,19 @@ void lcp_plateaus_device(Ctx &c, DeviceIndex *ix, const LibParams &p, std::vecto
 // Tier2LCPFinder.find_short_imperfect_repeats (bwt.py:2027-2095, 2562-2825); records appended
 // to `out` with chrom = `chrom`; `seen` = (start, end) pairs already found (tier1_seen)
 void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const std::vector<int64_t> &seen,
-                            int32_t chrom, std::vector<Rec> &out);
+                            int32_t chrom, RecVec &out);
 // Tier1STRFinder.find_strs (bwt.py:1426-1538) over text t (host) / d_text (device copy, n bytes)
 void tier1_device(Ctx &c, const uint8_t *d_text, const uint8_t *t, int64_t n, int32_t max_motif_length,
-                  int32_t chrom, std::vector<Rec> &out);
+                  int32_t chrom, RecVec &out);
 void index_backward_search(Ctx &c, DeviceIndex *, const uint8_t *pats, const int64_t *off, int64_t npat,
                            int64_t *sp_ep);
 void index_sa_rows(Ctx &c, const DeviceIndex *, const int64_t *rows, int64_t k, int64_t *out);
 // Tier2LCPFinder.find_long_repeats -> _find_repeats_simple (bwt.py:2097-2106, 2177-2498)
 void simple_scan_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const std::vector<int64_t> &seen_pairs,
-                        int32_t chrom, std::vector<Rec> &out);
+                        int32_t chrom, RecVec &out);
 // Tier3LongReadFinder.find_very_long_repeats (bwt.py:2837-3036) of `reads` (concatenated,
 // read_off[nreads + 1]) against the index; consolidated records with chrom = `chrom`
 void tier3_device(Ctx &c, DeviceIndex *ix, const uint8_t *reads, const int64_t *read_off, int64_t nreads,
-                  int32_t chrom, std::vector<Rec> &out);
+                  int32_t chrom, RecVec &out);
 
 }  // namespace bwtmi

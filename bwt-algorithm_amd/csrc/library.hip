@@ -644,7 +644,7 @@ void lcp_plateaus_device(Ctx &c, DeviceIndex *ix, const LibParams &p, std::vecto
 }
 
 void tier1_device(Ctx &c, const uint8_t *d_text, const uint8_t *t, int64_t n, int32_t max_motif_length,
-                  int32_t chrom, std::vector<Rec> &out) {
+                  int32_t chrom, RecVec &out) {
     if (n <= 0) return;
     hipStream_t st = c.stream;
     const int64_t step = n > 10000000 ? 50 : (n > 5000000 ? 20 : 1);   // bwt.py:1440-1447
@@ -715,7 +715,7 @@ void tier1_device(Ctx &c, const uint8_t *d_text, const uint8_t *t, int64_t n, in
 }
 
 void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const std::vector<int64_t> &seen_pairs,
-                            int32_t chrom, std::vector<Rec> &out) {
+                            int32_t chrom, RecVec &out) {
     const int64_t n = index_n(ix);
     if (n > 1000000 || n == 0) return;                    // bwt.py:2048
     const int kmin = std::max(1, p.min_period), kend = std::min(p.max_short_motif + 1, 10);
@@ -897,7 +897,7 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
 // SA; records are built and consolidated (3003-3036) on the host, in read and
 // window order.
 void tier3_device(Ctx &c, DeviceIndex *ix, const uint8_t *reads, const int64_t *read_off, int64_t nreads,
-                  int32_t chrom, std::vector<Rec> &out) {
+                  int32_t chrom, RecVec &out) {
     const int64_t n = index_n(ix);
     std::vector<int64_t> wpos;   // window starts (offsets into reads)
     std::vector<int64_t> wread;  // read of each window
@@ -955,7 +955,7 @@ void tier3_device(Ctx &c, DeviceIndex *ix, const uint8_t *reads, const int64_t *
     index_get_text(c, ix, text.data());
     const uint8_t *t = text.data();
     const int64_t max_len = (n > 0 && t[n - 1] == '$') ? n - 1 : n;   // 2877-2880
-    std::vector<Rec> recs;
+    RecVec recs;
     AlignSummary summ;
     for (size_t h = 0; h < rows.size(); ++h) {
         const int64_t q = hitw[h], w = cand[(size_t)q];
@@ -1112,7 +1112,7 @@ struct SimWalk {
 // iteration cap (100,000) to build the records.  The reference also stops after
 // 30 s of wall time (2238-2257); that machine-dependent stop is not reproduced.
 void simple_scan_device(Ctx &c, DeviceIndex *ix, const LibParams &P, const std::vector<int64_t> &seen_pairs,
-                        int32_t chrom, std::vector<Rec> &out) {
+                        int32_t chrom, RecVec &out) {
     const int64_t nt = index_n(ix);
     if (nt == 0) return;
     std::vector<uint8_t> text((size_t)nt);

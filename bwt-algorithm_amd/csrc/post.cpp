@@ -30,6 +30,7 @@
 #include <string>
 #include <string_view>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -229,6 +230,8 @@ struct Extra {                  // trivially destructible: strings live in the P
     bool stats_none = false;    // Rec::stats_none
 };
 
+static_assert(std::is_trivially_destructible<Extra>::value, "Extras live in raw arena blocks");
+
 struct Item {
     int64_t start, end;   // current frame (trimmed, then full after restore)
     int64_t count;        // strict: copies
@@ -241,26 +244,34 @@ struct Item {
 // once in parallel, so the first touch happens in the filling threads
 using ItemVec = std::vector<Item, NoInit<Item>>;
 
-// per-worker bump arenas for Extras and their strings (pointer-stable; freed
-// as a handful of blocks)
+// per-worker bump arenas for Extras and their strings (pointer-stable; the
+// blocks are cached huge-page blocks, mem.h)
 struct Pools {
+    struct Block {
+        void *p = nullptr;
+        size_t bytes = 0;
+        Block(size_t b) : p(big_alloc(b)), bytes(b) {}
+        Block(Block &&o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; }
+        Block(const Block &) = delete;
+        ~Block() { if (p) big_free(p, bytes); }
+    };
     struct Arena {
-        std::vector<std::unique_ptr<Extra[]>> xb;
+        std::vector<Block> xb;
         size_t xn = 0;                                   // used in the last Extra block
-        std::vector<std::unique_ptr<char[]>> cb;
+        std::vector<Block> cb;
         size_t cn = 0, ccap = 0;                         // used / size of the last char block
     };
-    static constexpr size_t XB = 4096, CB = 1 << 20;
+    static constexpr size_t XB = 16384, CB = size_t(2) << 20;   // Extras are trivially destructible
     std::vector<Arena> a;
     explicit Pools(int n) : a((size_t)n) {}
     std::string_view str(Arena &A, std::string_view s) {
         if (s.empty()) return {};
         if (A.cb.empty() || A.cn + s.size() > A.ccap) {
             A.ccap = std::max(CB, s.size());
-            A.cb.emplace_back(new char[A.ccap]);
+            A.cb.emplace_back(A.ccap);
             A.cn = 0;
         }
-        char *d = A.cb.back().get() + A.cn;
+        char *d = (char *)A.cb.back().p + A.cn;
         std::memcpy(d, s.data(), s.size());
         A.cn += s.size();
         return std::string_view(d, s.size());
@@ -268,11 +279,11 @@ struct Pools {
     Extra *add(int w, const Extra &e, std::string_view motif, std::string_view variations) {
         Arena &A = a[(size_t)w];
         if (A.xb.empty() || A.xn == XB) {
-            A.xb.emplace_back(new Extra[XB]);
+            A.xb.emplace_back(XB * sizeof(Extra));
             A.xn = 0;
         }
-        Extra *x = &A.xb.back()[A.xn++];
-        *x = e;
+        Extra *x = (Extra *)A.xb.back().p + A.xn++;
+        ::new ((void *)x) Extra(e);
         x->motif = str(A, motif);
         x->variations = str(A, variations);
         return x;
@@ -608,14 +619,14 @@ bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, Canon &c1,
 
 struct SpecOut {
     ItemVec emitted;                 // records emitted by the speculative run
-    std::vector<int64_t> emit_step;  // index i at which each was emitted
+    std::vector<int64_t, BigAlloc<int64_t>> emit_step;  // index i at which each was emitted
     Item pending;
     Canon pending_canon;
 };
 
 // speculative run over [b, e): starts with cur = R[b] as if fresh at b
 void spec_run(const UnitCtx &u, Pools &pools, int w, const ItemVec &R, int64_t b, int64_t e,
-              std::vector<uint8_t> &fresh, SpecOut &o) {
+              std::vector<uint8_t, BigAlloc<uint8_t>> &fresh, SpecOut &o) {
     Item cur = R[(size_t)b];
     Canon cc;
     fresh[(size_t)b] = 1;
@@ -646,7 +657,7 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
     const int64_t K = std::max<int64_t>(1, std::min<int64_t>((int64_t)nt * 8, n / 2048 + 1));
     std::vector<int64_t> cut((size_t)K + 1);
     for (int64_t k = 0; k <= K; ++k) cut[(size_t)k] = n * k / K;
-    std::vector<uint8_t> fresh((size_t)n, 0);
+    std::vector<uint8_t, BigAlloc<uint8_t>> fresh((size_t)n, 0);
     std::vector<SpecOut> spec((size_t)K);
     auto ts0 = std::chrono::steady_clock::now();
     std::vector<double> cms(g_stats ? (size_t)K : 0);
@@ -863,7 +874,7 @@ Rec materialize(const UnitCtx &u, const Item &it) {
 }
 
 void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vector<HitVec> &raw,
-                  std::vector<Rec> &out, double *ms, int nt) {
+                  RecVec &out, double *ms, int nt) {
     using clk = std::chrono::steady_clock;
     auto t0 = clk::now();
     UnitCtx u{&job, job.params.min_copies};
@@ -941,7 +952,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     if (!one_offset) sort_by_pos(recs, nt);
     auto r3 = clk::now();
     const size_t n_before_collapse = recs.size();
-    std::vector<uint32_t> col;   // collapsed list as indices into recs (the slot takes the preferred record)
+    std::vector<uint32_t, BigAlloc<uint32_t>> col;   // collapsed list as indices into recs (the slot takes the preferred record)
     col.reserve(recs.size() / 4 + 16);
     for (size_t k = 0; k < recs.size(); ++k) {
         if (!col.empty() && should_collapse(u, recs[col.back()], recs[k])) {
@@ -990,7 +1001,7 @@ void postprocess(Job &job) {
     std::vector<std::vector<int32_t>> units((size_t)job.nunits);
     for (size_t c = 0; c < job.contigs.size(); ++c) units[(size_t)job.contigs[c].unit].push_back((int32_t)c);
     if (job.hits.size() < job.contigs.size()) job.hits.resize(job.contigs.size());
-    std::vector<std::vector<Rec>> res((size_t)job.nunits);
+    std::vector<RecVec> res((size_t)job.nunits);
     std::vector<double> ms((size_t)job.nunits * 4, 0.0);
     const int T = host_threads(job.params);
     // many small units: one thread per unit; few large units: all threads inside each

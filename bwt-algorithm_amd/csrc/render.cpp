@@ -60,7 +60,7 @@ Rec kmer_piece(int32_t chrom, int64_t start, int64_t end, const std::string &mot
 }
 
 // _simple_kmer_scan(chrom, start, end, k=3, use_full_seq=True)
-void kmer_scan(const Job &job, int32_t chrom, int64_t start, int64_t end, std::vector<Rec> &out) {
+void kmer_scan(const Job &job, int32_t chrom, int64_t start, int64_t end, RecVec &out) {
     const std::string &seq = job.contigs[(size_t)chrom].full;
     const int64_t L = (int64_t)seq.size();
     const int64_t k = 3;
@@ -98,7 +98,7 @@ struct Compound {
 
 // _detect_compound_repeats (bwt.py:3995-4139) over the final records; works on
 // pointers, so the final records are never copied
-void detect_compounds(const Job &job, const std::vector<Rec> &recs, Compound &out) {
+void detect_compounds(const Job &job, const RecVec &recs, Compound &out) {
     std::vector<int32_t> chrom_order;
     std::vector<std::vector<const Rec *>> by(job.contigs.size());
     for (const Rec &r : recs) {
@@ -110,7 +110,7 @@ void detect_compounds(const Job &job, const std::vector<Rec> &recs, Compound &ou
         if (full.empty()) continue;
         std::vector<const Rec *> &lst = by[(size_t)ch];
         const size_t n0 = lst.size();
-        std::vector<Rec> kr;
+        RecVec kr;
         for (size_t q = 0; q < n0; ++q) {
             const Rec *r = lst[q];
             if (r->motif.size() != 3) continue;
@@ -203,7 +203,7 @@ void detect_compounds(const Job &job, const std::vector<Rec> &recs, Compound &ou
 
 // ---------------------------------------------------------------- formatting
 struct Out {
-    std::string s;
+    Text s;
     void put(const char *p, int64_t n) { s.append(p, (size_t)n); }
     void put(const std::string &x) { s.append(x); }
     void put(View v) { if (v.n > 0) s.append(v.p, (size_t)v.n); }
@@ -398,7 +398,7 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out) {
         a = e;
     }
     out.header = std::move(head);
-    out.parts.assign(chunks.size(), std::string());
+    out.parts.assign(chunks.size(), Text());
     out.part_unit.resize(chunks.size());
     for (size_t q = 0; q < chunks.size(); ++q) out.part_unit[q] = chunks[q].unit;
     run_tasks((int64_t)chunks.size(), host_threads(job.params), [&](int64_t ck) {
@@ -455,23 +455,23 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out) {
     job.stage_ms[6] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-std::vector<std::string> render_parts(Job &job, int fmt) {
+std::vector<Text> render_parts(Job &job, int fmt) {
     Rendered r;
     render_rows(job, fmt, nullptr, r);
-    std::vector<std::string> parts;
+    std::vector<Text> parts;
     parts.reserve(r.parts.size() + 1);
-    parts.push_back(std::move(r.header));
+    parts.emplace_back(r.header.data(), r.header.size());
     for (auto &p : r.parts) parts.push_back(std::move(p));
     return parts;
 }
 
 std::string render(Job &job, int fmt) {
-    std::vector<std::string> parts = render_parts(job, fmt);
+    std::vector<Text> parts = render_parts(job, fmt);
     size_t tot = 0;
     for (auto &p : parts) tot += p.size();
     std::string s;
     s.reserve(tot);
-    for (auto &p : parts) s.append(p);
+    for (auto &p : parts) s.append(p.data(), p.size());
     return s;
 }
 
