@@ -164,13 +164,32 @@ void prefix_max(Ctx &c, const int64_t *in, int64_t *out, int64_t n, int64_t *tmp
     hipLaunchKernelGGL(k_tile_scan_max, dim3((unsigned)nt), dim3(kB), 0, c.stream, in, out, (const int64_t *)tm, n);
 }
 
+// position buckets: B[b] = first rank k with S[k] >= b << kBucketShift (n if
+// none), so a search for "first rank with S >= x" starts inside one bucket
+// (a few hits) instead of spanning all n ranks with ~23 dependent loads
+constexpr int kBucketShift = 6;
+
+__global__ void k_buckets(const int64_t *__restrict__ S, int64_t n, int64_t nb, uint32_t *__restrict__ B) {
+    const int64_t b = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (b >= nb) return;
+    const int64_t x = b << kBucketShift;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (S[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    B[b] = (uint32_t)lo;
+}
+
 // one level (all hits of one primitive length m): nested test against the
 // kept spans of longer motif (bwt.py:3460-3490), predicate division for division
 __global__ __launch_bounds__(kB) void k_level(const uint32_t *__restrict__ lvl, int64_t cnt,
                                               const bwtmi_hit *__restrict__ H, const uint32_t *__restrict__ rank_of,
                                               const int64_t *__restrict__ S, const int64_t *__restrict__ E,
                                               const int32_t *__restrict__ M, const int64_t *__restrict__ PME,
-                                              uint8_t *__restrict__ kept, int64_t n, double thr) {
+                                              const uint32_t *__restrict__ B, uint8_t *__restrict__ kept, int64_t n,
+                                              double thr) {
     const int64_t t = (int64_t)blockIdx.x * kB + threadIdx.x;
     if (t >= cnt) return;
     const uint32_t idx = lvl[t];
@@ -178,7 +197,9 @@ __global__ __launch_bounds__(kB) void k_level(const uint32_t *__restrict__ lvl, 
     const int64_t s0 = h.start, e0 = h.end, m = h.prim_len, rl = e0 - s0;
     bool nested = false;
     if (rl > 0) {
-        int64_t lo = 0, hi = n;   // first rank with S >= e0
+        // first rank with S >= e0: inside bucket e0 >> shift (e0 <= text_len)
+        const int64_t bk = e0 >> kBucketShift;
+        int64_t lo = B[bk], hi = B[bk + 1];
         while (lo < hi) {
             const int64_t mid = (lo + hi) >> 1;
             if (S[mid] < e0) lo = mid + 1;
@@ -240,6 +261,8 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     c.slot[S_FLAG].ensure((size_t)(n + 1) * 4);
     c.slot[S_SCAN].ensure((size_t)(n + 1) * 4);
     c.slot[S_COUNTS].ensure((size_t)(lmax + 2) * 8);
+    const int64_t nb = (text_len >> kBucketShift) + 2;   // hit ends are <= text_len
+    c.slot[S_IDX6].ensure((size_t)nb * 4);
     uint64_t *kpos = c.slot[S_CAND_K].as<uint64_t>(), *kgrp = c.slot[S_CAND_K2].as<uint64_t>();
     uint32_t *vpos = c.slot[S_CAND_V].as<uint32_t>(), *vgrp = c.slot[S_CAND_V2].as<uint32_t>();
     int64_t *S = c.slot[S_MISC0].as<int64_t>(), *E = c.slot[S_MISC1].as<int64_t>();
@@ -270,6 +293,8 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     radix_sort_pairs32(c, kgrp, vgrp, n, 0, round8(mb));
     hipLaunchKernelGGL(k_gather, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, S, E, M, rank_of, kept);
     prefix_max(c, E, PME, n, c.slot[S_IDX5].as<int64_t>());
+    uint32_t *B = c.slot[S_IDX6].as<uint32_t>();
+    hipLaunchKernelGGL(k_buckets, dim3(blocks(nb)), dim3(kB), 0, st, S, n, nb, B);
     int64_t *first = reinterpret_cast<int64_t *>(d_max);
     HIPCHECK(hipMemsetAsync(first, 0xff, (size_t)(lmax + 2) * 8, st));
     hipLaunchKernelGGL(k_bounds, dim3(blocks(n)), dim3(kB), 0, st, kgrp, n, first);
@@ -287,7 +312,7 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     for (size_t q = 0; q < lv.size(); ++q) {
         const int64_t a = lv[q].first, b = q + 1 < lv.size() ? lv[q + 1].first : n;
         hipLaunchKernelGGL(k_level, dim3(blocks(b - a)), dim3(kB), 0, st, vgrp + a, b - a, d_hits, rank_of, S, E, M,
-                           PME, kept, n, 0.5);
+                           PME, B, kept, n, 0.5);
     }
     c.kend();
     c.kbegin("screen_compact", 0.0);

@@ -97,8 +97,9 @@ struct CandOut {
     int32_t umax;
 };
 
-__device__ __forceinline__ void emit(const CandOut &o, int64_t L, int64_t s, int64_t e) {
-    const unsigned long long idx = atomicAdd(o.count, 1ull);
+// candidate at a slot reserved by the wave (slots past cap are counted, not
+// written: the host retries with a larger buffer)
+__device__ __forceinline__ void put(const CandOut &o, unsigned long long idx, int64_t L, int64_t s, int64_t e) {
     if ((int64_t)idx < o.cap) {
         o.keys[idx] = ((uint64_t)(o.umax - L) << 40) | (uint64_t)s;
         o.vals[idx] = (uint64_t)e;
@@ -152,45 +153,83 @@ __global__ __launch_bounds__(256) void k_runs(const uint32_t *__restrict__ P, in
         }
         const uint32_t Mp = (uint32_t)__shfl_up((int)M, 1, 64);
         const uint32_t Mn = (uint32_t)__shfl_down((int)M, 1, 64);
-        if (!owned) continue;
+        // This lane's candidates are counted first -- at most one streak
+        // (first full word) or the short runs starting in its word -- so the
+        // wave reserves all its output slots with ONE atomic: per-candidate
+        // atomics on the single counter serialise millions of same-address
+        // operations across the chip.
+        int cnt = 0;
+        int64_t s1 = 0, e1 = 0;   // streak candidate
+        uint32_t qual = 0;        // qualifying short-run starts (bit k <-> position j0 + k)
+        // end of the run that starts at bit k of this word (exclusive), or -1
+        // when it joins a streak owned by word w+1
+        auto run_end = [&](int k) -> int64_t {
+            const uint32_t rr = M >> k;
+            const int len_in = __ffs(~rr) - 1;   // ~rr has its top k bits set
+            if (k + len_in < 32) return j0 + k + len_in;
+            if (Mn == FULL) return -1;
+            return j0 + 32 + (int64_t)__ffs(~Mn) - 1;
+        };
+        if (owned) {
+            if (M == FULL) {
+                if (Mp != FULL) {   // first full word of a streak
+                    const int64_t s = j0 - (int64_t)__clz(~Mp);
+                    int64_t q = w + 1;
+                    uint32_t Mq = Mn;
+                    while (Mq == FULL) {
+                        ++q;
+                        Mq = eq32<B>(P, q, L, n);
+                    }
+                    const int64_t e = q * 32 + (int64_t)__ffs(~Mq) - 1;
+                    if (e - s >= K) {
+                        cnt = 1;
+                        s1 = s;
+                        e1 = e;
+                    }
+                }
+            } else if (K <= 62 && M != 0u) {
+                // runs that start in this word and contain no full aligned word;
+                // only starts with K ones ahead (within M:Mn) can qualify
+                uint32_t starts = M & ~((M << 1) | (Mp >> 31));
+                const uint64_t V = (uint64_t)M | ((uint64_t)Mn << 32);
+                uint64_t A = V;
+                for (int64_t have = 1; have < K;) {
+                    const int64_t s = have < K - have ? have : K - have;
+                    A &= A >> s;
+                    have += s;
+                }
+                starts &= (uint32_t)A;
+                while (starts) {
+                    const int k = __ffs(starts) - 1;
+                    starts &= starts - 1;
+                    const int64_t e = run_end(k);
+                    if (e >= 0 && e - (j0 + k) >= K) {
+                        qual |= 1u << k;
+                        ++cnt;
+                    }
+                }
+            }
+        }
+        int incl = cnt;   // wave inclusive prefix of the counts
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        const int tot = __shfl(incl, 63, 64);
+        if (tot == 0) continue;   // wave-uniform
+        unsigned long long base = 0;
+        if (lane == 63) base = atomicAdd(out.count, (unsigned long long)tot);
+        base = __shfl(base, 63, 64);
+        unsigned long long at = base + (unsigned long long)(incl - cnt);
+        if (cnt == 0) continue;
         if (M == FULL) {
-            if (Mp != FULL) {   // first full word of a streak
-                const int64_t s = j0 - (int64_t)__clz(~Mp);
-                int64_t q = w + 1;
-                uint32_t Mq = Mn;
-                while (Mq == FULL) {
-                    ++q;
-                    Mq = eq32<B>(P, q, L, n);
-                }
-                const int64_t e = q * 32 + (int64_t)__ffs(~Mq) - 1;
-                if (e - s >= K) emit(out, L, s, e);
-            }
-        } else if (K <= 62 && M != 0u) {
-            // runs that start in this word and contain no full aligned word;
-            // only starts with K ones ahead (within M:Mn) can qualify
-            uint32_t starts = M & ~((M << 1) | (Mp >> 31));
-            const uint64_t V = (uint64_t)M | ((uint64_t)Mn << 32);
-            uint64_t A = V;
-            for (int64_t have = 1; have < K;) {
-                const int64_t s = have < K - have ? have : K - have;
-                A &= A >> s;
-                have += s;
-            }
-            starts &= (uint32_t)A;
-            while (starts) {
-                const int k = __ffs(starts) - 1;
-                starts &= starts - 1;
-                const uint32_t rr = M >> k;
-                const int len_in = __ffs(~rr) - 1;  // ~rr has its top k bits set
-                int64_t e;
-                if (k + len_in < 32) {
-                    e = j0 + k + len_in;
-                } else {
-                    if (Mn == FULL) continue;     // joins a streak owned by word w+1
-                    e = j0 + 32 + (int64_t)__ffs(~Mn) - 1;
-                }
-                const int64_t s = j0 + k;
-                if (e - s >= K) emit(out, L, s, e);
+            put(out, at, L, s1, e1);
+        } else {
+            while (qual) {
+                const int k = __ffs(qual) - 1;
+                qual &= qual - 1;
+                put(out, at++, L, j0 + k, run_end(k));
             }
         }
     }
@@ -279,12 +318,12 @@ __global__ __launch_bounds__(256) void k_period(const uint8_t *__restrict__ t, b
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nh) return;
     bwtmi_hit h = hits[k];
-    const int64_t L = h.unit_len;
+    const int32_t L = h.unit_len;   // 32-bit: the divisor tests are 32-bit remainders
     const uint8_t *s = t + h.start;
-    int64_t p = L;
-    for (int64_t d = 1; d < L; ++d) {
+    int32_t p = L;
+    for (int32_t d = 1; d < L; ++d) {
         if (L % d) continue;
-        int64_t x = d;
+        int32_t x = d;
         while (x < L && s[x] == s[x - d]) ++x;
         if (x == L) { p = d; break; }
     }
