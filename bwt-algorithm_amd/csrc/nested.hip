@@ -20,11 +20,13 @@
 //
 // Kernels: two stable LSD radix sorts give the position order P (by
 // (len, m desc) then start) and the level order G (by m desc); the position
-// arrays S/E/M and an inclusive prefix max of E (PME) are gathered once.  One
-// launch per distinct m (descending) decides that level: each thread binary
-// searches the last span starting before e0 and walks P backwards until PME
-// drops to s0 -- every span that can overlap r lies in that window.  A final
-// flag/scan/compact pass writes the kept, deduplicated hits in P order.
+// arrays S/E/M and an inclusive prefix max of E (PME) are gathered once, with
+// a bucket table of S (first rank per 64 bp).  One launch per distinct m
+// (descending) decides that level: each hit finds the last span starting
+// before e0 (bucket + short binary search) and walks P backwards until PME
+// drops to s0 -- every span that can overlap r lies in that window; small
+// levels (long motifs, long walks) use a wave per hit, 64 ranks per step.  A
+// final flag/scan/compact pass writes the kept, deduplicated hits in P order.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -168,6 +170,7 @@ void prefix_max(Ctx &c, const int64_t *in, int64_t *out, int64_t n, int64_t *tmp
 // none), so a search for "first rank with S >= x" starts inside one bucket
 // (a few hits) instead of spanning all n ranks with ~23 dependent loads
 constexpr int kBucketShift = 6;
+constexpr int64_t kWaveLevelMax = 65536;   // levels up to this many hits use k_level_wave
 
 __global__ void k_buckets(const int64_t *__restrict__ S, int64_t n, int64_t nb, uint32_t *__restrict__ B) {
     const int64_t b = (int64_t)blockIdx.x * kB + threadIdx.x;
@@ -218,6 +221,58 @@ __global__ __launch_bounds__(kB) void k_level(const uint32_t *__restrict__ lvl, 
         }
     }
     kept[rank_of[idx]] = nested ? 0 : 1;
+}
+
+// the same test with one WAVE per hit: the 64 lanes walk 64 consecutive ranks
+// at a time.  Long-motif levels hold few hits but long spans, whose backward
+// walks cover hundreds of ranks -- one lane walking them serially leaves the
+// launch latency-bound.  The visited set {k <= lo-1 : PME[k] > s0} is a
+// contiguous range (PME is non-decreasing), and the outcome is an "any".
+__global__ __launch_bounds__(kB) void k_level_wave(const uint32_t *__restrict__ lvl, int64_t cnt,
+                                                   const bwtmi_hit *__restrict__ H, const uint32_t *__restrict__ rank_of,
+                                                   const int64_t *__restrict__ S, const int64_t *__restrict__ E,
+                                                   const int32_t *__restrict__ M, const int64_t *__restrict__ PME,
+                                                   const uint32_t *__restrict__ B, uint8_t *__restrict__ kept,
+                                                   int64_t n, double thr) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t = ((int64_t)blockIdx.x * kB + threadIdx.x) >> 6;
+    if (t >= cnt) return;   // wave-uniform
+    const uint32_t idx = lvl[t];
+    const bwtmi_hit h = H[idx];
+    const int64_t s0 = h.start, e0 = h.end, m = h.prim_len, rl = e0 - s0;
+    bool nested = false;
+    if (rl > 0) {
+        const int64_t bk = e0 >> kBucketShift;
+        int64_t lo = B[bk], hi = B[bk + 1];
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (S[mid] < e0) lo = mid + 1;
+            else hi = mid;
+        }
+        for (int64_t top = lo - 1; top >= 0; top -= 64) {
+            const int64_t k = top - lane;
+            const bool live = k >= 0 && PME[k] > s0;
+            bool hit = false;
+            if (live) {
+                const int64_t Mk = M[k];
+                if (Mk > m && kept[k]) {   // same-level entries are being written now: never read
+                    const int64_t ov = min(e0, E[k]) - max(s0, S[k]);
+                    if (ov > 0) {
+                        const double ratio = (double)Mk / (double)m;
+                        const double frac = (double)ov / (double)rl;
+                        const double th = ratio >= 10 ? 0.1 : (ratio >= 5 ? 0.3 : thr);
+                        hit = (m == 1 && Mk > 1 && frac >= 0.8) || frac >= th;
+                    }
+                }
+            }
+            if (__any(hit)) {
+                nested = true;
+                break;
+            }
+            if (!__all(live)) break;
+        }
+    }
+    if (lane == 0) kept[rank_of[idx]] = nested ? 0 : 1;
 }
 
 __global__ void k_final_flags(const int64_t *__restrict__ S, const int64_t *__restrict__ E,
@@ -311,8 +366,12 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
         if (fh[(size_t)g] >= 0) lv.push_back({fh[(size_t)g], g});
     for (size_t q = 0; q < lv.size(); ++q) {
         const int64_t a = lv[q].first, b = q + 1 < lv.size() ? lv[q + 1].first : n;
-        hipLaunchKernelGGL(k_level, dim3(blocks(b - a)), dim3(kB), 0, st, vgrp + a, b - a, d_hits, rank_of, S, E, M,
-                           PME, B, kept, n, 0.5);
+        if (b - a <= kWaveLevelMax)   // few hits (long motifs, long walks): a wave per hit
+            hipLaunchKernelGGL(k_level_wave, dim3(blocks((b - a) * 64)), dim3(kB), 0, st, vgrp + a, b - a, d_hits,
+                               rank_of, S, E, M, PME, B, kept, n, 0.5);
+        else
+            hipLaunchKernelGGL(k_level, dim3(blocks(b - a)), dim3(kB), 0, st, vgrp + a, b - a, d_hits, rank_of, S, E,
+                               M, PME, B, kept, n, 0.5);
     }
     c.kend();
     c.kbegin("screen_compact", 0.0);

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <charconv>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <string>
@@ -99,12 +100,16 @@ struct Compound {
 // _detect_compound_repeats (bwt.py:3995-4139) over the final records; works on
 // pointers, so the final records are never copied
 void detect_compounds(const Job &job, const RecVec &recs, Compound &out) {
+    auto T0 = std::chrono::steady_clock::now();
     std::vector<int32_t> chrom_order;
     std::vector<std::vector<const Rec *>> by(job.contigs.size());
     for (const Rec &r : recs) {
         if (by[(size_t)r.chrom].empty()) chrom_order.push_back(r.chrom);
         by[(size_t)r.chrom].push_back(&r);
     }
+    auto T1 = std::chrono::steady_clock::now();
+    std::vector<size_t> n_main(job.contigs.size(), 0);
+    for (int32_t ch : chrom_order) n_main[(size_t)ch] = by[(size_t)ch].size();
     for (int32_t ch : chrom_order) {
         const std::string &full = job.contigs[(size_t)ch].full;
         if (full.empty()) continue;
@@ -125,13 +130,29 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out) {
                 }
         }
     }
+    auto T2 = std::chrono::steady_clock::now();
+    double tsort = 0;
     for (int32_t ch : chrom_order) {
+        auto S0 = std::chrono::steady_clock::now();
         std::vector<const Rec *> &rs = by[(size_t)ch];
-        std::stable_sort(rs.begin(), rs.end(), [](const Rec *a, const Rec *b) { return a->start < b->start; });
-        struct Long { int64_t s, e; };
+        // stable sort by start: the final records arrive sorted, only the
+        // k-mer pieces appended behind them need ordering and a stable merge
+        auto by_start = [](const Rec *a, const Rec *b) { return a->start < b->start; };
+        const size_t nmain = n_main[(size_t)ch];
+        if (std::is_sorted(rs.begin(), rs.begin() + (std::ptrdiff_t)nmain, by_start)) {
+            std::stable_sort(rs.begin() + (std::ptrdiff_t)nmain, rs.end(), by_start);
+            std::inplace_merge(rs.begin(), rs.begin() + (std::ptrdiff_t)nmain, rs.end(), by_start);
+        } else {
+            std::stable_sort(rs.begin(), rs.end(), by_start);
+        }
+        // spans of the > 10 bp motifs in start order, with the prefix max of
+        // their ends: the "covered" test visits only those that can overlap
+        struct Long { int64_t s, e, pe; };
         std::vector<Long> longs;
         for (auto *r : rs)
-            if (r->motif.size() > 10) longs.push_back({r->start, r->end});
+            if (r->motif.size() > 10)
+                longs.push_back({r->start, r->end, longs.empty() ? r->end : std::max(longs.back().pe, r->end)});
+        tsort += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - S0).count();
         const Contig &ctg = job.contigs[(size_t)ch];
         const int64_t TL = ctg.trimmed_len();
         const char *tseq = ctg.trimmed();
@@ -183,10 +204,18 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out) {
                 if (gap <= 5 && cur->motif.size() <= 4 && nx->motif.size() <= 4 && cur->motif != nx->motif &&
                     cur->copies >= 5 && nx->copies >= 5) {
                     const int64_t cs = cur->start, ce = nx->end;
+                    // any(long overlaps >= 80 %): a long with s >= ce or e <= cs has
+                    // ov = 0, so only those before the first s >= ce whose prefix
+                    // max end still exceeds cs can qualify
                     bool covered = false;
-                    for (auto &lm : longs) {
+                    size_t k = (size_t)(std::lower_bound(longs.begin(), longs.end(), ce,
+                                                         [](const Long &l, int64_t x) { return l.s < x; }) -
+                                        longs.begin());
+                    while (k > 0 && !covered) {
+                        const Long &lm = longs[--k];
+                        if (lm.pe <= cs) break;
                         const int64_t ov = std::max<int64_t>(0, std::min(ce, lm.e) - std::max(cs, lm.s));
-                        if ((double)ov / (double)(ce - cs) >= 0.8) { covered = true; break; }
+                        if ((double)ov / (double)(ce - cs) >= 0.8) covered = true;
                     }
                     if (!covered) {
                         out.rows.push_back({cur, nx});
@@ -199,6 +228,11 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out) {
             ++i;
         }
     }
+    if (const char *e = std::getenv("BWTMI_STATS"); e && *e == '1') {
+        auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "  compounds: group+kmer %.1f sort %.1f walk %.1f ms (%zu pieces)\n", d(T0, T1), tsort,
+                     d(T2, std::chrono::steady_clock::now()) - tsort, out.pool.size());
+    }
 }
 
 // ---------------------------------------------------------------- formatting
@@ -209,6 +243,11 @@ struct Out {
     void put(View v) { if (v.n > 0) s.append(v.p, (size_t)v.n); }
     void c(char ch) { s.push_back(ch); }
     void f(const char *fmt, double x) {   // printf keeps Python's exact-value rounding
+        if (fmt[1] == '.' && fmt[2] == '0' && fmt[3] == 'f' && x == std::floor(x) && std::fabs(x) < 1e15 &&
+            !(x == 0.0 && std::signbit(x))) {
+            i((int64_t)x);   // an integral value prints as that integer under %.0f
+            return;
+        }
         char b[64];
         int n = snprintf(b, sizeof b, fmt, x);
         s.append(b, (size_t)n);
@@ -293,30 +332,36 @@ void row_strfinder(Out &o, const Job &job, const Rec &r, const Rec *partner) {
         o.put(g);
     }
     o.c('\t');
-    std::string core_full;
-    View av = act_of(job, r);
-    if (!av.empty()) core_full.assign(av.p, (size_t)av.n);
-    else for (int64_t k = 0; k < (int64_t)r.copies; ++k) core_full += cons;
-    if ((int64_t)core_full.size() > 150) {
-        o.put(core_full.data(), 70);
+    // core sequence: the actual-sequence slice, or the motif repeated int(copies) times
+    thread_local std::string built;
+    View core = act_of(job, r);
+    if (core.empty()) {
+        built.clear();
+        for (int64_t k = 0; k < (int64_t)r.copies; ++k) built += cons;
+        core.p = built.data();
+        core.n = (int64_t)built.size();
+    }
+    if (core.n > 150) {
+        o.put(core.p, 70);
         o.put("... (x"); o.i(cc); o.c(')');
     } else {
-        o.put(core_full);
+        o.put(core);
     }
     o.c('\t');
     o.f("%.0f", r.pmatch);
     o.put("%\t-\t");
     o.i(cc); o.c(':'); o.i(r.n_eval); o.c('\t'); o.i(r.n_eval); o.c('\t');
-    const int64_t tot = (flanks ? fl.n + fr.n : 0) + (int64_t)core_full.size();
+    const int64_t tot = (flanks ? fl.n + fr.n : 0) + core.n;
     if (tot > 500) {
-        std::string fc;
-        if (flanks) { fc.append(fl.p ? fl.p : "", (size_t)fl.n); fc += core_full; fc.append(fr.p ? fr.p : "", (size_t)fr.n); }
-        else fc = core_full;
+        thread_local std::string fc;
+        fc.clear();
+        if (flanks) { fc.append(fl.p ? fl.p : "", (size_t)fl.n); fc.append(core.p, (size_t)core.n); fc.append(fr.p ? fr.p : "", (size_t)fr.n); }
+        else fc.assign(core.p, (size_t)core.n);
         o.put(fc.data(), 250);
         o.put("...");
         o.put(fc.data() + fc.size() - 200, 200);
     } else {
-        if (flanks) { o.put(fl); o.put(core_full); o.put(fr); } else o.put(core_full);
+        if (flanks) { o.put(fl); o.put(core); o.put(fr); } else o.put(core);
     }
     o.c('\t');
     if (!r.variations.empty()) o.put(r.variations); else o.c('-');
@@ -353,13 +398,40 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out) {
         for (const Rec &r : job.final_recs) rows.push_back({&r, nullptr});
     }
     // sorted(all_repeats, key=lambda r: (natural_sort_key(r.chrom), r.start, r.end)) (bwt.py:4150)
-    std::stable_sort(rows.begin(), rows.end(), [&](const Row &a, const Row &b) {
+    // The rows arrive ordered by (unit, start) in the usual case (one contig
+    // per unit): then only runs of equal (unit, start) need a stable order by
+    // end, which equals the full stable sort.
+    auto unit_start_lt = [&](const Row &a, const Row &b) {
         const Rec &x = *a.r, &y = *b.r;
         const int32_t ux = job.contigs[(size_t)x.chrom].unit, uy = job.contigs[(size_t)y.chrom].unit;
         if (ux != uy) return ux < uy;
-        if (x.start != y.start) return x.start < y.start;
-        return x.end < y.end;
-    });
+        return x.start < y.start;
+    };
+    if (std::is_sorted(rows.begin(), rows.end(), unit_start_lt)) {
+        for (size_t i = 0; i < rows.size();) {
+            size_t j = i + 1;
+            while (j < rows.size() && !unit_start_lt(rows[i], rows[j])) ++j;   // equal (unit, start)
+            for (size_t a = i + 1; a < j; ++a) {   // stable insertion sort by end (runs are short)
+                const Row x = rows[a];
+                size_t b = a;
+                while (b > i && rows[b - 1].r->end > x.r->end) {
+                    rows[b] = rows[b - 1];
+                    --b;
+                }
+                rows[b] = x;
+            }
+            i = j;
+        }
+    } else {
+        std::stable_sort(rows.begin(), rows.end(), [&](const Row &a, const Row &b) {
+            const Rec &x = *a.r, &y = *b.r;
+            const int32_t ux = job.contigs[(size_t)x.chrom].unit, uy = job.contigs[(size_t)y.chrom].unit;
+            if (ux != uy) return ux < uy;
+            if (x.start != y.start) return x.start < y.start;
+            return x.end < y.end;
+        });
+    }
+    auto t1 = std::chrono::steady_clock::now();
     std::string head;
     switch (fmt) {
         case BWTMI_FMT_BED:
@@ -401,11 +473,12 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out) {
     out.parts.assign(chunks.size(), Text());
     out.part_unit.resize(chunks.size());
     for (size_t q = 0; q < chunks.size(); ++q) out.part_unit[q] = chunks[q].unit;
+    auto t2 = std::chrono::steady_clock::now();
     run_tasks((int64_t)chunks.size(), host_threads(job.params), [&](int64_t ck) {
         Out o;
         const Chunk &C = chunks[(size_t)ck];
         const int64_t a = C.a, b = C.b;
-        o.s.reserve((size_t)(b - a) * 192);
+        o.s.reserve((size_t)(b - a) * 256);
         double cp[4], ent;
         for (int64_t k = a; k < b; ++k) {
             const Rec &r = *rows[(size_t)k].r;
@@ -452,7 +525,13 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out) {
         }
         out.parts[(size_t)ck] = std::move(o.s);
     });
-    job.stage_ms[6] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    auto t3 = std::chrono::steady_clock::now();
+    job.stage_ms[6] = std::chrono::duration<double, std::milli>(t3 - t0).count();
+    if (const char *e = std::getenv("BWTMI_STATS"); e && *e == '1') {
+        auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "  render: compounds+sort %.1f chunking %.1f format %.1f ms (%zu rows)\n", d(t0, t1),
+                     d(t1, t2), d(t2, t3), rows.size());
+    }
 }
 
 std::vector<Text> render_parts(Job &job, int fmt) {
