@@ -952,14 +952,48 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     if (!one_offset) sort_by_pos(recs, nt);
     auto r3 = clk::now();
     const size_t n_before_collapse = recs.size();
-    std::vector<uint32_t, BigAlloc<uint32_t>> col;   // collapsed list as indices into recs (the slot takes the preferred record)
-    col.reserve(recs.size() / 4 + 16);
-    for (size_t k = 0; k < recs.size(); ++k) {
-        if (!col.empty() && should_collapse(u, recs[col.back()], recs[k])) {
-            if (!prefer_first(u, recs[col.back()], recs[k])) col.back() = (uint32_t)k;
-        } else {
-            col.push_back((uint32_t)k);
-        }
+    // collapsed list as indices into recs (the slot takes the preferred record).
+    // The fold only ever compares with the last kept record, and a collapse
+    // needs an overlap, so an index whose start is >= every earlier end always
+    // starts fresh: chunks cut at such indices fold independently.
+    std::vector<uint32_t, BigAlloc<uint32_t>> col;
+    {
+        const int64_t N = (int64_t)recs.size();
+        const int C = N > 65536 ? 4 * std::max(1, nt) : 1;
+        std::vector<int64_t> cmax((size_t)C, INT64_MIN), sb((size_t)C + 1, N);
+        parallel_items(C, nt, [&](int64_t t, int) {
+            int64_t m = INT64_MIN;
+            for (int64_t k = N * t / C; k < N * (t + 1) / C; ++k) m = std::max(m, recs[(size_t)k].end);
+            cmax[(size_t)t] = m;
+        });
+        std::vector<int64_t> pre((size_t)C, INT64_MIN);   // max end before nominal chunk t
+        for (int t = 1; t < C; ++t) pre[(size_t)t] = std::max(pre[(size_t)t - 1], cmax[(size_t)t - 1]);
+        sb[0] = 0;
+        parallel_items(C - 1, nt, [&](int64_t q, int) {
+            const int64_t t = q + 1;
+            int64_t i = N * t / C, m = pre[(size_t)t];
+            while (i < N && recs[(size_t)i].start < m) m = std::max(m, recs[(size_t)i++].end);
+            sb[(size_t)t] = i;
+        });
+        for (int t = 1; t <= C; ++t) sb[(size_t)t] = std::max(sb[(size_t)t], sb[(size_t)t - 1]);
+        std::vector<std::vector<uint32_t>> part((size_t)C);
+        parallel_items(C, nt, [&](int64_t t, int) {
+            auto &pc = part[(size_t)t];
+            pc.reserve((size_t)(sb[(size_t)t + 1] - sb[(size_t)t]) / 2 + 16);
+            for (int64_t k = sb[(size_t)t]; k < sb[(size_t)t + 1]; ++k) {
+                if (!pc.empty() && should_collapse(u, recs[pc.back()], recs[(size_t)k])) {
+                    if (!prefer_first(u, recs[pc.back()], recs[(size_t)k])) pc.back() = (uint32_t)k;
+                } else {
+                    pc.push_back((uint32_t)k);
+                }
+            }
+        });
+        std::vector<size_t> at((size_t)C + 1, 0);
+        for (int t = 0; t < C; ++t) at[(size_t)t + 1] = at[(size_t)t] + part[(size_t)t].size();
+        col.resize(at[(size_t)C]);
+        parallel_items(C, nt, [&](int64_t t, int) {
+            std::copy(part[(size_t)t].begin(), part[(size_t)t].end(), col.begin() + (std::ptrdiff_t)at[(size_t)t]);
+        });
     }
     auto r4 = clk::now();
     // 7. final filter (bwt.py:3940-3944), counted and materialised in parallel chunks

@@ -93,13 +93,27 @@ struct Row {
 };
 
 struct Compound {
-    std::deque<Rec> pool;   // records created here (k-mer scan and split pieces), pointer-stable
+    std::deque<Rec> pool;                // k-mer pieces, pointer-stable
+    std::deque<std::deque<Rec>> pools;   // split pieces of the walk chunks (a moved deque keeps its
+                                         // elements in place; the outer deque never moves its deques)
     std::vector<Row> rows;
+};
+
+// rows emitted by a walk over some indices, with the index each was emitted from
+struct Walk {
+    std::vector<Row> rows;
+    std::vector<size_t> at;
+    std::deque<Rec> pool;
+    size_t next = 0;
+    void emit(Row r, size_t i0) {
+        rows.push_back(r);
+        at.push_back(i0);
+    }
 };
 
 // _detect_compound_repeats (bwt.py:3995-4139) over the final records; works on
 // pointers, so the final records are never copied
-void detect_compounds(const Job &job, const RecVec &recs, Compound &out) {
+void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt) {
     auto T0 = std::chrono::steady_clock::now();
     std::vector<int32_t> chrom_order;
     std::vector<std::vector<const Rec *>> by(job.contigs.size());
@@ -156,8 +170,14 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out) {
         const Contig &ctg = job.contigs[(size_t)ch];
         const int64_t TL = ctg.trimmed_len();
         const char *tseq = ctg.trimmed();
-        size_t i = 0;
-        while (i < rs.size()) {
+        // The walk's only state is the index i; a step may consume 1 or 2
+        // records, or more after splits.  Chunks are walked speculatively in
+        // parallel as if the walk arrived at their first index; a serial
+        // repair walks from the true index until it reaches an index the
+        // speculative run also stepped from, after which the two coincide.
+        const size_t N = rs.size();
+        auto step = [&](size_t i, Walk &w) -> size_t {
+            const size_t i0 = i;
             const Rec *cur = rs[i];
             if (cur->motif.size() == 3 && cur->copies >= 10 && TL > 0) {
                 // repeat_seq = sequences[chrom][cur.start:cur.end] (trimmed sequence, restored
@@ -187,18 +207,18 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out) {
                         // actual = repeat_seq[:c1*l1], repeat_seq[c1*l1 : c1*l1 + c2*l2]
                         const int64_t x1 = std::min(c1 * l1, rl);
                         const int64_t y0 = std::min(c1 * l1, rl), y1 = std::max(y0, std::min(c1 * l1 + c2 * l2, rl));
-                        out.pool.push_back(kmer_piece(ch, cur->start, e1, std::string(rsq, (size_t)l1), c1, cur->tier,
+                        w.pool.push_back(kmer_piece(ch, cur->start, e1, std::string(rsq, (size_t)l1), c1, cur->tier,
                                                       ACT_TRIMMED, a, x1));
-                        Rec *r1 = &out.pool.back();
-                        out.pool.push_back(kmer_piece(ch, e1, e1 + c2 * l2, std::string(rsq + sp, (size_t)l2), c2,
+                        Rec *r1 = &w.pool.back();
+                        w.pool.push_back(kmer_piece(ch, e1, e1 + c2 * l2, std::string(rsq + sp, (size_t)l2), c2,
                                                       cur->tier, ACT_TRIMMED, a + y0, y1 - y0));
                         r1->is_compound = true;
-                        out.rows.push_back({r1, &out.pool.back()});
+                        w.emit({r1, &w.pool.back()}, i0);
                         ++i;   // the reference advances i inside the split loop (bwt.py:4083)
                     }
                 }
             }
-            if (i + 1 < rs.size()) {
+            if (i + 1 < N) {
                 const Rec *nx = rs[i + 1];
                 const int64_t gap = nx->start - cur->end;
                 if (gap <= 5 && cur->motif.size() <= 4 && nx->motif.size() <= 4 && cur->motif != nx->motif &&
@@ -218,15 +238,41 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out) {
                         if ((double)ov / (double)(ce - cs) >= 0.8) covered = true;
                     }
                     if (!covered) {
-                        out.rows.push_back({cur, nx});
-                        i += 2;
-                        continue;
+                        w.emit({cur, nx}, i0);
+                        return i + 2;
                     }
                 }
             }
-            out.rows.push_back({cur, nullptr});
-            ++i;
+            w.emit({cur, nullptr}, i0);
+            return i + 1;
+        };
+        const int K = N > 32768 ? 4 * std::max(1, nt) : 1;
+        std::vector<size_t> cut((size_t)K + 1);
+        for (int k = 0; k <= K; ++k) cut[(size_t)k] = N * (size_t)k / (size_t)K;
+        std::vector<uint8_t> from(N, 0);   // from[i]: the speculative run of i's chunk stepped from i
+        std::vector<Walk> W((size_t)K);
+        run_tasks(K, nt, [&](int64_t k) {
+            size_t i = cut[(size_t)k];
+            while (i < cut[(size_t)k + 1]) {
+                from[i] = 1;
+                i = step(i, W[(size_t)k]);
+            }
+            W[(size_t)k].next = i;
+        });
+        size_t ti = 0;
+        for (int k = 0; k < K; ++k) {
+            Walk &sp = W[(size_t)k];
+            if (ti >= cut[(size_t)k + 1]) continue;   // the true walk stepped over this chunk
+            Walk rep;
+            while (ti < cut[(size_t)k + 1] && !from[ti]) ti = step(ti, rep);
+            out.rows.insert(out.rows.end(), rep.rows.begin(), rep.rows.end());
+            out.pools.push_back(std::move(rep.pool));
+            if (ti >= cut[(size_t)k + 1]) continue;
+            size_t q = (size_t)(std::lower_bound(sp.at.begin(), sp.at.end(), ti) - sp.at.begin());
+            out.rows.insert(out.rows.end(), sp.rows.begin() + (std::ptrdiff_t)q, sp.rows.end());
+            ti = sp.next;
         }
+        for (auto &w : W) out.pools.push_back(std::move(w.pool));
     }
     if (const char *e = std::getenv("BWTMI_STATS"); e && *e == '1') {
         auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -391,7 +437,7 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out) {
     Compound comp;
     std::vector<Row> rows;
     if (fmt == BWTMI_FMT_STRFINDER) {
-        detect_compounds(job, job.final_recs, comp);
+        detect_compounds(job, job.final_recs, comp, host_threads(job.params));
         rows.swap(comp.rows);
     } else {
         rows.reserve(job.final_recs.size());
@@ -407,21 +453,37 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out) {
         if (ux != uy) return ux < uy;
         return x.start < y.start;
     };
-    if (std::is_sorted(rows.begin(), rows.end(), unit_start_lt)) {
-        for (size_t i = 0; i < rows.size();) {
-            size_t j = i + 1;
-            while (j < rows.size() && !unit_start_lt(rows[i], rows[j])) ++j;   // equal (unit, start)
-            for (size_t a = i + 1; a < j; ++a) {   // stable insertion sort by end (runs are short)
-                const Row x = rows[a];
-                size_t b = a;
-                while (b > i && rows[b - 1].r->end > x.r->end) {
-                    rows[b] = rows[b - 1];
-                    --b;
+    const int nt = host_threads(job.params);
+    const size_t NR = rows.size();
+    const int RC = NR > 65536 ? 4 * nt : 1;
+    std::vector<uint8_t> chunk_ok((size_t)RC, 1);
+    run_tasks(RC, nt, [&](int64_t t) {   // sorted by (unit, start)?  chunk t checks pairs ending in it
+        const size_t a = std::max<size_t>(1, NR * (size_t)t / (size_t)RC), b = NR * (size_t)(t + 1) / (size_t)RC;
+        for (size_t k = a; k < b; ++k)
+            if (unit_start_lt(rows[k], rows[k - 1])) { chunk_ok[(size_t)t] = 0; return; }
+    });
+    bool by_unit_start = true;
+    for (auto v : chunk_ok) by_unit_start = by_unit_start && v;
+    if (by_unit_start) {
+        run_tasks(RC, nt, [&](int64_t t) {   // chunk t orders the equal-(unit, start) runs that begin in it
+            size_t i = NR * (size_t)t / (size_t)RC;
+            const size_t b = NR * (size_t)(t + 1) / (size_t)RC;
+            while (i > 0 && i < b && !unit_start_lt(rows[i - 1], rows[i])) ++i;
+            while (i < b) {
+                size_t j = i + 1;
+                while (j < NR && !unit_start_lt(rows[i], rows[j])) ++j;   // equal (unit, start)
+                for (size_t a = i + 1; a < j; ++a) {   // stable insertion sort by end (runs are short)
+                    const Row x = rows[a];
+                    size_t q = a;
+                    while (q > i && rows[q - 1].r->end > x.r->end) {
+                        rows[q] = rows[q - 1];
+                        --q;
+                    }
+                    rows[q] = x;
                 }
-                rows[b] = x;
+                i = j;
             }
-            i = j;
-        }
+        });
     } else {
         std::stable_sort(rows.begin(), rows.end(), [&](const Row &a, const Row &b) {
             const Rec &x = *a.r, &y = *b.r;
