@@ -8,7 +8,9 @@
 //             ranks keys of equal digit with 8 ballots (wave64 match-any) in
 //             index order, so the pass is stable; the tile is reordered by
 //             digit in LDS and streamed out in that order, so each digit's
-//             run of the tile is one contiguous, coalesced write.
+//             run of the tile is one contiguous, coalesced write.  Keys and
+//             then values take turns in one 32 KB LDS buffer (4 workgroups
+//             per CU instead of 3).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -92,14 +94,17 @@ __global__ __launch_bounds__(kBlock) void k_chunk_scan(const T *__restrict__ in,
 }
 
 // ------------------------------------------------------------------ radix
+// Pass geometry: 256-thread workgroups (thread t owns digit t in the tile
+// scan), ITEMS keys per thread, tile = 256 * ITEMS.
+template <int ITEMS>
 __global__ __launch_bounds__(kBlock) void k_hist(const uint64_t *__restrict__ keys, uint32_t *__restrict__ counts,
                                                  int64_t n, int shift, int64_t ntiles) {
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * kTile;
+    const int64_t base = (int64_t)blockIdx.x * (kBlock * ITEMS);
 #pragma unroll
-    for (int i = 0; i < kItems; ++i) {
+    for (int i = 0; i < ITEMS; ++i) {
         const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
         if (idx < n) atomicAdd(&h[(keys[idx] >> shift) & 255u], 1u);
     }
@@ -107,39 +112,52 @@ __global__ __launch_bounds__(kBlock) void k_hist(const uint64_t *__restrict__ ke
     counts[(int64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
+template <bool NT, class T>
+__device__ __forceinline__ void st(T *p, T v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // Scatter of one tile, staged through LDS so that the global writes are
 // coalesced: every key is ranked inside the tile (stable: wave order, then
 // item order, then lane order), written to LDS at its tile-sorted slot, and the
 // tile is then streamed out in slot order -- consecutive lanes write
 // consecutive addresses inside each digit's run.
-template <class V>
+//   NT    : nontemporal (streaming) global stores -- the pass output is not
+//           re-read before it has left the caches anyway
+//   SPLIT : keys and values take turns in one LDS staging buffer (the slot ->
+//           global position map stays in registers), so a tile needs 8 B of
+//           LDS per key instead of 8 + sizeof(V) and more workgroups fit a CU
+template <class V, int ITEMS, bool NT, bool SPLIT>
 __global__ __launch_bounds__(kBlock) void k_scatter(const uint64_t *__restrict__ kin, const V *__restrict__ vin,
                                                     uint64_t *__restrict__ kout, V *__restrict__ vout,
                                                     const uint32_t *__restrict__ offs, int64_t n, int shift,
                                                     int64_t ntiles) {
+    constexpr int kT = kBlock * ITEMS;
     __shared__ uint32_t wcnt[kWaves][256];   // per-wave digit counts, then per-wave digit bases
     __shared__ uint32_t gdelta[256];         // global position of tile slot j = gdelta[digit] + j
     __shared__ uint32_t dsum[kWaves];
-    __shared__ uint64_t ks[kTile];
-    __shared__ V vs[kTile];
+    __shared__ uint64_t ks[kT];
+    __shared__ V vs_own[SPLIT ? 1 : kT];
+    V *vs = SPLIT ? reinterpret_cast<V *>(ks) : vs_own;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int w = 0; w < kWaves; ++w) wcnt[w][threadIdx.x] = 0;
     __syncthreads();
-    const int64_t tbase = (int64_t)blockIdx.x * kTile;
-    const int64_t wbase = tbase + (int64_t)wv * (kItems * 64);
+    const int64_t tbase = (int64_t)blockIdx.x * kT;
+    const int64_t wbase = tbase + (int64_t)wv * (ITEMS * 64);
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint64_t k[kItems];
-    V v[kItems];
-    uint32_t r[kItems];   // rank among the wave's earlier keys of the same digit
+    uint64_t k[ITEMS];
+    V v[ITEMS];
+    uint32_t r[ITEMS];   // rank among the wave's earlier keys of the same digit
 #pragma unroll
-    for (int i = 0; i < kItems; ++i) {
+    for (int i = 0; i < ITEMS; ++i) {
         const int64_t idx = wbase + i * 64 + lane;
         const bool valid = idx < n;
         k[i] = valid ? kin[idx] : 0ull;
         if (vin) v[i] = valid ? vin[idx] : (V)0;
     }
 #pragma unroll
-    for (int i = 0; i < kItems; ++i) {
+    for (int i = 0; i < ITEMS; ++i) {
         const int64_t idx = wbase + i * 64 + lane;
         const bool valid = idx < n;
         const uint32_t d = (uint32_t)((k[i] >> shift) & 255u);
@@ -180,35 +198,51 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const uint64_t *__restrict__
         }
     }
     __syncthreads();
+    uint32_t slot[ITEMS];
 #pragma unroll
-    for (int i = 0; i < kItems; ++i) {
+    for (int i = 0; i < ITEMS; ++i) {
         const int64_t idx = wbase + i * 64 + lane;
+        slot[i] = 0;
         if (idx < n) {
             const uint32_t d = (uint32_t)((k[i] >> shift) & 255u);
-            const uint32_t slot = wcnt[wv][d] + r[i];
-            ks[slot] = k[i];
-            if (vin) vs[slot] = v[i];
+            slot[i] = wcnt[wv][d] + r[i];
+            ks[slot[i]] = k[i];
+            if (!SPLIT && vin) vs[slot[i]] = v[i];
         }
     }
     __syncthreads();
     const int64_t rem = n - tbase;
-    const int cntt = rem < kTile ? (int)rem : kTile;
+    const int cntt = rem < kT ? (int)rem : kT;
+    uint32_t pos[ITEMS];   // global position of tile slot i * 256 + t
 #pragma unroll
-    for (int i = 0; i < kItems; ++i) {
+    for (int i = 0; i < ITEMS; ++i) {
         const int j = i * kBlock + threadIdx.x;
+        pos[i] = 0;
         if (j < cntt) {
             const uint64_t key = ks[j];
-            const uint32_t pos = gdelta[(key >> shift) & 255u] + (uint32_t)j;
-            kout[pos] = key;
-            if (vout) vout[pos] = vs[j];
+            pos[i] = gdelta[(key >> shift) & 255u] + (uint32_t)j;
+            st<NT>(kout + pos[i], key);
+            if (!SPLIT && vout) st<NT>(vout + pos[i], vs[j]);
+        }
+    }
+    if (SPLIT && vin) {
+        __syncthreads();   // every key has left the staging buffer
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+            if (wbase + i * 64 + lane < n) vs[slot[i]] = v[i];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            const int j = i * kBlock + threadIdx.x;
+            if (j < cntt) st<NT>(vout + pos[i], vs[j]);
         }
     }
 }
 
-template <class V>
-void radix_sort_impl(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int bit1) {
-    if (n <= 1) return;
-    const int64_t ntiles = (n + kTile - 1) / kTile;
+template <class V, int ITEMS, bool NT, bool SPLIT>
+void radix_sort_cfg(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int bit1) {
+    constexpr int kT = kBlock * ITEMS;
+    const int64_t ntiles = (n + kT - 1) / kT;
     c.slot[S_SORT_TMP0].ensure((size_t)n * sizeof(uint64_t));
     if (vals) c.slot[S_SORT_TMP1].ensure((size_t)n * sizeof(V));
     c.slot[S_SORT_HIST].ensure((size_t)ntiles * 256 * sizeof(uint32_t));
@@ -218,14 +252,14 @@ void radix_sort_impl(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int b
     int passes = 0;
     for (int sh = bit0; sh < bit1; sh += 8) {
         c.kbegin("radix_hist", (double)n * 8.0);                       // read keys once
-        hipLaunchKernelGGL(k_hist, dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream, ka, cnt, n, sh, ntiles);
+        hipLaunchKernelGGL(k_hist<ITEMS>, dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream, ka, cnt, n, sh, ntiles);
         c.kend();
         exclusive_scan<uint32_t>(c, cnt, cnt, ntiles * 256);
         // read (key, value) once, write it once
         c.kbegin(sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16",
                  (double)n * 2.0 * (8.0 + (vals ? (double)sizeof(V) : 0.0)));
-        hipLaunchKernelGGL(k_scatter<V>, dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream, ka, va, kb, vb, cnt, n,
-                           sh, ntiles);
+        hipLaunchKernelGGL((k_scatter<V, ITEMS, NT, SPLIT>), dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream, ka, va,
+                           kb, vb, cnt, n, sh, ntiles);
         c.kend();
         std::swap(ka, kb);
         std::swap(va, vb);
@@ -236,6 +270,16 @@ void radix_sort_impl(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int b
         HIPCHECK(hipMemcpyAsync(keys, ka, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToDevice, c.stream));
         if (vals) HIPCHECK(hipMemcpyAsync(vals, va, (size_t)n * sizeof(V), hipMemcpyDeviceToDevice, c.stream));
     }
+}
+
+// Pass geometry measured on the bench workload (r01r/r01s, radix_scatter_kv12
+// = fraction of the 8 TB/s peak): 16 items + shared staging 0.50-0.51 (20
+// items 0.52, 12 items 0.50, 8 items 0.47); separate key and value staging
+// 0.44-0.45; nontemporal stores 0.34-0.41 in every geometry.
+template <class V>
+void radix_sort_impl(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int bit1) {
+    if (n <= 1) return;
+    radix_sort_cfg<V, 16, false, true>(c, keys, vals, n, bit0, bit1);
 }
 
 }  // namespace
