@@ -170,21 +170,38 @@ __global__ __launch_bounds__(256) void k_runs(const uint32_t *__restrict__ P, in
             if (Mn == FULL) return -1;
             return j0 + 32 + (int64_t)__ffs(~Mn) - 1;
         };
+        // Streaks (runs of full words): the first full word of each owns the
+        // run.  Its end lies in the first non-full word after it -- found by a
+        // ballot when that word is in this wave, else by the whole wave
+        // scanning 64 words per step (long exact arrays repeat for many L, and
+        // one lane walking them word by word stalls its wave on dependent loads).
+        const bool sstart = owned && M == FULL && Mp != FULL;
+        const uint64_t nf = __ballot(M != FULL);
+        const uint64_t above = lane == 63 ? 0ull : (nf & (~0ull << (lane + 1)));
+        const int src = above ? __ffsll((unsigned long long)above) - 1 : lane;
+        const uint32_t Mend = (uint32_t)__shfl((int)M, src, 64);
+        int64_t e_streak = sstart && above ? (w + (src - lane)) * 32 + (int64_t)__ffs(~Mend) - 1 : -1;
+        const bool beyond = sstart && !above;
+        if (__any(beyond)) {   // at most one lane: the streak runs past lane 63's word
+            for (int64_t q0 = wave_base + 63;; q0 += 64) {
+                const uint32_t Mq = eq32<B>(P, q0 + lane, L, n);   // 0 past the text: ends the scan
+                const uint64_t nb = __ballot(Mq != FULL);
+                if (nb) {
+                    const int f = __ffsll((unsigned long long)nb) - 1;
+                    const uint32_t Mf = (uint32_t)__shfl((int)Mq, f, 64);
+                    if (beyond) e_streak = (q0 + f) * 32 + (int64_t)__ffs(~Mf) - 1;
+                    break;
+                }
+            }
+        }
         if (owned) {
             if (M == FULL) {
-                if (Mp != FULL) {   // first full word of a streak
+                if (sstart) {   // first full word of a streak
                     const int64_t s = j0 - (int64_t)__clz(~Mp);
-                    int64_t q = w + 1;
-                    uint32_t Mq = Mn;
-                    while (Mq == FULL) {
-                        ++q;
-                        Mq = eq32<B>(P, q, L, n);
-                    }
-                    const int64_t e = q * 32 + (int64_t)__ffs(~Mq) - 1;
-                    if (e - s >= K) {
+                    if (e_streak - s >= K) {
                         cnt = 1;
                         s1 = s;
-                        e1 = e;
+                        e1 = e_streak;
                     }
                 }
             } else if (K <= 62 && M != 0u) {

@@ -19,10 +19,9 @@ import sys
 def short(name: str) -> str:
     m = re.search(r"::(k_[A-Za-z0-9_]+)", name)
     s = m.group(1) if m else name.split("(")[0].strip()
-    if "<unsigned int>" in name:
-        s += "<u32>"
-    elif "<unsigned long>" in name:
-        s += "<u64>"
+    t = re.search(r"<(unsigned int|unsigned long)[,>]", name)   # first template argument
+    if t:
+        s += "<u32>" if t.group(1) == "unsigned int" else "<u64>"
     return s
 
 
