@@ -9,8 +9,8 @@
 // Kernel pipeline (one launch each, all on the ctx stream):
 //   k_pack       bytes -> B-bit codes (B = 2/4/8 from the contig's alphabet),
 //                64-bit words, coalesced
-//   k_runs       grid (word tiles x L chunks): every lane owns 32 positions of
-//                one L; equality masks by XOR of packed windows, neighbour
+//   k_runs       grid (word tiles x L chunks): every lane owns 32 positions
+//                for every L of its chunk; equality masks by XOR of packed windows, neighbour
 //                masks by wave shuffles; emits the maximal runs long enough
 //                to hold min_copies copies (candidates)
 //   radix sort   candidates by (L desc, s asc) -- the reference order
@@ -89,53 +89,86 @@ __device__ __forceinline__ uint32_t eq32(const uint32_t *__restrict__ P, int64_t
     return m;
 }
 
+// Candidates go to kCandSegs segments of seg_cap slots, each with its own
+// counter (segment = workgroup index mod kCandSegs): one counter for the whole
+// grid serialises ~1.5M same-address atomics at the memory side.  The host
+// compacts the segments afterwards (their order is irrelevant: a radix sort
+// follows).
+constexpr int kCandSegs = 64;
+
 struct CandOut {
-    uint64_t *keys;
+    uint64_t *keys;   // [kCandSegs][seg_cap]
     uint64_t *vals;
-    unsigned long long *count;
-    int64_t cap;
+    unsigned long long *count;   // [kCandSegs]
+    int64_t seg_cap;
     int32_t umax;
 };
 
-// candidate at a slot reserved by the wave (slots past cap are counted, not
-// written: the host retries with a larger buffer)
-__device__ __forceinline__ void put(const CandOut &o, unsigned long long idx, int64_t L, int64_t s, int64_t e) {
-    if ((int64_t)idx < o.cap) {
-        o.keys[idx] = ((uint64_t)(o.umax - L) << 40) | (uint64_t)s;
-        o.vals[idx] = (uint64_t)e;
+// candidate at slot idx of segment seg, reserved by the wave (slots past
+// seg_cap are counted, not written: the host retries with larger segments)
+__device__ __forceinline__ void put(const CandOut &o, int seg, unsigned long long idx, int64_t L, int64_t s,
+                                    int64_t e) {
+    if ((int64_t)idx < o.seg_cap) {
+        const int64_t at = (int64_t)seg * o.seg_cap + (int64_t)idx;
+        o.keys[at] = ((uint64_t)(o.umax - L) << 40) | (uint64_t)s;
+        o.vals[at] = (uint64_t)e;
     }
+}
+
+// segments -> one contiguous array (segment order)
+__global__ void k_cand_gather(const uint64_t *__restrict__ ksegs, const uint64_t *__restrict__ vsegs,
+                              const unsigned long long *__restrict__ count, const int64_t *__restrict__ off,
+                              int64_t seg_cap, uint64_t *__restrict__ kout, uint64_t *__restrict__ vout) {
+    const int seg = blockIdx.y;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)count[seg]) return;
+    kout[off[seg] + i] = ksegs[(int64_t)seg * seg_cap + i];
+    vout[off[seg] + i] = vsegs[(int64_t)seg * seg_cap + i];
 }
 
 constexpr int kOwn = 62;   // words owned per wave: lanes 1..62; lanes 0 and 63 only feed neighbours
 
-// grid.x: tiles of 4 waves x 62 words; grid.y: group g of unit lengths
-// L in [32g, 32g+31].  All L of a group read the same two words q = w+g,
-// q+1, so a lane loads its planes once and derives every M_L in registers.
+// grid.x: tiles of 4 waves x 62 words; grid.y: runs of gper groups of unit
+// lengths, group g = L in [32g, 32g+31].  All L of a group read the same two
+// words q = w+g, q+1, so a lane holds its planes in registers and derives
+// every M_L of the group from them; a workgroup walks its groups in turn.
 template <int B>
 __global__ __launch_bounds__(256) void k_runs(const uint32_t *__restrict__ P, int64_t n, int64_t nwords32,
-                                              int32_t lmin, int32_t lmax, int64_t mc, CandOut out) {
+                                              int32_t lmin, int32_t lmax, int64_t mc, int32_t gper, CandOut out) {
     const int lane = threadIdx.x & 63;
     const int64_t wave_base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kOwn;
     const int64_t w = wave_base - 1 + lane;
     const bool owned = lane >= 1 && lane <= kOwn && w < nwords32;
-    const int64_t g = (int64_t)blockIdx.y + (lmin >> 5);
     const int64_t j0 = w * 32;
     const int64_t tile_j0 = (int64_t)blockIdx.x * 4 * kOwn * 32;
-    uint32_t a[B], lo[B], hi[B];
     const bool inb = w >= 0 && w < nwords32;
+    // this block's unit-length groups: g in [g0, g1), group g = L in [32g, 32g+31]
+    const int64_t g0 = (int64_t)blockIdx.y * gper + (lmin >> 5);
+    const int64_t g1 = min(g0 + (int64_t)gper, (int64_t)(lmax >> 5) + 1);
     // words past the text (the planes are zero-padded by 8 words) only feed
     // positions that the `lim` mask below discards
-    const bool lok = inb && w + g + 1 < nwords32 + 8;
+    auto word = [&](int64_t q, int p) { return inb && q < nwords32 + 8 ? P[q * B + p] : 0u; };
+    // group g compares word w with words w+g, w+g+1: consecutive groups share
+    // one of them, so each group loads one new word per plane (prefetched a
+    // group ahead)
+    uint32_t a[B], lo[B], hi[B], nx[B];
 #pragma unroll
     for (int p = 0; p < B; ++p) {
         a[p] = inb ? P[w * B + p] : 0u;
-        lo[p] = lok ? P[(w + g) * B + p] : 0u;
-        hi[p] = lok ? P[(w + g + 1) * B + p] : 0u;
+        lo[p] = word(w + g0, p);
+        hi[p] = word(w + g0 + 1, p);
     }
+    for (int64_t g = g0; g < g1; ++g) {
+#pragma unroll
+    for (int p = 0; p < B; ++p) nx[p] = g + 1 < g1 ? word(w + g + 2, p) : 0u;
+    bool done = false;
     for (int r = 0; r < 32; ++r) {
         const int64_t L = g * 32 + r;
         if (L < lmin) continue;
-        if (L > lmax || tile_j0 >= n - L) break;        // uniform across the block
+        if (L > lmax || tile_j0 >= n - L) {   // uniform across the block; L only grows
+            done = true;
+            break;
+        }
         uint32_t x = 0;
 #pragma unroll
         for (int p = 0; p < B; ++p) x |= a[p] ^ __builtin_amdgcn_alignbit(hi[p], lo[p], (uint32_t)r);
@@ -235,20 +268,28 @@ __global__ __launch_bounds__(256) void k_runs(const uint32_t *__restrict__ P, in
         }
         const int tot = __shfl(incl, 63, 64);
         if (tot == 0) continue;   // wave-uniform
+        const int seg = (int)(blockIdx.x & (kCandSegs - 1));
         unsigned long long base = 0;
-        if (lane == 63) base = atomicAdd(out.count, (unsigned long long)tot);
+        if (lane == 63) base = atomicAdd(out.count + seg, (unsigned long long)tot);
         base = __shfl(base, 63, 64);
         unsigned long long at = base + (unsigned long long)(incl - cnt);
         if (cnt == 0) continue;
         if (M == FULL) {
-            put(out, at, L, s1, e1);
+            put(out, seg, at, L, s1, e1);
         } else {
             while (qual) {
                 const int k = __ffs(qual) - 1;
                 qual &= qual - 1;
-                put(out, at++, L, j0 + k, run_end(k));
+                put(out, seg, at++, L, j0 + k, run_end(k));
             }
         }
+    }
+    if (done) break;
+#pragma unroll
+    for (int p = 0; p < B; ++p) {
+        lo[p] = hi[p];
+        hi[p] = nx[p];
+    }
     }
 }
 
@@ -364,8 +405,10 @@ void launch_runs(Ctx &c, const uint32_t *P, int64_t n, int32_t lmin, int32_t lma
     const int64_t nwords32 = (n + 31) / 32;
     const int64_t tiles = (nwords32 + 4 * kOwn - 1) / (4 * kOwn);
     const int64_t groups = (int64_t)(lmax >> 5) - (int64_t)(lmin >> 5) + 1;
-    hipLaunchKernelGGL((k_runs<B>), dim3((unsigned)tiles, (unsigned)groups), dim3(256), 0, c.stream, P, n, nwords32,
-                       lmin, lmax, mc, out);
+    const int32_t gper = 8;   // unit-length groups per workgroup (32 L each)
+    const int64_t gblocks = (groups + gper - 1) / gper;
+    hipLaunchKernelGGL((k_runs<B>), dim3((unsigned)tiles, (unsigned)gblocks), dim3(256), 0, c.stream, P, n, nwords32,
+                       lmin, lmax, mc, gper, out);
 }
 
 }  // namespace
@@ -455,16 +498,18 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     else hipLaunchKernelGGL(k_pack<8>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
     HIPCHECK(hipGetLastError());
 
-    // 2. candidate runs
-    int64_t cap = std::max<int64_t>(1 << 16, n / 8);
+    // 2. candidate runs (segmented output, compacted below)
+    int64_t seg_cap = std::max<int64_t>(1 << 12, n / 8 / kCandSegs + 1024);
+    unsigned long long segn[kCandSegs] = {0};
     unsigned long long ncand = 0;
-    for (int attempt = 0; attempt < 3; ++attempt) {
-        c.slot[S_CAND_K].ensure((size_t)cap * sizeof(uint64_t));
-        c.slot[S_CAND_V].ensure((size_t)cap * sizeof(uint64_t));
-        c.slot[S_MISC3].ensure(sizeof(unsigned long long));
-        HIPCHECK(hipMemsetAsync(c.slot[S_MISC3].p, 0, sizeof(unsigned long long), st));
-        CandOut co{c.slot[S_CAND_K].as<uint64_t>(), c.slot[S_CAND_V].as<uint64_t>(),
-                   c.slot[S_MISC3].as<unsigned long long>(), cap, lmax};
+    c.slot[S_MISC3].ensure(kCandSegs * (sizeof(unsigned long long) + sizeof(int64_t)));
+    unsigned long long *d_count = c.slot[S_MISC3].as<unsigned long long>();
+    int64_t *d_off = reinterpret_cast<int64_t *>(d_count + kCandSegs);
+    for (int attempt = 0;; ++attempt) {
+        c.slot[S_CAND_K2].ensure((size_t)(seg_cap * kCandSegs) * sizeof(uint64_t));
+        c.slot[S_CAND_V2].ensure((size_t)(seg_cap * kCandSegs) * sizeof(uint64_t));
+        HIPCHECK(hipMemsetAsync(d_count, 0, kCandSegs * sizeof(unsigned long long), st));
+        CandOut co{c.slot[S_CAND_K2].as<uint64_t>(), c.slot[S_CAND_V2].as<uint64_t>(), d_count, seg_cap, lmax};
         hipEvent_t ka = nullptr, kb = nullptr;
         if (c.timing) {
             HIPCHECK(hipEventCreate(&ka));
@@ -480,7 +525,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
         c.kend();
         HIPCHECK(hipGetLastError());
         if (c.timing) HIPCHECK(hipEventRecord(kb, st));
-        HIPCHECK(hipMemcpyAsync(&ncand, c.slot[S_MISC3].p, sizeof ncand, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(segn, d_count, sizeof segn, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
         if (c.timing) {
             float ms = 0;
@@ -492,8 +537,30 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
             (void)hipEventDestroy(ka);
             (void)hipEventDestroy(kb);
         }
-        if ((int64_t)ncand <= cap) break;
-        cap = (int64_t)ncand + (int64_t)ncand / 4 + 1024;
+        unsigned long long mx = 0;
+        ncand = 0;
+        for (int q = 0; q < kCandSegs; ++q) {
+            ncand += segn[q];
+            mx = std::max(mx, segn[q]);
+        }
+        if ((int64_t)mx <= seg_cap) break;
+        if (attempt >= 2) fail(BWTMI_E_STATE, "strict scan: candidate segments overflow after %d attempts", attempt + 1);
+        seg_cap = (int64_t)mx + (int64_t)mx / 4 + 1024;   // exact counts: the next attempt fits
+    }
+    if (ncand > 0) {
+        int64_t off[kCandSegs];
+        unsigned long long mx = 0;
+        for (int q = 0; q < kCandSegs; ++q) {
+            off[q] = q ? off[q - 1] + (int64_t)segn[q - 1] : 0;
+            mx = std::max(mx, segn[q]);
+        }
+        c.slot[S_CAND_K].ensure((size_t)ncand * sizeof(uint64_t));
+        c.slot[S_CAND_V].ensure((size_t)ncand * sizeof(uint64_t));
+        HIPCHECK(hipMemcpyAsync(d_off, off, sizeof off, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_cand_gather, dim3((unsigned)((mx + 255) / 256), kCandSegs), dim3(256), 0, st,
+                           c.slot[S_CAND_K2].as<uint64_t>(), c.slot[S_CAND_V2].as<uint64_t>(), d_count, d_off,
+                           seg_cap, c.slot[S_CAND_K].as<uint64_t>(), c.slot[S_CAND_V].as<uint64_t>());
+        HIPCHECK(hipGetLastError());
     }
     const int64_t nc = (int64_t)ncand;
     res.candidates = nc;
