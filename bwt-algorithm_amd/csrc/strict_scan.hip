@@ -94,7 +94,7 @@ __device__ __forceinline__ uint32_t eq32(const uint32_t *__restrict__ P, int64_t
 // grid serialises ~1.5M same-address atomics at the memory side.  The host
 // compacts the segments afterwards (their order is irrelevant: a radix sort
 // follows).
-constexpr int kCandSegs = 64;
+constexpr int kCandSegs = 256;
 
 struct CandOut {
     uint64_t *keys;   // [kCandSegs][seg_cap]
