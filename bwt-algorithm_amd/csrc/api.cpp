@@ -505,7 +505,18 @@ int bwtmi_job_reset(bwtmi_job *job) {
         job->j.hits.clear();
         job->j.screened.clear();
         job->j.raw_n.clear();
-        job->j.final_recs.clear();
+        {   // the records' heap strings are released in parallel; the serial
+            // destruction that follows only meets short (inline) strings
+            RecVec old;
+            old.swap(job->j.final_recs);
+            const int64_t n = (int64_t)old.size(), CH = 16384;
+            run_tasks((n + CH - 1) / CH, host_threads(job->j.params), [&](int64_t k) {
+                for (int64_t i = k * CH; i < std::min(n, (k + 1) * CH); ++i) {
+                    std::string().swap(old[(size_t)i].motif);
+                    std::string().swap(old[(size_t)i].variations);
+                }
+            });
+        }
         job->j.t3.clear();
         job->j.postprocessed = false;
     });

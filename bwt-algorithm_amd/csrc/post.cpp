@@ -438,21 +438,22 @@ ItemVec suppress_nested(const ItemVec &rs, double thr, int nt) {
     return kept;
 }
 
-// optional counters (BWTMI_STATS=1): recompute calls / time, merge accepts
 std::atomic<int64_t> g_recomputes{0}, g_recompute_ns{0}, g_merges{0}, g_canons{0}, g_tests{0}, g_same{0};
-const bool g_stats = [] { const char *e = std::getenv("BWTMI_STATS"); return e && *e == '1'; }();
+// BWTMI_STATS=1: stage timers; =2: also per-recompute / per-test counters (slow)
+const bool g_stats = [] { const char *e = std::getenv("BWTMI_STATS"); return e && (*e == '1' || *e == '2'); }();
+const bool g_counters = [] { const char *e = std::getenv("BWTMI_STATS"); return e && *e == '2'; }();
 std::atomic<int64_t> g_hist_n[8][8], g_hist_ns[8][8];   // [log4 motif len][log4 region len]
 inline int lg4(int64_t v) { int k = 0; while (v >= 4 && k < 7) { v >>= 2; ++k; } return k; }
 
 // bwt.py:3515-3614 (on the trimmed sequence, before coordinate restore)
 Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t start, int64_t end,
                int64_t motif_len, int32_t tier) {
-    struct Tick {   // BWTMI_STATS=1 only
+    struct Tick {   // BWTMI_STATS=2 only
         int a, b;
         std::chrono::steady_clock::time_point t;
-        Tick(int a_, int b_) : a(a_), b(b_) { if (g_stats) t = std::chrono::steady_clock::now(); }
+        Tick(int a_, int b_) : a(a_), b(b_) { if (g_counters) t = std::chrono::steady_clock::now(); }
         ~Tick() {
-            if (!g_stats) return;
+            if (!g_counters) return;
             const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t).count();
             g_recomputes.fetch_add(1, std::memory_order_relaxed);
             g_recompute_ns.fetch_add(ns, std::memory_order_relaxed);
@@ -547,7 +548,7 @@ struct Canon {
 
 inline const std::string &canon_get(const UnitCtx &u, const Item &it, Canon &c) {
     if (!c.ok) {
-        if (g_stats) g_canons.fetch_add(1, std::memory_order_relaxed);
+        if (g_counters) g_canons.fetch_add(1, std::memory_order_relaxed);
         thread_local std::string tmp;
         const std::string_view mv = motif_of(u, it);
         tmp.assign(mv.data(), mv.size());
@@ -602,16 +603,16 @@ bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, Canon &c1,
     if (r1.mlen == 0 || r2.mlen == 0) return false;
     const int64_t ml = std::min(r1.mlen, r2.mlen);
     if (std::max<int64_t>(0, r2.start - r1.end) > ml + 1) return false;   // cheap test first
-    if (g_stats) g_tests.fetch_add(1, std::memory_order_relaxed);
+    if (g_counters) g_tests.fetch_add(1, std::memory_order_relaxed);
     if (!same_canonical(u, r1, c1, r2, c2)) return false;
-    if (g_stats) g_same.fetch_add(1, std::memory_order_relaxed);
+    if (g_counters) g_same.fetch_add(1, std::memory_order_relaxed);
     const int64_t s = std::min(r1.start, r2.start), e = std::max(r1.end, r2.end);
     const int32_t tier = std::min(r1.tier, r2.tier);
     Item mg = recompute(u, pools, w, r1.chrom, s, e, std::max<int64_t>(1, ml), tier);
     if (mg.x->copies < (double)u.min_copies) return false;
     const double base = std::max(std::max(mm_of(r1), mm_of(r2)), 0.01);
     if (!(mg.x->mm <= base + 0.2)) return false;
-    if (g_stats) g_merges.fetch_add(1, std::memory_order_relaxed);
+    if (g_counters) g_merges.fetch_add(1, std::memory_order_relaxed);
     if ((int64_t)r1.mlen == std::max<int64_t>(1, ml)) merged = mg;   // len(r1.consensus_motif)
     else merged = recompute(u, pools, w, r1.chrom, s, e, r1.mlen, tier);
     return true;
@@ -710,6 +711,7 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
         cur = sp.pending;
         cc = std::move(sp.pending_canon);
     }
+    auto ts2 = std::chrono::steady_clock::now();
     std::vector<size_t> at((size_t)K + 1, 0);
     for (int64_t k = 0; k < K; ++k) {
         const SpecOut &sp = spec[(size_t)k];
@@ -726,6 +728,11 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
             std::copy(sp.emitted.begin() + (std::ptrdiff_t)from[(size_t)k], sp.emitted.end(), dst + rp.size());
     });
     out[at[(size_t)K]] = cur;
+    if (g_stats) {
+        auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "  merge: repair %.1f assemble %.1f ms\n", d(ts1, ts2),
+                     d(ts2, std::chrono::steady_clock::now()));
+    }
     return out;
 }
 
@@ -828,13 +835,13 @@ Item item_of_rec(Pools &pools, const Rec &r) {
 }
 
 // final Rec of an item (after restore): strict fields per bwt.py:1972-1993
-Rec materialize(const UnitCtx &u, const Item &it) {
+Rec materialize(const UnitCtx &u, const Item &it, int64_t shift) {
     Rec r;
     const Contig &c = u.job->contigs[(size_t)it.chrom];
     r.chrom = it.chrom;
     r.tier = it.tier;
-    r.start = it.start;
-    r.end = it.end;
+    r.start = it.start + shift;
+    r.end = it.end + shift;
     r.length = it.end - it.start;
     if (it.x) {
         const Extra &x = *it.x;
@@ -938,16 +945,20 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     auto r2 = clk::now();
     // 5. restore coordinates (bwt.py:3316-3325); actual_sequence is the frame slice.
     //    With one trim offset for the whole unit the (start, end) order is unchanged.
+    //    Collapse only compares overlaps, lengths and motifs, all shift-invariant,
+    //    so one common offset is added when the records are materialised.
     bool one_offset = true;
     for (int32_t c : chroms) one_offset = one_offset && job.contigs[(size_t)c].trim_left == job.contigs[(size_t)chroms[0]].trim_left;
-    parallel_for((int64_t)recs.size(), nt, [&](int64_t a, int64_t b) {
-        for (int64_t k = a; k < b; ++k) {
-            Item &r = recs[(size_t)k];
-            const int64_t off = job.contigs[(size_t)r.chrom].trim_left;
-            r.start += off;
-            r.end += off;
-        }
-    });
+    const int64_t shift = one_offset && !chroms.empty() ? job.contigs[(size_t)chroms[0]].trim_left : 0;
+    if (!one_offset)
+        parallel_for((int64_t)recs.size(), nt, [&](int64_t a, int64_t b) {
+            for (int64_t k = a; k < b; ++k) {
+                Item &r = recs[(size_t)k];
+                const int64_t off = job.contigs[(size_t)r.chrom].trim_left;
+                r.start += off;
+                r.end += off;
+            }
+        });
     // 6. collapse (bwt.py:3499-3513)
     if (!one_offset) sort_by_pos(recs, nt);
     auto r3 = clk::now();
@@ -1012,7 +1023,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     parallel_items(T, T, [&](int64_t t, int) {
         int64_t o = cnt[(size_t)t];
         for (int64_t q = ncol * t / T; q < ncol * (t + 1) / T; ++q)
-            if (pass(col[(size_t)q])) out[(size_t)o++] = materialize(u, recs[col[(size_t)q]]);
+            if (pass(col[(size_t)q])) out[(size_t)o++] = materialize(u, recs[col[(size_t)q]], shift);
     });
     auto t4 = clk::now();
     if (std::getenv("BWTMI_STATS")) {
@@ -1068,14 +1079,14 @@ void postprocess(Job &job) {
         job.stage_ms[2 + s] = 0;
         for (int32_t k = 0; k < job.nunits; ++k) job.stage_ms[2 + s] += ms[(size_t)k * 4 + s];
     }
-    if (const char *e = std::getenv("BWTMI_STATS"); e && *e == '1')
+    if (g_counters)
         std::fprintf(stderr, "[bwtmi] recomputes=%lld (%.1f ms thread-summed) merges=%lld canons=%lld final=%zu\n",
                      (long long)g_recomputes.exchange(0), g_recompute_ns.exchange(0) / 1e6,
                      (long long)g_merges.exchange(0), (long long)g_canons.exchange(0), job.final_recs.size());
-    if (const char *e = std::getenv("BWTMI_STATS"); e && *e == '1')
+    if (g_counters)
         std::fprintf(stderr, "[bwtmi] merge tests past the gap test=%lld, same canonical=%lld\n",
                      (long long)g_tests.exchange(0), (long long)g_same.exchange(0));
-    if (const char *e = std::getenv("BWTMI_STATS"); e && *e == '1')
+    if (g_counters)
         for (int a = 0; a < 8; ++a)
             for (int b = 0; b < 8; ++b)
                 if (int64_t c = g_hist_n[a][b].exchange(0))
