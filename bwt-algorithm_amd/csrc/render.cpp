@@ -90,7 +90,13 @@ void kmer_scan(const Job &job, int32_t chrom, int64_t start, int64_t end, RecVec
 struct Row {
     const Rec *r;
     const Rec *partner;   // nullptr unless is_compound
+    int64_t start, end;   // r's, kept inline so ordering the rows reads no record
+    int32_t unit;
 };
+
+inline Row row_of(const Job &job, const Rec *r, const Rec *partner) {
+    return Row{r, partner, r->start, r->end, job.contigs[(size_t)r->chrom].unit};
+}
 
 struct Compound {
     std::deque<Rec> pool;                // k-mer pieces, pointer-stable
@@ -115,35 +121,60 @@ struct Walk {
 // pointers, so the final records are never copied
 void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt) {
     auto T0 = std::chrono::steady_clock::now();
+    // one pass over the records, in parallel chunks: chromosome of each and the
+    // _simple_kmer_scan pieces after every 3-mer record (kept in record order)
+    const size_t NR = recs.size();
+    const int CK = NR > 65536 ? 4 * std::max(1, nt) : 1;
+    struct Chunk {
+        int32_t first = -1;
+        bool mixed = false;
+        std::vector<std::pair<size_t, Rec>> pieces;   // (record index, piece)
+    };
+    std::vector<Chunk> ck((size_t)CK);
+    run_tasks(CK, nt, [&](int64_t t) {
+        Chunk &C = ck[(size_t)t];
+        RecVec kr;
+        for (size_t q = NR * (size_t)t / (size_t)CK; q < NR * (size_t)(t + 1) / (size_t)CK; ++q) {
+            const Rec &r = recs[q];
+            if (C.first < 0) C.first = r.chrom;
+            else if (r.chrom != C.first) C.mixed = true;
+            if (r.motif.size() != 3) continue;
+            const std::string &full = job.contigs[(size_t)r.chrom].full;
+            if (full.empty()) continue;
+            const int64_t a = r.end, b = std::min<int64_t>((int64_t)full.size(), r.end + 50);
+            if (a >= b) continue;
+            kr.clear();
+            kmer_scan(job, r.chrom, a, b, kr);
+            for (auto &x : kr)
+                if (x.motif != r.motif) C.pieces.emplace_back(q, std::move(x));
+        }
+    });
+    bool single = true;
+    for (auto &C : ck) single = single && !C.mixed && (C.first < 0 || C.first == ck[0].first);
     std::vector<int32_t> chrom_order;
     std::vector<std::vector<const Rec *>> by(job.contigs.size());
-    for (const Rec &r : recs) {
-        if (by[(size_t)r.chrom].empty()) chrom_order.push_back(r.chrom);
-        by[(size_t)r.chrom].push_back(&r);
+    if (single && NR > 0) {   // one chromosome: its list is every record, in order
+        chrom_order.push_back(recs[0].chrom);
+        auto &lst = by[(size_t)recs[0].chrom];
+        lst.resize(NR);
+        run_tasks(CK, nt, [&](int64_t t) {
+            for (size_t q = NR * (size_t)t / (size_t)CK; q < NR * (size_t)(t + 1) / (size_t)CK; ++q) lst[q] = &recs[q];
+        });
+    } else {
+        for (const Rec &r : recs) {
+            if (by[(size_t)r.chrom].empty()) chrom_order.push_back(r.chrom);
+            by[(size_t)r.chrom].push_back(&r);
+        }
     }
     auto T1 = std::chrono::steady_clock::now();
     std::vector<size_t> n_main(job.contigs.size(), 0);
     for (int32_t ch : chrom_order) n_main[(size_t)ch] = by[(size_t)ch].size();
-    for (int32_t ch : chrom_order) {
-        const std::string &full = job.contigs[(size_t)ch].full;
-        if (full.empty()) continue;
-        std::vector<const Rec *> &lst = by[(size_t)ch];
-        const size_t n0 = lst.size();
-        RecVec kr;
-        for (size_t q = 0; q < n0; ++q) {
-            const Rec *r = lst[q];
-            if (r->motif.size() != 3) continue;
-            const int64_t a = r->end, b = std::min<int64_t>((int64_t)full.size(), r->end + 50);
-            if (a >= b) continue;
-            kr.clear();
-            kmer_scan(job, ch, a, b, kr);
-            for (auto &x : kr)
-                if (x.motif != r->motif) {
-                    out.pool.push_back(std::move(x));
-                    lst.push_back(&out.pool.back());
-                }
+    // pieces go behind their chromosome's records, in record order (bwt.py:4011-4024)
+    for (auto &C : ck)
+        for (auto &pc : C.pieces) {
+            out.pool.push_back(std::move(pc.second));
+            by[(size_t)recs[pc.first].chrom].push_back(&out.pool.back());
         }
-    }
     auto T2 = std::chrono::steady_clock::now();
     double tsort = 0;
     for (int32_t ch : chrom_order) {
@@ -153,7 +184,15 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
         // k-mer pieces appended behind them need ordering and a stable merge
         auto by_start = [](const Rec *a, const Rec *b) { return a->start < b->start; };
         const size_t nmain = n_main[(size_t)ch];
-        if (std::is_sorted(rs.begin(), rs.begin() + (std::ptrdiff_t)nmain, by_start)) {
+        std::vector<uint8_t> chunk_sorted((size_t)CK, 1);
+        run_tasks(CK, nt, [&](int64_t t) {   // chunk t checks the pairs ending in it
+            const size_t a = std::max<size_t>(1, nmain * (size_t)t / (size_t)CK), b = nmain * (size_t)(t + 1) / (size_t)CK;
+            for (size_t k = a; k < b; ++k)
+                if (rs[k]->start < rs[k - 1]->start) { chunk_sorted[(size_t)t] = 0; return; }
+        });
+        bool main_sorted = true;
+        for (auto v : chunk_sorted) main_sorted = main_sorted && v;
+        if (main_sorted) {
             std::stable_sort(rs.begin() + (std::ptrdiff_t)nmain, rs.end(), by_start);
             std::inplace_merge(rs.begin(), rs.begin() + (std::ptrdiff_t)nmain, rs.end(), by_start);
         } else {
@@ -162,10 +201,18 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
         // spans of the > 10 bp motifs in start order, with the prefix max of
         // their ends: the "covered" test visits only those that can overlap
         struct Long { int64_t s, e, pe; };
+        std::vector<std::vector<Long>> lpart((size_t)CK);
+        const size_t NS = rs.size();
+        run_tasks(CK, nt, [&](int64_t t) {
+            for (size_t k = NS * (size_t)t / (size_t)CK; k < NS * (size_t)(t + 1) / (size_t)CK; ++k)
+                if (rs[k]->motif.size() > 10) lpart[(size_t)t].push_back({rs[k]->start, rs[k]->end, 0});
+        });
         std::vector<Long> longs;
-        for (auto *r : rs)
-            if (r->motif.size() > 10)
-                longs.push_back({r->start, r->end, longs.empty() ? r->end : std::max(longs.back().pe, r->end)});
+        for (auto &lp : lpart)
+            for (auto &l : lp) {
+                l.pe = longs.empty() ? l.e : std::max(longs.back().pe, l.e);
+                longs.push_back(l);
+            }
         tsort += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - S0).count();
         const Contig &ctg = job.contigs[(size_t)ch];
         const int64_t TL = ctg.trimmed_len();
@@ -213,7 +260,7 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
                         w.pool.push_back(kmer_piece(ch, e1, e1 + c2 * l2, std::string(rsq + sp, (size_t)l2), c2,
                                                       cur->tier, ACT_TRIMMED, a + y0, y1 - y0));
                         r1->is_compound = true;
-                        w.emit({r1, &w.pool.back()}, i0);
+                        w.emit(row_of(job, r1, &w.pool.back()), i0);
                         ++i;   // the reference advances i inside the split loop (bwt.py:4083)
                     }
                 }
@@ -238,12 +285,12 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
                         if ((double)ov / (double)(ce - cs) >= 0.8) covered = true;
                     }
                     if (!covered) {
-                        w.emit({cur, nx}, i0);
+                        w.emit(row_of(job, cur, nx), i0);
                         return i + 2;
                     }
                 }
             }
-            w.emit({cur, nullptr}, i0);
+            w.emit(row_of(job, cur, nullptr), i0);
             return i + 1;
         };
         const int K = N > 32768 ? 4 * std::max(1, nt) : 1;
@@ -441,17 +488,15 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out) {
         rows.swap(comp.rows);
     } else {
         rows.reserve(job.final_recs.size());
-        for (const Rec &r : job.final_recs) rows.push_back({&r, nullptr});
+        for (const Rec &r : job.final_recs) rows.push_back(row_of(job, &r, nullptr));
     }
     // sorted(all_repeats, key=lambda r: (natural_sort_key(r.chrom), r.start, r.end)) (bwt.py:4150)
     // The rows arrive ordered by (unit, start) in the usual case (one contig
     // per unit): then only runs of equal (unit, start) need a stable order by
     // end, which equals the full stable sort.
-    auto unit_start_lt = [&](const Row &a, const Row &b) {
-        const Rec &x = *a.r, &y = *b.r;
-        const int32_t ux = job.contigs[(size_t)x.chrom].unit, uy = job.contigs[(size_t)y.chrom].unit;
-        if (ux != uy) return ux < uy;
-        return x.start < y.start;
+    auto unit_start_lt = [](const Row &a, const Row &b) {
+        if (a.unit != b.unit) return a.unit < b.unit;
+        return a.start < b.start;
     };
     const int nt = host_threads(job.params);
     const size_t NR = rows.size();
@@ -475,7 +520,7 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out) {
                 for (size_t a = i + 1; a < j; ++a) {   // stable insertion sort by end (runs are short)
                     const Row x = rows[a];
                     size_t q = a;
-                    while (q > i && rows[q - 1].r->end > x.r->end) {
+                    while (q > i && rows[q - 1].end > x.end) {
                         rows[q] = rows[q - 1];
                         --q;
                     }
@@ -485,12 +530,10 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out) {
             }
         });
     } else {
-        std::stable_sort(rows.begin(), rows.end(), [&](const Row &a, const Row &b) {
-            const Rec &x = *a.r, &y = *b.r;
-            const int32_t ux = job.contigs[(size_t)x.chrom].unit, uy = job.contigs[(size_t)y.chrom].unit;
-            if (ux != uy) return ux < uy;
-            if (x.start != y.start) return x.start < y.start;
-            return x.end < y.end;
+        std::stable_sort(rows.begin(), rows.end(), [](const Row &a, const Row &b) {
+            if (a.unit != b.unit) return a.unit < b.unit;
+            if (a.start != b.start) return a.start < b.start;
+            return a.end < b.end;
         });
     }
     auto t1 = std::chrono::steady_clock::now();
@@ -520,7 +563,7 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out) {
     // caller renders only its own shard), else the local index
     const int64_t n = (int64_t)rows.size();
     const int64_t CH = 8192;
-    auto unit_of = [&](int64_t k) { return job.contigs[(size_t)rows[(size_t)k].r->chrom].unit; };
+    auto unit_of = [&](int64_t k) { return rows[(size_t)k].unit; };
     struct Chunk { int64_t a, b, id0; int32_t unit; };
     std::vector<Chunk> chunks;
     for (int64_t a = 0; a < n;) {
