@@ -10,6 +10,7 @@
 #include <fcntl.h>
 #include <unistd.h>
 
+#include <memory>
 #include <new>
 #include <string>
 #include <vector>
@@ -505,17 +506,11 @@ int bwtmi_job_reset(bwtmi_job *job) {
         job->j.hits.clear();
         job->j.screened.clear();
         job->j.raw_n.clear();
-        {   // the records' heap strings are released in parallel; the serial
-            // destruction that follows only meets short (inline) strings
-            RecVec old;
-            old.swap(job->j.final_recs);
-            const int64_t n = (int64_t)old.size(), CH = 16384;
-            run_tasks((n + CH - 1) / CH, host_threads(job->j.params), [&](int64_t k) {
-                for (int64_t i = k * CH; i < std::min(n, (k + 1) * CH); ++i) {
-                    std::string().swap(old[(size_t)i].motif);
-                    std::string().swap(old[(size_t)i].variations);
-                }
-            });
+        {   // the last records are released on the background reaper thread,
+            // behind the next step's device phase
+            auto old = std::make_shared<RecVec>();
+            old->swap(job->j.final_recs);
+            defer([old] { RecVec().swap(*old); });
         }
         job->j.t3.clear();
         job->j.postprocessed = false;

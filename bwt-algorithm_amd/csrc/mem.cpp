@@ -3,9 +3,12 @@
 
 #include <sys/mman.h>
 
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 
 namespace bwtmi {
@@ -95,5 +98,67 @@ void big_trim() {
     c.free_.clear();
     c.cached = 0;
 }
+
+namespace {
+class Reaper {
+public:
+    static Reaper &get() {
+        static Reaper r;
+        return r;
+    }
+    void push(std::function<void()> fn) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!th.joinable()) th = std::thread([this] { loop(); });
+            q.push_back(std::move(fn));
+            ++submitted;
+        }
+        cv.notify_all();
+    }
+    void drain() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t want = submitted;
+        done_cv.wait(lk, [&] { return finished >= want; });
+    }
+    ~Reaper() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        if (th.joinable()) th.join();   // runs what is still queued first
+    }
+
+private:
+    void loop() {
+        for (;;) {
+            std::function<void()> fn;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || !q.empty(); });
+                if (q.empty()) return;
+                fn = std::move(q.front());
+                q.pop_front();
+            }
+            fn();
+            fn = nullptr;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                ++finished;
+            }
+            done_cv.notify_all();
+        }
+    }
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    std::deque<std::function<void()>> q;
+    std::thread th;
+    uint64_t submitted = 0, finished = 0;
+    bool stop = false;
+};
+}  // namespace
+
+void defer(std::function<void()> fn) { Reaper::get().push(std::move(fn)); }
+void defer_drain() { Reaper::get().drain(); }
 
 }  // namespace bwtmi

@@ -11,6 +11,7 @@
 #pragma once
 
 #include <cstddef>
+#include <functional>
 #include <new>
 #include <utility>
 
@@ -22,6 +23,12 @@ void *big_alloc(size_t bytes);             // throws std::bad_alloc
 void big_free(void *p, size_t bytes) noexcept;
 size_t big_cached_bytes();                 // bytes held in the cache (tests / stats)
 void big_trim();                           // unmap every cached block
+
+// Runs fn on a background thread, in submission order: releasing a step's
+// large record sets overlaps the next step's device phase instead of
+// delaying it.  defer_drain() waits for everything submitted so far.
+void defer(std::function<void()> fn);
+void defer_drain();
 
 // Allocator for vectors of trivially-copyable (or default-constructible)
 // elements: small arrays from operator new, large ones from big_alloc.

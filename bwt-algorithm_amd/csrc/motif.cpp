@@ -2,6 +2,7 @@
 // Float arithmetic follows the Python expressions operation by operation; the
 // library is built with -ffp-contract=off so no FMA changes a rounding.
 #include <algorithm>
+#include <charconv>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -172,8 +173,8 @@ struct UnitOut {
 
 inline void put_num(std::string &s, int64_t v) {
     char b[24];
-    int n = snprintf(b, sizeof b, "%lld", (long long)v);
-    s.append(b, (size_t)n);
+    const auto r = std::to_chars(b, b + sizeof b, v);
+    s.append(b, (size_t)(r.ptr - b));
 }
 
 // ops of one copy are formatted with a placeholder-free prefix; the copy index

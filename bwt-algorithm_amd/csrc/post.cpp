@@ -835,8 +835,7 @@ Item item_of_rec(Pools &pools, const Rec &r) {
 }
 
 // final Rec of an item (after restore): strict fields per bwt.py:1972-1993
-Rec materialize(const UnitCtx &u, const Item &it, int64_t shift) {
-    Rec r;
+void materialize(const UnitCtx &u, const Item &it, int64_t shift, Rec &r) {   // r: a fresh Rec
     const Contig &c = u.job->contigs[(size_t)it.chrom];
     r.chrom = it.chrom;
     r.tier = it.tier;
@@ -877,7 +876,6 @@ Rec materialize(const UnitCtx &u, const Item &it, int64_t shift) {
         r.act_off = a;
         r.act_len = b - a;
     }
-    return r;
 }
 
 void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vector<HitVec> &raw,
@@ -1023,7 +1021,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     parallel_items(T, T, [&](int64_t t, int) {
         int64_t o = cnt[(size_t)t];
         for (int64_t q = ncol * t / T; q < ncol * (t + 1) / T; ++q)
-            if (pass(col[(size_t)q])) out[(size_t)o++] = materialize(u, recs[col[(size_t)q]], shift);
+            if (pass(col[(size_t)q])) materialize(u, recs[col[(size_t)q]], shift, out[(size_t)o++]);
     });
     auto t4 = clk::now();
     if (std::getenv("BWTMI_STATS")) {

@@ -9,7 +9,9 @@ from bwtmi.records import Job
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 100_000_000
 ctx = _lib.ctx(0)
-job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True, build_index=True, sa_sample=32)
+threads = int(os.environ.get("STEP_THREADS", "0"))   # 0 = the library default (<= 16)
+job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True, build_index=True, sa_sample=32,
+          threads=threads)
 job.add_contig("contig1", synth.generate_contig(n, 1, 0.0), 30, 30)
 job.select([0])
 job.upload(ctx)
