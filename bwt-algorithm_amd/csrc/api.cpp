@@ -505,6 +505,7 @@ int bwtmi_job_reset(bwtmi_job *job) {
         CHECK_ARG(job, "null argument");
         job->j.hits.clear();
         job->j.screened.clear();
+        job->j.shits.clear();
         job->j.raw_n.clear();
         {   // the last records are released on the background reaper thread,
             // behind the next step's device phase
@@ -548,6 +549,7 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
         Ctx &c = ctx->c;
         J.hits.assign(J.contigs.size(), {});
         J.screened.assign(J.contigs.size(), 0);
+        J.shits.assign(J.contigs.size(), {});
         J.raw_n.assign(J.contigs.size(), 0);
         // nested suppression + sort + dedup on the device (BWTMI_HOST_SCREEN=1: on the host)
         const char *hs = std::getenv("BWTMI_HOST_SCREEN");
@@ -569,8 +571,9 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
             const bool t3 = i < J.t3.size() && !J.t3[i].empty();
             ScanResult r;
             strict_scan_device(c, job->dev.seqs[i].buf.as<uint8_t>(), len, 1, (int32_t)std::min<int64_t>(U, INT32_MAX),
-                               P.min_copies, r, screen && !t3);
+                               P.min_copies, r, screen && !t3 && len < (int64_t)UINT32_MAX);   // 32-bit hit lengths
             J.hits[i].swap(r.hits);   // Rule 1 (bwt.py:3118-3130) never fires on strict hits
+            J.shits[i].swap(r.shits);
             J.screened[i] = r.screened ? 1 : 0;
             J.raw_n[i] = r.raw;
         }

@@ -27,6 +27,17 @@ template <class T>
 using NoInit = BigAlloc<T>;
 using HitVec = std::vector<bwtmi_hit, NoInit<bwtmi_hit>>;
 
+// a device-screened strict hit as downloaded (16 B instead of 32): the hit is
+// [start, start + len) with primitive motif length prim, and its copies are
+// len / prim (count after primitive reduction, bwt.py:1957-1961; (end-i)/L
+// otherwise, as end = i + count*L)
+struct ScreenedHit {
+    int64_t start;
+    uint32_t len;
+    uint32_t prim;
+};
+using ScreenedVec = std::vector<ScreenedHit, NoInit<ScreenedHit>>;
+
 // ---------------------------------------------------------------- contigs
 struct Contig {
     std::string name;
@@ -120,6 +131,7 @@ struct Job {
     std::vector<HitVec> hits;                        // per contig strict hits: raw (worker order), or
     std::vector<uint8_t> screened;                   // screened[c]: nested-suppressed, sorted by
                                                      // (start, end, m desc, worker order) and deduped
+    std::vector<ScreenedVec> shits;                  // per contig: those screened hits (hits[c] empty)
     std::vector<int64_t> raw_n;                      // raw strict hits per contig
     RecVec final_recs;                               // after bwt.py:3940-3944
     std::vector<RecVec> t3;                          // per contig: Tier 3 records (bwt.py:3918-3924), joined

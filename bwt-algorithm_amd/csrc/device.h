@@ -169,7 +169,8 @@ void radix_sort_pairs32(Ctx &c, uint64_t *keys, uint32_t *vals, int64_t n, int b
 
 // ----- strict scan (strict_scan.hip)
 struct ScanResult {
-    HitVec hits;                   // raw hits in worker order, or screened hits (see below)
+    HitVec hits;                   // raw hits in worker order (screen = false)
+    ScreenedVec shits;             // screened hits (screen = true)
     double kernel_ms = 0;
     int64_t candidates = 0;
     int64_t raw = 0;               // raw strict hits found
@@ -183,7 +184,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
 
 // ----- nested suppression / sort / dedup of one contig's strict hits (nested.hip)
 void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
-                        HitVec &out);
+                        ScreenedVec &out);
 
 // ----- index (index.hip)
 struct DeviceIndex;

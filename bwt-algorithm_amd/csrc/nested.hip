@@ -287,19 +287,21 @@ __global__ void k_final_flags(const int64_t *__restrict__ S, const int64_t *__re
 
 __global__ void k_final_compact(const bwtmi_hit *__restrict__ H, const uint32_t *__restrict__ vpos,
                                 const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos, int64_t n,
-                                bwtmi_hit *__restrict__ out) {
+                                ScreenedHit *__restrict__ out) {
     const int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x;
     if (k >= n || !flag[k]) return;
-    out[pos[k]] = H[vpos[k]];
+    const bwtmi_hit h = H[vpos[k]];
+    out[pos[k]] = ScreenedHit{h.start, (uint32_t)(h.end - h.start), (uint32_t)h.prim_len};
 }
 
 }  // namespace
 
 void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
-                        HitVec &out) {
+                        ScreenedVec &out) {
     out.clear();
     if (n <= 0) return;
     if (n >= (int64_t)UINT32_MAX) fail(BWTMI_E_ARG, "too many strict hits for one contig (%lld)", (long long)n);
+    if (text_len >= (int64_t)UINT32_MAX) fail(BWTMI_E_ARG, "contig too long for the screened-hit records (%lld)", (long long)text_len);
     hipStream_t st = c.stream;
     c.slot[S_CAND_K].ensure((size_t)n * 8);
     c.slot[S_CAND_V].ensure((size_t)n * 4);
@@ -325,7 +327,7 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     int32_t *M = c.slot[S_IDX1].as<int32_t>();
     uint32_t *rank_of = c.slot[S_IDX2].as<uint32_t>();
     uint8_t *kept = c.slot[S_IDX3].as<uint8_t>();
-    bwtmi_hit *dout = c.slot[S_IDX4].as<bwtmi_hit>();
+    ScreenedHit *dout = c.slot[S_IDX4].as<ScreenedHit>();
     uint32_t *flag = c.slot[S_FLAG].as<uint32_t>(), *pos = c.slot[S_SCAN].as<uint32_t>();
     unsigned long long *d_max = c.slot[S_COUNTS].as<unsigned long long>();
 
@@ -385,7 +387,7 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     HIPCHECK(hipMemcpyAsync(&nk, pos + n, 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     out.resize(nk);
-    if (nk) HIPCHECK(hipMemcpyAsync(out.data(), dout, (size_t)nk * sizeof(bwtmi_hit), hipMemcpyDeviceToHost, st));
+    if (nk) HIPCHECK(hipMemcpyAsync(out.data(), dout, (size_t)nk * sizeof(ScreenedHit), hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
 }
 

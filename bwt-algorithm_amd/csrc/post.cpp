@@ -879,7 +879,7 @@ void materialize(const UnitCtx &u, const Item &it, int64_t shift, Rec &r) {   //
 }
 
 void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vector<HitVec> &raw,
-                  RecVec &out, double *ms, int nt) {
+                  std::vector<ScreenedVec> &shits, RecVec &out, double *ms, int nt) {
     using clk = std::chrono::steady_clock;
     auto t0 = clk::now();
     UnitCtx u{&job, job.params.min_copies};
@@ -894,13 +894,27 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
         auto &h = raw[(size_t)c];
         const bool scr = (size_t)c < job.screened.size() && job.screened[(size_t)c];
         presorted = presorted && scr;
-        ItemVec items(h.size());
-        parallel_for((int64_t)h.size(), nt, [&](int64_t a, int64_t b) {
-            for (int64_t k = a; k < b; ++k) {
-                const bwtmi_hit &x = h[(size_t)k];
-                items[(size_t)k] = Item{x.start, x.end, x.copies, x.start, nullptr, c, x.prim_len, 2, 0};
-            }
-        });
+        ItemVec items;
+        if (scr && (size_t)c < shits.size()) {   // device-screened: compact records
+            auto &sh = shits[(size_t)c];
+            items.resize(sh.size());
+            parallel_for((int64_t)sh.size(), nt, [&](int64_t a, int64_t b) {
+                for (int64_t k = a; k < b; ++k) {
+                    const ScreenedHit &x = sh[(size_t)k];
+                    const int64_t len = x.len, prim = x.prim;
+                    items[(size_t)k] = Item{x.start, x.start + len, len / prim, x.start, nullptr, c, (int32_t)prim, 2, 0};
+                }
+            });
+            ScreenedVec().swap(sh);
+        } else {
+            items.resize(h.size());
+            parallel_for((int64_t)h.size(), nt, [&](int64_t a, int64_t b) {
+                for (int64_t k = a; k < b; ++k) {
+                    const bwtmi_hit &x = h[(size_t)k];
+                    items[(size_t)k] = Item{x.start, x.end, x.copies, x.start, nullptr, c, x.prim_len, 2, 0};
+                }
+            });
+        }
         HitVec().swap(h);
         // Tier 3 records of this chromosome come after all worker records (bwt.py:3918-3924)
         const bool mine = job.selected.empty() || ((size_t)c < job.selected.size() && job.selected[(size_t)c]);
@@ -1049,15 +1063,16 @@ void postprocess(Job &job) {
     const int T = host_threads(job.params);
     // many small units: one thread per unit; few large units: all threads inside each
     int64_t busy = 0;
-    for (auto &v : job.hits) busy += v.empty() ? 0 : 1;
+    for (size_t c = 0; c < job.hits.size(); ++c)
+        busy += (job.hits[c].empty() && (c >= job.shits.size() || job.shits[c].empty())) ? 0 : 1;
     if (busy >= T) {
         parallel_items(job.nunits, T, [&](int64_t k, int) {
-            process_unit(job, units[(size_t)k], job.hits, res[(size_t)k], &ms[(size_t)k * 4], 1);
+            process_unit(job, units[(size_t)k], job.hits, job.shits, res[(size_t)k], &ms[(size_t)k * 4], 1);
         });
     } else {
         for (int32_t k = 0; k < job.nunits; ++k) {
             auto a = std::chrono::steady_clock::now();
-            process_unit(job, units[(size_t)k], job.hits, res[(size_t)k], &ms[(size_t)k * 4], T);
+            process_unit(job, units[(size_t)k], job.hits, job.shits, res[(size_t)k], &ms[(size_t)k * 4], T);
             if (g_stats)
                 std::fprintf(stderr, "  unit %d: %.1f ms total\n", k,
                              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count());

@@ -416,6 +416,7 @@ void launch_runs(Ctx &c, const uint32_t *P, int64_t n, int32_t lmin, int32_t lma
 void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
                         int32_t min_copies, ScanResult &res, bool screen) {
     res.hits.clear();
+    res.shits.clear();
     res.candidates = 0;
     res.kernel_ms = 0;
     res.raw = 0;
@@ -461,7 +462,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
         HIPCHECK(hipGetLastError());
         res.raw = nh;
         if (screen) {
-            screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.hits);
+            screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.shits);
             c.kresolve();
             return;
         }
@@ -598,7 +599,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     HIPCHECK(hipGetLastError());
     res.raw = nh;
     if (screen) {
-        screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.hits);
+        screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.shits);
         if (c.timing) HIPCHECK(hipEventRecord(c.ev1, st));
     } else {
         if (c.timing) HIPCHECK(hipEventRecord(c.ev1, st));
