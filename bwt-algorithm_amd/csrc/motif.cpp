@@ -373,6 +373,33 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
     const int64_t tol = std::max<int64_t>(1, (int64_t)std::floor((double)m * frac));
     const int64_t max_indel = max_indel_arg < 0 ? std::max<int64_t>(1, std::min<int64_t>(10, m >= 4 ? m / 2 : 1))
                                                 : max_indel_arg;
+    if (m == 1 && max_indel >= 1) {
+        // One-base motif: a window that differs from the consensus base has
+        // the deletion end j = 0 among its best alignments (cost 1, tied with
+        // the substitution, first j wins), so _align_unit_to_window reports
+        // failure and the walk stops there.  The consensus never changes, so
+        // the result is the run of the template base from start (up to limit).
+        const int64_t limit = std::min<int64_t>(
+            seq_len, std::max<int64_t>(end, start + min_copies) + std::max<int64_t>(3, max_indel * 4));
+        const char b = tmpl[0];
+        int64_t pos = start;
+        while (pos < limit && seq[pos] == b) ++pos;
+        const int64_t copies = pos - start;
+        if (copies < min_copies || copies <= 0) return false;
+        out.copy_len.assign((size_t)copies, 1);
+        out.copy_err.assign((size_t)copies, 0);
+        out.variations.clear();
+        out.any_variation = false;
+        out.consensus.assign(1, b);
+        out.motif_len = 1;
+        out.copies = copies;
+        out.consumed = copies;
+        out.mismatch_rate = 0.0;
+        out.max_errors = 0;
+        out.tot_ins = 0;
+        out.tot_del = 0;
+        return true;
+    }
     thread_local Scratch S;
     pc_reset(S, m);
     out.copy_len.clear();
