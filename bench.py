@@ -101,14 +101,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     td = None
+    # BWTMI_BENCH_GLOO=1 (rehearsal aid on a box with fewer GPUs than ranks):
+    # collectives over gloo on host tensors, rank r on device r mod #devices
+    rehearsal = os.environ.get("BWTMI_BENCH_GLOO") == "1"
     if world > 1:
         import torch
         from bwtmi import dist
-        td = dist.init()                      # RCCL (nccl backend) over xGMI
+        td = dist.init("gloo" if rehearsal else None)   # RCCL (nccl backend) over xGMI
 
     from bwtmi import _lib, dist, synth
     from bwtmi.records import Job
 
+    if rehearsal:
+        local = local % max(1, _lib.device_count())
     ctx = _lib.ctx(local)
     # every rank registers every contig (fold-unit ids match across ranks) but
     # holds only its own sequence: rows are rendered and written by their owner
@@ -126,7 +131,7 @@ def main():
     job.upload(ctx)                           # host -> HBM once; outside the timed region
     upload_ms = (time.perf_counter() - t_up) * 1000.0
     out_path = os.path.join(tempfile.gettempdir(), f"bwtmi_bench_{os.environ.get('MASTER_PORT', 'single')}.tab")
-    dev = torch.device("cuda", local) if world > 1 else None
+    dev = torch.device("cuda", local) if world > 1 and not rehearsal else None
 
     calls = {}
 
@@ -144,7 +149,7 @@ def main():
         if world > 1:
             # each rank writes its own contig's rows at offsets from two
             # all-reduces of per-unit sizes (RCCL); no record leaves its GPU
-            timed("write", dist.write_sharded, td, job, "strfinder", out_path, dev)
+            timed("write", dist.write_sharded, td, job, "strfinder", out_path, dev if dev is not None else "cpu")
         else:
             timed("write", job.write, "strfinder", out_path)     # repeat.tab, as the CLI writes it
         timed("index_wait", job.wait, ctx)    # the FM index build ran behind the host work
@@ -169,7 +174,7 @@ def main():
     kstats = _lib.kernel_stats(ctx, enable=False, reset=True)
     stages = job.stage_ms()
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local))
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dev is not None else "cpu")
         td.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     if a.stages:
@@ -193,7 +198,7 @@ def main():
         name, (kms, launches, kbytes) = dom
         achieved = kbytes / (kms / 1e3) / 1e9 if kms > 0 else 0.0
         traffic = None
-        if a.pmc_summary and os.path.exists(a.pmc_summary):
+        if a.pmc_summary and os.path.exists(a.pmc_summary) and a.contig_bp == CONTIG_BP:   # measured at C3
             with open(a.pmc_summary) as f:
                 pk = json.load(f).get("kernels", {}).get(KERNEL_OF.get(name, name))
             if pk:
