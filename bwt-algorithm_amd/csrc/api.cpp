@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -11,6 +12,7 @@
 #include <unistd.h>
 
 #include <memory>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -677,13 +679,54 @@ int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len) {
     });
 }
 
+// The file is written while it is being formatted: a part whose predecessors
+// are all formatted has a known offset, and the thread that completes the
+// prefix writes the parts it extends it by.  The content is that of one
+// open(path, 'w') + write (the file is overwritten in place, then cut).
 int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path) {
     return guard([&] {
         CHECK_ARG(job && path, "null argument");
-        const std::vector<Text> parts = render_parts(job->j, fmt);
-        std::vector<size_t> at(parts.size() + 1, 0);
-        for (size_t k = 0; k < parts.size(); ++k) at[k + 1] = at[k] + parts[k].size();
-        pwrite_parts(path, true, parts, at, host_threads(job->j.params));
+        const int fd = ::open(path, O_WRONLY | O_CREAT, 0644);
+        if (fd < 0) fail(BWTMI_E_IO, "cannot open %s for writing", path);
+        Rendered R;
+        std::mutex mu;
+        std::vector<uint8_t> done;
+        size_t next = 0, off = 0;
+        std::atomic<bool> bad{false};
+        auto put = [&](const char *p, size_t n, size_t at) {
+            size_t w = 0;
+            while (w < n) {
+                const ssize_t k = ::pwrite(fd, p + w, n - w, (off_t)(at + w));
+                if (k <= 0) { bad = true; return; }
+                w += (size_t)k;
+            }
+        };
+        const std::function<void(size_t)> on_part = [&](size_t k) {
+            std::vector<std::pair<size_t, size_t>> mine;   // (part, offset)
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (done.empty()) {   // first call: the parts vector and the header exist
+                    done.assign(R.parts.size(), 0);
+                    put(R.header.data(), R.header.size(), 0);
+                    off = R.header.size();
+                }
+                done[k] = 1;
+                while (next < done.size() && done[next]) {
+                    mine.push_back({next, off});
+                    off += R.parts[next].size();
+                    ++next;
+                }
+            }
+            for (auto &m : mine) put(R.parts[m.first].data(), R.parts[m.first].size(), m.second);
+        };
+        render_rows(job->j, fmt, nullptr, R, &on_part);
+        if (done.empty()) {   // no rows: the header alone
+            put(R.header.data(), R.header.size(), 0);
+            off = R.header.size();
+        }
+        bool good = !bad && ::ftruncate(fd, (off_t)off) == 0;
+        good = (::close(fd) == 0) && good;
+        if (!good) fail(BWTMI_E_IO, "short write to %s", path);
     });
 }
 

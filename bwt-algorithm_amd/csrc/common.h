@@ -147,7 +147,9 @@ struct Job {
 void postprocess(Job &job);
 // render.cpp: the output as consecutive parts (formatted in parallel).
 // row_base (per fold unit, may be null): global VCF row id of the unit's first row.
-void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out);
+// on_part (may be null): called from the formatting thread as soon as part k is complete.
+void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
+                 const std::function<void(size_t)> *on_part = nullptr);
 std::vector<Text> render_parts(Job &job, int fmt);
 std::string render(Job &job, int fmt);
 // fasta.cpp

@@ -478,7 +478,8 @@ const char *kVcfHeader =
 
 // Rows are formatted in parallel, in chunks of consecutive rows; each chunk is
 // one part of the output, so concatenating the parts gives the file.
-void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out) {
+void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
+                 const std::function<void(size_t)> *on_part) {
     auto t0 = std::chrono::steady_clock::now();
     job.assign_units();
     Compound comp;
@@ -629,6 +630,7 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out) {
             }
         }
         out.parts[(size_t)ck] = std::move(o.s);
+        if (on_part) (*on_part)((size_t)ck);
     });
     auto t3 = std::chrono::steady_clock::now();
     job.stage_ms[6] = std::chrono::duration<double, std::milli>(t3 - t0).count();

@@ -16,8 +16,8 @@
 //   radix sort   candidates by (L desc, s asc) -- the reference order
 //   k_resolve    chains of candidates closer than L (where carry can act) are
 //                walked by their head lane; all others resolve independently
-//   scan+compact hits in candidate order
-//   k_period     smallest divisor period of the first unit per hit
+//   scan+compact hits in candidate order, each with the smallest divisor
+//                period of its first unit (k_period on the min_copies = 1 path)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -354,10 +354,24 @@ __global__ __launch_bounds__(256) void k_resolve(const uint64_t *__restrict__ ke
     }
 }
 
+// smallest_period_str of s[0 : L) (bwt.py:1125-1133): the first divisor d of L
+// with s[x] == s[x - d] for all x in [d, L)
+__device__ __forceinline__ int32_t smallest_period(const uint8_t *__restrict__ s, int32_t L) {
+    for (int32_t d = 1; d < L; ++d) {   // 32-bit: the divisor tests are 32-bit remainders
+        if (L % d) continue;
+        int32_t x = d;
+        while (x < L && s[x] == s[x - d]) ++x;
+        if (x == L) return d;
+    }
+    return L;
+}
+
+// compaction of the resolved hits, with the smallest period of each hit's
+// first unit and the count after primitive reduction (bwt.py:1956-1961)
 __global__ __launch_bounds__(256) void k_compact(const uint64_t *__restrict__ keys, int64_t nc, int32_t umax,
                                                  const int64_t *__restrict__ hit_i, const int64_t *__restrict__ hit_c,
                                                  const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
-                                                 bwtmi_hit *__restrict__ hits) {
+                                                 const uint8_t *__restrict__ t, bwtmi_hit *__restrict__ hits) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nc || !flag[k]) return;
     const int64_t L = (int64_t)umax - (int64_t)(keys[k] >> 40);
@@ -365,8 +379,9 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t *__restrict__ ke
     h.start = hit_i[k];
     h.end = hit_i[k] + hit_c[k] * L;
     h.unit_len = (int32_t)L;
-    h.prim_len = 0;
-    h.copies = hit_c[k];
+    const int32_t p = smallest_period(t + h.start, (int32_t)L);
+    h.prim_len = p;
+    h.copies = p < L ? (h.end - h.start) / p : hit_c[k];
     hits[pos[k]] = h;
 }
 
@@ -376,15 +391,8 @@ __global__ __launch_bounds__(256) void k_period(const uint8_t *__restrict__ t, b
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nh) return;
     bwtmi_hit h = hits[k];
-    const int32_t L = h.unit_len;   // 32-bit: the divisor tests are 32-bit remainders
-    const uint8_t *s = t + h.start;
-    int32_t p = L;
-    for (int32_t d = 1; d < L; ++d) {
-        if (L % d) continue;
-        int32_t x = d;
-        while (x < L && s[x] == s[x - d]) ++x;
-        if (x == L) { p = d; break; }
-    }
+    const int32_t L = h.unit_len;
+    const int32_t p = smallest_period(t + h.start, L);
     h.prim_len = (int32_t)p;
     if (p < L) h.copies = (h.end - h.start) / p;
     hits[k] = h;
@@ -592,10 +600,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     c.slot[S_HITS].ensure((size_t)std::max<int64_t>(nh, 1) * sizeof(bwtmi_hit));
     hipLaunchKernelGGL(k_compact, dim3(g), dim3(256), 0, st, c.slot[S_CAND_K].as<uint64_t>(), nc, lmax,
                        c.slot[S_MISC0].as<int64_t>(), c.slot[S_MISC1].as<int64_t>(), c.slot[S_FLAG].as<uint32_t>(),
-                       c.slot[S_SCAN].as<uint32_t>(), c.slot[S_HITS].as<bwtmi_hit>());
-    if (nh > 0)
-        hipLaunchKernelGGL(k_period, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st, d_text,
-                           c.slot[S_HITS].as<bwtmi_hit>(), nh);
+                       c.slot[S_SCAN].as<uint32_t>(), d_text, c.slot[S_HITS].as<bwtmi_hit>());
     HIPCHECK(hipGetLastError());
     res.raw = nh;
     if (screen) {
