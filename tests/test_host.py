@@ -266,3 +266,29 @@ def test_shard_assignment_is_lpt_and_keeps_natural_key_units():
     assert [sorted(u) for u in units] == [[0, 2, 4], [1], [3]]
     parts = dist.assign([[0], [1], [2], [3]], [10, 40, 30, 20], 2)
     assert parts == [[1, 0], [2, 3]] or parts == [[0, 1], [2, 3]]
+
+
+def test_job_write_streams_the_rendered_file(tmp_path, built_lib):
+    """bwtmi_job_write formats and writes in one pass (parts land as soon as
+    their offsets are known, the file is overwritten in place and cut): the
+    file equals the rendered output in every format, a longer stale file is
+    cut, and a job without rows writes the header alone."""
+    from bwtmi import synth
+    from bwtmi.records import Job
+    seq = synth.generate_contig(300_000, 3, 0.02)
+    hits = oracle.strict_scan(seq[30:-30], 1, 1000, 0, 3)
+    out = tmp_path / "repeat.tab"
+    for fmt in ("strfinder", "bed", "vcf", "trf_table", "trf_dat"):
+        j = Job(min_copies=3, show_progress=True, threads=4)
+        j.add_contig("c1", seq, 30, 30)
+        j.add_hits(0, hits)
+        j.postprocess()
+        want = j.render(fmt)
+        out.write_bytes(b"x" * (len(want) + 4321))
+        j.write(fmt, str(out))
+        assert out.read_bytes() == want, fmt
+    j = Job(min_copies=3)
+    j.add_contig("e", b"ACGT", 0, 0)
+    j.postprocess()
+    j.write("bed", str(out))
+    assert out.read_bytes() == j.render("bed")
