@@ -161,22 +161,27 @@ __global__ __launch_bounds__(256) void k_runs(const uint32_t *__restrict__ P, in
     for (int64_t g = g0; g < g1; ++g) {
 #pragma unroll
     for (int p = 0; p < B; ++p) nx[p] = g + 1 < g1 ? word(w + g + 2, p) : 0u;
-    bool done = false;
-    for (int r = 0; r < 32; ++r) {
-        const int64_t L = g * 32 + r;
-        if (L < lmin) continue;
-        if (L > lmax || tile_j0 >= n - L) {   // uniform across the block; L only grows
-            done = true;
-            break;
-        }
+    // this group's unit lengths, bounds hoisted out of the loop (the kernel is
+    // scalar-issue bound: every uniform test per L costs SALU slots): L >= lmin,
+    // L <= lmax, and the tile must hold positions below n - L
+    const int64_t Lg = g * 32;
+    const int r_lo = (int)max((int64_t)0, (int64_t)lmin - Lg);
+    const int r_hi = (int)min(min((int64_t)31, (int64_t)lmax - Lg), n - tile_j0 - 1 - Lg);
+    const bool done = r_hi < 31;   // later groups have no work
+    // positions j0 + k are valid for k < n - L - j0: only the text's last words need the mask
+    const bool tail = !inb || j0 + 32 + Lg + 31 >= n;
+    int64_t K = (mc - 1) * (Lg + r_lo);
+    for (int r = r_lo; r <= r_hi; ++r, K += mc - 1) {
+        const int64_t L = Lg + r;
         uint32_t x = 0;
 #pragma unroll
         for (int p = 0; p < B; ++p) x |= a[p] ^ __builtin_amdgcn_alignbit(hi[p], lo[p], (uint32_t)r);
         uint32_t M = ~x;
-        const int64_t lim = n - L - j0;
-        if (!inb || lim <= 0) M = 0u;
-        else if (lim < 32) M &= (1u << lim) - 1u;
-        const int64_t K = (mc - 1) * L;
+        if (tail) {
+            const int64_t lim = n - L - j0;
+            if (!inb || lim <= 0) M = 0u;
+            else if (lim < 32) M &= (1u << lim) - 1u;
+        }
         if (K > 62) {
             // a qualifying run is >= 64 long, so it contains a full aligned
             // word: only the first full word of a streak can own it
