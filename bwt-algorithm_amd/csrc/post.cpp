@@ -629,13 +629,15 @@ struct SpecOut {
 void spec_run(const UnitCtx &u, Pools &pools, int w, const ItemVec &R, int64_t b, int64_t e,
               std::vector<uint8_t, BigAlloc<uint8_t>> &fresh, SpecOut &o) {
     Item cur = R[(size_t)b];
-    Canon cc;
+    Canon cb[2];   // canonical forms of cur and of the next record; roles swap by index
+    int ci_cur = 0;
     fresh[(size_t)b] = 1;
     Item mg;
     o.emitted.reserve((size_t)(e - b));
     o.emit_step.reserve((size_t)(e - b));
     for (int64_t i = b + 1; i < e; ++i) {
-        Canon ci;
+        Canon &cc = cb[ci_cur], &ci = cb[ci_cur ^ 1];
+        ci.ok = false;
         if (try_merge(u, pools, w, cur, cc, R[(size_t)i], ci, mg)) {
             cur = mg;
             cc.ok = false;
@@ -644,12 +646,12 @@ void spec_run(const UnitCtx &u, Pools &pools, int w, const ItemVec &R, int64_t b
             o.emitted.push_back(cur);
             o.emit_step.push_back(i);
             cur = R[(size_t)i];
-            std::swap(cc, ci);
+            ci_cur ^= 1;
             fresh[(size_t)i] = 1;
         }
     }
     o.pending = cur;
-    o.pending_canon = std::move(cc);
+    o.pending_canon = std::move(cb[ci_cur]);
 }
 
 ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
@@ -685,21 +687,24 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
     std::vector<uint8_t> synced((size_t)K, 0);
     synced[0] = 1;
     Item cur = spec[0].pending;
-    Canon cc = std::move(spec[0].pending_canon);
+    Canon cb[2];
+    int ci_cur = 0;
+    cb[0] = std::move(spec[0].pending_canon);
     Item mg;
     for (int64_t k = 1; k < K; ++k) {
         const int64_t b = cut[(size_t)k], e = cut[(size_t)k + 1];
         SpecOut &sp = spec[(size_t)k];
         int64_t sync = -1;
         for (int64_t i = b; i < e; ++i) {
-            Canon ci;
+            Canon &cc = cb[ci_cur], &ci = cb[ci_cur ^ 1];
+            ci.ok = false;
             if (try_merge(u, pools, 0, cur, cc, R[(size_t)i], ci, mg)) {
                 cur = mg;
                 cc.ok = false;
             } else {
                 rep[(size_t)k].push_back(cur);
                 cur = R[(size_t)i];
-                std::swap(cc, ci);
+                ci_cur ^= 1;
                 if (fresh[(size_t)i]) { sync = i; break; }
             }
         }
@@ -709,7 +714,7 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
         from[(size_t)k] = q;
         synced[(size_t)k] = 1;
         cur = sp.pending;
-        cc = std::move(sp.pending_canon);
+        cb[ci_cur] = std::move(sp.pending_canon);
     }
     auto ts2 = std::chrono::steady_clock::now();
     std::vector<size_t> at((size_t)K + 1, 0);
