@@ -85,8 +85,8 @@ def fm_all_motifs(seq: bytes, reps: int = 5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--contig-bp", type=int, default=CONTIG_BP)
     ap.add_argument("--cpu-sample-bp", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
