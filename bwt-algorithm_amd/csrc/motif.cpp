@@ -212,17 +212,28 @@ bool align_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_
         char *prow = ptr + i * W + band - i;
         if (pjmax + 1 <= n) prev[pjmax + 1] = INF;            // (i-1, i-1+band+1) is out of band
         cur[jmin - 1] = jmin - 1 == 0 ? (int32_t)i : INF;
-        int32_t rowmin = INF;
+        // two passes over the band: the diagonal/deletion choice has no
+        // dependence along the row (vectorisable); the insertion choice
+        // (cur[j-1] + 1 strictly better) is the only serial chain.  Same tie
+        // order as one pass: sub/match, then deletion, then insertion.
+        const int32_t *pv = prev, *pw = prev;   // prev[j - 1], prev[j]
+        int32_t *cw = cur;
+        const char *wj = win - 1;               // win[j - 1]
         for (int64_t j = jmin; j <= jmax; ++j) {
-            const bool eq = mi == win[j - 1];
-            int32_t best = prev[j - 1] + (eq ? 0 : 1);
-            char op = eq ? 'M' : 'S';
-            const int32_t dc = prev[j] + 1;
-            if (dc < best) { best = dc; op = 'D'; }
-            const int32_t ic = cur[j - 1] + 1;
-            if (ic < best) { best = ic; op = 'I'; }
-            cur[j] = best;
-            prow[j] = op;
+            const int32_t sub = pv[j - 1] + (mi == wj[j] ? 0 : 1);
+            const int32_t dc = pw[j] + 1;
+            cw[j] = dc < sub ? dc : sub;
+            prow[j] = dc < sub ? 'D' : (mi == wj[j] ? 'M' : 'S');
+        }
+        int32_t rowmin = INF, left = cur[jmin - 1];
+        for (int64_t j = jmin; j <= jmax; ++j) {
+            int32_t best = cur[j];
+            if (left + 1 < best) {
+                best = left + 1;
+                prow[j] = 'I';
+                cur[j] = best;
+            }
+            left = best;
             rowmin = std::min(rowmin, best);
         }
         if (rowmin > reject && (jmin > 1 || i > reject)) return false;
