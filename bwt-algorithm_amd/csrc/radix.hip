@@ -2,15 +2,15 @@
 // stable LSD radix sort (8-bit digits) over 64-bit keys with 32/64-bit values.
 //
 // Radix pass = three launches:
-//   hist    : one workgroup per 4096-key tile, LDS histogram -> counts[d][tile]
+//   hist    : one workgroup per 8192-key tile, LDS histogram -> counts[d][tile]
 //   scan    : exclusive scan of counts (digit-major) -> global offsets
-//   scatter : each of the 4 waves owns 1024 consecutive keys of the tile; it
+//   scatter : each of the 8 waves owns 1024 consecutive keys of the tile; it
 //             ranks keys of equal digit with 8 ballots (wave64 match-any) in
 //             index order, so the pass is stable; the tile is reordered by
 //             digit in LDS and streamed out in that order, so each digit's
 //             run of the tile is one contiguous, coalesced write.  Keys and
-//             then values take turns in one 32 KB LDS buffer (4 workgroups
-//             per CU instead of 3).
+//             then values take turns in one 64 KB LDS buffer (2 workgroups
+//             of 8 waves per CU).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -128,20 +128,21 @@ __device__ __forceinline__ void st(T *p, T v) {
 //   SPLIT : keys and values take turns in one LDS staging buffer (the slot ->
 //           global position map stays in registers), so a tile needs 8 B of
 //           LDS per key instead of 8 + sizeof(V) and more workgroups fit a CU
-template <class V, int ITEMS, bool NT, bool SPLIT>
-__global__ __launch_bounds__(kBlock) void k_scatter(const uint64_t *__restrict__ kin, const V *__restrict__ vin,
-                                                    uint64_t *__restrict__ kout, V *__restrict__ vout,
-                                                    const uint32_t *__restrict__ offs, int64_t n, int shift,
-                                                    int64_t ntiles) {
-    constexpr int kT = kBlock * ITEMS;
-    __shared__ uint32_t wcnt[kWaves][256];   // per-wave digit counts, then per-wave digit bases
-    __shared__ uint32_t gdelta[256];         // global position of tile slot j = gdelta[digit] + j
-    __shared__ uint32_t dsum[kWaves];
+template <class V, int BLOCK, int ITEMS, bool NT, bool SPLIT>
+__global__ __launch_bounds__(BLOCK) void k_scatter(const uint64_t *__restrict__ kin, const V *__restrict__ vin,
+                                                   uint64_t *__restrict__ kout, V *__restrict__ vout,
+                                                   const uint32_t *__restrict__ offs, int64_t n, int shift,
+                                                   int64_t ntiles) {
+    constexpr int kT = BLOCK * ITEMS;
+    constexpr int NW = BLOCK / 64;
+    __shared__ uint32_t wcnt[NW][256];   // per-wave digit counts, then per-wave digit bases
+    __shared__ uint32_t gdelta[256];     // global position of tile slot j = gdelta[digit] + j
+    __shared__ uint32_t dsum[4];
     __shared__ uint64_t ks[kT];
     __shared__ V vs_own[SPLIT ? 1 : kT];
     V *vs = SPLIT ? reinterpret_cast<V *>(ks) : vs_own;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int w = 0; w < kWaves; ++w) wcnt[w][threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < NW * 256; i += BLOCK) (&wcnt[0][0])[i] = 0;
     __syncthreads();
     const int64_t tbase = (int64_t)blockIdx.x * kT;
     const int64_t wbase = tbase + (int64_t)wv * (ITEMS * 64);
@@ -175,24 +176,27 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const uint64_t *__restrict__
         __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
-    // thread t owns digit t: tile count, exclusive scan over digits, per-wave bases
+    // threads 0..255 own one digit each: tile count, exclusive scan over
+    // digits (waves 0-3), per-wave bases
     const int dg = threadIdx.x;
-    uint32_t cnt[kWaves], tot = 0;
+    uint32_t cnt[NW], tot = 0, inc = 0;
+    if (dg < 256) {
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-        cnt[w] = wcnt[w][dg];
-        tot += cnt[w];
+        for (int w = 0; w < NW; ++w) {
+            cnt[w] = wcnt[w][dg];
+            tot += cnt[w];
+        }
+        inc = wave_incl_scan<uint32_t>(tot);
+        if (lane == 63) dsum[wv] = inc;
     }
-    const uint32_t inc = wave_incl_scan<uint32_t>(tot);
-    if (lane == 63) dsum[wv] = inc;
     __syncthreads();
-    uint32_t toff = inc - tot;
-    for (int w = 0; w < wv; ++w) toff += dsum[w];
-    gdelta[dg] = offs[(int64_t)dg * ntiles + blockIdx.x] - toff;
-    {
+    if (dg < 256) {
+        uint32_t toff = inc - tot;
+        for (int w = 0; w < wv; ++w) toff += dsum[w];
+        gdelta[dg] = offs[(int64_t)dg * ntiles + blockIdx.x] - toff;
         uint32_t b = toff;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) {
+        for (int w = 0; w < NW; ++w) {
             wcnt[w][dg] = b;
             b += cnt[w];
         }
@@ -213,10 +217,10 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const uint64_t *__restrict__
     __syncthreads();
     const int64_t rem = n - tbase;
     const int cntt = rem < kT ? (int)rem : kT;
-    uint32_t pos[ITEMS];   // global position of tile slot i * 256 + t
+    uint32_t pos[ITEMS];   // global position of tile slot i * BLOCK + t
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-        const int j = i * kBlock + threadIdx.x;
+        const int j = i * BLOCK + threadIdx.x;
         pos[i] = 0;
         if (j < cntt) {
             const uint64_t key = ks[j];
@@ -233,15 +237,16 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const uint64_t *__restrict__
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
-            const int j = i * kBlock + threadIdx.x;
+            const int j = i * BLOCK + threadIdx.x;
             if (j < cntt) st<NT>(vout + pos[i], vs[j]);
         }
     }
 }
 
-template <class V, int ITEMS, bool NT, bool SPLIT>
+template <class V, int BLOCK, int ITEMS, bool NT, bool SPLIT>
 void radix_sort_cfg(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int bit1) {
-    constexpr int kT = kBlock * ITEMS;
+    constexpr int kT = BLOCK * ITEMS;
+    static_assert(kT % kBlock == 0, "histogram tiles are 256-thread tiles");
     const int64_t ntiles = (n + kT - 1) / kT;
     c.slot[S_SORT_TMP0].ensure((size_t)n * sizeof(uint64_t));
     if (vals) c.slot[S_SORT_TMP1].ensure((size_t)n * sizeof(V));
@@ -252,13 +257,13 @@ void radix_sort_cfg(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int bi
     int passes = 0;
     for (int sh = bit0; sh < bit1; sh += 8) {
         c.kbegin("radix_hist", (double)n * 8.0);                       // read keys once
-        hipLaunchKernelGGL(k_hist<ITEMS>, dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream, ka, cnt, n, sh, ntiles);
+        hipLaunchKernelGGL(k_hist<kT / kBlock>, dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream, ka, cnt, n, sh, ntiles);
         c.kend();
         exclusive_scan<uint32_t>(c, cnt, cnt, ntiles * 256);
         // read (key, value) once, write it once
         c.kbegin(sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16",
                  (double)n * 2.0 * (8.0 + (vals ? (double)sizeof(V) : 0.0)));
-        hipLaunchKernelGGL((k_scatter<V, ITEMS, NT, SPLIT>), dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream, ka, va,
+        hipLaunchKernelGGL((k_scatter<V, BLOCK, ITEMS, NT, SPLIT>), dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, ka, va,
                            kb, vb, cnt, n, sh, ntiles);
         c.kend();
         std::swap(ka, kb);
@@ -272,14 +277,18 @@ void radix_sort_cfg(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int bi
     }
 }
 
-// Pass geometry measured on the bench workload (r01r/r01s, radix_scatter_kv12
-// = fraction of the 8 TB/s peak): 16 items + shared staging 0.50-0.51 (20
-// items 0.52, 12 items 0.50, 8 items 0.47); separate key and value staging
-// 0.44-0.45; nontemporal stores 0.34-0.41 in every geometry.
+// Pass geometry measured on the bench workload (radix_scatter_kv12 = fraction
+// of the 8 TB/s peak).  r01r/r01s, 256-thread workgroups: 16 items + shared
+// staging 0.50-0.51 (20 items 0.52, 12 items 0.50, 8 items 0.47); separate key
+// and value staging 0.44-0.45; nontemporal stores 0.34-0.41 in every geometry.
+// r01ak, same box session for every variant: 512x16 0.50, 256x16 0.47, 512x8
+// 0.47, 1024x4 0.47, 256x20 0.48, 1024x8 0.44, 256x32 0.43.
 template <class V>
 void radix_sort_impl(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int bit1) {
     if (n <= 1) return;
-    radix_sort_cfg<V, 16, false, true>(c, keys, vals, n, bit0, bit1);
+    // 512 threads x 16 keys: 8192-key tiles, 8 waves per workgroup, 64 KB LDS
+    // (2 workgroups per CU)
+    radix_sort_cfg<V, 512, 16, false, true>(c, keys, vals, n, bit0, bit1);
 }
 
 }  // namespace

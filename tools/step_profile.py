@@ -16,6 +16,8 @@ job.add_contig("contig1", synth.generate_contig(n, 1, 0.0), 30, 30)
 job.select([0])
 job.upload(ctx)
 out = os.path.join(os.environ.get("TMPDIR", "/tmp"), "step_profile.tab")
+if os.environ.get("STEP_KSTATS") == "1":   # live per-kernel HIP-event timing, as bench.py runs it
+    _lib.kernel_stats(ctx, enable=True, reset=True)
 for s in range(steps):
     row = []
     for name, fn in (("reset", job.reset), ("scan", lambda: job.scan(ctx)), ("post", job.postprocess),
