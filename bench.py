@@ -1,27 +1,37 @@
 #!/usr/bin/env python3
 """Benchmark of the hot path: Mbp/s indexed+scanned (Tier 1+2) on 100 Mbp
-synthetic contigs, 1/2/4/8 GPUs (BASELINE.json `metric`).
+synthetic FASTA, 1/2/4/8 GPUs (BASELINE.json `metric`).
 
-Workload (with --progress so the reference's >50 Mbp Tier-2
-gate does not turn the run into a header-only no-op): one 100,000,000 bp
-synthetic contig per rank (seeded generator bwtmi/synth.py, contig k+1 on
-rank k), default parameters (min_copies 3, max_unit_len 120 -> U = 1000).
-Contigs are the sharding unit (one per GPU, weak scaling).
+One step = the reference's CLI path from FASTA read to output file closed
+(SURVEY.md §8(d)), per rank:
+  native parallel FASTA parse of the rank's contigs      [bwt.py:3713-3756]
+  H2D upload of the analysed sequences (pinned)
+  device FM index (SA, BWT, C, Occ, sampled SA, 8-mer hash; runs behind
+    the host stages)                                      [bwt.py:3053-3054]
+  device strict adjacency scan + nested screening         [bwt.py:3103-3106]
+  native post-processing to the final records             [bwt.py:3928-3944]
+  compound detection + STRfinder rows written to repeat.tab
+                                                          [bwt.py:4141-4198]
+The synthetic FASTA is written to local disk once, before timing.
 
-One step = one pass of the whole path over the resident contig(s):
-  device FM index (SA, BWT, C, Occ, sampled SA, 8-mer hash)  [bwt.py:3053-3054]
-  device strict adjacency scan + hit download                [bwt.py:3103-3106]
-  native post-processing to the final records                [bwt.py:3928-3944]
-  compound detection + STRfinder rows of the rank's own contig,
-  written into one repeat.tab at offsets from an RCCL
-  all-reduce of per-contig sizes (N > 1)                   [bwt.py:4141-4198]
-  (sha256 and row count of the file are reported)
-Inputs are resident in HBM before timing starts (uploaded during warmup).
+Workloads (`--workload`, default C3 on 1 GPU, C4 on N):
+  C3  one 100,000,000 bp contig, defaults + --progress (the reference's
+      >50 Mbp Tier-2 gate would otherwise make the output header-only);
+      N > 1: one such FASTA per rank (weak scaling)
+  C4  8 x 12,500,000 bp contigs in ONE FASTA; contigs sharded over the N
+      ranks (longest-processing-time), each rank reads its contigs from the
+      shared file and writes its rows into one shared repeat.tab at offsets
+      from RCCL all-reduces of per-contig sizes (strong scaling)
+  C5  C3 with 0.02 substitutions inside the planted arrays (the imperfect
+      input; --no-mismatches is a no-op in the reference, bwt.py:3105)
+The output sha256 is checked against the reference-pipeline golden
+(tests/golden/expected_large.json) when the workload has one.
 """
 import argparse
 import hashlib
 import json
 import os
+import platform
 import sys
 import tempfile
 import time
@@ -32,41 +42,71 @@ for _p in (REPO, os.path.join(REPO, "bwt-algorithm_amd")):
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# VALU issue ceiling: 256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz (MI355X_MICROARCH.md)
+VALU_LANE_OPS_PEAK = 256 * 4 * 32 * 2.4e9
+B_ALG_PER_BASE = 16.7          # compulsory HBM bytes per base, CLI path
 PMC_SUMMARY = os.path.join(REPO, "profiles", "pmc_traffic.json")
 # bench kernel-timer names -> kernel names in the rocprofv3 summaries
 KERNEL_OF = {"radix_scatter_kv12": "k_scatter<u32>", "radix_scatter_kv16": "k_scatter<u64>",
-             "radix_hist": "k_hist", "k_runs": "k_runs", "screen_levels": "k_level",
-             "bwt_gather": "k_bwt", "occ_blocks": "k_occ_blocks", "sa_init_keys": "k_init_keys"}
-CONTIG_BP = 100_000_000
+             "radix_hist": "k_hist", "bwt_gather": "k_bwt", "occ_blocks": "k_occ_blocks",
+             "sa_init_keys": "k_init_keys"}
 FLANK = 30
+METRIC = "Mbp/s indexed+scanned (Tier1+2) on 100 Mbp synthetic FASTA, 1/2/4/8 GPU"
+WORKLOADS = {
+    "C3": dict(lengths=[100_000_000], sub_rate=0.0, shared=False, golden="C3p"),
+    "C4": dict(lengths=[12_500_000] * 8, sub_rate=0.0, shared=True, golden="C4"),
+    "C5": dict(lengths=[100_000_000], sub_rate=0.02, shared=False, golden="C5p"),
+}
 
 
-def cpu_baseline(sample_bp: int):
-    """Oracle port (C index + C strict scan + Python post-processing, 1 thread)
-    on the first `sample_bp` bases of the rank-0 contig."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(sample_bp: int, sub_rate: float, threads: int):
+    """Native CPU comparator on a bounded sample: the C oracle's index build
+    (1 thread) and OpenMP strict scan, then the product's multithreaded host
+    post-processing + writer fed through bwtmi_job_add_hits."""
     import oracle
-    from oracle import post
     from bwtmi import synth
-    seq = synth.generate_contig(sample_bp, 1, 0.0)
+    from bwtmi.records import Job
+    seq = synth.generate_contig(sample_bp, 1, sub_rate)
+    out = os.path.join(tempfile.gettempdir(), f"bwtmi_cpu_{os.getpid()}.tab")
     t0 = time.perf_counter()
     trimmed = seq[FLANK:len(seq) - FLANK]
     oracle.Index(trimmed + b"$")
+    t1 = time.perf_counter()
     U = max(120, min(len(trimmed) // 3, 1000))
-    hits = oracle.strict_scan(trimmed, 1, U, 0, 3, threads=1)
-    s = trimmed.decode()
-    p = post.Pipeline({"contig1": s}, {"contig1": seq.decode()}, {"contig1": FLANK}, 3)
-    recs = p.run(post.worker_records("contig1", s, hits))
-    post.render(p, recs, "strfinder")
-    dt = time.perf_counter() - t0
-    return dict(value=round(sample_bp / 1e6 / dt, 5), unit="Mbp/s", cores=1, kind="port",
-                sample=f"first {sample_bp:,} bp of contig1 (C3 workload): oracle index + strict scan "
-                       f"+ post-processing + STRfinder render, 1 thread, {dt:.1f} s")
+    hits = oracle.strict_scan(trimmed, 1, U, 0, 3, threads=threads)
+    t2 = time.perf_counter()
+    job = Job(min_copies=3, show_progress=True, threads=threads)
+    job.add_contig("contig1", seq, FLANK, FLANK)
+    job.add_hits(0, hits)
+    job.postprocess()
+    job.write("strfinder", out)
+    t3 = time.perf_counter()
+    os.unlink(out)
+    dt = t3 - t0
+    return dict(value=round(sample_bp / 1e6 / dt, 5), unit="Mbp/s", cores=threads, kind="port",
+                sample=f"first {sample_bp:,} bp of contig1 (same generator): C oracle index (1 thread) + "
+                       f"OpenMP strict scan + native post-processing and STRfinder write ({threads} threads), "
+                       f"{dt:.1f} s",
+                phases_s=dict(index=round(t1 - t0, 2), strict_scan=round(t2 - t1, 2),
+                              post_and_write=round(t3 - t2, 2)),
+                extrapolated_100mbp_s=round(dt * 100e6 / sample_bp, 1))
 
 
 def fm_all_motifs(seq: bytes, reps: int = 5):
     """FM backward search over every canonical primitive ACGT motif of length
     1..10 (bwt.py:1369-1381 + 359-389; 145,338 patterns) on a device index of
-    the rank's contig; outside the timed steps."""
+    the rank's first contig; outside the timed steps."""
     from bwtmi import BWTCore, MotifUtils
     core = BWTCore((seq[FLANK:len(seq) - FLANK] + b"$").decode("latin-1"))
     pats = [m for k in range(1, 11) for m in MotifUtils.enumerate_motifs(k)]
@@ -82,13 +122,19 @@ def fm_all_motifs(seq: bytes, reps: int = 5):
                 mpatterns_per_s=round(len(pats) / dt / 1e6, 2))
 
 
+def word_compares(n: int, U: int) -> int:
+    """k_runs' 32-position word compares of one contig: sum_L ceil((n - L) / 32)."""
+    return sum((n - L + 31) // 32 for L in range(1, min(U, n // 3) + 1))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--contig-bp", type=int, default=CONTIG_BP)
-    ap.add_argument("--cpu-sample-bp", type=int, default=1_000_000)
+    ap.add_argument("--workload", choices=["auto"] + sorted(WORKLOADS), default="auto")
+    ap.add_argument("--contig-bp", type=int, default=0, help="override every contig length (tests)")
+    ap.add_argument("--cpu-sample-bp", type=int, default=5_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-index", action="store_true", help="skip the FM index (scan-only step)")
     ap.add_argument("--no-fm", action="store_true", help="skip the all-motif FM search report")
@@ -100,39 +146,42 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    td = None
-    # BWTMI_BENCH_GLOO=1 (rehearsal aid on a box with fewer GPUs than ranks):
-    # collectives over gloo on host tensors, rank r on device r mod #devices
-    rehearsal = os.environ.get("BWTMI_BENCH_GLOO") == "1"
-    if world > 1:
-        import torch
-        from bwtmi import dist
-        td = dist.init("gloo" if rehearsal else None)   # RCCL (nccl backend) over xGMI
+    wl_name = a.workload if a.workload != "auto" else ("C3" if world == 1 else "C4")
+    wl = dict(WORKLOADS[wl_name])
+    if a.contig_bp:
+        wl["lengths"] = [a.contig_bp] * len(wl["lengths"])
+    shared = wl["shared"]
 
-    from bwtmi import _lib, dist, synth
+    from bwtmi import _lib, comm as _comm, dist, synth
     from bwtmi.records import Job
 
+    # BWTMI_BENCH_GLOO=1 (rehearsal with more ranks than GPUs): collectives over
+    # the host transport, rank r on device r mod #devices
+    rehearsal = os.environ.get("BWTMI_BENCH_GLOO") == "1"
+    c = _comm.get("host" if rehearsal else None) if world > 1 else None
     if rehearsal:
         local = local % max(1, _lib.device_count())
     ctx = _lib.ctx(local)
-    # every rank registers every contig (fold-unit ids match across ranks) but
-    # holds only its own sequence: rows are rendered and written by their owner
+    host = _lib.host_info()
+
+    # input FASTA on local disk, written once before timing
+    tmp = tempfile.gettempdir()
+    tag = os.environ.get("MASTER_PORT", "single")
+    if shared:
+        fa = os.path.join(tmp, f"bwtmi_bench_{wl_name}_{tag}.fa")
+        if rank == 0:
+            synth.write_fasta(fa, wl["lengths"], wl["sub_rate"])
+        out = os.path.join(tmp, f"bwtmi_bench_{wl_name}_{tag}.tab")
+    else:   # one contig (index rank + 1) per rank, own FASTA, own output
+        fa = os.path.join(tmp, f"bwtmi_bench_{wl_name}_{tag}_r{rank}.fa")
+        synth.write_fasta(fa, wl["lengths"], wl["sub_rate"], first_index=rank + 1)
+        out = os.path.join(tmp, f"bwtmi_bench_{wl_name}_{tag}_r{rank}.tab")
+    if c is not None:
+        c.barrier()
+    load_world, load_rank = (world, rank) if shared else (1, 0)
+
     job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True,
               build_index=not a.no_index, sa_sample=32)
-    own_seq = b""
-    for k in range(world):
-        seq = synth.generate_contig(a.contig_bp, k + 1, 0.0) if k == rank else b""
-        trim = FLANK if len(seq) > 2 * FLANK else 0
-        job.add_contig(f"contig{k + 1}", seq, trim, trim)
-        if k == rank:
-            own_seq = seq
-    job.select([rank])
-    t_up = time.perf_counter()
-    job.upload(ctx)                           # host -> HBM once; outside the timed region
-    upload_ms = (time.perf_counter() - t_up) * 1000.0
-    out_path = os.path.join(tempfile.gettempdir(), f"bwtmi_bench_{os.environ.get('MASTER_PORT', 'single')}.tab")
-    dev = torch.device("cuda", local) if world > 1 and not rehearsal else None
-
     calls = {}
 
     def timed(name, fn, *args):
@@ -143,23 +192,22 @@ def main():
 
     def step():
         timed("reset", job.reset)
-        job.select([rank])
+        timed("load_fasta", job.load_fasta, fa, FLANK, load_world, load_rank)
+        timed("upload", job.upload, ctx)
         timed("scan", job.scan, ctx)
         timed("postprocess", job.postprocess)
-        if world > 1:
-            # each rank writes its own contig's rows at offsets from two
-            # all-reduces of per-unit sizes (RCCL); no record leaves its GPU
-            timed("write", dist.write_sharded, td, job, "strfinder", out_path, dev if dev is not None else "cpu")
+        if shared and world > 1:
+            # each rank writes its own contigs' rows at offsets from two
+            # all-reduces of per-unit sizes; no record leaves its GPU
+            timed("write", dist.write_sharded, c, job, "strfinder", out)
         else:
-            timed("write", job.write, "strfinder", out_path)     # repeat.tab, as the CLI writes it
+            timed("write", job.write, "strfinder", out)     # repeat.tab, as the CLI writes it
         timed("index_wait", job.wait, ctx)    # the FM index build ran behind the host work
-        return out_path
 
     def sync():
-        if world > 1:
-            torch.cuda.synchronize()
-            td.barrier()
-            torch.cuda.synchronize()
+        _lib.lib().bwtmi_device_sync(local)
+        if c is not None:
+            c.barrier()
 
     for _ in range(a.warmup):
         step()
@@ -173,32 +221,52 @@ def main():
     elapsed = time.perf_counter() - t0
     kstats = _lib.kernel_stats(ctx, enable=False, reset=True)
     stages = job.stage_ms()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dev is not None else "cpu")
-        td.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    if c is not None:
+        import numpy as np
+        elapsed = float(c.allreduce(np.array([elapsed], dtype=np.float64), _comm.MAX)[0])
     if a.stages:
-        print(json.dumps(dict(rank=rank, stage_ms=stages, kernels=kstats)), file=sys.stderr)
+        print(json.dumps(dict(rank=rank, stage_ms=stages, kernels=kstats, calls=calls)), file=sys.stderr)
+
+    def cleanup():
+        for p in ((out, fa) if (not shared or rank == 0) else ()):
+            try:
+                os.unlink(p)
+            except OSError:
+                pass
+
     if rank != 0:
-        if td is not None:
-            td.barrier()
+        if c is not None:
+            c.barrier()      # rank 0 has read the shared output
+        cleanup()
         return 0
 
-    with open(out_path, "rb") as f:
+    with open(out, "rb") as f:
         data = f.read()
     rows, digest = data.count(b"\n") - 1, hashlib.sha256(data).hexdigest()
-    os.unlink(out_path)
+    golden = None
+    gpath = os.path.join(REPO, "tests", "golden", "expected_large.json")
+    if not a.contig_bp and os.path.exists(gpath):
+        with open(gpath) as f:
+            g = json.load(f).get(wl["golden"])
+        if g and (shared or world == 1):
+            golden = dict(name=wl["golden"], sha256=g["out_sha256"], rows=g["out_rows"],
+                          match=g["out_sha256"] == digest)
+    total_bp = sum(wl["lengths"]) * (1 if shared else world)
     ms_step = elapsed / a.steps * 1000.0
-    total_bp = world * a.contig_bp
     value = total_bp / 1e6 / (elapsed / a.steps)
-    # dominant kernel = largest total device time in the timed steps
-    dom = max(kstats.items(), key=lambda kv: kv[1][0]) if kstats else None
+    per_call = {k: v / a.steps for k, v in calls.items()}
+
+    # dominant kernel = largest total device time in the timed steps (every launch is timed)
+    dev_ms = sum(v[0] for v in kstats.values())
     roofline = None
-    if dom:
-        name, (kms, launches, kbytes) = dom
+    with_bytes = {k: v for k, v in kstats.items() if v[2] > 0}
+    if with_bytes:
+        name, (kms, launches, kbytes) = max(kstats.items(), key=lambda kv: kv[1][0])
+        if kbytes <= 0:   # the largest kernel has no byte model: fall back to the largest modelled one
+            name, (kms, launches, kbytes) = max(with_bytes.items(), key=lambda kv: kv[1][0])
         achieved = kbytes / (kms / 1e3) / 1e9 if kms > 0 else 0.0
         traffic = None
-        if a.pmc_summary and os.path.exists(a.pmc_summary) and a.contig_bp == CONTIG_BP:   # measured at C3
+        if a.pmc_summary and os.path.exists(a.pmc_summary) and wl_name in ("C3", "C5") and not a.contig_bp:
             with open(a.pmc_summary) as f:
                 pk = json.load(f).get("kernels", {}).get(KERNEL_OF.get(name, name))
             if pk:
@@ -206,36 +274,63 @@ def main():
         roofline = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(achieved / HBM_PEAK_GBS, 5), traffic=traffic, kernel=name,
                         alg_bytes_per_launch=round(kbytes / launches), avg_launch_ms=round(kms / launches, 4),
-                        launches_per_step=launches / a.steps)
-    cpu = None if a.no_cpu_baseline else cpu_baseline(a.cpu_sample_bp)
-    fm = None if a.no_fm else fm_all_motifs(own_seq)
+                        launches_per_step=launches / a.steps,
+                        share_of_device_time=round(kms / dev_ms, 4) if dev_ms else None)
+    # strict scan: word compares of k_runs against the VALU issue ceiling
+    mine = job.select_shard(load_world, load_rank) if shared else range(job.contig_count())
+    wc = sum(word_compares(job.contig_weight(i), max(120, min(job.contig_weight(i) // 3, 1000))) for i in mine)
+    kr = kstats.get("k_runs")
+    scan_rate = None
+    if kr and kr[0] > 0:
+        per_s = wc / (kr[0] / a.steps / 1e3)
+        scan_rate = dict(word_compares_per_step=wc, k_runs_ms_per_step=round(kr[0] / a.steps, 3),
+                         gcompares_per_s=round(per_s / 1e9, 1), valu_lane_ops_peak=VALU_LANE_OPS_PEAK,
+                         frac_of_valu_issue_at_1_op_per_compare=round(per_s / VALU_LANE_OPS_PEAK, 4))
+    e2e_gbs = B_ALG_PER_BASE * total_bp / (elapsed / a.steps) / 1e9
+    cpu = None if a.no_cpu_baseline else cpu_baseline(a.cpu_sample_bp, wl["sub_rate"], host["threads_per_rank"])
+    fm = None
+    if not a.no_fm:
+        first = min(i for i in range(job.contig_count()) if job.contig_info(i)[1] > 0)
+        fm = fm_all_motifs(job.contig_seq(first))
+    load_up = per_call.get("load_fasta", 0.0) + per_call.get("upload", 0.0)
     line = {
-        "metric": "Mbp/s indexed+scanned (Tier1+2) on 100 Mbp synthetic FASTA, 1/2/4/8 GPU",
+        "metric": METRIC,
         "value": round(value, 3), "unit": "Mbp/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic (seeded splitmix64 generator, bwtmi/synth.py)",
-        "config": {"workload": "C3: one 100 Mbp synthetic contig per GPU, Tier1+2 defaults with "
-                               "--progress (ungated), FM index + strict scan + post-processing + "
-                               "STRfinder render", "contig_bp": a.contig_bp, "contigs": world,
+        "scaling": "strong" if shared else "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic FASTA on local disk (seeded splitmix64 generator, bwtmi/synth.py), "
+                "read and parsed inside every step",
+        "config": {"workload": f"{wl_name}: " + {
+                       "C3": "one 100 Mbp synthetic contig per GPU, Tier1+2 defaults with --progress (ungated)",
+                       "C4": "8 x 12.5 Mbp contigs in one FASTA, contigs sharded over the GPUs",
+                       "C5": "one 100 Mbp contig with 0.02 substitutions in the planted arrays, --progress"}[wl_name]
+                   + "; FASTA read -> FM index + strict scan + post-processing -> STRfinder repeat.tab closed",
+                   "contig_bp": wl["lengths"][0], "contigs": len(wl["lengths"]) * (1 if shared else world),
                    "parallelism": f"contig-shard x{world}", "index": not a.no_index},
         "roofline": roofline,
+        "e2e_roofline": {"b_alg_bytes_per_base": B_ALG_PER_BASE, "achieved_gbs": round(e2e_gbs, 2),
+                         "peak_gbs": HBM_PEAK_GBS * world, "frac": round(e2e_gbs / (HBM_PEAK_GBS * world), 6)},
+        "strict_scan_rate": scan_rate,
         "cpu_baseline": cpu,
+        "host": dict(host, nproc=os.cpu_count(), cpu_model=cpu_model()),
         "rows": rows,
         "output_sha256": digest,
-        "stage_ms_last_step": {"scan+index": round(stages[0], 2), "index": round(stages[1], 2),
+        "golden": golden,
+        "stage_ms_last_step": {"scan": round(stages[0], 2), "index": round(stages[1], 2),
                                "nested": round(stages[2], 2), "dedup": round(stages[3], 2),
                                "merge": round(stages[4], 2), "refine..filter": round(stages[5], 2),
                                "render": round(stages[6], 2)},
-        "kernels_ms_per_step": {k: round(v[0] / a.steps, 3) for k, v in sorted(kstats.items())},
-        "h2d_upload_ms": round(upload_ms, 2),
+        "device_ms_per_step": round(dev_ms / a.steps, 3),
+        "kernels_ms_per_step": {k: round(v[0] / a.steps, 3) for k, v in
+                                sorted(kstats.items(), key=lambda kv: -kv[1][0])},
+        "calls_ms_per_step": {k: round(v, 2) for k, v in per_call.items()},
+        "value_resident_text": round(total_bp / 1e6 / ((ms_step - load_up) / 1e3), 3) if ms_step > load_up else None,
         "fm_all_motifs_1_10": fm,
-        "calls_ms_per_step": {k: round(v / a.steps, 2) for k, v in calls.items()},
-        "value_incl_upload": round(total_bp / 1e6 / (elapsed / a.steps + upload_ms / 1e3), 3),
     }
     print(json.dumps(line))
-    if td is not None:
-        td.barrier()
+    if c is not None:
+        c.barrier()
+    cleanup()
     return 0
 
 

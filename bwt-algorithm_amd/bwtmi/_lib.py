@@ -108,6 +108,15 @@ _SIGS = {
     "bwtmi_job_contig_info": (C.c_int64, [_P, C.c_int32, C.c_char_p, C.c_int64, C.POINTER(C.c_int64),
                                           C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "bwtmi_job_contig_seq": (C.c_int, [_P, C.c_int32, _P]),
+    "bwtmi_job_load_fasta_shard": (C.c_int, [_P, C.c_char_p, C.c_int32, C.c_int32, C.c_int32]),
+    "bwtmi_job_contig_weight": (C.c_int64, [_P, C.c_int32]),
+    "bwtmi_job_select_shard": (C.c_int, [_P, C.c_int32, C.c_int32, _P, _P]),
+    "bwtmi_host_info": (C.c_int, [C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "bwtmi_comm_unique_id": (C.c_int, [_P]),
+    "bwtmi_comm_init": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, _P, C.POINTER(_P)]),
+    "bwtmi_comm_allreduce": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32]),
+    "bwtmi_comm_free": (C.c_int, [_P]),
+    "bwtmi_device_sync": (C.c_int, [C.c_int32]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -177,6 +186,13 @@ def kernel_stats(h, enable: bool = True, reset: bool = True) -> dict:
         name, ms, n, b = line.split()
         out[name] = (float(ms), int(n), float(b))
     return out
+
+
+def host_info() -> dict:
+    """CPUs visible to this process, ranks on the node, post-processing threads per rank."""
+    v, lw, t = C.c_int32(), C.c_int32(), C.c_int32()
+    check(lib().bwtmi_host_info(C.byref(v), C.byref(lw), C.byref(t)))
+    return {"cpus_visible": v.value, "local_world": lw.value, "threads_per_rank": t.value}
 
 
 def last_timing(h) -> tuple:

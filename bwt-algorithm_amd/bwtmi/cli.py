@@ -74,19 +74,18 @@ def main(argv=None) -> int:
                                 min_period=a.min_period, max_period=a.max_period,
                                 min_copies=a.min_copies, min_entropy=a.min_entropy,
                                 flank_trim=a.flank_trim, max_unit_len=a.max_unit_len)
-    sequences = finder.load_reference()
     from . import dist
     if dist.is_distributed() and not a.tier3:
-        # one process per GPU: shard fold units, each rank writes its own rows
-        if a.format not in ("bed", "vcf", "trf_table", "trf_dat", "strfinder"):
-            raise SystemExit(f"unknown format {a.format}")
+        # one process per GPU: each rank loads and analyses its own fold units
+        # and writes their rows into the shared output (no torch, no record gather)
         n = finder.find_and_write_sharded(tier2, a.output, a.format)
-        if dist._torch_dist().get_rank() == 0:
+        if dist.init().rank == 0:
             print()
             print("=" * 60)
             print(f"Completed! Found {n} total tandem repeats.")
             print(f"Results saved to {a.output}")
         return 0
+    sequences = finder.load_reference()
     if os.environ.get("BWTMI_SKIP_INDEX", "0") != "1":
         finder.build_indices(sequences)
     long_reads = _read_long_reads(a.long_reads) if (a.long_reads and a.tier3) else []
@@ -94,7 +93,7 @@ def main(argv=None) -> int:
         repeats = finder.find_tandem_repeats_parallel(True, tier2, a.tier3, long_reads or None, None)
     else:
         repeats = finder.find_tandem_repeats(True, tier2, a.tier3, long_reads or None)
-    if dist.is_distributed() and dist._torch_dist().get_rank() != 0:
+    if dist.is_distributed() and dist.init().rank != 0:
         return 0
     finder.save_results(repeats, a.output, a.format)
     print()

@@ -6,7 +6,7 @@ process.
   build_indices       device FM index per contig (bwt.py:3758-3790)
   find_tandem_repeats / find_tandem_repeats_parallel
                       device strict scan per contig + native post-processing
-                      (bwt.py:3792-3954); with torch.distributed initialised
+                      (bwt.py:3792-3954); under a multi-rank launch
                       the contigs are sharded over ranks (bwtmi.dist)
   save_results        native writers incl. compound detection (bwt.py:4141-4198)
 """
@@ -120,25 +120,19 @@ class TandemRepeatFinder:
         rank.  Returns the total number of records (all ranks)."""
         import numpy as np
         from . import dist
+        c = dist.init()
         if self.job is None:
-            self.load_reference()
+            job = self._new_job()
+            job.load_fasta(self.reference_file, self.flank_trim, c.world, c.rank)
+            self.job = job
         job = self.job
         job.reset()
         job.set_tier2(enable_tier2)
-        td = dist.init()
-        rank, world = td.get_rank(), td.get_world_size()
-        infos = [job.contig_info(i) for i in range(job.contig_count())]
-        shard = dist.assign(dist.natural_units([x[0] for x in infos]), [x[1] - x[2] - x[3] for x in infos],
-                            world)[rank]
-        job.select(shard)
+        job.select_shard(c.world, c.rank)
         job.scan(_lib.ctx(self.device))
         job.postprocess()
-        device = "cpu"
-        if td.get_backend() == "nccl":
-            import torch
-            device = torch.device("cuda", torch.cuda.current_device())
-        total = int(dist._allreduce_sum(td, np.array([job.count()], dtype=np.int64), device)[0])
-        dist.write_sharded(td, job, format_type, output_file, device)
+        total = int(c.allreduce(np.array([job.count()], dtype=np.int64))[0])
+        dist.write_sharded(c, job, format_type, output_file)
         job.wait(_lib.ctx(self.device))
         return total
 

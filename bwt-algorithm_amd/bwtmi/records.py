@@ -120,9 +120,26 @@ class Job:
         self.names.append(name)
         return cid.value
 
-    def load_fasta(self, path: str, flank_trim: int) -> None:
-        check(lib().bwtmi_job_load_fasta(self.h, path.encode(), flank_trim))
-        self.names = [self.contig_info(i)[0] for i in range(self.contig_count())]
+    def load_fasta(self, path: str, flank_trim: int, world: int = 1, rank: int = 0) -> None:
+        """load_reference (bwt.py:3713-3756), natively; with world > 1 only this
+        rank's fold units get their bases (and the job is restricted to them)."""
+        if world > 1:
+            check(lib().bwtmi_job_load_fasta_shard(self.h, path.encode(), flank_trim, world, rank))
+        else:
+            check(lib().bwtmi_job_load_fasta(self.h, path.encode(), flank_trim))
+        if len(self.names) != self.contig_count():
+            self.names = [self.contig_info(i)[0] for i in range(self.contig_count())]
+
+    def contig_weight(self, i: int) -> int:
+        """Analysed (trimmed) length of contig i, also when its bases are on another rank."""
+        return lib().bwtmi_job_contig_weight(self.h, i)
+
+    def select_shard(self, world: int, rank: int) -> List[int]:
+        """Restrict the job to this rank's fold units (LPT over analysed lengths)."""
+        ids = np.zeros(max(1, self.contig_count()), dtype=np.int32)
+        n = C.c_int32()
+        check(lib().bwtmi_job_select_shard(self.h, world, rank, ids.ctypes.data_as(C.c_void_p), C.byref(n)))
+        return ids[:n.value].tolist()
 
     def contig_count(self) -> int:
         return lib().bwtmi_job_contig_count(self.h)

@@ -15,6 +15,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "common.h"
@@ -63,7 +64,38 @@ static int guard(F &&f) {
 struct DevContig {
     DBuf buf;
     int64_t n = -1;
+    uint64_t gen = 0;   // Contig::gen of the uploaded content
 };
+
+// Host blocks of contig bases (mem.h cached blocks) are registered for DMA the
+// first time they are uploaded and stay registered while the block lives
+// (cached blocks keep it); the unmap hook drops the registration.
+std::mutex g_reg_mu;
+std::unordered_map<void *, size_t> g_registered;
+
+void unregister_block(void *p, size_t) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_registered.find(p);
+    if (it == g_registered.end()) return;
+    (void)hipHostUnregister(p);
+    g_registered.erase(it);
+}
+
+// true when [p, p+n) lies in a registered (pinned) block
+bool ensure_pinned(const void *base, const void *p, size_t n) {
+    const size_t sz = big_block_size(base);
+    if (!sz || (const char *)p + n > (const char *)base + sz) return false;
+    static std::once_flag hook;
+    std::call_once(hook, [] { big_set_unmap_hook(unregister_block); });
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    if (g_registered.count(const_cast<void *>(base))) return true;
+    if (hipHostRegister(const_cast<void *>(base), sz, hipHostRegisterDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;   // pageable copy
+    }
+    g_registered.emplace(const_cast<void *>(base), sz);
+    return true;
+}
 
 struct JobDev {
     int device = -1;
@@ -78,14 +110,38 @@ static Ctx &use(Ctx &c) {
     return c;
 }
 
+// Output file descriptor: closed on every path; when the write fails part-way
+// (an exception or a short write) the file is cut to 0 bytes rather than left
+// holding a mix of old and new rows.
+struct OutFd {
+    int fd = -1;
+    bool ok = false;
+    explicit OutFd(const char *path) : fd(::open(path, O_WRONLY | O_CREAT, 0644)) {
+        if (fd < 0) fail(BWTMI_E_IO, "cannot open %s for writing", path);
+    }
+    ~OutFd() {
+        if (fd < 0) return;
+        if (!ok) (void)::ftruncate(fd, 0);
+        (void)::close(fd);
+    }
+    // cut to `size` (when whole) and close; false on error
+    bool finish(bool whole, size_t size) {
+        bool good = !whole || ::ftruncate(fd, (off_t)size) == 0;
+        ok = good;
+        good = (::close(fd) == 0) && good;
+        fd = -1;
+        return good;
+    }
+};
+
 // parts[k] lands at byte offset at[k] of `path`, in parallel (page-cache copies).
 // `whole`: the parts are the whole file -- it is overwritten in place and cut to
 // at.back() bytes afterwards (the content is that of open(path, 'w') + write;
 // rewriting a file of the same size reuses its page-cache pages).
 static void pwrite_parts(const char *path, bool whole, const std::vector<Text> &parts,
                          const std::vector<size_t> &at, int threads) {
-    const int fd = ::open(path, O_WRONLY | O_CREAT, 0644);
-    if (fd < 0) fail(BWTMI_E_IO, "cannot open %s for writing", path);
+    OutFd out(path);
+    const int fd = out.fd;
     std::vector<uint8_t> ok(parts.size(), 1);
     run_tasks((int64_t)parts.size(), threads, [&](int64_t k) {
         const Text &s = parts[(size_t)k];
@@ -96,10 +152,10 @@ static void pwrite_parts(const char *path, bool whole, const std::vector<Text> &
             done += (size_t)w;
         }
     });
-    bool good = !whole || ::ftruncate(fd, (off_t)at.back()) == 0;
-    good = (::close(fd) == 0) && good;
+    bool good = true;
     for (auto v : ok) good = good && v;
-    if (!good) fail(BWTMI_E_IO, "short write to %s", path);
+    if (!good) fail(BWTMI_E_IO, "short write to %s", path);   // ~OutFd cuts a whole-file write
+    if (!out.finish(whole, at.back())) fail(BWTMI_E_IO, "short write to %s", path);
 }
 
 }  // namespace bwtmi
@@ -396,7 +452,7 @@ int bwtmi_job_tier1(bwtmi_ctx *ctx, bwtmi_job *job, int32_t contig_id, int32_t m
         CHECK_ARG(contig_id >= 0 && contig_id < (int32_t)job->j.contigs.size(), "bad contig id");
         Ctx &c = ctx->c;
         use(c);
-        const std::string &full = job->j.contigs[(size_t)contig_id].full;
+        const Seq &full = job->j.contigs[(size_t)contig_id].full;
         const int64_t n = (int64_t)full.size();
         upload_text(c, c.slot[S_TEXT], (const uint8_t *)full.data(), n);
         tier1_device(c, c.slot[S_TEXT].as<uint8_t>(), (const uint8_t *)full.data(), n, max_motif_length, contig_id,
@@ -436,6 +492,8 @@ int bwtmi_job_add_contig(bwtmi_job *job, const char *name, const uint8_t *full, 
         c.full.assign((const char *)full, (size_t)full_len);
         c.trim_left = trim_left;
         c.trim_right = trim_right;
+        c.weight = full_len - trim_left - trim_right;
+        c.gen = next_contig_gen();
         job->j.contigs.push_back(std::move(c));
         if (contig_id) *contig_id = (int32_t)job->j.contigs.size() - 1;
     });
@@ -448,7 +506,41 @@ int bwtmi_job_load_fasta(bwtmi_job *job, const char *path, int32_t flank_trim) {
     });
 }
 
+int bwtmi_job_load_fasta_shard(bwtmi_job *job, const char *path, int32_t flank_trim, int32_t world, int32_t rank) {
+    return guard([&] {
+        CHECK_ARG(job && path && world >= 1 && rank >= 0 && rank < world, "bad argument");
+        load_fasta(job->j, path, flank_trim, world, rank);
+    });
+}
+
+int bwtmi_job_select_shard(bwtmi_job *job, int32_t world, int32_t rank, int32_t *ids, int32_t *n) {
+    return guard([&] {
+        CHECK_ARG(job && world >= 1 && rank >= 0 && rank < world, "bad argument");
+        std::vector<int32_t> v = shard_units(job->j, world, rank);
+        Job &J = job->j;
+        J.selected.assign(J.contigs.size(), 0);
+        for (int32_t c : v) J.selected[(size_t)c] = 1;
+        if (n) *n = (int32_t)v.size();
+        if (ids) std::copy(v.begin(), v.end(), ids);
+    });
+}
+
+int bwtmi_host_info(int32_t *cpus_visible, int32_t *local_world, int32_t *threads) {
+    return guard([&] {
+        int v = 0, lw = 0;
+        const int t = host_cpu_budget(&v, &lw);
+        if (cpus_visible) *cpus_visible = v;
+        if (local_world) *local_world = lw;
+        if (threads) *threads = t;
+    });
+}
+
 int32_t bwtmi_job_contig_count(const bwtmi_job *job) { return job ? (int32_t)job->j.contigs.size() : -1; }
+
+int64_t bwtmi_job_contig_weight(const bwtmi_job *job, int32_t id) {
+    if (!job || id < 0 || id >= (int32_t)job->j.contigs.size()) return -1;
+    return job->j.contigs[(size_t)id].weight;
+}
 
 int64_t bwtmi_job_contig_info(const bwtmi_job *job, int32_t id, char *name, int64_t cap, int64_t *full_len,
                               int64_t *trim_left, int64_t *trim_right) {
@@ -488,9 +580,11 @@ static void job_upload(bwtmi_ctx *ctx, bwtmi_job *job) {
         const Contig &ct = job->j.contigs[i];
         DevContig &dc = d.seqs[i];
         if (!job->j.selected.empty() && !job->j.selected[i]) continue;   // another rank's shard
-        if (dc.n == ct.trimmed_len()) continue;
+        if (dc.n == ct.trimmed_len() && dc.gen == ct.gen) continue;
+        ensure_pinned(ct.full.data(), ct.trimmed(), (size_t)ct.trimmed_len());
         upload_text(c, dc.buf, (const uint8_t *)ct.trimmed(), ct.trimmed_len());
         dc.n = ct.trimmed_len();
+        dc.gen = ct.gen;
     }
     HIPCHECK(hipStreamSynchronize(c.stream));
 }
@@ -686,8 +780,8 @@ int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len) {
 int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path) {
     return guard([&] {
         CHECK_ARG(job && path, "null argument");
-        const int fd = ::open(path, O_WRONLY | O_CREAT, 0644);
-        if (fd < 0) fail(BWTMI_E_IO, "cannot open %s for writing", path);
+        OutFd out(path);
+        const int fd = out.fd;
         Rendered R;
         std::mutex mu;
         std::vector<uint8_t> done;
@@ -724,9 +818,8 @@ int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path) {
             put(R.header.data(), R.header.size(), 0);
             off = R.header.size();
         }
-        bool good = !bad && ::ftruncate(fd, (off_t)off) == 0;
-        good = (::close(fd) == 0) && good;
-        if (!good) fail(BWTMI_E_IO, "short write to %s", path);
+        if (bad) fail(BWTMI_E_IO, "short write to %s", path);   // ~OutFd cuts the file to 0
+        if (!out.finish(true, off)) fail(BWTMI_E_IO, "short write to %s", path);
     });
 }
 

@@ -39,11 +39,70 @@ struct ScreenedHit {
 using ScreenedVec = std::vector<ScreenedHit, NoInit<ScreenedHit>>;
 
 // ---------------------------------------------------------------- contigs
+// contig bases live in cached huge-page blocks (mem.h); the device layer pins
+// those blocks once for DMA (api.cpp), so re-loading a FASTA of the same shape
+// reuses already-faulted, already-registered memory
+class Seq {
+public:
+    Seq() = default;
+    Seq(const Seq &o) { assign(o.data(), o.size()); }
+    Seq(Seq &&o) noexcept { swap(o); }
+    Seq &operator=(const Seq &o) {
+        if (this != &o) assign(o.data(), o.size());
+        return *this;
+    }
+    Seq &operator=(Seq &&o) noexcept {
+        swap(o);
+        return *this;
+    }
+    ~Seq() { release(); }
+    const char *data() const { return p_ ? p_ : ""; }
+    char *data() { return p_; }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    char operator[](size_t i) const { return p_[i]; }
+    void swap(Seq &o) noexcept {
+        std::swap(p_, o.p_);
+        std::swap(n_, o.n_);
+        std::swap(cap_, o.cap_);
+    }
+    void clear() { release(); }
+    // n bytes of unspecified content (written by the caller)
+    char *resize_uninit(size_t n) {
+        if (n > cap_) {
+            release();
+            p_ = (char *)(n >= kBigMin ? big_alloc(n) : ::operator new(n));
+            cap_ = n;
+        }
+        n_ = n;
+        return p_;
+    }
+    void assign(const char *s, size_t n) {
+        char *d = resize_uninit(n);
+        if (n) std::memcpy(d, s, n);
+    }
+
+private:
+    void release() {
+        if (p_) {
+            if (cap_ >= kBigMin) big_free(p_, cap_);
+            else ::operator delete(p_);
+        }
+        p_ = nullptr;
+        n_ = cap_ = 0;
+    }
+    char *p_ = nullptr;
+    size_t n_ = 0, cap_ = 0;
+};
+uint64_t next_contig_gen();   // fresh content id (device copies are keyed by it)
+
 struct Contig {
     std::string name;
-    std::string full;      // untrimmed, upper-cased (bwt.py:3739)
+    Seq full;               // untrimmed, upper-cased (bwt.py:3739); empty for another rank's contig
     int64_t trim_left = 0;  // trim_offsets[name] (bwt.py:3733)
     int64_t trim_right = 0;
+    int64_t weight = 0;     // analysed length (shard weight), also for contigs not loaded here
+    uint64_t gen = 0;       // content id of `full`
     int32_t unit = 0;       // fold unit (contigs with equal natural sort key)
     const char *trimmed() const { return full.data() + trim_left; }
     int64_t trimmed_len() const { return (int64_t)full.size() - trim_left - trim_right; }
@@ -152,10 +211,18 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
                  const std::function<void(size_t)> *on_part = nullptr);
 std::vector<Text> render_parts(Job &job, int fmt);
 std::string render(Job &job, int fmt);
-// fasta.cpp
-void load_fasta(Job &job, const char *path, int32_t flank_trim);
+// fasta.cpp: load_reference; with world > 1 only this rank's shard (fold units by
+// longest-processing-time over the analysed lengths, shard_units) gets its bases
+void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world = 1, int32_t rank = 0);
+// fold units -> ranks by longest-processing-time greedy (deterministic; same as
+// bwtmi.dist.assign): returns the contig ids owned by `rank`
+std::vector<int32_t> shard_units(Job &job, int32_t world, int32_t rank);
 
+// host threads of one process: params.threads, else this process's share of
+// the CPUs it may run on (affinity mask and cgroup quota, divided among the
+// LOCAL_WORLD_SIZE ranks of the node), at most 16
 int host_threads(const bwtmi_params &p);
+int host_cpu_budget(int *cpus_visible, int *local_world);
 // fn(task) for task in [0, n) on up to nt threads (dynamic scheduling)
 void run_tasks(int64_t n, int nt, const std::function<void(int64_t)> &fn);
 

@@ -91,11 +91,20 @@ struct Ctx {
     std::vector<Pend> pending;
     std::vector<size_t> open;   // kbegin/kend nest (a stage timer around primitive timers)
     std::vector<std::pair<std::string, KStat>> kstats;
+    std::vector<hipEvent_t> evpool;   // reused across kresolve calls
+    size_t evused = 0;
+    hipEvent_t pooled_event() {
+        if (evused == evpool.size()) {
+            hipEvent_t e;
+            HIPCHECK(hipEventCreate(&e));
+            evpool.push_back(e);
+        }
+        return evpool[evused++];
+    }
+    // every kernel launch is a leaf timer (KLAUNCH); kbegin/kend must not nest
     void kbegin(const char *name, double alg_bytes = 0) {
         if (!ktiming) return;
-        hipEvent_t a, b;
-        HIPCHECK(hipEventCreate(&a));
-        HIPCHECK(hipEventCreate(&b));
+        hipEvent_t a = pooled_event(), b = pooled_event();
         HIPCHECK(hipEventRecord(a, stream));
         open.push_back(pending.size());
         pending.push_back({name, a, b, alg_bytes});
@@ -122,11 +131,10 @@ struct Ctx {
                     break;
                 }
             if (!found) kstats.push_back({p.name, KStat{ms, 1, p.bytes}});
-            (void)hipEventDestroy(p.a);
-            (void)hipEventDestroy(p.b);
         }
         pending.clear();
         open.clear();
+        evused = 0;
     }
     DBuf slot[S_NSLOTS];
     HBuf host[4];
@@ -145,6 +153,15 @@ struct Ctx {
     bool timing = true;
     void activate() const { HIPCHECK(hipSetDevice(device)); }
 };
+
+// A kernel launch on ctx `c`'s stream `st`, timed as `name` (algorithmic bytes
+// `bytes`, 0 when not modelled) when kernel statistics are on.
+#define KLAUNCH(name, bytes, kern, grid, block, shm, st, ...)                  \
+    do {                                                                       \
+        c.kbegin(name, bytes);                                                 \
+        hipLaunchKernelGGL(kern, grid, block, shm, st, __VA_ARGS__);           \
+        c.kend();                                                              \
+    } while (0)
 
 // join the context's background device work; rethrows its error
 inline void ctx_join(Ctx &c) {

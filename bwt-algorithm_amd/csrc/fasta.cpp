@@ -1,9 +1,29 @@
-// fasta.cpp -- TandemRepeatFinder.load_reference (bwt.py:3713-3756), native.
+// fasta.cpp -- TandemRepeatFinder.load_reference (bwt.py:3713-3756), native and
+// parallel.
+//
 // Python reads the file in text mode: universal newlines (\n, \r\n, \r end a
 // line), each line .strip()-ed (ASCII whitespace incl. \x1c-\x1f), headers
 // '>' take line[1:].split()[0], other non-empty lines are upper-cased and
-// appended (inner whitespace kept).  A repeated name keeps its first position
-// and the last content.  Trim: 30+30 flanks when len > 2*flank_trim.
+// appended (inner whitespace kept); lines before the first header are
+// dropped.  A repeated name keeps its first position and the last content.
+// Trim: 30+30 flanks when len > 2*flank_trim.
+//
+// The file is cut into chunks at line starts (empty lines are skipped, so a
+// cut between '\r' and '\n' is harmless).  Pass 1 measures, per chunk, the
+// stripped content before its first header and after each header; a serial
+// stitch turns those into contig lengths and the destination offset of every
+// chunk piece; pass 2 writes the upper-cased bytes straight into the contig
+// buffers.  With world > 1 only this rank's fold units (shard_units) are
+// written -- the others keep their names and lengths for the shard layout.
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
 #include <cstdio>
 #include <string>
 #include <unordered_map>
@@ -13,83 +33,229 @@
 
 namespace bwtmi {
 
-static inline bool py_space(unsigned char c) {
-    return c == ' ' || (c >= 9 && c <= 13) || (c >= 0x1c && c <= 0x1f);
+static std::atomic<uint64_t> g_gen{0};
+uint64_t next_contig_gen() { return ++g_gen; }
+
+namespace {
+
+inline bool py_space(unsigned char c) { return c == ' ' || (c >= 9 && c <= 13) || (c >= 0x1c && c <= 0x1f); }
+inline bool eol(char c) { return c == '\n' || c == '\r'; }
+
+struct Hdr {
+    int64_t name_a, name_b;   // name bytes in the file buffer
+    int64_t len;              // stripped content after the header, inside the chunk
+};
+struct Chunk {
+    int64_t a = 0, b = 0;     // [a, b): whole lines
+    int64_t pre = 0;          // content before the chunk's first header
+    std::vector<Hdr> hdrs;
+    // pass 2 destinations (nullptr: not written)
+    char *pre_dst = nullptr;
+    std::vector<char *> dst;
+};
+
+// calls line(a, b) with the stripped bounds of every non-empty line in [a, e)
+template <class F>
+void for_lines(const char *p, int64_t a, int64_t e, F &&line) {
+    int64_t i = a;
+    while (i < e) {
+        // line end: the next '\n' (memchr), or an earlier '\r'
+        const char *nl = (const char *)std::memchr(p + i, '\n', (size_t)(e - i));
+        int64_t j = nl ? (int64_t)(nl - p) : e;
+        if (const char *cr = (const char *)std::memchr(p + i, '\r', (size_t)(j - i))) j = (int64_t)(cr - p);
+        int64_t s = i, t = j;
+        while (s < t && py_space((unsigned char)p[s])) ++s;
+        while (t > s && py_space((unsigned char)p[t - 1])) --t;
+        if (t > s) line(s, t);
+        i = j + 1;   // "\r\n": the '\n' becomes an empty line
+    }
 }
 
-void load_fasta(Job &job, const char *path, int32_t flank_trim) {
-    FILE *f = std::fopen(path, "rb");
-    if (!f) fail(BWTMI_E_IO, "cannot open %s", path);
-    std::string data;
-    {
-        std::fseek(f, 0, SEEK_END);
-        long sz = std::ftell(f);
-        std::fseek(f, 0, SEEK_SET);
-        if (sz < 0) sz = 0;
-        data.resize((size_t)sz);
-        if (sz && std::fread(&data[0], 1, (size_t)sz, f) != (size_t)sz) {
-            std::fclose(f);
-            fail(BWTMI_E_IO, "read error on %s", path);
-        }
-        std::fclose(f);
+// upper-cased copy (ASCII a-z), vectorised
+inline void upper_copy(char *__restrict d, const char *__restrict s, int64_t n) {
+    for (int64_t q = 0; q < n; ++q) {
+        const unsigned char ch = (unsigned char)s[q];
+        d[q] = (char)(ch - ((unsigned char)(ch - 'a') < 26u ? 32 : 0));
     }
-    const int64_t flank = flank_trim < 0 ? 0 : flank_trim;
-    std::unordered_map<std::string, size_t> index;
-    for (size_t i = 0; i < job.contigs.size(); ++i) index[job.contigs[i].name] = i;
-    std::string name;
-    bool have = false;
-    std::string seq;
-    auto flush = [&]() {
-        Contig c;
-        c.name = name;
-        c.full.swap(seq);
-        const int64_t L = (int64_t)c.full.size();
-        if (L <= 2 * flank) {
-            c.trim_left = c.trim_right = 0;
-        } else {
-            c.trim_left = c.trim_right = flank;
+}
+
+void read_file(const char *path, Seq &data, int nt) {
+    const int fd = ::open(path, O_RDONLY);
+    if (fd < 0) fail(BWTMI_E_IO, "cannot open %s", path);
+    struct stat st;
+    if (::fstat(fd, &st) != 0) {
+        ::close(fd);
+        fail(BWTMI_E_IO, "cannot stat %s", path);
+    }
+    const int64_t n = (int64_t)st.st_size;
+    char *buf = data.resize_uninit((size_t)n);
+    std::atomic<bool> bad{false};
+    const int64_t piece = int64_t(4) << 20;
+    run_tasks((n + piece - 1) / piece, nt, [&](int64_t k) {
+        int64_t o = k * piece;
+        const int64_t e = std::min(n, o + piece);
+        while (o < e) {
+            const ssize_t r = ::pread(fd, buf + o, (size_t)(e - o), (off_t)o);
+            if (r <= 0) { bad = true; return; }
+            o += r;
         }
-        auto it = index.find(c.name);
-        if (it != index.end()) {
-            job.contigs[it->second] = std::move(c);
-        } else {
-            index[c.name] = job.contigs.size();
-            job.contigs.push_back(std::move(c));
-        }
-        seq.clear();
-    };
+    });
+    ::close(fd);
+    if (bad) fail(BWTMI_E_IO, "read error on %s", path);
+}
+
+}  // namespace
+
+void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, int32_t rank) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    const int nt = host_threads(job.params);
+    thread_local Seq data;   // the file image (kept for the next load)
+    read_file(path, data, nt);
+    const auto t1 = clk::now();
     const char *p = data.data();
-    const size_t n = data.size();
-    size_t i = 0;
-    while (i < n) {
-        size_t j = i;
-        while (j < n && p[j] != '\n' && p[j] != '\r') ++j;
-        size_t a = i, b = j;
-        while (a < b && py_space((unsigned char)p[a])) ++a;
-        while (b > a && py_space((unsigned char)p[b - 1])) --b;
-        if (b > a) {
-            if (p[a] == '>') {
-                if (have) flush();
-                size_t x = a + 1;
-                while (x < b && py_space((unsigned char)p[x])) ++x;
-                size_t y = x;
-                while (y < b && !py_space((unsigned char)p[y])) ++y;
-                if (y == x) fail(BWTMI_E_IO, "empty FASTA header in %s", path);  // split()[0] IndexError
-                name.assign(p + x, y - x);
-                have = true;
-                seq.clear();
+    const int64_t N = (int64_t)data.size();
+
+    // chunks at line starts
+    const int64_t T = std::max<int64_t>(1, std::min<int64_t>(4 * (int64_t)nt, N / (int64_t(1) << 20) + 1));
+    std::vector<Chunk> ck((size_t)T);
+    std::vector<int64_t> cut((size_t)T + 1, N);
+    cut[0] = 0;
+    run_tasks(T - 1, nt, [&](int64_t q) {
+        int64_t i = N * (q + 1) / T;
+        while (i < N && !eol(p[i - 1])) ++i;
+        cut[(size_t)q + 1] = i;
+    });
+    for (int64_t t = 1; t <= T; ++t) cut[(size_t)t] = std::max(cut[(size_t)t], cut[(size_t)t - 1]);
+
+    // pass 1: lengths
+    run_tasks(T, nt, [&](int64_t t) {
+        Chunk &C = ck[(size_t)t];
+        C.a = cut[(size_t)t];
+        C.b = cut[(size_t)t + 1];
+        for_lines(p, C.a, C.b, [&](int64_t s, int64_t e) {
+            if (p[s] == '>') {
+                int64_t x = s + 1;
+                while (x < e && py_space((unsigned char)p[x])) ++x;
+                int64_t y = x;
+                while (y < e && !py_space((unsigned char)p[y])) ++y;
+                C.hdrs.push_back(Hdr{x, y, 0});
+            } else if (C.hdrs.empty()) {
+                C.pre += e - s;
             } else {
-                const size_t o = seq.size();
-                seq.append(p + a, b - a);
-                for (size_t k = o; k < seq.size(); ++k)
-                    if (seq[k] >= 'a' && seq[k] <= 'z') seq[k] = (char)(seq[k] - 32);
+                C.hdrs.back().len += e - s;
+            }
+        });
+    });
+
+    // stitch: header instances in file order -> contigs (a repeated name reuses its slot)
+    struct Inst {
+        int32_t contig;
+        int64_t len;
+    };
+    std::vector<Inst> inst;
+    std::unordered_map<std::string, int32_t> index;
+    for (size_t i = 0; i < job.contigs.size(); ++i) index[job.contigs[i].name] = (int32_t)i;
+    std::vector<int32_t> last_inst;   // per contig: the instance whose content it keeps
+    for (int64_t t = 0; t < T; ++t) {
+        Chunk &C = ck[(size_t)t];
+        if (!inst.empty()) inst.back().len += C.pre;
+        for (auto &h : C.hdrs) {
+            if (h.name_b == h.name_a) fail(BWTMI_E_IO, "empty FASTA header in %s", path);   // split()[0]
+            std::string name(p + h.name_a, (size_t)(h.name_b - h.name_a));
+            auto it = index.find(name);
+            int32_t cid;
+            if (it == index.end()) {
+                cid = (int32_t)job.contigs.size();
+                index.emplace(name, cid);
+                Contig c;
+                c.name = std::move(name);
+                job.contigs.push_back(std::move(c));
+            } else {
+                cid = it->second;
+            }
+            inst.push_back(Inst{cid, h.len});
+        }
+    }
+    last_inst.assign(job.contigs.size(), -1);
+    for (size_t k = 0; k < inst.size(); ++k) last_inst[(size_t)inst[k].contig] = (int32_t)k;
+    const int64_t flank = flank_trim < 0 ? 0 : flank_trim;
+    for (size_t cid = 0; cid < job.contigs.size(); ++cid) {
+        const int32_t k = last_inst[cid];
+        if (k < 0) continue;   // registered before this call and not in the file
+        Contig &c = job.contigs[cid];
+        const int64_t L = inst[(size_t)k].len;
+        c.trim_left = c.trim_right = (L <= 2 * flank) ? 0 : flank;
+        c.weight = L - c.trim_left - c.trim_right;
+        c.gen = next_contig_gen();
+    }
+
+    // this rank's contigs
+    std::vector<uint8_t> mine(job.contigs.size(), 1);
+    if (world > 1) {
+        std::fill(mine.begin(), mine.end(), 0);
+        for (int32_t c : shard_units(job, world, rank)) mine[(size_t)c] = 1;
+        job.selected.assign(mine.begin(), mine.end());
+    }
+    // buffers (allocation only; pass 2 fills them in parallel)
+    std::vector<char *> base(job.contigs.size(), nullptr);
+    for (size_t cid = 0; cid < job.contigs.size(); ++cid) {
+        const int32_t k = last_inst[cid];
+        if (k < 0) continue;
+        Contig &c = job.contigs[cid];
+        if (!mine[cid]) {   // another rank's contig: name and weight only
+            c.full.clear();
+            c.trim_left = c.trim_right = 0;
+            continue;
+        }
+        base[cid] = c.full.resize_uninit((size_t)inst[(size_t)k].len);   // filled by pass 2
+    }
+    // destinations of every chunk piece
+    {
+        size_t k = 0;
+        int64_t off = 0;   // offset inside the current instance
+        bool have = false;
+        auto dst_of = [&](size_t kk, int64_t o) -> char * {
+            const Inst &I = inst[kk];
+            if (last_inst[(size_t)I.contig] != (int32_t)kk || !base[(size_t)I.contig]) return nullptr;
+            return base[(size_t)I.contig] + o;
+        };
+        for (int64_t t = 0; t < T; ++t) {
+            Chunk &C = ck[(size_t)t];
+            if (have) {
+                C.pre_dst = C.pre ? dst_of(k - 1, off) : nullptr;
+                off += C.pre;
+            }
+            C.dst.resize(C.hdrs.size());
+            for (size_t h = 0; h < C.hdrs.size(); ++h) {
+                C.dst[h] = C.hdrs[h].len ? dst_of(k, 0) : nullptr;
+                off = C.hdrs[h].len;
+                ++k;
+                have = true;
             }
         }
-        // line end: \r\n counts once
-        if (j < n && p[j] == '\r' && j + 1 < n && p[j + 1] == '\n') ++j;
-        i = j + 1;
     }
-    if (have) flush();
+    const auto t2 = clk::now();
+    // pass 2: upper-cased content into place
+    run_tasks(T, nt, [&](int64_t t) {
+        Chunk &C = ck[(size_t)t];
+        char *d = C.pre_dst;
+        size_t h = 0;
+        for_lines(p, C.a, C.b, [&](int64_t s, int64_t e) {
+            if (p[s] == '>') {
+                d = C.dst[h++];
+                return;
+            }
+            if (!d) return;
+            upper_copy(d, p + s, e - s);
+            d += e - s;
+        });
+    });
+    if (std::getenv("BWTMI_STATS")) {
+        auto d = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "  load_fasta: read %.1f pass1+stitch %.1f pass2 %.1f ms (%d threads, %lld chunks)\n",
+                     d(t0, t1), d(t1, t2), d(t2, clk::now()), nt, (long long)T);
+    }
 }
 
 }  // namespace bwtmi

@@ -340,7 +340,7 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     // histogram -> alphabet, totals, C (bwt.py:129-134, 276-286)
     c.slot[S_COUNTS].ensure(256 * 8);
     HIPCHECK(hipMemsetAsync(c.slot[S_COUNTS].p, 0, 256 * 8, st));
-    if (n) hipLaunchKernelGGL(k_hist_bytes, dim3(1024), dim3(256), 0, st, T, n, c.slot[S_COUNTS].as<unsigned long long>());
+    if (n) KLAUNCH("k_hist_bytes", 0.0, k_hist_bytes, dim3(1024), dim3(256), 0, st, T, n, c.slot[S_COUNTS].as<unsigned long long>());
     unsigned long long h[256];
     HIPCHECK(hipMemcpyAsync(h, c.slot[S_COUNTS].p, sizeof h, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
@@ -387,27 +387,25 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     uint32_t *U2 = c.slot[S_MISC2].as<uint32_t>();
     uint32_t *SA = ix->sa.as<uint32_t>();
     HIPCHECK(hipMemcpyAsync(c.slot[S_MISC3].p, code, 256, hipMemcpyHostToDevice, st));
-    c.kbegin("sa_init_keys", (double)n * (1.0 + 12.0));   // text in, (key, value) out
-    hipLaunchKernelGGL(k_init_keys, dim3(blocks(n)), dim3(256), 0, st, T, n, c.slot[S_MISC3].as<uint8_t>(), b, k, keys,
+    KLAUNCH("sa_init_keys", (double)n * (1.0 + 12.0), k_init_keys, dim3(blocks(n)), dim3(256), 0, st, T, n, c.slot[S_MISC3].as<uint8_t>(), b, k, keys,
                        vals);
-    c.kend();
     radix_sort_pairs32(c, keys, vals, n, 0, ((b * k + 7) / 8) * 8);
     HIPCHECK(hipMemcpyAsync(SA, vals, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
     auto group_ids = [&](int64_t m) {   // head -> gid (group index), uses flag as scratch
         exclusive_scan<uint32_t>(c, head, flag, m);
-        hipLaunchKernelGGL(k_gid, dim3(blocks(m)), dim3(256), 0, st, flag, head, m, gid);
+        KLAUNCH("k_gid", 0.0, k_gid, dim3(blocks(m)), dim3(256), 0, st, flag, head, m, gid);
     };
-    hipLaunchKernelGGL(k_heads, dim3(blocks(n)), dim3(256), 0, st, keys, n, head);
+    KLAUNCH("k_heads", 0.0, k_heads, dim3(blocks(n)), dim3(256), 0, st, keys, n, head);
     group_ids(n);
-    hipLaunchKernelGGL(k_rank0, dim3(blocks(n)), dim3(256), 0, st, head, gid, SA, n, gstart, rank, flag, 0);
-    hipLaunchKernelGGL(k_rank0, dim3(blocks(n)), dim3(256), 0, st, head, gid, SA, n, gstart, rank, flag, 1);
+    KLAUNCH("k_rank0", 0.0, k_rank0, dim3(blocks(n)), dim3(256), 0, st, head, gid, SA, n, gstart, rank, flag, 0);
+    KLAUNCH("k_rank0", 0.0, k_rank0, dim3(blocks(n)), dim3(256), 0, st, head, gid, SA, n, gstart, rank, flag, 1);
     // U = SA slots in groups of size >= 2
     auto compact = [&](int64_t m, const uint32_t *src, uint32_t *dst) -> int64_t {
         exclusive_scan<uint32_t>(c, flag, head, m);   // head reused as positions
         uint32_t lastp = 0, lastf = 0;
         HIPCHECK(hipMemcpyAsync(&lastp, head + m - 1, 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipMemcpyAsync(&lastf, flag + m - 1, 4, hipMemcpyDeviceToHost, st));
-        hipLaunchKernelGGL(k_compact_idx, dim3(blocks(m)), dim3(256), 0, st, flag, head, m, dst, src);
+        KLAUNCH("k_compact_idx", 0.0, k_compact_idx, dim3(blocks(m)), dim3(256), 0, st, flag, head, m, dst, src);
         HIPCHECK(hipStreamSynchronize(st));
         return (int64_t)lastp + lastf;
     };
@@ -416,13 +414,13 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     while ((1ll << nb) <= n) ++nb;   // rank + 1 <= n fits in nb bits
     int64_t hlen = k;
     while (m > 0) {
-        hipLaunchKernelGGL(k_round_keys, dim3(blocks(m)), dim3(256), 0, st, U, m, SA, rank, n, hlen, nb, keys, vals);
+        KLAUNCH("k_round_keys", 0.0, k_round_keys, dim3(blocks(m)), dim3(256), 0, st, U, m, SA, rank, n, hlen, nb, keys, vals);
         radix_sort_pairs32(c, keys, vals, m, 0, ((2 * nb + 7) / 8) * 8);
-        hipLaunchKernelGGL(k_heads, dim3(blocks(m)), dim3(256), 0, st, keys, m, head);
+        KLAUNCH("k_heads", 0.0, k_heads, dim3(blocks(m)), dim3(256), 0, st, keys, m, head);
         group_ids(m);
-        hipLaunchKernelGGL(k_round_apply, dim3(blocks(m)), dim3(256), 0, st, U, m, vals, head, gid, SA, gstart, 0,
+        KLAUNCH("k_round_apply", 0.0, k_round_apply, dim3(blocks(m)), dim3(256), 0, st, U, m, vals, head, gid, SA, gstart, 0,
                            rank, flag);
-        hipLaunchKernelGGL(k_round_apply, dim3(blocks(m)), dim3(256), 0, st, U, m, vals, head, gid, SA, gstart, 1,
+        KLAUNCH("k_round_apply", 0.0, k_round_apply, dim3(blocks(m)), dim3(256), 0, st, U, m, vals, head, gid, SA, gstart, 1,
                            rank, flag);
         m = compact(m, U, U2);
         std::swap(U, U2);
@@ -434,32 +432,28 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     // ------------------------------------------------------------ BWT, Occ, sampled SA
     ix->bwt.ensure((size_t)n + 128);
     HIPCHECK(hipMemsetAsync(ix->bwt.p, 0, (size_t)n + 128, st));
-    c.kbegin("bwt_gather", (double)n * (4.0 + 1.0 + 1.0));   // SA in, text gather, BWT out
-    hipLaunchKernelGGL(k_bwt, dim3(blocks(n)), dim3(256), 0, st, T, SA, n, ix->bwt.as<uint8_t>());
-    c.kend();
+    KLAUNCH("bwt_gather", (double)n * (4.0 + 1.0 + 1.0), k_bwt, dim3(blocks(n)), dim3(256), 0, st, T, SA, n, ix->bwt.as<uint8_t>());
     const int64_t nblk = (n + occ_sample - 1) / occ_sample;
     ix->occ_len = 1 + n / occ_sample + (n % occ_sample != 0);   // == nblk + 1
     ix->occ.ensure((size_t)sigma * (nblk + 1) * 4);
     HIPCHECK(hipMemsetAsync(ix->occ.p, 0, (size_t)sigma * (nblk + 1) * 4, st));
     HIPCHECK(hipMemcpyAsync(c.slot[S_MISC3].p, present, 256, hipMemcpyHostToDevice, st));
-    c.kbegin("occ_blocks", (double)n + (double)sigma * (double)(nblk + 1) * 4.0);
-    hipLaunchKernelGGL(k_occ_blocks, dim3(blocks(nblk * 64)), dim3(256), 0, st, ix->bwt.as<uint8_t>(), n, nblk,
+    KLAUNCH("occ_blocks", (double)n + (double)sigma * (double)(nblk + 1) * 4.0, k_occ_blocks, dim3(blocks(nblk * 64)), dim3(256), 0, st, ix->bwt.as<uint8_t>(), n, nblk,
                        occ_sample, c.slot[S_MISC3].as<uint8_t>(), sigma, ix->occ.as<uint32_t>());
-    c.kend();
     for (int cc = 0; cc < sigma; ++cc) {
         uint32_t *row = ix->occ.as<uint32_t>() + (int64_t)cc * (nblk + 1);
         exclusive_scan<uint32_t>(c, row, row, nblk + 1);
     }
     ix->sampled_len = (n + sa_sample - 1) / sa_sample;
     ix->sampled.ensure((size_t)ix->sampled_len * 4 + 4);
-    hipLaunchKernelGGL(k_sample, dim3(blocks(ix->sampled_len)), dim3(256), 0, st, SA, n, sa_sample,
+    KLAUNCH("k_sample", 0.0, k_sample, dim3(blocks(ix->sampled_len)), dim3(256), 0, st, SA, n, sa_sample,
                        ix->sampled.as<int32_t>(), ix->sampled_len);
 
     // ------------------------------------------------------------ 8-mer hash
     const int K = 8;
     if (!(flags & BWTMI_INDEX_NO_KMER) && n >= K) {
         ix->has_kmer = true;
-        hipLaunchKernelGGL(k_kvalid, dim3(blocks(n)), dim3(256), 0, st, T, n, flag);
+        KLAUNCH("k_kvalid", 0.0, k_kvalid, dim3(blocks(n)), dim3(256), 0, st, T, n, flag);
         exclusive_scan<uint32_t>(c, flag, head, n);   // head = vpos
         uint32_t vk = 0, vkf = 0, vlast = 0, vlastf = 0;
         HIPCHECK(hipMemcpyAsync(&vk, head + K - 1, 4, hipMemcpyDeviceToHost, st));
@@ -472,15 +466,15 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
         const int first = valid_first == K ? 1 : 0;
         const int64_t nent = first + (nvalid - valid_first);
         uint8_t *V = (uint8_t *)gid;   // reuse: nvalid bytes <= 4n
-        hipLaunchKernelGGL(k_kcompact, dim3(blocks(n)), dim3(256), 0, st, T, n, head, V);
+        KLAUNCH("k_kcompact", 0.0, k_kcompact, dim3(blocks(n)), dim3(256), 0, st, T, n, head, V);
         ix->kmer_pos.ensure((size_t)std::max<int64_t>(nent, 1) * 4);
         if (nent > 0) {
-            hipLaunchKernelGGL(k_kentries, dim3(blocks(n)), dim3(256), 0, st, T, n, K, head, V, first, keys,
+            KLAUNCH("k_kentries", 0.0, k_kentries, dim3(blocks(n)), dim3(256), 0, st, T, n, K, head, V, first, keys,
                                ix->kmer_pos.as<uint32_t>(), (uint32_t)valid_first);
             radix_sort_pairs32(c, keys, ix->kmer_pos.as<uint32_t>(), nent, 0, 16);
         }
         ix->kmer_off.ensure((size_t)(65537) * 8);
-        hipLaunchKernelGGL(k_kbounds, dim3(blocks(nent + 1)), dim3(256), 0, st, keys, nent,
+        KLAUNCH("k_kbounds", 0.0, k_kbounds, dim3(blocks(nent + 1)), dim3(256), 0, st, keys, nent,
                            ix->kmer_off.as<int64_t>());
         ix->kmer_count = nent;
     }
@@ -567,19 +561,19 @@ const int32_t *index_lcp_device(Ctx &c, DeviceIndex *ix) {
     uint32_t *isa = c.slot[S_MISC0].as<uint32_t>();
     int32_t *lcp = c.slot[S_MISC1].as<int32_t>();
     HIPCHECK(hipMemsetAsync(lcp, 0, (size_t)n * 4, st));
-    hipLaunchKernelGGL(k_isa, dim3(blocks(n)), dim3(256), 0, st, ix->sa.as<uint32_t>(), n, isa);
+    KLAUNCH("k_isa", 0.0, k_isa, dim3(blocks(n)), dim3(256), 0, st, ix->sa.as<uint32_t>(), n, isa);
     uint32_t sa0 = 0;
     HIPCHECK(hipMemcpyAsync(&sa0, ix->sa.p, 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     if ((int64_t)sa0 == n - 1) {
         const int64_t chunk = 64;
         const int64_t nch = (n + chunk - 1) / chunk;
-        hipLaunchKernelGGL(k_kasai, dim3(blocks(nch)), dim3(256), 0, st, ix->text.as<uint8_t>(),
+        KLAUNCH("k_kasai", 0.0, k_kasai, dim3(blocks(nch)), dim3(256), 0, st, ix->text.as<uint8_t>(),
                            ix->sa.as<uint32_t>(), isa, n, chunk, lcp);
     } else {
         // the smallest suffix is not the last one (no unique final sentinel):
         // Kasai's h then carries over the skipped rank-0 step, so replay it serially
-        hipLaunchKernelGGL(k_kasai_serial, dim3(1), dim3(64), 0, st, ix->text.as<uint8_t>(), ix->sa.as<uint32_t>(),
+        KLAUNCH("k_kasai_serial", 0.0, k_kasai_serial, dim3(1), dim3(64), 0, st, ix->text.as<uint8_t>(), ix->sa.as<uint32_t>(),
                            isa, n, lcp);
     }
     HIPCHECK(hipGetLastError());
@@ -603,7 +597,7 @@ void index_sa_rows(Ctx &c, const DeviceIndex *ix, const int64_t *rows, int64_t k
     c.slot[S_MISC0].ensure((size_t)k * 8);
     c.slot[S_MISC1].ensure((size_t)k * 8);
     HIPCHECK(hipMemcpyAsync(c.slot[S_MISC0].p, rows, (size_t)k * 8, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_sa_rows, dim3(blocks(k)), dim3(256), 0, st, ix->sa.as<uint32_t>(),
+    KLAUNCH("k_sa_rows", 0.0, k_sa_rows, dim3(blocks(k)), dim3(256), 0, st, ix->sa.as<uint32_t>(),
                        c.slot[S_MISC0].as<int64_t>(), k, c.slot[S_MISC1].as<int64_t>());
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipMemcpyAsync(out, c.slot[S_MISC1].p, (size_t)k * 8, hipMemcpyDeviceToHost, st));
@@ -634,7 +628,7 @@ void index_backward_search(Ctx &c, DeviceIndex *ix, const uint8_t *pats, const i
     f.n = ix->n;
     f.olen = index_occ_len(ix);
     f.k = ix->occ_sample;
-    hipLaunchKernelGGL(k_bsearch, dim3(blocks(npat)), dim3(256), 0, st, f, c.slot[S_MISC0].as<uint8_t>(),
+    KLAUNCH("k_bsearch", 0.0, k_bsearch, dim3(blocks(npat)), dim3(256), 0, st, f, c.slot[S_MISC0].as<uint8_t>(),
                        c.slot[S_MISC1].as<int64_t>(), npat, c.slot[S_MISC2].as<int64_t>());
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipMemcpyAsync(sp_ep, c.slot[S_MISC2].p, (size_t)npat * 16, hipMemcpyDeviceToHost, st));

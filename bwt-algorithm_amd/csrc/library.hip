@@ -591,7 +591,7 @@ void lcp_plateaus_device(Ctx &c, DeviceIndex *ix, const LibParams &p, std::vecto
     c.slot[S_COUNTS].ensure(64);
     int *d_max = c.slot[S_COUNTS].as<int>();
     HIPCHECK(hipMemsetAsync(d_max, 0, 4, st));
-    hipLaunchKernelGGL(k_max_i32, dim3((unsigned)std::min<int64_t>(1024, blocks(n))), dim3(kB), 0, st, lcp, n, d_max);
+    KLAUNCH("k_max_i32", 0.0, k_max_i32, dim3((unsigned)std::min<int64_t>(1024, blocks(n))), dim3(kB), 0, st, lcp, n, d_max);
     int lmax = 0;
     HIPCHECK(hipMemcpyAsync(&lmax, d_max, 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
@@ -603,7 +603,7 @@ void lcp_plateaus_device(Ctx &c, DeviceIndex *ix, const LibParams &p, std::vecto
     c.slot[S_IDX4].ensure((size_t)(n + 1) * 4);
     uint32_t *inrun = c.slot[S_IDX1].as<uint32_t>(), *head = c.slot[S_IDX2].as<uint32_t>();
     uint32_t *hscan = c.slot[S_IDX3].as<uint32_t>(), *cpos = c.slot[S_IDX4].as<uint32_t>();
-    hipLaunchKernelGGL(k_plateau_flags, dim3(blocks(n)), dim3(kB), 0, st, lcp, n, (int32_t)thr, inrun, head);
+    KLAUNCH("k_plateau_flags", 0.0, k_plateau_flags, dim3(blocks(n)), dim3(kB), 0, st, lcp, n, (int32_t)thr, inrun, head);
     HIPCHECK(hipMemsetAsync(inrun + n, 0, 4, st));
     HIPCHECK(hipMemsetAsync(head + n, 0, 4, st));
     exclusive_scan<uint32_t>(c, head, hscan, n + 1);
@@ -621,12 +621,12 @@ void lcp_plateaus_device(Ctx &c, DeviceIndex *ix, const LibParams &p, std::vecto
     uint64_t *keys = c.slot[S_IDX0].as<uint64_t>();
     int64_t *copies = c.slot[S_IDX5].as<int64_t>();
     uint32_t *flag = c.slot[S_IDX6].as<uint32_t>(), *pos = c.slot[S_IDX7].as<uint32_t>();
-    hipLaunchKernelGGL(k_plateau_keys, dim3(blocks(n)), dim3(kB), 0, st, index_sa_device(ix), inrun, head, hscan, cpos,
+    KLAUNCH("k_plateau_keys", 0.0, k_plateau_keys, dim3(blocks(n)), dim3(kB), 0, st, index_sa_device(ix), inrun, head, hscan, cpos,
                        n, keys);
     int rb = 0;
     while (rb < 32 && ((uint64_t)runs >> rb)) ++rb;
     radix_sort_pairs32(c, keys, nullptr, m, 0, ((32 + rb + 7) / 8) * 8);
-    hipLaunchKernelGGL(k_plateau_eval, dim3(blocks(m)), dim3(kB), 0, st, keys, m, index_text_device(ix), n, thr,
+    KLAUNCH("k_plateau_eval", 0.0, k_plateau_eval, dim3(blocks(m)), dim3(kB), 0, st, keys, m, index_text_device(ix), n, thr,
                        (int64_t)p.min_copies, flag, copies);
     HIPCHECK(hipMemsetAsync(flag + m, 0, 4, st));
     exclusive_scan<uint32_t>(c, flag, pos, m + 1);
@@ -635,7 +635,7 @@ void lcp_plateaus_device(Ctx &c, DeviceIndex *ix, const LibParams &p, std::vecto
     HIPCHECK(hipStreamSynchronize(st));
     if (k32 == 0) return;
     c.slot[S_MISC2].ensure((size_t)k32 * 24);
-    hipLaunchKernelGGL(k_plateau_out, dim3(blocks(m)), dim3(kB), 0, st, keys, flag, pos, copies, m, thr,
+    KLAUNCH("k_plateau_out", 0.0, k_plateau_out, dim3(blocks(m)), dim3(kB), 0, st, keys, flag, pos, copies, m, thr,
                        c.slot[S_MISC2].as<int64_t>());
     HIPCHECK(hipGetLastError());
     out.resize((size_t)k32 * 3);
@@ -656,7 +656,7 @@ void tier1_device(Ctx &c, const uint8_t *d_text, const uint8_t *t, int64_t n, in
     HIPCHECK(hipMemsetAsync(seen, 0, (size_t)n, st));
     std::vector<int64_t> cand, ranges;
     for (int L = std::min(max_motif_length, 9); L >= 1; --L) {   // longest unit first (bwt.py:1451)
-        hipLaunchKernelGGL(k_t1_flags, dim3(blocks(n)), dim3(kB), 0, st, d_text, n, L, seen, flag);
+        KLAUNCH("k_t1_flags", 0.0, k_t1_flags, dim3(blocks(n)), dim3(kB), 0, st, d_text, n, L, seen, flag);
         HIPCHECK(hipMemsetAsync(flag + n, 0, 4, st));
         exclusive_scan<uint32_t>(c, flag, pos, n + 1);
         uint32_t m = 0;
@@ -664,7 +664,7 @@ void tier1_device(Ctx &c, const uint8_t *d_text, const uint8_t *t, int64_t n, in
         HIPCHECK(hipStreamSynchronize(st));
         if (m == 0) continue;
         c.slot[S_MISC3].ensure((size_t)m * 8);
-        hipLaunchKernelGGL(k_t1_compact, dim3(blocks(n)), dim3(kB), 0, st, flag, pos, n, c.slot[S_MISC3].as<int64_t>());
+        KLAUNCH("k_t1_compact", 0.0, k_t1_compact, dim3(blocks(n)), dim3(kB), 0, st, flag, pos, n, c.slot[S_MISC3].as<int64_t>());
         HIPCHECK(hipGetLastError());
         cand.resize(m);
         HIPCHECK(hipMemcpyAsync(cand.data(), c.slot[S_MISC3].p, (size_t)m * 8, hipMemcpyDeviceToHost, st));
@@ -708,7 +708,7 @@ void tier1_device(Ctx &c, const uint8_t *d_text, const uint8_t *t, int64_t n, in
         const int64_t nr = (int64_t)ranges.size() / 2;
         c.slot[S_MISC3].ensure(ranges.size() * 8);
         HIPCHECK(hipMemcpyAsync(c.slot[S_MISC3].p, ranges.data(), ranges.size() * 8, hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(k_t1_mark, dim3(blocks(nr)), dim3(kB), 0, st, c.slot[S_MISC3].as<int64_t>(), nr, seen);
+        KLAUNCH("k_t1_mark", 0.0, k_t1_mark, dim3(blocks(nr)), dim3(kB), 0, st, c.slot[S_MISC3].as<int64_t>(), nr, seen);
         HIPCHECK(hipGetLastError());
         HIPCHECK(hipStreamSynchronize(st));
     }
@@ -731,7 +731,7 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
     c.slot[S_IDX1].ensure((size_t)tot * 4);
     c.slot[S_IDX2].ensure((size_t)tot * 4);
     c.slot[S_IDX3].ensure((size_t)tot);
-    hipLaunchKernelGGL(k_extend, dim3(blocks(tot)), dim3(kB), 0, st, index_text_device(ix), n, Lmax,
+    KLAUNCH("k_extend", 0.0, k_extend, dim3(blocks(tot)), dim3(kB), 0, st, index_text_device(ix), n, Lmax,
                        c.slot[S_IDX0].as<int32_t>(), c.slot[S_IDX1].as<int32_t>(), c.slot[S_IDX2].as<int32_t>(),
                        c.slot[S_IDX3].as<uint8_t>());
     HIPCHECK(hipGetLastError());
@@ -918,7 +918,7 @@ void tier3_device(Ctx &c, DeviceIndex *ix, const uint8_t *reads, const int64_t *
     c.slot[S_IDX2].ensure((size_t)nwin * 4);
     HIPCHECK(hipMemcpyAsync(c.slot[S_IDX0].p, reads, (size_t)rbytes, hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemcpyAsync(c.slot[S_IDX1].p, wpos.data(), (size_t)nwin * 8, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_t3_windows, dim3((unsigned)((nwin + 3) / 4)), dim3(256), 0, st, c.slot[S_IDX0].as<uint8_t>(),
+    KLAUNCH("k_t3_windows", 0.0, k_t3_windows, dim3((unsigned)((nwin + 3) / 4)), dim3(256), 0, st, c.slot[S_IDX0].as<uint8_t>(),
                        c.slot[S_IDX1].as<int64_t>(), nwin, c.slot[S_IDX2].as<int32_t>());
     HIPCHECK(hipGetLastError());
     std::vector<int32_t> best((size_t)nwin);
@@ -1234,7 +1234,7 @@ void simple_scan_device(Ctx &c, DeviceIndex *ix, const LibParams &P, const std::
         c.slot[S_IDX3].ensure((size_t)nr);
         HIPCHECK(hipMemcpyAsync(c.slot[S_IDX0].p, t, (size_t)nt, hipMemcpyHostToDevice, st));
         HIPCHECK(hipMemcpyAsync(c.slot[S_IDX1].p, req.data(), (size_t)nr * 16, hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(k_simple_extend, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, st,
+        KLAUNCH("k_simple_extend", 0.0, k_simple_extend, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, st,
                            c.slot[S_IDX0].as<uint8_t>(), n, c.slot[S_IDX1].as<int64_t>(), nr,
                            c.slot[S_IDX2].as<int64_t>(), c.slot[S_IDX3].as<uint8_t>());
         HIPCHECK(hipGetLastError());

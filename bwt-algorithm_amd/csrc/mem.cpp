@@ -29,6 +29,13 @@ Cache &cache() {
     return *c;
 }
 
+void (*g_unmap_hook)(void *, size_t) = nullptr;
+
+void unmap_block(void *p, size_t size) {
+    if (g_unmap_hook) g_unmap_hook(p, size);
+    munmap(p, size);
+}
+
 void *map_block(size_t size) {
     // over-map by 2 MiB and trim to a 2 MiB-aligned block so that every huge
     // page of it can be backed by a transparent huge page
@@ -79,7 +86,7 @@ void big_free(void *p, size_t bytes) noexcept {
     c.cached += sz;
     while (c.cached > kCacheCap && !c.free_.empty()) {   // drop the largest cached blocks first
         auto last = std::prev(c.free_.end());
-        munmap(last->second, last->first);
+        unmap_block(last->second, last->first);
         c.cached -= last->first;
         c.free_.erase(last);
     }
@@ -94,9 +101,22 @@ size_t big_cached_bytes() {
 void big_trim() {
     Cache &c = cache();
     std::lock_guard<std::mutex> lk(c.mu);
-    for (auto &kv : c.free_) munmap(kv.second, kv.first);
+    for (auto &kv : c.free_) unmap_block(kv.second, kv.first);
     c.free_.clear();
     c.cached = 0;
+}
+
+size_t big_block_size(const void *p) {
+    Cache &c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.live.find(const_cast<void *>(p));
+    return it == c.live.end() ? 0 : it->second;
+}
+
+void big_set_unmap_hook(void (*hook)(void *, size_t)) {
+    Cache &c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    g_unmap_hook = hook;
 }
 
 namespace {

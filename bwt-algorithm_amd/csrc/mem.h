@@ -23,6 +23,11 @@ void *big_alloc(size_t bytes);             // throws std::bad_alloc
 void big_free(void *p, size_t bytes) noexcept;
 size_t big_cached_bytes();                 // bytes held in the cache (tests / stats)
 void big_trim();                           // unmap every cached block
+// mapped size of the live block that starts at p (0 if p is not a block start)
+size_t big_block_size(const void *p);
+// called (under the cache lock) before a block is unmapped; the device layer
+// uses it to drop its DMA registration of blocks it pinned (api.cpp)
+void big_set_unmap_hook(void (*hook)(void *p, size_t bytes));
 
 // Runs fn on a background thread, in submission order: releasing a step's
 // large record sets overlaps the next step's device phase instead of

@@ -157,13 +157,13 @@ __global__ __launch_bounds__(kB) void k_tile_scan_max(const int64_t *__restrict_
 void prefix_max(Ctx &c, const int64_t *in, int64_t *out, int64_t n, int64_t *tmp) {
     const int64_t nt = (n + kTile - 1) / kTile;
     if (nt == 1) {
-        hipLaunchKernelGGL(k_tile_scan_max, dim3(1), dim3(kB), 0, c.stream, in, out, (const int64_t *)nullptr, n);
+        KLAUNCH("k_tile_scan_max", 0.0, k_tile_scan_max, dim3(1), dim3(kB), 0, c.stream, in, out, (const int64_t *)nullptr, n);
         return;
     }
     int64_t *tm = tmp;
-    hipLaunchKernelGGL(k_tile_max, dim3((unsigned)nt), dim3(kB), 0, c.stream, in, tm, n);
+    KLAUNCH("k_tile_max", 0.0, k_tile_max, dim3((unsigned)nt), dim3(kB), 0, c.stream, in, tm, n);
     prefix_max(c, tm, tm, nt, tmp + nt);   // inclusive max over tiles
-    hipLaunchKernelGGL(k_tile_scan_max, dim3((unsigned)nt), dim3(kB), 0, c.stream, in, out, (const int64_t *)tm, n);
+    KLAUNCH("k_tile_scan_max", 0.0, k_tile_scan_max, dim3((unsigned)nt), dim3(kB), 0, c.stream, in, out, (const int64_t *)tm, n);
 }
 
 // position buckets: B[b] = first rank k with S[k] >= b << kBucketShift (n if
@@ -333,7 +333,7 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
 
     // longest span -> key widths
     HIPCHECK(hipMemsetAsync(d_max, 0, 8, st));
-    hipLaunchKernelGGL(k_maxlen, dim3((unsigned)std::min<int64_t>(1024, blocks(n))), dim3(kB), 0, st, d_hits, n, d_max);
+    KLAUNCH("k_maxlen", 0.0, k_maxlen, dim3((unsigned)std::min<int64_t>(1024, blocks(n))), dim3(kB), 0, st, d_hits, n, d_max);
     unsigned long long maxlen = 0;
     HIPCHECK(hipMemcpyAsync(&maxlen, d_max, 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
@@ -342,46 +342,40 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     if (lb + mb > 64) fail(BWTMI_E_ARG, "span too long for the screen keys");
     auto round8 = [](int b) { return ((b + 7) / 8) * 8; };
 
-    c.kbegin("screen_sort", 0.0);
-    hipLaunchKernelGGL(k_keys, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, mb, (int64_t)lmax, kpos, vpos, kgrp, vgrp);
+    KLAUNCH("k_keys", 0.0, k_keys, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, mb, (int64_t)lmax, kpos, vpos, kgrp, vgrp);
     radix_sort_pairs32(c, kpos, vpos, n, 0, round8(lb + mb));
-    hipLaunchKernelGGL(k_keys_start, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, kpos);
+    KLAUNCH("k_keys_start", 0.0, k_keys_start, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, kpos);
     radix_sort_pairs32(c, kpos, vpos, n, 0, round8(std::max(1, bits_for((uint64_t)text_len))));   // start < text_len
     radix_sort_pairs32(c, kgrp, vgrp, n, 0, round8(mb));
-    hipLaunchKernelGGL(k_gather, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, S, E, M, rank_of, kept);
+    KLAUNCH("k_gather", 0.0, k_gather, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, S, E, M, rank_of, kept);
     prefix_max(c, E, PME, n, c.slot[S_IDX5].as<int64_t>());
     uint32_t *B = c.slot[S_IDX6].as<uint32_t>();
-    hipLaunchKernelGGL(k_buckets, dim3(blocks(nb)), dim3(kB), 0, st, S, n, nb, B);
+    KLAUNCH("k_buckets", 0.0, k_buckets, dim3(blocks(nb)), dim3(kB), 0, st, S, n, nb, B);
     int64_t *first = reinterpret_cast<int64_t *>(d_max);
     HIPCHECK(hipMemsetAsync(first, 0xff, (size_t)(lmax + 2) * 8, st));
-    hipLaunchKernelGGL(k_bounds, dim3(blocks(n)), dim3(kB), 0, st, kgrp, n, first);
-    c.kend();
+    KLAUNCH("k_bounds", 0.0, k_bounds, dim3(blocks(n)), dim3(kB), 0, st, kgrp, n, first);
     std::vector<int64_t> fh((size_t)lmax + 2);
     HIPCHECK(hipMemcpyAsync(fh.data(), first, fh.size() * 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipStreamSynchronize(st));
 
     // levels in descending m (ascending group key)
-    c.kbegin("screen_levels", 0.0);
     std::vector<std::pair<int64_t, int64_t>> lv;   // (first, group key)
     for (int64_t g = 0; g <= lmax; ++g)
         if (fh[(size_t)g] >= 0) lv.push_back({fh[(size_t)g], g});
     for (size_t q = 0; q < lv.size(); ++q) {
         const int64_t a = lv[q].first, b = q + 1 < lv.size() ? lv[q + 1].first : n;
         if (b - a <= kWaveLevelMax)   // few hits (long motifs, long walks): a wave per hit
-            hipLaunchKernelGGL(k_level_wave, dim3(blocks((b - a) * 64)), dim3(kB), 0, st, vgrp + a, b - a, d_hits,
+            KLAUNCH("k_level_wave", 0.0, k_level_wave, dim3(blocks((b - a) * 64)), dim3(kB), 0, st, vgrp + a, b - a, d_hits,
                                rank_of, S, E, M, PME, B, kept, n, 0.5);
         else
-            hipLaunchKernelGGL(k_level, dim3(blocks(b - a)), dim3(kB), 0, st, vgrp + a, b - a, d_hits, rank_of, S, E,
+            KLAUNCH("k_level", 0.0, k_level, dim3(blocks(b - a)), dim3(kB), 0, st, vgrp + a, b - a, d_hits, rank_of, S, E,
                                M, PME, B, kept, n, 0.5);
     }
-    c.kend();
-    c.kbegin("screen_compact", 0.0);
-    hipLaunchKernelGGL(k_final_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, kept, n, flag);
+    KLAUNCH("k_final_flags", 0.0, k_final_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, kept, n, flag);
     HIPCHECK(hipMemsetAsync(flag + n, 0, 4, st));
     exclusive_scan<uint32_t>(c, flag, pos, n + 1);
-    hipLaunchKernelGGL(k_final_compact, dim3(blocks(n)), dim3(kB), 0, st, d_hits, vpos, flag, pos, n, dout);
-    c.kend();
+    KLAUNCH("k_final_compact", 0.0, k_final_compact, dim3(blocks(n)), dim3(kB), 0, st, d_hits, vpos, flag, pos, n, dout);
     HIPCHECK(hipGetLastError());
     uint32_t nk = 0;
     HIPCHECK(hipMemcpyAsync(&nk, pos + n, 4, hipMemcpyDeviceToHost, st));

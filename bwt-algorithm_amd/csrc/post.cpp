@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
+#include <exception>
 #include <functional>
 #include <memory>
 #include <string>
@@ -33,15 +34,54 @@
 #include <type_traits>
 #include <vector>
 
+#include <sched.h>
+
 #include "common.h"
 
 namespace bwtmi {
 
+// CPUs this process may use: the affinity mask, capped by a cgroup CPU quota
+static int cpus_visible() {
+    int n = 0;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) n = (int)std::max(1u, std::thread::hardware_concurrency());
+    long q = -1, per = -1;
+    if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {   // cgroup v2: "max 100000" or "Q P"
+        char a[32] = {0};
+        long b = 0;
+        if (std::fscanf(f, "%31s %ld", a, &b) == 2 && std::strcmp(a, "max") != 0) {
+            q = std::atol(a);
+            per = b;
+        }
+        std::fclose(f);
+    } else if (FILE *g = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {   // cgroup v1
+        if (std::fscanf(g, "%ld", &q) != 1) q = -1;
+        std::fclose(g);
+        if (FILE *h = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+            if (std::fscanf(h, "%ld", &per) != 1) per = -1;
+            std::fclose(h);
+        }
+    }
+    if (q > 0 && per > 0) n = std::min<int>(n, (int)std::max<long>(1, (q + per - 1) / per));
+    return n;
+}
+
+int host_cpu_budget(int *visible, int *local_world) {
+    static const int vis = cpus_visible();
+    static const int lw = [] {
+        const char *e = std::getenv("LOCAL_WORLD_SIZE");
+        const int v = e ? std::atoi(e) : 1;
+        return v > 0 ? v : 1;
+    }();
+    if (visible) *visible = vis;
+    if (local_world) *local_world = lw;
+    return std::max(1, std::min(16, vis / lw));   // 16 measured fastest per rank
+}
+
 int host_threads(const bwtmi_params &p) {
     if (p.threads > 0) return p.threads;
-    unsigned hc = std::thread::hardware_concurrency();
-    int t = hc ? (int)hc : 4;
-    return std::min(t, 16);
+    return host_cpu_budget(nullptr, nullptr);
 }
 
 // Persistent worker pool: parallel regions reuse the same threads (and their
@@ -67,15 +107,27 @@ public:
             job = &f;
             want = nt - 1;
             pending = nt - 1;
+            err = nullptr;
             ++gen;
         }
         cv.notify_all();
         in_worker = true;
-        f(0);
+        try {
+            f(0);
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!err) err = std::current_exception();
+        }
         in_worker = false;
+        // every worker finishes before f (and what it references) goes out of scope
         std::unique_lock<std::mutex> lk(mu);
         done.wait(lk, [&] { return pending == 0; });
         job = nullptr;
+        if (err) {
+            std::exception_ptr e = err;
+            err = nullptr;
+            std::rethrow_exception(e);
+        }
     }
     ~Pool() {
         {
@@ -112,7 +164,12 @@ private:
                 if (id >= want) continue;
                 f = job;
             }
-            (*f)(id + 1);
+            try {
+                (*f)(id + 1);
+            } catch (...) {   // reported to the caller of run(); never escapes the thread
+                std::lock_guard<std::mutex> lk(mu);
+                if (!err) err = std::current_exception();
+            }
             std::lock_guard<std::mutex> lk(mu);
             if (--pending == 0) done.notify_one();
         }
@@ -121,6 +178,7 @@ private:
     std::mutex mu, region_mu;
     std::condition_variable cv, done;
     const std::function<void(int)> *job = nullptr;
+    std::exception_ptr err;
     int want = 0, pending = 0;
     int64_t gen = 0;
     bool stop = false;
@@ -216,6 +274,28 @@ void Job::assign_units() {
         }
         contigs[order[k]].unit = nunits - 1;   // unit ids are ranks by natural key
     }
+}
+
+std::vector<int32_t> shard_units(Job &job, int32_t world, int32_t rank) {
+    job.assign_units();
+    std::vector<int64_t> w((size_t)job.nunits, 0);
+    for (auto &c : job.contigs) w[(size_t)c.unit] += c.weight;
+    std::vector<int32_t> order((size_t)job.nunits);
+    for (int32_t u = 0; u < job.nunits; ++u) order[(size_t)u] = u;
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return w[(size_t)a] > w[(size_t)b]; });
+    std::vector<int64_t> load((size_t)std::max(1, world), 0);
+    std::vector<int32_t> owner((size_t)job.nunits, 0);
+    for (int32_t u : order) {
+        int32_t r = 0;
+        for (int32_t x = 1; x < world; ++x)
+            if (load[(size_t)x] < load[(size_t)r]) r = x;
+        load[(size_t)r] += w[(size_t)u];
+        owner[(size_t)u] = r;
+    }
+    std::vector<int32_t> out;
+    for (size_t c = 0; c < job.contigs.size(); ++c)
+        if (owner[(size_t)job.contigs[c].unit] == rank) out.push_back((int32_t)c);
+    return out;
 }
 
 namespace {

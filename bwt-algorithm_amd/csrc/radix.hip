@@ -256,16 +256,13 @@ void radix_sort_cfg(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int bi
     uint32_t *cnt = c.slot[S_SORT_HIST].as<uint32_t>();
     int passes = 0;
     for (int sh = bit0; sh < bit1; sh += 8) {
-        c.kbegin("radix_hist", (double)n * 8.0);                       // read keys once
-        hipLaunchKernelGGL(k_hist<kT / kBlock>, dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream, ka, cnt, n, sh, ntiles);
-        c.kend();
+        // read the keys once
+        KLAUNCH("radix_hist", (double)n * 8.0, k_hist<kT / kBlock>, dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream, ka, cnt, n, sh, ntiles);
         exclusive_scan<uint32_t>(c, cnt, cnt, ntiles * 256);
         // read (key, value) once, write it once
-        c.kbegin(sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16",
-                 (double)n * 2.0 * (8.0 + (vals ? (double)sizeof(V) : 0.0)));
-        hipLaunchKernelGGL((k_scatter<V, BLOCK, ITEMS, NT, SPLIT>), dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, ka, va,
-                           kb, vb, cnt, n, sh, ntiles);
-        c.kend();
+        KLAUNCH(sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16",
+                (double)n * 2.0 * (8.0 + (vals ? (double)sizeof(V) : 0.0)), (k_scatter<V, BLOCK, ITEMS, NT, SPLIT>),
+                dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, ka, va, kb, vb, cnt, n, sh, ntiles);
         std::swap(ka, kb);
         std::swap(va, vb);
         ++passes;
@@ -297,13 +294,13 @@ template <class T>
 static void scan_rec(Ctx &c, const T *in, T *out, int64_t n, T *tmp) {
     const int64_t nch = (n + kTile - 1) / kTile;
     if (nch == 1) {
-        hipLaunchKernelGGL(k_chunk_scan<T>, dim3(1), dim3(kBlock), 0, c.stream, in, out, (const T *)nullptr, n);
+        KLAUNCH("k_chunk_scan", 0.0, k_chunk_scan<T>, dim3(1), dim3(kBlock), 0, c.stream, in, out, (const T *)nullptr, n);
         return;
     }
     T *sums = tmp;
-    hipLaunchKernelGGL(k_chunk_sums<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, sums, n);
+    KLAUNCH("k_chunk_sums", 0.0, k_chunk_sums<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, sums, n);
     scan_rec<T>(c, sums, sums, nch, tmp + nch);
-    hipLaunchKernelGGL(k_chunk_scan<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, out, (const T *)sums, n);
+    KLAUNCH("k_chunk_scan", 0.0, k_chunk_scan<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, out, (const T *)sums, n);
 }
 
 template <class T>

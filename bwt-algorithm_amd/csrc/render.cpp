@@ -62,7 +62,7 @@ Rec kmer_piece(int32_t chrom, int64_t start, int64_t end, const std::string &mot
 
 // _simple_kmer_scan(chrom, start, end, k=3, use_full_seq=True)
 void kmer_scan(const Job &job, int32_t chrom, int64_t start, int64_t end, RecVec &out) {
-    const std::string &seq = job.contigs[(size_t)chrom].full;
+    const Seq &seq = job.contigs[(size_t)chrom].full;
     const int64_t L = (int64_t)seq.size();
     const int64_t k = 3;
     if (seq.empty() || start >= end || start < 0 || end > L) return;
@@ -139,7 +139,7 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
             if (C.first < 0) C.first = r.chrom;
             else if (r.chrom != C.first) C.mixed = true;
             if (r.motif.size() != 3) continue;
-            const std::string &full = job.contigs[(size_t)r.chrom].full;
+            const Seq &full = job.contigs[(size_t)r.chrom].full;
             if (full.empty()) continue;
             const int64_t a = r.end, b = std::min<int64_t>((int64_t)full.size(), r.end + 50);
             if (a >= b) continue;
@@ -374,7 +374,7 @@ void comp_entropy(const Rec &r, double comp[4], double &ent) {
 
 void row_strfinder(Out &o, const Job &job, const Rec &r, const Rec *partner) {
     const Contig &c = job.contigs[(size_t)r.chrom];
-    const std::string &full = c.full;
+    const Seq &full = c.full;
     const int64_t FL = (int64_t)full.size();
     View fl, fr;
     if (!full.empty()) {   // full[max(0,start-30):start], full[end:end+30]

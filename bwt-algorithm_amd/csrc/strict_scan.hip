@@ -420,7 +420,7 @@ void launch_runs(Ctx &c, const uint32_t *P, int64_t n, int32_t lmin, int32_t lma
     const int64_t groups = (int64_t)(lmax >> 5) - (int64_t)(lmin >> 5) + 1;
     const int32_t gper = 8;   // unit-length groups per workgroup (32 L each)
     const int64_t gblocks = (groups + gper - 1) / gper;
-    hipLaunchKernelGGL((k_runs<B>), dim3((unsigned)tiles, (unsigned)gblocks), dim3(256), 0, c.stream, P, n, nwords32,
+    KLAUNCH("k_runs", 0.0, (k_runs<B>), dim3((unsigned)tiles, (unsigned)gblocks), dim3(256), 0, c.stream, P, n, nwords32,
                        lmin, lmax, mc, gper, out);
 }
 
@@ -451,7 +451,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
         c.slot[S_MISC1].ensure((size_t)tot * sizeof(bwtmi_hit));
         c.slot[S_MISC2].ensure((size_t)nL * sizeof(int64_t));
         HIPCHECK(hipMemcpyAsync(c.slot[S_MISC0].p, off.data(), off.size() * 8, hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(k_mc1, dim3((unsigned)((nL + 63) / 64)), dim3(64), 0, st, d_text, n, lmin, lmax,
+        KLAUNCH("k_mc1", 0.0, k_mc1, dim3((unsigned)((nL + 63) / 64)), dim3(64), 0, st, d_text, n, lmin, lmax,
                            c.slot[S_MISC0].as<int64_t>(), c.slot[S_MISC1].as<bwtmi_hit>(),
                            c.slot[S_MISC2].as<int64_t>());
         HIPCHECK(hipGetLastError());
@@ -470,7 +470,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
             w += np[(size_t)row];
         }
         if (nh > 0)
-            hipLaunchKernelGGL(k_period, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st, d_text,
+            KLAUNCH("k_period", 0.0, k_period, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st, d_text,
                                c.slot[S_HITS].as<bwtmi_hit>(), nh);
         HIPCHECK(hipGetLastError());
         res.raw = nh;
@@ -490,7 +490,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     // 1. alphabet -> code width
     c.slot[S_COUNTS].ensure(256 * sizeof(unsigned long long));
     HIPCHECK(hipMemsetAsync(c.slot[S_COUNTS].p, 0, 256 * sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(k_hist256, dim3(1024), dim3(256), 0, st, d_text, n, c.slot[S_COUNTS].as<unsigned long long>());
+    KLAUNCH("k_hist256", 0.0, k_hist256, dim3(1024), dim3(256), 0, st, d_text, n, c.slot[S_COUNTS].as<unsigned long long>());
     unsigned long long hist[256];
     HIPCHECK(hipMemcpyAsync(hist, c.slot[S_COUNTS].p, sizeof hist, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
@@ -506,10 +506,10 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     uint32_t *P = c.slot[S_PACK].as<uint32_t>();
     HIPCHECK(hipMemsetAsync(P, 0, (size_t)nwords * B * sizeof(uint32_t), st));
     const unsigned pgrid = (unsigned)((nwords + 255) / 256);
-    if (B == 1) hipLaunchKernelGGL(k_pack<1>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
-    else if (B == 2) hipLaunchKernelGGL(k_pack<2>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
-    else if (B == 4) hipLaunchKernelGGL(k_pack<4>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
-    else hipLaunchKernelGGL(k_pack<8>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
+    if (B == 1) KLAUNCH("k_pack", 0.0, k_pack<1>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
+    else if (B == 2) KLAUNCH("k_pack", 0.0, k_pack<2>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
+    else if (B == 4) KLAUNCH("k_pack", 0.0, k_pack<4>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
+    else KLAUNCH("k_pack", 0.0, k_pack<8>, dim3(pgrid), dim3(256), 0, st, d_text, n, d_code, P, nwords - 8);
     HIPCHECK(hipGetLastError());
 
     // 2. candidate runs (segmented output, compacted below)
@@ -530,13 +530,10 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
             HIPCHECK(hipEventCreate(&kb));
             HIPCHECK(hipEventRecord(ka, st));
         }
-        // compulsory traffic: the packed text once (0.25 B/base at 2 bits)
-        c.kbegin("k_runs", (double)n * (double)B / 8.0);
         if (B == 1) launch_runs<1>(c, P, n, lmin, lmax, min_copies, co);
         else if (B == 2) launch_runs<2>(c, P, n, lmin, lmax, min_copies, co);
         else if (B == 4) launch_runs<4>(c, P, n, lmin, lmax, min_copies, co);
         else launch_runs<8>(c, P, n, lmin, lmax, min_copies, co);
-        c.kend();
         HIPCHECK(hipGetLastError());
         if (c.timing) HIPCHECK(hipEventRecord(kb, st));
         HIPCHECK(hipMemcpyAsync(segn, d_count, sizeof segn, hipMemcpyDeviceToHost, st));
@@ -571,7 +568,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
         c.slot[S_CAND_K].ensure((size_t)ncand * sizeof(uint64_t));
         c.slot[S_CAND_V].ensure((size_t)ncand * sizeof(uint64_t));
         HIPCHECK(hipMemcpyAsync(d_off, off, sizeof off, hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(k_cand_gather, dim3((unsigned)((mx + 255) / 256), kCandSegs), dim3(256), 0, st,
+        KLAUNCH("k_cand_gather", 0.0, k_cand_gather, dim3((unsigned)((mx + 255) / 256), kCandSegs), dim3(256), 0, st,
                            c.slot[S_CAND_K2].as<uint64_t>(), c.slot[S_CAND_V2].as<uint64_t>(), d_count, d_off,
                            seg_cap, c.slot[S_CAND_K].as<uint64_t>(), c.slot[S_CAND_V].as<uint64_t>());
         HIPCHECK(hipGetLastError());
@@ -592,7 +589,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     c.slot[S_FLAG].ensure((size_t)nc * sizeof(uint32_t));
     c.slot[S_SCAN].ensure((size_t)(nc + 1) * sizeof(uint32_t));
     const unsigned g = (unsigned)((nc + 255) / 256);
-    hipLaunchKernelGGL(k_resolve, dim3(g), dim3(256), 0, st, c.slot[S_CAND_K].as<uint64_t>(),
+    KLAUNCH("k_resolve", 0.0, k_resolve, dim3(g), dim3(256), 0, st, c.slot[S_CAND_K].as<uint64_t>(),
                        c.slot[S_CAND_V].as<uint64_t>(), nc, lmax, (int64_t)min_copies, c.slot[S_MISC0].as<int64_t>(),
                        c.slot[S_MISC1].as<int64_t>(), c.slot[S_FLAG].as<uint32_t>());
     HIPCHECK(hipMemsetAsync(c.slot[S_SCAN].as<uint32_t>() + nc, 0, sizeof(uint32_t), st));
@@ -603,7 +600,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     HIPCHECK(hipStreamSynchronize(st));
     const int64_t nh = (int64_t)last_pos + last_flag;
     c.slot[S_HITS].ensure((size_t)std::max<int64_t>(nh, 1) * sizeof(bwtmi_hit));
-    hipLaunchKernelGGL(k_compact, dim3(g), dim3(256), 0, st, c.slot[S_CAND_K].as<uint64_t>(), nc, lmax,
+    KLAUNCH("k_compact", 0.0, k_compact, dim3(g), dim3(256), 0, st, c.slot[S_CAND_K].as<uint64_t>(), nc, lmax,
                        c.slot[S_MISC0].as<int64_t>(), c.slot[S_MISC1].as<int64_t>(), c.slot[S_FLAG].as<uint32_t>(),
                        c.slot[S_SCAN].as<uint32_t>(), d_text, c.slot[S_HITS].as<bwtmi_hit>());
     HIPCHECK(hipGetLastError());

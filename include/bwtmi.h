@@ -230,6 +230,33 @@ int bwtmi_job_import(bwtmi_job *job, const uint8_t *buf, int64_t len);
 /* per-stage wall times (ms) of the last scan/postprocess/render calls */
 int bwtmi_job_stage_ms(const bwtmi_job *job, double *out8);
 
+/* Shard layout over ranks (replaces the Pool over contigs, bwt.py:3850-3912):
+ * fold units (contigs with equal natural sort keys, bwt.py:22-36) go to ranks
+ * by longest-processing-time greedy over their analysed lengths (ties: lower
+ * unit, then lower rank).  Restricts the job to rank's contigs; ids (may be
+ * NULL, else room for every contig) receives them ascending, n their count. */
+int bwtmi_job_select_shard(bwtmi_job *job, int32_t world, int32_t rank, int32_t *ids, int32_t *n);
+
+/* host CPUs this process may use (affinity mask, cgroup quota), the ranks on
+ * this node (LOCAL_WORLD_SIZE) and the post-processing threads per rank that
+ * follow from them (threads = 0 in bwtmi_params) */
+int bwtmi_host_info(int32_t *cpus_visible, int32_t *local_world, int32_t *threads);
+
+/* ------------------------------------------------------------ collective
+ * The multi-GPU path's only exchange: RCCL (over xGMI) all-reduce of small
+ * host vectors -- per-unit row / byte counts for the sharded output file and
+ * the step time.  librccl is loaded on first use.  The 128-byte id comes from
+ * bwtmi_comm_unique_id on one rank and reaches the others out of band
+ * (bwtmi/comm.py: a TCP rendezvous next to MASTER_ADDR:MASTER_PORT). */
+typedef struct bwtmi_comm bwtmi_comm;
+int bwtmi_comm_unique_id(uint8_t *id /* 128 bytes */);
+int bwtmi_comm_init(int32_t device, int32_t world, int32_t rank, const uint8_t *id, bwtmi_comm **out);
+/* in place over `count` host values; dtype 0 = int64, 1 = float64; op 0 = sum, 1 = max */
+int bwtmi_comm_allreduce(bwtmi_comm *comm, void *vals, int64_t count, int32_t dtype, int32_t op);
+int bwtmi_comm_free(bwtmi_comm *comm);
+/* hipDeviceSynchronize on device (bench step brackets) */
+int bwtmi_device_sync(int32_t device);
+
 /* ------------------------------------------------------------ helpers
  * MotifUtils.align_repeat_region (bwt.py:998-1102) -- the banded per-copy
  * alignment used by merge/refine; exposed for the Python MotifUtils mirror.
@@ -248,7 +275,16 @@ int bwtmi_align_region(const char *seq, int64_t seq_len, int64_t start, int64_t 
  * blank lines skipped, duplicate names overwrite in place.  Registers every
  * contig in job (trim = flank_trim if len > 2*flank_trim). */
 int bwtmi_job_load_fasta(bwtmi_job *job, const char *path, int32_t flank_trim);
+/* the same for rank `rank` of `world` processes: every contig is registered
+ * (names and analysed lengths, for the shard layout), but only the fold units
+ * this rank owns (bwtmi_job_select_shard) get their bases, and the job is
+ * restricted to them */
+int bwtmi_job_load_fasta_shard(bwtmi_job *job, const char *path, int32_t flank_trim, int32_t world,
+                               int32_t rank);
 int32_t bwtmi_job_contig_count(const bwtmi_job *job);
+/* analysed length of contig id (its shard weight), also for contigs whose bases
+ * live on another rank */
+int64_t bwtmi_job_contig_weight(const bwtmi_job *job, int32_t id);
 int64_t bwtmi_job_contig_info(const bwtmi_job *job, int32_t id, char *name, int64_t cap,
                               int64_t *full_len, int64_t *trim_left, int64_t *trim_right);
 int bwtmi_job_contig_seq(const bwtmi_job *job, int32_t id, uint8_t *dst /* full_len */);

@@ -213,28 +213,31 @@ def test_device_screen_matches_host(gpu_ctx, case):
         assert d == h, (case, fmt)
 
 
-def test_full_size_goldens(gpu_ctx, golden_dir, tmp_path):
-    """BASELINE configs at full size (C2 1 Mbp --tier1, C4 8x12.5 Mbp, C3 100 Mbp
-    --progress when generated) against repeat.tab hashes of the reference
-    pipeline (tests/golden/make_goldens.py hybrid; strict scan and nested
-    suppression restated, everything else the reference's own code)."""
-    from bwtmi import TandemRepeatFinder, synth
-    with open(os.path.join(golden_dir, "expected_large.json")) as f:
-        man = json.load(f)
-    for name, g in sorted(man.items()):
-        fa = str(tmp_path / f"{name}.fa")
-        assert synth.write_fasta(fa, g["lengths"], g["sub_rate"]) == g["fasta_sha256"], name
-        args = g["args"]
-        mml = int(args[args.index("--max-motif-len") + 1]) if "--max-motif-len" in args else 9
-        f = TandemRepeatFinder(fa, show_progress="--progress" in args, max_motif_length=mml)
-        f.load_reference()
-        reps = f.find_tandem_repeats_parallel(True, "--tier1" not in args, False, None)
-        out = tmp_path / f"{name}.tab"
-        f.save_results(reps, str(out), "strfinder")
-        data = out.read_bytes()
-        assert data.count(b"\n") - 1 == g["out_rows"], name
-        assert hashlib.sha256(data).hexdigest() == g["out_sha256"], name
-        os.unlink(fa)
+def _large_goldens():
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "expected_large.json")
+    with open(here) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name", sorted(_large_goldens()))
+def test_full_size_goldens(gpu_ctx, golden_dir, tmp_path, name):
+    """BASELINE configs at full size -- C2 (1 Mbp --tier1), C3 (100 Mbp
+    --progress), C4 (8 x 12.5 Mbp), C5 (100 Mbp with 0.02 substitutions inside
+    the planted arrays, --progress, default and --no-mismatches arms) -- run
+    through the drop-in CLI (`bwt.py IN.fa -o OUT --jobs -1 ARGS`, bwt.py:4201-4370)
+    against repeat.tab hashes of the reference pipeline
+    (tests/golden/make_goldens.py hybrid; strict scan and nested suppression
+    restated, everything else the reference's own code)."""
+    from bwtmi import cli, synth
+    g = _large_goldens()[name]
+    fa = str(tmp_path / f"{name}.fa")
+    assert synth.write_fasta(fa, g["lengths"], g["sub_rate"]) == g["fasta_sha256"], name
+    out = tmp_path / f"{name}.tab"
+    assert cli.main([fa, "-o", str(out), "--jobs", "-1"] + list(g["args"])) == 0
+    data = out.read_bytes()
+    assert data.count(b"\n") - 1 == g["out_rows"], name
+    assert hashlib.sha256(data).hexdigest() == g["out_sha256"], name
+    os.unlink(fa)
 
 
 # ------------------------------------------------------------------ FM index

@@ -84,6 +84,76 @@ def test_native_loader_matches_reference_loader(golden_dir):
             assert tl == offs[nm] and j.contig_seq(cid)[tl:fl - tr].decode() == seqs[nm]
 
 
+def _messy_fasta(seed: int) -> bytes:
+    """A multi-MB FASTA whose lines end in \\n, \\r\\n or \\r, with blank and
+    whitespace-padded lines, lower case, text before the first header, repeated
+    names, empty contigs and lines far longer than one loader chunk."""
+    r = np.random.default_rng(seed)
+    eols = [b"\n", b"\r\n", b"\r"]
+    out = bytearray(b"acgt orphan line before any header\n\n")
+    names = [f"chr{k}".encode() for k in range(12)] + [b"chr3", b"scaffold_7", b"chr3"]
+    for i, nm in enumerate(names):
+        out += b"  >" + nm + b" description " + str(i).encode() + eols[int(r.integers(3))]
+        if i % 7 == 5:
+            continue                                           # empty contig
+        total = int(r.integers(1, 600_000))
+        width = int(r.choice([60, 61, 80, 1, 3_000_000]))
+        seq = bytes(b"ACGTNacgtn"[k] for k in r.integers(0, 10, total))
+        for a in range(0, total, width):
+            pad = b" \t" if r.random() < 0.05 else b""
+            out += pad + seq[a:a + width] + pad + eols[int(r.integers(3))]
+            if r.random() < 0.02:
+                out += b"   " + eols[int(r.integers(3))]
+    return bytes(out)
+
+
+@pytest.mark.parametrize("threads", [1, 3, 16])
+def test_parallel_loader_matches_reference_semantics(tmp_path, threads):
+    """The chunked two-pass loader (fasta.cpp) against the line-by-line
+    restatement of load_reference (bwt.py:3713-3756) on a messy multi-chunk
+    file, for several thread counts (chunk layouts); and the sharded load
+    registers every contig but holds only this rank's bases."""
+    from bwtmi import dist
+    from bwtmi.records import Job
+    path = str(tmp_path / "messy.fa")
+    with open(path, "wb") as f:
+        f.write(_messy_fasta(threads))
+    seqs, full, offs = post.load_fasta(path, 30)
+    j = Job(threads=threads)
+    j.load_fasta(path, 30)
+    assert j.names == list(seqs)
+    for cid, nm in enumerate(j.names):
+        _, fl, tl, tr = j.contig_info(cid)
+        assert j.contig_seq(cid).decode() == full[nm], nm
+        assert tl == offs[nm] and j.contig_seq(cid)[tl:fl - tr].decode() == seqs[nm]
+        assert j.contig_weight(cid) == len(seqs[nm])
+    weights = [len(seqs[nm]) for nm in j.names]
+    for world in (2, 3):
+        parts = dist.assign(dist.natural_units(j.names), weights, world)
+        for rank in range(world):
+            s = Job(threads=threads)
+            s.load_fasta(path, 30, world, rank)
+            assert s.names == j.names and s.select_shard(world, rank) == parts[rank]
+            for cid in range(s.contig_count()):
+                own = cid in parts[rank]
+                assert s.contig_seq(cid) == (j.contig_seq(cid) if own else b"")
+                assert s.contig_weight(cid) == weights[cid]
+
+
+def test_reload_replaces_content(tmp_path):
+    """Loading a file again into the same job refreshes every contig (the bench
+    re-reads its FASTA each step); a repeated name keeps its first slot."""
+    from bwtmi.records import Job
+    a, b = tmp_path / "a.fa", tmp_path / "b.fa"
+    a.write_text(">x\nACGT\n>y\nGGGG\n")
+    b.write_text(">y\nTTTTTT\n>x\nCC\n")
+    j = Job()
+    j.load_fasta(str(a), 0)
+    j.load_fasta(str(b), 0)
+    assert j.names == ["x", "y"]
+    assert j.contig_seq(0) == b"CC" and j.contig_seq(1) == b"TTTTTT"
+
+
 def test_native_postprocess_and_writers_match_goldens(golden_dir, built_lib):
     for name, m, d in _cases(golden_dir):
         j = _native_job(os.path.join(golden_dir, "inputs", m["input"]), d)
@@ -191,9 +261,9 @@ def _dist_worker(rank, world, port, fa, outdir):
     for p in (os.path.join(here, ".."), os.path.join(here, "..", "bwt-algorithm_amd")):
         sys.path.insert(0, os.path.abspath(p))
     import oracle as orc
-    from bwtmi import dist
+    from bwtmi import comm, dist
     from bwtmi.records import Job
-    td = dist.init("gloo")
+    c = dist.init("host")
     j = Job()
     j.load_fasta(fa, 30)
 
@@ -209,14 +279,29 @@ def _dist_worker(rank, world, port, fa, outdir):
             f.write(j.render("strfinder"))
         with open(os.path.join(outdir, "n.txt"), "w") as f:
             f.write(str(len(recs)))
-    td.barrier()
-    td.destroy_process_group()
+    c.barrier()
+    comm.close()
 
 
-def test_two_rank_gloo_gather_matches_single_process(tmp_path, golden_dir, built_lib):
-    import torch.multiprocessing as mp
+def _spawn(fn, args, nprocs):
+    """One process per rank (spawn: no fork after a HIP context), all must exit 0."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=fn, args=(r,) + tuple(args)) for r in range(nprocs)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(300)
+    codes = [p.exitcode for p in ps]
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * nprocs, codes
+
+
+def test_two_rank_gather_matches_single_process(tmp_path, golden_dir, built_lib):
     fa = os.path.join(golden_dir, "inputs", "test2.fa")
-    mp.spawn(_dist_worker, args=(2, _free_port(), fa, str(tmp_path)), nprocs=2, join=True)
+    _spawn(_dist_worker, (2, _free_port(), fa, str(tmp_path)), 2)
     single = post.run_file(fa, "strfinder").encode()
     assert open(tmp_path / "dist.out", "rb").read() == single
     assert int(open(tmp_path / "n.txt").read()) > 0
@@ -230,32 +315,41 @@ def _sharded_write_worker(rank, world, port, fa, outdir):
     for p in (os.path.join(here, ".."), os.path.join(here, "..", "bwt-algorithm_amd")):
         sys.path.insert(0, os.path.abspath(p))
     import oracle as orc
-    from bwtmi import dist
+    from bwtmi import comm, dist
     from bwtmi.records import Job
-    td = dist.init("gloo")
+    c = dist.init("host")
+    full = Job()
+    full.load_fasta(fa, 30)
+    infos = [full.contig_info(i) for i in range(full.contig_count())]
+    want = dist.assign(dist.natural_units([x[0] for x in infos]), [x[1] - x[2] - x[3] for x in infos],
+                       world)[rank]
     j = Job()
-    j.load_fasta(fa, 30)
-    infos = [j.contig_info(i) for i in range(j.contig_count())]
-    shard = dist.assign(dist.natural_units([x[0] for x in infos]), [x[1] for x in infos], world)[rank]
-    j.select(shard)
+    j.load_fasta(fa, 30, world, rank)          # only this rank's bases are loaded
+    shard = j.select_shard(world, rank)
+    assert shard == want, (shard, want)
+    for cid in range(j.contig_count()):
+        assert j.contig_weight(cid) == infos[cid][1] - infos[cid][2] - infos[cid][3]
+        if cid in shard:
+            assert j.contig_info(cid) == infos[cid] and j.contig_seq(cid) == full.contig_seq(cid)
+        else:
+            assert j.contig_info(cid)[1] == 0
     for cid in shard:
         _, fl, tl, tr = infos[cid]
         seq = j.contig_seq(cid)[tl:fl - tr]
         j.add_hits(cid, orc.strict_scan(seq, 1, max(120, min(len(seq) // 3, 1000)), 0, 3))
     j.postprocess()
     for fmt in ("strfinder", "bed", "vcf", "trf_table", "trf_dat"):
-        dist.write_sharded(td, j, fmt, os.path.join(outdir, f"{fmt}.out"))
-    td.barrier()
-    td.destroy_process_group()
+        dist.write_sharded(c, j, fmt, os.path.join(outdir, f"{fmt}.out"))
+    c.barrier()
+    comm.close()
 
 
 @pytest.mark.parametrize("world,name", [(2, "test_all_12.fa"), (3, "edge_mixed.fa")])
 def test_sharded_write_matches_single_process(tmp_path, golden_dir, built_lib, world, name):
     """Each rank writes its own fold units at exchanged offsets; the file equals
     the single-process output in every format (incl. global VCF row ids)."""
-    import torch.multiprocessing as mp
     fa = os.path.join(golden_dir, "inputs", name)
-    mp.spawn(_sharded_write_worker, args=(world, _free_port(), fa, str(tmp_path)), nprocs=world, join=True)
+    _spawn(_sharded_write_worker, (world, _free_port(), fa, str(tmp_path)), world)
     for fmt in ("strfinder", "bed", "vcf", "trf_table", "trf_dat"):
         assert (tmp_path / f"{fmt}.out").read_text() == post.run_file(fa, fmt), fmt
 
