@@ -356,6 +356,19 @@ struct Pools {
         A.cn += s.size();
         return std::string_view(d, s.size());
     }
+    // motif already lives in static storage, no variations
+    Extra *add_static(int w, const Extra &e, std::string_view motif) {
+        Arena &A = a[(size_t)w];
+        if (A.xb.empty() || A.xn == XB) {
+            A.xb.emplace_back(XB * sizeof(Extra));
+            A.xn = 0;
+        }
+        Extra *x = (Extra *)A.xb.back().p + A.xn++;
+        ::new ((void *)x) Extra(e);
+        x->motif = motif;
+        x->variations = {};
+        return x;
+    }
     Extra *add(int w, const Extra &e, std::string_view motif, std::string_view variations) {
         Arena &A = a[(size_t)w];
         if (A.xb.empty() || A.xn == XB) {
@@ -518,6 +531,23 @@ ItemVec suppress_nested(const ItemVec &rs, double thr, int nt) {
     return kept;
 }
 
+// every byte value as a one-character string (motifs of one-base recomputes)
+const struct ByteChars {
+    char c[256];
+    ByteChars() { for (int i = 0; i < 256; ++i) c[i] = (char)i; }
+    const char &operator[](size_t i) const { return c[i]; }
+} kByteChars;
+
+inline char comp_of(char c) {   // bwt.py:688-691
+    switch (c) {
+        case 'A': return 'T';
+        case 'T': return 'A';
+        case 'C': return 'G';
+        case 'G': return 'C';
+        default: return c;
+    }
+}
+
 std::atomic<int64_t> g_recomputes{0}, g_recompute_ns{0}, g_merges{0}, g_canons{0}, g_tests{0}, g_same{0};
 // BWTMI_STATS=1: stage timers; =2: also per-recompute / per-test counters (slow)
 const bool g_stats = [] { const char *e = std::getenv("BWTMI_STATS"); return e && (*e == '1' || *e == '2'); }();
@@ -548,6 +578,41 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     start = std::max<int64_t>(0, start);
     end = end > 0 ? std::min(L, end) : L;
     if (end <= start) end = std::min(L, start + m);
+    if (m == 1 && start < L) {
+        // One-base motif (~75 % of the recomputes): align_repeat_region's closed
+        // form (motif.cpp) without building any strings.  The template is
+        // seq[start]; the walk is the run of that base up to its limit, first
+        // with min_copies, then (bwt.py:3530-3534) with min_copies 1, which
+        // always succeeds (the run holds the template itself).
+        const char b = seq[start];
+        const int64_t mc = std::max<int64_t>(1, u.min_copies);
+        auto run_to = [&](int64_t limit) {
+            int64_t pos = start;
+            while (pos < limit && seq[pos] == b) ++pos;
+            return pos - start;
+        };
+        int64_t run = run_to(std::min<int64_t>(L, std::max<int64_t>(end, start + mc) + 4));
+        if (run < mc) run = run_to(std::min<int64_t>(L, std::max<int64_t>(end, start + 1) + 4));
+        Extra x;
+        x.copies = (double)run;        // tl / 1 is integral
+        x.confidence = 1.0;            // max(0.3, 1 - 0)
+        x.mm = 0.0;
+        x.n_eval = std::max<int64_t>(1, run);
+        x.max_mm = 0;
+        const char rc = comp_of(b);
+        x.strand = (unsigned char)b <= (unsigned char)rc ? '+' : '-';   // get_canonical_motif_stranded
+        x.pmatch = 100.0;
+        x.pindel = 0.0;
+        x.score = trf_score(run, 0.0);
+        Item it{};
+        it.start = start;
+        it.end = start + run;
+        it.chrom = chrom;
+        it.mlen = 1;
+        it.tier = tier;
+        it.x = pools.add_static(w, x, std::string_view(&kByteChars[(uint8_t)b], 1));
+        return it;
+    }
     auto slice = [&](int64_t a, int64_t b) {   // Python seq[a:b], a,b >= 0
         a = std::min(a, L);
         b = std::min(b, L);
@@ -637,16 +702,6 @@ inline const std::string &canon_get(const UnitCtx &u, const Item &it, Canon &c) 
         c.ok = true;
     }
     return c.s;
-}
-
-inline char comp_of(char c) {   // bwt.py:688-691
-    switch (c) {
-        case 'A': return 'T';
-        case 'T': return 'A';
-        case 'C': return 'G';
-        case 'G': return 'C';
-        default: return c;
-    }
 }
 
 // get_canonical_motif_stranded(m1)[0] == ...(m2)[0] (bwt.py:694-716): the

@@ -371,6 +371,12 @@ __device__ __forceinline__ int32_t smallest_period(const uint8_t *__restrict__ s
     return L;
 }
 
+// hits of unit length up to kThreadPeriodL get their period from one thread
+// (at most kThreadPeriodL - 1 divisor candidates over a few cached bytes);
+// longer units from one wave (k_period_wave): a thread walking a 1000-byte unit
+// byte by byte is a serial chain of loads that held every launch for ~2.6 ms
+constexpr int32_t kThreadPeriodL = 32;
+
 // compaction of the resolved hits, with the smallest period of each hit's
 // first unit and the count after primitive reduction (bwt.py:1956-1961)
 __global__ __launch_bounds__(256) void k_compact(const uint64_t *__restrict__ keys, int64_t nc, int32_t umax,
@@ -384,10 +390,64 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t *__restrict__ ke
     h.start = hit_i[k];
     h.end = hit_i[k] + hit_c[k] * L;
     h.unit_len = (int32_t)L;
+    if (L > kThreadPeriodL) {   // k_period_wave fills prim_len / copies
+        h.prim_len = (int32_t)L;
+        h.copies = hit_c[k];
+        hits[pos[k]] = h;
+        return;
+    }
     const int32_t p = smallest_period(t + h.start, (int32_t)L);
     h.prim_len = p;
     h.copies = p < L ? (h.end - h.start) / p : hit_c[k];
     hits[pos[k]] = h;
+}
+
+// number of candidates with unit length > lthr: a prefix of the (L desc) order
+__global__ void k_count_long(const uint64_t *__restrict__ keys, int64_t nc, int32_t umax, int32_t lthr,
+                             int64_t *__restrict__ out) {
+    if (blockIdx.x || threadIdx.x) return;
+    int64_t lo = 0, hi = nc;   // first k with L(k) <= lthr
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)umax - (int64_t)(keys[mid] >> 40) > lthr) lo = mid + 1;
+        else hi = mid;
+    }
+    *out = lo;
+}
+
+// smallest_period_str (bwt.py:1125-1133) of one long first unit per wave: the
+// lanes mark which of 64 consecutive d divide L (ballot), each divisor in
+// ascending order is tested over the unit 64 bytes at a time (coalesced), the
+// first one without a mismatch is the period
+__global__ __launch_bounds__(256) void k_period_wave(const uint64_t *__restrict__ keys, int64_t nlong, int32_t umax,
+                                                     const int64_t *__restrict__ hit_i, const int64_t *__restrict__ hit_c,
+                                                     const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
+                                                     const uint8_t *__restrict__ t, bwtmi_hit *__restrict__ hits) {
+    const int lane = threadIdx.x & 63;
+    const int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (k >= nlong || !flag[k]) return;   // wave-uniform
+    const int32_t L = (int32_t)((int64_t)umax - (int64_t)(keys[k] >> 40));
+    const uint8_t *s = t + hit_i[k];
+    int32_t p = L;
+    for (int32_t base = 1; base < L && p == L; base += 64) {
+        const int32_t dl = base + lane;
+        uint64_t m = __ballot(dl < L && L % dl == 0);
+        while (m) {
+            const int32_t d = base + (__ffsll((unsigned long long)m) - 1);
+            m &= m - 1;
+            bool ok = true;
+            for (int32_t x0 = d; x0 < L; x0 += 64) {
+                const int32_t x = x0 + lane;
+                if (__any(x < L && s[x] != s[x - d])) { ok = false; break; }
+            }
+            if (ok) { p = d; break; }
+        }
+    }
+    if (lane == 0) {
+        bwtmi_hit &h = hits[pos[k]];
+        h.prim_len = p;
+        h.copies = p < L ? (h.end - h.start) / p : hit_c[k];
+    }
 }
 
 // smallest_period_str of text[i : i+L] (bwt.py:1125-1133), then
@@ -516,7 +576,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     int64_t seg_cap = std::max<int64_t>(1 << 12, n / 8 / kCandSegs + 1024);
     unsigned long long segn[kCandSegs] = {0};
     unsigned long long ncand = 0;
-    c.slot[S_MISC3].ensure(kCandSegs * (sizeof(unsigned long long) + sizeof(int64_t)));
+    c.slot[S_MISC3].ensure(kCandSegs * (sizeof(unsigned long long) + sizeof(int64_t)) + 64);
     unsigned long long *d_count = c.slot[S_MISC3].as<unsigned long long>();
     int64_t *d_off = reinterpret_cast<int64_t *>(d_count + kCandSegs);
     for (int attempt = 0;; ++attempt) {
@@ -595,14 +655,24 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     HIPCHECK(hipMemsetAsync(c.slot[S_SCAN].as<uint32_t>() + nc, 0, sizeof(uint32_t), st));
     exclusive_scan<uint32_t>(c, c.slot[S_FLAG].as<uint32_t>(), c.slot[S_SCAN].as<uint32_t>(), nc);
     uint32_t last_pos = 0, last_flag = 0;
+    int64_t nlong = 0;
+    int64_t *d_nlong = d_off + kCandSegs;   // after the segment offsets
+    KLAUNCH("k_count_long", 0.0, k_count_long, dim3(1), dim3(64), 0, st, c.slot[S_CAND_K].as<uint64_t>(), nc, lmax,
+            kThreadPeriodL, d_nlong);
     HIPCHECK(hipMemcpyAsync(&last_pos, c.slot[S_SCAN].as<uint32_t>() + nc - 1, 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(&last_flag, c.slot[S_FLAG].as<uint32_t>() + nc - 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(&nlong, d_nlong, 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     const int64_t nh = (int64_t)last_pos + last_flag;
     c.slot[S_HITS].ensure((size_t)std::max<int64_t>(nh, 1) * sizeof(bwtmi_hit));
     KLAUNCH("k_compact", 0.0, k_compact, dim3(g), dim3(256), 0, st, c.slot[S_CAND_K].as<uint64_t>(), nc, lmax,
                        c.slot[S_MISC0].as<int64_t>(), c.slot[S_MISC1].as<int64_t>(), c.slot[S_FLAG].as<uint32_t>(),
                        c.slot[S_SCAN].as<uint32_t>(), d_text, c.slot[S_HITS].as<bwtmi_hit>());
+    if (nlong > 0)
+        KLAUNCH("k_period_wave", 0.0, k_period_wave, dim3((unsigned)((nlong * 64 + 255) / 256)), dim3(256), 0, st,
+                c.slot[S_CAND_K].as<uint64_t>(), nlong, lmax, c.slot[S_MISC0].as<int64_t>(),
+                c.slot[S_MISC1].as<int64_t>(), c.slot[S_FLAG].as<uint32_t>(), c.slot[S_SCAN].as<uint32_t>(), d_text,
+                c.slot[S_HITS].as<bwtmi_hit>());
     HIPCHECK(hipGetLastError());
     res.raw = nh;
     if (screen) {
