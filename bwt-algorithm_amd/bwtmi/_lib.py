@@ -117,6 +117,9 @@ _SIGS = {
     "bwtmi_comm_allreduce": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32]),
     "bwtmi_comm_free": (C.c_int, [_P]),
     "bwtmi_device_sync": (C.c_int, [C.c_int32]),
+    "bwtmi_job_set_records": (C.c_int, [_P, _P, C.c_int64]),
+    "bwtmi_wire_record_size": (C.c_int, []),
+    "bwtmi_job_contig_error": (C.c_int64, [_P, C.c_int32, C.c_char_p, C.c_int64]),
 }
 EXPORTED = tuple(_SIGS)
 

@@ -97,9 +97,18 @@ class TandemRepeatFinder:
         if dist.is_distributed():
             return dist.run_sharded(self, job)
         job.scan(_lib.ctx(self.device))
+        self._report_errors(job)
         job.postprocess()
         job.wait(_lib.ctx(self.device))     # the worker's FM index build ran behind post-processing
         return job.records()
+
+    @staticmethod
+    def _report_errors(job) -> None:
+        """The worker's failure convention (bwt.py:3137-3141): a contig whose
+        device work failed is reported and contributes no records."""
+        for cid, msg in job.contig_errors().items():
+            print(f"ERROR processing chromosome {job.names[cid]}: {msg}")
+            print(f"bwtmi: contig {job.names[cid]!r} failed on the device: {msg}", file=sys.stderr)
 
     def _tier3(self, job, long_reads) -> None:
         """Tier 3 (bwt.py:3917-3924, parallel mode only): every built index
@@ -130,6 +139,7 @@ class TandemRepeatFinder:
         job.set_tier2(enable_tier2)
         job.select_shard(c.world, c.rank)
         job.scan(_lib.ctx(self.device))
+        self._report_errors(job)
         job.postprocess()
         total = int(c.allreduce(np.array([job.count()], dtype=np.int64))[0])
         dist.write_sharded(c, job, format_type, output_file)
@@ -156,8 +166,14 @@ class TandemRepeatFinder:
         if isinstance(repeats, RepeatList):
             repeats.job.write(format_type, output_file)
             return
-        if not repeats:
-            empty = self._new_job()
-            empty.write(format_type, output_file)
-            return
-        raise TypeError("save_results renders the records returned by find_tandem_repeats*")
+        # any other list of records (e.g. a filtered RepeatList): rendered by a
+        # job holding the same contigs, without touching this finder's records
+        job = self._new_job()
+        if repeats:
+            if not self.full_sequences:
+                self.load_reference()
+            for name, full in self.full_sequences.items():
+                t = self.trim_offsets.get(name, 0)
+                job.add_contig(name, full.encode("latin-1"), t, t)
+            job.set_records(list(repeats), self.full_sequences)
+        job.write(format_type, output_file)

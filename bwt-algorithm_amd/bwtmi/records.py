@@ -247,6 +247,56 @@ class Job:
         finally:
             lib().bwtmi_free(p)
 
+    def contig_errors(self) -> Dict[int, str]:
+        """{contig id: message} of the contigs whose worker failed in the last scan."""
+        out = {}
+        for i in range(self.contig_count()):
+            n = lib().bwtmi_job_contig_error(self.h, i, None, 0)
+            if n > 0:
+                buf = C.create_string_buffer(n + 1)
+                lib().bwtmi_job_contig_error(self.h, i, buf, n + 1)
+                out[i] = buf.value.decode(errors="replace")
+        return out
+
+    def set_records(self, repeats: Sequence["TandemRepeat"], full_sequences: Dict[str, str]) -> None:
+        """Replace the final records by caller-provided TandemRepeat objects
+        (save_results over a plain list, bwt.py:4141-4198).  actual_sequence
+        must be None or the slice full_sequence[start:end] of its contig."""
+        import struct
+        ids = {}
+        for i, nm in enumerate(self.names):
+            ids.setdefault(nm, i)
+        hdr = struct.Struct("<ii8q5d5b3xii")
+        if hdr.size != lib().bwtmi_wire_record_size():
+            raise RuntimeError("record wire format mismatch with libbwtmi")
+        parts = [struct.pack("<q", len(repeats))]
+        for r in repeats:
+            if r.chrom not in ids:
+                raise KeyError(f"record for unknown chromosome {r.chrom!r}")
+            if r.consensus_motif not in (None, r.motif):
+                raise ValueError("records whose consensus_motif differs from motif are not supported")
+            kind, off, ln = 0, 0, 0
+            if r.actual_sequence is not None:
+                full = full_sequences[r.chrom]
+                if full[r.start:r.end] != r.actual_sequence:
+                    raise ValueError("actual_sequence must be the slice [start:end) of the contig")
+                kind, off, ln = 2, max(0, min(r.start, len(full))), len(r.actual_sequence)
+            comp = r.composition
+            stats_none = comp is None and r.entropy == 0.0
+            kmer = comp is not None and all(v == 0 for v in comp.values()) and r.entropy == 1.5
+            motif = r.motif.encode("latin-1")
+            var = ";".join(r.variations).encode("latin-1") if r.variations else b""
+            parts.append(hdr.pack(ids[r.chrom], int(r.tier), int(r.start), int(r.end), int(r.length),
+                                  int(r.max_mismatches_per_copy), int(r.n_copies_evaluated), int(r.score), off, ln,
+                                  float(r.copies), float(r.confidence), float(r.mismatch_rate),
+                                  float(r.percent_matches), float(r.percent_indels), kind, ord(r.strand[:1] or "+"),
+                                  0, int(kmer), int(stats_none), len(motif), len(var)))
+            parts.append(motif)
+            parts.append(var)
+        blob = b"".join(parts)
+        buf = C.create_string_buffer(blob, len(blob))
+        check(lib().bwtmi_job_set_records(self.h, buf, len(blob)))
+
     def import_records(self, blob: bytes) -> None:
         buf = C.create_string_buffer(blob, len(blob))
         check(lib().bwtmi_job_import(self.h, buf, len(blob)))

@@ -647,6 +647,8 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
         J.screened.assign(J.contigs.size(), 0);
         J.shits.assign(J.contigs.size(), {});
         J.raw_n.assign(J.contigs.size(), 0);
+        J.errors.assign(J.contigs.size(), std::string());
+        const char *fail_contig = std::getenv("BWTMI_FAIL_CONTIG");   // test hook: this contig's worker fails
         // nested suppression + sort + dedup on the device (BWTMI_HOST_SCREEN=1: on the host)
         const char *hs = std::getenv("BWTMI_HOST_SCREEN");
         const bool screen = !(hs && *hs == '1');
@@ -666,8 +668,22 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
             // a contig with Tier 3 records is screened on the host, together with them
             const bool t3 = i < J.t3.size() && !J.t3[i].empty();
             ScanResult r;
-            strict_scan_device(c, job->dev.seqs[i].buf.as<uint8_t>(), len, 1, (int32_t)std::min<int64_t>(U, INT32_MAX),
-                               P.min_copies, r, screen && !t3 && len < (int64_t)UINT32_MAX);   // 32-bit hit lengths
+            // a failing contig yields no records and an error message, the others go on
+            // (the worker's `except Exception: print(...); return []`, bwt.py:3137-3141)
+            try {
+                if (fail_contig && ct.name == fail_contig) fail(BWTMI_E_STATE, "injected failure (BWTMI_FAIL_CONTIG)");
+                strict_scan_device(c, job->dev.seqs[i].buf.as<uint8_t>(), len, 1,
+                                   (int32_t)std::min<int64_t>(U, INT32_MAX), P.min_copies, r,
+                                   screen && !t3 && len < (int64_t)UINT32_MAX);   // 32-bit hit lengths
+            } catch (const Error &) {
+                J.errors[i] = g_err;
+                (void)hipGetLastError();
+                (void)hipStreamSynchronize(c.stream);
+                continue;
+            } catch (const std::bad_alloc &) {
+                J.errors[i] = "out of host memory";
+                continue;
+            }
             J.hits[i].swap(r.hits);   // Rule 1 (bwt.py:3118-3130) never fires on strict hits
             J.shits[i].swap(r.shits);
             J.screened[i] = r.screened ? 1 : 0;
@@ -946,43 +962,72 @@ int bwtmi_job_export(bwtmi_job *job, uint8_t **buf, int64_t *len) {
     });
 }
 
-int bwtmi_job_import(bwtmi_job *job, const uint8_t *buf, int64_t len) {
-    return guard([&] {
-        CHECK_ARG(job && buf && len >= 8, "bad argument");
-        int64_t n;
-        std::memcpy(&n, buf, 8);
-        int64_t o = 8;
-        for (int64_t k = 0; k < n; ++k) {
-            CHECK_ARG(o + (int64_t)sizeof(WireRec) <= len, "truncated record buffer");
-            WireRec w;
-            std::memcpy(&w, buf + o, sizeof w);
-            o += sizeof w;
-            CHECK_ARG(o + w.motif_len + w.var_len <= len, "truncated record strings");
-            CHECK_ARG(w.chrom >= 0 && w.chrom < (int32_t)job->j.contigs.size(), "record for unknown contig");
-            Rec r;
-            r.chrom = w.chrom; r.tier = w.tier; r.start = w.start; r.end = w.end; r.length = w.length;
-            r.max_mm = w.max_mm; r.n_eval = w.n_eval; r.score = w.score; r.act_off = w.act_off; r.act_len = w.act_len;
-            r.copies = w.copies; r.confidence = w.confidence; r.mismatch_rate = w.mismatch_rate;
-            r.pmatch = w.pmatch; r.pindel = w.pindel; r.act_kind = w.act_kind; r.strand = (char)w.strand;
-            r.is_compound = w.is_compound; r.kmer_stats = w.kmer_stats; r.stats_none = w.stats_none;
-            r.motif.assign((const char *)buf + o, (size_t)w.motif_len);
-            o += w.motif_len;
-            r.variations.assign((const char *)buf + o, (size_t)w.var_len);
-            o += w.var_len;
-            job->j.final_recs.push_back(std::move(r));
+static void import_wire(bwtmi_job *job, const uint8_t *buf, int64_t len) {
+    CHECK_ARG(job && buf && len >= 8, "bad argument");
+    int64_t n;
+    std::memcpy(&n, buf, 8);
+    int64_t o = 8;
+    for (int64_t k = 0; k < n; ++k) {
+        CHECK_ARG(o + (int64_t)sizeof(WireRec) <= len, "truncated record buffer");
+        WireRec w;
+        std::memcpy(&w, buf + o, sizeof w);
+        o += sizeof w;
+        CHECK_ARG(w.motif_len >= 0 && w.var_len >= 0 && o + w.motif_len + w.var_len <= len, "truncated record strings");
+        CHECK_ARG(w.chrom >= 0 && w.chrom < (int32_t)job->j.contigs.size(), "record for unknown contig");
+        if (w.act_kind != ACT_NONE) {
+            const Contig &c = job->j.contigs[(size_t)w.chrom];
+            const int64_t L = w.act_kind == ACT_FULL ? (int64_t)c.full.size() : c.trimmed_len();
+            CHECK_ARG(w.act_off >= 0 && w.act_len >= 0 && w.act_off + w.act_len <= L, "actual_sequence outside its contig");
         }
-        // keep the reference's global order (natural chrom, start, end); every
-        // unit arrives whole from one rank, already in order
-        Job &J = job->j;
-        J.assign_units();
-        std::stable_sort(J.final_recs.begin(), J.final_recs.end(), [&](const Rec &a, const Rec &b) {
-            const int32_t ua = J.contigs[(size_t)a.chrom].unit, ub = J.contigs[(size_t)b.chrom].unit;
-            if (ua != ub) return ua < ub;
-            if (a.start != b.start) return a.start < b.start;
-            return a.end < b.end;
-        });
-        J.postprocessed = true;
+        Rec r;
+        r.chrom = w.chrom; r.tier = w.tier; r.start = w.start; r.end = w.end; r.length = w.length;
+        r.max_mm = w.max_mm; r.n_eval = w.n_eval; r.score = w.score; r.act_off = w.act_off; r.act_len = w.act_len;
+        r.copies = w.copies; r.confidence = w.confidence; r.mismatch_rate = w.mismatch_rate;
+        r.pmatch = w.pmatch; r.pindel = w.pindel; r.act_kind = w.act_kind; r.strand = (char)w.strand;
+        r.is_compound = w.is_compound; r.kmer_stats = w.kmer_stats; r.stats_none = w.stats_none;
+        r.motif.assign((const char *)buf + o, (size_t)w.motif_len);
+        o += w.motif_len;
+        r.variations.assign((const char *)buf + o, (size_t)w.var_len);
+        o += w.var_len;
+        job->j.final_recs.push_back(std::move(r));
+    }
+    // keep the reference's global order (natural chrom, start, end; stable,
+    // bwt.py:3184-3187, 4147): every unit arrives whole, in order
+    Job &J = job->j;
+    J.assign_units();
+    std::stable_sort(J.final_recs.begin(), J.final_recs.end(), [&](const Rec &a, const Rec &b) {
+        const int32_t ua = J.contigs[(size_t)a.chrom].unit, ub = J.contigs[(size_t)b.chrom].unit;
+        if (ua != ub) return ua < ub;
+        if (a.start != b.start) return a.start < b.start;
+        return a.end < b.end;
     });
+    J.postprocessed = true;
+}
+
+int bwtmi_job_import(bwtmi_job *job, const uint8_t *buf, int64_t len) {
+    return guard([&] { import_wire(job, buf, len); });
+}
+
+int bwtmi_job_set_records(bwtmi_job *job, const uint8_t *buf, int64_t len) {
+    return guard([&] {
+        CHECK_ARG(job, "null argument");
+        job->j.final_recs.clear();
+        import_wire(job, buf, len);
+    });
+}
+
+int bwtmi_wire_record_size(void) { return (int)sizeof(WireRec); }
+
+int64_t bwtmi_job_contig_error(const bwtmi_job *job, int32_t id, char *buf, int64_t cap) {
+    if (!job || id < 0 || id >= (int32_t)job->j.contigs.size()) return -1;
+    if ((size_t)id >= job->j.errors.size()) return 0;
+    const std::string &e = job->j.errors[(size_t)id];
+    if (buf && cap > 0) {
+        const size_t m = std::min<size_t>((size_t)cap - 1, e.size());
+        std::memcpy(buf, e.data(), m);
+        buf[m] = 0;
+    }
+    return (int64_t)e.size();
 }
 
 int bwtmi_job_stage_ms(const bwtmi_job *job, double *out8) {

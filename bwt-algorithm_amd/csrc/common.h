@@ -192,6 +192,7 @@ struct Job {
                                                      // (start, end, m desc, worker order) and deduped
     std::vector<ScreenedVec> shits;                  // per contig: those screened hits (hits[c] empty)
     std::vector<int64_t> raw_n;                      // raw strict hits per contig
+    std::vector<std::string> errors;                 // per contig: the worker's error (empty = none)
     RecVec final_recs;                               // after bwt.py:3940-3944
     std::vector<RecVec> t3;                          // per contig: Tier 3 records (bwt.py:3918-3924), joined
                                                      // after the contig's strict hits before nested suppression

@@ -47,6 +47,7 @@ struct Hdr {
 };
 struct Chunk {
     int64_t a = 0, b = 0;     // [a, b): whole lines
+    int64_t bad = -1;         // first non-ASCII byte of a sequence line, or of an invalid header
     int64_t pre = 0;          // content before the chunk's first header
     std::vector<Hdr> hdrs;
     // pass 2 destinations (nullptr: not written)
@@ -69,6 +70,31 @@ void for_lines(const char *p, int64_t a, int64_t e, F &&line) {
         if (t > s) line(s, t);
         i = j + 1;   // "\r\n": the '\n' becomes an empty line
     }
+}
+
+// a header line the reference reads like we do: ASCII, or valid UTF-8 without
+// the Unicode whitespace that str.split() / strip() would also cut at
+bool header_ok(const char *h, int64_t n) {
+    int64_t i = 0;
+    while (i < n) {
+        const unsigned char c = (unsigned char)h[i];
+        if (c < 0x80) { ++i; continue; }
+        int len = c >= 0xF0 && c < 0xF5 ? 4 : c >= 0xE0 ? 3 : c >= 0xC2 && c < 0xE0 ? 2 : 0;
+        if (!len || i + len > n) return false;
+        uint32_t cp = c & (len == 2 ? 0x1F : len == 3 ? 0x0F : 0x07);
+        for (int k = 1; k < len; ++k) {
+            const unsigned char d = (unsigned char)h[i + k];
+            if ((d & 0xC0) != 0x80) return false;
+            cp = (cp << 6) | (d & 0x3F);
+        }
+        if ((len == 3 && cp < 0x800) || (len == 4 && (cp < 0x10000 || cp > 0x10FFFF)) || (cp >= 0xD800 && cp <= 0xDFFF))
+            return false;
+        if (cp == 0x85 || cp == 0xA0 || cp == 0x1680 || (cp >= 0x2000 && cp <= 0x200A) || cp == 0x2028 ||
+            cp == 0x2029 || cp == 0x202F || cp == 0x205F || cp == 0x3000)
+            return false;
+        i += len;
+    }
+    return true;
 }
 
 // upper-cased copy (ASCII a-z), vectorised
@@ -140,13 +166,27 @@ void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, i
                 int64_t y = x;
                 while (y < e && !py_space((unsigned char)p[y])) ++y;
                 C.hdrs.push_back(Hdr{x, y, 0});
-            } else if (C.hdrs.empty()) {
-                C.pre += e - s;
-            } else {
-                C.hdrs.back().len += e - s;
+                if (C.bad < 0 && !header_ok(p + s, e - s)) C.bad = s;
+                return;
             }
+            if (C.bad < 0)
+                for (int64_t q = s; q < e; ++q)
+                    if ((unsigned char)p[q] >= 0x80) { C.bad = q; break; }
+            if (C.hdrs.empty()) C.pre += e - s;
+            else C.hdrs.back().len += e - s;
         });
     });
+
+    // Non-ASCII text: the reference reads the file as UTF-8 str (bwt.py:3719), so an
+    // invalid byte raises UnicodeDecodeError there, and a valid multi-byte character
+    // in a sequence makes BWTCore's text_arr (seq.encode('utf-8'), bwt.py:121) longer
+    // than the str, which aborts its parent-side index build (ValueError from
+    // np.lexsort, bwt.py:3782; tests/golden/expected_edge.json).  Either way the
+    // reference writes no output: fail likewise, before touching the job.
+    for (const Chunk &C : ck)
+        if (C.bad >= 0)
+            fail(BWTMI_E_IO, "non-ASCII text at byte %lld of %s: the reference (bwt.py:3719, 121) fails on it",
+                 (long long)C.bad, path);
 
     // stitch: header instances in file order -> contigs (a repeated name reuses its slot)
     struct Inst {

@@ -306,19 +306,23 @@ struct Extra {                  // trivially destructible: strings live in the P
     std::string_view variations;  // ';'-joined, empty == None
     double copies = 0, confidence = 0, mm = 0, pmatch = 0, pindel = 0;
     int64_t max_mm = 0, n_eval = 0, score = 0;
+    int32_t tier = 2;
     char strand = '+';
     bool stats_none = false;    // Rec::stats_none
 };
 
 static_assert(std::is_trivially_destructible<Extra>::value, "Extras live in raw arena blocks");
 
+// 32 bytes: a strict hit (x == nullptr) is fully determined by its span and
+// primitive motif length -- motif = sequence[start, start + mlen) of the frame,
+// copies = (end - start) / mlen (bwt.py:1957-1961; also (end - i) / L when the
+// unit is primitive), tier 2; every other record carries an Extra
 struct Item {
     int64_t start, end;   // current frame (trimmed, then full after restore)
-    int64_t count;        // strict: copies
-    int64_t moff;         // strict: motif = trimmed[moff, moff + mlen)
     const Extra *x;       // recomputed record, nullptr for a strict hit
-    int32_t chrom, mlen, tier, pad;
+    int32_t chrom, mlen;
 };
+static_assert(sizeof(Item) == 32, "fold items stay 32 bytes");
 
 // vector storage without value-initialisation: large item arrays are written
 // once in parallel, so the first touch happens in the filling threads
@@ -386,13 +390,17 @@ struct Pools {
 struct UnitCtx {
     const Job *job;
     int64_t min_copies;
+    bool restored = false;   // items are in full-sequence coordinates (multi-offset units)
 };
 
 inline std::string_view motif_of(const UnitCtx &u, const Item &it) {
     if (it.x) return it.x->motif;
-    return std::string_view(u.job->contigs[(size_t)it.chrom].trimmed() + it.moff, (size_t)it.mlen);
+    const Contig &c = u.job->contigs[(size_t)it.chrom];
+    return std::string_view((u.restored ? c.full.data() : c.trimmed()) + it.start, (size_t)it.mlen);
 }
-inline double copies_of(const Item &it) { return it.x ? it.x->copies : (double)it.count; }
+inline int64_t strict_copies(const Item &it) { return (it.end - it.start) / it.mlen; }
+inline int32_t tier_of(const Item &it) { return it.x ? it.x->tier : 2; }
+inline double copies_of(const Item &it) { return it.x ? it.x->copies : (double)strict_copies(it); }
 inline double mm_of(const Item &it) { return it.x ? it.x->mm : 0.0; }
 inline double conf_of(const Item &it) { return it.x ? it.x->confidence : 0.95; }
 
@@ -604,12 +612,12 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
         x.pmatch = 100.0;
         x.pindel = 0.0;
         x.score = trf_score(run, 0.0);
+        x.tier = tier;
         Item it{};
         it.start = start;
         it.end = start + run;
         it.chrom = chrom;
         it.mlen = 1;
-        it.tier = tier;
         it.x = pools.add_static(w, x, std::string_view(&kByteChars[(uint8_t)b], 1));
         return it;
     }
@@ -668,14 +676,12 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     x.pmatch = std::max(0.0, 100.0 - mm * 100.0);
     x.pindel = pind;
     x.score = trf_score(tl, mm);
+    x.tier = tier;
     Item it{};
     it.start = start;
     it.end = start + tl;
-    it.count = 0;
-    it.moff = 0;
     it.chrom = chrom;
     it.mlen = (int32_t)motif_s->size();
-    it.tier = tier;
     it.x = pools.add(w, x, *motif_s, var_s);
     return it;
 }
@@ -742,7 +748,7 @@ bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, Canon &c1,
     if (!same_canonical(u, r1, c1, r2, c2)) return false;
     if (g_counters) g_same.fetch_add(1, std::memory_order_relaxed);
     const int64_t s = std::min(r1.start, r2.start), e = std::max(r1.end, r2.end);
-    const int32_t tier = std::min(r1.tier, r2.tier);
+    const int32_t tier = std::min(tier_of(r1), tier_of(r2));
     Item mg = recompute(u, pools, w, r1.chrom, s, e, std::max<int64_t>(1, ml), tier);
     if (mg.x->copies < (double)u.min_copies) return false;
     const double base = std::max(std::max(mm_of(r1), mm_of(r2)), 0.01);
@@ -942,7 +948,7 @@ void dedup_sorted(const UnitCtx &u, ItemVec &recs) {
             if (conf_of(r) > conf_of(ex)) repl = true;
             else if (conf_of(r) == conf_of(ex)) {
                 if (mm_of(r) < mm_of(ex)) repl = true;
-                else if (mm_of(r) == mm_of(ex) && r.tier < ex.tier) repl = true;
+                else if (mm_of(r) == mm_of(ex) && tier_of(r) < tier_of(ex)) repl = true;
             }
             if (repl) d[hit] = r;
         }
@@ -964,12 +970,12 @@ Item item_of_rec(Pools &pools, const Rec &r) {
     x.score = r.score;
     x.strand = r.strand;
     x.stats_none = r.stats_none;
+    x.tier = r.tier;
     Item it{};
     it.start = r.start;
     it.end = r.end;
     it.chrom = r.chrom;
     it.mlen = (int32_t)r.motif.size();
-    it.tier = r.tier;
     it.x = pools.add(0, x, r.motif, r.variations);
     return it;
 }
@@ -978,7 +984,7 @@ Item item_of_rec(Pools &pools, const Rec &r) {
 void materialize(const UnitCtx &u, const Item &it, int64_t shift, Rec &r) {   // r: a fresh Rec
     const Contig &c = u.job->contigs[(size_t)it.chrom];
     r.chrom = it.chrom;
-    r.tier = it.tier;
+    r.tier = tier_of(it);
     r.start = it.start + shift;
     r.end = it.end + shift;
     r.length = it.end - it.start;
@@ -997,12 +1003,13 @@ void materialize(const UnitCtx &u, const Item &it, int64_t shift, Rec &r) {   //
         r.variations = x.variations;
         r.stats_none = x.stats_none;
     } else {
-        r.motif.assign(c.trimmed() + it.moff, (size_t)it.mlen);
-        r.copies = (double)it.count;
+        r.motif.assign(c.trimmed() + (it.start - (u.restored ? c.trim_left : 0)), (size_t)it.mlen);
+        const int64_t count = strict_copies(it);
+        r.copies = (double)count;
         r.confidence = 0.95;
         r.mismatch_rate = 0.0;
         r.max_mm = 0;
-        r.n_eval = it.count;
+        r.n_eval = count;
         r.strand = '+';
         r.pmatch = (1.0 - 0.0) * 100.0;
         r.pindel = 0.0;
@@ -1042,7 +1049,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
                 for (int64_t k = a; k < b; ++k) {
                     const ScreenedHit &x = sh[(size_t)k];
                     const int64_t len = x.len, prim = x.prim;
-                    items[(size_t)k] = Item{x.start, x.start + len, len / prim, x.start, nullptr, c, (int32_t)prim, 2, 0};
+                    items[(size_t)k] = Item{x.start, x.start + len, nullptr, c, (int32_t)prim};
                 }
             });
             ScreenedVec().swap(sh);
@@ -1051,7 +1058,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
             parallel_for((int64_t)h.size(), nt, [&](int64_t a, int64_t b) {
                 for (int64_t k = a; k < b; ++k) {
                     const bwtmi_hit &x = h[(size_t)k];
-                    items[(size_t)k] = Item{x.start, x.end, x.copies, x.start, nullptr, c, x.prim_len, 2, 0};
+                    items[(size_t)k] = Item{x.start, x.end, nullptr, c, x.prim_len};
                 }
             });
         }
@@ -1088,7 +1095,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
                     const int64_t rc = (int64_t)std::nearbyint(copies_of(r));
                     m = std::max<int64_t>(1, (r.end - r.start) / std::max<int64_t>(1, rc ? rc : 1));
                 }
-                r = recompute(u, pools, w, r.chrom, r.start, r.end, m, r.tier);
+                r = recompute(u, pools, w, r.chrom, r.start, r.end, m, tier_of(r));
             }
         });
     }
@@ -1111,6 +1118,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
                 r.end += off;
             }
         });
+    if (!one_offset) u.restored = true;
     // 6. collapse (bwt.py:3499-3513)
     if (!one_offset) sort_by_pos(recs, nt);
     auto r3 = clk::now();

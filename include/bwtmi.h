@@ -227,6 +227,16 @@ int64_t bwtmi_job_get_string(bwtmi_job *job, int64_t i, int which, char *buf, in
 /* serialise final records for a gather to another rank; import appends them */
 int bwtmi_job_export(bwtmi_job *job, uint8_t **buf, int64_t *len);
 int bwtmi_job_import(bwtmi_job *job, const uint8_t *buf, int64_t len);
+/* replace the final records by a serialised list (bwtmi_job_export's format;
+ * save_results over a caller-built list of records, bwt.py:4141-4198);
+ * bwtmi_wire_record_size = size of one fixed record header in that format */
+int bwtmi_job_set_records(bwtmi_job *job, const uint8_t *buf, int64_t len);
+int bwtmi_wire_record_size(void);
+/* the worker's error of contig id in the last bwtmi_job_scan (0 = none): a
+ * failing contig yields no records and the others go on, as the reference's
+ * `except Exception: print("ERROR processing chromosome ..."); return []`
+ * (bwt.py:3137-3141); copies the message, returns its length */
+int64_t bwtmi_job_contig_error(const bwtmi_job *job, int32_t id, char *buf, int64_t cap);
 /* per-stage wall times (ms) of the last scan/postprocess/render calls */
 int bwtmi_job_stage_ms(const bwtmi_job *job, double *out8);
 

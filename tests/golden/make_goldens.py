@@ -17,6 +17,9 @@ here is product code.  Outputs land in tests/golden/ as small data files:
   tier3         Tier3LongReadFinder on seeded contigs + long reads (library
                 call) and the CLI with --tier3 --long-reads (FASTA and FASTQ
                 reads, four formats, parallel and sequential modes)
+  edge          reference CLI on crafted edge inputs (natural-key collisions,
+                CRLF / CR line ends, '$' in sequences, 0-64 bp contigs,
+                non-ASCII text) -> expected_edge.json
   simple        Tier2LCPFinder.find_long_repeats (_find_repeats_simple) on
                 small seeded / crafted / edge contigs (each well inside the
                 reference's 30 s wall-clock stop)
@@ -547,6 +550,93 @@ def cmd_simple(a):
         json.dump(out, f, indent=0)
 
 
+# ------------------------------------------------------------ edge inputs
+def _edge_inputs():
+    """Input edge cases of SURVEY.md §7.3: natural-key
+    collisions (chr1 / chr01 / CHR1, chr2 / Chr02) inside one fold unit with
+    different trims, CRLF and bare-CR line ends, a '$' inside and at the end of
+    a sequence, contigs of 0-62 bp around the 2 x 30 bp trim, and non-ASCII
+    text (valid UTF-8 'é', and an invalid byte)."""
+    r = np.random.default_rng(11)
+    B = "ACGT"
+
+    def rnd(n):
+        return "".join(B[i] for i in r.integers(0, 4, n))
+
+    def body(n, arrays):
+        s = rnd(n)
+        for pos, unit, cps in arrays:
+            arr = unit * cps
+            s = s[:pos] + arr + s[pos + len(arr):]
+        return s[:n]
+
+    def lines(seq, w=60, eol="\n"):
+        return "".join(seq[i:i + w] + eol for i in range(0, len(seq), w))
+
+    files = {}
+    c1 = body(260, [(40, "CAG", 8), (100, "A", 9), (130, "GT", 7), (200, "ACGTT", 4)])
+    c01 = body(50, [(5, "TG", 6), (25, "C", 7)])
+    C1 = body(150, [(35, "GATA", 5), (90, "TTAGG", 4)])
+    c2 = body(100, [(40, "AC", 10)])
+    C02 = body(70, [(32, "G", 8)])
+    files["edge_collide.fa"] = (">chr1 first copy\r\n" + lines(c1, 60, "\r\n") + ">chr01\n" + lines(c01) +
+                                ">CHR1\r" + lines(C1, 70, "\r") + ">chr2\n" + lines(c2) + ">Chr02 x\n" +
+                                lines(C02.lower(), 35))
+    d1 = body(180, [(40, "CA", 8)])
+    d1 = d1[:70] + "$$$" + d1[73:120] + "AC$AC$AC$AC$" + d1[132:]
+    d2 = body(90, [(20, "T", 10)]) + "$"
+    files["edge_dollar.fa"] = ">withdollar\n" + lines(d1) + ">enddollar\n" + lines(d2)
+    parts = []
+    for k, n in enumerate([0, 1, 6, 59, 60, 61, 62, 64]):
+        seq = body(n, [(max(0, n // 2 - 6), "A", 6)] if n >= 12 else [])
+        parts.append(f">short{k}  \t\n\n" + lines(seq, 25))
+    files["edge_short.fa"] = "".join(parts)
+    u = body(140, [(30, "CT", 9), (80, "A", 8)])
+    files["edge_utf8.fa"] = ">u1\n" + u[:50] + "é" + u[50:] + "\n>u2\n" + lines(body(100, [(10, "GA", 8)]))
+    return files
+
+
+def cmd_edge(a):
+    """Reference CLI on the edge inputs -> expected_edge.json (+ *.out)."""
+    ref = ref_module()
+    inp = os.path.join(HERE, "inputs")
+    out_dir = os.path.join(HERE, "cli")
+    work = tempfile.mkdtemp()
+    man = {}
+    files = _edge_inputs()
+    for fn, text in files.items():
+        with open(os.path.join(inp, fn), "w", newline="", encoding="utf-8") as f:
+            f.write(text)
+    with open(os.path.join(inp, "edge_badbyte.fa"), "wb") as f:
+        f.write(b">bad\nACGTACGTACGT\xffACGTACGTACGTACGT\n")
+    cases = []
+    for fn in files:
+        cases += [(f"{fn}.strfinder", fn, []), (f"{fn}.bed", fn, ["--format", "bed"]),
+                  (f"{fn}.trim0", fn, ["--flank-trim", "0"])]
+    cases.append(("edge_badbyte.fa.strfinder", "edge_badbyte.fa", []))
+    for name, fn, args in cases:
+        shutil.copy(os.path.join(inp, fn), os.path.join(work, fn))
+        outp = os.path.join(work, "out.tab")
+        if os.path.exists(outp):
+            os.unlink(outp)
+        err = None
+        try:
+            run_ref_cli(ref, [fn, "-o", "out.tab", "--jobs", "-1"] + args, work)
+        except Exception as e:        # the reference's own failure is the golden
+            err = f"{type(e).__name__}: {e}"
+        rec = dict(input=fn, args=args)
+        if err is None:
+            dst = os.path.join(out_dir, name + ".out")
+            shutil.copy(outp, dst)
+            rec["sha256"] = sha(dst)
+        else:
+            rec["error"] = err
+        man[name] = rec
+        print(name, rec.get("sha256", rec.get("error"))[:60], flush=True)
+    with open(os.path.join(HERE, "expected_edge.json"), "w") as f:
+        json.dump(man, f, indent=1, sort_keys=True)
+
+
 def cmd_hybrid(a):
     """Full-size golden via the validated hybrid oracle."""
     ref = ref_module()
@@ -591,6 +681,7 @@ def main():
     sp.add_parser("library")
     sp.add_parser("tier3")
     sp.add_parser("simple")
+    sp.add_parser("edge")
     p = sp.add_parser("hybrid")
     p.add_argument("name")
     p.add_argument("--config")
@@ -603,7 +694,7 @@ def main():
     p.add_argument("--save-out", action="store_true")
     a = ap.parse_args()
     dict(fixtures=cmd_fixtures, rawhits=cmd_rawhits, index=cmd_index, motif=cmd_motif,
-         hybrid=cmd_hybrid, library=cmd_library, tier3=cmd_tier3, simple=cmd_simple)[a.cmd](a)
+         hybrid=cmd_hybrid, library=cmd_library, tier3=cmd_tier3, simple=cmd_simple, edge=cmd_edge)[a.cmd](a)
 
 
 if __name__ == "__main__":

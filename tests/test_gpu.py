@@ -213,6 +213,52 @@ def test_device_screen_matches_host(gpu_ctx, case):
         assert d == h, (case, fmt)
 
 
+def test_failing_contig_yields_error_and_no_records(gpu_ctx, golden_dir, tmp_path, capsys, monkeypatch):
+    """The worker's failure convention (bwt.py:3137-3141): a contig whose device
+    work fails is reported as `ERROR processing chromosome NAME: ...` and
+    contributes no records; the other contigs are unaffected (the expected
+    file is the oracle pipeline with that contig's strict hits removed)."""
+    from bwtmi import cli
+    fa = os.path.join(golden_dir, "inputs", "test2.fa")
+    seqs, _, _ = post.load_fasta(fa, 30)
+    victim = sorted(seqs)[3]
+    monkeypatch.setenv("BWTMI_FAIL_CONTIG", victim)
+    out = tmp_path / "out.tab"
+    assert cli.main([fa, "-o", str(out), "--jobs", "-1"]) == 0
+    assert f"ERROR processing chromosome {victim}:" in capsys.readouterr().out
+    vseq = seqs[victim].encode()
+
+    def scan(b, U, mc):
+        return oracle.strict_scan(b, 1, U, 0, mc)[:0] if b == vseq else oracle.strict_scan(b, 1, U, 0, mc)
+    assert out.read_text() == post.run_file(fa, "strfinder", strict_scan=scan)
+
+
+def _edge_goldens():
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "expected_edge.json")
+    with open(here) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name", sorted(_edge_goldens()))
+def test_edge_inputs_on_device(gpu_ctx, golden_dir, tmp_path, name):
+    """The drop-in CLI on the edge inputs against the
+    reference CLI's outputs -- or its failure, for non-ASCII text: no output
+    file and an error."""
+    import shutil
+    from bwtmi import cli
+    m = _edge_goldens()[name]
+    fa = tmp_path / m["input"]
+    shutil.copy(os.path.join(golden_dir, "inputs", m["input"]), fa)
+    out = tmp_path / "out.tab"
+    if "error" in m:
+        with pytest.raises(Exception, match="non-ASCII"):
+            cli.main([str(fa), "-o", str(out), "--jobs", "-1"] + m["args"])
+        assert not out.exists()
+        return
+    assert cli.main([str(fa), "-o", str(out), "--jobs", "-1"] + m["args"]) == 0
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == m["sha256"], name
+
+
 def _large_goldens():
     here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "expected_large.json")
     with open(here) as f:

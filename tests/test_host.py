@@ -154,6 +154,70 @@ def test_reload_replaces_content(tmp_path):
     assert j.contig_seq(0) == b"CC" and j.contig_seq(1) == b"TTTTTT"
 
 
+def _edge_cases(golden_dir):
+    with open(os.path.join(golden_dir, "expected_edge.json")) as f:
+        man = json.load(f)
+    for name, m in sorted(man.items()):
+        d = dict(fmt="strfinder", mc=3, trim=30, tier2=True)
+        a = m["args"]
+        for i, x in enumerate(a):
+            if x == "--format":
+                d["fmt"] = a[i + 1]
+            elif x == "--flank-trim":
+                d["trim"] = int(a[i + 1])
+        yield name, m, d
+
+
+def test_edge_inputs_match_reference_goldens(golden_dir, built_lib):
+    """SURVEY.md §7.3 edge inputs (natural-key collisions in one fold unit with
+    different trims, CRLF / CR line ends, '$' inside sequences, 0-64 bp contigs)
+    through the native loader + native post-processing + writers, against the
+    reference CLI's own outputs; the non-ASCII inputs, on which the reference
+    fails (UnicodeDecodeError / ValueError), fail here too."""
+    from bwtmi._lib import BwtmiError
+    for name, m, d in _edge_cases(golden_dir):
+        path = os.path.join(golden_dir, "inputs", m["input"])
+        if "error" in m:
+            from bwtmi.records import Job
+            with pytest.raises(BwtmiError, match="non-ASCII"):
+                Job().load_fasta(path, d["trim"])
+            continue
+        j = _native_job(path, d)
+        j.postprocess()
+        assert hashlib.sha256(j.render(d["fmt"])).hexdigest() == m["sha256"], name
+
+
+def test_save_results_over_plain_record_lists(golden_dir, tmp_path, built_lib):
+    """save_results(list_of_records) (bwt.py:4141-4198) with a copy of the
+    records and with a filtered subset, in all five formats, against the
+    oracle's writers over the same records."""
+    from bwtmi import TandemRepeatFinder
+    fa = os.path.join(golden_dir, "inputs", "test_all_12.fa")
+    f = TandemRepeatFinder(fa)
+    f.load_reference()
+    j = f.job
+    for cid in range(j.contig_count()):
+        _, fl, tl, tr = j.contig_info(cid)
+        seq = j.contig_seq(cid)[tl:fl - tr]
+        j.add_hits(cid, oracle.strict_scan(seq, 1, max(120, min(len(seq) // 3, 1000)), 0, 3))
+    j.postprocess()
+    recs = j.records()
+    seqs, full, offs = post.load_fasta(fa, 30)
+    p = post.Pipeline(seqs, full, offs, 3)
+    want = p.run([r for c, s in seqs.items() for r in post.worker_records(
+        c, s, oracle.strict_scan(s.encode(), 1, max(120, min(len(s) // 3, 1000)), 0, 3))])
+    keep = lambda r: r.copies >= 5 or len(r.motif) > 3            # noqa: E731
+    for fmt in ("strfinder", "bed", "vcf", "trf_table", "trf_dat"):
+        out = tmp_path / f"all.{fmt}"
+        f.save_results(list(recs), str(out), fmt)
+        assert out.read_bytes() == j.render(fmt), fmt
+        f.save_results([r for r in recs if keep(r)], str(out), fmt)
+        assert out.read_text() == post.render(p, [r for r in want if keep(r)], fmt), fmt
+    for fmt in ("strfinder", "vcf"):
+        f.save_results([], str(out), fmt)
+        assert out.read_text() == post.render(p, [], fmt), fmt
+
+
 def test_native_postprocess_and_writers_match_goldens(golden_dir, built_lib):
     for name, m, d in _cases(golden_dir):
         j = _native_job(os.path.join(golden_dir, "inputs", m["input"]), d)
