@@ -158,6 +158,7 @@ void composition_of(const char *s, int64_t n, double out[4]);
 int64_t trf_score(int64_t length, double mm);
 
 struct AlignSummary {
+    bool want_copies = true;                  // fill copy_len / copy_err (bwtmi_align_region)
     std::vector<int64_t> copy_len, copy_err;  // per copy: consumed bases, errors
     std::string consensus;
     int64_t motif_len = 0, copies = 0, consumed = 0, max_errors = 0, tot_ins = 0, tot_del = 0;

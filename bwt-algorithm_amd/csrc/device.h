@@ -63,7 +63,7 @@ struct HBuf {  // pinned host staging
 enum Slot {
     S_TEXT = 0, S_PACK, S_CAND_K, S_CAND_V, S_CAND_K2, S_CAND_V2, S_FLAG, S_SCAN, S_HITS, S_COUNTS,
     S_SORT_TMP0, S_SORT_TMP1, S_SORT_HIST, S_SCAN_TMP, S_MISC0, S_MISC1, S_MISC2, S_MISC3,
-    S_IDX0, S_IDX1, S_IDX2, S_IDX3, S_IDX4, S_IDX5, S_IDX6, S_IDX7, S_NSLOTS
+    S_IDX0, S_IDX1, S_IDX2, S_IDX3, S_IDX4, S_IDX5, S_IDX6, S_IDX7, S_IDX8, S_IDX9, S_IDX10, S_IDX11, S_NSLOTS
 };
 
 struct KernelTimer {
@@ -183,6 +183,7 @@ template <class T>
 void exclusive_scan(Ctx &c, const T *in, T *out, int64_t n);   // out may alias in
 void radix_sort_pairs(Ctx &c, uint64_t *keys, uint64_t *vals, int64_t n, int bit0, int bit1);
 void radix_sort_pairs32(Ctx &c, uint64_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1);
+void radix_sort_pairs_k32(Ctx &c, uint32_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1);
 
 // ----- strict scan (strict_scan.hip)
 struct ScanResult {
@@ -202,6 +203,10 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
 // ----- nested suppression / sort / dedup of one contig's strict hits (nested.hip)
 void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
                         ScreenedVec &out);
+
+// ----- suffix array + BWT of ACGT* '$' texts (sa_dna.hip)
+bool sa_dna_eligible(uint8_t last, int64_t n, const int64_t *totals);
+bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT);
 
 // ----- index (index.hip)
 struct DeviceIndex;

@@ -324,45 +324,10 @@ inline unsigned blocks(int64_t n, int b = 256) { return (unsigned)((n + b - 1) /
 
 }  // namespace
 
-DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t sa_sample, int32_t occ_sample,
-                                uint32_t flags, DeviceIndex *reuse) {
-    auto *ix = reuse ? reuse : new DeviceIndex();   // reuse: keep the buffers of an earlier build
-    ix->has_kmer = false;
-    ix->kmer_count = 0;
+// Suffix array of any text by prefix doubling over radix sorts (see the file
+// header), then the BWT gather.
+void sa_doubling(Ctx &c, DeviceIndex *ix, const uint8_t *T, int64_t n, int sigma, const uint8_t *code) {
     hipStream_t st = c.stream;
-    ix->n = n;
-    ix->sa_sample = sa_sample;
-    ix->occ_sample = occ_sample;
-    ix->text.ensure((size_t)n + 128);
-    HIPCHECK(hipMemsetAsync(ix->text.p, 0, (size_t)n + 128, st));
-    if (n) HIPCHECK(hipMemcpyAsync(ix->text.p, d_text, (size_t)n, hipMemcpyDeviceToDevice, st));
-    const uint8_t *T = ix->text.as<uint8_t>();
-    // histogram -> alphabet, totals, C (bwt.py:129-134, 276-286)
-    c.slot[S_COUNTS].ensure(256 * 8);
-    HIPCHECK(hipMemsetAsync(c.slot[S_COUNTS].p, 0, 256 * 8, st));
-    if (n) KLAUNCH("k_hist_bytes", 0.0, k_hist_bytes, dim3(1024), dim3(256), 0, st, T, n, c.slot[S_COUNTS].as<unsigned long long>());
-    unsigned long long h[256];
-    HIPCHECK(hipMemcpyAsync(h, c.slot[S_COUNTS].p, sizeof h, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
-    int64_t cum = 0;
-    uint8_t code[256] = {0}, present[256] = {0};
-    int sigma = 0;
-    std::memset(ix->code_of, 0, sizeof ix->code_of);
-    for (int b = 0; b < 256; ++b) {
-        ix->totals[b] = (int64_t)h[b];
-        ix->C[b] = cum;
-        cum += (int64_t)h[b];
-        if (h[b]) {
-            present[sigma] = (uint8_t)b;
-            ix->code_of[b] = (uint8_t)sigma;
-            code[b] = (uint8_t)(++sigma);   // 0 = past the end
-        }
-    }
-    ix->sigma = sigma;
-    ix->sa.ensure((size_t)std::max<int64_t>(n, 1) * 4);
-    if (n == 0) return ix;
-
-    // ------------------------------------------------------------ suffix array
     int b = 1;
     while ((1 << b) < sigma + 1) ++b;
     const int k = 64 / b;
@@ -429,10 +394,67 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     }
     HIPCHECK(hipGetLastError());
 
-    // ------------------------------------------------------------ BWT, Occ, sampled SA
+    // BWT (bwt.py:266-274)
+    KLAUNCH("bwt_gather", (double)n * (4.0 + 1.0 + 1.0), k_bwt, dim3(blocks(n)), dim3(256), 0, st, T, SA, n, ix->bwt.as<uint8_t>());
+}
+
+DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t sa_sample, int32_t occ_sample,
+                                uint32_t flags, DeviceIndex *reuse) {
+    auto *ix = reuse ? reuse : new DeviceIndex();   // reuse: keep the buffers of an earlier build
+    ix->has_kmer = false;
+    ix->kmer_count = 0;
+    hipStream_t st = c.stream;
+    ix->n = n;
+    ix->sa_sample = sa_sample;
+    ix->occ_sample = occ_sample;
+    ix->text.ensure((size_t)n + 128);
+    HIPCHECK(hipMemsetAsync(ix->text.p, 0, (size_t)n + 128, st));
+    if (n) HIPCHECK(hipMemcpyAsync(ix->text.p, d_text, (size_t)n, hipMemcpyDeviceToDevice, st));
+    const uint8_t *T = ix->text.as<uint8_t>();
+    // histogram -> alphabet, totals, C (bwt.py:129-134, 276-286)
+    c.slot[S_COUNTS].ensure(256 * 8);
+    HIPCHECK(hipMemsetAsync(c.slot[S_COUNTS].p, 0, 256 * 8, st));
+    if (n) KLAUNCH("k_hist_bytes", 0.0, k_hist_bytes, dim3(1024), dim3(256), 0, st, T, n, c.slot[S_COUNTS].as<unsigned long long>());
+    unsigned long long h[256];
+    HIPCHECK(hipMemcpyAsync(h, c.slot[S_COUNTS].p, sizeof h, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    int64_t cum = 0;
+    uint8_t code[256] = {0}, present[256] = {0};
+    int sigma = 0;
+    std::memset(ix->code_of, 0, sizeof ix->code_of);
+    for (int b = 0; b < 256; ++b) {
+        ix->totals[b] = (int64_t)h[b];
+        ix->C[b] = cum;
+        cum += (int64_t)h[b];
+        if (h[b]) {
+            present[sigma] = (uint8_t)b;
+            ix->code_of[b] = (uint8_t)sigma;
+            code[b] = (uint8_t)(++sigma);   // 0 = past the end
+        }
+    }
+    ix->sigma = sigma;
+    ix->sa.ensure((size_t)std::max<int64_t>(n, 1) * 4);
+    if (n == 0) return ix;
     ix->bwt.ensure((size_t)n + 128);
     HIPCHECK(hipMemsetAsync(ix->bwt.p, 0, (size_t)n + 128, st));
-    KLAUNCH("bwt_gather", (double)n * (4.0 + 1.0 + 1.0), k_bwt, dim3(blocks(n)), dim3(256), 0, st, T, SA, n, ix->bwt.as<uint8_t>());
+    uint8_t last = 0;
+    HIPCHECK(hipMemcpyAsync(&last, T + n - 1, 1, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    // ACGT* '$' (every CLI contig): string sort over 2-bit words (sa_dna.hip)
+    const bool dna = sa_dna_eligible(last, n, ix->totals) &&
+                     sa_dna_device(c, T, n, ix->sa.as<uint32_t>(), ix->bwt.as<uint8_t>());
+    if (!dna) sa_doubling(c, ix, T, n, sigma, code);
+    // scratch of the Occ / k-mer stages
+    c.slot[S_IDX0].ensure((size_t)n * 8);
+    c.slot[S_IDX3].ensure((size_t)(n + 1) * 4);
+    c.slot[S_IDX4].ensure((size_t)(n + 1) * 4);
+    c.slot[S_IDX6].ensure((size_t)(n + 1) * 4);
+    uint64_t *keys = c.slot[S_IDX0].as<uint64_t>();
+    uint32_t *head = c.slot[S_IDX3].as<uint32_t>();
+    uint32_t *gid = c.slot[S_IDX4].as<uint32_t>();
+    uint32_t *flag = c.slot[S_IDX6].as<uint32_t>();
+    const uint32_t *SA = ix->sa.as<uint32_t>();
+
     const int64_t nblk = (n + occ_sample - 1) / occ_sample;
     ix->occ_len = 1 + n / occ_sample + (n % occ_sample != 0);   // == nblk + 1
     ix->occ.ensure((size_t)sigma * (nblk + 1) * 4);

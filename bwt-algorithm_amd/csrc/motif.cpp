@@ -397,8 +397,10 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
         while (pos < limit && seq[pos] == b) ++pos;
         const int64_t copies = pos - start;
         if (copies < min_copies || copies <= 0) return false;
-        out.copy_len.assign((size_t)copies, 1);
-        out.copy_err.assign((size_t)copies, 0);
+        if (out.want_copies) {
+            out.copy_len.assign((size_t)copies, 1);
+            out.copy_err.assign((size_t)copies, 0);
+        }
         out.variations.clear();
         out.any_variation = false;
         out.consensus.assign(1, b);
@@ -417,7 +419,7 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
     out.copy_err.clear();
     out.variations.clear();
     out.any_variation = false;
-    int64_t tot_ins = 0, tot_del = 0;
+    int64_t tot_ins = 0, tot_del = 0, tot_err = 0, max_err = 0;
     thread_local std::string cur, nxt;
     cur = tmpl;
     int64_t pos = start;
@@ -440,12 +442,28 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
         if (wlen >= m && std::memcmp(cur.data(), seq + pos, (size_t)m) == 0) {
             // exact copy: the DP's unique zero is (m, m) on the all-'M' diagonal,
             // so no ops, consumed m, every base observed; each cur[p] is already
-            // its position's first maximal count, so the consensus is unchanged
-            ++copies;
-            out.copy_err.push_back(0);
-            out.copy_len.push_back(m);
-            ++pend;
-            pos += m;
+            // its position's first maximal count, so the consensus is unchanged.
+            // The copies after it stay exact while the text is m-periodic, so a
+            // whole run of them is taken at once: copy j (at pos + j*m) is taken
+            // while pos + j*m < limit and pos + (j+1)*m <= seq_len.
+            const int64_t top = std::min<int64_t>(seq_len, limit - 1 + m);   // last copy ends by here
+            int64_t x = pos + m;
+            while (x + 8 <= top) {   // periodic extent, 8 bytes at a time
+                uint64_t a, b;
+                std::memcpy(&a, seq + x, 8);
+                std::memcpy(&b, seq + x - m, 8);
+                if (a != b) break;
+                x += 8;
+            }
+            while (x < top && seq[x] == seq[x - m]) ++x;
+            const int64_t k = (x - pos) / m;   // >= 1 (the first copy)
+            copies += k;
+            pend += k;
+            if (out.want_copies) {
+                out.copy_err.insert(out.copy_err.end(), (size_t)k, 0);
+                out.copy_len.insert(out.copy_len.end(), (size_t)k, m);
+            }
+            pos += k * m;
             continue;
         }
         if (!align_unit(cur.data(), m, seq + pos, wlen, max_indel, tol, S, res) || res.consumed == 0) break;
@@ -460,8 +478,12 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
             out.any_variation = true;
             from = e;
         }
-        out.copy_err.push_back(res.n_sub + res.n_ins + res.n_del);
-        out.copy_len.push_back(res.consumed);
+        if (out.want_copies) {
+            out.copy_err.push_back(res.n_sub + res.n_ins + res.n_del);
+            out.copy_len.push_back(res.consumed);
+        }
+        tot_err += res.n_sub + res.n_ins + res.n_del;
+        max_err = std::max<int64_t>(max_err, res.n_sub + res.n_ins + res.n_del);
         tot_ins += res.n_ins;
         tot_del += res.n_del;
         for (size_t q = 0; q < S.obs_idx.size(); ++q) {
@@ -477,14 +499,12 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
     if (consumed <= 0) return false;
     flush();
     consensus_from(S, m, cur, out.consensus);
-    int64_t tot = 0, mx = 0;
-    for (auto e : out.copy_err) { tot += e; mx = std::max(mx, e); }
     const int64_t denom = copies * m;
     out.motif_len = m;
     out.copies = copies;
     out.consumed = consumed;
-    out.mismatch_rate = denom > 0 ? (double)tot / (double)denom : 0.0;
-    out.max_errors = mx;
+    out.mismatch_rate = denom > 0 ? (double)tot_err / (double)denom : 0.0;
+    out.max_errors = max_err;
     out.tot_ins = tot_ins;
     out.tot_del = tot_del;
     return true;

@@ -633,6 +633,7 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     }
     if (tmpl.empty()) tmpl.assign((size_t)m, 'N');
     thread_local AlignSummary s;
+    s.want_copies = false;
     bool ok = align_repeat_region(seq, L, start, end, tmpl, std::max<int64_t>(1, u.min_copies), s);
     if (!ok) ok = align_repeat_region(seq, L, start, end, tmpl, 1, s);
     Extra x;
@@ -759,39 +760,67 @@ bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, Canon &c1,
     return true;
 }
 
+// Output of a speculative run, compactly: most records leave the fold
+// unchanged, so an emitted record is its index in R (>= 0), or ~k for side[k],
+// a merged record with the index of its run's first item.  The step at which
+// entry q was emitted is the first index of the next run (entry q + 1, or the
+// pending run).
 struct SpecOut {
-    ItemVec emitted;                 // records emitted by the speculative run
-    std::vector<int64_t, BigAlloc<int64_t>> emit_step;  // index i at which each was emitted
+    struct Side {
+        int64_t j;
+        Item it;
+    };
+    std::vector<int64_t, BigAlloc<int64_t>> emitted;
+    std::vector<Side> side;
     Item pending;
+    int64_t pending_j = 0;
     Canon pending_canon;
+    int64_t start(size_t q) const {
+        if (q >= emitted.size()) return pending_j;
+        const int64_t e = emitted[q];
+        return e >= 0 ? e : side[(size_t)~e].j;
+    }
+    const Item &record(const ItemVec &R, size_t q) const {
+        const int64_t e = emitted[q];
+        return e >= 0 ? R[(size_t)e] : side[(size_t)~e].it;
+    }
 };
 
 // speculative run over [b, e): starts with cur = R[b] as if fresh at b
 void spec_run(const UnitCtx &u, Pools &pools, int w, const ItemVec &R, int64_t b, int64_t e,
               std::vector<uint8_t, BigAlloc<uint8_t>> &fresh, SpecOut &o) {
     Item cur = R[(size_t)b];
+    int64_t cur_j = b;
+    bool merged = false;
     Canon cb[2];   // canonical forms of cur and of the next record; roles swap by index
     int ci_cur = 0;
     fresh[(size_t)b] = 1;
     Item mg;
     o.emitted.reserve((size_t)(e - b));
-    o.emit_step.reserve((size_t)(e - b));
     for (int64_t i = b + 1; i < e; ++i) {
         Canon &cc = cb[ci_cur], &ci = cb[ci_cur ^ 1];
         ci.ok = false;
         if (try_merge(u, pools, w, cur, cc, R[(size_t)i], ci, mg)) {
             cur = mg;
+            merged = true;
             cc.ok = false;
             fresh[(size_t)i] = 0;
         } else {
-            o.emitted.push_back(cur);
-            o.emit_step.push_back(i);
+            if (merged) {
+                o.emitted.push_back(~(int64_t)o.side.size());
+                o.side.push_back({cur_j, cur});
+            } else {
+                o.emitted.push_back(cur_j);
+            }
             cur = R[(size_t)i];
+            cur_j = i;
+            merged = false;
             ci_cur ^= 1;
             fresh[(size_t)i] = 1;
         }
     }
     o.pending = cur;
+    o.pending_j = cur_j;
     o.pending_canon = std::move(cb[ci_cur]);
 }
 
@@ -822,7 +851,7 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
     // where the speculative run restarted too
     // The serial part only walks each chunk up to its sync point; the output
     // is then assembled in parallel: chunk k contributes rep[k] (records the
-    // true run emitted before syncing) and spec[k].emitted[from[k]..].
+    // true run emitted before syncing) and its speculative entries from[k] on.
     std::vector<ItemVec> rep((size_t)K);
     std::vector<size_t> from((size_t)K, 0);
     std::vector<uint8_t> synced((size_t)K, 0);
@@ -850,8 +879,8 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
             }
         }
         if (sync < 0) continue;   // never re-synchronised: `cur` carries into chunk k+1
-        size_t q = 0;
-        while (q < sp.emitted.size() && sp.emit_step[q] <= sync) ++q;
+        size_t q = 0;             // the speculative entry of the run starting at sync
+        while (q < sp.emitted.size() && sp.start(q + 1) <= sync) ++q;
         from[(size_t)k] = q;
         synced[(size_t)k] = 1;
         cur = sp.pending;
@@ -869,9 +898,9 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
         const SpecOut &sp = spec[(size_t)k];
         Item *dst = out.data() + at[(size_t)k];
         const ItemVec &rp = rep[(size_t)k];
-        std::copy(rp.begin(), rp.end(), dst);
+        dst = std::copy(rp.begin(), rp.end(), dst);
         if (synced[(size_t)k])
-            std::copy(sp.emitted.begin() + (std::ptrdiff_t)from[(size_t)k], sp.emitted.end(), dst + rp.size());
+            for (size_t q = from[(size_t)k]; q < sp.emitted.size(); ++q) *dst++ = sp.record(R, q);
     });
     out[at[(size_t)K]] = cur;
     if (g_stats) {

@@ -1,5 +1,6 @@
 // radix.hip -- hand-written device primitives for gfx950: exclusive scan and a
-// stable LSD radix sort (8-bit digits) over 64-bit keys with 32/64-bit values.
+// stable LSD radix sort (8-bit digits) over 64- or 32-bit keys with 32/64-bit
+// values.
 //
 // Radix pass = three launches:
 //   hist    : one workgroup per 8192-key tile, LDS histogram -> counts[d][tile]
@@ -10,7 +11,7 @@
 //             digit in LDS and streamed out in that order, so each digit's
 //             run of the tile is one contiguous, coalesced write.  Keys and
 //             then values take turns in one 64 KB LDS buffer (2 workgroups
-//             of 8 waves per CU).
+//             of 8 waves per CU; 32 KB with 32-bit keys).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -96,8 +97,8 @@ __global__ __launch_bounds__(kBlock) void k_chunk_scan(const T *__restrict__ in,
 // ------------------------------------------------------------------ radix
 // Pass geometry: 256-thread workgroups (thread t owns digit t in the tile
 // scan), ITEMS keys per thread, tile = 256 * ITEMS.
-template <int ITEMS>
-__global__ __launch_bounds__(kBlock) void k_hist(const uint64_t *__restrict__ keys, uint32_t *__restrict__ counts,
+template <int ITEMS, class KT>
+__global__ __launch_bounds__(kBlock) void k_hist(const KT *__restrict__ keys, uint32_t *__restrict__ counts,
                                                  int64_t n, int shift, int64_t ntiles) {
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
@@ -128,17 +129,23 @@ __device__ __forceinline__ void st(T *p, T v) {
 //   SPLIT : keys and values take turns in one LDS staging buffer (the slot ->
 //           global position map stays in registers), so a tile needs 8 B of
 //           LDS per key instead of 8 + sizeof(V) and more workgroups fit a CU
-template <class V, int BLOCK, int ITEMS, bool NT, bool SPLIT>
-__global__ __launch_bounds__(BLOCK) void k_scatter(const uint64_t *__restrict__ kin, const V *__restrict__ vin,
-                                                   uint64_t *__restrict__ kout, V *__restrict__ vout,
+template <class KT, class V, int BLOCK, int ITEMS, bool NT, bool SPLIT>
+__global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, const V *__restrict__ vin,
+                                                   KT *__restrict__ kout, V *__restrict__ vout,
                                                    const uint32_t *__restrict__ offs, int64_t n, int shift,
                                                    int64_t ntiles) {
     constexpr int kT = BLOCK * ITEMS;
     constexpr int NW = BLOCK / 64;
+    static_assert(BLOCK >= 256 && BLOCK % 64 == 0, "threads 0..255 own one digit each");
+    static_assert(!SPLIT || sizeof(V) <= sizeof(KT), "values are staged in the key buffer");
+    // static LDS: the 256 per-wave digit counters of every wave, the digit bases,
+    // the 256/64 wave sums of the digit scan and the key (and value) staging
+    static_assert(sizeof(uint32_t) * (NW * 256 + 256 + 256 / 64) + sizeof(KT) * kT + (SPLIT ? 0 : sizeof(V) * kT) <=
+                      160 * 1024, "exceeds gfx950's 160 KB of LDS per workgroup");
     __shared__ uint32_t wcnt[NW][256];   // per-wave digit counts, then per-wave digit bases
     __shared__ uint32_t gdelta[256];     // global position of tile slot j = gdelta[digit] + j
-    __shared__ uint32_t dsum[4];
-    __shared__ uint64_t ks[kT];
+    __shared__ uint32_t dsum[256 / 64];  // waves 0-3 own the 256 digits of the scan
+    __shared__ KT ks[kT];
     __shared__ V vs_own[SPLIT ? 1 : kT];
     V *vs = SPLIT ? reinterpret_cast<V *>(ks) : vs_own;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -147,14 +154,14 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const uint64_t *__restrict__ 
     const int64_t tbase = (int64_t)blockIdx.x * kT;
     const int64_t wbase = tbase + (int64_t)wv * (ITEMS * 64);
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint64_t k[ITEMS];
+    KT k[ITEMS];
     V v[ITEMS];
     uint32_t r[ITEMS];   // rank among the wave's earlier keys of the same digit
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const int64_t idx = wbase + i * 64 + lane;
         const bool valid = idx < n;
-        k[i] = valid ? kin[idx] : 0ull;
+        k[i] = valid ? kin[idx] : (KT)0;
         if (vin) v[i] = valid ? vin[idx] : (V)0;
     }
 #pragma unroll
@@ -223,7 +230,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const uint64_t *__restrict__ 
         const int j = i * BLOCK + threadIdx.x;
         pos[i] = 0;
         if (j < cntt) {
-            const uint64_t key = ks[j];
+            const KT key = ks[j];
             pos[i] = gdelta[(key >> shift) & 255u] + (uint32_t)j;
             st<NT>(kout + pos[i], key);
             if (!SPLIT && vout) st<NT>(vout + pos[i], vs[j]);
@@ -243,33 +250,35 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const uint64_t *__restrict__ 
     }
 }
 
-template <class V, int BLOCK, int ITEMS, bool NT, bool SPLIT>
-void radix_sort_cfg(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int bit1) {
+template <class KT, class V, int BLOCK, int ITEMS, bool NT, bool SPLIT>
+void radix_sort_cfg(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
     constexpr int kT = BLOCK * ITEMS;
     static_assert(kT % kBlock == 0, "histogram tiles are 256-thread tiles");
     const int64_t ntiles = (n + kT - 1) / kT;
-    c.slot[S_SORT_TMP0].ensure((size_t)n * sizeof(uint64_t));
+    c.slot[S_SORT_TMP0].ensure((size_t)n * sizeof(KT));
     if (vals) c.slot[S_SORT_TMP1].ensure((size_t)n * sizeof(V));
     c.slot[S_SORT_HIST].ensure((size_t)ntiles * 256 * sizeof(uint32_t));
-    uint64_t *ka = keys, *kb = c.slot[S_SORT_TMP0].as<uint64_t>();
+    KT *ka = keys, *kb = c.slot[S_SORT_TMP0].as<KT>();
     V *va = vals, *vb = vals ? c.slot[S_SORT_TMP1].as<V>() : nullptr;
     uint32_t *cnt = c.slot[S_SORT_HIST].as<uint32_t>();
     int passes = 0;
     for (int sh = bit0; sh < bit1; sh += 8) {
         // read the keys once
-        KLAUNCH("radix_hist", (double)n * 8.0, k_hist<kT / kBlock>, dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream, ka, cnt, n, sh, ntiles);
+        KLAUNCH("radix_hist", (double)n * (double)sizeof(KT), (k_hist<kT / kBlock, KT>), dim3((unsigned)ntiles),
+                dim3(kBlock), 0, c.stream, ka, cnt, n, sh, ntiles);
         exclusive_scan<uint32_t>(c, cnt, cnt, ntiles * 256);
         // read (key, value) once, write it once
-        KLAUNCH(sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16",
-                (double)n * 2.0 * (8.0 + (vals ? (double)sizeof(V) : 0.0)), (k_scatter<V, BLOCK, ITEMS, NT, SPLIT>),
-                dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, ka, va, kb, vb, cnt, n, sh, ntiles);
+        KLAUNCH(sizeof(KT) == 4 ? "radix_scatter_kv8" : sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16",
+                (double)n * 2.0 * ((double)sizeof(KT) + (vals ? (double)sizeof(V) : 0.0)),
+                (k_scatter<KT, V, BLOCK, ITEMS, NT, SPLIT>), dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, ka, va,
+                kb, vb, cnt, n, sh, ntiles);
         std::swap(ka, kb);
         std::swap(va, vb);
         ++passes;
     }
     HIPCHECK(hipGetLastError());
     if (passes & 1) {
-        HIPCHECK(hipMemcpyAsync(keys, ka, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToDevice, c.stream));
+        HIPCHECK(hipMemcpyAsync(keys, ka, (size_t)n * sizeof(KT), hipMemcpyDeviceToDevice, c.stream));
         if (vals) HIPCHECK(hipMemcpyAsync(vals, va, (size_t)n * sizeof(V), hipMemcpyDeviceToDevice, c.stream));
     }
 }
@@ -280,12 +289,13 @@ void radix_sort_cfg(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int bi
 // and value staging 0.44-0.45; nontemporal stores 0.34-0.41 in every geometry.
 // r01ak, same box session for every variant: 512x16 0.50, 256x16 0.47, 512x8
 // 0.47, 1024x4 0.47, 256x20 0.48, 1024x8 0.44, 256x32 0.43.
-template <class V>
-void radix_sort_impl(Ctx &c, uint64_t *keys, V *vals, int64_t n, int bit0, int bit1) {
+template <class KT, class V>
+void radix_sort_impl(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
     if (n <= 1) return;
-    // 512 threads x 16 keys: 8192-key tiles, 8 waves per workgroup, 64 KB LDS
-    // (2 workgroups per CU)
-    radix_sort_cfg<V, 512, 16, false, true>(c, keys, vals, n, bit0, bit1);
+    // 512 threads x 16 keys: 8192-key tiles, 8 waves per workgroup, ~75 KB of
+    // LDS with 64-bit keys (64 KB staging + 8 KB wave counters + digit tables),
+    // ~43 KB with 32-bit keys; 2 (3) workgroups per CU within gfx950's 160 KB
+    radix_sort_cfg<KT, V, 512, 16, false, true>(c, keys, vals, n, bit0, bit1);
 }
 
 }  // namespace
@@ -321,10 +331,13 @@ template void exclusive_scan<uint64_t>(Ctx &, const uint64_t *, uint64_t *, int6
 template void exclusive_scan<int64_t>(Ctx &, const int64_t *, int64_t *, int64_t);
 
 void radix_sort_pairs(Ctx &c, uint64_t *keys, uint64_t *vals, int64_t n, int bit0, int bit1) {
-    radix_sort_impl<uint64_t>(c, keys, vals, n, bit0, bit1);
+    radix_sort_impl<uint64_t, uint64_t>(c, keys, vals, n, bit0, bit1);
 }
 void radix_sort_pairs32(Ctx &c, uint64_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1) {
-    radix_sort_impl<uint32_t>(c, keys, vals, n, bit0, bit1);
+    radix_sort_impl<uint64_t, uint32_t>(c, keys, vals, n, bit0, bit1);
+}
+void radix_sort_pairs_k32(Ctx &c, uint32_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1) {
+    radix_sort_impl<uint32_t, uint32_t>(c, keys, vals, n, bit0, bit1);
 }
 
 }  // namespace bwtmi

@@ -1,0 +1,589 @@
+// sa_dna.hip -- suffix array + BWT of an ACGT text with its single final '$'
+// (BWTCore._build_suffix_array / _build_bwt_array, bwt.py:212-274), the text
+// every CLI contig produces (seq + '$', bwt.py:3053 / 3782).  Any other text
+// (N, IUPAC, lower case, an inner '$') takes index.hip's general prefix
+// doubling.
+//
+// The reference orders suffixes by byte value with the unique '$' smallest;
+// 2-bit codes A0 C1 G2 T3 keep that order among bases.  Instead of doubling
+// over a rank array, suffixes are sorted as strings:
+//   1. the text is packed to 2 bits (32 bases per 64-bit word);
+//   2. one LSD radix sort of (first 16 bases: 32-bit key, value) -- 4 passes
+//      of 8 B keys+values instead of 8+ passes of 12 B; the value carries the
+//      suffix start and the code of the base before it (BWT symbol);
+//   3. runs of equal keys (groups) are finished by prefix doubling over a rank
+//      array (Larsson-Sadakane): rank[i] = SA index of the head of i's group;
+//      a round with h sorts every group by rank[i + h] -- the groups are then
+//      2h-sorted -- and writes the new heads.  Only group members take part,
+//      and each group is sorted where it fits:
+//        <= 64 members     one wave (4, 16 or 64 lanes per group), bitonic
+//                          over lane shuffles
+//        <= kMedium        one workgroup, bitonic in LDS
+//        larger            one segmented radix pass over all such groups
+//      Each round gathers every member's key first (one pass over all groups)
+//      and only then sorts and rewrites heads: a mix of old and new heads
+//      would split suffixes that are still tied.
+//   4. one streaming pass writes SA and BWT.
+// The end of the text: keys pad past the end with A, so the (at most 16)
+// suffixes with fewer than 16 bases before '$' tie with suffixes that really
+// continue with A.  One small fix-up moves each of them to the front of its
+// group (a suffix ending sooner is smaller) before the rounds start, so the
+// first round's ranks are an exact 16-sort.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "device.h"
+
+namespace bwtmi {
+namespace {
+
+constexpr int kB = 256;
+constexpr int kMedium = 1024;                   // largest group sorted by one workgroup
+constexpr uint32_t kPosMask = (1u << 29) - 1;   // value: start (29 bits) | BWT code << 29
+
+inline unsigned nblocks(int64_t n, int b = kB) { return (unsigned)((n + b - 1) / b); }
+
+__device__ __forceinline__ uint32_t code2(uint8_t c) { return (uint32_t)(((c >> 2) ^ (c >> 1)) & 3u); }   // A0 C1 G2 T3
+
+// P[w] = bases 32w .. 32w+31, first base in the top bits; '$' and past the end read as A (0)
+__global__ __launch_bounds__(kB) void k_dna_pack(const uint8_t *__restrict__ t, int64_t n, uint64_t *__restrict__ P,
+                                                 int64_t nw) {
+    const int64_t w = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (w >= nw) return;
+    const int64_t base = w * 32;
+    uint64_t v = 0;
+    if (base + 32 <= n - 1) {
+        const uint4 a = *reinterpret_cast<const uint4 *>(t + base);
+        const uint4 b = *reinterpret_cast<const uint4 *>(t + base + 16);
+        const uint32_t ws[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v = (v << 2) | code2((uint8_t)(ws[q] >> (8 * k)));
+    } else {
+        for (int k = 0; k < 32; ++k) {
+            const int64_t i = base + k;
+            v = (v << 2) | (i < n - 1 ? code2(t[i]) : 0u);
+        }
+    }
+    P[w] = v;
+}
+
+// bases pos .. pos+31 (P is padded with two zero words)
+__device__ __forceinline__ uint64_t window(const uint64_t *__restrict__ P, int64_t pos) {
+    const int64_t w = pos >> 5;
+    const int sh = (int)(pos & 31) * 2;
+    const uint64_t hi = P[w];
+    return sh ? (hi << sh) | (P[w + 1] >> (64 - sh)) : hi;
+}
+
+__device__ __forceinline__ uint32_t base_code(const uint64_t *__restrict__ P, int64_t i) {
+    return (uint32_t)((P[i >> 5] >> (62 - 2 * (i & 31))) & 3u);
+}
+
+// key = first 16 bases of suffix i; value = i | BWT code << 29 (code of the base
+// before i, '$' = 4 for i == 0)
+__global__ __launch_bounds__(kB) void k_dna_keys(const uint64_t *__restrict__ P, int64_t n, uint32_t *__restrict__ keys,
+                                                 uint32_t *__restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = (uint32_t)(window(P, i) >> 32);
+    const uint32_t prev = i == 0 ? 4u : base_code(P, i - 1);
+    vals[i] = (uint32_t)i | (prev << 29);
+}
+
+// flags of the multi-member groups (runs of equal keys): S = first member, E = last member
+__global__ __launch_bounds__(kB) void k_dna_flags(const uint32_t *__restrict__ keys, int64_t n,
+                                                  uint32_t *__restrict__ fs, uint32_t *__restrict__ fe) {
+    const int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (r >= n) return;
+    const uint32_t k = keys[r];
+    const bool head = r == 0 || keys[r - 1] != k;
+    const bool tail = r + 1 == n || keys[r + 1] != k;
+    fs[r] = head && !tail;
+    fe[r] = tail && !head;
+}
+
+__global__ __launch_bounds__(kB) void k_dna_compact2(const uint32_t *__restrict__ fs, const uint32_t *__restrict__ ps,
+                                                     const uint32_t *__restrict__ fe, const uint32_t *__restrict__ pe,
+                                                     int64_t n, uint32_t *__restrict__ gs, uint32_t *__restrict__ ge) {
+    const int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (r >= n) return;
+    if (fs[r]) gs[ps[r]] = (uint32_t)r;
+    if (fe[r]) ge[pe[r]] = (uint32_t)r + 1;   // exclusive end
+}
+
+// rank[i] = SA index of the head of i's 16-base group, or i's own index when
+// alone.  ps / pe: exclusive counts of group starts / ends (index r is inside
+// a group when more groups started up to r than ended before it)
+__global__ __launch_bounds__(kB) void k_dna_rank0(const uint32_t *__restrict__ vals, const uint32_t *__restrict__ ps,
+                                                  const uint32_t *__restrict__ pe, const uint32_t *__restrict__ gs,
+                                                  int64_t n, uint32_t *__restrict__ rank) {
+    const int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (r >= n) return;
+    const uint32_t started = ps[r + 1];
+    rank[vals[r] & kPosMask] = started > pe[r] ? gs[started - 1] : (uint32_t)r;
+}
+
+// the <= 16 suffixes with fewer than 16 bases before '$' (their keys are
+// A-padded): each goes to the front of its group, shorter first, and leaves
+// the group; the rest of the group gets the head behind them.  One workgroup.
+__global__ __launch_bounds__(1024) void k_dna_short_fix(uint32_t *__restrict__ vals, uint32_t *__restrict__ rank,
+                                                        uint32_t *__restrict__ gs, const uint32_t *__restrict__ ge,
+                                                        int64_t G, int64_t n) {
+    __shared__ int64_t grp[16];      // group index of the short suffix with r bases left, or -1
+    __shared__ uint32_t where[16];   // its index in vals
+    const int ns = (int)min<int64_t>(16, n);
+    if (threadIdx.x < 16) {
+        grp[threadIdx.x] = -1;
+        if ((int)threadIdx.x < ns) {
+            const uint32_t hd = rank[n - 1 - threadIdx.x];
+            int64_t lo = 0, hi = G;   // gs ascends: find gs[x] == hd
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) / 2;
+                if (gs[mid] < hd) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo < G && gs[lo] == hd && ge[lo] - gs[lo] >= 2) grp[threadIdx.x] = lo;
+        }
+    }
+    __syncthreads();
+    for (int r0 = 0; r0 < ns; ++r0) {
+        const int64_t g = grp[r0];
+        bool first = g >= 0;
+        for (int r = 0; r < r0 && first; ++r) first = grp[r] != g;
+        if (!first) continue;   // each group once, at its shortest member
+        const uint32_t s = gs[g], e = ge[g];
+        for (uint32_t x = s + threadIdx.x; x < e; x += blockDim.x) {
+            const int64_t pos = vals[x] & kPosMask;
+            if (pos >= n - 16) where[n - 1 - pos] = x;
+        }
+        __syncthreads();
+        __shared__ uint32_t k_sh;
+        if (threadIdx.x == 0) {   // swap the shorts to s, s+1, ... in order of r
+            uint32_t k = 0;
+            for (int r = 0; r < ns; ++r) {
+                if (grp[r] != g) continue;
+                const uint32_t t = s + k, from = where[r];
+                const uint32_t moved = vals[t];
+                vals[t] = vals[from];
+                vals[from] = moved;
+                const int64_t mp = moved & kPosMask;
+                if (mp >= n - 16) where[n - 1 - mp] = from;
+                rank[n - 1 - r] = t;
+                ++k;
+            }
+            k_sh = k;
+            gs[g] = s + k;
+        }
+        __syncthreads();
+        const uint32_t k = k_sh;
+        for (uint32_t x = s + k + threadIdx.x; x < e; x += blockDim.x) rank[vals[x] & kPosMask] = s + k;
+        __syncthreads();
+    }
+}
+
+// groups by size class; the order inside a class does not matter (groups are disjoint)
+constexpr int kClasses = 5;   // <= 4, <= 16, <= 64 members (one wave), <= kMedium (workgroup), larger
+__device__ __forceinline__ int size_class(uint32_t sz) {
+    return sz <= 4 ? 0 : sz <= 16 ? 1 : sz <= 64 ? 2 : sz <= (uint32_t)kMedium ? 3 : 4;
+}
+
+__device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
+// append (start, end) to a list, one atomic per workgroup of NT threads (a
+// single counter hit once per wave by ~10^6 waves serialises in L2); every
+// thread of the workgroup must call it
+template <int NT>
+__device__ __forceinline__ void block_append(bool on, uint32_t st, uint32_t en, uint32_t *__restrict__ ls,
+                                             uint32_t *__restrict__ le, uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t wc[NT / 64 + 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t m = __ballot(on);
+    if (lane == 0) wc[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < NT / 64; ++w) {
+            const uint32_t x = wc[w];
+            wc[w] = tot;
+            tot += x;
+        }
+        wc[NT / 64] = tot ? atomicAdd(cnt, tot) : 0u;
+    }
+    __syncthreads();
+    if (on) {
+        const uint32_t at = wc[NT / 64] + wc[wv] + (uint32_t)__popcll(m & lanes_below(lane));
+        ls[at] = st;
+        le[at] = en;
+    }
+    __syncthreads();   // wc is reused by the next call
+}
+
+__global__ __launch_bounds__(kB) void k_dna_classify(const uint32_t *__restrict__ gs, const uint32_t *__restrict__ ge,
+                                                     int64_t G, uint32_t *__restrict__ cls_start,
+                                                     uint32_t *__restrict__ cls_size, uint32_t *__restrict__ counts,
+                                                     int64_t cap) {
+    const int64_t g = (int64_t)blockIdx.x * kB + threadIdx.x;
+    const bool live = g < G;
+    const uint32_t s = live ? gs[g] : 0u, sz = live ? ge[g] - s : 0u;
+    const int c = size_class(sz);
+    for (int k = 0; k < kClasses; ++k)   // one atomic per workgroup and class
+        block_append<kB>(live && c == k, s, sz, cls_start + (int64_t)k * cap, cls_size + (int64_t)k * cap, &counts[k]);
+}
+
+// the doubling key of member v: rank of the suffix h bases on (a group member
+// always has more than h bases before '$': its h-prefix is shared)
+__device__ __forceinline__ uint32_t ls_key(const uint32_t *__restrict__ rank, uint32_t v, int64_t n, int64_t h) {
+    const int64_t a = v & kPosMask;
+    return a + h < n ? rank[a + h] : 0u;
+}
+
+// one doubling pass over groups of <= W members, 64/W groups per wave: bitonic
+// sort of (rank[a+h], value) in W-lane segments, new heads from ballots, the
+// still-tied runs appended to the next round's list
+// (KEYS: the gather pass -- kb[i] = key of the member at vals[i])
+constexpr int kLB = 1024;   // threads per workgroup of the wave-sort passes
+template <int W, bool KEYS>
+__global__ __launch_bounds__(kLB) void k_ls_wave(const uint32_t *__restrict__ starts, const uint32_t *__restrict__ sizes,
+                                                int64_t cnt, uint32_t *__restrict__ vals, uint32_t *__restrict__ rank,
+                                                uint32_t *__restrict__ kb, int64_t n, int64_t h, uint32_t *__restrict__ ngs,
+                                                uint32_t *__restrict__ nge, uint32_t *__restrict__ ncnt) {
+    const int lane = threadIdx.x & 63, kk = lane & (W - 1);
+    const int64_t g = (((int64_t)blockIdx.x * kLB + threadIdx.x) >> 6) * (64 / W) + lane / W;
+    uint32_t s = 0, sz = 0;
+    if (g < cnt) {
+        s = starts[g];
+        sz = sizes[g];
+    }
+    const bool live = kk < (int)sz;
+    if (KEYS) {
+        if (live) kb[s + kk] = ls_key(rank, vals[s + kk], n, h);
+        return;
+    }
+    uint64_t x = live ? ((uint64_t)kb[s + kk] << 32) | vals[s + kk] : ~0ull;
+#pragma unroll
+    for (int k2 = 2; k2 <= W; k2 <<= 1)
+#pragma unroll
+        for (int j = k2 >> 1; j > 0; j >>= 1) {
+            const uint64_t y = __shfl_xor(x, j, 64);
+            const bool keep_min = ((kk & j) == 0) == ((kk & k2) == 0);
+            x = keep_min ? (y < x ? y : x) : (y > x ? y : x);
+        }
+    const uint32_t key = (uint32_t)(x >> 32), v = (uint32_t)x;
+    const uint32_t kp = __shfl(key, (lane + 63) & 63, 64), kn = __shfl(key, (lane + 1) & 63, 64);
+    const bool start = live && (kk == 0 || kp != key);
+    const bool tail = live && (kk == (int)sz - 1 || kn != key);
+    const uint64_t S = __ballot(start), T = __ballot(tail);
+    const int seg = lane - kk;
+    if (live) {
+        const int hl = 63 - __clzll((long long)(S & (lanes_below(lane) | (1ull << lane))));
+        vals[s + kk] = v;
+        rank[v & kPosMask] = s + (uint32_t)(hl - seg);
+    }
+    const bool multi = start && !tail;
+    const int el = multi ? __ffsll((unsigned long long)(T & (~0ull << lane))) - 1 : 0;
+    block_append<kLB>(multi, s + kk, s + (uint32_t)(el - seg) + 1, ngs, nge, ncnt);
+}
+
+// one doubling pass over a group of <= kMedium members in one workgroup
+constexpr int kWB = 1024;
+template <bool KEYS>
+__global__ __launch_bounds__(kWB) void k_ls_block(const uint32_t *__restrict__ starts, const uint32_t *__restrict__ sizes,
+                                                  uint32_t *__restrict__ vals, uint32_t *__restrict__ rank,
+                                                  uint32_t *__restrict__ kb, int64_t n, int64_t h,
+                                                  uint32_t *__restrict__ ngs, uint32_t *__restrict__ nge,
+                                                  uint32_t *__restrict__ ncnt) {
+    __shared__ uint64_t x[kMedium];
+    __shared__ int wl[kWB / 64], wf[kWB / 64];
+    const uint32_t s = starts[blockIdx.x], sz = sizes[blockIdx.x];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint32_t p2 = 1;
+    while (p2 < sz) p2 <<= 1;
+    if (KEYS) {
+        if (t < (int)sz) kb[s + t] = ls_key(rank, vals[s + t], n, h);
+        return;
+    }
+    if (t < (int)p2) x[t] = t < (int)sz ? ((uint64_t)kb[s + t] << 32) | vals[s + t] : ~0ull;
+    __syncthreads();
+    for (uint32_t k2 = 2; k2 <= p2; k2 <<= 1)
+        for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+            const uint32_t q = (uint32_t)t ^ j;
+            if (t < (int)p2 && q > (uint32_t)t) {
+                const uint64_t a = x[t], b = x[q];
+                if ((a > b) == (((uint32_t)t & k2) == 0)) {
+                    x[t] = b;
+                    x[q] = a;
+                }
+            }
+            __syncthreads();
+        }
+    const bool live = t < (int)sz;
+    const uint64_t me = live ? x[t] : ~0ull;
+    const uint32_t key = (uint32_t)(me >> 32);
+    const bool start = live && (t == 0 || (uint32_t)(x[t - 1] >> 32) != key);
+    const bool tail = live && (t == (int)sz - 1 || (uint32_t)(x[t + 1] >> 32) != key);
+    const uint64_t S = __ballot(start), T = __ballot(tail);
+    if (lane == 0) {
+        wl[wv] = S ? wv * 64 + 63 - __clzll((long long)S) : -1;
+        wf[wv] = T ? wv * 64 + __ffsll((unsigned long long)T) - 1 : 1 << 30;
+    }
+    __syncthreads();
+    int head = -1;
+    const uint64_t Sb = S & (lanes_below(lane) | (1ull << lane));
+    if (Sb) head = wv * 64 + 63 - __clzll((long long)Sb);
+    else
+        for (int w = 0; w < wv; ++w) head = max(head, wl[w]);
+    if (live) {
+        const uint32_t v = (uint32_t)me;
+        vals[s + t] = v;
+        rank[v & kPosMask] = s + (uint32_t)head;
+    }
+    const bool multi = start && !tail;
+    int end = 1 << 30;
+    if (multi) {
+        const uint64_t Ta = T & (~0ull << lane);
+        if (Ta) end = wv * 64 + __ffsll((unsigned long long)Ta) - 1;
+        else
+            for (int w = wv + 1; w < kWB / 64; ++w) end = min(end, wf[w]);
+    }
+    block_append<kWB>(multi, s + (uint32_t)t, s + (uint32_t)end + 1, ngs, nge, ncnt);
+}
+
+// groups larger than kMedium: (group index << 30 | rank[a+h]) keys gathered
+// into one segmented radix sort; starts/sizes/offs = the large-group table
+__global__ __launch_bounds__(kB) void k_dna_refine_keys(const uint32_t *__restrict__ starts, const uint32_t *__restrict__ sizes,
+                                                        const uint32_t *__restrict__ offs, const uint32_t *__restrict__ vals,
+                                                        const uint32_t *__restrict__ rank, int64_t n, int64_t h,
+                                                        uint64_t *__restrict__ rk, uint32_t *__restrict__ rv) {
+    const uint32_t q = blockIdx.y;
+    const uint32_t s = starts[q], sz = sizes[q], at = offs[q];
+    for (uint32_t k = blockIdx.x * kB + threadIdx.x; k < sz; k += gridDim.x * kB) {
+        const uint32_t v = vals[s + k];
+        rk[at + k] = ((uint64_t)q << 30) | ls_key(rank, v, n, h);
+        rv[at + k] = v;
+    }
+}
+
+__global__ __launch_bounds__(kB) void k_dna_refine_back(const uint32_t *__restrict__ starts, const uint32_t *__restrict__ sizes,
+                                                        const uint32_t *__restrict__ offs, const uint32_t *__restrict__ rv,
+                                                        uint32_t *__restrict__ vals) {
+    const uint32_t q = blockIdx.y;
+    const uint32_t s = starts[q], sz = sizes[q], at = offs[q];
+    for (uint32_t k = blockIdx.x * kB + threadIdx.x; k < sz; k += gridDim.x * kB) vals[s + k] = rv[at + k];
+}
+
+// subgroups after the pass: runs of equal keys (same q)
+__global__ __launch_bounds__(kB) void k_dna_refine_flags(const uint64_t *__restrict__ rk, int64_t m,
+                                                         uint32_t *__restrict__ fs, uint32_t *__restrict__ fe) {
+    const int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (k >= m) return;
+    const uint64_t x = rk[k];
+    const bool head = k == 0 || rk[k - 1] != x;
+    const bool tail = k + 1 == m || rk[k + 1] != x;
+    fs[k] = head && !tail;
+    fe[k] = tail && !head;
+}
+
+// new heads of the large groups' members: the subgroup start (gs, gathered
+// index) when inside a tied run, else the member itself, mapped to vals
+__global__ __launch_bounds__(kB) void k_dna_refine_rank(const uint64_t *__restrict__ rk, const uint32_t *__restrict__ rv,
+                                                        const uint32_t *__restrict__ ps, const uint32_t *__restrict__ pe,
+                                                        const uint32_t *__restrict__ gs, const uint32_t *__restrict__ starts,
+                                                        const uint32_t *__restrict__ offs, int64_t m,
+                                                        uint32_t *__restrict__ rank) {
+    const int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (k >= m) return;
+    const uint32_t started = ps[k + 1];
+    const uint32_t hk = started > pe[k] ? gs[started - 1] : (uint32_t)k;
+    const uint32_t q = (uint32_t)(rk[k] >> 30);
+    rank[rv[k] & kPosMask] = starts[q] + (hk - offs[q]);
+}
+
+// subgroup bounds from gathered indices to positions in vals: index k of large
+// group q = rk[k] >> 30 sits at starts[q] + (k - offs[q]); ends are exclusive
+__global__ __launch_bounds__(kB) void k_dna_refine_pos(const uint64_t *__restrict__ rk, const uint32_t *__restrict__ starts,
+                                                       const uint32_t *__restrict__ offs, uint32_t *__restrict__ gs,
+                                                       uint32_t *__restrict__ ge, int64_t G) {
+    const int64_t x = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (x >= G) return;
+    const uint32_t k = gs[x], kl = ge[x] - 1;
+    const uint32_t q = (uint32_t)(rk[k] >> 30);
+    gs[x] = starts[q] + (k - offs[q]);
+    ge[x] = starts[q] + (kl - offs[q]) + 1;
+}
+
+__global__ __launch_bounds__(kB) void k_dna_final(const uint32_t *__restrict__ vals, int64_t n, uint32_t *__restrict__ sa,
+                                                  uint8_t *__restrict__ bwt) {
+    const int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (r >= n) return;
+    const uint32_t v = vals[r];
+    sa[r] = v & kPosMask;
+    const uint32_t c = v >> 29;
+    bwt[r] = c == 4 ? (uint8_t)'$' : (uint8_t)"ACGT"[c];
+}
+
+}  // namespace
+
+bool sa_dna_eligible(const uint8_t last, int64_t n, const int64_t *totals) {
+    if (n < 2 || n > (int64_t)kPosMask || last != '$' || totals['$'] != 1) return false;
+    return totals['A'] + totals['C'] + totals['G'] + totals['T'] + 1 == n;
+}
+
+// SA (uint32[n]) and BWT (uint8[n]) of t[0, n) = ACGT* '$'; false when the
+// refinement needed more than kMaxRounds passes (the caller then runs the
+// general prefix doubling)
+bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT) {
+    hipStream_t st = c.stream;
+    const int64_t nw = (n + 31) / 32 + 2;
+    c.slot[S_IDX0].ensure((size_t)n * 4 + 64);      // keys, then class lists
+    c.slot[S_IDX1].ensure((size_t)n * 4 + 64);      // values
+    c.slot[S_IDX2].ensure((size_t)nw * 8 + 64);     // packed text
+    c.slot[S_IDX3].ensure((size_t)(n + 1) * 4);     // group-start flags
+    c.slot[S_IDX4].ensure((size_t)(n + 1) * 4);     // their positions
+    c.slot[S_IDX5].ensure((size_t)(n + 1) * 4);     // group-end flags
+    c.slot[S_IDX6].ensure((size_t)(n + 1) * 4);     // their positions
+    c.slot[S_MISC3].ensure(64);
+    uint32_t *keys = c.slot[S_IDX0].as<uint32_t>();
+    uint32_t *vals = c.slot[S_IDX1].as<uint32_t>();
+    uint64_t *P = c.slot[S_IDX2].as<uint64_t>();
+    uint32_t *fs = c.slot[S_IDX3].as<uint32_t>(), *ps = c.slot[S_IDX4].as<uint32_t>();
+    uint32_t *fe = c.slot[S_IDX5].as<uint32_t>(), *pe = c.slot[S_IDX6].as<uint32_t>();
+    uint32_t *counts = c.slot[S_MISC3].as<uint32_t>();
+
+    KLAUNCH("dna_pack", (double)n + (double)n / 4.0, k_dna_pack, dim3(nblocks(nw)), dim3(kB), 0, st, t, n, P, nw);
+    KLAUNCH("dna_keys", (double)n / 4.0 + 8.0 * (double)n, k_dna_keys, dim3(nblocks(n)), dim3(kB), 0, st, P, n, keys,
+            vals);
+    radix_sort_pairs_k32(c, keys, vals, n, 0, 32);
+
+    // groups of equal 16-base prefixes -> (start, end) lists
+    auto groups = [&](const uint32_t *f_s, uint32_t *p_s, const uint32_t *f_e, uint32_t *p_e, int64_t m,
+                      uint32_t *gs, uint32_t *ge) -> int64_t {
+        HIPCHECK(hipMemsetAsync(const_cast<uint32_t *>(f_s) + m, 0, 4, st));
+        exclusive_scan<uint32_t>(c, f_s, p_s, m + 1);
+        exclusive_scan<uint32_t>(c, f_e, p_e, m);
+        uint32_t G = 0;
+        HIPCHECK(hipMemcpyAsync(&G, p_s + m, 4, hipMemcpyDeviceToHost, st));
+        KLAUNCH("dna_compact", 0.0, k_dna_compact2, dim3(nblocks(m)), dim3(kB), 0, st, f_s, p_s, f_e, p_e, m, gs, ge);
+        HIPCHECK(hipStreamSynchronize(st));
+        return (int64_t)G;
+    };
+    KLAUNCH("dna_flags", 8.0 * (double)n, k_dna_flags, dim3(nblocks(n)), dim3(kB), 0, st, keys, n, fs, fe);
+    // group lists: current round and next round, (start, exclusive end) in vals
+    for (int q : {S_MISC0, S_MISC1, S_IDX9, S_IDX10}) c.slot[q].ensure((size_t)(n / 2 + 64) * 4);
+    c.slot[S_IDX8].ensure((size_t)n * 4 + 64);
+    c.slot[S_IDX11].ensure((size_t)n * 4 + 64);
+    uint32_t *kb = c.slot[S_IDX11].as<uint32_t>();   // a round's keys, aligned with vals
+    uint32_t *gs = c.slot[S_MISC0].as<uint32_t>(), *ge = c.slot[S_MISC1].as<uint32_t>();
+    uint32_t *xs = c.slot[S_IDX9].as<uint32_t>(), *xe = c.slot[S_IDX10].as<uint32_t>();
+    uint32_t *rank = c.slot[S_IDX8].as<uint32_t>();
+    int64_t G = groups(fs, ps, fe, pe, n, gs, ge);
+    KLAUNCH("dna_rank0", 12.0 * (double)n, k_dna_rank0, dim3(nblocks(n)), dim3(kB), 0, st, vals, ps, pe, gs, n, rank);
+    if (G) KLAUNCH("dna_short_fix", 0.0, k_dna_short_fix, dim3(1), dim3(1024), 0, st, vals, rank, gs, ge, G, n);
+
+    std::vector<uint32_t> lstart, lsize, loff;
+    for (int64_t h = 16; G > 0; h *= 2) {
+        if (h >= 2 * n) return false;   // cannot happen ('$' is unique); the general path if it does
+        // the keys are dead: class lists (5 x (start, size), capacity G each) and
+        // the large-group table (3 x <= G) live in their buffer
+        c.slot[S_IDX0].ensure((size_t)(13 * G + 16) * 4);
+        keys = c.slot[S_IDX0].as<uint32_t>();
+        uint32_t *cs = keys, *cz = keys + kClasses * G;
+        HIPCHECK(hipMemsetAsync(counts, 0, 64, st));
+        KLAUNCH("dna_classify", 0.0, k_dna_classify, dim3(nblocks(G)), dim3(kB), 0, st, gs, ge, G, cs, cz, counts, G);
+        uint32_t cnt[kClasses];
+        HIPCHECK(hipMemcpyAsync(cnt, counts, sizeof cnt, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        uint32_t *ncnt = counts + 8;
+        const int per_block = kLB / 64;
+        const unsigned gw[3] = {nblocks(cnt[0], per_block * 16), nblocks(cnt[1], per_block * 4),
+                                nblocks(cnt[2], per_block)};
+        // gather pass over every class, then the sorts (large groups gather
+        // straight into their radix keys, before any head is rewritten)
+        if (cnt[0])
+            KLAUNCH("dna_ls_keys", 0.0, (k_ls_wave<4, true>), dim3(gw[0]), dim3(kLB), 0, st, cs, cz, (int64_t)cnt[0], vals,
+                    rank, kb, n, h, xs, xe, ncnt);
+        if (cnt[1])
+            KLAUNCH("dna_ls_keys", 0.0, (k_ls_wave<16, true>), dim3(gw[1]), dim3(kLB), 0, st, cs + G, cz + G,
+                    (int64_t)cnt[1], vals, rank, kb, n, h, xs, xe, ncnt);
+        if (cnt[2])
+            KLAUNCH("dna_ls_keys", 0.0, (k_ls_wave<64, true>), dim3(gw[2]), dim3(kLB), 0, st, cs + 2 * G, cz + 2 * G,
+                    (int64_t)cnt[2], vals, rank, kb, n, h, xs, xe, ncnt);
+        if (cnt[3])
+            KLAUNCH("dna_ls_keys", 0.0, k_ls_block<true>, dim3(cnt[3]), dim3(kWB), 0, st, cs + 3 * G, cz + 3 * G, vals,
+                    rank, kb, n, h, xs, xe, ncnt);
+        const int64_t L = cnt[4];
+        int64_t M = 0;
+        uint32_t *tab = keys + 2 * kClasses * G;
+        uint64_t *rk = nullptr;
+        uint32_t *rv = nullptr;
+        dim3 grid2;
+        if (L) {
+            if (L > 65535) return false;   // grid.y bound: such texts take the general path
+            lstart.resize((size_t)L);
+            lsize.resize((size_t)L);
+            loff.resize((size_t)L);
+            HIPCHECK(hipMemcpyAsync(lstart.data(), cs + 4 * G, (size_t)L * 4, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipMemcpyAsync(lsize.data(), cz + 4 * G, (size_t)L * 4, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipStreamSynchronize(st));
+            uint32_t mx = 0;
+            for (int64_t q = 0; q < L; ++q) {
+                loff[(size_t)q] = (uint32_t)M;
+                M += lsize[(size_t)q];
+                mx = std::max(mx, lsize[(size_t)q]);
+            }
+            c.slot[S_IDX7].ensure((size_t)M * 8 + 64);
+            c.slot[S_MISC2].ensure((size_t)M * 4 + 64);
+            rk = c.slot[S_IDX7].as<uint64_t>();
+            rv = c.slot[S_MISC2].as<uint32_t>();
+            HIPCHECK(hipMemcpyAsync(tab, lstart.data(), (size_t)L * 4, hipMemcpyHostToDevice, st));
+            HIPCHECK(hipMemcpyAsync(tab + L, lsize.data(), (size_t)L * 4, hipMemcpyHostToDevice, st));
+            HIPCHECK(hipMemcpyAsync(tab + 2 * L, loff.data(), (size_t)L * 4, hipMemcpyHostToDevice, st));
+            grid2 = dim3((unsigned)std::min<int64_t>(64, (mx + kB - 1) / kB), (unsigned)L);
+            KLAUNCH("dna_refine_keys", 0.0, k_dna_refine_keys, grid2, dim3(kB), 0, st, tab, tab + L, tab + 2 * L, vals,
+                    rank, n, h, rk, rv);
+        }
+        if (cnt[0])
+            KLAUNCH("dna_ls_w4", 0.0, (k_ls_wave<4, false>), dim3(gw[0]), dim3(kLB), 0, st, cs, cz, (int64_t)cnt[0], vals,
+                    rank, kb, n, h, xs, xe, ncnt);
+        if (cnt[1])
+            KLAUNCH("dna_ls_w16", 0.0, (k_ls_wave<16, false>), dim3(gw[1]), dim3(kLB), 0, st, cs + G, cz + G,
+                    (int64_t)cnt[1], vals, rank, kb, n, h, xs, xe, ncnt);
+        if (cnt[2])
+            KLAUNCH("dna_ls_w64", 0.0, (k_ls_wave<64, false>), dim3(gw[2]), dim3(kLB), 0, st, cs + 2 * G, cz + 2 * G,
+                    (int64_t)cnt[2], vals, rank, kb, n, h, xs, xe, ncnt);
+        if (cnt[3])
+            KLAUNCH("dna_ls_block", 0.0, k_ls_block<false>, dim3(cnt[3]), dim3(kWB), 0, st, cs + 3 * G, cz + 3 * G, vals,
+                    rank, kb, n, h, xs, xe, ncnt);
+        uint32_t nc = 0;
+        HIPCHECK(hipMemcpyAsync(&nc, ncnt, 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        int64_t next = nc;
+        if (L) {   // large groups: one segmented radix pass
+            int qb = 1;
+            while ((1ll << qb) < L) ++qb;
+            radix_sort_pairs32(c, rk, rv, M, 0, ((30 + qb + 7) / 8) * 8);
+            KLAUNCH("dna_refine_back", 0.0, k_dna_refine_back, grid2, dim3(kB), 0, st, tab, tab + L, tab + 2 * L, rv,
+                    vals);
+            KLAUNCH("dna_refine_flags", 0.0, k_dna_refine_flags, dim3(nblocks(M)), dim3(kB), 0, st, rk, M, fs, fe);
+            const int64_t Gl = groups(fs, ps, fe, pe, M, xs + nc, xe + nc);
+            KLAUNCH("dna_refine_rank", 0.0, k_dna_refine_rank, dim3(nblocks(M)), dim3(kB), 0, st, rk, rv, ps, pe,
+                    xs + nc, tab, tab + 2 * L, M, rank);
+            if (Gl)
+                KLAUNCH("dna_refine_pos", 0.0, k_dna_refine_pos, dim3(nblocks(Gl)), dim3(kB), 0, st, rk, tab,
+                        tab + 2 * L, xs + nc, xe + nc, Gl);
+            next += Gl;
+        }
+        std::swap(gs, xs);
+        std::swap(ge, xe);
+        G = next;
+    }
+    KLAUNCH("dna_final", 9.0 * (double)n, k_dna_final, dim3(nblocks(n)), dim3(kB), 0, st, vals, n, SA, BWT);
+    HIPCHECK(hipGetLastError());
+    return true;
+}
+
+}  // namespace bwtmi

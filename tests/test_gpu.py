@@ -343,6 +343,43 @@ def test_index_repetitive_text(gpu_ctx):
     _check_index(b"CA" * 2000 + b"C" + b"$")
 
 
+@pytest.mark.parametrize("case", ["tiny", "edges", "groups", "long_lcp", "many_arrays", "homopolymer_peel"])
+def test_dna_suffix_sort_vs_oracle(gpu_ctx, case):
+    """The ACGT* '$' string sort (sa_dna.hip) against the oracle's prefix
+    doubling: texts built to hit every group class -- pairs (thread sort),
+    tens to a thousand members (workgroup bitonic sort), many short arrays
+    sharing a 16-mer (radix refinement rounds), long common prefixes, and
+    suffixes running into the end inside a tied key."""
+    r = np.random.default_rng(sum(map(ord, case)))
+    B = np.frombuffer(b"ACGT", dtype=np.uint8)
+
+    def rnd(k):
+        return B[r.integers(0, 4, k)].tobytes()
+    if case == "tiny":
+        for t in (b"A", b"C", b"AC", b"CA", b"AAAA", b"ACGTACGT", b"TTTTTTTTTTTTTTTTTAAAA"):
+            _check_index(t + b"$")
+        return
+    if case == "edges":      # the last 16 suffixes tie with A-padded keys of inner ones
+        t = rnd(500) + b"A" * 40 + rnd(30) + b"AC" + b"A" * 14
+    elif case == "groups":   # random duplicated 16-40-mers: groups of 2..60 members
+        parts = []
+        for _ in range(300):
+            w = rnd(int(r.integers(16, 40)))
+            parts += [w + rnd(int(r.integers(1, 30))) for _ in range(int(r.integers(2, 60)))]
+        t = b"".join(parts)
+    elif case == "long_lcp":  # long tandem arrays: groups with thousands of equal bases
+        t = rnd(200) + rnd(120) * 30 + rnd(300) + rnd(7) * 400 + rnd(50) + rnd(97) * 25 + rnd(100)
+    elif case == "many_arrays":   # > 1024 arrays of the same short units: refinement rounds
+        parts = []
+        for _ in range(3000):
+            parts.append(rnd(int(r.integers(5, 40))))
+            parts.append([b"AC", b"G", b"CAG", b"TTA"][int(r.integers(0, 4))] * int(r.integers(6, 30)))
+        t = b"".join(parts)
+    else:   # one base repeated: a large group that loses 16 suffixes per round
+        t = rnd(300) + b"G" * 2500 + rnd(300)
+    _check_index(t + b"$")
+
+
 def test_backward_search_all_short_motifs(gpu_ctx):
     from bwtmi import BWTCore, MotifUtils, synth
     text = synth.generate_contig(50000, 77) + b"$"

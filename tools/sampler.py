@@ -87,9 +87,28 @@ def main():
             name = tab[k][1] if k >= 0 else name
         by_fn[f"{os.path.basename(mod)[:18]}: {name}"] += cnt
     tot = sum(by_fn.values())
+    # source lines of the hottest libbwtmi addresses (needs -g; addr2line -i shows the inline chain)
+    hot = collections.Counter()
+    for line in open(raw):
+        mod, off, cnt = line.split()
+        if "libbwtmi" in mod:
+            hot[(mod, int(off, 16))] += int(cnt)
+    lines = collections.Counter()
+    top = hot.most_common(400)
+    if top:
+        mod = top[0][0][0]
+        delta = tabs[mod][1] if mod in tabs else 0
+        for ((m, off), c) in top:   # innermost inlined frame of each address
+            r = subprocess.run(["addr2line", "-e", m, "-C", "-f", hex(off + delta)], stdout=subprocess.PIPE,
+                               text=True).stdout.splitlines()
+            if len(r) >= 2:
+                lines[f"{r[1].split('/')[-1]} {r[0][:60]}"] += c
     with open(prefix + ".txt", "w") as f:
         for name, c in by_fn.most_common(80):
             f.write(f"{100.0 * c / tot:6.2f}% {c:8d} {name[:160]}\n")
+        f.write("\n-- hottest source lines (libbwtmi)\n")
+        for name, c in lines.most_common(60):
+            f.write(f"{100.0 * c / tot:6.2f}% {c:8d} {name}\n")
     print(open(prefix + ".txt").read()[:6000])
     os.unlink(fa)
     os.unlink(out)
