@@ -147,23 +147,50 @@ __global__ __launch_bounds__(256) void k_bwt(const uint8_t *__restrict__ t, cons
     bwt[r] = t[p < 0 ? p + n : p];
 }
 
-// per 128-byte block counts of each present code: one wave per block (occ_sample = 128)
+// zero bytes of y, exactly (no carries between bytes)
+__device__ __forceinline__ uint32_t zero_bytes(uint64_t y) {
+    constexpr uint64_t lo7 = 0x7f7f7f7f7f7f7f7full;
+    const uint64_t t = ~(((y & lo7) + lo7) | y | lo7);
+    return (uint32_t)__popcll(t);
+}
+
+// per occ_sample-byte block counts of each present code: one thread per block,
+// 16-byte loads, SWAR byte compares + popcount (the BWT buffer is padded)
 __global__ __launch_bounds__(256) void k_occ_blocks(const uint8_t *__restrict__ bwt, int64_t n, int64_t nblk, int blk,
                                                     const uint8_t *__restrict__ present, int sigma,
                                                     uint32_t *__restrict__ cnt /* [sigma][nblk+1] */) {
-    const int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int lane = threadIdx.x & 63;
-    if (wv >= nblk) return;
-    const int64_t base = wv * blk;
-    for (int c = 0; c < sigma; ++c) {
-        const uint8_t code = present[c];
-        uint32_t s = 0;
-        for (int o = lane; o < blk; o += 64) {
-            const int64_t i = base + o;
-            s += (i < n && bwt[i] == code) ? 1u : 0u;
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblk) return;
+    constexpr int kMaxSig = 16;
+    uint32_t s[kMaxSig] = {0};
+    uint64_t pat[kMaxSig];
+    // 16-byte loads need 16-aligned blocks; other sample rates take the byte loop
+    const int sg = (blk & 15) ? 0 : (sigma < kMaxSig ? sigma : kMaxSig);
+    for (int c = 0; c < sg; ++c) pat[c] = 0x0101010101010101ull * present[c];
+    const int64_t base = b * blk;
+    for (int o = 0; o < blk && sg; o += 16) {
+        const int64_t i = base + o;
+        if (i >= n) break;
+        const uint4 v = *reinterpret_cast<const uint4 *>(bwt + i);
+        uint64_t w0 = ((uint64_t)v.y << 32) | v.x, w1 = ((uint64_t)v.w << 32) | v.z;
+        const int64_t left = n - i;   // bytes past n must not count: force them to differ
+        uint64_t m0 = ~0ull, m1 = ~0ull;
+        if (left < 16) {
+            m0 = left >= 8 ? ~0ull : (left <= 0 ? 0ull : (~0ull >> (64 - 8 * left)));
+            m1 = left <= 8 ? 0ull : (~0ull >> (64 - 8 * (left - 8)));
         }
-        for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
-        if (lane == 0) cnt[(int64_t)c * (nblk + 1) + wv] = s;
+        for (int c = 0; c < sg; ++c) {
+            // a byte outside the text is made to differ from the pattern
+            const uint64_t y0 = (w0 ^ pat[c]) | (~m0 & 0x0101010101010101ull);
+            const uint64_t y1 = (w1 ^ pat[c]) | (~m1 & 0x0101010101010101ull);
+            s[c] += zero_bytes(y0) + zero_bytes(y1);
+        }
+    }
+    for (int c = 0; c < sg; ++c) cnt[(int64_t)c * (nblk + 1) + b] = s[c];
+    for (int c = sg; c < sigma; ++c) {   // alphabets past 16 symbols: byte loop
+        uint32_t x = 0;
+        for (int o = 0; o < blk && base + o < n; ++o) x += bwt[base + o] == present[c];
+        cnt[(int64_t)c * (nblk + 1) + b] = x;
     }
 }
 
@@ -224,9 +251,33 @@ __global__ void k_kentries(const uint8_t *__restrict__ t, int64_t n, int k, cons
     vals[e] = (uint32_t)(i - k + 1);
 }
 
+// ACGT* '$' texts: every 8-mer that ends before the '$' is an entry, in
+// position order (p = 0 .. n-9), so the entries need no compaction; codes
+// A0 C1 G2 T3 as kbits.  Four positions per thread from one 12-byte window.
+__global__ __launch_bounds__(256) void k_kmer_dna(const uint8_t *__restrict__ t, int64_t n,
+                                                  uint32_t *__restrict__ keys, uint32_t *__restrict__ pos) {
+    const int64_t p0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    const int64_t m = n - 8;
+    if (p0 >= m) return;
+    uint32_t w = 0;   // codes of t[p0 .. p0+10], first in the high bits
+#pragma unroll
+    for (int q = 0; q < 11; ++q) {
+        const int64_t i = p0 + q;
+        const uint8_t ch = i < n ? t[i] : (uint8_t)'A';
+        w = (w << 2) | (uint32_t)(((ch >> 2) ^ (ch >> 1)) & 3u);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (p0 + q < m) {
+            keys[p0 + q] = (w >> (2 * (3 - q))) & 0xffffu;
+            pos[p0 + q] = (uint32_t)(p0 + q);
+        }
+}
+
 // CSR offsets from the sorted k-mer codes: boundary i (between keys[i-1] and
 // keys[i]) owns the codes (keys[i-1], keys[i]]; every code is written once
-__global__ void k_kbounds(const uint64_t *__restrict__ keys, int64_t m, int64_t *__restrict__ off) {
+template <typename KT>
+__global__ void k_kbounds(const KT *__restrict__ keys, int64_t m, int64_t *__restrict__ off) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > m) return;
     const int64_t prev = i == 0 ? -1 : (int64_t)keys[i - 1];
@@ -460,7 +511,7 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     ix->occ.ensure((size_t)sigma * (nblk + 1) * 4);
     HIPCHECK(hipMemsetAsync(ix->occ.p, 0, (size_t)sigma * (nblk + 1) * 4, st));
     HIPCHECK(hipMemcpyAsync(c.slot[S_MISC3].p, present, 256, hipMemcpyHostToDevice, st));
-    KLAUNCH("occ_blocks", (double)n + (double)sigma * (double)(nblk + 1) * 4.0, k_occ_blocks, dim3(blocks(nblk * 64)), dim3(256), 0, st, ix->bwt.as<uint8_t>(), n, nblk,
+    KLAUNCH("occ_blocks", (double)n + (double)sigma * (double)(nblk + 1) * 4.0, k_occ_blocks, dim3(blocks(nblk)), dim3(256), 0, st, ix->bwt.as<uint8_t>(), n, nblk,
                        occ_sample, c.slot[S_MISC3].as<uint8_t>(), sigma, ix->occ.as<uint32_t>());
     for (int cc = 0; cc < sigma; ++cc) {
         uint32_t *row = ix->occ.as<uint32_t>() + (int64_t)cc * (nblk + 1);
@@ -473,7 +524,21 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
 
     // ------------------------------------------------------------ 8-mer hash
     const int K = 8;
-    if (!(flags & BWTMI_INDEX_NO_KMER) && n >= K) {
+    if (!(flags & BWTMI_INDEX_NO_KMER) && n >= K + 1 && dna) {
+        // every char but the final '$' is valid: n-8 entries, one stable
+        // 16-bit radix sort of (code, position)
+        ix->has_kmer = true;
+        const int64_t nent = n - K;
+        uint32_t *k32 = c.slot[S_IDX0].as<uint32_t>();
+        ix->kmer_pos.ensure((size_t)nent * 4);
+        KLAUNCH("kmer_dna", 3.0 * (double)n + 8.0 * (double)nent, k_kmer_dna, dim3(blocks((nent + 3) / 4)), dim3(256),
+                0, st, T, n, k32, ix->kmer_pos.as<uint32_t>());
+        radix_sort_pairs_k32(c, k32, ix->kmer_pos.as<uint32_t>(), nent, 0, 16);
+        ix->kmer_off.ensure((size_t)(65537) * 8);
+        KLAUNCH("k_kbounds", 0.0, k_kbounds<uint32_t>, dim3(blocks(nent + 1)), dim3(256), 0, st, k32, nent,
+                ix->kmer_off.as<int64_t>());
+        ix->kmer_count = nent;
+    } else if (!(flags & BWTMI_INDEX_NO_KMER) && n >= K) {
         ix->has_kmer = true;
         KLAUNCH("k_kvalid", 0.0, k_kvalid, dim3(blocks(n)), dim3(256), 0, st, T, n, flag);
         exclusive_scan<uint32_t>(c, flag, head, n);   // head = vpos
@@ -496,7 +561,7 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
             radix_sort_pairs32(c, keys, ix->kmer_pos.as<uint32_t>(), nent, 0, 16);
         }
         ix->kmer_off.ensure((size_t)(65537) * 8);
-        KLAUNCH("k_kbounds", 0.0, k_kbounds, dim3(blocks(nent + 1)), dim3(256), 0, st, keys, nent,
+        KLAUNCH("k_kbounds", 0.0, k_kbounds<uint64_t>, dim3(blocks(nent + 1)), dim3(256), 0, st, keys, nent,
                            ix->kmer_off.as<int64_t>());
         ix->kmer_count = nent;
     }
