@@ -152,6 +152,12 @@ using RecVec = std::vector<Rec, BigAlloc<Rec>>;
 // motif utilities (MotifUtils, bwt.py:675-1381)
 std::string min_rotation(const std::string &s);
 void canonical_stranded(const std::string &s, std::string &canon, char &strand);
+char canonical_strand(const char *s, int64_t n);   // the strand of canonical_stranded only
+// ACGT strings of <= 32 bases as 2-bit codes (A0 C1 G2 T3, first base high):
+// rotations compare as integers, rc2 = reverse complement, min_rot2 = least rotation
+bool pack2_acgt(const char *s, int64_t n, uint64_t &x);
+uint64_t rc2(uint64_t x, int64_t n);
+uint64_t min_rot2(uint64_t x, int64_t n);
 int64_t smallest_period(const char *s, int64_t n);
 double entropy_of(const char *s, int64_t n);
 void composition_of(const char *s, int64_t n, double out[4]);

@@ -1,6 +1,8 @@
 // motif.cpp -- exact host restatement of the MotifUtils pieces on the CLI path.
 // Float arithmetic follows the Python expressions operation by operation; the
 // library is built with -ffp-contract=off so no FMA changes a rounding.
+#include <immintrin.h>
+
 #include <algorithm>
 #include <charconv>
 #include <cmath>
@@ -62,11 +64,58 @@ static inline char comp_base(char c) {       // bwt.py:688-691
     }
 }
 
+bool pack2_acgt(const char *s, int64_t n, uint64_t &x) {
+    if (n > 32) return false;
+    x = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        uint64_t c;
+        switch (s[i]) {
+            case 'A': c = 0; break;
+            case 'C': c = 1; break;
+            case 'G': c = 2; break;
+            case 'T': c = 3; break;
+            default: return false;
+        }
+        x = (x << 2) | c;
+    }
+    return true;
+}
+
+uint64_t rc2(uint64_t x, int64_t n) {
+    x = ~x;   // complement: 3 - code
+    x = ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
+    x = ((x >> 4) & 0x0f0f0f0f0f0f0f0full) | ((x & 0x0f0f0f0f0f0f0f0full) << 4);
+    x = __builtin_bswap64(x);   // 2-bit groups reversed over the whole word
+    return n ? x >> (64 - 2 * n) : 0;
+}
+
+uint64_t min_rot2(uint64_t x, int64_t n) {
+    if (n <= 1) return x;
+    const int bits = (int)(2 * n);
+    const uint64_t mask = bits == 64 ? ~0ull : ((1ull << bits) - 1);
+    uint64_t best = x;
+    for (int sh = 2; sh < bits; sh += 2) {
+        const uint64_t r = ((x << sh) | (x >> (bits - sh))) & mask;
+        best = r < best ? r : best;
+    }
+    return best;
+}
+
 void canonical_stranded(const std::string &s, std::string &canon, char &strand) {  // 694-716
     const int64_t n = (int64_t)s.size();
     if (n == 0) {
         canon.clear();
         strand = '+';
+        return;
+    }
+    uint64_t x;
+    if (pack2_acgt(s.data(), n, x)) {   // least rotations of s and rc(s) over packed words
+        const uint64_t bf = min_rot2(x, n), br = min_rot2(rc2(x, n), n);
+        const bool fwd = bf <= br;
+        const uint64_t v = fwd ? bf : br;
+        canon.resize((size_t)n);
+        for (int64_t i = 0; i < n; ++i) canon[(size_t)i] = "ACGT"[(v >> (2 * (n - 1 - i))) & 3u];
+        strand = fwd ? '+' : '-';
         return;
     }
     thread_local std::vector<int32_t> f;
@@ -82,6 +131,16 @@ void canonical_stranded(const std::string &s, std::string &canon, char &strand) 
     const bool fwd = std::memcmp(ss.data() + kf, rr.data() + kr, (size_t)n) <= 0;
     canon.assign((fwd ? ss.data() + kf : rr.data() + kr), (size_t)n);
     strand = fwd ? '+' : '-';
+}
+
+char canonical_strand(const char *s, int64_t n) {
+    uint64_t x;
+    if (n > 0 && pack2_acgt(s, n, x)) return min_rot2(x, n) <= min_rot2(rc2(x, n), n) ? '+' : '-';
+    thread_local std::string t, c;
+    t.assign(s, (size_t)n);
+    char st;
+    canonical_stranded(t, c, st);
+    return st;
 }
 
 int64_t smallest_period(const char *s, int64_t n) {   // bwt.py:1125-1133
@@ -152,6 +211,7 @@ namespace {
 
 struct Scratch {
     std::vector<int32_t> cost;
+    std::vector<unsigned char> wpad;           // the window with 64 bytes of 0xff on each side
     std::vector<char> ptr;
     std::vector<char> cref, cqry;              // aligned columns (reversed)
     std::vector<int64_t> obs_idx;              // observed bases of the current copy
@@ -177,6 +237,92 @@ inline void put_num(std::string &s, int64_t v) {
     s.append(b, (size_t)(r.ptr - b));
 }
 
+template <typename CostF>
+bool finish_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_t lower, int64_t upper,
+                 int64_t band, int64_t W, int32_t INF, int64_t tol, int64_t max_indel, CostF cost, Scratch &S,
+                 UnitOut &res);
+
+// The banded DP of align_unit in diagonal coordinates, one AVX-512 register
+// per row: cell (i, j) sits in lane d = j - i + band (W = 2 band + 1 <= 25 of
+// 32 lanes), so the diagonal neighbour is lane d of the previous row, the one
+// above is lane d + 1 and the left one lane d - 1.  Substitution/deletion are
+// lane-parallel; the insertion chain cur[j] = min(base[j], cur[j-1] + 1) is a
+// prefix minimum of base[d] - d (5 shift/min steps).  Choices and tie order are
+// the scalar loop's: match/sub, then deletion if strictly cheaper, then
+// insertion if strictly cheaper.  ptr rows get the same codes at the same
+// offsets (row i at i*W, 32 bytes written per row: rows are written in order
+// and the buffer has 32 bytes of slack).  Returns 0 = reject (the row-min
+// test), 1 = done; last[d] = row m.
+__attribute__((target("avx512f,avx512bw,avx512vl"))) static int dp_rows_avx512(
+    const char *motif, int64_t m, const unsigned char *wp, int64_t n, int64_t band, int32_t INF, int32_t reject,
+    char *ptr, int64_t W, int16_t *last) {
+    const __m512i iota = _mm512_set_epi16(31, 30, 29, 28, 27, 26, 25, 24, 23, 22, 21, 20, 19, 18, 17, 16, 15, 14, 13,
+                                          12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0);
+    const __m512i inf = _mm512_set1_epi16((int16_t)INF), one = _mm512_set1_epi16(1);
+    const __m512i up_idx = _mm512_add_epi16(iota, one);   // lane d <- lane d + 1 (lane 31 masked)
+    __m512i sh_idx[5];
+    __mmask32 sh_mask[5];
+    for (int q = 0; q < 5; ++q) {   // lane d <- lane d - 2^q
+        sh_idx[q] = _mm512_sub_epi16(iota, _mm512_set1_epi16((int16_t)(1 << q)));
+        sh_mask[q] = (__mmask32)(0xffffffffu << (1 << q));
+    }
+    const __m512i cS = _mm512_set1_epi16('S'), cM = _mm512_set1_epi16('M'), cD = _mm512_set1_epi16('D'),
+                  cI = _mm512_set1_epi16('I');
+    // row 0: cost j for j in [0, n] (every column), lane d -> j = d - band
+    const __m512i j0 = _mm512_sub_epi16(iota, _mm512_set1_epi16((int16_t)band));
+    const __mmask32 r0 = _mm512_cmpge_epi16_mask(j0, _mm512_setzero_si512()) &
+                         _mm512_cmple_epi16_mask(j0, _mm512_set1_epi16((int16_t)n));
+    __m512i prev = _mm512_mask_mov_epi16(inf, r0, j0);
+    for (int64_t i = 1; i <= m; ++i) {
+        const int64_t jmin = std::max<int64_t>(1, i - band), jmax = std::min<int64_t>(n, i + band);
+        const int64_t dlo = jmin - i + band, dhi = jmax - i + band;
+        __mmask32 valid = dhi >= dlo ? (__mmask32)(((1ull << (dhi + 1)) - 1) & ~((1ull << dlo) - 1)) : 0;
+        // text: lane d compares win[j - 1] = wp[i - band - 1 + d]
+        const __m512i tv = _mm512_cvtepu8_epi16(_mm256_loadu_si256((const __m256i *)(wp + (i - band - 1))));
+        const __mmask32 eq = _mm512_cmpeq_epi16_mask(tv, _mm512_set1_epi16((int16_t)(unsigned char)motif[i - 1]));
+        const __m512i p1 = _mm512_add_epi16(prev, one);
+        const __m512i sub = _mm512_mask_mov_epi16(p1, eq, prev);
+        const __m512i up = _mm512_mask_permutexvar_epi16(inf, (__mmask32)0x7fffffffu, up_idx, prev);
+        const __m512i dc = _mm512_add_epi16(up, one);
+        const __mmask32 isD = _mm512_cmplt_epi16_mask(dc, sub);
+        __m512i base = _mm512_mask_mov_epi16(inf, valid, _mm512_min_epi16(sub, dc));
+        __mmask32 keep = valid;
+        if (i <= band) {   // column 0 (j = 0): cost i, the left end of the chain
+            const __mmask32 c0 = (__mmask32)(1u << (band - i));
+            base = _mm512_mask_mov_epi16(base, c0, _mm512_set1_epi16((int16_t)i));
+            keep |= c0;
+        }
+        __m512i t = _mm512_sub_epi16(base, iota);
+        // row band + 1: column 0 (cost i) is the left neighbour of lane 0 --
+        // the scalar loop's cur[jmin - 1] -- one lane below the register
+        if (i == band + 1) t = _mm512_min_epi16(t, _mm512_set1_epi16((int16_t)(i + 1)));
+        for (int q = 0; q < 5; ++q)
+            t = _mm512_min_epi16(t, _mm512_mask_permutexvar_epi16(inf, sh_mask[q], sh_idx[q], t));
+        const __m512i fin = _mm512_mask_mov_epi16(inf, keep, _mm512_add_epi16(t, iota));
+        const __mmask32 isI = _mm512_cmplt_epi16_mask(fin, base) & valid;
+        __m512i code = _mm512_mask_mov_epi16(cS, eq, cM);
+        code = _mm512_mask_mov_epi16(code, isD, cD);
+        code = _mm512_mask_mov_epi16(code, isI, cI);
+        _mm256_storeu_si256((__m256i *)(ptr + i * W), _mm512_cvtepi16_epi8(code));
+        // row minimum over the band (INF elsewhere)
+        const __m512i fv = _mm512_mask_mov_epi16(inf, valid, fin);
+        __m256i h = _mm256_min_epu16(_mm512_castsi512_si256(fv), _mm512_extracti64x4_epi64(fv, 1));
+        __m128i h2 = _mm_min_epu16(_mm256_castsi256_si128(h), _mm256_extracti128_si256(h, 1));
+        const int32_t rowmin = (int32_t)(uint16_t)_mm_cvtsi128_si32(_mm_minpos_epu16(h2));
+        if (rowmin > reject && (jmin > 1 || i > reject)) return 0;
+        prev = fin;
+    }
+    _mm512_storeu_si512((void *)last, prev);
+    return 1;
+}
+
+static const bool g_avx512 = [] {
+    __builtin_cpu_init();
+    const char *e = std::getenv("BWTMI_NO_AVX512");
+    return !(e && *e == '1') && __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+           __builtin_cpu_supports("avx512vl");
+}();
+
 // ops of one copy are formatted with a placeholder-free prefix; the copy index
 // is prepended when the copy is accepted (ops hold "pos:..." pieces)
 bool align_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_t max_indel, int64_t tol,
@@ -194,8 +340,20 @@ bool align_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_
     const int32_t INF = (int32_t)(m + n + 10);
     const int64_t band = max_indel + 2;
     const int64_t W = 2 * band + 1;
-    const size_t cells = (size_t)((m + 1) * W);
+    const size_t cells = (size_t)((m + 1) * W) + 32;
     if (S.ptr.size() < cells) S.ptr.resize(cells);
+    const int32_t reject = (int32_t)(tol + 2 * max_indel);
+    if (g_avx512 && W <= 31 && INF < 30000) {
+        // 64 bytes of never-matching padding on both sides of the window
+        if (S.wpad.size() < (size_t)(n + 128)) S.wpad.resize((size_t)(n + 128));
+        std::memset(S.wpad.data(), 0xff, 64);
+        std::memcpy(S.wpad.data() + 64, win, (size_t)n);
+        std::memset(S.wpad.data() + 64 + n, 0xff, 64);
+        alignas(64) int16_t last[32];
+        if (!dp_rows_avx512(motif, m, S.wpad.data() + 64, n, band, INF, reject, S.ptr.data(), W, last)) return false;
+        return finish_unit(motif, m, win, n, lower, upper, band, W, INF, tol, max_indel,
+                           [&](int64_t j) -> int64_t { return last[j - m + band]; }, S, res);
+    }
     if (S.cost.size() < (size_t)(2 * (n + 2))) S.cost.resize((size_t)(2 * (n + 2)));
     char *ptr = S.ptr.data();
     int32_t *prev = S.cost.data(), *cur = prev + (n + 2);
@@ -205,7 +363,6 @@ bool align_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_
     // costs never decrease along a path, so once a whole row exceeds
     // tol + 2*max_indel every alignment has n_sub > tol or an indel count
     // > max_indel, and the copy is rejected below anyway
-    const int32_t reject = (int32_t)(tol + 2 * max_indel);
     for (int64_t i = 1; i <= m; ++i) {
         const int64_t jmin = std::max<int64_t>(1, i - band), jmax = std::min<int64_t>(n, i + band);
         const char mi = motif[i - 1];
@@ -241,12 +398,26 @@ bool align_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_
         std::swap(prev, cur);
     }
     // prev = row m over [max(1, m-band), min(n, m+band)]; column 0 reads m
+    return finish_unit(motif, m, win, n, lower, upper, band, W, INF, tol, max_indel,
+                       [&](int64_t j) -> int64_t { return j == 0 ? m : prev[j]; }, S, res);
+}
+
+// best end column on row m (first minimum in [lower, upper]), traceback and
+// the copy's ops / observed bases / acceptance (cost(j) = row m, column j)
+template <typename CostF>
+bool finish_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_t lower, int64_t upper,
+                 int64_t band, int64_t W, int32_t INF, int64_t tol, int64_t max_indel, CostF cost, Scratch &S,
+                 UnitOut &res) {
+    const char *ptr = S.ptr.data();
     int64_t bj = -1, bc = INF;
     for (int64_t j = lower; j <= upper; ++j) {
-        const int64_t c = j == 0 ? m : prev[j];
+        const int64_t c = cost(j);
         if (c < bc) { bc = c; bj = j; }
     }
     if (bj <= 0 || bc >= INF) return false;
+    // an accepted copy has n_sub <= tol and both indel counts <= max_indel, so
+    // its cost (= bc) is at most tol + 2 max_indel: skip the traceback otherwise
+    if (bc > tol + 2 * max_indel) return false;
     // traceback (columns collected in reverse)
     S.cref.clear();
     S.cqry.clear();

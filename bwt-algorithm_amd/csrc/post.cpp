@@ -306,6 +306,8 @@ struct Extra {                  // trivially destructible: strings live in the P
     std::string_view variations;  // ';'-joined, empty == None
     double copies = 0, confidence = 0, mm = 0, pmatch = 0, pindel = 0;
     int64_t max_mm = 0, n_eval = 0, score = 0;
+    int64_t req_end = -1;       // the (clamped) end and motif length the recompute
+    int32_t req_m = 0;          // was asked for
     int32_t tier = 2;
     char strand = '+';
     bool stats_none = false;    // Rec::stats_none
@@ -586,6 +588,7 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     start = std::max<int64_t>(0, start);
     end = end > 0 ? std::min(L, end) : L;
     if (end <= start) end = std::min(L, start + m);
+    const int64_t req_end = end;
     if (m == 1 && start < L) {
         // One-base motif (~75 % of the recomputes): align_repeat_region's closed
         // form (motif.cpp) without building any strings.  The template is
@@ -613,6 +616,8 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
         x.pindel = 0.0;
         x.score = trf_score(run, 0.0);
         x.tier = tier;
+        x.req_end = req_end;
+        x.req_m = (int32_t)m;
         Item it{};
         it.start = start;
         it.end = start + run;
@@ -672,12 +677,13 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     x.confidence = std::max(0.3, 1.0 - mm);
     x.mm = mm;
     x.n_eval = std::max<int64_t>(1, cint);
-    thread_local std::string canon;
-    canonical_stranded(*motif_s, canon, x.strand);
+    x.strand = canonical_strand(motif_s->data(), (int64_t)motif_s->size());
     x.pmatch = std::max(0.0, 100.0 - mm * 100.0);
     x.pindel = pind;
     x.score = trf_score(tl, mm);
     x.tier = tier;
+    x.req_end = req_end;
+    x.req_m = (int32_t)m;
     Item it{};
     it.start = start;
     it.end = start + tl;
@@ -714,13 +720,26 @@ inline const std::string &canon_get(const UnitCtx &u, const Item &it, Canon &c) 
 // get_canonical_motif_stranded(m1)[0] == ...(m2)[0] (bwt.py:694-716): the
 // canonical form is the least string over the rotations of m and of its
 // reverse complement, a set that is the same for every member, so equality
-// holds iff m2 is a rotation of m1 or of rc(m1).  Motifs up to 8 bytes are
-// compared as packed words; longer ones through the canonical strings.
+// holds iff m2 is a rotation of m1 or of rc(m1).  ACGT motifs up to 32 bases
+// compare as 2-bit words, other motifs up to 8 bytes as byte words, longer
+// ones through the canonical strings.
 inline bool same_canonical(const UnitCtx &u, const Item &r1, Canon &c1, const Item &r2, Canon &c2) {
     const std::string_view a = motif_of(u, r1), b = motif_of(u, r2);
     if (a.size() != b.size()) return false;
     const size_t m = a.size();
     if (m == 0) return true;
+    uint64_t pa, pb;
+    if (m <= 32 && pack2_acgt(a.data(), (int64_t)m, pa) && pack2_acgt(b.data(), (int64_t)m, pb)) {
+        const unsigned bits = (unsigned)(2 * m);
+        const uint64_t mask = bits == 64 ? ~0ull : ((1ull << bits) - 1);
+        const uint64_t pr = rc2(pa, (int64_t)m);
+        for (unsigned s = 0; s < bits; s += 2) {
+            const uint64_t rx = s ? (((pa << s) | (pa >> (bits - s))) & mask) : pa;
+            const uint64_t rr = s ? (((pr << s) | (pr >> (bits - s))) & mask) : pr;
+            if (rx == pb || rr == pb) return true;
+        }
+        return false;
+    }
     if (m > 8) return canon_get(u, r1, c1) == canon_get(u, r2, c2);
     uint64_t x = 0, r = 0, y = 0;
     for (size_t i = 0; i < m; ++i) {
@@ -1119,6 +1138,9 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
             for (int64_t k = a; k < b; ++k) {
                 Item &r = recs[(size_t)k];
                 if (!r.x || r.x->mm == 0.0) continue;
+                // a record whose recompute already covered exactly [start, end)
+                // would be recomputed with the same arguments: same result
+                if (r.mlen > 0 && r.mlen == r.x->req_m && r.x->req_end == r.end) continue;
                 int64_t m = r.mlen;
                 if (m <= 0) {
                     const int64_t rc = (int64_t)std::nearbyint(copies_of(r));

@@ -21,13 +21,30 @@
 #include <vector>
 
 namespace {
-constexpr size_t kCap = 1 << 22;
-uint64_t g_buf[kCap];
+constexpr size_t kCap = 1 << 20;
+constexpr int kDepth = 16;
+uint64_t g_buf[kCap][kDepth];
 volatile size_t g_n = 0;
 
-void on_prof(int, siginfo_t *, void *uc) {
+void on_prof(int, siginfo_t *, void *ucv) {
     const size_t i = __atomic_fetch_add(&g_n, 1, __ATOMIC_RELAXED);
-    if (i < kCap) g_buf[i] = (uint64_t)((ucontext_t *)uc)->uc_mcontext.gregs[REG_RIP];
+    if (i >= kCap) return;
+    const ucontext_t *uc = (const ucontext_t *)ucv;
+    uint64_t *o = g_buf[i];
+    o[0] = (uint64_t)uc->uc_mcontext.gregs[REG_RIP];
+    const uint64_t rsp = (uint64_t)uc->uc_mcontext.gregs[REG_RSP];
+    uint64_t fp = (uint64_t)uc->uc_mcontext.gregs[REG_RBP];
+    int d = 1;
+    // walk only inside this thread's stack: fp above rsp, increasing, aligned
+    while (d < kDepth && fp >= rsp && fp < rsp + (64u << 20) && (fp & 7) == 0) {
+        const uint64_t *f = (const uint64_t *)fp;
+        const uint64_t next = f[0], ret = f[1];
+        if (ret < 4096) break;
+        o[d++] = ret - 1;   // inside the call instruction
+        if (next <= fp) break;
+        fp = next;
+    }
+    if (d < kDepth) o[d] = 0;
 }
 }  // namespace
 
@@ -85,14 +102,27 @@ int sampler_stop(const char *path) {
     }
     std::map<std::pair<std::string, uint64_t>, uint64_t> hist;
     const size_t n = g_n < kCap ? g_n : kCap;
-    for (size_t i = 0; i < n; ++i) {
-        const uint64_t ip = g_buf[i];
-        std::string mod = "?";
-        uint64_t rel = ip;
+    auto locate = [&](uint64_t ip, std::string &mod, uint64_t &rel) {
+        mod = "?";
+        rel = ip;
         for (auto &m : maps)
-            if (ip >= m.a && ip < m.b) { mod = m.name; rel = ip - m.a + m.off; break; }
+            if (ip >= m.a && ip < m.b) { mod = m.name; rel = ip - m.a + m.off; return; }
+    };
+    std::string chains_path = std::string(path) + ".chains";
+    FILE *ch = std::fopen(chains_path.c_str(), "w");
+    for (size_t i = 0; i < n; ++i) {
+        std::string mod;
+        uint64_t rel;
+        locate(g_buf[i][0], mod, rel);
         ++hist[{mod, rel}];
+        if (!ch) continue;
+        for (int d = 0; d < kDepth && g_buf[i][d]; ++d) {
+            locate(g_buf[i][d], mod, rel);
+            std::fprintf(ch, d ? " %s:%lx" : "%s:%lx", mod.c_str(), (unsigned long)rel);
+        }
+        std::fputc('\n', ch);
     }
+    if (ch) std::fclose(ch);
     FILE *o = std::fopen(path, "w");
     if (!o) return -1;
     for (auto &kv : hist) std::fprintf(o, "%s %lx %lu\n", kv.first.first.c_str(), (unsigned long)kv.first.second, (unsigned long)kv.second);

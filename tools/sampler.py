@@ -42,6 +42,48 @@ def load_delta(path):
     return 0
 
 
+def inclusive(path, tabs):
+    """Samples per function anywhere on the stack (each function once per sample)."""
+    if not os.path.exists(path):
+        return collections.Counter()
+    chains = [line.split() for line in open(path)]
+    addrs = {}
+    for ch in chains:
+        for fr in ch:
+            mod, off = fr.rsplit(":", 1)
+            if "libbwtmi" in mod:
+                addrs.setdefault(mod, set()).add(int(off, 16))
+    names = {}
+    for mod, offs in addrs.items():
+        delta = tabs[mod][1] if mod in tabs else load_delta(mod)
+        offs = sorted(offs)
+        out = subprocess.run(["addr2line", "-e", mod, "-C", "-f", "-i", "-a"],
+                             input="\n".join(hex(o + delta) for o in offs), stdout=subprocess.PIPE,
+                             text=True).stdout.splitlines()
+        cur, k = None, 0
+        while k < len(out):
+            line = out[k]
+            if line.startswith("0x"):
+                cur = int(line, 16) - delta
+                names[(mod, cur)] = []
+                k += 1
+                continue
+            fn = line.replace("(anonymous namespace)::", "").split("(")[0].strip()
+            if not fn.startswith(("std::", "__", "operator", "void std::")):
+                names[(mod, cur)].append(fn[:100])
+            k += 2   # function line, then file:line
+    incl = collections.Counter()
+    for ch in chains:
+        seen = set()
+        for fr in ch:
+            mod, off = fr.rsplit(":", 1)
+            for fn in names.get((mod, int(off, 16)), [os.path.basename(mod)[:20]]):
+                seen.add(fn)
+        for fn in seen:
+            incl[fn] += 1
+    return incl
+
+
 def main():
     prefix = sys.argv[1]
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
@@ -103,12 +145,16 @@ def main():
                                text=True).stdout.splitlines()
             if len(r) >= 2:
                 lines[f"{r[1].split('/')[-1]} {r[0][:60]}"] += c
+    incl = inclusive(raw + ".chains", tabs)
     with open(prefix + ".txt", "w") as f:
         for name, c in by_fn.most_common(80):
             f.write(f"{100.0 * c / tot:6.2f}% {c:8d} {name[:160]}\n")
         f.write("\n-- hottest source lines (libbwtmi)\n")
         for name, c in lines.most_common(60):
             f.write(f"{100.0 * c / tot:6.2f}% {c:8d} {name}\n")
+        f.write("\n-- inclusive (frame-pointer chains; inlined frames from addr2line -i)\n")
+        for name, c in incl.most_common(80):
+            f.write(f"{100.0 * c / tot:6.2f}% {c:8d} {name[:150]}\n")
     print(open(prefix + ".txt").read()[:6000])
     os.unlink(fa)
     os.unlink(out)

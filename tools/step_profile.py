@@ -1,4 +1,4 @@
-"""Per-call wall time and minor page faults of the bench step on the GPU box
+"""Per-call wall time, CPU time (all threads) and minor page faults of the bench step on the GPU box
 (C3, one 100 Mbp contig).  usage: python tools/step_profile.py [steps] [contig_bp]"""
 import os, resource, sys, time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -24,8 +24,10 @@ for s in range(steps):
                      ("write", lambda: job.write("strfinder", out)), ("wait", lambda: job.wait(ctx))):
         if name == "scan":
             job.select([0])
-        f0 = resource.getrusage(resource.RUSAGE_SELF).ru_minflt
+        r0 = resource.getrusage(resource.RUSAGE_SELF)
         t = time.perf_counter(); fn(); dt = (time.perf_counter() - t) * 1e3
-        row.append(f"{name} {dt:.1f}ms/{resource.getrusage(resource.RUSAGE_SELF).ru_minflt - f0}pf")
+        r1 = resource.getrusage(resource.RUSAGE_SELF)
+        cpu = (r1.ru_utime + r1.ru_stime - r0.ru_utime - r0.ru_stime) * 1e3
+        row.append(f"{name} {dt:.1f}ms/cpu {cpu:.0f}ms/{r1.ru_minflt - r0.ru_minflt}pf")
     print(f"step {s}: " + "  ".join(row), " stages", [round(x, 1) for x in job.stage_ms()], flush=True)
 os.unlink(out)
