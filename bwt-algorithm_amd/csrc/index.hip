@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <cstdlib>
 #include <vector>
 
 #include "device.h"
@@ -39,6 +40,12 @@ struct DeviceIndex {
     int64_t kmer_count = 0;
     bool has_kmer = false;
     int64_t occ_len = 0, sampled_len = 0;
+    // ACGT* '$' texts: packed rank structure, one 32-byte block per 64 BWT rows:
+    // uint32 count[4] of A C G T before the block, then the rows' 2-bit codes
+    // as two bit planes (row 64b + k at bit k; '$' stored as A, dollar_row)
+    DBuf fm2;
+    bool has_fm2 = false;
+    int64_t dollar_row = -1;
 };
 
 namespace {
@@ -324,6 +331,107 @@ __global__ void k_kasai_serial(const uint8_t *__restrict__ t, const uint32_t *__
     }
 }
 
+// ---- packed FM rank for ACGT* '$' texts (bwt.py:335-357 semantics)
+// per block: planes and counts of A C G T (the '$' row is not counted)
+__global__ __launch_bounds__(256) void k_fm2_local(const uint8_t *__restrict__ bwt, int64_t n, int64_t nb,
+                                                   uint64_t *__restrict__ fm2, uint32_t *__restrict__ cnt4,
+                                                   unsigned long long *__restrict__ dollar) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    uint64_t lo = 0, hi = 0;
+    uint32_t c[4] = {0, 0, 0, 0};
+    const int64_t base = b * 64;
+    for (int q = 0; q < 4; ++q) {   // 16 rows per load (the BWT buffer is padded)
+        const uint4 v = *reinterpret_cast<const uint4 *>(bwt + base + 16 * q);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        for (int k = 0; k < 16; ++k) {
+            const int64_t i = base + 16 * q + k;
+            if (i >= n) break;
+            const uint8_t ch = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+            if (ch == '$') {
+                *dollar = (unsigned long long)i;
+                continue;
+            }
+            const uint32_t code = ((ch >> 2) ^ (ch >> 1)) & 3u;   // A0 C1 G2 T3
+            ++c[code];
+            lo |= (uint64_t)(code & 1u) << (16 * q + k);
+            hi |= (uint64_t)(code >> 1) << (16 * q + k);
+        }
+    }
+    fm2[4 * b + 2] = lo;
+    fm2[4 * b + 3] = hi;
+    for (int q = 0; q < 4; ++q) cnt4[(int64_t)q * (nb + 1) + b] = c[q];
+}
+
+__global__ __launch_bounds__(256) void k_fm2_counts(const uint32_t *__restrict__ cnt4, int64_t nb,
+                                                    uint32_t *__restrict__ fm2u32) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    for (int q = 0; q < 4; ++q) fm2u32[8 * b + q] = cnt4[(int64_t)q * (nb + 1) + b];
+}
+
+struct FM2View {
+    const uint4 *blk;      // 2 x uint4 per block
+    int64_t C[5], tot[5];  // codes A C G T $
+    int64_t n, dollar;
+};
+
+// occurrences of code c (0-3; 4 = '$') in bwt[0, i), 0 <= i <= n
+__device__ __forceinline__ int64_t rank2(const FM2View &f, int c, int64_t i) {
+    if (c == 4) return f.dollar < i ? 1 : 0;
+    const int64_t b = i >> 6;
+    const int r = (int)(i & 63);
+    const uint4 h = f.blk[2 * b], p = f.blk[2 * b + 1];
+    const uint32_t cnt = c == 0 ? h.x : c == 1 ? h.y : c == 2 ? h.z : h.w;
+    const uint64_t lo = ((uint64_t)p.y << 32) | p.x, hi = ((uint64_t)p.w << 32) | p.z;
+    const uint64_t m = ((c & 1) ? lo : ~lo) & ((c & 2) ? hi : ~hi);
+    const uint64_t below = r ? (~0ull >> (64 - r)) : 0ull;
+    int64_t x = (int64_t)cnt + __popcll(m & below);
+    if (c == 0 && f.dollar >= 64 * b && f.dollar < i) --x;   // the '$' row reads as A in the planes
+    return x;
+}
+
+__device__ __forceinline__ int code5(uint8_t ch) {
+    switch (ch) {
+        case 'A': return 0;
+        case 'C': return 1;
+        case 'G': return 2;
+        case 'T': return 3;
+        case '$': return 4;
+        default: return -1;
+    }
+}
+
+// backward search over the packed rank, one pattern per lane: each step is
+// two 32-byte block loads and two popcounts
+__global__ __launch_bounds__(256) void k_bsearch2(FM2View f, const uint8_t *__restrict__ pats,
+                                                  const int64_t *__restrict__ off, int64_t np,
+                                                  int64_t *__restrict__ out) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= np) return;
+    const int64_t a = off[p], b = off[p + 1];
+    int64_t sp = -1, ep = -1;
+    if (b == a) {
+        sp = 0;
+        ep = f.n - 1;
+    } else {
+        int c = code5(pats[b - 1]);
+        if (c >= 0 && f.tot[c] > 0) {
+            sp = f.C[c];
+            ep = sp + f.tot[c] - 1;
+            for (int64_t i = b - 2; i >= a; --i) {
+                c = code5(pats[i]);
+                if (c < 0 || f.tot[c] == 0) { sp = ep = -1; break; }
+                sp = f.C[c] + rank2(f, c, sp);
+                ep = f.C[c] + rank2(f, c, ep + 1) - 1;
+                if (sp > ep) { sp = ep = -1; break; }
+            }
+        }
+    }
+    out[2 * p] = sp;
+    out[2 * p + 1] = ep;
+}
+
 // ---- backward search (bwt.py:335-389), one pattern per lane
 struct FMView {
     const uint8_t *bwt;
@@ -495,9 +603,9 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     const bool dna = sa_dna_eligible(last, n, ix->totals) &&
                      sa_dna_device(c, T, n, ix->sa.as<uint32_t>(), ix->bwt.as<uint8_t>());
     if (!dna) sa_doubling(c, ix, T, n, sigma, code);
-    // scratch of the Occ / k-mer stages
+    // scratch of the Occ / k-mer / packed-rank stages
     c.slot[S_IDX0].ensure((size_t)n * 8);
-    c.slot[S_IDX3].ensure((size_t)(n + 1) * 4);
+    c.slot[S_IDX3].ensure((size_t)std::max<int64_t>(n + 1, 4 * (n / 64 + 2)) * 4);
     c.slot[S_IDX4].ensure((size_t)(n + 1) * 4);
     c.slot[S_IDX6].ensure((size_t)(n + 1) * 4);
     uint64_t *keys = c.slot[S_IDX0].as<uint64_t>();
@@ -521,6 +629,29 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     ix->sampled.ensure((size_t)ix->sampled_len * 4 + 4);
     KLAUNCH("k_sample", 0.0, k_sample, dim3(blocks(ix->sampled_len)), dim3(256), 0, st, SA, n, sa_sample,
                        ix->sampled.as<int32_t>(), ix->sampled_len);
+
+    // ------------------------------------------------ packed rank (ACGT* '$')
+    ix->has_fm2 = false;
+    if (dna) {
+        const int64_t nb = n / 64 + 1;   // rank(c, n) reads block n >> 6
+        ix->fm2.ensure((size_t)nb * 32);
+        uint32_t *cnt4 = head;   // 4 x (nb + 1) words, sized above
+        unsigned long long *d_dollar = reinterpret_cast<unsigned long long *>(c.slot[S_COUNTS].p);
+        HIPCHECK(hipMemsetAsync(d_dollar, 0, 8, st));
+        KLAUNCH("fm2_local", (double)n + 16.0 * (double)nb + 16.0 * (double)nb, k_fm2_local, dim3(blocks(nb)),
+                dim3(256), 0, st, ix->bwt.as<uint8_t>(), n, nb, ix->fm2.as<uint64_t>(), cnt4, d_dollar);
+        for (int q = 0; q < 4; ++q) {
+            HIPCHECK(hipMemsetAsync(cnt4 + (int64_t)q * (nb + 1) + nb, 0, 4, st));
+            exclusive_scan<uint32_t>(c, cnt4 + (int64_t)q * (nb + 1), cnt4 + (int64_t)q * (nb + 1), nb + 1);
+        }
+        KLAUNCH("fm2_counts", 32.0 * (double)nb, k_fm2_counts, dim3(blocks(nb)), dim3(256), 0, st, cnt4, nb,
+                ix->fm2.as<uint32_t>());
+        unsigned long long dr = 0;
+        HIPCHECK(hipMemcpyAsync(&dr, d_dollar, 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        ix->dollar_row = (int64_t)dr;
+        ix->has_fm2 = true;
+    }
 
     // ------------------------------------------------------------ 8-mer hash
     const int K = 8;
@@ -581,6 +712,7 @@ void index_free(DeviceIndex *ix) {
     ix->sampled.release();
     ix->kmer_off.release();
     ix->kmer_pos.release();
+    ix->fm2.release();
     delete ix;
 }
 
@@ -706,6 +838,23 @@ void index_backward_search(Ctx &c, DeviceIndex *ix, const uint8_t *pats, const i
     HIPCHECK(hipMemcpyAsync(tabs, ix->C, 256 * 8, hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemcpyAsync(tabs + 256, ix->totals, 256 * 8, hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemcpyAsync(tabs + 512, ix->code_of, 256, hipMemcpyHostToDevice, st));
+    if (ix->has_fm2 && !std::getenv("BWTMI_FM_BYTES")) {
+        FM2View g;
+        g.blk = ix->fm2.as<uint4>();
+        const char sym[5] = {'A', 'C', 'G', 'T', '$'};
+        for (int q = 0; q < 5; ++q) {
+            g.C[q] = ix->C[(uint8_t)sym[q]];
+            g.tot[q] = ix->totals[(uint8_t)sym[q]];
+        }
+        g.n = ix->n;
+        g.dollar = ix->dollar_row;
+        KLAUNCH("k_bsearch2", 0.0, k_bsearch2, dim3(blocks(npat)), dim3(256), 0, st, g, c.slot[S_MISC0].as<uint8_t>(),
+                c.slot[S_MISC1].as<int64_t>(), npat, c.slot[S_MISC2].as<int64_t>());
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemcpyAsync(sp_ep, c.slot[S_MISC2].p, (size_t)npat * 16, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        return;
+    }
     FMView f;
     f.bwt = ix->bwt.as<uint8_t>();
     f.occ = ix->occ.as<int32_t>();

@@ -380,13 +380,19 @@ def test_dna_suffix_sort_vs_oracle(gpu_ctx, case):
     _check_index(t + b"$")
 
 
-def test_backward_search_all_short_motifs(gpu_ctx):
+@pytest.mark.parametrize("rank", ["packed", "bytes"])
+def test_backward_search_all_short_motifs(gpu_ctx, monkeypatch, rank):
+    """Both rank structures: the packed 2-bit blocks of ACGT texts (k_bsearch2)
+    and the byte BWT + sampled Occ (k_bsearch, BWTMI_FM_BYTES=1)."""
     from bwtmi import BWTCore, MotifUtils, synth
+    if rank == "bytes":
+        monkeypatch.setenv("BWTMI_FM_BYTES", "1")
     text = synth.generate_contig(50000, 77) + b"$"
     core = BWTCore(text.decode())
     ref = oracle.Index(text)
     pats = [m for k in range(1, 7) for m in MotifUtils.enumerate_motifs(k)]
-    pats += ["ACGTACGTAC", "N", "", "TTTTTTTTTT", "GATTACA"]
+    pats += ["ACGTACGTAC", "N", "", "TTTTTTTTTT", "GATTACA", "$", "A$", "$A", "C$", text[-9:].decode(),
+             text[:12].decode(), text[100:164].decode(), "ACGN"]
     got = core.backward_search_batch(pats)
     for p, (sp, ep) in zip(pats, got.tolist()):
         assert (sp, ep) == ref.backward_search(p.encode()), p
