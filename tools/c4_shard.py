@@ -1,0 +1,62 @@
+"""One rank's share of C4 at N=8 on this box: the 8 x 12.5 Mbp
+FASTA, LPT shard (world 8, rank R) loaded by this process alone, the bench
+step (load -> index + scan -> post-processing -> write of the shard's rows)
+with T host threads -- T = cores/8 is the per-rank share of a node whose host
+cores are split evenly among 8 GPU ranks.  Projected 8-rank C4 throughput =
+100 Mbp / the slowest shard's step (ranks share no data path; the only
+collectives are two small all-reduces in the sharded write).
+
+usage: python tools/c4_shard.py OUT.json [threads ...]"""
+import json, os, sys, tempfile, time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "bwt-algorithm_amd")]
+FLANK = 30
+
+
+def main():
+    out_json = sys.argv[1]
+    tlist = [int(x) for x in sys.argv[2:]] or [2, 16]
+    from bwtmi import _lib, synth
+    from bwtmi.records import Job
+    ctx = _lib.ctx(0)
+    fa = os.path.join(tempfile.gettempdir(), "c4_shard.fa")
+    synth.write_fasta(fa, [12_500_000] * 8, 0.0)
+    out = os.path.join(tempfile.gettempdir(), "c4_shard.tab")
+    res = dict(workload="C4 shard: 8 x 12.5 Mbp FASTA, world 8, LPT shards", host=_lib.host_info(), runs=[])
+    for T in tlist:
+        for r in (0, 7):
+            job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True, build_index=True,
+                      sa_sample=32, threads=T)
+
+            def step():
+                job.reset()
+                job.load_fasta(fa, FLANK, 8, r)
+                job.upload(ctx)
+                job.scan(ctx)
+                job.postprocess()
+                job.write("strfinder", out)
+                job.wait(ctx)
+            step()
+            ts = []
+            for _ in range(3):
+                t = time.perf_counter()
+                step()
+                ts.append((time.perf_counter() - t) * 1e3)
+            bp = sum(job.contig_weight(i) for i in job.select_shard(8, r))
+            ms = sorted(ts)[1]
+            res["runs"].append(dict(threads=T, rank=r, shard_bp=bp, step_ms=round(ms, 2),
+                                    steps_ms=[round(x, 2) for x in ts], stage_ms=[round(x, 2) for x in job.stage_ms()]))
+            print(json.dumps(res["runs"][-1]), flush=True)
+    for T in tlist:
+        worst = max(x["step_ms"] for x in res["runs"] if x["threads"] == T)
+        res[f"projected_8rank_mbp_per_s_at_{T}_threads_per_rank"] = round(100.0 / (worst / 1e3), 1)
+    with open(out_json, "w") as f:
+        json.dump(res, f, indent=1)
+    os.unlink(fa)
+    if os.path.exists(out):
+        os.unlink(out)
+
+
+if __name__ == "__main__":
+    main()
