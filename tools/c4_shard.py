@@ -29,15 +29,23 @@ def main():
             job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True, build_index=True,
                       sa_sample=32, threads=T)
 
+            calls = {}
+
+            def timed(name, fn, *args):
+                t = time.perf_counter()
+                fn(*args)
+                calls[name] = calls.get(name, 0.0) + (time.perf_counter() - t) * 1e3
+
             def step():
-                job.reset()
-                job.load_fasta(fa, FLANK, 8, r)
-                job.upload(ctx)
-                job.scan(ctx)
-                job.postprocess()
-                job.write("strfinder", out)
-                job.wait(ctx)
+                timed("reset", job.reset)
+                timed("load_fasta", job.load_fasta, fa, FLANK, 8, r)
+                timed("upload", job.upload, ctx)
+                timed("scan", job.scan, ctx)
+                timed("postprocess", job.postprocess)
+                timed("write", job.write, "strfinder", out)
+                timed("index_wait", job.wait, ctx)
             step()
+            calls.clear()
             ts = []
             for _ in range(3):
                 t = time.perf_counter()
@@ -46,7 +54,8 @@ def main():
             bp = sum(job.contig_weight(i) for i in job.select_shard(8, r))
             ms = sorted(ts)[1]
             res["runs"].append(dict(threads=T, rank=r, shard_bp=bp, step_ms=round(ms, 2),
-                                    steps_ms=[round(x, 2) for x in ts], stage_ms=[round(x, 2) for x in job.stage_ms()]))
+                                    steps_ms=[round(x, 2) for x in ts], stage_ms=[round(x, 2) for x in job.stage_ms()],
+                                    calls_ms={k: round(v / 3, 2) for k, v in calls.items()}))
             print(json.dumps(res["runs"][-1]), flush=True)
     for T in tlist:
         worst = max(x["step_ms"] for x in res["runs"] if x["threads"] == T)
