@@ -47,9 +47,17 @@ VALU_LANE_OPS_PEAK = 256 * 4 * 32 * 2.4e9
 B_ALG_PER_BASE = 16.7          # compulsory HBM bytes per base, CLI path
 PMC_SUMMARY = os.path.join(REPO, "profiles", "pmc_traffic.json")
 # bench kernel-timer names -> kernel names in the rocprofv3 summaries
-KERNEL_OF = {"radix_scatter_kv12": "k_scatter<u32>", "radix_scatter_kv16": "k_scatter<u64>",
-             "radix_hist": "k_hist", "bwt_gather": "k_bwt", "occ_blocks": "k_occ_blocks",
-             "sa_init_keys": "k_init_keys"}
+KERNEL_OF = {"radix_scatter_kv8": "k_scatter<u32,u32>", "radix_scatter_kv12": "k_scatter<u64,u32>",
+             "radix_scatter_kv16": "k_scatter<u64,u64>", "bwt_gather": "k_bwt", "occ_blocks": "k_occ_blocks",
+             "sa_init_keys": "k_init_keys", "kmer_dna": "k_kmer_dna", "fm2_local": "k_fm2_local",
+             "fm2_counts": "k_fm2_counts", "dna_ls_keys": "k_ls_wave"}
+
+
+def rocprof_name(timer: str) -> str:
+    """bench kernel-timer name -> the kernel's short name in the rocprofv3 summaries"""
+    if timer in KERNEL_OF:
+        return KERNEL_OF[timer]
+    return "k_" + timer if timer.startswith("dna_") else timer
 FLANK = 30
 METRIC = "Mbp/s indexed+scanned (Tier1+2) on 100 Mbp synthetic FASTA, 1/2/4/8 GPU"
 WORKLOADS = {
@@ -268,7 +276,7 @@ def main():
         traffic = None
         if a.pmc_summary and os.path.exists(a.pmc_summary) and wl_name in ("C3", "C5") and not a.contig_bp:
             with open(a.pmc_summary) as f:
-                pk = json.load(f).get("kernels", {}).get(KERNEL_OF.get(name, name))
+                pk = json.load(f).get("kernels", {}).get(rocprof_name(name))
             if pk:
                 traffic = pk["hbm_bytes_per_launch"]
         roofline = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",

@@ -59,11 +59,14 @@ struct Chunk {
 template <class F>
 void for_lines(const char *p, int64_t a, int64_t e, F &&line) {
     int64_t i = a;
+    // the per-line '\r' search only runs when the range holds one at all
+    const bool has_cr = std::memchr(p + a, '\r', (size_t)(e - a)) != nullptr;
     while (i < e) {
         // line end: the next '\n' (memchr), or an earlier '\r'
         const char *nl = (const char *)std::memchr(p + i, '\n', (size_t)(e - i));
         int64_t j = nl ? (int64_t)(nl - p) : e;
-        if (const char *cr = (const char *)std::memchr(p + i, '\r', (size_t)(j - i))) j = (int64_t)(cr - p);
+        if (has_cr)
+            if (const char *cr = (const char *)std::memchr(p + i, '\r', (size_t)(j - i))) j = (int64_t)(cr - p);
         int64_t s = i, t = j;
         while (s < t && py_space((unsigned char)p[s])) ++s;
         while (t > s && py_space((unsigned char)p[t - 1])) --t;
@@ -95,6 +98,19 @@ bool header_ok(const char *h, int64_t n) {
         i += len;
     }
     return true;
+}
+
+// index of the first byte >= 0x80 in [s, s + n), or -1 (8 bytes per step)
+inline int64_t first_high(const char *s, int64_t n) {
+    int64_t q = 0;
+    for (; q + 32 <= n; q += 32) {
+        uint64_t w[4];
+        std::memcpy(w, s + q, 32);
+        if ((w[0] | w[1] | w[2] | w[3]) & 0x8080808080808080ull) break;
+    }
+    for (; q < n; ++q)
+        if ((unsigned char)s[q] >= 0x80) return q;
+    return -1;
 }
 
 // upper-cased copy (ASCII a-z), vectorised
@@ -170,8 +186,7 @@ void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, i
                 return;
             }
             if (C.bad < 0)
-                for (int64_t q = s; q < e; ++q)
-                    if ((unsigned char)p[q] >= 0x80) { C.bad = q; break; }
+                if (const int64_t q = first_high(p + s, e - s); q >= 0) C.bad = s + q;
             if (C.hdrs.empty()) C.pre += e - s;
             else C.hdrs.back().len += e - s;
         });

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "device.h"
 
@@ -337,7 +338,14 @@ void radix_sort_pairs32(Ctx &c, uint64_t *keys, uint32_t *vals, int64_t n, int b
     radix_sort_impl<uint64_t, uint32_t>(c, keys, vals, n, bit0, bit1);
 }
 void radix_sort_pairs_k32(Ctx &c, uint32_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1) {
-    radix_sort_impl<uint32_t, uint32_t>(c, keys, vals, n, bit0, bit1);
+    static const int v = [] { const char *e = std::getenv("BWTMI_RADIX32"); return e ? std::atoi(e) : 0; }();
+    switch (v) {   // geometry A/B (tools/gpu_radix_ab.sh)
+        case 1: radix_sort_cfg<uint32_t, uint32_t, 512, 32, false, true>(c, keys, vals, n, bit0, bit1); return;
+        case 2: radix_sort_cfg<uint32_t, uint32_t, 256, 32, false, true>(c, keys, vals, n, bit0, bit1); return;
+        case 3: radix_sort_cfg<uint32_t, uint32_t, 1024, 16, false, true>(c, keys, vals, n, bit0, bit1); return;
+        case 4: radix_sort_cfg<uint32_t, uint32_t, 512, 24, false, true>(c, keys, vals, n, bit0, bit1); return;
+        default: radix_sort_impl<uint32_t, uint32_t>(c, keys, vals, n, bit0, bit1);
+    }
 }
 
 }  // namespace bwtmi

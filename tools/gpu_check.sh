@@ -16,5 +16,5 @@ for W in C5 C4; do
   timeout -k 10 600 python bench.py --workload $W --steps 5 --warmup 2 --no-cpu-baseline --no-fm --stages > "$OUT/bench_$W.json" 2> "$OUT/bench_$W.err" || { echo BENCH_${W}_FAIL; tail -20 "$OUT/bench_$W.err"; exit 1; }
   cat "$OUT/bench_$W.json"
 done
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-fm > "$OUT/bench_prof.json" 2> "$OUT/prof_stderr.log" || { echo PROF_FAIL; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/bench_prof.json" 2> "$OUT/prof_stderr.log" || { echo PROF_FAIL; exit 1; }
 echo ALL_OK

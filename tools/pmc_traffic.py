@@ -19,9 +19,10 @@ import sys
 def short(name: str) -> str:
     m = re.search(r"::(k_[A-Za-z0-9_]+)", name)
     s = m.group(1) if m else name.split("(")[0].strip()
-    t = re.search(r"<(unsigned int|unsigned long)[,>]", name)   # first template argument
-    if t:
-        s += "<u32>" if t.group(1) == "unsigned int" else "<u64>"
+    # type template arguments (k_scatter<key, value, ...>: kv8 = <u32,u32>, kv12 = <u64,u32>)
+    ts = re.findall(r"(unsigned int|unsigned long)", name.replace("(anonymous namespace)", "").split("(")[0])
+    if ts:
+        s += "<" + ",".join("u32" if t == "unsigned int" else "u64" for t in ts[:2]) + ">"
     return s
 
 

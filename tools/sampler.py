@@ -84,37 +84,7 @@ def inclusive(path, tabs):
     return incl
 
 
-def main():
-    prefix = sys.argv[1]
-    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-    n = int(sys.argv[3]) if len(sys.argv) > 3 else 100_000_000
-    lib = ctypes.CDLL(os.path.join(REPO, "tools", "libsampler.so"))
-    from bwtmi import _lib, synth
-    from bwtmi.records import Job
-    ctx = _lib.ctx(0)
-    fa = os.path.join(tempfile.gettempdir(), "sampler_c3.fa")
-    synth.write_fasta(fa, [n], 0.0)
-    out = os.path.join(tempfile.gettempdir(), "sampler_c3.tab")
-    job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True, build_index=True, sa_sample=32)
-
-    def step():
-        job.reset()
-        job.load_fasta(fa, 30)
-        job.upload(ctx)
-        job.scan(ctx)
-        job.postprocess()
-        job.write("strfinder", out)
-        job.wait(ctx)
-
-    step()
-    print("threads sampled:", lib.sampler_start(2000), flush=True)
-    t0 = time.time()
-    for _ in range(steps):
-        step()
-    dt = time.time() - t0
-    raw = prefix + ".raw"
-    ns = lib.sampler_stop(raw.encode())
-    print(f"{steps} steps {dt * 1e3 / steps:.1f} ms/step, {ns} samples", flush=True)
+def report(prefix, raw):
     tabs = {}
     by_fn = collections.Counter()
     for line in open(raw):
@@ -156,6 +126,40 @@ def main():
         for name, c in incl.most_common(80):
             f.write(f"{100.0 * c / tot:6.2f}% {c:8d} {name[:150]}\n")
     print(open(prefix + ".txt").read()[:6000])
+
+
+def main():
+    prefix = sys.argv[1]
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    n = int(sys.argv[3]) if len(sys.argv) > 3 else 100_000_000
+    lib = ctypes.CDLL(os.path.join(REPO, "tools", "libsampler.so"))
+    from bwtmi import _lib, synth
+    from bwtmi.records import Job
+    ctx = _lib.ctx(0)
+    fa = os.path.join(tempfile.gettempdir(), "sampler_c3.fa")
+    synth.write_fasta(fa, [n], 0.0)
+    out = os.path.join(tempfile.gettempdir(), "sampler_c3.tab")
+    job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True, build_index=True, sa_sample=32)
+
+    def step():
+        job.reset()
+        job.load_fasta(fa, 30)
+        job.upload(ctx)
+        job.scan(ctx)
+        job.postprocess()
+        job.write("strfinder", out)
+        job.wait(ctx)
+
+    step()
+    print("threads sampled:", lib.sampler_start(2000), flush=True)
+    t0 = time.time()
+    for _ in range(steps):
+        step()
+    dt = time.time() - t0
+    raw = prefix + ".raw"
+    ns = lib.sampler_stop(raw.encode())
+    print(f"{steps} steps {dt * 1e3 / steps:.1f} ms/step, {ns} samples", flush=True)
+    report(prefix, raw)
     os.unlink(fa)
     os.unlink(out)
 
