@@ -853,7 +853,12 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
     std::vector<SpecOut> spec((size_t)K);
     auto ts0 = std::chrono::steady_clock::now();
     std::vector<double> cms(g_stats ? (size_t)K : 0);
+    // test hook: BWTMI_FAIL_MERGE_CHUNK=k throws inside worker task k (k < 0: the last
+    // task) -- the pool must hand the error back through the C ABI (tests/test_host.py)
+    const char *inj_e = std::getenv("BWTMI_FAIL_MERGE_CHUNK");
+    const int64_t inj = inj_e ? (std::atoll(inj_e) < 0 ? K - 1 : std::atoll(inj_e)) : -1;
     parallel_items(K, nt, [&](int64_t k, int w) {
+        if (k == inj) fail(BWTMI_E_STATE, "injected failure in merge task %lld", (long long)k);
         auto a = std::chrono::steady_clock::now();
         spec_run(u, pools, w, R, cut[(size_t)k], cut[(size_t)k + 1], fresh, spec[(size_t)k]);
         if (g_stats) cms[(size_t)k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();

@@ -187,6 +187,31 @@ def test_edge_inputs_match_reference_goldens(golden_dir, built_lib):
         assert hashlib.sha256(j.render(d["fmt"])).hexdigest() == m["sha256"], name
 
 
+@pytest.mark.parametrize("task", ["0", "-1"])
+def test_worker_exception_returns_an_error(built_lib, monkeypatch, task):
+    """An exception inside a pooled worker task (the first, run by the caller
+    thread, and the last, run by a pool thread) comes back through the C ABI as
+    an error; the pool stays usable and the next call gives the normal result."""
+    from bwtmi import _lib, synth
+    from bwtmi.records import Job
+    seq = synth.generate_contig(300_000, 4, 0.02)
+    trimmed = seq[30:len(seq) - 30]
+    hits = oracle.strict_scan(trimmed, 1, 1000, 0, 3)
+
+    def run():
+        j = Job(min_copies=3, show_progress=True, threads=4)
+        j.add_contig("c", seq, 30, 30)
+        j.add_hits(0, hits)
+        j.postprocess()
+        return j.render("strfinder")
+    want = run()
+    monkeypatch.setenv("BWTMI_FAIL_MERGE_CHUNK", task)
+    with pytest.raises(_lib.BwtmiError, match="injected failure"):
+        run()
+    monkeypatch.delenv("BWTMI_FAIL_MERGE_CHUNK")
+    assert run() == want
+
+
 def test_save_results_over_plain_record_lists(golden_dir, tmp_path, built_lib):
     """save_results(list_of_records) (bwt.py:4141-4198) with a copy of the
     records and with a filtered subset, in all five formats, against the
