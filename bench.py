@@ -200,7 +200,8 @@ def main():
 
     def step():
         timed("reset", job.reset)
-        timed("load_fasta", job.load_fasta, fa, FLANK, load_world, load_rank)
+        # shared FASTA over N ranks: each scans 1/N of it, the part tables are all-gathered
+        timed("load_fasta", job.load_fasta, fa, FLANK, load_world, load_rank, c if load_world > 1 else None)
         timed("upload", job.upload, ctx)
         timed("scan", job.scan, ctx)
         timed("postprocess", job.postprocess)

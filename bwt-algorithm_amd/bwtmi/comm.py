@@ -196,6 +196,22 @@ class RcclComm:
             self.h = None
 
 
+def allgather_words(c, words: np.ndarray) -> List[np.ndarray]:
+    """Every rank's int64 vector, in rank order, through two sum all-reduces
+    (sizes, then each rank's words at its offset of a zeroed buffer)."""
+    w = np.ascontiguousarray(words, dtype=np.int64)
+    if c is None or c.world == 1:
+        return [w.copy()]
+    sizes = np.zeros(c.world, dtype=np.int64)
+    sizes[c.rank] = w.size
+    sizes = c.allreduce(sizes)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    buf = np.zeros(int(off[-1]), dtype=np.int64)
+    buf[off[c.rank]:off[c.rank + 1]] = w
+    buf = c.allreduce(buf)
+    return [buf[off[r]:off[r + 1]] for r in range(c.world)]
+
+
 _COMM = None
 
 

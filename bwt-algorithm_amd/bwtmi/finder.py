@@ -132,7 +132,7 @@ class TandemRepeatFinder:
         c = dist.init()
         if self.job is None:
             job = self._new_job()
-            job.load_fasta(self.reference_file, self.flank_trim, c.world, c.rank)
+            job.load_fasta(self.reference_file, self.flank_trim, c.world, c.rank, comm=c)
             self.job = job
         job = self.job
         job.reset()

@@ -120,10 +120,23 @@ class Job:
         self.names.append(name)
         return cid.value
 
-    def load_fasta(self, path: str, flank_trim: int, world: int = 1, rank: int = 0) -> None:
+    def load_fasta(self, path: str, flank_trim: int, world: int = 1, rank: int = 0, comm=None) -> None:
         """load_reference (bwt.py:3713-3756), natively; with world > 1 only this
-        rank's fold units get their bases (and the job is restricted to them)."""
-        if world > 1:
+        rank's fold units get their bases (and the job is restricted to them).
+        With a communicator (bwtmi.comm) no rank reads the whole file: each scans
+        its 1/world, the part tables are all-gathered, each reads its own contigs."""
+        if world > 1 and comm is not None:
+            from . import comm as _comm
+            blob, nw = C.c_void_p(), C.c_int64()
+            check(lib().bwtmi_job_fasta_scan_part(self.h, path.encode(), world, rank, C.byref(blob), C.byref(nw)))
+            try:
+                mine = np.ctypeslib.as_array(C.cast(blob, C.POINTER(C.c_int64)), shape=(nw.value,)).copy()
+            finally:
+                lib().bwtmi_free(blob)
+            parts = np.frombuffer(b"".join(_comm.allgather_bytes(comm, mine.tobytes())), dtype=np.int64)
+            check(lib().bwtmi_job_load_fasta_parts(self.h, path.encode(), flank_trim, world, rank,
+                                                  parts.ctypes.data_as(C.c_void_p), parts.size))
+        elif world > 1:
             check(lib().bwtmi_job_load_fasta_shard(self.h, path.encode(), flank_trim, world, rank))
         else:
             check(lib().bwtmi_job_load_fasta(self.h, path.encode(), flank_trim))

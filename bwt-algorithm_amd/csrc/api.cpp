@@ -41,7 +41,7 @@ void fail(int code, const char *fmt, ...) {
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
     g_err = buf;
-    throw Error{code};
+    throw Error{code, buf};
 }
 
 template <class F>
@@ -50,6 +50,7 @@ static int guard(F &&f) {
         f();
         return BWTMI_OK;
     } catch (const Error &e) {
+        g_err = e.msg;
         return e.code;
     } catch (const std::bad_alloc &) {
         g_err = "out of host memory";
@@ -513,6 +514,28 @@ int bwtmi_job_load_fasta_shard(bwtmi_job *job, const char *path, int32_t flank_t
     });
 }
 
+int bwtmi_job_fasta_scan_part(bwtmi_job *job, const char *path, int32_t world, int32_t rank, int64_t **blob,
+                              int64_t *nwords) {
+    return guard([&] {
+        CHECK_ARG(job && path && blob && nwords && world >= 1 && rank >= 0 && rank < world, "bad argument");
+        std::vector<int64_t> v;
+        fasta_scan_part(job->j, path, world, rank, v);
+        auto *o = (int64_t *)std::malloc(std::max<size_t>(1, v.size()) * sizeof(int64_t));
+        if (!o) fail(BWTMI_E_NOMEM, "malloc");
+        std::memcpy(o, v.data(), v.size() * sizeof(int64_t));
+        *blob = o;
+        *nwords = (int64_t)v.size();
+    });
+}
+
+int bwtmi_job_load_fasta_parts(bwtmi_job *job, const char *path, int32_t flank_trim, int32_t world, int32_t rank,
+                               const int64_t *blob, int64_t nwords) {
+    return guard([&] {
+        CHECK_ARG(job && path && blob && nwords >= 6 && world >= 1 && rank >= 0 && rank < world, "bad argument");
+        fasta_load_parts(job->j, path, flank_trim, world, rank, blob, nwords);
+    });
+}
+
 int bwtmi_job_select_shard(bwtmi_job *job, int32_t world, int32_t rank, int32_t *ids, int32_t *n) {
     return guard([&] {
         CHECK_ARG(job && world >= 1 && rank >= 0 && rank < world, "bad argument");
@@ -675,8 +698,8 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
                 strict_scan_device(c, job->dev.seqs[i].buf.as<uint8_t>(), len, 1,
                                    (int32_t)std::min<int64_t>(U, INT32_MAX), P.min_copies, r,
                                    screen && !t3 && len < (int64_t)UINT32_MAX);   // 32-bit hit lengths
-            } catch (const Error &) {
-                J.errors[i] = g_err;
+            } catch (const Error &e) {
+                J.errors[i] = e.msg;
                 (void)hipGetLastError();
                 (void)hipStreamSynchronize(c.stream);
                 continue;
@@ -718,7 +741,7 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
                 HIPCHECK(hipStreamSynchronize(c.stream));
             } catch (const Error &e) {
                 c.bg_code = e.code;
-                c.bg_err = "background index build: " + g_err;
+                c.bg_err = "background index build: " + e.msg;
             } catch (const std::bad_alloc &) {
                 c.bg_code = BWTMI_E_NOMEM;
                 c.bg_err = "background index build: out of host memory";

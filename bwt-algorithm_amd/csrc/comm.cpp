@@ -82,6 +82,7 @@ static int cguard(F &&f) {
         f();
         return BWTMI_OK;
     } catch (const Error &e) {
+        set_error("%s", e.msg.c_str());
         return e.code;
     } catch (const std::bad_alloc &) {
         set_error("out of host memory");

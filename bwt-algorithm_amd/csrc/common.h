@@ -14,8 +14,9 @@ namespace bwtmi {
 
 // ---------------------------------------------------------------- errors
 void set_error(const char *fmt, ...);
-struct Error {
+struct Error {   // the message travels with the exception (it may cross threads)
     int code;
+    std::string msg;
 };
 [[noreturn]] void fail(int code, const char *fmt, ...);
 
@@ -222,6 +223,11 @@ std::string render(Job &job, int fmt);
 // fasta.cpp: load_reference; with world > 1 only this rank's shard (fold units by
 // longest-processing-time over the analysed lengths, shard_units) gets its bases
 void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world = 1, int32_t rank = 0);
+// split multi-rank load: pass 1 over this rank's 1/world of the file -> part
+// table; all ranks' tables (rank order) -> contigs, shard, own bases only
+void fasta_scan_part(Job &job, const char *path, int32_t world, int32_t rank, std::vector<int64_t> &blob);
+void fasta_load_parts(Job &job, const char *path, int32_t flank_trim, int32_t world, int32_t rank,
+                      const int64_t *blob, int64_t nwords);
 // fold units -> ranks by longest-processing-time greedy (deterministic; same as
 // bwtmi.dist.assign): returns the contig ids owned by `rank`
 std::vector<int32_t> shard_units(Job &job, int32_t world, int32_t rank);

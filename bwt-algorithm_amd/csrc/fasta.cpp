@@ -44,6 +44,7 @@ inline bool eol(char c) { return c == '\n' || c == '\r'; }
 struct Hdr {
     int64_t name_a, name_b;   // name bytes in the file buffer
     int64_t len;              // stripped content after the header, inside the chunk
+    int64_t line = 0;         // the header's '>' in the buffer
 };
 struct Chunk {
     int64_t a = 0, b = 0;     // [a, b): whole lines
@@ -181,7 +182,7 @@ void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, i
                 while (x < e && py_space((unsigned char)p[x])) ++x;
                 int64_t y = x;
                 while (y < e && !py_space((unsigned char)p[y])) ++y;
-                C.hdrs.push_back(Hdr{x, y, 0});
+                C.hdrs.push_back(Hdr{x, y, 0, s});
                 if (C.bad < 0 && !header_ok(p + s, e - s)) C.bad = s;
                 return;
             }
@@ -310,6 +311,244 @@ void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, i
         auto d = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         std::fprintf(stderr, "  load_fasta: read %.1f pass1+stitch %.1f pass2 %.1f ms (%d threads, %lld chunks)\n",
                      d(t0, t1), d(t1, t2), d(t2, clk::now()), nt, (long long)T);
+    }
+}
+
+// ------------------------------------------------------------------ split load
+// Multi-rank load with an exchange (bwtmi_job_fasta_scan_part +
+// bwtmi_job_load_fasta_parts): rank r runs pass 1 over its 1/world of the
+// file only, the ranks exchange the resulting header tables (a few words per
+// contig), and each rank then reads and copies only its own contigs' bytes.
+// Every rank sees every header and every bad byte, so names, lengths, trims,
+// the shard layout and a non-ASCII failure come out identical everywhere.
+namespace {
+
+// the first line start >= x (0, or the byte after '\n' / '\r'), N if none
+int64_t line_start_from(int fd, int64_t N, int64_t x) {
+    if (x <= 0) return 0;
+    if (x >= N) return N;
+    char buf[1 << 16];
+    int64_t pos = x - 1;
+    while (pos < N) {
+        const ssize_t r = ::pread(fd, buf, (size_t)std::min<int64_t>((int64_t)sizeof buf, N - pos), (off_t)pos);
+        if (r <= 0) fail(BWTMI_E_IO, "read error");
+        for (ssize_t k = 0; k < r; ++k)
+            if (eol(buf[k])) return pos + k + 1;
+        pos += r;
+    }
+    return N;
+}
+
+void pread_range(int fd, char *dst, int64_t a, int64_t b, int nt) {
+    std::atomic<bool> bad{false};
+    const int64_t piece = int64_t(4) << 20;
+    run_tasks((b - a + piece - 1) / piece, nt, [&](int64_t k) {
+        int64_t o = a + k * piece;
+        const int64_t e = std::min(b, o + piece);
+        while (o < e) {
+            const ssize_t r = ::pread(fd, dst + (o - a), (size_t)(e - o), (off_t)o);
+            if (r <= 0) { bad = true; return; }
+            o += r;
+        }
+    });
+    if (bad) fail(BWTMI_E_IO, "read error");
+}
+
+struct Fd {
+    int fd;
+    explicit Fd(const char *path) : fd(::open(path, O_RDONLY)) {
+        if (fd < 0) fail(BWTMI_E_IO, "cannot open %s", path);
+    }
+    ~Fd() { ::close(fd); }
+    int64_t size() const {
+        struct stat st;
+        if (::fstat(fd, &st) != 0) fail(BWTMI_E_IO, "cannot stat");
+        return (int64_t)st.st_size;
+    }
+};
+
+// [a, b) of the buffer p cut into T chunks at line starts
+std::vector<int64_t> cut_lines(const char *p, int64_t a, int64_t b, int64_t T, int nt) {
+    std::vector<int64_t> cut((size_t)T + 1, b);
+    cut[0] = a;
+    run_tasks(T - 1, nt, [&](int64_t q) {
+        int64_t i = a + (b - a) * (q + 1) / T;
+        while (i < b && !eol(p[i - 1])) ++i;
+        cut[(size_t)q + 1] = i;
+    });
+    for (int64_t t = 1; t <= T; ++t) cut[(size_t)t] = std::max(cut[(size_t)t], cut[(size_t)t - 1]);
+    return cut;
+}
+
+}  // namespace
+
+// blob (int64 words): N, A, B, bad, pre, nh, then per header: line, len,
+// name bytes, name words (the name's bytes, zero-padded to 8)
+void fasta_scan_part(Job &job, const char *path, int32_t world, int32_t rank, std::vector<int64_t> &blob) {
+    const int nt = host_threads(job.params);
+    Fd f(path);
+    const int64_t N = f.size();
+    const int64_t A = line_start_from(f.fd, N, N * rank / world), B = line_start_from(f.fd, N, N * (rank + 1) / world);
+    thread_local Seq part;
+    char *p = part.resize_uninit((size_t)std::max<int64_t>(0, B - A));
+    if (B > A) pread_range(f.fd, p, A, B, nt);
+    const int64_t n = B - A;
+    const int64_t T = std::max<int64_t>(1, std::min<int64_t>(4 * (int64_t)nt, n / (int64_t(1) << 20) + 1));
+    const std::vector<int64_t> cut = cut_lines(p, 0, n, T, nt);
+    std::vector<Chunk> ck((size_t)T);
+    run_tasks(T, nt, [&](int64_t t) {
+        Chunk &C = ck[(size_t)t];
+        C.a = cut[(size_t)t];
+        C.b = cut[(size_t)t + 1];
+        for_lines(p, C.a, C.b, [&](int64_t s, int64_t e) {
+            if (p[s] == '>') {
+                int64_t x = s + 1;
+                while (x < e && py_space((unsigned char)p[x])) ++x;
+                int64_t y = x;
+                while (y < e && !py_space((unsigned char)p[y])) ++y;
+                C.hdrs.push_back(Hdr{x, y, 0, s});
+                if (C.bad < 0 && !header_ok(p + s, e - s)) C.bad = s;
+                return;
+            }
+            if (C.bad < 0)
+                if (const int64_t q = first_high(p + s, e - s); q >= 0) C.bad = s + q;
+            if (C.hdrs.empty()) C.pre += e - s;
+            else C.hdrs.back().len += e - s;
+        });
+    });
+    int64_t bad = -1, pre = 0, nh = 0;
+    for (const Chunk &C : ck) {
+        if (bad < 0 && C.bad >= 0) bad = A + C.bad;
+        nh += (int64_t)C.hdrs.size();
+    }
+    blob.assign({N, A, B, bad, 0, nh});
+    bool have = false;   // content after the last header so far lands in blob[last_at]
+    size_t last_at = 0;
+    for (const Chunk &C : ck) {
+        if (have) blob[last_at] += C.pre;
+        else pre += C.pre;
+        for (const Hdr &h : C.hdrs) {
+            const int64_t nb = h.name_b - h.name_a;
+            blob.push_back(A + h.line);
+            last_at = blob.size();
+            blob.push_back(h.len);
+            have = true;
+            blob.push_back(nb);
+            const size_t w0 = blob.size();
+            blob.resize(w0 + (size_t)((nb + 7) / 8), 0);
+            std::memcpy(blob.data() + w0, p + h.name_a, (size_t)nb);
+        }
+    }
+    blob[4] = pre;
+}
+
+void fasta_load_parts(Job &job, const char *path, int32_t flank_trim, int32_t world, int32_t rank,
+                      const int64_t *blob, int64_t nwords) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    const int nt = host_threads(job.params);
+    struct Inst {
+        int32_t contig;
+        int64_t len, line;
+    };
+    std::vector<Inst> inst;
+    std::unordered_map<std::string, int32_t> index;
+    for (size_t i = 0; i < job.contigs.size(); ++i) index[job.contigs[i].name] = (int32_t)i;
+    int64_t N = -1, bad = -1, q = 0;
+    for (int32_t r = 0; r < world; ++r) {
+        if (q + 6 > nwords) fail(BWTMI_E_ARG, "truncated FASTA part table");
+        const int64_t n = blob[q], b = blob[q + 3], pre = blob[q + 4], nh = blob[q + 5];
+        if (N >= 0 && n != N) fail(BWTMI_E_ARG, "FASTA part tables of different files");
+        N = n;
+        if (b >= 0 && (bad < 0 || b < bad)) bad = b;
+        if (!inst.empty()) inst.back().len += pre;
+        q += 6;
+        for (int64_t h = 0; h < nh; ++h) {
+            if (q + 3 > nwords) fail(BWTMI_E_ARG, "truncated FASTA part table");
+            const int64_t line = blob[q], len = blob[q + 1], nb = blob[q + 2];
+            q += 3;
+            if (nb < 0 || q + (nb + 7) / 8 > nwords) fail(BWTMI_E_ARG, "truncated FASTA part table");
+            if (nb == 0) fail(BWTMI_E_IO, "empty FASTA header in %s", path);   // split()[0]
+            std::string name((const char *)(blob + q), (size_t)nb);
+            q += (nb + 7) / 8;
+            auto it = index.find(name);
+            int32_t cid;
+            if (it == index.end()) {
+                cid = (int32_t)job.contigs.size();
+                index.emplace(name, cid);
+                Contig c;
+                c.name = std::move(name);
+                job.contigs.push_back(std::move(c));
+            } else {
+                cid = it->second;
+            }
+            inst.push_back(Inst{cid, len, line});
+        }
+    }
+    if (bad >= 0)
+        fail(BWTMI_E_IO, "non-ASCII text at byte %lld of %s: the reference (bwt.py:3719, 121) fails on it",
+             (long long)bad, path);
+    std::vector<int32_t> last_inst(job.contigs.size(), -1);
+    for (size_t k = 0; k < inst.size(); ++k) last_inst[(size_t)inst[k].contig] = (int32_t)k;
+    const int64_t flank = flank_trim < 0 ? 0 : flank_trim;
+    for (size_t cid = 0; cid < job.contigs.size(); ++cid) {
+        const int32_t k = last_inst[cid];
+        if (k < 0) continue;
+        Contig &c = job.contigs[cid];
+        const int64_t L = inst[(size_t)k].len;
+        c.trim_left = c.trim_right = (L <= 2 * flank) ? 0 : flank;
+        c.weight = L - c.trim_left - c.trim_right;
+        c.gen = next_contig_gen();
+    }
+    std::vector<uint8_t> mine(job.contigs.size(), 1);
+    if (world > 1) {
+        std::fill(mine.begin(), mine.end(), 0);
+        for (int32_t c : shard_units(job, world, rank)) mine[(size_t)c] = 1;
+        job.selected.assign(mine.begin(), mine.end());
+    }
+    const auto t1 = clk::now();
+    Fd f(path);
+    thread_local Seq raw;
+    for (size_t cid = 0; cid < job.contigs.size(); ++cid) {
+        const int32_t k = last_inst[cid];
+        if (k < 0) continue;
+        Contig &c = job.contigs[cid];
+        if (!mine[cid]) {   // another rank's contig: name and weight only
+            c.full.clear();
+            c.trim_left = c.trim_right = 0;
+            continue;
+        }
+        const int64_t a = inst[(size_t)k].line;
+        const int64_t b = (size_t)k + 1 < inst.size() ? inst[(size_t)k + 1].line : N;
+        char *p = raw.resize_uninit((size_t)(b - a));
+        pread_range(f.fd, p, a, b, nt);
+        const int64_t n = b - a;
+        const int64_t T = std::max<int64_t>(1, std::min<int64_t>(4 * (int64_t)nt, n / (int64_t(1) << 20) + 1));
+        const std::vector<int64_t> cut = cut_lines(p, 0, n, T, nt);
+        std::vector<int64_t> cnt((size_t)T + 1, 0);
+        run_tasks(T, nt, [&](int64_t t) {   // content bytes per chunk (the header line is skipped)
+            int64_t m = 0;
+            for_lines(p, cut[(size_t)t], cut[(size_t)t + 1], [&](int64_t s, int64_t e) {
+                if (p[s] != '>') m += e - s;
+            });
+            cnt[(size_t)t + 1] = m;
+        });
+        for (int64_t t = 0; t < T; ++t) cnt[(size_t)t + 1] += cnt[(size_t)t];
+        if (cnt[(size_t)T] != inst[(size_t)k].len)
+            fail(BWTMI_E_IO, "%s changed while it was read (contig %s)", path, c.name.c_str());
+        char *dst = c.full.resize_uninit((size_t)cnt[(size_t)T]);
+        run_tasks(T, nt, [&](int64_t t) {
+            char *d = dst + cnt[(size_t)t];
+            for_lines(p, cut[(size_t)t], cut[(size_t)t + 1], [&](int64_t s, int64_t e) {
+                if (p[s] == '>') return;
+                upper_copy(d, p + s, e - s);
+                d += e - s;
+            });
+        });
+    }
+    if (std::getenv("BWTMI_STATS")) {
+        auto d = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+        std::fprintf(stderr, "  load_fasta_parts: stitch %.1f own contigs %.1f ms\n", d(t0, t1), d(t1, clk::now()));
     }
 }
 

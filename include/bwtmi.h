@@ -291,6 +291,18 @@ int bwtmi_job_load_fasta(bwtmi_job *job, const char *path, int32_t flank_trim);
  * restricted to them */
 int bwtmi_job_load_fasta_shard(bwtmi_job *job, const char *path, int32_t flank_trim, int32_t world,
                                int32_t rank);
+/* Split multi-rank load (no rank reads the whole file): rank r runs the
+ * loader's first pass over its 1/world of the file and returns a part table
+ * (int64 words, freed with bwtmi_free); the ranks exchange the tables (an
+ * all-gather, bwtmi.comm); bwtmi_job_load_fasta_parts takes all of them in
+ * rank order, builds the contig table (names, lengths, trims, fold units --
+ * identical on every rank), restricts the job to this rank's shard and reads
+ * only those contigs' bytes.  A non-ASCII byte anywhere fails every rank.
+ * Replaces load_reference (bwt.py:3713-3756) + the contig split of 3850-3912. */
+int bwtmi_job_fasta_scan_part(bwtmi_job *job, const char *path, int32_t world, int32_t rank, int64_t **blob,
+                              int64_t *nwords);
+int bwtmi_job_load_fasta_parts(bwtmi_job *job, const char *path, int32_t flank_trim, int32_t world, int32_t rank,
+                               const int64_t *blob, int64_t nwords);
 int32_t bwtmi_job_contig_count(const bwtmi_job *job);
 /* analysed length of contig id (its shard weight), also for contigs whose bases
  * live on another rank */

@@ -396,6 +396,77 @@ def test_two_rank_gather_matches_single_process(tmp_path, golden_dir, built_lib)
     assert int(open(tmp_path / "n.txt").read()) > 0
 
 
+def _split_load_worker(rank, world, port, fa, outdir, threads):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(here, ".."), os.path.join(here, "..", "bwt-algorithm_amd")):
+        sys.path.insert(0, os.path.abspath(p))
+    from bwtmi import _lib, comm, dist
+    from bwtmi.records import Job
+    c = dist.init("host")
+    res = "ok"
+    try:
+        full = Job(threads=threads)
+        full_err = None
+        try:
+            full.load_fasta(fa, 30)
+        except _lib.BwtmiError as e:
+            full_err = str(e)
+        j = Job(threads=threads)
+        try:
+            j.load_fasta(fa, 30, world, rank, comm=c)   # split: 1/world scanned per rank
+            err = None
+        except _lib.BwtmiError as e:
+            err = str(e)
+        if full_err or err:
+            assert full_err and err and "non-ASCII" in err, (full_err, err)
+            res = "error"
+        else:
+            infos = [full.contig_info(i) for i in range(full.contig_count())]
+            w = [x[1] - x[2] - x[3] for x in infos]
+            want = dist.assign(dist.natural_units([x[0] for x in infos]), w, world)[rank]
+            assert j.names == full.names
+            assert j.select_shard(world, rank) == want
+            for cid in range(j.contig_count()):
+                assert j.contig_weight(cid) == w[cid]
+                if cid in want:
+                    assert j.contig_info(cid) == infos[cid] and j.contig_seq(cid) == full.contig_seq(cid), cid
+                else:
+                    assert j.contig_info(cid)[1] == 0
+    except AssertionError as e:
+        res = f"assert {e}"
+    with open(os.path.join(outdir, f"split_{rank}.txt"), "w") as f:
+        f.write(res)
+    c.barrier()
+    comm.close()
+
+
+@pytest.mark.parametrize("world,threads", [(2, 1), (3, 3), (4, 16)])
+def test_split_load_matches_single_process(tmp_path, built_lib, world, threads):
+    """The split multi-rank loader (each rank scans 1/world of the file, the
+    part tables are all-gathered, each rank reads only its contigs): same names,
+    lengths, trims and shard as one process reading everything, own bases
+    identical, on the messy file (CR/CRLF/LF, padding, duplicate names, empty
+    contigs, lines longer than a rank's range)."""
+    fa = str(tmp_path / "messy.fa")
+    with open(fa, "wb") as f:
+        f.write(_messy_fasta(world + threads))
+    _spawn(_split_load_worker, (world, _free_port(), fa, str(tmp_path), threads), world)
+    for r in range(world):
+        assert (tmp_path / f"split_{r}.txt").read_text() == "ok", r
+
+
+def test_split_load_fails_on_every_rank_for_non_ascii(tmp_path, built_lib):
+    fa = str(tmp_path / "bad.fa")
+    with open(fa, "wb") as f:
+        f.write(_messy_fasta(5)[:-200_000] + b"\n>late\nACGT\xc3\xa9ACGT\n")
+    _spawn(_split_load_worker, (3, _free_port(), fa, str(tmp_path), 2), 3)
+    for r in range(3):
+        assert (tmp_path / f"split_{r}.txt").read_text() == "error", r
+
+
 def _sharded_write_worker(rank, world, port, fa, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))

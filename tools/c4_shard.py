@@ -14,6 +14,34 @@ sys.path[:0] = [REPO, os.path.join(REPO, "bwt-algorithm_amd")]
 FLANK = 30
 
 
+class PartsComm:
+    """Stands in for the other 7 ranks of the split load: their part tables are
+    computed once, before timing (on a real node they come from the ranks
+    themselves, through two small all-reduces); allreduce returns what the
+    collective would."""
+
+    def __init__(self, fa, world, rank):
+        import ctypes as C
+        import numpy as np
+        from bwtmi import _lib
+        from bwtmi.records import Job
+        self.world, self.rank = world, rank
+        self.parts = []
+        for r in range(world):
+            j = Job()
+            blob, nw = C.c_void_p(), C.c_int64()
+            _lib.check(_lib.lib().bwtmi_job_fasta_scan_part(j.h, fa.encode(), world, r, C.byref(blob), C.byref(nw)))
+            arr = np.ctypeslib.as_array(C.cast(blob, C.POINTER(C.c_int64)), shape=(nw.value,)).copy()
+            _lib.lib().bwtmi_free(blob)
+            self.parts.append(arr)
+
+    def allreduce(self, arr, op=0):
+        import numpy as np
+        if arr.size == self.world:   # sizes
+            return np.array([p.size * 8 for p in self.parts], dtype=np.int64)
+        return np.concatenate(self.parts).astype(np.int64)
+
+
 def main():
     out_json = sys.argv[1]
     tlist = [int(x) for x in sys.argv[2:]] or [2, 16]
@@ -24,6 +52,8 @@ def main():
     synth.write_fasta(fa, [12_500_000] * 8, 0.0)
     out = os.path.join(tempfile.gettempdir(), "c4_shard.tab")
     res = dict(workload="C4 shard: 8 x 12.5 Mbp FASTA, world 8, LPT shards", host=_lib.host_info(), runs=[])
+    split = os.environ.get("C4_SHARD_SPLIT", "1") == "1"   # the split loader (bench / CLI at N > 1)
+    res["split_load"] = split
     for T in tlist:
         for r in (0, 7):
             job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True, build_index=True,
@@ -36,9 +66,11 @@ def main():
                 fn(*args)
                 calls[name] = calls.get(name, 0.0) + (time.perf_counter() - t) * 1e3
 
+            pc = PartsComm(fa, 8, r) if split else None
+
             def step():
                 timed("reset", job.reset)
-                timed("load_fasta", job.load_fasta, fa, FLANK, 8, r)
+                timed("load_fasta", job.load_fasta, fa, FLANK, 8, r, pc)
                 timed("upload", job.upload, ctx)
                 timed("scan", job.scan, ctx)
                 timed("postprocess", job.postprocess)
