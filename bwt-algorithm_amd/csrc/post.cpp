@@ -1186,7 +1186,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     std::vector<uint32_t, BigAlloc<uint32_t>> col;
     {
         const int64_t N = (int64_t)recs.size();
-        const int C = N > 65536 ? 4 * std::max(1, nt) : 1;
+        const int C = N > 8192 ? 4 * std::max(1, nt) : 1;
         std::vector<int64_t> cmax((size_t)C, INT64_MIN), sb((size_t)C + 1, N);
         parallel_items(C, nt, [&](int64_t t, int) {
             int64_t m = INT64_MIN;

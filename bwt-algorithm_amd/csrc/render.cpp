@@ -124,7 +124,7 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
     // one pass over the records, in parallel chunks: chromosome of each and the
     // _simple_kmer_scan pieces after every 3-mer record (kept in record order)
     const size_t NR = recs.size();
-    const int CK = NR > 65536 ? 4 * std::max(1, nt) : 1;
+    const int CK = NR > 8192 ? 4 * std::max(1, nt) : 1;
     struct Chunk {
         int32_t first = -1;
         bool mixed = false;
@@ -293,7 +293,7 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
             w.emit(row_of(job, cur, nullptr), i0);
             return i + 1;
         };
-        const int K = N > 32768 ? 4 * std::max(1, nt) : 1;
+        const int K = N > 8192 ? 4 * std::max(1, nt) : 1;
         std::vector<size_t> cut((size_t)K + 1);
         for (int k = 0; k <= K; ++k) cut[(size_t)k] = N * (size_t)k / (size_t)K;
         std::vector<uint8_t> from(N, 0);   // from[i]: the speculative run of i's chunk stepped from i
@@ -501,7 +501,7 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
     };
     const int nt = host_threads(job.params);
     const size_t NR = rows.size();
-    const int RC = NR > 65536 ? 4 * nt : 1;
+    const int RC = NR > 8192 ? 4 * nt : 1;
     std::vector<uint8_t> chunk_ok((size_t)RC, 1);
     run_tasks(RC, nt, [&](int64_t t) {   // sorted by (unit, start)?  chunk t checks pairs ending in it
         const size_t a = std::max<size_t>(1, NR * (size_t)t / (size_t)RC), b = NR * (size_t)(t + 1) / (size_t)RC;
@@ -563,7 +563,9 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
     // ids are row_base[unit] + rank within the unit (global index when the
     // caller renders only its own shard), else the local index
     const int64_t n = (int64_t)rows.size();
-    const int64_t CH = 8192;
+    // >= 4 chunks per thread while that keeps them >= 1024 rows (a 40k-row shard
+    // in 8192-row chunks kept 5 of 16 threads busy)
+    const int64_t CH = std::max<int64_t>(1024, std::min<int64_t>(8192, n / (4 * (int64_t)host_threads(job.params)) + 1));
     auto unit_of = [&](int64_t k) { return rows[(size_t)k].unit; };
     struct Chunk { int64_t a, b, id0; int32_t unit; };
     std::vector<Chunk> chunks;
