@@ -177,6 +177,14 @@ struct AlignSummary {
 bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_t end,
                          const std::string &tmpl, int64_t min_copies, AlignSummary &out,
                          double frac = 0.1, int64_t max_indel_arg = -1);
+// the same with caller-owned DP scratch (one per worker: no thread-local
+// lookups on the hot path -- __tls_get_addr was 14 % of a recompute)
+struct AlignScratch;
+AlignScratch *align_scratch_new();
+void align_scratch_free(AlignScratch *);
+bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_t end,
+                         const std::string &tmpl, int64_t min_copies, AlignSummary &out, double frac,
+                         int64_t max_indel_arg, AlignScratch *ws);
 
 // ---------------------------------------------------------------- job
 // formatted text in cached huge-page blocks (mem.h)

@@ -266,6 +266,8 @@ __attribute__((target("avx512f,avx512bw,avx512vl"))) static int dp_rows_avx512(
         sh_idx[q] = _mm512_sub_epi16(iota, _mm512_set1_epi16((int16_t)(1 << q)));
         sh_mask[q] = (__mmask32)(0xffffffffu << (1 << q));
     }
+    int nsteps = 0;
+    while (nsteps < 5 && (1 << nsteps) < W) ++nsteps;
     const __m512i cS = _mm512_set1_epi16('S'), cM = _mm512_set1_epi16('M'), cD = _mm512_set1_epi16('D'),
                   cI = _mm512_set1_epi16('I');
     // row 0: cost j for j in [0, n] (every column), lane d -> j = d - band
@@ -296,7 +298,7 @@ __attribute__((target("avx512f,avx512bw,avx512vl"))) static int dp_rows_avx512(
         // row band + 1: column 0 (cost i) is the left neighbour of lane 0 --
         // the scalar loop's cur[jmin - 1] -- one lane below the register
         if (i == band + 1) t = _mm512_min_epi16(t, _mm512_set1_epi16((int16_t)(i + 1)));
-        for (int q = 0; q < 5; ++q)
+        for (int q = 0; q < nsteps; ++q)   // ceil(log2 W) doubling steps cover the band
             t = _mm512_min_epi16(t, _mm512_mask_permutexvar_epi16(inf, sh_mask[q], sh_idx[q], t));
         const __m512i fin = _mm512_mask_mov_epi16(inf, keep, _mm512_add_epi16(t, iota));
         const __mmask32 isI = _mm512_cmplt_epi16_mask(fin, base) & valid;
@@ -418,21 +420,30 @@ bool finish_unit(const char *motif, int64_t m, const char *win, int64_t n, int64
     // an accepted copy has n_sub <= tol and both indel counts <= max_indel, so
     // its cost (= bc) is at most tol + 2 max_indel: skip the traceback otherwise
     if (bc > tol + 2 * max_indel) return false;
-    // traceback (columns collected in reverse)
-    S.cref.clear();
-    S.cqry.clear();
+    // traceback (columns collected in reverse, into buffers sized once: a path
+    // has at most m + bj columns)
+    if (S.cref.size() < (size_t)(m + bj + 1)) {
+        S.cref.resize((size_t)(m + bj + 1));
+        S.cqry.resize((size_t)(m + bj + 1));
+    }
+    char *cr = S.cref.data(), *cq = S.cqry.data();
+    size_t nc = 0;
     int64_t i = m, j = bj;
+    int64_t ns = 0, ni = 0, nd = 0;
     while (i > 0 || j > 0) {
         char op;
         if (i == 0) op = 'I';
         else if (j == 0) op = 'D';
         else if (j < i - band || j > i + band) op = 0;
         else op = ptr[i * W + (j - i + band)];
-        if (op == 'M' || op == 'S') { S.cref.push_back(motif[i - 1]); S.cqry.push_back(win[j - 1]); --i; --j; }
-        else if (op == 'D') { S.cref.push_back(motif[i - 1]); S.cqry.push_back('-'); --i; }
-        else if (op == 'I') { S.cref.push_back('-'); S.cqry.push_back(win[j - 1]); --j; }
+        if (op == 'M' || op == 'S') { cr[nc] = motif[i - 1]; cq[nc++] = win[j - 1]; ns += op == 'S'; --i; --j; }
+        else if (op == 'D') { cr[nc] = motif[i - 1]; cq[nc++] = '-'; ++nd; --i; }
+        else if (op == 'I') { cr[nc] = '-'; cq[nc++] = win[j - 1]; ++ni; --j; }
         else break;
     }
+    // the copy tests below, decided before any op is formatted ('S' = a
+    // mismatching diagonal step, 'D' / 'I' = one deleted / inserted base)
+    if (ns > tol || ni > max_indel || nd > max_indel) return false;
     S.obs_idx.clear();
     S.obs_base.clear();
     S.ops.clear();
@@ -447,7 +458,7 @@ bool finish_unit(const char *motif, int64_t m, const char *win, int64_t n, int64
         o.push_back(':');
         put_num(o, ins_at);
         o.append(":ins(");
-        for (size_t q = ins_from; q < upto; ++q) o.push_back(S.cqry[S.cqry.size() - 1 - q]);
+        for (size_t q = ins_from; q < upto; ++q) o.push_back(cq[nc - 1 - q]);
         o.push_back(')');
         S.op_end.push_back((uint32_t)o.size());
         res.n_ins += (int64_t)(upto - ins_from);
@@ -461,9 +472,9 @@ bool finish_unit(const char *motif, int64_t m, const char *win, int64_t n, int64
         S.op_end.push_back((uint32_t)o.size());
         res.n_del += del_len;
     };
-    const size_t ncols = S.cref.size();
+    const size_t ncols = nc;
     for (size_t q = 0; q < ncols; ++q) {
-        const char r = S.cref[ncols - 1 - q], qq = S.cqry[ncols - 1 - q];
+        const char r = cr[ncols - 1 - q], qq = cq[ncols - 1 - q];
         if (r == '-') {
             if (!ins_open) { ins_at = ref; ins_from = q; ins_open = true; }
             continue;
@@ -545,9 +556,23 @@ void consensus_from(const Scratch &S, int64_t m, const std::string &fallback, st
 
 }  // namespace
 
+struct AlignScratch {
+    Scratch S;
+    std::string cur;
+};
+AlignScratch *align_scratch_new() { return new AlignScratch(); }
+void align_scratch_free(AlignScratch *w) { delete w; }
+
 bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_t end,
                          const std::string &tmpl, int64_t min_copies, AlignSummary &out, double frac,
                          int64_t max_indel_arg) {
+    thread_local AlignScratch tls;
+    return align_repeat_region(seq, seq_len, start, end, tmpl, min_copies, out, frac, max_indel_arg, &tls);
+}
+
+bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_t end,
+                         const std::string &tmpl, int64_t min_copies, AlignSummary &out, double frac,
+                         int64_t max_indel_arg, AlignScratch *ws) {
     if (tmpl.empty() || seq_len == 0) return false;
     start = std::max<int64_t>(0, start);
     end = std::min<int64_t>(seq_len, end > start ? end : seq_len);
@@ -584,14 +609,14 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
         out.tot_del = 0;
         return true;
     }
-    thread_local Scratch S;
+    Scratch &S = ws->S;
     pc_reset(S, m);
     out.copy_len.clear();
     out.copy_err.clear();
     out.variations.clear();
     out.any_variation = false;
     int64_t tot_ins = 0, tot_del = 0, tot_err = 0, max_err = 0;
-    thread_local std::string cur, nxt;
+    std::string &cur = ws->cur;
     cur = tmpl;
     int64_t pos = start;
     const int64_t limit = std::min<int64_t>(
@@ -657,13 +682,17 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
         max_err = std::max<int64_t>(max_err, res.n_sub + res.n_ins + res.n_del);
         tot_ins += res.n_ins;
         tot_del += res.n_del;
+        // only the observed positions' counts change, so only their most-common
+        // base can (consensus_from over all m positions, incrementally)
         for (size_t q = 0; q < S.obs_idx.size(); ++q) {
             const int64_t idx = S.obs_idx[q];
-            if (idx >= 0 && idx < m) pc_add(S, idx, S.obs_base[q]);
+            if (idx >= 0 && idx < m) {
+                pc_add(S, idx, S.obs_base[q]);
+                char b;
+                if (pc_top(S, idx, b)) cur[(size_t)idx] = b;
+            }
         }
         pos += res.consumed;
-        consensus_from(S, m, cur, nxt);
-        cur.swap(nxt);
     }
     if (copies < min_copies) return false;
     const int64_t consumed = pos - start;

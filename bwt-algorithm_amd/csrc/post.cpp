@@ -346,6 +346,9 @@ struct Pools {
         size_t xn = 0;                                   // used in the last Extra block
         std::vector<Block> cb;
         size_t cn = 0, ccap = 0;                         // used / size of the last char block
+        // the worker's DP scratch and summary (recompute)
+        std::unique_ptr<AlignScratch, void (*)(AlignScratch *)> as{align_scratch_new(), align_scratch_free};
+        AlignSummary sum;
     };
     static constexpr size_t XB = 16384, CB = size_t(2) << 20;   // Extras are trivially destructible
     std::vector<Arena> a;
@@ -562,6 +565,7 @@ std::atomic<int64_t> g_recomputes{0}, g_recompute_ns{0}, g_merges{0}, g_canons{0
 // BWTMI_STATS=1: stage timers; =2: also per-recompute / per-test counters (slow)
 const bool g_stats = [] { const char *e = std::getenv("BWTMI_STATS"); return e && (*e == '1' || *e == '2'); }();
 const bool g_counters = [] { const char *e = std::getenv("BWTMI_STATS"); return e && *e == '2'; }();
+const char *const g_dump = std::getenv("BWTMI_DUMP_RECOMPUTE");
 std::atomic<int64_t> g_hist_n[8][8], g_hist_ns[8][8];   // [log4 motif len][log4 region len]
 inline int lg4(int64_t v) { int k = 0; while (v >= 4 && k < 7) { v >>= 2; ++k; } return k; }
 
@@ -626,6 +630,13 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
         it.x = pools.add_static(w, x, std::string_view(&kByteChars[(uint8_t)b], 1));
         return it;
     }
+    if (g_dump) {   // BWTMI_DUMP_RECOMPUTE=path: the DP recomputes' arguments (tools/recompute_bench.cpp)
+        static std::mutex mu;
+        std::lock_guard<std::mutex> lk(mu);
+        static FILE *df = std::fopen(g_dump, "w");
+        if (df) std::fprintf(df, "%lld %lld %lld %lld\n", (long long)start, (long long)end, (long long)m,
+                             (long long)std::max<int64_t>(1, u.min_copies));
+    }
     auto slice = [&](int64_t a, int64_t b) {   // Python seq[a:b], a,b >= 0
         a = std::min(a, L);
         b = std::min(b, L);
@@ -637,10 +648,11 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
         tmpl = slice(a, a + m);
     }
     if (tmpl.empty()) tmpl.assign((size_t)m, 'N');
-    thread_local AlignSummary s;
+    Pools::Arena &A = pools.a[(size_t)w];
+    AlignSummary &s = A.sum;
     s.want_copies = false;
-    bool ok = align_repeat_region(seq, L, start, end, tmpl, std::max<int64_t>(1, u.min_copies), s);
-    if (!ok) ok = align_repeat_region(seq, L, start, end, tmpl, 1, s);
+    bool ok = align_repeat_region(seq, L, start, end, tmpl, std::max<int64_t>(1, u.min_copies), s, 0.1, -1, A.as.get());
+    if (!ok) ok = align_repeat_region(seq, L, start, end, tmpl, 1, s, 0.1, -1, A.as.get());
     Extra x;
     int64_t consumed, cint;
     double mm, pind;
