@@ -855,6 +855,23 @@ void spec_run(const UnitCtx &u, Pools &pools, int w, const ItemVec &R, int64_t b
     o.pending_canon = std::move(cb[ci_cur]);
 }
 
+// _refine_repeats (bwt.py:3291-3314) for one record: only recomputed records
+// can carry mismatches; a record whose recompute already covered exactly
+// [start, end) with this motif length would be recomputed with the same
+// arguments (same result)
+inline void refine_one(const UnitCtx &u, Pools &pools, int w, Item &r) {
+    if (!r.x || r.x->mm == 0.0) return;
+    if (r.mlen > 0 && r.mlen == r.x->req_m && r.x->req_end == r.end) return;
+    int64_t m = r.mlen;
+    if (m <= 0) {
+        const int64_t rc = (int64_t)std::nearbyint(copies_of(r));
+        m = std::max<int64_t>(1, (r.end - r.start) / std::max<int64_t>(1, rc ? rc : 1));
+    }
+    r = recompute(u, pools, w, r.chrom, r.start, r.end, m, tier_of(r));
+}
+
+// the fold's output, refined (the refine pass runs inside the parallel
+// assembly: records are independent there)
 ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
     const int64_t n = (int64_t)R.size();
     if (n == 0) return {};
@@ -930,15 +947,18 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
                             (synced[(size_t)k] ? sp.emitted.size() - from[(size_t)k] : 0);
     }
     ItemVec out(at[(size_t)K] + 1);
-    parallel_items(K, nt, [&](int64_t k, int) {
+    parallel_items(K, nt, [&](int64_t k, int w) {
         const SpecOut &sp = spec[(size_t)k];
-        Item *dst = out.data() + at[(size_t)k];
+        Item *const d0 = out.data() + at[(size_t)k];
+        Item *dst = d0;
         const ItemVec &rp = rep[(size_t)k];
         dst = std::copy(rp.begin(), rp.end(), dst);
         if (synced[(size_t)k])
             for (size_t q = from[(size_t)k]; q < sp.emitted.size(); ++q) *dst++ = sp.record(R, q);
+        for (Item *it = d0; it < dst; ++it) refine_one(u, pools, w, *it);
     });
     out[at[(size_t)K]] = cur;
+    refine_one(u, pools, 0, out[at[(size_t)K]]);
     if (g_stats) {
         auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         std::fprintf(stderr, "  merge: repair %.1f assemble %.1f ms\n", d(ts1, ts2),
@@ -1146,27 +1166,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     // 3. merge adjacent (bwt.py:3222-3289)
     recs = merge_fold(u, pools, recs, nt);
     auto t3 = clk::now();
-    // 4. refine (bwt.py:3291-3314): only recomputed records can carry mismatches
-    //    (dynamic chunks: recomputes cluster along the contig)
-    {
-        const int64_t nr = (int64_t)recs.size(), CH = 4096;
-        parallel_items((nr + CH - 1) / CH, nt, [&](int64_t ch, int w) {
-            const int64_t a = ch * CH, b = std::min(nr, a + CH);
-            for (int64_t k = a; k < b; ++k) {
-                Item &r = recs[(size_t)k];
-                if (!r.x || r.x->mm == 0.0) continue;
-                // a record whose recompute already covered exactly [start, end)
-                // would be recomputed with the same arguments: same result
-                if (r.mlen > 0 && r.mlen == r.x->req_m && r.x->req_end == r.end) continue;
-                int64_t m = r.mlen;
-                if (m <= 0) {
-                    const int64_t rc = (int64_t)std::nearbyint(copies_of(r));
-                    m = std::max<int64_t>(1, (r.end - r.start) / std::max<int64_t>(1, rc ? rc : 1));
-                }
-                r = recompute(u, pools, w, r.chrom, r.start, r.end, m, tier_of(r));
-            }
-        });
-    }
+    // 4. refine (bwt.py:3291-3314): done inside merge_fold's assembly
     auto r1 = clk::now();
     sort_by_pos(recs, nt);
     auto r2 = clk::now();
@@ -1191,11 +1191,16 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     if (!one_offset) sort_by_pos(recs, nt);
     auto r3 = clk::now();
     const size_t n_before_collapse = recs.size();
+    clk::time_point t_collapse;
     // collapsed list as indices into recs (the slot takes the preferred record).
     // The fold only ever compares with the last kept record, and a collapse
     // needs an overlap, so an index whose start is >= every earlier end always
-    // starts fresh: chunks cut at such indices fold independently.
-    std::vector<uint32_t, BigAlloc<uint32_t>> col;
+    // starts fresh: chunks cut at such indices fold independently.  Each chunk
+    // then counts its records that pass the final filter (bwt.py:3940-3944),
+    // and every chunk materialises its passing records at its offset.
+    const double mc = (double)job.params.min_copies;
+    auto pass = [&](uint32_t i) { return copies_of(recs[i]) >= mc && recs[i].end - recs[i].start >= 6; };
+    size_t n_collapsed = 0;
     {
         const int64_t N = (int64_t)recs.size();
         const int C = N > 8192 ? 4 * std::max(1, nt) : 1;
@@ -1216,6 +1221,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
         });
         for (int t = 1; t <= C; ++t) sb[(size_t)t] = std::max(sb[(size_t)t], sb[(size_t)t - 1]);
         std::vector<std::vector<uint32_t>> part((size_t)C);
+        std::vector<int64_t> cnt((size_t)C + 1, 0);
         parallel_items(C, nt, [&](int64_t t, int) {
             auto &pc = part[(size_t)t];
             pc.reserve((size_t)(sb[(size_t)t + 1] - sb[(size_t)t]) / 2 + 16);
@@ -1226,38 +1232,28 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
                     pc.push_back((uint32_t)k);
                 }
             }
+            int64_t c = 0;
+            for (uint32_t i : pc) c += pass(i);
+            cnt[(size_t)t + 1] = c;
         });
-        std::vector<size_t> at((size_t)C + 1, 0);
-        for (int t = 0; t < C; ++t) at[(size_t)t + 1] = at[(size_t)t] + part[(size_t)t].size();
-        col.resize(at[(size_t)C]);
+        for (int t = 0; t < C; ++t) {
+            cnt[(size_t)t + 1] += cnt[(size_t)t];
+            n_collapsed += part[(size_t)t].size();
+        }
+        t_collapse = clk::now();
+        out.resize((size_t)cnt[(size_t)C]);
         parallel_items(C, nt, [&](int64_t t, int) {
-            std::copy(part[(size_t)t].begin(), part[(size_t)t].end(), col.begin() + (std::ptrdiff_t)at[(size_t)t]);
+            int64_t o = cnt[(size_t)t];
+            for (uint32_t i : part[(size_t)t])
+                if (pass(i)) materialize(u, recs[i], shift, out[(size_t)o++]);
         });
     }
-    auto r4 = clk::now();
-    // 7. final filter (bwt.py:3940-3944), counted and materialised in parallel chunks
-    const double mc = (double)job.params.min_copies;
-    auto pass = [&](uint32_t i) { return copies_of(recs[i]) >= mc && recs[i].end - recs[i].start >= 6; };
-    const int64_t ncol = (int64_t)col.size();
-    const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nt, ncol / 16384 + 1));
-    std::vector<int64_t> cnt((size_t)T + 1, 0);
-    parallel_items(T, T, [&](int64_t t, int) {
-        int64_t c = 0;
-        for (int64_t q = ncol * t / T; q < ncol * (t + 1) / T; ++q) c += pass(col[(size_t)q]);
-        cnt[(size_t)t + 1] = c;
-    });
-    for (int t = 0; t < T; ++t) cnt[(size_t)t + 1] += cnt[(size_t)t];
-    out.resize((size_t)cnt[(size_t)T]);
-    parallel_items(T, T, [&](int64_t t, int) {
-        int64_t o = cnt[(size_t)t];
-        for (int64_t q = ncol * t / T; q < ncol * (t + 1) / T; ++q)
-            if (pass(col[(size_t)q])) materialize(u, recs[col[(size_t)q]], shift, out[(size_t)o++]);
-    });
     auto t4 = clk::now();
     if (std::getenv("BWTMI_STATS")) {
         auto d = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         std::fprintf(stderr, "  merge %.1f (-> %zu) refine %.1f sort %.1f restore+sort %.1f collapse %.1f (%zu -> %zu) filter+mat %.1f ms\n",
-                     d(t2, t3), n_before_collapse, d(t3, r1), d(r1, r2), d(r2, r3), d(r3, r4), n_before_collapse, col.size(), d(r4, t4));
+                     d(t2, t3), n_before_collapse, d(t3, r1), d(r1, r2), d(r2, r3), d(r3, t_collapse), n_before_collapse,
+                     n_collapsed, d(t_collapse, t4));
     }
     if (ms) {
         ms[0] += std::chrono::duration<double, std::milli>(t1 - t0).count();

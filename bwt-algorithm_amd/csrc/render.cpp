@@ -192,9 +192,25 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
         });
         bool main_sorted = true;
         for (auto v : chunk_sorted) main_sorted = main_sorted && v;
-        if (main_sorted) {
+        if (main_sorted && rs.size() > nmain) {
+            // few k-mer pieces into a long sorted list: each piece goes behind the
+            // main records with an equal start (a stable merge), and the main
+            // list is copied in parallel segments between the insertion points
             std::stable_sort(rs.begin() + (std::ptrdiff_t)nmain, rs.end(), by_start);
-            std::inplace_merge(rs.begin(), rs.begin() + (std::ptrdiff_t)nmain, rs.end(), by_start);
+            const size_t np = rs.size() - nmain;
+            std::vector<size_t> at(np);
+            for (size_t q = 0; q < np; ++q)
+                at[q] = (size_t)(std::upper_bound(rs.begin(), rs.begin() + (std::ptrdiff_t)nmain, rs[nmain + q], by_start) -
+                                 rs.begin());
+            std::vector<const Rec *> merged(rs.size());
+            run_tasks((int64_t)np + 1, nt, [&](int64_t q) {   // segment q: main [at[q-1], at[q]) then piece q
+                const size_t a0 = q ? at[(size_t)q - 1] : 0, a1 = (size_t)q < np ? at[(size_t)q] : nmain;
+                std::copy(rs.begin() + (std::ptrdiff_t)a0, rs.begin() + (std::ptrdiff_t)a1,
+                          merged.begin() + (std::ptrdiff_t)(a0 + (size_t)q));
+                if ((size_t)q < np) merged[a1 + (size_t)q] = rs[nmain + (size_t)q];
+            });
+            rs.swap(merged);
+        } else if (main_sorted) {
         } else {
             std::stable_sort(rs.begin(), rs.end(), by_start);
         }
