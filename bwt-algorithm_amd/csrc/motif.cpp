@@ -101,6 +101,30 @@ uint64_t min_rot2(uint64_t x, int64_t n) {
     return best;
 }
 
+// 33..64 bases: the same over 128-bit words
+typedef unsigned __int128 u128;
+static bool pack2_acgt128(const char *s, int64_t n, u128 &x) {
+    uint64_t hi, lo;
+    if (n <= 32 || n > 64 || !pack2_acgt(s, n - 32, hi) || !pack2_acgt(s + (n - 32), 32, lo)) return false;
+    x = ((u128)hi << 64) | lo;
+    return true;
+}
+static u128 rc2_128(u128 x, int64_t n) {
+    const uint64_t hi = (uint64_t)(x >> 64), lo = (uint64_t)x;   // hi: first n-32 bases, lo: last 32
+    // reverse complement: rc(lo) (32 bases) first, then rc(hi) (n-32 bases)
+    return ((u128)rc2(lo, 32) << (2 * (n - 32))) | rc2(hi, n - 32);
+}
+static u128 min_rot2_128(u128 x, int64_t n) {
+    const int bits = (int)(2 * n);
+    const u128 mask = bits == 128 ? ~(u128)0 : (((u128)1 << bits) - 1);
+    u128 best = x;
+    for (int sh = 2; sh < bits; sh += 2) {
+        const u128 r = ((x << sh) | (x >> (bits - sh))) & mask;
+        best = r < best ? r : best;
+    }
+    return best;
+}
+
 void canonical_stranded(const std::string &s, std::string &canon, char &strand) {  // 694-716
     const int64_t n = (int64_t)s.size();
     if (n == 0) {
@@ -115,6 +139,16 @@ void canonical_stranded(const std::string &s, std::string &canon, char &strand) 
         const uint64_t v = fwd ? bf : br;
         canon.resize((size_t)n);
         for (int64_t i = 0; i < n; ++i) canon[(size_t)i] = "ACGT"[(v >> (2 * (n - 1 - i))) & 3u];
+        strand = fwd ? '+' : '-';
+        return;
+    }
+    u128 y;
+    if (pack2_acgt128(s.data(), n, y)) {
+        const u128 bf = min_rot2_128(y, n), br = min_rot2_128(rc2_128(y, n), n);
+        const bool fwd = bf <= br;
+        const u128 v = fwd ? bf : br;
+        canon.resize((size_t)n);
+        for (int64_t i = 0; i < n; ++i) canon[(size_t)i] = "ACGT"[(unsigned)(v >> (2 * (n - 1 - i))) & 3u];
         strand = fwd ? '+' : '-';
         return;
     }
@@ -136,6 +170,8 @@ void canonical_stranded(const std::string &s, std::string &canon, char &strand) 
 char canonical_strand(const char *s, int64_t n) {
     uint64_t x;
     if (n > 0 && pack2_acgt(s, n, x)) return min_rot2(x, n) <= min_rot2(rc2(x, n), n) ? '+' : '-';
+    u128 y;
+    if (pack2_acgt128(s, n, y)) return min_rot2_128(y, n) <= min_rot2_128(rc2_128(y, n), n) ? '+' : '-';
     thread_local std::string t, c;
     t.assign(s, (size_t)n);
     char st;

@@ -347,6 +347,7 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
 // ---------------------------------------------------------------- formatting
 struct Out {
     Text s;
+    std::string built, fc;   // per-chunk scratch of the row formatters (no thread-local lookups per row)
     void put(const char *p, int64_t n) { s.append(p, (size_t)n); }
     void put(const std::string &x) { s.append(x); }
     void put(View v) { if (v.n > 0) s.append(v.p, (size_t)v.n); }
@@ -442,7 +443,7 @@ void row_strfinder(Out &o, const Job &job, const Rec &r, const Rec *partner) {
     }
     o.c('\t');
     // core sequence: the actual-sequence slice, or the motif repeated int(copies) times
-    thread_local std::string built;
+    std::string &built = o.built;
     View core = act_of(job, r);
     if (core.empty()) {
         built.clear();
@@ -462,7 +463,7 @@ void row_strfinder(Out &o, const Job &job, const Rec &r, const Rec *partner) {
     o.i(cc); o.c(':'); o.i(r.n_eval); o.c('\t'); o.i(r.n_eval); o.c('\t');
     const int64_t tot = (flanks ? fl.n + fr.n : 0) + core.n;
     if (tot > 500) {
-        thread_local std::string fc;
+        std::string &fc = o.fc;
         fc.clear();
         if (flanks) { fc.append(fl.p ? fl.p : "", (size_t)fl.n); fc.append(core.p, (size_t)core.n); fc.append(fr.p ? fr.p : "", (size_t)fr.n); }
         else fc.assign(core.p, (size_t)core.n);

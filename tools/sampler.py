@@ -74,6 +74,9 @@ def inclusive(path, tabs):
             k += 2   # function line, then file:line
     incl = collections.Counter()
     for ch in chains:
+        if not any("libbwtmi" in fr for fr in ch):
+            continue   # idle / other threads: only samples inside the library count
+        incl["(samples in libbwtmi)"] += 1
         seen = set()
         for fr in ch:
             mod, off = fr.rsplit(":", 1)
