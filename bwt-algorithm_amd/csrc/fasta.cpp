@@ -16,6 +16,7 @@
 // buffers.  With world > 1 only this rank's fold units (shard_units) are
 // written -- the others keep their names and lengths for the shard layout.
 #include <fcntl.h>
+#include <immintrin.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -50,6 +51,7 @@ struct Chunk {
     int64_t a = 0, b = 0;     // [a, b): whole lines
     int64_t bad = -1;         // first non-ASCII byte of a sequence line, or of an invalid header
     int64_t pre = 0;          // content before the chunk's first header
+    bool plain = false;       // only '\n' and bytes 0x21..0x7f, no '>': lines need no strip
     std::vector<Hdr> hdrs;
     // pass 2 destinations (nullptr: not written)
     char *pre_dst = nullptr;
@@ -114,6 +116,29 @@ inline int64_t first_high(const char *s, int64_t n) {
     return -1;
 }
 
+// A chunk whose bytes are all '\n' or 0x21..0x7f other than '>' has no header,
+// no CR, no strippable whitespace and no non-ASCII byte: its content is every
+// byte but the newlines.  Returns the newline count, or -1 if not plain.
+// (AVX2, 32 bytes per step; a signed compare also flags bytes >= 0x80.)
+int64_t plain_newlines(const char *p, int64_t n) {
+    const __m256i vnl = _mm256_set1_epi8('\n'), vgt = _mm256_set1_epi8('>'), v21 = _mm256_set1_epi8(0x21);
+    int64_t q = 0, nl = 0;
+    for (; q + 32 <= n; q += 32) {
+        const __m256i v = _mm256_loadu_si256((const __m256i *)(p + q));
+        const __m256i isnl = _mm256_cmpeq_epi8(v, vnl);
+        const __m256i low = _mm256_cmpgt_epi8(v21, v);   // v < 0x21 or v >= 0x80
+        const __m256i bad = _mm256_or_si256(_mm256_andnot_si256(isnl, low), _mm256_cmpeq_epi8(v, vgt));
+        if (!_mm256_testz_si256(bad, bad)) return -1;
+        nl += __builtin_popcount((unsigned)_mm256_movemask_epi8(isnl));
+    }
+    for (; q < n; ++q) {
+        const unsigned char c = (unsigned char)p[q];
+        if (c == '\n') ++nl;
+        else if (c < 0x21 || c >= 0x80 || c == '>') return -1;
+    }
+    return nl;
+}
+
 // upper-cased copy (ASCII a-z), vectorised
 inline void upper_copy(char *__restrict d, const char *__restrict s, int64_t n) {
     for (int64_t q = 0; q < n; ++q) {
@@ -176,6 +201,12 @@ void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, i
         Chunk &C = ck[(size_t)t];
         C.a = cut[(size_t)t];
         C.b = cut[(size_t)t + 1];
+        static const bool no_plain = std::getenv("BWTMI_NO_PLAIN") != nullptr;   // A/B switch
+        if (const int64_t nl = no_plain ? -1 : plain_newlines(p + C.a, C.b - C.a); nl >= 0) {   // no header: all content
+            C.plain = true;
+            C.pre = (C.b - C.a) - nl;
+            return;
+        }
         for_lines(p, C.a, C.b, [&](int64_t s, int64_t e) {
             if (p[s] == '>') {
                 int64_t x = s + 1;
@@ -296,6 +327,17 @@ void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, i
     run_tasks(T, nt, [&](int64_t t) {
         Chunk &C = ck[(size_t)t];
         char *d = C.pre_dst;
+        if (C.plain) {   // lines end at '\n' only and need no strip
+            if (!d) return;
+            for (int64_t i = C.a; i < C.b;) {
+                const char *nl = (const char *)std::memchr(p + i, '\n', (size_t)(C.b - i));
+                const int64_t j = nl ? (int64_t)(nl - p) : C.b;
+                upper_copy(d, p + i, j - i);
+                d += j - i;
+                i = j + 1;
+            }
+            return;
+        }
         size_t h = 0;
         for_lines(p, C.a, C.b, [&](int64_t s, int64_t e) {
             if (p[s] == '>') {

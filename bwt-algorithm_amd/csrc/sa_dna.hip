@@ -187,9 +187,11 @@ __global__ __launch_bounds__(1024) void k_dna_short_fix(uint32_t *__restrict__ v
 }
 
 // groups by size class; the order inside a class does not matter (groups are disjoint)
-constexpr int kClasses = 5;   // <= 4, <= 16, <= 64 members (one wave), <= kMedium (workgroup), larger
+// <= 4, <= 16, <= 32, <= 64 members (W-lane segments of one wave), <= kMedium
+// (one workgroup), larger (segmented radix)
+constexpr int kClasses = 6;
 __device__ __forceinline__ int size_class(uint32_t sz) {
-    return sz <= 4 ? 0 : sz <= 16 ? 1 : sz <= 64 ? 2 : sz <= (uint32_t)kMedium ? 3 : 4;
+    return sz <= 4 ? 0 : sz <= 16 ? 1 : sz <= 32 ? 2 : sz <= 64 ? 3 : sz <= (uint32_t)kMedium ? 4 : 5;
 }
 
 __device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
@@ -353,6 +355,16 @@ __global__ __launch_bounds__(kWB) void k_ls_block(const uint32_t *__restrict__ s
     block_append<kWB>(multi, s + (uint32_t)t, s + (uint32_t)end + 1, ngs, nge, ncnt);
 }
 
+// one wave-class pass (KEYS: the gather) over the cnt groups of a class list
+template <int W, bool KEYS>
+void ls_wave_pass(Ctx &c, const char *name, const uint32_t *cs, const uint32_t *cz, uint32_t cnt, uint32_t *vals,
+                  uint32_t *rank, uint32_t *kb, int64_t n, int64_t h, uint32_t *xs, uint32_t *xe, uint32_t *ncnt) {
+    if (!cnt) return;
+    const unsigned grid = (unsigned)((cnt + (kLB / 64) * (64 / W) - 1) / ((kLB / 64) * (64 / W)));
+    KLAUNCH(name, 0.0, (k_ls_wave<W, KEYS>), dim3(grid), dim3(kLB), 0, c.stream, cs, cz, (int64_t)cnt, vals, rank, kb,
+            n, h, xs, xe, ncnt);
+}
+
 // groups larger than kMedium: (group index << 30 | rank[a+h]) keys gathered
 // into one segmented radix sort; starts/sizes/offs = the large-group table
 __global__ __launch_bounds__(kB) void k_dna_refine_keys(const uint32_t *__restrict__ starts, const uint32_t *__restrict__ sizes,
@@ -489,7 +501,7 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
         if (h >= 2 * n) return false;   // cannot happen ('$' is unique); the general path if it does
         // the keys are dead: class lists (5 x (start, size), capacity G each) and
         // the large-group table (3 x <= G) live in their buffer
-        c.slot[S_IDX0].ensure((size_t)(13 * G + 16) * 4);
+        c.slot[S_IDX0].ensure((size_t)((2 * kClasses + 3) * G + 16) * 4);
         keys = c.slot[S_IDX0].as<uint32_t>();
         uint32_t *cs = keys, *cz = keys + kClasses * G;
         HIPCHECK(hipMemsetAsync(counts, 0, 64, st));
@@ -498,24 +510,16 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
         HIPCHECK(hipMemcpyAsync(cnt, counts, sizeof cnt, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
         uint32_t *ncnt = counts + 8;
-        const int per_block = kLB / 64;
-        const unsigned gw[3] = {nblocks(cnt[0], per_block * 16), nblocks(cnt[1], per_block * 4),
-                                nblocks(cnt[2], per_block)};
         // gather pass over every class, then the sorts (large groups gather
         // straight into their radix keys, before any head is rewritten)
-        if (cnt[0])
-            KLAUNCH("dna_ls_keys", 0.0, (k_ls_wave<4, true>), dim3(gw[0]), dim3(kLB), 0, st, cs, cz, (int64_t)cnt[0], vals,
+        ls_wave_pass<4, true>(c, "dna_ls_keys", cs, cz, cnt[0], vals, rank, kb, n, h, xs, xe, ncnt);
+        ls_wave_pass<16, true>(c, "dna_ls_keys", cs + G, cz + G, cnt[1], vals, rank, kb, n, h, xs, xe, ncnt);
+        ls_wave_pass<32, true>(c, "dna_ls_keys", cs + 2 * G, cz + 2 * G, cnt[2], vals, rank, kb, n, h, xs, xe, ncnt);
+        ls_wave_pass<64, true>(c, "dna_ls_keys", cs + 3 * G, cz + 3 * G, cnt[3], vals, rank, kb, n, h, xs, xe, ncnt);
+        if (cnt[4])
+            KLAUNCH("dna_ls_keys", 0.0, k_ls_block<true>, dim3(cnt[4]), dim3(kWB), 0, st, cs + 4 * G, cz + 4 * G, vals,
                     rank, kb, n, h, xs, xe, ncnt);
-        if (cnt[1])
-            KLAUNCH("dna_ls_keys", 0.0, (k_ls_wave<16, true>), dim3(gw[1]), dim3(kLB), 0, st, cs + G, cz + G,
-                    (int64_t)cnt[1], vals, rank, kb, n, h, xs, xe, ncnt);
-        if (cnt[2])
-            KLAUNCH("dna_ls_keys", 0.0, (k_ls_wave<64, true>), dim3(gw[2]), dim3(kLB), 0, st, cs + 2 * G, cz + 2 * G,
-                    (int64_t)cnt[2], vals, rank, kb, n, h, xs, xe, ncnt);
-        if (cnt[3])
-            KLAUNCH("dna_ls_keys", 0.0, k_ls_block<true>, dim3(cnt[3]), dim3(kWB), 0, st, cs + 3 * G, cz + 3 * G, vals,
-                    rank, kb, n, h, xs, xe, ncnt);
-        const int64_t L = cnt[4];
+        const int64_t L = cnt[5];
         int64_t M = 0;
         uint32_t *tab = keys + 2 * kClasses * G;
         uint64_t *rk = nullptr;
@@ -526,8 +530,8 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
             lstart.resize((size_t)L);
             lsize.resize((size_t)L);
             loff.resize((size_t)L);
-            HIPCHECK(hipMemcpyAsync(lstart.data(), cs + 4 * G, (size_t)L * 4, hipMemcpyDeviceToHost, st));
-            HIPCHECK(hipMemcpyAsync(lsize.data(), cz + 4 * G, (size_t)L * 4, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipMemcpyAsync(lstart.data(), cs + 5 * G, (size_t)L * 4, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipMemcpyAsync(lsize.data(), cz + 5 * G, (size_t)L * 4, hipMemcpyDeviceToHost, st));
             HIPCHECK(hipStreamSynchronize(st));
             uint32_t mx = 0;
             for (int64_t q = 0; q < L; ++q) {
@@ -546,17 +550,12 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
             KLAUNCH("dna_refine_keys", 0.0, k_dna_refine_keys, grid2, dim3(kB), 0, st, tab, tab + L, tab + 2 * L, vals,
                     rank, n, h, rk, rv);
         }
-        if (cnt[0])
-            KLAUNCH("dna_ls_w4", 0.0, (k_ls_wave<4, false>), dim3(gw[0]), dim3(kLB), 0, st, cs, cz, (int64_t)cnt[0], vals,
-                    rank, kb, n, h, xs, xe, ncnt);
-        if (cnt[1])
-            KLAUNCH("dna_ls_w16", 0.0, (k_ls_wave<16, false>), dim3(gw[1]), dim3(kLB), 0, st, cs + G, cz + G,
-                    (int64_t)cnt[1], vals, rank, kb, n, h, xs, xe, ncnt);
-        if (cnt[2])
-            KLAUNCH("dna_ls_w64", 0.0, (k_ls_wave<64, false>), dim3(gw[2]), dim3(kLB), 0, st, cs + 2 * G, cz + 2 * G,
-                    (int64_t)cnt[2], vals, rank, kb, n, h, xs, xe, ncnt);
-        if (cnt[3])
-            KLAUNCH("dna_ls_block", 0.0, k_ls_block<false>, dim3(cnt[3]), dim3(kWB), 0, st, cs + 3 * G, cz + 3 * G, vals,
+        ls_wave_pass<4, false>(c, "dna_ls_w4", cs, cz, cnt[0], vals, rank, kb, n, h, xs, xe, ncnt);
+        ls_wave_pass<16, false>(c, "dna_ls_w16", cs + G, cz + G, cnt[1], vals, rank, kb, n, h, xs, xe, ncnt);
+        ls_wave_pass<32, false>(c, "dna_ls_w32", cs + 2 * G, cz + 2 * G, cnt[2], vals, rank, kb, n, h, xs, xe, ncnt);
+        ls_wave_pass<64, false>(c, "dna_ls_w64", cs + 3 * G, cz + 3 * G, cnt[3], vals, rank, kb, n, h, xs, xe, ncnt);
+        if (cnt[4])
+            KLAUNCH("dna_ls_block", 0.0, k_ls_block<false>, dim3(cnt[4]), dim3(kWB), 0, st, cs + 4 * G, cz + 4 * G, vals,
                     rank, kb, n, h, xs, xe, ncnt);
         uint32_t nc = 0;
         HIPCHECK(hipMemcpyAsync(&nc, ncnt, 4, hipMemcpyDeviceToHost, st));
