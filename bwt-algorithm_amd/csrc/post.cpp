@@ -712,62 +712,47 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
 // result is reused.  Canonical motifs are computed lazily: most neighbours
 // fail the distance test first.
 struct Canon {
-    std::string s;
+    std::string s;     // canonical string (motifs that do not pack)
+    uint64_t key = 0;  // packed canonical word of an ACGT motif <= 32 bases
+    int32_t len = -1;  // motif length; -1 = not computed yet
+    bool packed = false;
     bool ok = false;
 };
 
-inline const std::string &canon_get(const UnitCtx &u, const Item &it, Canon &c) {
-    if (!c.ok) {
-        if (g_counters) g_canons.fetch_add(1, std::memory_order_relaxed);
+// the canonical form of an item's motif, computed once per fold position:
+// for ACGT motifs <= 32 bases the least of the packed rotations of the motif
+// and of its reverse complement (the packed word orders like the string)
+inline void canon_fill(const UnitCtx &u, const Item &it, Canon &c) {
+    if (c.ok) return;
+    if (g_counters) g_canons.fetch_add(1, std::memory_order_relaxed);
+    const std::string_view mv = motif_of(u, it);
+    c.len = (int32_t)mv.size();
+    uint64_t x;
+    c.packed = mv.size() <= 32 && pack2_acgt(mv.data(), (int64_t)mv.size(), x);
+    if (c.packed) {
+        const uint64_t f = min_rot2(x, (int64_t)mv.size()), r = min_rot2(rc2(x, (int64_t)mv.size()), (int64_t)mv.size());
+        c.key = f < r ? f : r;
+    } else {
         thread_local std::string tmp;
-        const std::string_view mv = motif_of(u, it);
         tmp.assign(mv.data(), mv.size());
         char st;
         canonical_stranded(tmp, c.s, st);
-        c.ok = true;
     }
-    return c.s;
+    c.ok = true;
 }
 
-// get_canonical_motif_stranded(m1)[0] == ...(m2)[0] (bwt.py:694-716): the
-// canonical form is the least string over the rotations of m and of its
-// reverse complement, a set that is the same for every member, so equality
-// holds iff m2 is a rotation of m1 or of rc(m1).  ACGT motifs up to 32 bases
-// compare as 2-bit words, other motifs up to 8 bytes as byte words, longer
-// ones through the canonical strings.
+// get_canonical_motif_stranded(m1)[0] == ...(m2)[0] (bwt.py:694-716): equal
+// canonical forms.  A motif that packs (ACGT only) and one that does not never
+// share a canonical form (rotations and the reverse complement keep non-ACGT
+// symbols), so mixed pairs are unequal without building strings.
 inline bool same_canonical(const UnitCtx &u, const Item &r1, Canon &c1, const Item &r2, Canon &c2) {
-    const std::string_view a = motif_of(u, r1), b = motif_of(u, r2);
-    if (a.size() != b.size()) return false;
-    const size_t m = a.size();
-    if (m == 0) return true;
-    uint64_t pa, pb;
-    if (m <= 32 && pack2_acgt(a.data(), (int64_t)m, pa) && pack2_acgt(b.data(), (int64_t)m, pb)) {
-        const unsigned bits = (unsigned)(2 * m);
-        const uint64_t mask = bits == 64 ? ~0ull : ((1ull << bits) - 1);
-        const uint64_t pr = rc2(pa, (int64_t)m);
-        for (unsigned s = 0; s < bits; s += 2) {
-            const uint64_t rx = s ? (((pa << s) | (pa >> (bits - s))) & mask) : pa;
-            const uint64_t rr = s ? (((pr << s) | (pr >> (bits - s))) & mask) : pr;
-            if (rx == pb || rr == pb) return true;
-        }
-        return false;
-    }
-    if (m > 8) return canon_get(u, r1, c1) == canon_get(u, r2, c2);
-    uint64_t x = 0, r = 0, y = 0;
-    for (size_t i = 0; i < m; ++i) {
-        x = (x << 8) | (uint8_t)a[i];
-        r = (r << 8) | (uint8_t)comp_of(a[m - 1 - i]);
-        y = (y << 8) | (uint8_t)b[i];
-    }
-    const unsigned bits = (unsigned)(8 * m);
-    const uint64_t mask = bits == 64 ? ~0ull : ((1ull << bits) - 1);
-    for (size_t k = 0; k < m; ++k) {
-        const unsigned s = (unsigned)(8 * k);
-        const uint64_t rx = s ? (((x << s) | (x >> (bits - s))) & mask) : x;
-        const uint64_t rr = s ? (((r << s) | (r >> (bits - s))) & mask) : r;
-        if (rx == y || rr == y) return true;
-    }
-    return false;
+    const int64_t m1 = r1.x ? (int64_t)r1.x->motif.size() : r1.mlen, m2 = r2.x ? (int64_t)r2.x->motif.size() : r2.mlen;
+    if (m1 != m2) return false;
+    if (m1 == 0) return true;
+    canon_fill(u, r1, c1);
+    canon_fill(u, r2, c2);
+    if (c1.packed != c2.packed) return false;
+    return c1.packed ? c1.key == c2.key : c1.s == c2.s;
 }
 
 bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, Canon &c1, const Item &r2, Canon &c2,
