@@ -209,6 +209,10 @@ bool sa_dna_eligible(uint8_t last, int64_t n, const int64_t *totals);
 bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT);
 
 // ----- index (index.hip)
+// true when [p, p+n) lies in a host block of mem.h that is (now) registered
+// for DMA (api.cpp); the block stays registered while it is cached
+bool ensure_pinned(const void *base, const void *p, size_t n);
+
 struct DeviceIndex;
 // d_text: device text incl. sentinel, n bytes (padded by >= 64 bytes)
 DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t sa_sample,

@@ -381,6 +381,8 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     HIPCHECK(hipMemcpyAsync(&nk, pos + n, 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     out.resize(nk);
+    // into a registered block: a pinned DMA instead of a staged pageable copy
+    if (nk) (void)ensure_pinned(out.data(), out.data(), (size_t)nk * sizeof(ScreenedHit));
     if (nk) HIPCHECK(hipMemcpyAsync(out.data(), dout, (size_t)nk * sizeof(ScreenedHit), hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
 }

@@ -346,12 +346,37 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
 
 // ---------------------------------------------------------------- formatting
 struct Out {
+    // rows are written through a raw cursor into s (sized ahead, grown by
+    // doubling); finish() cuts s to what was written
     Text s;
+    char *w = nullptr, *e = nullptr;
     std::string built, fc;   // per-chunk scratch of the row formatters (no thread-local lookups per row)
-    void put(const char *p, int64_t n) { s.append(p, (size_t)n); }
-    void put(const std::string &x) { s.append(x); }
-    void put(View v) { if (v.n > 0) s.append(v.p, (size_t)v.n); }
-    void c(char ch) { s.push_back(ch); }
+    void reserve(size_t n) {
+        const size_t used = w ? (size_t)(w - s.data()) : 0;
+        if (s.size() < used + n) s.resize(used + n);
+        w = s.data() + used;
+        e = s.data() + s.size();
+    }
+    void need(size_t n) {
+        if ((size_t)(e - w) < n) reserve(std::max(n, s.size() + 4096));
+    }
+    Text finish() {
+        s.resize(w ? (size_t)(w - s.data()) : 0);
+        w = e = nullptr;
+        return std::move(s);
+    }
+    void put(const char *p, int64_t n) {
+        if (n <= 0) return;
+        need((size_t)n);
+        std::memcpy(w, p, (size_t)n);
+        w += n;
+    }
+    void put(const std::string &x) { put(x.data(), (int64_t)x.size()); }
+    void put(View v) { put(v.p, v.n); }
+    void c(char ch) {
+        need(1);
+        *w++ = ch;
+    }
     void f(const char *fmt, double x) {   // printf keeps Python's exact-value rounding
         if (fmt[1] == '.' && fmt[2] == '0' && fmt[3] == 'f' && x == std::floor(x) && std::fabs(x) < 1e15 &&
             !(x == 0.0 && std::signbit(x))) {
@@ -360,15 +385,14 @@ struct Out {
         }
         char b[64];
         int n = snprintf(b, sizeof b, fmt, x);
-        s.append(b, (size_t)n);
+        put(b, n);
     }
     void i(int64_t x) {
-        char b[24];
-        auto r = std::to_chars(b, b + sizeof b, x);
-        s.append(b, (size_t)(r.ptr - b));
+        need(24);
+        w = std::to_chars(w, w + 24, x).ptr;
     }
     void rep(const std::string &m, int64_t times) {
-        for (int64_t k = 0; k < times; ++k) s.append(m);
+        for (int64_t k = 0; k < times; ++k) put(m);
     }
 };
 
@@ -603,7 +627,7 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
         Out o;
         const Chunk &C = chunks[(size_t)ck];
         const int64_t a = C.a, b = C.b;
-        o.s.reserve((size_t)(b - a) * 256);
+        o.reserve((size_t)(b - a) * 256);
         double cp[4], ent;
         for (int64_t k = a; k < b; ++k) {
             const Rec &r = *rows[(size_t)k].r;
@@ -648,7 +672,7 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
                     row_strfinder(o, job, r, rows[(size_t)k].partner);
             }
         }
-        out.parts[(size_t)ck] = std::move(o.s);
+        out.parts[(size_t)ck] = o.finish();
         if (on_part) (*on_part)((size_t)ck);
     });
     auto t3 = std::chrono::steady_clock::now();
