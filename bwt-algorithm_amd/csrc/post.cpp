@@ -932,6 +932,12 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
                             (synced[(size_t)k] ? sp.emitted.size() - from[(size_t)k] : 0);
     }
     ItemVec out(at[(size_t)K] + 1);
+    // assembly, refine, and the (start, end) order of the result: the fold's
+    // output is ordered by start (a merged record starts where its run did);
+    // refine only moves ends, so only runs of equal start need ordering by end
+    // -- done here per chunk, then for the runs that cross a chunk edge
+    std::vector<uint8_t> by_start((size_t)K, 1);
+    auto by_end = [](const Item &x, const Item &y) { return x.end < y.end; };
     parallel_items(K, nt, [&](int64_t k, int w) {
         const SpecOut &sp = spec[(size_t)k];
         Item *const d0 = out.data() + at[(size_t)k];
@@ -941,9 +947,31 @@ ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
         if (synced[(size_t)k])
             for (size_t q = from[(size_t)k]; q < sp.emitted.size(); ++q) *dst++ = sp.record(R, q);
         for (Item *it = d0; it < dst; ++it) refine_one(u, pools, w, *it);
+        for (Item *it = d0 + 1; it < dst; ++it)
+            if (it[-1].start > it->start) { by_start[(size_t)k] = 0; return; }
+        for (Item *i = d0; i < dst;) {
+            Item *j = i + 1;
+            while (j < dst && j->start == i->start) ++j;
+            if (j - i > 1) std::stable_sort(i, j, by_end);
+            i = j;
+        }
     });
     out[at[(size_t)K]] = cur;
     refine_one(u, pools, 0, out[at[(size_t)K]]);
+    bool ordered = true;
+    for (int64_t k = 0; k < K; ++k) ordered = ordered && by_start[(size_t)k];
+    const size_t N = out.size();
+    for (int64_t k = 1; k <= K && ordered; ++k) {   // chunk edges (the last edge precedes `cur`)
+        const size_t b = at[(size_t)k];
+        if (b == 0 || b >= N) continue;
+        if (out[b - 1].start > out[b].start) { ordered = false; break; }
+        if (out[b - 1].start < out[b].start || out[b - 1].end <= out[b].end) continue;
+        size_t i = b - 1, j = b + 1;   // the equal-start run across the edge
+        while (i > 0 && out[i - 1].start == out[b].start) --i;
+        while (j < N && out[j].start == out[b].start) ++j;
+        std::stable_sort(out.begin() + (std::ptrdiff_t)i, out.begin() + (std::ptrdiff_t)j, by_end);
+    }
+    if (!ordered) sort_by_pos(out, nt);   // not expected: the general stable sort
     if (g_stats) {
         auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         std::fprintf(stderr, "  merge: repair %.1f assemble %.1f ms\n", d(ts1, ts2),
@@ -1152,8 +1180,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     recs = merge_fold(u, pools, recs, nt);
     auto t3 = clk::now();
     // 4. refine (bwt.py:3291-3314): done inside merge_fold's assembly
-    auto r1 = clk::now();
-    sort_by_pos(recs, nt);
+    auto r1 = clk::now();   // merge_fold returns its records in (start, end) order
     auto r2 = clk::now();
     // 5. restore coordinates (bwt.py:3316-3325); actual_sequence is the frame slice.
     //    With one trim offset for the whole unit the (start, end) order is unchanged.
