@@ -47,7 +47,8 @@ VALU_LANE_OPS_PEAK = 256 * 4 * 32 * 2.4e9
 B_ALG_PER_BASE = 16.7          # compulsory HBM bytes per base, CLI path
 PMC_SUMMARY = os.path.join(REPO, "profiles", "pmc_traffic.json")
 # bench kernel-timer names -> kernel names in the rocprofv3 summaries
-KERNEL_OF = {"radix_scatter_kv8": "k_scatter<u32,u32>", "radix_scatter_kv12": "k_scatter<u64,u32>",
+KERNEL_OF = {"radix_scatter_kv8": "k_scatter<u32,u32>", "radix_partition_kv8": "k_scatter<u32,u32>",
+             "radix_scatter_kv12": "k_scatter<u64,u32>",
              "radix_scatter_kv16": "k_scatter<u64,u64>", "bwt_gather": "k_bwt", "occ_blocks": "k_occ_blocks",
              "sa_init_keys": "k_init_keys", "kmer_dna": "k_kmer_dna", "fm2_local": "k_fm2_local",
              "fm2_counts": "k_fm2_counts", "dna_ls_keys": "k_ls_wave"}

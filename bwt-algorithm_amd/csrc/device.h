@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <thread>
 #include <vector>
@@ -101,6 +103,15 @@ struct Ctx {
         }
         return evpool[evused++];
     }
+    // BWTMI_KTRACE=path (timing on): one line per launch (name, ms, idle ms
+    // since the previous launch ended) and the drivers' notes, appended to path
+    static FILE *ktrace_file() {
+        static FILE *f = [] {
+            const char *e = std::getenv("BWTMI_KTRACE");
+            return e && *e ? std::fopen(e, "a") : (FILE *)nullptr;
+        }();
+        return f;
+    }
     // every kernel launch is a leaf timer (KLAUNCH); kbegin/kend must not nest
     void kbegin(const char *name, double alg_bytes = 0) {
         if (!ktiming) return;
@@ -115,11 +126,21 @@ struct Ctx {
         open.pop_back();
     }
     void kresolve() {   // after a stream sync
-        for (auto &p : pending) {
+        FILE *trace = ktrace_file();
+        for (size_t i = 0; i < pending.size(); ++i) {
+            auto &p = pending[i];
             float ms = 0;
             if (hipEventElapsedTime(&ms, p.a, p.b) != hipSuccess) {
                 ms = 0;
                 (void)hipGetLastError();   // do not leave a sticky error for the next check
+            }
+            if (trace) {
+                float gap = 0;
+                if (i && hipEventElapsedTime(&gap, pending[i - 1].b, p.a) != hipSuccess) {
+                    gap = -1;
+                    (void)hipGetLastError();
+                }
+                std::fprintf(trace, "%s %.4f %.4f\n", p.name.c_str(), ms, gap);
             }
             bool found = false;
             for (auto &k : kstats)
@@ -131,6 +152,10 @@ struct Ctx {
                     break;
                 }
             if (!found) kstats.push_back({p.name, KStat{ms, 1, p.bytes}});
+        }
+        if (trace) {
+            std::fprintf(trace, "-- resolve\n");
+            std::fflush(trace);
         }
         pending.clear();
         open.clear();
@@ -184,6 +209,19 @@ void exclusive_scan(Ctx &c, const T *in, T *out, int64_t n);   // out may alias 
 void radix_sort_pairs(Ctx &c, uint64_t *keys, uint64_t *vals, int64_t n, int bit0, int bit1);
 void radix_sort_pairs32(Ctx &c, uint64_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1);
 void radix_sort_pairs_k32(Ctx &c, uint32_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1);
+// XCD-aware tile order: blocks b and b + 8 share an XCD (and its L2) under the
+// observed round-robin placement, so each group of blocks b % 8 takes one
+// contiguous range of tiles and neighbouring tiles run on one L2 at about the
+// same time (their writes to a shared 128-B line merge there before HBM).
+// Bijective for any ntiles; speed only, never correctness.
+__device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t ntiles) {
+    const int64_t q = ntiles / 8, r = ntiles % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// one stable 8-bit pass at `shift` from (kin, vin) into (kout, vout)
+void radix_pass_k32(Ctx &c, const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int64_t n,
+                    int shift);
 
 // ----- strict scan (strict_scan.hip)
 struct ScanResult {

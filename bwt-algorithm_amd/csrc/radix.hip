@@ -134,7 +134,7 @@ template <class KT, class V, int BLOCK, int ITEMS, bool NT, bool SPLIT>
 __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, const V *__restrict__ vin,
                                                    KT *__restrict__ kout, V *__restrict__ vout,
                                                    const uint32_t *__restrict__ offs, int64_t n, int shift,
-                                                   int64_t ntiles) {
+                                                   int64_t ntiles, int swz) {
     constexpr int kT = BLOCK * ITEMS;
     constexpr int NW = BLOCK / 64;
     static_assert(BLOCK >= 256 && BLOCK % 64 == 0, "threads 0..255 own one digit each");
@@ -152,7 +152,8 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, c
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < NW * 256; i += BLOCK) (&wcnt[0][0])[i] = 0;
     __syncthreads();
-    const int64_t tbase = (int64_t)blockIdx.x * kT;
+    const int64_t tile = swz ? xcd_tile(blockIdx.x, ntiles) : (int64_t)blockIdx.x;
+    const int64_t tbase = tile * kT;
     const int64_t wbase = tbase + (int64_t)wv * (ITEMS * 64);
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     KT k[ITEMS];
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, c
     if (dg < 256) {
         uint32_t toff = inc - tot;
         for (int w = 0; w < wv; ++w) toff += dsum[w];
-        gdelta[dg] = offs[(int64_t)dg * ntiles + blockIdx.x] - toff;
+        gdelta[dg] = offs[(int64_t)dg * ntiles + tile] - toff;
         uint32_t b = toff;
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
@@ -262,6 +263,7 @@ void radix_sort_cfg(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
     KT *ka = keys, *kb = c.slot[S_SORT_TMP0].as<KT>();
     V *va = vals, *vb = vals ? c.slot[S_SORT_TMP1].as<V>() : nullptr;
     uint32_t *cnt = c.slot[S_SORT_HIST].as<uint32_t>();
+    static const int swz = [] { const char *e = std::getenv("BWTMI_RADIX_SWZ"); return e ? std::atoi(e) : 1; }();
     int passes = 0;
     for (int sh = bit0; sh < bit1; sh += 8) {
         // read the keys once
@@ -272,7 +274,7 @@ void radix_sort_cfg(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
         KLAUNCH(sizeof(KT) == 4 ? "radix_scatter_kv8" : sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16",
                 (double)n * 2.0 * ((double)sizeof(KT) + (vals ? (double)sizeof(V) : 0.0)),
                 (k_scatter<KT, V, BLOCK, ITEMS, NT, SPLIT>), dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, ka, va,
-                kb, vb, cnt, n, sh, ntiles);
+                kb, vb, cnt, n, sh, ntiles, swz);
         std::swap(ka, kb);
         std::swap(va, vb);
         ++passes;
@@ -337,6 +339,22 @@ void radix_sort_pairs(Ctx &c, uint64_t *keys, uint64_t *vals, int64_t n, int bit
 void radix_sort_pairs32(Ctx &c, uint64_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1) {
     radix_sort_impl<uint64_t, uint32_t>(c, keys, vals, n, bit0, bit1);
 }
+// one pass: (kin, vin) -> (kout, vout) ordered by the 8-bit digit at `shift`
+void radix_pass_k32(Ctx &c, const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int64_t n,
+                    int shift) {
+    if (n <= 0) return;
+    constexpr int BLOCK = 512, ITEMS = 16, kT = BLOCK * ITEMS;
+    const int64_t ntiles = (n + kT - 1) / kT;
+    c.slot[S_SORT_HIST].ensure((size_t)ntiles * 256 * sizeof(uint32_t));
+    uint32_t *cnt = c.slot[S_SORT_HIST].as<uint32_t>();
+    KLAUNCH("radix_hist", (double)n * 4.0, (k_hist<kT / kBlock, uint32_t>), dim3((unsigned)ntiles), dim3(kBlock), 0,
+            c.stream, kin, cnt, n, shift, ntiles);
+    exclusive_scan<uint32_t>(c, cnt, cnt, ntiles * 256);
+    KLAUNCH("radix_partition_kv8", (double)n * 16.0, (k_scatter<uint32_t, uint32_t, BLOCK, ITEMS, false, true>),
+            dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, kin, vin, kout, vout, cnt, n, shift, ntiles, 1);
+    HIPCHECK(hipGetLastError());
+}
+
 void radix_sort_pairs_k32(Ctx &c, uint32_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1) {
     static const int v = [] { const char *e = std::getenv("BWTMI_RADIX32"); return e ? std::atoi(e) : 0; }();
     switch (v) {   // geometry A/B (tools/gpu_radix_ab.sh)

@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -126,6 +127,34 @@ __global__ __launch_bounds__(kB) void k_dna_rank0(const uint32_t *__restrict__ v
     if (r >= n) return;
     const uint32_t started = ps[r + 1];
     rank[vals[r] & kPosMask] = started > pe[r] ? gs[started - 1] : (uint32_t)r;
+}
+
+// the same ranks in two steps: the heads in SA order (coalesced), then -- after
+// a pass that orders the (position, head) pairs by the position's top 8 bits --
+// the writes, each workgroup's confined to one 2^shift-position window that
+// its XCD's L2 holds, so the scattered 4-byte stores reach HBM as whole lines
+__global__ __launch_bounds__(kB) void k_dna_heads(const uint32_t *__restrict__ ps, const uint32_t *__restrict__ pe,
+                                                  const uint32_t *__restrict__ gs, int64_t n, uint32_t *__restrict__ hd) {
+    const int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (r >= n) return;
+    const uint32_t started = ps[r + 1];
+    hd[r] = started > pe[r] ? gs[started - 1] : (uint32_t)r;
+}
+
+constexpr int kPutItems = 16;
+__global__ __launch_bounds__(kB) void k_dna_rank_put(const uint32_t *__restrict__ pv, const uint32_t *__restrict__ hd,
+                                                     int64_t n, int64_t ntiles, uint32_t *__restrict__ rank) {
+    const int64_t base = xcd_tile(blockIdx.x, ntiles) * (kB * kPutItems) + threadIdx.x;
+    uint32_t p[kPutItems], h[kPutItems];
+#pragma unroll
+    for (int i = 0; i < kPutItems; ++i) {
+        const int64_t r = base + (int64_t)i * kB;
+        p[i] = r < n ? pv[r] : 0u;
+        h[i] = r < n ? hd[r] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < kPutItems; ++i)
+        if (base + (int64_t)i * kB < n) rank[p[i] & kPosMask] = h[i];
 }
 
 // the <= 16 suffixes with fewer than 16 bases before '$' (their keys are
@@ -225,16 +254,103 @@ __device__ __forceinline__ void block_append(bool on, uint32_t st, uint32_t en, 
     __syncthreads();   // wc is reused by the next call
 }
 
+// The next round's group list is appended by ~10^4 workgroups per pass; one
+// counter would serialise them in L2 (~10 ns each).  Eight counters instead,
+// one per blockIdx % 8: shard q owns list chunks q, q + 8, q + 16, ... of kCH
+// slots, so an entry's slot follows from its shard and its index there.  The
+// unused tail of each shard's last chunk is a hole the reader skips
+// (ShardedList::live).  A slot past cap raises *ovf (the caller then takes
+// the general path).
+constexpr uint32_t kCH = 1024;
+__device__ __forceinline__ uint32_t shard_slot(uint32_t v, uint32_t q) { return ((v / kCH) * 8 + q) * kCH + v % kCH; }
+
+struct ShardedList {
+    uint32_t cnt[8];   // entries of each shard
+    uint32_t S;        // slots [0, S) are sharded; [S, G) are plain
+    __device__ __forceinline__ bool live(uint32_t j) const {
+        if (j >= S) return true;
+        const uint32_t ch = j / kCH;
+        return (ch / 8) * kCH + j % kCH < cnt[ch % 8];
+    }
+};
+
+template <int NT>
+__device__ __forceinline__ void block_append_sharded(bool on, uint32_t st, uint32_t en, uint32_t *__restrict__ ls,
+                                                     uint32_t *__restrict__ le, uint32_t *__restrict__ cnt8,
+                                                     uint32_t cap, uint32_t *__restrict__ ovf) {
+    __shared__ uint32_t wc[NT / 64 + 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t q = blockIdx.x & 7u;
+    const uint64_t m = __ballot(on);
+    if (lane == 0) wc[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < NT / 64; ++w) {
+            const uint32_t x = wc[w];
+            wc[w] = tot;
+            tot += x;
+        }
+        wc[NT / 64] = tot ? atomicAdd(&cnt8[q], tot) : 0u;
+    }
+    __syncthreads();
+    if (on) {
+        const uint32_t at = shard_slot(wc[NT / 64] + wc[wv] + (uint32_t)__popcll(m & lanes_below(lane)), q);
+        if (at < cap) {
+            ls[at] = st;
+            le[at] = en;
+        } else {
+            atomicOr(ovf, 1u);
+        }
+    }
+    __syncthreads();   // wc is reused by the next call
+}
+
+// the round's groups into the size-class lists: kCI groups per thread, slots
+// inside the workgroup from wave ballots + LDS counters, then one atomic per
+// class and workgroup
+constexpr int kCI = 16;
 __global__ __launch_bounds__(kB) void k_dna_classify(const uint32_t *__restrict__ gs, const uint32_t *__restrict__ ge,
-                                                     int64_t G, uint32_t *__restrict__ cls_start,
+                                                     int64_t G, ShardedList sl, uint32_t *__restrict__ cls_start,
                                                      uint32_t *__restrict__ cls_size, uint32_t *__restrict__ counts,
                                                      int64_t cap) {
-    const int64_t g = (int64_t)blockIdx.x * kB + threadIdx.x;
-    const bool live = g < G;
-    const uint32_t s = live ? gs[g] : 0u, sz = live ? ge[g] - s : 0u;
-    const int c = size_class(sz);
-    for (int k = 0; k < kClasses; ++k)   // one atomic per workgroup and class
-        block_append<kB>(live && c == k, s, sz, cls_start + (int64_t)k * cap, cls_size + (int64_t)k * cap, &counts[k]);
+    __shared__ uint32_t lc[kClasses], base[kClasses];
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x < kClasses) lc[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t st[kCI], sz[kCI], slot[kCI];
+    int cl[kCI];
+#pragma unroll
+    for (int i = 0; i < kCI; ++i) {
+        const int64_t g = (int64_t)blockIdx.x * (kB * kCI) + (int64_t)i * kB + threadIdx.x;
+        cl[i] = -1;
+        st[i] = sz[i] = slot[i] = 0;
+        if (g < G && sl.live((uint32_t)g)) {
+            st[i] = gs[g];
+            sz[i] = ge[g] - st[i];
+            cl[i] = size_class(sz[i]);
+        }
+#pragma unroll
+        for (int k = 0; k < kClasses; ++k) {
+            const uint64_t m = __ballot(cl[i] == k);
+            if (!m) continue;
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            uint32_t b = 0;
+            if (lane == leader) b = atomicAdd(&lc[k], (uint32_t)__popcll(m));
+            b = __shfl(b, leader, 64);
+            if (cl[i] == k) slot[i] = b + (uint32_t)__popcll(m & lanes_below(lane));
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < kClasses) base[threadIdx.x] = lc[threadIdx.x] ? atomicAdd(&counts[threadIdx.x], lc[threadIdx.x]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kCI; ++i)
+        if (cl[i] >= 0) {
+            const int64_t at = (int64_t)cl[i] * cap + base[cl[i]] + slot[i];
+            cls_start[at] = st[i];
+            cls_size[at] = sz[i];
+        }
 }
 
 // the doubling key of member v: rank of the suffix h bases on (a group member
@@ -253,7 +369,7 @@ template <int W, bool KEYS>
 __global__ __launch_bounds__(kLB) void k_ls_wave(const uint32_t *__restrict__ starts, const uint32_t *__restrict__ sizes,
                                                 int64_t cnt, uint32_t *__restrict__ vals, uint32_t *__restrict__ rank,
                                                 uint32_t *__restrict__ kb, int64_t n, int64_t h, uint32_t *__restrict__ ngs,
-                                                uint32_t *__restrict__ nge, uint32_t *__restrict__ ncnt) {
+                                                uint32_t *__restrict__ nge, uint32_t *__restrict__ ncnt, uint32_t cap) {
     const int lane = threadIdx.x & 63, kk = lane & (W - 1);
     const int64_t g = (((int64_t)blockIdx.x * kLB + threadIdx.x) >> 6) * (64 / W) + lane / W;
     uint32_t s = 0, sz = 0;
@@ -266,7 +382,8 @@ __global__ __launch_bounds__(kLB) void k_ls_wave(const uint32_t *__restrict__ st
         if (live) kb[s + kk] = ls_key(rank, vals[s + kk], n, h);
         return;
     }
-    uint64_t x = live ? ((uint64_t)kb[s + kk] << 32) | vals[s + kk] : ~0ull;
+    const uint32_t orig = live ? vals[s + kk] : 0u;
+    uint64_t x = live ? ((uint64_t)kb[s + kk] << 32) | orig : ~0ull;
 #pragma unroll
     for (int k2 = 2; k2 <= W; k2 <<= 1)
 #pragma unroll
@@ -282,13 +399,15 @@ __global__ __launch_bounds__(kLB) void k_ls_wave(const uint32_t *__restrict__ st
     const uint64_t S = __ballot(start), T = __ballot(tail);
     const int seg = lane - kk;
     if (live) {
+        // every member's rank is s when the round starts: only the members of
+        // the later subgroups move, and only moved values are stored
         const int hl = 63 - __clzll((long long)(S & (lanes_below(lane) | (1ull << lane))));
-        vals[s + kk] = v;
-        rank[v & kPosMask] = s + (uint32_t)(hl - seg);
+        if (v != orig) vals[s + kk] = v;
+        if (hl != seg) rank[v & kPosMask] = s + (uint32_t)(hl - seg);
     }
     const bool multi = start && !tail;
     const int el = multi ? __ffsll((unsigned long long)(T & (~0ull << lane))) - 1 : 0;
-    block_append<kLB>(multi, s + kk, s + (uint32_t)(el - seg) + 1, ngs, nge, ncnt);
+    block_append_sharded<kLB>(multi, s + kk, s + (uint32_t)(el - seg) + 1, ngs, nge, ncnt, cap, ncnt + 8);
 }
 
 // one doubling pass over a group of <= kMedium members in one workgroup
@@ -298,7 +417,7 @@ __global__ __launch_bounds__(kWB) void k_ls_block(const uint32_t *__restrict__ s
                                                   uint32_t *__restrict__ vals, uint32_t *__restrict__ rank,
                                                   uint32_t *__restrict__ kb, int64_t n, int64_t h,
                                                   uint32_t *__restrict__ ngs, uint32_t *__restrict__ nge,
-                                                  uint32_t *__restrict__ ncnt) {
+                                                  uint32_t *__restrict__ ncnt, uint32_t cap) {
     __shared__ uint64_t x[kMedium];
     __shared__ int wl[kWB / 64], wf[kWB / 64];
     const uint32_t s = starts[blockIdx.x], sz = sizes[blockIdx.x];
@@ -309,7 +428,8 @@ __global__ __launch_bounds__(kWB) void k_ls_block(const uint32_t *__restrict__ s
         if (t < (int)sz) kb[s + t] = ls_key(rank, vals[s + t], n, h);
         return;
     }
-    if (t < (int)p2) x[t] = t < (int)sz ? ((uint64_t)kb[s + t] << 32) | vals[s + t] : ~0ull;
+    const uint32_t orig = t < (int)sz ? vals[s + t] : 0u;
+    if (t < (int)p2) x[t] = t < (int)sz ? ((uint64_t)kb[s + t] << 32) | orig : ~0ull;
     __syncthreads();
     for (uint32_t k2 = 2; k2 <= p2; k2 <<= 1)
         for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
@@ -339,10 +459,10 @@ __global__ __launch_bounds__(kWB) void k_ls_block(const uint32_t *__restrict__ s
     if (Sb) head = wv * 64 + 63 - __clzll((long long)Sb);
     else
         for (int w = 0; w < wv; ++w) head = max(head, wl[w]);
-    if (live) {
+    if (live) {   // as in k_ls_wave: only moved values and later subgroups are stored
         const uint32_t v = (uint32_t)me;
-        vals[s + t] = v;
-        rank[v & kPosMask] = s + (uint32_t)head;
+        if (v != orig) vals[s + t] = v;
+        if (head) rank[v & kPosMask] = s + (uint32_t)head;
     }
     const bool multi = start && !tail;
     int end = 1 << 30;
@@ -352,17 +472,18 @@ __global__ __launch_bounds__(kWB) void k_ls_block(const uint32_t *__restrict__ s
         else
             for (int w = wv + 1; w < kWB / 64; ++w) end = min(end, wf[w]);
     }
-    block_append<kWB>(multi, s + (uint32_t)t, s + (uint32_t)end + 1, ngs, nge, ncnt);
+    block_append_sharded<kWB>(multi, s + (uint32_t)t, s + (uint32_t)end + 1, ngs, nge, ncnt, cap, ncnt + 8);
 }
 
 // one wave-class pass (KEYS: the gather) over the cnt groups of a class list
 template <int W, bool KEYS>
 void ls_wave_pass(Ctx &c, const char *name, const uint32_t *cs, const uint32_t *cz, uint32_t cnt, uint32_t *vals,
-                  uint32_t *rank, uint32_t *kb, int64_t n, int64_t h, uint32_t *xs, uint32_t *xe, uint32_t *ncnt) {
+                  uint32_t *rank, uint32_t *kb, int64_t n, int64_t h, uint32_t *xs, uint32_t *xe, uint32_t *ncnt,
+                  uint32_t cap) {
     if (!cnt) return;
     const unsigned grid = (unsigned)((cnt + (kLB / 64) * (64 / W) - 1) / ((kLB / 64) * (64 / W)));
     KLAUNCH(name, 0.0, (k_ls_wave<W, KEYS>), dim3(grid), dim3(kLB), 0, c.stream, cs, cz, (int64_t)cnt, vals, rank, kb,
-            n, h, xs, xe, ncnt);
+            n, h, xs, xe, ncnt, cap);
 }
 
 // groups larger than kMedium: (group index << 30 | rank[a+h]) keys gathered
@@ -458,7 +579,7 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
     c.slot[S_IDX4].ensure((size_t)(n + 1) * 4);     // their positions
     c.slot[S_IDX5].ensure((size_t)(n + 1) * 4);     // group-end flags
     c.slot[S_IDX6].ensure((size_t)(n + 1) * 4);     // their positions
-    c.slot[S_MISC3].ensure(64);
+    c.slot[S_MISC3].ensure(128);   // 6 class counts | 8 shard counts, overflow flag
     uint32_t *keys = c.slot[S_IDX0].as<uint32_t>();
     uint32_t *vals = c.slot[S_IDX1].as<uint32_t>();
     uint64_t *P = c.slot[S_IDX2].as<uint64_t>();
@@ -485,7 +606,12 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
     };
     KLAUNCH("dna_flags", 8.0 * (double)n, k_dna_flags, dim3(nblocks(n)), dim3(kB), 0, st, keys, n, fs, fe);
     // group lists: current round and next round, (start, exclusive end) in vals
-    for (int q : {S_MISC0, S_MISC1, S_IDX9, S_IDX10}) c.slot[q].ensure((size_t)(n / 2 + 64) * 4);
+    // (<= n/2 groups; the sharded appends leave holes: slack for them and for
+    // uneven shards -- a list that would outgrow it takes the general path)
+    const int64_t lalloc = n / 2 + n / 8 + 16 * (int64_t)kCH + 64;
+    for (int q : {S_MISC0, S_MISC1, S_IDX9, S_IDX10}) c.slot[q].ensure((size_t)lalloc * 4);
+    int64_t lcap = lalloc;
+    if (const char *e = std::getenv("BWTMI_LS_CAP")) lcap = std::min<int64_t>(lcap, std::atoll(e));   // test hook
     c.slot[S_IDX8].ensure((size_t)n * 4 + 64);
     c.slot[S_IDX11].ensure((size_t)n * 4 + 64);
     uint32_t *kb = c.slot[S_IDX11].as<uint32_t>();   // a round's keys, aligned with vals
@@ -493,10 +619,34 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
     uint32_t *xs = c.slot[S_IDX9].as<uint32_t>(), *xe = c.slot[S_IDX10].as<uint32_t>();
     uint32_t *rank = c.slot[S_IDX8].as<uint32_t>();
     int64_t G = groups(fs, ps, fe, pe, n, gs, ge);
-    KLAUNCH("dna_rank0", 12.0 * (double)n, k_dna_rank0, dim3(nblocks(n)), dim3(kB), 0, st, vals, ps, pe, gs, n, rank);
+    static const int rank0_direct = [] { const char *e = std::getenv("BWTMI_RANK0_DIRECT"); return e && *e == '1'; }();
+    if (rank0_direct || n < (1 << 16)) {
+        KLAUNCH("dna_rank0", 12.0 * (double)n, k_dna_rank0, dim3(nblocks(n)), dim3(kB), 0, st, vals, ps, pe, gs, n,
+                rank);
+    } else {
+        // keys are dead: heads there; the pass output in the sort's buffers
+        int bits = 0;
+        while ((int64_t{1} << bits) < n) ++bits;
+        c.slot[S_SORT_TMP0].ensure((size_t)n * 4);
+        c.slot[S_SORT_TMP1].ensure((size_t)n * 4);
+        uint32_t *pv = c.slot[S_SORT_TMP0].as<uint32_t>(), *ph = c.slot[S_SORT_TMP1].as<uint32_t>();
+        KLAUNCH("dna_heads", 12.0 * (double)n, k_dna_heads, dim3(nblocks(n)), dim3(kB), 0, st, ps, pe, gs, n, keys);
+        radix_pass_k32(c, vals, keys, pv, ph, n, bits - 8);
+        const int64_t nt = (n + kB * kPutItems - 1) / (kB * kPutItems);
+        // (unused) LDS caps the workgroups per CU, and so the span of positions
+        // an XCD writes at once: at 1 workgroup per CU an XCD's 32 x 4096
+        // pairs stay within about a quarter of a 2^shift window (2 MB at
+        // 100 Mbp) and the L2 merges the stores into whole lines.  r02aj:
+        // 1.13-1.36 ms at full occupancy, 0.63 at 2 per CU, 0.55 at 1 per CU
+        // (the direct scatter: 2.35)
+        static const int put_lds = [] { const char *e = std::getenv("BWTMI_PUT_LDS"); return e ? std::atoi(e) : 128; }();
+        KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put, dim3((unsigned)nt), dim3(kB), (size_t)put_lds * 1024,
+                st, pv, ph, n, nt, rank);
+    }
     if (G) KLAUNCH("dna_short_fix", 0.0, k_dna_short_fix, dim3(1), dim3(1024), 0, st, vals, rank, gs, ge, G, n);
 
     std::vector<uint32_t> lstart, lsize, loff;
+    ShardedList sl{};   // the first list is plain
     for (int64_t h = 16; G > 0; h *= 2) {
         if (h >= 2 * n) return false;   // cannot happen ('$' is unique); the general path if it does
         // the keys are dead: class lists (5 x (start, size), capacity G each) and
@@ -504,21 +654,29 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
         c.slot[S_IDX0].ensure((size_t)((2 * kClasses + 3) * G + 16) * 4);
         keys = c.slot[S_IDX0].as<uint32_t>();
         uint32_t *cs = keys, *cz = keys + kClasses * G;
-        HIPCHECK(hipMemsetAsync(counts, 0, 64, st));
-        KLAUNCH("dna_classify", 0.0, k_dna_classify, dim3(nblocks(G)), dim3(kB), 0, st, gs, ge, G, cs, cz, counts, G);
+        HIPCHECK(hipMemsetAsync(counts, 0, 128, st));
+        KLAUNCH("dna_classify", 0.0, k_dna_classify, dim3(nblocks(G, kB * kCI)), dim3(kB), 0, st, gs, ge, G, sl, cs, cz,
+                counts, G);
         uint32_t cnt[kClasses];
         HIPCHECK(hipMemcpyAsync(cnt, counts, sizeof cnt, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
+        if (FILE *tf = Ctx::ktrace_file())
+            std::fprintf(tf, "# round h=%lld G=%lld classes %u %u %u %u %u %u\n", (long long)h, (long long)G, cnt[0],
+                         cnt[1], cnt[2], cnt[3], cnt[4], cnt[5]);
         uint32_t *ncnt = counts + 8;
         // gather pass over every class, then the sorts (large groups gather
         // straight into their radix keys, before any head is rewritten)
-        ls_wave_pass<4, true>(c, "dna_ls_keys", cs, cz, cnt[0], vals, rank, kb, n, h, xs, xe, ncnt);
-        ls_wave_pass<16, true>(c, "dna_ls_keys", cs + G, cz + G, cnt[1], vals, rank, kb, n, h, xs, xe, ncnt);
-        ls_wave_pass<32, true>(c, "dna_ls_keys", cs + 2 * G, cz + 2 * G, cnt[2], vals, rank, kb, n, h, xs, xe, ncnt);
-        ls_wave_pass<64, true>(c, "dna_ls_keys", cs + 3 * G, cz + 3 * G, cnt[3], vals, rank, kb, n, h, xs, xe, ncnt);
+        ls_wave_pass<4, true>(c, "dna_ls_keys", cs, cz, cnt[0], vals, rank, kb, n, h, xs, xe, ncnt,
+                                    (uint32_t)lcap);
+        ls_wave_pass<16, true>(c, "dna_ls_keys", cs + G, cz + G, cnt[1], vals, rank, kb, n, h, xs, xe, ncnt,
+                                    (uint32_t)lcap);
+        ls_wave_pass<32, true>(c, "dna_ls_keys", cs + 2 * G, cz + 2 * G, cnt[2], vals, rank, kb, n, h, xs, xe, ncnt,
+                                    (uint32_t)lcap);
+        ls_wave_pass<64, true>(c, "dna_ls_keys", cs + 3 * G, cz + 3 * G, cnt[3], vals, rank, kb, n, h, xs, xe, ncnt,
+                                    (uint32_t)lcap);
         if (cnt[4])
             KLAUNCH("dna_ls_keys", 0.0, k_ls_block<true>, dim3(cnt[4]), dim3(kWB), 0, st, cs + 4 * G, cz + 4 * G, vals,
-                    rank, kb, n, h, xs, xe, ncnt);
+                    rank, kb, n, h, xs, xe, ncnt, (uint32_t)lcap);
         const int64_t L = cnt[5];
         int64_t M = 0;
         uint32_t *tab = keys + 2 * kClasses * G;
@@ -550,18 +708,30 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
             KLAUNCH("dna_refine_keys", 0.0, k_dna_refine_keys, grid2, dim3(kB), 0, st, tab, tab + L, tab + 2 * L, vals,
                     rank, n, h, rk, rv);
         }
-        ls_wave_pass<4, false>(c, "dna_ls_w4", cs, cz, cnt[0], vals, rank, kb, n, h, xs, xe, ncnt);
-        ls_wave_pass<16, false>(c, "dna_ls_w16", cs + G, cz + G, cnt[1], vals, rank, kb, n, h, xs, xe, ncnt);
-        ls_wave_pass<32, false>(c, "dna_ls_w32", cs + 2 * G, cz + 2 * G, cnt[2], vals, rank, kb, n, h, xs, xe, ncnt);
-        ls_wave_pass<64, false>(c, "dna_ls_w64", cs + 3 * G, cz + 3 * G, cnt[3], vals, rank, kb, n, h, xs, xe, ncnt);
+        ls_wave_pass<4, false>(c, "dna_ls_w4", cs, cz, cnt[0], vals, rank, kb, n, h, xs, xe, ncnt,
+                                    (uint32_t)lcap);
+        ls_wave_pass<16, false>(c, "dna_ls_w16", cs + G, cz + G, cnt[1], vals, rank, kb, n, h, xs, xe, ncnt,
+                                    (uint32_t)lcap);
+        ls_wave_pass<32, false>(c, "dna_ls_w32", cs + 2 * G, cz + 2 * G, cnt[2], vals, rank, kb, n, h, xs, xe, ncnt,
+                                    (uint32_t)lcap);
+        ls_wave_pass<64, false>(c, "dna_ls_w64", cs + 3 * G, cz + 3 * G, cnt[3], vals, rank, kb, n, h, xs, xe, ncnt,
+                                    (uint32_t)lcap);
         if (cnt[4])
             KLAUNCH("dna_ls_block", 0.0, k_ls_block<false>, dim3(cnt[4]), dim3(kWB), 0, st, cs + 4 * G, cz + 4 * G, vals,
-                    rank, kb, n, h, xs, xe, ncnt);
-        uint32_t nc = 0;
-        HIPCHECK(hipMemcpyAsync(&nc, ncnt, 4, hipMemcpyDeviceToHost, st));
+                    rank, kb, n, h, xs, xe, ncnt, (uint32_t)lcap);
+        uint32_t sc[9];   // shard counts, overflow
+        HIPCHECK(hipMemcpyAsync(sc, ncnt, sizeof sc, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
+        if (sc[8]) return false;
+        ShardedList nsl{};
+        for (int q = 0; q < 8; ++q) {
+            nsl.cnt[q] = sc[q];
+            if (sc[q]) nsl.S = std::max<uint32_t>(nsl.S, (((sc[q] - 1) / kCH) * 8 + (uint32_t)q + 1) * kCH);
+        }
+        const int64_t nc = nsl.S;
         int64_t next = nc;
         if (L) {   // large groups: one segmented radix pass
+            if (nc + M / 2 + 1 > lcap) return false;
             int qb = 1;
             while ((1ll << qb) < L) ++qb;
             radix_sort_pairs32(c, rk, rv, M, 0, ((30 + qb + 7) / 8) * 8);
@@ -579,6 +749,7 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
         std::swap(gs, xs);
         std::swap(ge, xe);
         G = next;
+        sl = nsl;
     }
     KLAUNCH("dna_final", 9.0 * (double)n, k_dna_final, dim3(nblocks(n)), dim3(kB), 0, st, vals, n, SA, BWT);
     HIPCHECK(hipGetLastError());

@@ -343,13 +343,17 @@ def test_index_repetitive_text(gpu_ctx):
     _check_index(b"CA" * 2000 + b"C" + b"$")
 
 
-@pytest.mark.parametrize("case", ["tiny", "edges", "groups", "long_lcp", "many_arrays", "homopolymer_peel"])
-def test_dna_suffix_sort_vs_oracle(gpu_ctx, case):
+@pytest.mark.parametrize("case", ["tiny", "edges", "groups", "long_lcp", "many_arrays", "homopolymer_peel",
+                                  "arrays_300k", "arrays_300k_small_lists"])
+def test_dna_suffix_sort_vs_oracle(gpu_ctx, monkeypatch, case):
     """The ACGT* '$' string sort (sa_dna.hip) against the oracle's prefix
     doubling: texts built to hit every group class -- pairs (thread sort),
     tens to a thousand members (workgroup bitonic sort), many short arrays
     sharing a 16-mer (radix refinement rounds), long common prefixes, and
-    suffixes running into the end inside a tied key."""
+    suffixes running into the end inside a tied key.  The 300 kbp texts take
+    the partitioned first-rank writes (>= 2^16 bases) and fill every shard of
+    the next-round lists past one chunk; with the lists capped
+    (BWTMI_LS_CAP) the sort gives up and the general doubling must agree."""
     r = np.random.default_rng(sum(map(ord, case)))
     B = np.frombuffer(b"ACGT", dtype=np.uint8)
 
@@ -375,6 +379,15 @@ def test_dna_suffix_sort_vs_oracle(gpu_ctx, case):
             parts.append(rnd(int(r.integers(5, 40))))
             parts.append([b"AC", b"G", b"CAG", b"TTA"][int(r.integers(0, 4))] * int(r.integers(6, 30)))
         t = b"".join(parts)
+    elif case.startswith("arrays_300k"):
+        parts = []
+        for _ in range(12000):
+            parts.append(rnd(int(r.integers(3, 20))))
+            parts.append([b"AC", b"G", b"CAG", b"TTA", b"GATC"][int(r.integers(0, 5))] * int(r.integers(3, 12)))
+        t = b"".join(parts)
+        assert len(t) > 1 << 16
+        if case.endswith("small_lists"):
+            monkeypatch.setenv("BWTMI_LS_CAP", "3000")
     else:   # one base repeated: a large group that loses 16 suffixes per round
         t = rnd(300) + b"G" * 2500 + rnd(300)
     _check_index(t + b"$")
