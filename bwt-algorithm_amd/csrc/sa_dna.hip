@@ -11,19 +11,23 @@
 //   2. one LSD radix sort of (first 16 bases: 32-bit key, value) -- 4 passes
 //      of 8 B keys+values instead of 8+ passes of 12 B; the value carries the
 //      suffix start and the code of the base before it (BWT symbol);
-//   3. runs of equal keys (groups) are finished by prefix doubling over a rank
-//      array (Larsson-Sadakane): rank[i] = SA index of the head of i's group;
-//      a round with h sorts every group by rank[i + h] -- the groups are then
+//   3. runs of equal keys (groups): one tiled pass finds them (gs / ge in SA
+//      order) and every suffix's run head; the first ranks go out through a
+//      position partition so the scattered stores stay L2-local;
+//   4. groups are finished by prefix doubling over a rank array
+//      (Larsson-Sadakane): rank[i] = SA index of the head of i's group; a
+//      round with h sorts every group by rank[i + h] -- the groups are then
 //      2h-sorted -- and writes the new heads.  Only group members take part,
 //      and each group is sorted where it fits:
-//        <= 64 members     one wave (4, 16 or 64 lanes per group), bitonic
+//        <= 64 members     one wave (4, 16, 32 or 64 lanes per group), bitonic
 //                          over lane shuffles
 //        <= kMedium        one workgroup, bitonic in LDS
 //        larger            one segmented radix pass over all such groups
-//      Each round gathers every member's key first (one pass over all groups)
-//      and only then sorts and rewrites heads: a mix of old and new heads
-//      would split suffixes that are still tied.
-//   4. one streaming pass writes SA and BWT.
+//      The sorts read rank[a + h] as the round found it and push their rank
+//      changes to a list that is stored after all of them: a mix of old and
+//      new heads would order suffixes wrongly.  The next round's groups and
+//      the changes are appended through 8 counters (sharded chunks).
+//   5. one streaming pass writes SA and BWT.
 // The end of the text: keys pad past the end with A, so the (at most 16)
 // suffixes with fewer than 16 bases before '$' tie with suffixes that really
 // continue with A.  One small fix-up moves each of them to the front of its
@@ -46,6 +50,8 @@ constexpr int kMedium = 1024;                   // largest group sorted by one w
 constexpr uint32_t kPosMask = (1u << 29) - 1;   // value: start (29 bits) | BWT code << 29
 
 inline unsigned nblocks(int64_t n, int b = kB) { return (unsigned)((n + b - 1) / b); }
+
+__device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
 __device__ __forceinline__ uint32_t code2(uint8_t c) { return (uint32_t)(((c >> 2) ^ (c >> 1)) & 3u); }   // A0 C1 G2 T3
 
@@ -97,17 +103,6 @@ __global__ __launch_bounds__(kB) void k_dna_keys(const uint64_t *__restrict__ P,
 }
 
 // flags of the multi-member groups (runs of equal keys): S = first member, E = last member
-__global__ __launch_bounds__(kB) void k_dna_flags(const uint32_t *__restrict__ keys, int64_t n,
-                                                  uint32_t *__restrict__ fs, uint32_t *__restrict__ fe) {
-    const int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x;
-    if (r >= n) return;
-    const uint32_t k = keys[r];
-    const bool head = r == 0 || keys[r - 1] != k;
-    const bool tail = r + 1 == n || keys[r + 1] != k;
-    fs[r] = head && !tail;
-    fe[r] = tail && !head;
-}
-
 __global__ __launch_bounds__(kB) void k_dna_compact2(const uint32_t *__restrict__ fs, const uint32_t *__restrict__ ps,
                                                      const uint32_t *__restrict__ fe, const uint32_t *__restrict__ pe,
                                                      int64_t n, uint32_t *__restrict__ gs, uint32_t *__restrict__ ge) {
@@ -117,30 +112,169 @@ __global__ __launch_bounds__(kB) void k_dna_compact2(const uint32_t *__restrict_
     if (fe[r]) ge[pe[r]] = (uint32_t)r + 1;   // exclusive end
 }
 
-// rank[i] = SA index of the head of i's 16-base group, or i's own index when
-// alone.  ps / pe: exclusive counts of group starts / ends (index r is inside
-// a group when more groups started up to r than ended before it)
-__global__ __launch_bounds__(kB) void k_dna_rank0(const uint32_t *__restrict__ vals, const uint32_t *__restrict__ ps,
-                                                  const uint32_t *__restrict__ pe, const uint32_t *__restrict__ gs,
-                                                  int64_t n, uint32_t *__restrict__ rank) {
-    const int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x;
-    if (r >= n) return;
-    const uint32_t started = ps[r + 1];
-    rank[vals[r] & kPosMask] = started > pe[r] ? gs[started - 1] : (uint32_t)r;
+// Groups of equal 16-base keys, three launches over the sorted keys instead of
+// flags + two scans + compaction + heads (five passes over n):
+//   count : per 4096-key tile, the group starts and ends (runs of >= 2 equal
+//           keys) and the last run start
+//   scan  : one workgroup, exclusive sums / max over the tiles
+//   apply : the tile again: gs / ge in SA order (ballot prefix counts), and
+//           hd[r] = the SA index where r's run starts (r itself when alone)
+constexpr int kGRows = 16;                 // 256-key rows per tile
+constexpr int kGTile = kGRows * kB;        // 4096
+struct RunFlags {
+    bool run, gstart, gend;   // r starts a run; starts / ends a group of >= 2
+};
+// one coalesced load per key: the neighbours come from the adjacent lanes
+// (lanes 0 and 63 load theirs); every lane of the wave must call it
+__device__ __forceinline__ RunFlags run_flags(const uint32_t *__restrict__ keys, int64_t r, int64_t n) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t k = r < n ? keys[r] : 0u;
+    uint32_t kp = __shfl_up(k, 1, 64), kn = __shfl_down(k, 1, 64);
+    if (lane == 0 && r > 0 && r < n) kp = keys[r - 1];
+    if (lane == 63 && r + 1 < n) kn = keys[r + 1];
+    RunFlags f{false, false, false};
+    if (r >= n) return f;
+    const bool head = r == 0 || kp != k;
+    const bool tail = r + 1 == n || kn != k;
+    f.run = head;
+    f.gstart = head && !tail;
+    f.gend = tail && !head;
+    return f;
 }
 
-// the same ranks in two steps: the heads in SA order (coalesced), then -- after
-// a pass that orders the (position, head) pairs by the position's top 8 bits --
-// the writes, each workgroup's confined to one 2^shift-position window that
-// its XCD's L2 holds, so the scattered 4-byte stores reach HBM as whole lines
-__global__ __launch_bounds__(kB) void k_dna_heads(const uint32_t *__restrict__ ps, const uint32_t *__restrict__ pe,
-                                                  const uint32_t *__restrict__ gs, int64_t n, uint32_t *__restrict__ hd) {
-    const int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x;
-    if (r >= n) return;
-    const uint32_t started = ps[r + 1];
-    hd[r] = started > pe[r] ? gs[started - 1] : (uint32_t)r;
+__global__ __launch_bounds__(kB) void k_grp_count(const uint32_t *__restrict__ keys, int64_t n,
+                                                  uint32_t *__restrict__ tcnt) {
+    __shared__ uint32_t ws[kB / 64], we[kB / 64], wl[kB / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t base = (int64_t)blockIdx.x * kGTile;
+    uint32_t cs = 0, ce = 0, last = 0;
+    for (int i = 0; i < kGRows; ++i) {
+        const int64_t r = base + (int64_t)i * kB + threadIdx.x;
+        const RunFlags f = run_flags(keys, r, n);
+        const uint64_t mr = __ballot(f.run);
+        cs += (uint32_t)__popcll(__ballot(f.gstart));
+        ce += (uint32_t)__popcll(__ballot(f.gend));
+        if (mr) last = (uint32_t)(r - lane) + 63u - (uint32_t)__clzll((long long)mr);
+    }
+    if (lane == 0) {
+        ws[wv] = cs;
+        we[wv] = ce;
+        wl[wv] = last;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t a = 0, b = 0, l = 0;
+        for (int w = 0; w < kB / 64; ++w) {
+            a += ws[w];
+            b += we[w];
+            l = max(l, wl[w]);
+        }
+        const int64_t nt = (n + kGTile - 1) / kGTile;
+        tcnt[blockIdx.x] = a;
+        tcnt[nt + blockIdx.x] = b;
+        tcnt[2 * nt + blockIdx.x] = l;
+    }
 }
 
+// in place: exclusive sums of the start / end counts, exclusive max of the
+// last run starts; the total start count (G) at tcnt[3 * nt].  One workgroup,
+// 1024 tiles per step (coalesced), a block scan per step.
+__global__ __launch_bounds__(1024) void k_grp_scan(uint32_t *__restrict__ tcnt, int64_t nt) {
+    __shared__ uint32_t wa[16], wb[16], wl[16];
+    __shared__ uint32_t carry[3];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t < 3) carry[t] = 0;
+    __syncthreads();
+    for (int64_t x0 = 0; x0 < nt; x0 += 1024) {
+        const int64_t x = x0 + t;
+        const uint32_t a = x < nt ? tcnt[x] : 0u, b = x < nt ? tcnt[nt + x] : 0u, l = x < nt ? tcnt[2 * nt + x] : 0u;
+        uint32_t ia = a, ib = b, il = l;   // inclusive wave scans
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t pa = __shfl_up(ia, o, 64), pb = __shfl_up(ib, o, 64), pl = __shfl_up(il, o, 64);
+            if (lane >= o) {
+                ia += pa;
+                ib += pb;
+                il = max(il, pl);
+            }
+        }
+        if (lane == 63) {
+            wa[wv] = ia;
+            wb[wv] = ib;
+            wl[wv] = il;
+        }
+        __syncthreads();
+        uint32_t ea = carry[0], eb = carry[1], el = carry[2];
+        for (int w = 0; w < wv; ++w) {
+            ea += wa[w];
+            eb += wb[w];
+            el = max(el, wl[w]);
+        }
+        const uint32_t pl = __shfl_up(il, 1, 64);   // exclusive max: the previous lane's inclusive one
+        if (x < nt) {
+            tcnt[x] = ea + ia - a;
+            tcnt[nt + x] = eb + ib - b;
+            tcnt[2 * nt + x] = lane ? max(el, pl) : el;
+        }
+        __syncthreads();
+        if (t == 1023) {
+            carry[0] = ea + ia;
+            carry[1] = eb + ib;
+            carry[2] = max(el, il);
+        }
+        __syncthreads();
+    }
+    if (t == 0) tcnt[3 * nt] = carry[0];
+}
+
+__global__ __launch_bounds__(kB) void k_grp_apply(const uint32_t *__restrict__ keys, int64_t n,
+                                                  const uint32_t *__restrict__ tcnt, uint32_t *__restrict__ gs,
+                                                  uint32_t *__restrict__ ge, uint32_t *__restrict__ hd) {
+    __shared__ uint32_t ws[kB / 64], we[kB / 64], wl[kB / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t nt = (n + kGTile - 1) / kGTile;
+    const int64_t base = (int64_t)blockIdx.x * kGTile;
+    uint32_t cs = tcnt[blockIdx.x], ce = tcnt[nt + blockIdx.x], cl = tcnt[2 * nt + blockIdx.x];   // carries
+    const uint64_t below = lanes_below(lane);
+    for (int i = 0; i < kGRows; ++i) {
+        const int64_t r = base + (int64_t)i * kB + threadIdx.x;
+        const RunFlags f = run_flags(keys, r, n);
+        const uint64_t ms = __ballot(f.gstart), me = __ballot(f.gend), mr = __ballot(f.run);
+        const uint32_t wbase = (uint32_t)(r - lane);
+        if (lane == 0) {
+            ws[wv] = (uint32_t)__popcll(ms);
+            we[wv] = (uint32_t)__popcll(me);
+            wl[wv] = mr ? wbase + 63u - (uint32_t)__clzll((long long)mr) : 0u;
+        }
+        __syncthreads();
+        uint32_t ps = cs, pe = ce, pl = cl;
+        for (int w = 0; w < wv; ++w) {
+            ps += ws[w];
+            pe += we[w];
+            pl = max(pl, wl[w]);
+        }
+        if (r < n) {
+            if (f.gstart) gs[ps + (uint32_t)__popcll(ms & below)] = (uint32_t)r;
+            if (f.gend) ge[pe + (uint32_t)__popcll(me & below)] = (uint32_t)r + 1;   // exclusive end
+            const uint64_t mine = mr & (below | (1ull << lane));
+            hd[r] = mine ? wbase + 63u - (uint32_t)__clzll((long long)mine) : pl;
+        }
+        for (int w = wv; w < kB / 64; ++w) {   // carries into the next row (every thread, same values)
+            ps += ws[w];
+            pe += we[w];
+            pl = max(pl, wl[w]);
+        }
+        cs = ps;
+        ce = pe;
+        cl = pl;
+        __syncthreads();   // ws / we / wl are rewritten by the next row
+    }
+}
+
+// rank[pos] = head, from (position | code, head) pairs: after a pass that
+// orders the pairs by the position's top 8 bits, each workgroup's writes stay
+// in one 2^shift-position window that its XCD's L2 holds, so the scattered
+// 4-byte stores reach HBM as whole lines
 constexpr int kPutItems = 16;
 __global__ __launch_bounds__(kB) void k_dna_rank_put(const uint32_t *__restrict__ pv, const uint32_t *__restrict__ hd,
                                                      int64_t n, int64_t ntiles, uint32_t *__restrict__ rank) {
@@ -223,7 +357,6 @@ __device__ __forceinline__ int size_class(uint32_t sz) {
     return sz <= 4 ? 0 : sz <= 16 ? 1 : sz <= 32 ? 2 : sz <= 64 ? 3 : sz <= (uint32_t)kMedium ? 4 : 5;
 }
 
-__device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
 // append (start, end) to a list, one atomic per workgroup of NT threads (a
 // single counter hit once per wave by ~10^6 waves serialises in L2); every
@@ -306,6 +439,55 @@ __device__ __forceinline__ void block_append_sharded(bool on, uint32_t st, uint3
     __syncthreads();   // wc is reused by the next call
 }
 
+// a round's rank changes, (position << 32 | new head), pushed like the group
+// lists (sharded chunks, holes skipped by the reader) and stored after every
+// sort of the round has read its keys: the sorts gather rank[a + h] from the
+// state at the start of the round
+template <int NT>
+__device__ __forceinline__ void block_push_sharded(bool on, uint64_t item, uint64_t *__restrict__ ls,
+                                                   uint32_t *__restrict__ cnt8, uint32_t cap,
+                                                   uint32_t *__restrict__ ovf) {
+    __shared__ uint32_t wc[NT / 64 + 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t q = blockIdx.x & 7u;
+    const uint64_t m = __ballot(on);
+    if (lane == 0) wc[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < NT / 64; ++w) {
+            const uint32_t x = wc[w];
+            wc[w] = tot;
+            tot += x;
+        }
+        wc[NT / 64] = tot ? atomicAdd(&cnt8[q], tot) : 0u;
+    }
+    __syncthreads();
+    if (on) {
+        const uint32_t at = shard_slot(wc[NT / 64] + wc[wv] + (uint32_t)__popcll(m & lanes_below(lane)), q);
+        if (at < cap) ls[at] = item;
+        else atomicOr(ovf, 1u);
+    }
+    __syncthreads();
+}
+
+// where a round's sorts write: the next round's groups and the rank changes
+struct LsOut {
+    uint32_t *ngs, *nge, *ncnt;   // ncnt[0..7] shard counts, ncnt[8] overflow
+    uint32_t cap;
+    uint64_t *chg;
+    uint32_t *ccnt;               // ccnt[0..7], ccnt[8] overflow
+    uint32_t ccap;
+};
+
+__global__ __launch_bounds__(kB) void k_ls_apply(const uint64_t *__restrict__ chg, int64_t S, ShardedList sl,
+                                                 uint32_t *__restrict__ rank) {
+    const int64_t j = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (j >= S || !sl.live((uint32_t)j)) return;
+    const uint64_t e = chg[j];
+    rank[e >> 32] = (uint32_t)e;
+}
+
 // the round's groups into the size-class lists: kCI groups per thread, slots
 // inside the workgroup from wave ballots + LDS counters, then one atomic per
 // class and workgroup
@@ -365,11 +547,10 @@ __device__ __forceinline__ uint32_t ls_key(const uint32_t *__restrict__ rank, ui
 // still-tied runs appended to the next round's list
 // (KEYS: the gather pass -- kb[i] = key of the member at vals[i])
 constexpr int kLB = 1024;   // threads per workgroup of the wave-sort passes
-template <int W, bool KEYS>
+template <int W>
 __global__ __launch_bounds__(kLB) void k_ls_wave(const uint32_t *__restrict__ starts, const uint32_t *__restrict__ sizes,
-                                                int64_t cnt, uint32_t *__restrict__ vals, uint32_t *__restrict__ rank,
-                                                uint32_t *__restrict__ kb, int64_t n, int64_t h, uint32_t *__restrict__ ngs,
-                                                uint32_t *__restrict__ nge, uint32_t *__restrict__ ncnt, uint32_t cap) {
+                                                int64_t cnt, uint32_t *__restrict__ vals,
+                                                const uint32_t *__restrict__ rank, int64_t n, int64_t h, LsOut o) {
     const int lane = threadIdx.x & 63, kk = lane & (W - 1);
     const int64_t g = (((int64_t)blockIdx.x * kLB + threadIdx.x) >> 6) * (64 / W) + lane / W;
     uint32_t s = 0, sz = 0;
@@ -378,12 +559,8 @@ __global__ __launch_bounds__(kLB) void k_ls_wave(const uint32_t *__restrict__ st
         sz = sizes[g];
     }
     const bool live = kk < (int)sz;
-    if (KEYS) {
-        if (live) kb[s + kk] = ls_key(rank, vals[s + kk], n, h);
-        return;
-    }
     const uint32_t orig = live ? vals[s + kk] : 0u;
-    uint64_t x = live ? ((uint64_t)kb[s + kk] << 32) | orig : ~0ull;
+    uint64_t x = live ? ((uint64_t)ls_key(rank, orig, n, h) << 32) | orig : ~0ull;
 #pragma unroll
     for (int k2 = 2; k2 <= W; k2 <<= 1)
 #pragma unroll
@@ -398,38 +575,32 @@ __global__ __launch_bounds__(kLB) void k_ls_wave(const uint32_t *__restrict__ st
     const bool tail = live && (kk == (int)sz - 1 || kn != key);
     const uint64_t S = __ballot(start), T = __ballot(tail);
     const int seg = lane - kk;
+    // every member's rank is s when the round starts: only the members of the
+    // later subgroups change rank, and only moved values are stored
     if (live) {
-        // every member's rank is s when the round starts: only the members of
-        // the later subgroups move, and only moved values are stored
-        const int hl = 63 - __clzll((long long)(S & (lanes_below(lane) | (1ull << lane))));
         if (v != orig) vals[s + kk] = v;
-        if (hl != seg) rank[v & kPosMask] = s + (uint32_t)(hl - seg);
     }
+    const int hl = live ? 63 - __clzll((long long)(S & (lanes_below(lane) | (1ull << lane)))) : seg;
+    block_push_sharded<kLB>(hl != seg, ((uint64_t)(v & kPosMask) << 32) | (s + (uint32_t)(hl - seg)), o.chg, o.ccnt,
+                            o.ccap, o.ccnt + 8);
     const bool multi = start && !tail;
     const int el = multi ? __ffsll((unsigned long long)(T & (~0ull << lane))) - 1 : 0;
-    block_append_sharded<kLB>(multi, s + kk, s + (uint32_t)(el - seg) + 1, ngs, nge, ncnt, cap, ncnt + 8);
+    block_append_sharded<kLB>(multi, s + kk, s + (uint32_t)(el - seg) + 1, o.ngs, o.nge, o.ncnt, o.cap, o.ncnt + 8);
 }
 
 // one doubling pass over a group of <= kMedium members in one workgroup
 constexpr int kWB = 1024;
-template <bool KEYS>
 __global__ __launch_bounds__(kWB) void k_ls_block(const uint32_t *__restrict__ starts, const uint32_t *__restrict__ sizes,
-                                                  uint32_t *__restrict__ vals, uint32_t *__restrict__ rank,
-                                                  uint32_t *__restrict__ kb, int64_t n, int64_t h,
-                                                  uint32_t *__restrict__ ngs, uint32_t *__restrict__ nge,
-                                                  uint32_t *__restrict__ ncnt, uint32_t cap) {
+                                                  uint32_t *__restrict__ vals, const uint32_t *__restrict__ rank,
+                                                  int64_t n, int64_t h, LsOut o) {
     __shared__ uint64_t x[kMedium];
     __shared__ int wl[kWB / 64], wf[kWB / 64];
     const uint32_t s = starts[blockIdx.x], sz = sizes[blockIdx.x];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     uint32_t p2 = 1;
     while (p2 < sz) p2 <<= 1;
-    if (KEYS) {
-        if (t < (int)sz) kb[s + t] = ls_key(rank, vals[s + t], n, h);
-        return;
-    }
     const uint32_t orig = t < (int)sz ? vals[s + t] : 0u;
-    if (t < (int)p2) x[t] = t < (int)sz ? ((uint64_t)kb[s + t] << 32) | orig : ~0ull;
+    if (t < (int)p2) x[t] = t < (int)sz ? ((uint64_t)ls_key(rank, orig, n, h) << 32) | orig : ~0ull;
     __syncthreads();
     for (uint32_t k2 = 2; k2 <= p2; k2 <<= 1)
         for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
@@ -459,11 +630,10 @@ __global__ __launch_bounds__(kWB) void k_ls_block(const uint32_t *__restrict__ s
     if (Sb) head = wv * 64 + 63 - __clzll((long long)Sb);
     else
         for (int w = 0; w < wv; ++w) head = max(head, wl[w]);
-    if (live) {   // as in k_ls_wave: only moved values and later subgroups are stored
-        const uint32_t v = (uint32_t)me;
-        if (v != orig) vals[s + t] = v;
-        if (head) rank[v & kPosMask] = s + (uint32_t)head;
-    }
+    const uint32_t v = (uint32_t)me;   // as in k_ls_wave: moved values, changed ranks
+    if (live && v != orig) vals[s + t] = v;
+    block_push_sharded<kWB>(live && head != 0, ((uint64_t)(v & kPosMask) << 32) | (s + (uint32_t)head), o.chg,
+                            o.ccnt, o.ccap, o.ccnt + 8);
     const bool multi = start && !tail;
     int end = 1 << 30;
     if (multi) {
@@ -472,18 +642,16 @@ __global__ __launch_bounds__(kWB) void k_ls_block(const uint32_t *__restrict__ s
         else
             for (int w = wv + 1; w < kWB / 64; ++w) end = min(end, wf[w]);
     }
-    block_append_sharded<kWB>(multi, s + (uint32_t)t, s + (uint32_t)end + 1, ngs, nge, ncnt, cap, ncnt + 8);
+    block_append_sharded<kWB>(multi, s + (uint32_t)t, s + (uint32_t)end + 1, o.ngs, o.nge, o.ncnt, o.cap, o.ncnt + 8);
 }
 
-// one wave-class pass (KEYS: the gather) over the cnt groups of a class list
-template <int W, bool KEYS>
+// one wave-class pass over the cnt groups of a class list
+template <int W>
 void ls_wave_pass(Ctx &c, const char *name, const uint32_t *cs, const uint32_t *cz, uint32_t cnt, uint32_t *vals,
-                  uint32_t *rank, uint32_t *kb, int64_t n, int64_t h, uint32_t *xs, uint32_t *xe, uint32_t *ncnt,
-                  uint32_t cap) {
+                  const uint32_t *rank, int64_t n, int64_t h, const LsOut &o) {
     if (!cnt) return;
     const unsigned grid = (unsigned)((cnt + (kLB / 64) * (64 / W) - 1) / ((kLB / 64) * (64 / W)));
-    KLAUNCH(name, 0.0, (k_ls_wave<W, KEYS>), dim3(grid), dim3(kLB), 0, c.stream, cs, cz, (int64_t)cnt, vals, rank, kb,
-            n, h, xs, xe, ncnt, cap);
+    KLAUNCH(name, 0.0, (k_ls_wave<W>), dim3(grid), dim3(kLB), 0, c.stream, cs, cz, (int64_t)cnt, vals, rank, n, h, o);
 }
 
 // groups larger than kMedium: (group index << 30 | rank[a+h]) keys gathered
@@ -576,10 +744,10 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
     c.slot[S_IDX1].ensure((size_t)n * 4 + 64);      // values
     c.slot[S_IDX2].ensure((size_t)nw * 8 + 64);     // packed text
     c.slot[S_IDX3].ensure((size_t)(n + 1) * 4);     // group-start flags
-    c.slot[S_IDX4].ensure((size_t)(n + 1) * 4);     // their positions
+    c.slot[S_IDX4].ensure((size_t)(n + 1) * 4 + 256);   // their positions (first: the group tiles' counts)
     c.slot[S_IDX5].ensure((size_t)(n + 1) * 4);     // group-end flags
     c.slot[S_IDX6].ensure((size_t)(n + 1) * 4);     // their positions
-    c.slot[S_MISC3].ensure(128);   // 6 class counts | 8 shard counts, overflow flag
+    c.slot[S_MISC3].ensure(256);   // 6 class counts | 8 + 1 group-list counters | 8 + 1 change counters
     uint32_t *keys = c.slot[S_IDX0].as<uint32_t>();
     uint32_t *vals = c.slot[S_IDX1].as<uint32_t>();
     uint64_t *P = c.slot[S_IDX2].as<uint64_t>();
@@ -604,7 +772,6 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
         HIPCHECK(hipStreamSynchronize(st));
         return (int64_t)G;
     };
-    KLAUNCH("dna_flags", 8.0 * (double)n, k_dna_flags, dim3(nblocks(n)), dim3(kB), 0, st, keys, n, fs, fe);
     // group lists: current round and next round, (start, exclusive end) in vals
     // (<= n/2 groups; the sharded appends leave holes: slack for them and for
     // uneven shards -- a list that would outgrow it takes the general path)
@@ -613,26 +780,45 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
     int64_t lcap = lalloc;
     if (const char *e = std::getenv("BWTMI_LS_CAP")) lcap = std::min<int64_t>(lcap, std::atoll(e));   // test hook
     c.slot[S_IDX8].ensure((size_t)n * 4 + 64);
-    c.slot[S_IDX11].ensure((size_t)n * 4 + 64);
-    uint32_t *kb = c.slot[S_IDX11].as<uint32_t>();   // a round's keys, aligned with vals
+    // a round's rank changes (<= its members; holes and uneven shards as above)
+    const int64_t calloc_ = n + n / 4 + 16 * (int64_t)kCH + 64;
+    c.slot[S_IDX11].ensure((size_t)calloc_ * 8);
+    int64_t ccap = calloc_;
+    if (const char *e = std::getenv("BWTMI_LS_CAP")) ccap = std::min<int64_t>(ccap, 2 * std::atoll(e));
+    uint64_t *chg = c.slot[S_IDX11].as<uint64_t>();
     uint32_t *gs = c.slot[S_MISC0].as<uint32_t>(), *ge = c.slot[S_MISC1].as<uint32_t>();
     uint32_t *xs = c.slot[S_IDX9].as<uint32_t>(), *xe = c.slot[S_IDX10].as<uint32_t>();
     uint32_t *rank = c.slot[S_IDX8].as<uint32_t>();
-    int64_t G = groups(fs, ps, fe, pe, n, gs, ge);
+    // the 16-base groups: gs / ge in SA order and every suffix's run head (in
+    // the flag buffer, dead until the large-group rounds)
+    uint32_t *hd = fs;
+    int64_t G = 0;
+    {
+        const int64_t nt = (n + kGTile - 1) / kGTile;
+        uint32_t *tcnt = ps;   // 3 nt + 1 words
+        KLAUNCH("dna_grp_count", 4.0 * (double)n, k_grp_count, dim3((unsigned)nt), dim3(kB), 0, st, keys, n, tcnt);
+        KLAUNCH("dna_grp_scan", 0.0, k_grp_scan, dim3(1), dim3(1024), 0, st, tcnt, nt);
+        KLAUNCH("dna_grp_apply", 8.0 * (double)n, k_grp_apply, dim3((unsigned)nt), dim3(kB), 0, st, keys, n, tcnt, gs,
+                ge, hd);
+        uint32_t g32 = 0;
+        HIPCHECK(hipMemcpyAsync(&g32, tcnt + 3 * nt, 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        G = g32;
+    }
+    // rank[pos] = head
+    const int64_t nput = (n + kB * kPutItems - 1) / (kB * kPutItems);
     static const int rank0_direct = [] { const char *e = std::getenv("BWTMI_RANK0_DIRECT"); return e && *e == '1'; }();
     if (rank0_direct || n < (1 << 16)) {
-        KLAUNCH("dna_rank0", 12.0 * (double)n, k_dna_rank0, dim3(nblocks(n)), dim3(kB), 0, st, vals, ps, pe, gs, n,
-                rank);
+        KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put, dim3((unsigned)nput), dim3(kB), 0, st, vals, hd, n,
+                nput, rank);
     } else {
-        // keys are dead: heads there; the pass output in the sort's buffers
+        // through a position partition (the pass output in the sort's buffers)
         int bits = 0;
         while ((int64_t{1} << bits) < n) ++bits;
         c.slot[S_SORT_TMP0].ensure((size_t)n * 4);
         c.slot[S_SORT_TMP1].ensure((size_t)n * 4);
         uint32_t *pv = c.slot[S_SORT_TMP0].as<uint32_t>(), *ph = c.slot[S_SORT_TMP1].as<uint32_t>();
-        KLAUNCH("dna_heads", 12.0 * (double)n, k_dna_heads, dim3(nblocks(n)), dim3(kB), 0, st, ps, pe, gs, n, keys);
-        radix_pass_k32(c, vals, keys, pv, ph, n, bits - 8);
-        const int64_t nt = (n + kB * kPutItems - 1) / (kB * kPutItems);
+        radix_pass_k32(c, vals, hd, pv, ph, n, bits - 8);
         // (unused) LDS caps the workgroups per CU, and so the span of positions
         // an XCD writes at once: at 1 workgroup per CU an XCD's 32 x 4096
         // pairs stay within about a quarter of a 2^shift window (2 MB at
@@ -640,8 +826,8 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
         // 1.13-1.36 ms at full occupancy, 0.63 at 2 per CU, 0.55 at 1 per CU
         // (the direct scatter: 2.35)
         static const int put_lds = [] { const char *e = std::getenv("BWTMI_PUT_LDS"); return e ? std::atoi(e) : 128; }();
-        KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put, dim3((unsigned)nt), dim3(kB), (size_t)put_lds * 1024,
-                st, pv, ph, n, nt, rank);
+        KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put, dim3((unsigned)nput), dim3(kB),
+                (size_t)put_lds * 1024, st, pv, ph, n, nput, rank);
     }
     if (G) KLAUNCH("dna_short_fix", 0.0, k_dna_short_fix, dim3(1), dim3(1024), 0, st, vals, rank, gs, ge, G, n);
 
@@ -654,7 +840,7 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
         c.slot[S_IDX0].ensure((size_t)((2 * kClasses + 3) * G + 16) * 4);
         keys = c.slot[S_IDX0].as<uint32_t>();
         uint32_t *cs = keys, *cz = keys + kClasses * G;
-        HIPCHECK(hipMemsetAsync(counts, 0, 128, st));
+        HIPCHECK(hipMemsetAsync(counts, 0, 256, st));
         KLAUNCH("dna_classify", 0.0, k_dna_classify, dim3(nblocks(G, kB * kCI)), dim3(kB), 0, st, gs, ge, G, sl, cs, cz,
                 counts, G);
         uint32_t cnt[kClasses];
@@ -663,20 +849,8 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
         if (FILE *tf = Ctx::ktrace_file())
             std::fprintf(tf, "# round h=%lld G=%lld classes %u %u %u %u %u %u\n", (long long)h, (long long)G, cnt[0],
                          cnt[1], cnt[2], cnt[3], cnt[4], cnt[5]);
-        uint32_t *ncnt = counts + 8;
-        // gather pass over every class, then the sorts (large groups gather
-        // straight into their radix keys, before any head is rewritten)
-        ls_wave_pass<4, true>(c, "dna_ls_keys", cs, cz, cnt[0], vals, rank, kb, n, h, xs, xe, ncnt,
-                                    (uint32_t)lcap);
-        ls_wave_pass<16, true>(c, "dna_ls_keys", cs + G, cz + G, cnt[1], vals, rank, kb, n, h, xs, xe, ncnt,
-                                    (uint32_t)lcap);
-        ls_wave_pass<32, true>(c, "dna_ls_keys", cs + 2 * G, cz + 2 * G, cnt[2], vals, rank, kb, n, h, xs, xe, ncnt,
-                                    (uint32_t)lcap);
-        ls_wave_pass<64, true>(c, "dna_ls_keys", cs + 3 * G, cz + 3 * G, cnt[3], vals, rank, kb, n, h, xs, xe, ncnt,
-                                    (uint32_t)lcap);
-        if (cnt[4])
-            KLAUNCH("dna_ls_keys", 0.0, k_ls_block<true>, dim3(cnt[4]), dim3(kWB), 0, st, cs + 4 * G, cz + 4 * G, vals,
-                    rank, kb, n, h, xs, xe, ncnt, (uint32_t)lcap);
+        uint32_t *ncnt = counts + 8;   // [0, 8) shards, [8] overflow; the changes' at +16
+        const LsOut o{xs, xe, ncnt, (uint32_t)lcap, chg, counts + 24, (uint32_t)ccap};
         const int64_t L = cnt[5];
         int64_t M = 0;
         uint32_t *tab = keys + 2 * kClasses * G;
@@ -708,20 +882,27 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
             KLAUNCH("dna_refine_keys", 0.0, k_dna_refine_keys, grid2, dim3(kB), 0, st, tab, tab + L, tab + 2 * L, vals,
                     rank, n, h, rk, rv);
         }
-        ls_wave_pass<4, false>(c, "dna_ls_w4", cs, cz, cnt[0], vals, rank, kb, n, h, xs, xe, ncnt,
-                                    (uint32_t)lcap);
-        ls_wave_pass<16, false>(c, "dna_ls_w16", cs + G, cz + G, cnt[1], vals, rank, kb, n, h, xs, xe, ncnt,
-                                    (uint32_t)lcap);
-        ls_wave_pass<32, false>(c, "dna_ls_w32", cs + 2 * G, cz + 2 * G, cnt[2], vals, rank, kb, n, h, xs, xe, ncnt,
-                                    (uint32_t)lcap);
-        ls_wave_pass<64, false>(c, "dna_ls_w64", cs + 3 * G, cz + 3 * G, cnt[3], vals, rank, kb, n, h, xs, xe, ncnt,
-                                    (uint32_t)lcap);
+        // the sorts read rank[a + h] as the round found it (the large groups'
+        // keys are gathered above); their rank changes are stored after them
+        ls_wave_pass<4>(c, "dna_ls_w4", cs, cz, cnt[0], vals, rank, n, h, o);
+        ls_wave_pass<16>(c, "dna_ls_w16", cs + G, cz + G, cnt[1], vals, rank, n, h, o);
+        ls_wave_pass<32>(c, "dna_ls_w32", cs + 2 * G, cz + 2 * G, cnt[2], vals, rank, n, h, o);
+        ls_wave_pass<64>(c, "dna_ls_w64", cs + 3 * G, cz + 3 * G, cnt[3], vals, rank, n, h, o);
         if (cnt[4])
-            KLAUNCH("dna_ls_block", 0.0, k_ls_block<false>, dim3(cnt[4]), dim3(kWB), 0, st, cs + 4 * G, cz + 4 * G, vals,
-                    rank, kb, n, h, xs, xe, ncnt, (uint32_t)lcap);
-        uint32_t sc[9];   // shard counts, overflow
+            KLAUNCH("dna_ls_block", 0.0, k_ls_block, dim3(cnt[4]), dim3(kWB), 0, st, cs + 4 * G, cz + 4 * G, vals,
+                    rank, n, h, o);
+        uint32_t sc[25];   // group shards, overflow | 7 unused | change shards, overflow
         HIPCHECK(hipMemcpyAsync(sc, ncnt, sizeof sc, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
+        if (sc[8] || sc[24]) return false;
+        ShardedList csl{};
+        for (int q = 0; q < 8; ++q) {
+            csl.cnt[q] = sc[16 + q];
+            if (sc[16 + q]) csl.S = std::max<uint32_t>(csl.S, (((sc[16 + q] - 1) / kCH) * 8 + (uint32_t)q + 1) * kCH);
+        }
+        if (csl.S)
+            KLAUNCH("dna_ls_apply", 0.0, k_ls_apply, dim3(nblocks(csl.S)), dim3(kB), 0, st, chg, (int64_t)csl.S, csl,
+                    rank);
         if (sc[8]) return false;
         ShardedList nsl{};
         for (int q = 0; q < 8; ++q) {
