@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <fcntl.h>
 #include <unistd.h>
 
@@ -15,6 +16,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -210,6 +212,19 @@ int bwtmi_open(int device, bwtmi_ctx **out) {
         auto *ctx = new bwtmi_ctx();
         ctx->c.device = device;
         HIPCHECK(hipSetDevice(device));
+        // how a host thread waits for the device: the background index build
+        // waits on the device while every host thread post-processes, so a
+        // spinning wait would take a core from them.  Blocking waits by default
+        // (r02az, C3: 1949 vs 1895 Mbp/s over 3 runs each; BWTMI_SYNC=spin|yield|
+        // block|auto overrides)
+        {
+            const char *e = std::getenv("BWTMI_SYNC");
+            const std::string m = e ? e : "block";
+            const unsigned f = m == "yield" ? hipDeviceScheduleYield
+                               : m == "block" ? hipDeviceScheduleBlockingSync
+                               : m == "spin" ? hipDeviceScheduleSpin : hipDeviceScheduleAuto;
+            if (hipSetDeviceFlags(f) != hipSuccess) (void)hipGetLastError();   // context already active: keep its mode
+        }
         HIPCHECK(hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking));
         HIPCHECK(hipEventCreate(&ctx->c.ev0));
         HIPCHECK(hipEventCreate(&ctx->c.ev1));
@@ -217,18 +232,43 @@ int bwtmi_open(int device, bwtmi_ctx **out) {
     });
 }
 
+static void ctx_release(Ctx &c) {
+    (void)hipStreamSynchronize(c.stream);
+    for (auto &l : c.lanes) ctx_release(*l);
+    c.lanes.clear();
+    if (c.scratch_index) index_free(c.scratch_index);
+    c.scratch_index = nullptr;
+    for (auto &s : c.slot) s.release();
+    for (auto &h : c.host) h.release();
+    for (hipEvent_t e : c.evpool) (void)hipEventDestroy(e);
+    c.evpool.clear();
+    (void)hipEventDestroy(c.ev0);
+    (void)hipEventDestroy(c.ev1);
+    (void)hipStreamDestroy(c.stream);
+}
+
+// lane k of c (k >= 1): a context of its own on c's device, created on first use
+static Ctx &scan_lane(Ctx &c, size_t k) {
+    while (c.lanes.size() < k) {
+        auto l = std::make_unique<Ctx>();
+        l->device = c.device;
+        HIPCHECK(hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking));
+        HIPCHECK(hipEventCreate(&l->ev0));
+        HIPCHECK(hipEventCreate(&l->ev1));
+        c.lanes.push_back(std::move(l));
+    }
+    Ctx &l = *c.lanes[k - 1];
+    l.ktiming = c.ktiming;
+    l.timing = c.timing;
+    return l;
+}
+
 int bwtmi_close(bwtmi_ctx *ctx) {
     return guard([&] {
         if (!ctx) return;
         ctx_join(ctx->c);   // a background error dies with the context
         ctx->c.activate();
-        (void)hipStreamSynchronize(ctx->c.stream);
-        if (ctx->c.scratch_index) index_free(ctx->c.scratch_index);
-        for (auto &s : ctx->c.slot) s.release();
-        for (auto &h : ctx->c.host) h.release();
-        (void)hipEventDestroy(ctx->c.ev0);
-        (void)hipEventDestroy(ctx->c.ev1);
-        (void)hipStreamDestroy(ctx->c.stream);
+        ctx_release(ctx->c);
         delete ctx;
     });
 }
@@ -679,6 +719,7 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
         J.postprocessed = false;
         const bwtmi_params &P = J.params;
         std::vector<std::pair<const uint8_t *, int64_t>> to_index;
+        std::vector<size_t> todo;   // contigs to scan
         for (size_t i = 0; i < J.contigs.size(); ++i) {
             const Contig &ct = J.contigs[i];
             const int64_t len = ct.trimmed_len();
@@ -687,6 +728,11 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
             if (!P.tier2) continue;                                  // bwt.py:3068
             if (len > 50000000 && !P.show_progress) continue;        // bwt.py:3070
             if (P.min_copies <= 0) continue;                         // worker raises -> [] (bwt.py:3137)
+            todo.push_back(i);
+        }
+        auto scan_one = [&](Ctx &lc, size_t i) {
+            const Contig &ct = J.contigs[i];
+            const int64_t len = ct.trimmed_len();
             const int64_t U = std::max<int64_t>(P.max_unit_len, std::min<int64_t>(len / P.min_copies, 1000));
             // a contig with Tier 3 records is screened on the host, together with them
             const bool t3 = i < J.t3.size() && !J.t3[i].empty();
@@ -695,22 +741,70 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
             // (the worker's `except Exception: print(...); return []`, bwt.py:3137-3141)
             try {
                 if (fail_contig && ct.name == fail_contig) fail(BWTMI_E_STATE, "injected failure (BWTMI_FAIL_CONTIG)");
-                strict_scan_device(c, job->dev.seqs[i].buf.as<uint8_t>(), len, 1,
+                strict_scan_device(lc, job->dev.seqs[i].buf.as<uint8_t>(), len, 1,
                                    (int32_t)std::min<int64_t>(U, INT32_MAX), P.min_copies, r,
                                    screen && !t3 && len < (int64_t)UINT32_MAX);   // 32-bit hit lengths
             } catch (const Error &e) {
                 J.errors[i] = e.msg;
                 (void)hipGetLastError();
-                (void)hipStreamSynchronize(c.stream);
-                continue;
+                (void)hipStreamSynchronize(lc.stream);
+                return;
             } catch (const std::bad_alloc &) {
                 J.errors[i] = "out of host memory";
-                continue;
+                return;
             }
             J.hits[i].swap(r.hits);   // Rule 1 (bwt.py:3118-3130) never fires on strict hits
             J.shits[i].swap(r.shits);
             J.screened[i] = r.screened ? 1 : 0;
             J.raw_n[i] = r.raw;
+        };
+        // several contigs: up to kLanes scans in flight, each lane a context with
+        // its own stream and scratch driven by its own host thread (a contig's
+        // scan is a chain of small dependent launches and host reads, so one
+        // stream leaves the device idle between them); contigs go to lanes
+        // longest first, each to the least loaded lane
+        static const int kLanes = [] {
+            const char *e = std::getenv("BWTMI_SCAN_LANES");
+            return e && *e ? std::max(1, std::min(8, std::atoi(e))) : 4;
+        }();
+        const size_t nl = std::min<size_t>((size_t)kLanes, todo.size());
+        if (nl <= 1) {
+            for (size_t i : todo) scan_one(c, i);
+        } else {
+            std::vector<size_t> ord(todo);
+            std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) {
+                return J.contigs[x].trimmed_len() > J.contigs[y].trimmed_len();
+            });
+            std::vector<std::vector<size_t>> part(nl);
+            std::vector<int64_t> load(nl, 0);
+            for (size_t i : ord) {
+                const size_t k = (size_t)(std::min_element(load.begin(), load.end()) - load.begin());
+                part[k].push_back(i);
+                load[k] += J.contigs[i].trimmed_len();
+            }
+            std::vector<Ctx *> lc(nl);
+            lc[0] = &c;
+            for (size_t k = 1; k < nl; ++k) lc[k] = &scan_lane(c, k);
+            std::vector<std::exception_ptr> ex(nl);
+            std::vector<std::thread> th;
+            for (size_t k = 1; k < nl; ++k)
+                th.emplace_back([&, k] {
+                    try {
+                        lc[k]->activate();
+                        for (size_t i : part[k]) scan_one(*lc[k], i);
+                    } catch (...) {
+                        ex[k] = std::current_exception();
+                    }
+                });
+            try {
+                for (size_t i : part[0]) scan_one(c, i);
+            } catch (...) {
+                ex[0] = std::current_exception();
+            }
+            for (auto &t : th) t.join();
+            for (size_t k = 1; k < nl; ++k) c.absorb_kstats(*lc[k]);
+            for (auto &e : ex)
+                if (e) std::rethrow_exception(e);
         }
         J.stage_ms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         J.stage_ms[1] = 0;

@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -176,7 +177,26 @@ struct Ctx {
     int last_dom_launches = 0;
     std::string dom_name;
     bool timing = true;
+    // scan lanes: extra contexts (own stream and scratch) on the same device, so
+    // the strict scans of several contigs overlap (api.cpp bwtmi_job_scan)
+    std::vector<std::unique_ptr<Ctx>> lanes;
     void activate() const { HIPCHECK(hipSetDevice(device)); }
+    // per-kernel statistics of another context (a lane) folded into this one
+    void absorb_kstats(Ctx &o) {
+        for (auto &k : o.kstats) {
+            bool found = false;
+            for (auto &m : kstats)
+                if (m.first == k.first) {
+                    m.second.ms += k.second.ms;
+                    m.second.launches += k.second.launches;
+                    m.second.bytes += k.second.bytes;
+                    found = true;
+                    break;
+                }
+            if (!found) kstats.push_back(k);
+        }
+        o.kstats.clear();
+    }
 };
 
 // A kernel launch on ctx `c`'s stream `st`, timed as `name` (algorithmic bytes

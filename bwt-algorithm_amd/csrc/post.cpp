@@ -84,19 +84,22 @@ int host_threads(const bwtmi_params &p) {
     return host_cpu_budget(nullptr, nullptr);
 }
 
-// Persistent worker pool: parallel regions reuse the same threads (and their
+// Persistent worker pools: parallel regions reuse the same threads (and their
 // thread-local DP scratch) instead of spawning per call.  The caller takes
-// part as worker 0; a region started from inside a worker runs inline.
+// part as worker 0; a region started from inside a worker of the same pool
+// runs inline.  Parallel regions go to the calling thread's current pool (the
+// process-wide one unless the thread belongs to a unit group, postprocess).
 namespace {
 class Pool {
 public:
-    static Pool &get() {
+    static Pool &global() {
         static Pool p;
         return p;
     }
+    static Pool &current() { return tl_pool ? *tl_pool : global(); }
     // f(w) for w in [0, nt)
     void run(int nt, const std::function<void(int)> &f) {
-        if (nt <= 1 || in_worker) {
+        if (nt <= 1 || worker_of == this) {
             for (int w = 0; w < nt; ++w) f(w);
             return;
         }
@@ -111,14 +114,15 @@ public:
             ++gen;
         }
         cv.notify_all();
-        in_worker = true;
+        Pool *const outer = worker_of;
+        worker_of = this;
         try {
             f(0);
         } catch (...) {
             std::lock_guard<std::mutex> lk(mu);
             if (!err) err = std::current_exception();
         }
-        in_worker = false;
+        worker_of = outer;
         // every worker finishes before f (and what it references) goes out of scope
         std::unique_lock<std::mutex> lk(mu);
         done.wait(lk, [&] { return pending == 0; });
@@ -138,6 +142,7 @@ public:
         cv.notify_all();
         for (auto &t : th) t.join();
     }
+    static thread_local Pool *tl_pool;   // the pool this thread's regions go to (nullptr: global)
 
 private:
     void grow(int n) {
@@ -147,7 +152,8 @@ private:
         }
     }
     void loop(int id) {
-        in_worker = true;
+        worker_of = this;
+        tl_pool = this;
         int64_t seen = 0;
         {
             std::lock_guard<std::mutex> lk(mu);
@@ -182,9 +188,10 @@ private:
     int want = 0, pending = 0;
     int64_t gen = 0;
     bool stop = false;
-    static thread_local bool in_worker;
+    static thread_local Pool *worker_of;   // the pool whose region this thread is running
 };
-thread_local bool Pool::in_worker = false;
+thread_local Pool *Pool::worker_of = nullptr;
+thread_local Pool *Pool::tl_pool = nullptr;
 }  // namespace
 
 // fn(begin, end) over [0, n) in contiguous chunks
@@ -196,7 +203,7 @@ static void parallel_for(int64_t n, int nt, F &&fn) {
         fn((int64_t)0, n);
         return;
     }
-    Pool::get().run(nt, [&](int t) { fn(n * t / nt, n * (t + 1) / nt); });
+    Pool::current().run(nt, [&](int t) { fn(n * t / nt, n * (t + 1) / nt); });
 }
 
 // dynamic scheduling: fn(item, worker)
@@ -213,7 +220,7 @@ static void parallel_items(int64_t n, int nt, F &&fn) {
         }
     };
     if (nt == 1) { work(0); return; }
-    Pool::get().run(nt, work);
+    Pool::current().run(nt, work);
 }
 
 void run_tasks(int64_t n, int nt, const std::function<void(int64_t)> &fn) {
@@ -1289,9 +1296,49 @@ void postprocess(Job &job) {
     int64_t busy = 0;
     for (size_t c = 0; c < job.hits.size(); ++c)
         busy += (job.hits[c].empty() && (c >= job.shits.size() || job.shits[c].empty())) ? 0 : 1;
+    // a few units and threads to spare: G groups of T / G threads, each its own
+    // pool, take units longest first (a unit's parallel regions carry serial
+    // parts and joins that one 16-thread region per unit paid unit by unit)
+    static const int kGroupThreads = [] {
+        const char *e = std::getenv("BWTMI_UNIT_GROUP_THREADS");
+        return e && *e ? std::max(1, std::atoi(e)) : 4;
+    }();
+    const int G = (int)std::min<int64_t>(busy, T / kGroupThreads);
     if (busy >= T) {
         parallel_items(job.nunits, T, [&](int64_t k, int) {
             process_unit(job, units[(size_t)k], job.hits, job.shits, res[(size_t)k], &ms[(size_t)k * 4], 1);
+        });
+    } else if (G >= 2 && job.nunits >= 2) {
+        static std::vector<std::unique_ptr<Pool>> groups;   // persistent, like the global pool
+        while ((int)groups.size() < G) groups.push_back(std::make_unique<Pool>());
+        std::vector<int32_t> order((size_t)job.nunits);
+        std::vector<int64_t> work((size_t)job.nunits, 0);
+        for (int32_t k = 0; k < job.nunits; ++k) {
+            order[(size_t)k] = k;
+            for (int32_t ci : units[(size_t)k]) {
+                const size_t c = (size_t)ci;
+                work[(size_t)k] += (c < job.hits.size() ? (int64_t)job.hits[c].size() : 0) +
+                                   (c < job.shits.size() ? (int64_t)job.shits[c].size() : 0);
+            }
+        }
+        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return work[(size_t)a] > work[(size_t)b]; });
+        std::atomic<int64_t> next{0};
+        const int per = T / G;
+        parallel_items(G, G, [&](int64_t g, int) {
+            Pool *const prev = Pool::tl_pool;
+            Pool::tl_pool = groups[(size_t)g].get();
+            try {
+                for (;;) {
+                    const int64_t q = next.fetch_add(1, std::memory_order_relaxed);
+                    if (q >= job.nunits) break;
+                    const size_t k = (size_t)order[(size_t)q];
+                    process_unit(job, units[k], job.hits, job.shits, res[k], &ms[k * 4], per);
+                }
+            } catch (...) {
+                Pool::tl_pool = prev;
+                throw;
+            }
+            Pool::tl_pool = prev;
         });
     } else {
         for (int32_t k = 0; k < job.nunits; ++k) {
