@@ -442,6 +442,11 @@ void fasta_scan_part(Job &job, const char *path, int32_t world, int32_t rank, st
         Chunk &C = ck[(size_t)t];
         C.a = cut[(size_t)t];
         C.b = cut[(size_t)t + 1];
+        if (const int64_t nl = plain_newlines(p + C.a, C.b - C.a); nl >= 0) {   // no header: all content
+            C.plain = true;
+            C.pre = (C.b - C.a) - nl;
+            return;
+        }
         for_lines(p, C.a, C.b, [&](int64_t s, int64_t e) {
             if (p[s] == '>') {
                 int64_t x = s + 1;
@@ -550,7 +555,17 @@ void fasta_load_parts(Job &job, const char *path, int32_t flank_trim, int32_t wo
     }
     const auto t1 = clk::now();
     Fd f(path);
-    thread_local Seq raw;
+    // this rank's contigs: their byte ranges read into one buffer by one
+    // parallel read, then cut into line-start chunks that the count and copy
+    // passes process as one flat list (not contig by contig: a 12.5 Mbp
+    // contig alone gave the pool three read pieces and short regions)
+    struct Own {
+        size_t cid;
+        int64_t a, b, off;   // file range [a, b) at off in the buffer
+        size_t c0, c1;       // its chunks [c0, c1) of the flat list
+    };
+    std::vector<Own> own;
+    int64_t tot = 0;
     for (size_t cid = 0; cid < job.contigs.size(); ++cid) {
         const int32_t k = last_inst[cid];
         if (k < 0) continue;
@@ -562,32 +577,89 @@ void fasta_load_parts(Job &job, const char *path, int32_t flank_trim, int32_t wo
         }
         const int64_t a = inst[(size_t)k].line;
         const int64_t b = (size_t)k + 1 < inst.size() ? inst[(size_t)k + 1].line : N;
-        char *p = raw.resize_uninit((size_t)(b - a));
-        pread_range(f.fd, p, a, b, nt);
-        const int64_t n = b - a;
-        const int64_t T = std::max<int64_t>(1, std::min<int64_t>(4 * (int64_t)nt, n / (int64_t(1) << 20) + 1));
-        const std::vector<int64_t> cut = cut_lines(p, 0, n, T, nt);
-        std::vector<int64_t> cnt((size_t)T + 1, 0);
-        run_tasks(T, nt, [&](int64_t t) {   // content bytes per chunk (the header line is skipped)
-            int64_t m = 0;
-            for_lines(p, cut[(size_t)t], cut[(size_t)t + 1], [&](int64_t s, int64_t e) {
-                if (p[s] != '>') m += e - s;
-            });
-            cnt[(size_t)t + 1] = m;
-        });
-        for (int64_t t = 0; t < T; ++t) cnt[(size_t)t + 1] += cnt[(size_t)t];
-        if (cnt[(size_t)T] != inst[(size_t)k].len)
-            fail(BWTMI_E_IO, "%s changed while it was read (contig %s)", path, c.name.c_str());
-        char *dst = c.full.resize_uninit((size_t)cnt[(size_t)T]);
-        run_tasks(T, nt, [&](int64_t t) {
-            char *d = dst + cnt[(size_t)t];
-            for_lines(p, cut[(size_t)t], cut[(size_t)t + 1], [&](int64_t s, int64_t e) {
-                if (p[s] == '>') return;
-                upper_copy(d, p + s, e - s);
-                d += e - s;
-            });
-        });
+        own.push_back(Own{cid, a, b, tot, 0, 0});
+        tot += b - a;
     }
+    thread_local Seq raw;
+    char *p = raw.resize_uninit((size_t)tot);
+    {
+        const int64_t piece = int64_t(4) << 20;
+        std::vector<std::pair<size_t, int64_t>> rd;   // (own index, piece start in its range)
+        for (size_t u = 0; u < own.size(); ++u)
+            for (int64_t o = 0; o < own[u].b - own[u].a; o += piece) rd.push_back({u, o});
+        std::atomic<bool> bad{false};
+        run_tasks((int64_t)rd.size(), nt, [&](int64_t q) {
+            const Own &w = own[rd[(size_t)q].first];
+            int64_t o = w.a + rd[(size_t)q].second;
+            const int64_t e = std::min(w.b, o + piece);
+            while (o < e) {
+                const ssize_t r = ::pread(f.fd, p + w.off + (o - w.a), (size_t)(e - o), (off_t)o);
+                if (r <= 0) { bad = true; return; }
+                o += r;
+            }
+        });
+        if (bad) fail(BWTMI_E_IO, "read error");
+    }
+    std::vector<int64_t> ca, cb;   // chunk [ca, cb) in the buffer
+    for (Own &w : own) {
+        const int64_t n = w.b - w.a;
+        const int64_t T = std::max<int64_t>(1, std::min<int64_t>(4 * (int64_t)nt, n / (int64_t(1) << 20) + 1));
+        const std::vector<int64_t> cut = cut_lines(p, w.off, w.off + n, T, nt);
+        w.c0 = ca.size();
+        for (int64_t t = 0; t < T; ++t) {
+            ca.push_back(cut[(size_t)t]);
+            cb.push_back(cut[(size_t)t + 1]);
+        }
+        w.c1 = ca.size();
+    }
+    const size_t NC = ca.size();
+    std::vector<int64_t> cnt(NC, 0);
+    std::vector<uint8_t> plain(NC, 0);
+    run_tasks((int64_t)NC, nt, [&](int64_t t) {   // content bytes per chunk (the header line is skipped)
+        const int64_t a0 = ca[(size_t)t], b0 = cb[(size_t)t];
+        if (const int64_t nl = plain_newlines(p + a0, b0 - a0); nl >= 0) {   // lines need no per-line work
+            plain[(size_t)t] = 1;
+            cnt[(size_t)t] = (b0 - a0) - nl;
+            return;
+        }
+        int64_t m = 0;
+        for_lines(p, a0, b0, [&](int64_t s, int64_t e) {
+            if (p[s] != '>') m += e - s;
+        });
+        cnt[(size_t)t] = m;
+    });
+    std::vector<char *> dst(NC, nullptr);   // where each chunk's content goes
+    for (const Own &w : own) {
+        int64_t len = 0;
+        for (size_t t = w.c0; t < w.c1; ++t) len += cnt[t];
+        Contig &c = job.contigs[w.cid];
+        if (len != inst[(size_t)last_inst[w.cid]].len)
+            fail(BWTMI_E_IO, "%s changed while it was read (contig %s)", path, c.name.c_str());
+        char *d = c.full.resize_uninit((size_t)len);
+        for (size_t t = w.c0; t < w.c1; ++t) {
+            dst[t] = d;
+            d += cnt[t];
+        }
+    }
+    run_tasks((int64_t)NC, nt, [&](int64_t t) {
+        char *d = dst[(size_t)t];
+        const int64_t a0 = ca[(size_t)t], b0 = cb[(size_t)t];
+        if (plain[(size_t)t]) {   // runs between newlines, as load_fasta's pass 2
+            for (int64_t i = a0; i < b0;) {
+                const char *nl = (const char *)std::memchr(p + i, '\n', (size_t)(b0 - i));
+                const int64_t j = nl ? (int64_t)(nl - p) : b0;
+                upper_copy(d, p + i, j - i);
+                d += j - i;
+                i = j + 1;
+            }
+            return;
+        }
+        for_lines(p, a0, b0, [&](int64_t s, int64_t e) {
+            if (p[s] == '>') return;
+            upper_copy(d, p + s, e - s);
+            d += e - s;
+        });
+    });
     if (std::getenv("BWTMI_STATS")) {
         auto d = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
         std::fprintf(stderr, "  load_fasta_parts: stitch %.1f own contigs %.1f ms\n", d(t0, t1), d(t1, clk::now()));

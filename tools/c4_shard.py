@@ -6,6 +6,9 @@ cores are split evenly among 8 GPU ranks.  Projected 8-rank C4 throughput =
 100 Mbp / the slowest shard's step (ranks share no data path; the only
 collectives are two small all-reduces in the sharded write).
 
+Worlds other than 8 (C4_SHARD_WORLDS="8,4,2"): the same for the shards of a
+2- or 4-rank run (4 or 2 contigs per rank).
+
 usage: python tools/c4_shard.py OUT.json [threads ...]"""
 import json, os, sys, tempfile, time
 
@@ -51,11 +54,13 @@ def main():
     fa = os.path.join(tempfile.gettempdir(), "c4_shard.fa")
     synth.write_fasta(fa, [12_500_000] * 8, 0.0)
     out = os.path.join(tempfile.gettempdir(), "c4_shard.tab")
-    res = dict(workload="C4 shard: 8 x 12.5 Mbp FASTA, world 8, LPT shards", host=_lib.host_info(), runs=[])
+    worlds = [int(x) for x in os.environ.get("C4_SHARD_WORLDS", "8").split(",")]
+    res = dict(workload="C4 shard: 8 x 12.5 Mbp FASTA, LPT shards of worlds %s" % worlds, host=_lib.host_info(),
+               runs=[])
     split = os.environ.get("C4_SHARD_SPLIT", "1") == "1"   # the split loader (bench / CLI at N > 1)
     res["split_load"] = split
-    for T in tlist:
-        for r in (0, 7):
+    for W, T in [(w, t) for w in worlds for t in tlist]:
+        for r in sorted({0, W - 1}):
             job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True, build_index=True,
                       sa_sample=32, threads=T)
 
@@ -66,11 +71,11 @@ def main():
                 fn(*args)
                 calls[name] = calls.get(name, 0.0) + (time.perf_counter() - t) * 1e3
 
-            pc = PartsComm(fa, 8, r) if split else None
+            pc = PartsComm(fa, W, r) if split else None
 
             def step():
                 timed("reset", job.reset)
-                timed("load_fasta", job.load_fasta, fa, FLANK, 8, r, pc)
+                timed("load_fasta", job.load_fasta, fa, FLANK, W, r, pc)
                 timed("upload", job.upload, ctx)
                 timed("scan", job.scan, ctx)
                 timed("postprocess", job.postprocess)
@@ -83,15 +88,15 @@ def main():
                 t = time.perf_counter()
                 step()
                 ts.append((time.perf_counter() - t) * 1e3)
-            bp = sum(job.contig_weight(i) for i in job.select_shard(8, r))
+            bp = sum(job.contig_weight(i) for i in job.select_shard(W, r))
             ms = sorted(ts)[1]
-            res["runs"].append(dict(threads=T, rank=r, shard_bp=bp, step_ms=round(ms, 2),
+            res["runs"].append(dict(world=W, threads=T, rank=r, shard_bp=bp, step_ms=round(ms, 2),
                                     steps_ms=[round(x, 2) for x in ts], stage_ms=[round(x, 2) for x in job.stage_ms()],
                                     calls_ms={k: round(v / 3, 2) for k, v in calls.items()}))
             print(json.dumps(res["runs"][-1]), flush=True)
-    for T in tlist:
-        worst = max(x["step_ms"] for x in res["runs"] if x["threads"] == T)
-        res[f"projected_8rank_mbp_per_s_at_{T}_threads_per_rank"] = round(100.0 / (worst / 1e3), 1)
+    for W, T in [(w, t) for w in worlds for t in tlist]:
+        worst = max(x["step_ms"] for x in res["runs"] if x["threads"] == T and x["world"] == W)
+        res[f"projected_{W}rank_mbp_per_s_at_{T}_threads_per_rank"] = round(100.0 / (worst / 1e3), 1)
     with open(out_json, "w") as f:
         json.dump(res, f, indent=1)
     os.unlink(fa)
