@@ -32,6 +32,9 @@ import hashlib
 import json
 import os
 import platform
+import signal
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -131,9 +134,79 @@ def fm_all_motifs(seq: bytes, reps: int = 5):
                 mpatterns_per_s=round(len(pats) / dt / 1e6, 2))
 
 
+def cli_drop_in(fa: str, args, reps: int = 2):
+    """The drop-in CLI (`bwt.py FA -o OUT ARGS`, bwt.py:4201-4370) run
+    in-process on the workload's FASTA: wall time of each run (a fresh
+    TandemRepeatFinder and job every time, so the first run carries the
+    process's cold costs) and the output's sha256.  Outside the timed steps."""
+    import contextlib
+    import io
+    from bwtmi import cli
+    out = fa + ".cli.tab"
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        with contextlib.redirect_stdout(io.StringIO()):
+            rc = cli.main([fa, "-o", out] + list(args))
+        times.append(round(time.perf_counter() - t0, 4))
+        if rc != 0:
+            raise RuntimeError(f"bwt.py CLI exited with {rc}")
+    with open(out, "rb") as f:
+        digest = hashlib.sha256(f.read()).hexdigest()
+    os.unlink(out)
+    return dict(argv=["bwt.py", "FA", "-o", "OUT"] + list(args), wall_s=times, output_sha256=digest)
+
+
 def word_compares(n: int, U: int) -> int:
     """k_runs' 32-position word compares of one contig: sum_L ceil((n - L) / 32)."""
     return sum((n - L + 31) // 32 for L in range(1, min(U, n // 3) + 1))
+
+
+def launch_ranks(n: int, argv, script: str = None) -> int:
+    """`bench.py --gpus N` without an external launcher: start N rank processes
+    of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT
+    in their environment, one per GPU) and return the first failing exit code,
+    else 0.  Rank 0 prints the JSON line.  This parent never touches the GPU
+    (no HIP call, nothing loaded from libbwtmi), so starting children is safe;
+    the reference's unit of parallelism is the same: one worker per contig
+    group (bwt.py:3850-3912)."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BWTMI_RDZV_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env,
+                                      start_new_session=True))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            time.sleep(0.05)
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                          file=sys.stderr)
+                    for q in live:      # the peers would wait for it in a collective forever
+                        try:
+                            os.killpg(q.pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+    return rc
 
 
 def main():
@@ -147,12 +220,18 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-index", action="store_true", help="skip the FM index (scan-only step)")
     ap.add_argument("--no-fm", action="store_true", help="skip the all-motif FM search report")
+    ap.add_argument("--no-cli", action="store_true", help="skip the in-process drop-in CLI timing")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--pmc-summary", default=PMC_SUMMARY,
                     help="tools/pmc_traffic.py output giving HBM bytes per launch (roofline.traffic)")
     a = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a.gpus, sys.argv[1:])
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     wl_name = a.workload if a.workload != "auto" else ("C3" if world == 1 else "C4")
@@ -302,6 +381,11 @@ def main():
     if not a.no_fm:
         first = min(i for i in range(job.contig_count()) if job.contig_info(i)[1] > 0)
         fm = fm_all_motifs(job.contig_seq(first))
+    cli = None
+    if world == 1 and not shared and not a.no_cli:
+        cli = cli_drop_in(fa, ["--progress", "--jobs", "0"])
+        cli["vs_step"] = round(min(cli["wall_s"]) * 1e3 / ms_step, 2)
+        cli["golden_match"] = golden["sha256"] == cli["output_sha256"] if golden else None
     load_up = per_call.get("load_fasta", 0.0) + per_call.get("upload", 0.0)
     line = {
         "metric": METRIC,
@@ -336,6 +420,7 @@ def main():
         "calls_ms_per_step": {k: round(v, 2) for k, v in per_call.items()},
         "value_resident_text": round(total_bp / 1e6 / ((ms_step - load_up) / 1e3), 3) if ms_step > load_up else None,
         "fm_all_motifs_1_10": fm,
+        "cli_drop_in": cli,
     }
     print(json.dumps(line))
     if c is not None:

@@ -14,17 +14,57 @@ from . import _lib
 from ._lib import check, lib
 
 
+class _LazyText:
+    """`BWTCore.text` for an index built from bytes: the str is decoded on
+    first use only (nothing on the CLI path reads it)."""
+
+    def __init__(self, raw: bytes):
+        self._raw, self._s = raw, None
+
+    def _str(self) -> str:
+        if self._s is None:
+            self._s = self._raw.decode("latin-1")
+        return self._s
+
+    def __len__(self):
+        return len(self._raw)
+
+    def __str__(self):
+        return self._str()
+
+    def __eq__(self, other):
+        return self._str() == (str(other) if isinstance(other, _LazyText) else other)
+
+    def __hash__(self):
+        return hash(self._str())
+
+    def __getitem__(self, k):
+        return self._str()[k]
+
+    def __iter__(self):
+        return iter(self._str())
+
+    def __contains__(self, x):
+        return x in self._str()
+
+    def __getattr__(self, name):
+        return getattr(self._str(), name)
+
+
 class BWTCore:
     BASE_TO_BITS = {"A": 0, "C": 1, "G": 2, "T": 3, "N": 0}
     BITS_TO_BASE = {0: "A", 1: "C", 2: "G", 3: "T"}
 
-    def __init__(self, text: str, sa_sample_rate: int = 32, occ_sample_rate: int = 128,
+    def __init__(self, text: Union[str, bytes], sa_sample_rate: int = 32, occ_sample_rate: int = 128,
                  device: Optional[int] = None, build_kmer: bool = True):
-        self.text = text
+        # bytes are taken as the encoded text itself (no str is built: the CLI
+        # hands over the loader's native contig bytes)
+        raw = bytes(text) if isinstance(text, (bytes, bytearray, memoryview)) else None
+        self.text = text if raw is None else _LazyText(raw)
         self.n = len(text)
         self.sa_sample_rate = sa_sample_rate
         self.occ_sample_rate = occ_sample_rate
-        self.text_arr = np.frombuffer(text.encode("utf-8"), dtype=np.uint8)
+        self.text_arr = np.frombuffer(raw if raw is not None else text.encode("utf-8"), dtype=np.uint8)
         self._ctx = _lib.ctx(device)
         self._h = C.c_void_p()
         buf = self.text_arr if self.text_arr.size else np.zeros(1, dtype=np.uint8)
@@ -36,7 +76,12 @@ class BWTCore:
         check(lib().bwtmi_index_get_counts(self._h, totals.ctypes.data_as(C.c_void_p),
                                            cum.ctypes.data_as(C.c_void_p)))
         self._totals, self._C = totals, cum
-        self.alphabet = sorted(set(text))
+        if raw is not None or text.isascii():
+            # ASCII text (O(1) test on a CPython str): the characters are the
+            # byte values the device histogram found (bwt.py:129)
+            self.alphabet = [chr(c) for c in np.nonzero(totals)[0].tolist()]
+        else:
+            self.alphabet = sorted(set(text))
         self.char_to_code = {c: ord(c) for c in self.alphabet}
         self.code_to_char = {ord(c): c for c in self.alphabet}
         self.char_counts = {c: int(cum[ord(c)]) for c in self.alphabet if ord(c) < 256}

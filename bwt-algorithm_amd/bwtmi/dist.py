@@ -101,6 +101,8 @@ def run_sharded(finder, job, scan_fn: Optional[Callable] = None):
         scan_fn(job, shard)
     else:
         job.scan(_lib.ctx(int(os.environ.get("LOCAL_RANK", "0"))))
+    from .finder import TandemRepeatFinder
+    TandemRepeatFinder._report_errors(job)   # the worker's ERROR line per failed contig (bwt.py:3137-3141)
     job.postprocess()
     if scan_fn is None:
         job.wait(_lib.ctx(int(os.environ.get("LOCAL_RANK", "0"))))

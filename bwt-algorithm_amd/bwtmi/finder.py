@@ -12,13 +12,87 @@ process.
 """
 from __future__ import annotations
 
+import os
 import sys
 import time
+from collections.abc import MutableMapping
 from typing import Dict, List, Optional
 
 from . import _lib
 from .core import BWTCore
 from .records import Job, RepeatList, TandemRepeat
+
+
+class _ContigMap(MutableMapping):
+    """`sequences` / `full_sequences` of a loaded finder: name -> str, decoded
+    from the native loader's bytes on first access only (the CLI path never
+    reads them, so no per-base Python work is done at 100 Mbp).  Same keys,
+    order and duplicate-name rule as load_reference (bwt.py:3713-3756)."""
+
+    def __init__(self, job: Job, trimmed: bool):
+        self._job, self._trimmed = job, trimmed
+        self._ids: Dict[str, int] = {}
+        for i in range(job.contig_count()):
+            self._ids[job.contig_info(i)[0]] = i          # a later duplicate wins, in place
+        self._vals: Dict[str, str] = {}
+
+    def raw(self, name: str) -> bytes:
+        name_, fl, tl, tr = self._job.contig_info(self._ids[name])
+        full = self._job.contig_seq(self._ids[name])
+        return full[tl:fl - tr] if self._trimmed else full
+
+    def contig_id(self, name: str) -> int:
+        return self._ids[name]
+
+    def __getitem__(self, name: str) -> str:
+        v = self._vals.get(name)
+        if v is None:
+            if name not in self._ids:
+                raise KeyError(name)
+            v = self._vals[name] = self.raw(name).decode("latin-1")
+        return v
+
+    def __setitem__(self, name: str, value: str) -> None:
+        if name not in self._ids:
+            self._ids[name] = -1
+        self._vals[name] = value
+
+    def __delitem__(self, name: str) -> None:
+        del self._ids[name]
+        self._vals.pop(name, None)
+
+    def __iter__(self):
+        return iter(self._ids)
+
+    def __len__(self):
+        return len(self._ids)
+
+
+class _DeferredCore(BWTCore):
+    """BWTCore over a loaded contig + '$', built on the device on first use.
+    build_indices of the reference (bwt.py:3758-3790) builds a parent index per
+    contig that the default path never reads (SURVEY.md §0.2, only Tier 3 does);
+    the worker's own index (bwt.py:3053-3054) is built by the job behind the
+    post-processing.  So the parent's indices are deferred, not dropped: any
+    attribute or query builds it exactly as BWTCore(seq + '$') would."""
+
+    def __init__(self, seqs: "_ContigMap", name: str, sa_sample_rate: int, device: Optional[int]):
+        object.__setattr__(self, "_deferred", (seqs, name, sa_sample_rate, device))
+
+    def _build(self) -> None:
+        seqs, name, rate, dev = object.__getattribute__(self, "_deferred")
+        object.__setattr__(self, "_deferred", None)
+        BWTCore.__init__(self, seqs.raw(name) + b"$", rate, device=dev)
+
+    def __getattr__(self, attr):
+        if attr.startswith("__") or object.__getattribute__(self, "_deferred") is None:
+            raise AttributeError(attr)
+        self._build()
+        return getattr(self, attr)
+
+    def __del__(self):
+        if object.__getattribute__(self, "_deferred") is None:
+            BWTCore.__del__(self)
 
 
 class TandemRepeatFinder:
@@ -48,35 +122,42 @@ class TandemRepeatFinder:
 
     # ------------------------------------------------------------------ input
     def _new_job(self, tier2: bool = True) -> Job:
+        # the worker's FM index (bwt.py:3053-3054) is built by the job on the
+        # device, behind the host post-processing (BWTMI_SKIP_INDEX=1: not at all)
+        build = os.environ.get("BWTMI_SKIP_INDEX", "0") != "1"
         return Job(min_copies=self.min_copies, max_unit_len=self.max_unit_len,
                    show_progress=self.show_progress, tier2=tier2, threads=self.threads,
-                   build_index=False, sa_sample=self.sa_sample_rate)
+                   build_index=build, sa_sample=self.sa_sample_rate)
 
     def load_reference(self) -> Dict[str, str]:
         job = self._new_job()
         job.load_fasta(self.reference_file, self.flank_trim)
         self.job = job
-        seqs: Dict[str, str] = {}
-        self.full_sequences = {}
+        self.full_sequences = _ContigMap(job, trimmed=False)
+        self.sequences = _ContigMap(job, trimmed=True)
         self.trim_offsets = {}
         for i in range(job.contig_count()):
             name, fl, tl, tr = job.contig_info(i)
-            full = job.contig_seq(i).decode("latin-1")
-            self.full_sequences[name] = full
             self.trim_offsets[name] = tl
-            seqs[name] = full[tl:fl - tr]
-        self.sequences = seqs
-        return seqs
+        return self.sequences
 
     def build_indices(self, sequences: Dict[str, str]):
-        """One device FM index per contig over seq + '$' (bwt.py:3758-3790)."""
+        """One device FM index per contig over seq + '$' (bwt.py:3758-3790).
+        Sequences of this finder's own load_reference get deferred indices
+        (_DeferredCore); any other mapping is indexed now."""
         print("Building BWT indices...")
         t0 = time.time()
-        items = list(sequences.items())
-        for i, (chrom, seq) in enumerate(items, 1):
+        items = list(sequences.keys())
+        own = isinstance(sequences, _ContigMap) and sequences is self.sequences
+        for i, chrom in enumerate(items, 1):
             pct = (i - 1) / len(items) * 100
-            print(f"\r  {pct:5.1f}% Building index for {chrom} ({len(seq):,} bp)", end="", flush=True)
-            self.bwt_cores[chrom] = BWTCore(seq + "$", self.sa_sample_rate, device=self.device)
+            if own:
+                self.bwt_cores[chrom] = _DeferredCore(sequences, chrom, self.sa_sample_rate, self.device)
+                print(f"\r  {pct:5.1f}% Index for {chrom} queued", end="", flush=True)
+            else:
+                seq = sequences[chrom]
+                print(f"\r  {pct:5.1f}% Building index for {chrom} ({len(seq):,} bp)", end="", flush=True)
+                self.bwt_cores[chrom] = BWTCore(seq + "$", self.sa_sample_rate, device=self.device)
         print(f"\r  100.0% BWT indices built for {len(items)} chromosome(s) - {time.time() - t0:.1f}s     ")
         print()
 

@@ -712,6 +712,7 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
         J.raw_n.assign(J.contigs.size(), 0);
         J.errors.assign(J.contigs.size(), std::string());
         const char *fail_contig = std::getenv("BWTMI_FAIL_CONTIG");   // test hook: this contig's worker fails
+        const char *fail_kind = std::getenv("BWTMI_FAIL_KIND");       // "hip": as a device fault
         // nested suppression + sort + dedup on the device (BWTMI_HOST_SCREEN=1: on the host)
         const char *hs = std::getenv("BWTMI_HOST_SCREEN");
         const bool screen = !(hs && *hs == '1');
@@ -739,12 +740,20 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
             ScanResult r;
             // a failing contig yields no records and an error message, the others go on
             // (the worker's `except Exception: print(...); return []`, bwt.py:3137-3141)
+            // A device fault (BWTMI_E_HIP: a failed launch, copy or synchronisation) is
+            // not contig-local -- the lanes share one device, and a sticky fault fails
+            // every later contig -- and the reference has no such failure: the scan
+            // stops and the call returns the error, so the run fails instead of
+            // writing a partial repeat.tab.
             try {
-                if (fail_contig && ct.name == fail_contig) fail(BWTMI_E_STATE, "injected failure (BWTMI_FAIL_CONTIG)");
+                if (fail_contig && ct.name == fail_contig)
+                    fail(fail_kind && !std::strcmp(fail_kind, "hip") ? BWTMI_E_HIP : BWTMI_E_STATE,
+                         "injected failure (BWTMI_FAIL_CONTIG)");
                 strict_scan_device(lc, job->dev.seqs[i].buf.as<uint8_t>(), len, 1,
                                    (int32_t)std::min<int64_t>(U, INT32_MAX), P.min_copies, r,
                                    screen && !t3 && len < (int64_t)UINT32_MAX);   // 32-bit hit lengths
             } catch (const Error &e) {
+                if (e.code == BWTMI_E_HIP) throw;
                 J.errors[i] = e.msg;
                 (void)hipGetLastError();
                 (void)hipStreamSynchronize(lc.stream);

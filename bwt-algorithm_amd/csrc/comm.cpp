@@ -11,6 +11,7 @@
 // librccl is opened with dlopen on first use: single-GPU runs never load it.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cstring>
 #include <mutex>
@@ -20,20 +21,14 @@
 
 namespace {
 
-// the subset of rccl.h used here (ABI of RCCL 2.x, ROCm 7)
-typedef struct {
-    char internal[128];
-} ncclUniqueId;
-typedef struct ncclComm *ncclComm_t;
-typedef int ncclResult_t;   // 0 = ncclSuccess
-enum { ncclInt64 = 5, ncclFloat64 = 8 };
-enum { ncclSum = 0, ncclMax = 2 };
-
+// types, enums and the id layout come from the image's own header; the
+// functions are resolved with dlsym so single-GPU runs never load librccl
 struct Rccl {
     void *h = nullptr;
     ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
     ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
-    ncclResult_t (*AllReduce)(const void *, void *, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                              hipStream_t) = nullptr;
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
     const char *(*GetErrorString)(ncclResult_t) = nullptr;
 };
@@ -41,12 +36,16 @@ struct Rccl {
 Rccl &rccl() {
     static Rccl r;
     static std::once_flag once;
+    static const char *open_error = nullptr;
     std::call_once(once, [] {
         for (const char *name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
             r.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
             if (r.h) break;
         }
-        if (!r.h) return;
+        if (!r.h) {
+            open_error = dlerror();   // read once: the call clears it
+            return;
+        }
         r.GetUniqueId = (decltype(r.GetUniqueId))dlsym(r.h, "ncclGetUniqueId");
         r.CommInitRank = (decltype(r.CommInitRank))dlsym(r.h, "ncclCommInitRank");
         r.AllReduce = (decltype(r.AllReduce))dlsym(r.h, "ncclAllReduce");
@@ -54,12 +53,12 @@ Rccl &rccl() {
         r.GetErrorString = (decltype(r.GetErrorString))dlsym(r.h, "ncclGetErrorString");
     });
     if (!r.h || !r.GetUniqueId || !r.CommInitRank || !r.AllReduce || !r.CommDestroy)
-        bwtmi::fail(BWTMI_E_NODEVICE, "librccl could not be loaded: %s", dlerror() ? dlerror() : "missing symbols");
+        bwtmi::fail(BWTMI_E_NODEVICE, "librccl could not be loaded: %s", open_error ? open_error : "missing symbols");
     return r;
 }
 
 void nccl_check(ncclResult_t e, const char *what) {
-    if (e != 0) {
+    if (e != ncclSuccess) {
         Rccl &r = rccl();
         bwtmi::fail(BWTMI_E_HIP, "%s failed: %s", what, r.GetErrorString ? r.GetErrorString(e) : "rccl error");
     }

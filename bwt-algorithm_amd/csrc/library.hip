@@ -338,15 +338,18 @@ __device__ __forceinline__ int64_t max_mm_for_array_dev(int64_t L, int64_t c) { 
     return m > 1 ? m : 1;
 }
 
+// Wave reductions return a scalar (readfirstlane): loops and branches that
+// exit on them are uniform by construction, never a per-lane copy the compiler
+// could treat as divergent (the r02al-r02ap hang).
 __device__ __forceinline__ int wave_sum_i(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return __builtin_amdgcn_readfirstlane(v);
 }
 __device__ __forceinline__ int wave_min_i(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
+    return __builtin_amdgcn_readfirstlane(v);
 }
 
 struct SimCol {

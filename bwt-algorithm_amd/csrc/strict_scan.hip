@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) void k_runs(const uint32_t *__restrict__ P, in
             const int v = __shfl_up(incl, o, 64);
             if (lane >= o) incl += v;
         }
-        const int tot = __shfl(incl, 63, 64);
+        const int tot = __builtin_amdgcn_readlane(incl, 63);   // scalar: the `continue` below is uniform
         if (tot == 0) continue;   // wave-uniform
         const int seg = (int)(blockIdx.x & (kCandSegs - 1));
         unsigned long long base = 0;

@@ -1,0 +1,195 @@
+"""Device tests at the benched sizes and on the multi-GPU plumbing:
+
+* the >50 Mbp Tier-2 gate of the worker (bwt.py:3068-3072) at its boundary;
+* the FM index of a C3-size (100 Mbp) contig through size-independent
+  properties (bwt.py:138-333: SA, BWT, C/Occ, sampled SA, 8-mer hash) and
+  backward search (bwt.py:359-389) for every canonical motif of 1..10 bp
+  against k-mer counts taken straight from the text;
+* the RCCL transport (csrc/comm.cpp) on one rank: typed all-reduces and the
+  sharded writer going through it;
+* a device fault fails the run instead of being reported per contig;
+* the CLI's deferred parent indices (bwt.py:3758-3790) build on first use.
+Integer work: every comparison is exact."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from oracle import post
+
+pytestmark = pytest.mark.gpu
+
+HEADER_SHA = "02f1e37be1d898b12b48ab0c380fad02c0bd48aaebb8300fe8cd68fe35752b3b"
+
+
+def _cli_sha(fa, out, args):
+    from bwtmi import cli
+    assert cli.main([str(fa), "-o", str(out), "--jobs", "-1"] + list(args)) == 0
+    data = out.read_bytes()
+    return hashlib.sha256(data).hexdigest(), data.count(b"\n") - 1
+
+
+def test_tier2_gate_boundary_50mbp(gpu_ctx, tmp_path):
+    """Trimmed length 50,000,000 is analysed with default parameters (the
+    output equals the --progress run, which only changes stdout below the
+    gate); 50,000,001 skips Tier 2: header-only, while --progress still
+    analyses it."""
+    from bwtmi import synth
+    body = synth.generate_contig(50_000_061, 61)
+    for n, gated in ((50_000_060, False), (50_000_061, True)):
+        fa = tmp_path / f"b{n}.fa"
+        fa.write_bytes(synth.format_fasta_record("contig1", body[:n]))
+        d_sha, d_rows = _cli_sha(fa, tmp_path / "d.tab", [])
+        p_sha, p_rows = _cli_sha(fa, tmp_path / "p.tab", ["--progress"])
+        assert p_rows > 100_000, n
+        if gated:
+            assert (d_sha, d_rows) == (HEADER_SHA, 0), n
+        else:
+            assert (d_sha, d_rows) == (p_sha, p_rows), n
+        fa.unlink()
+
+
+def _rolling_counts(t2: np.ndarray, k: int) -> np.ndarray:
+    """Occurrences of every k-mer (2-bit code, A<C<G<T) in an ACGT array."""
+    m = t2.size - k + 1
+    code = np.zeros(m, dtype=np.uint32)
+    for j in range(k):
+        code = (code << np.uint32(2)) | t2[j:j + m]
+    return np.bincount(code, minlength=4 ** k)
+
+
+def test_index_100mbp_properties(gpu_ctx):
+    """C3's contig (100 Mbp after the trim): SA is a permutation with the
+    sentinel first, sampled adjacent suffixes ascend, BWT = t[SA-1], C/Occ
+    totals, sampled SA = SA[::32], the 8-mer CSR buckets = a bincount of the
+    text's 8-mers (positions ascending inside buckets), and backward search of
+    all 145,338 canonical motifs of 1..10 bp gives intervals whose widths are
+    the motifs' occurrence counts and whose SA rows are occurrences."""
+    from bwtmi import BWTCore, MotifUtils, synth
+    seq = synth.generate_contig(100_000_000, 1)          # C3's contig1
+    body = seq[30:len(seq) - 30]
+    text = body + b"$"
+    n = len(text)
+    core = BWTCore(text)
+    sa = core.suffix_array
+    assert sa.size == n and sa[0] == n - 1
+    seen = np.zeros(n, dtype=bool)
+    seen[sa] = True
+    assert seen.all()
+    del seen
+    r = np.random.default_rng(1)
+    for k in r.integers(1, n, 4000).tolist():
+        a, b = int(sa[k - 1]), int(sa[k])
+        w = 4096
+        while text[a:a + w] == text[b:b + w]:
+            w *= 2
+        assert text[a:a + w] < text[b:b + w], k
+    t = np.frombuffer(text, dtype=np.uint8)
+    bwt = core.bwt_arr
+    assert np.array_equal(bwt, t[(sa.astype(np.int64) - 1) % n])
+    del bwt
+    occ = core.occ_checkpoints
+    cnt = np.bincount(t, minlength=256)
+    assert sorted(occ) == [36, 65, 67, 71, 84]
+    for c in (36, 65, 67, 71, 84):
+        assert occ[c][-1] == cnt[c] and core.char_totals[chr(c)] == cnt[c]
+        assert core.char_counts[chr(c)] == int(cnt[:c].sum())
+    samp = core.sampled_sa
+    assert len(samp) == (n + 31) // 32
+    for i in r.integers(0, len(samp), 20000).tolist():
+        assert samp[i * 32] == int(sa[i * 32])
+    del samp
+    t2 = np.searchsorted(np.frombuffer(b"ACGT", dtype=np.uint8), t[:-1]).astype(np.uint32)
+    off, pos = core.kmer_csr()
+    c8 = _rolling_counts(t2, 8)
+    assert np.array_equal(np.diff(off), c8) and off[-1] == n - 8
+    for code in r.integers(0, 65536, 200).tolist():
+        p = pos[off[code]:off[code + 1]]
+        assert (np.diff(p) > 0).all()
+    del off, pos
+    pats = [mt for k in range(1, 11) for mt in MotifUtils.enumerate_motifs(k)]
+    assert len(pats) == 145338
+    got = core.backward_search_batch(pats)
+    width = np.where(got[:, 0] >= 0, got[:, 1] - got[:, 0] + 1, 0)
+    lut = {ord("A"): 0, ord("C"): 1, ord("G"): 2, ord("T"): 3}
+    start = 0
+    for k in range(1, 11):
+        ck = c8 if k == 8 else _rolling_counts(t2, k)
+        ks = [p for p in pats[start:] if len(p) == k]
+        codes = np.array([sum(lut[ord(ch)] << (2 * (k - 1 - j)) for j, ch in enumerate(p)) for p in ks],
+                         dtype=np.int64)
+        assert np.array_equal(width[start:start + len(ks)], ck[codes]), k
+        start += len(ks)
+    for i in r.integers(0, len(pats), 300).tolist():   # the interval's rows are occurrences
+        sp, ep = got[i].tolist()
+        if sp < 0:
+            continue
+        p = pats[i].encode()
+        for row in range(sp, min(ep + 1, sp + 5)):
+            s = int(sa[row])
+            assert text[s:s + len(p)] == p, pats[i]
+
+
+def test_rccl_one_rank_collectives_and_sharded_write(gpu_ctx, golden_dir, tmp_path):
+    """The RCCL transport on one rank (ncclCommInitRank with nranks = 1):
+    int64 SUM / MAX with negative values and float64 MAX come back exactly,
+    and the sharded writer run through it writes the single-process file in
+    every format.  (One rank cannot tell a signed from an unsigned reduction;
+    the types now come from rccl.h itself.)"""
+    from bwtmi import _lib, comm, dist
+    from bwtmi.records import Job
+    c = comm.RcclComm(comm.Rendezvous(1, 0), 0)
+    try:
+        a = np.array([-7, 3, -(1 << 40), 0, (1 << 62)], dtype=np.int64)
+        assert np.array_equal(c.allreduce(a, comm.SUM), a)
+        assert np.array_equal(c.allreduce(a, comm.MAX), a)
+        f = np.array([-1.5, 2.25, -1e300, 0.0], dtype=np.float64)
+        assert np.array_equal(c.allreduce(f, comm.MAX), f)
+        assert np.array_equal(c.allreduce(f, comm.SUM), f)
+        words = comm.allgather_words(c, np.arange(-3, 9, dtype=np.int64))
+        assert len(words) == 1 and words[0].tolist() == list(range(-3, 9))
+        assert comm.allgather_bytes(c, b"xyz\x00\xff") == [b"xyz\x00\xff"]
+        fa = os.path.join(golden_dir, "inputs", "test_all_12.fa")
+        j = Job(min_copies=3)
+        j.load_fasta(fa, 30)
+        j.select_shard(1, 0)
+        j.scan(_lib.ctx(0))
+        j.postprocess()
+        for fmt in ("strfinder", "bed", "vcf", "trf_table", "trf_dat"):
+            out = tmp_path / f"{fmt}.out"
+            dist.write_sharded(c, j, fmt, str(out))
+            assert out.read_bytes() == j.render(fmt), fmt
+            assert out.read_text() == post.run_file(fa, fmt), fmt
+    finally:
+        c.close()
+
+
+def test_device_fault_fails_the_run(gpu_ctx, golden_dir, tmp_path, monkeypatch):
+    """A BWTMI_E_HIP error inside a contig's scan is not the worker's per-contig
+    `except Exception` (bwt.py:3137-3141): the CLI raises and writes nothing."""
+    from bwtmi import _lib, cli
+    fa = os.path.join(golden_dir, "inputs", "test2.fa")
+    seqs, _, _ = post.load_fasta(fa, 30)
+    monkeypatch.setenv("BWTMI_FAIL_CONTIG", sorted(seqs)[2])
+    monkeypatch.setenv("BWTMI_FAIL_KIND", "hip")
+    out = tmp_path / "out.tab"
+    with pytest.raises(_lib.BwtmiError, match="injected failure"):
+        cli.main([fa, "-o", str(out), "--jobs", "0"])
+    assert not out.exists()
+
+
+def test_cli_deferred_indices_build_on_use(gpu_ctx, golden_dir):
+    """build_indices over the finder's own sequences: each contig's index is
+    built on first use and equals BWTCore(seq + '$') (oracle arrays)."""
+    from bwtmi import TandemRepeatFinder
+    f = TandemRepeatFinder(os.path.join(golden_dir, "inputs", "test2.fa"))
+    seqs = f.load_reference()
+    f.build_indices(seqs)
+    for name in list(seqs)[:4]:
+        core = f.bwt_cores[name]
+        ref = oracle.Index(seqs[name].encode() + b"$")
+        assert (core.suffix_array == ref.sa).all() and (core.bwt_arr == ref.bwt).all(), name
+        assert core.backward_search("AC") == ref.backward_search(b"AC")
+        assert core.text == seqs[name] + "$"

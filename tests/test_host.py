@@ -546,3 +546,43 @@ def test_job_write_streams_the_rendered_file(tmp_path, built_lib):
     j.postprocess()
     j.write("bed", str(out))
     assert out.read_bytes() == j.render("bed")
+
+
+def test_bench_launches_n_ranks_without_a_launcher(tmp_path):
+    """`bench.py --gpus N` with no WORLD_SIZE starts N rank processes with the
+    launcher environment, each rank runs the body (here: a host-transport
+    all-reduce through bwtmi.comm), and a failing rank makes the parent stop
+    the others and return non-zero instead of hanging."""
+    import importlib.util
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.abspath(os.path.join(here, ".."))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    script = tmp_path / "rank.py"
+    script.write_text(
+        "import os, sys\n"
+        f"sys.path[:0] = [{repo!r}, {os.path.join(repo, 'bwt-algorithm_amd')!r}]\n"
+        "import numpy as np\n"
+        "from bwtmi import comm\n"
+        "r, w, l = comm.env_rank()\n"
+        "assert os.environ['LOCAL_WORLD_SIZE'] == str(w) and l == r\n"
+        "if sys.argv[1] == 'fail' and r == 1:\n"
+        "    sys.exit(3)\n"
+        "c = comm.get('host')\n"
+        "tot = c.allreduce(np.array([r + 1, -r], dtype=np.int64))\n"
+        "mx = c.allreduce(np.array([-5 - r], dtype=np.int64), comm.MAX)\n"
+        f"open(os.path.join({str(tmp_path)!r}, f'r{{r}}.txt'), 'w').write(f'{{w}} {{tot[0]}} {{tot[1]}} {{mx[0]}}')\n"
+        "comm.close()\n")
+    env_before = os.environ.pop("WORLD_SIZE", None)
+    try:
+        assert bench.launch_ranks(3, ["ok"], script=str(script)) == 0
+        for r in range(3):
+            assert (tmp_path / f"r{r}.txt").read_text() == "3 6 -3 -5"
+        t0 = __import__("time").time()
+        assert bench.launch_ranks(3, ["fail"], script=str(script)) == 3
+        assert __import__("time").time() - t0 < 60
+    finally:
+        if env_before is not None:
+            os.environ["WORLD_SIZE"] = env_before
