@@ -94,6 +94,12 @@ def _entropy(s: str) -> float:
     return float(e)
 
 
+# bwtmi_hit as a numpy record (same layout as the ctypes Hit)
+_HIT_DTYPE = np.dtype([("start", "<i8"), ("end", "<i8"), ("unit_len", "<i4"), ("prim_len", "<i4"),
+                       ("copies", "<i8")])
+assert _HIT_DTYPE.itemsize == C.sizeof(Hit)
+
+
 class Job:
     """Owner of one native bwtmi_job (contigs, raw hits, final records)."""
 
@@ -204,10 +210,10 @@ class Job:
     def add_hits(self, cid: int, hits: np.ndarray) -> None:
         """hits: int64[k,5] rows (start, end, unit_len, prim_len, copies)."""
         hits = np.asarray(hits, dtype=np.int64).reshape(-1, 5)
-        arr = (Hit * max(len(hits), 1))()
-        for i, (s, e, L, p, c) in enumerate(hits.tolist()):
-            arr[i] = Hit(s, e, L, p, c)
-        check(lib().bwtmi_job_add_hits(self.h, cid, arr, len(hits)))
+        arr = np.zeros(max(len(hits), 1), dtype=_HIT_DTYPE)
+        for k, name in enumerate(_HIT_DTYPE.names):
+            arr[name][:len(hits)] = hits[:, k]
+        check(lib().bwtmi_job_add_hits(self.h, cid, arr.ctypes.data_as(C.c_void_p), len(hits)))
 
     def raw_count(self) -> int:
         return lib().bwtmi_job_raw_count(self.h)

@@ -20,14 +20,15 @@ from .records import TandemRepeat
 
 
 def strict_scan_hits(text_arr: np.ndarray, min_unit: int, max_unit: int, min_copies: int,
-                     device: Optional[int] = None) -> np.ndarray:
-    """Device strict scan -> int64[k, 5] rows (start, end, unit_len, prim_len, copies)."""
+                     device: Optional[int] = None, max_mismatch: int = 0) -> np.ndarray:
+    """Device strict scan -> int64[k, 5] rows (start, end, unit_len, prim_len, copies);
+    max_mismatch > 0 takes the Hamming-tolerant adjacency (bwt.py:1929-1944)."""
     t = np.ascontiguousarray(text_arr, dtype=np.uint8)
     buf = t if t.size else np.zeros(1, dtype=np.uint8)
     out = C.POINTER(Hit)()
     n = C.c_int64()
     check(lib().bwtmi_strict_scan(_lib.ctx(device), buf.ctypes.data_as(C.c_void_p), t.size, min_unit,
-                                  max_unit, 0, min_copies, C.byref(out), C.byref(n)))
+                                  max_unit, max_mismatch, min_copies, C.byref(out), C.byref(n)))
     try:
         if n.value == 0:
             return np.zeros((0, 5), dtype=np.int64)
@@ -86,11 +87,8 @@ class Tier2LCPFinder:
                                       max_unit_len: int = 120, max_mismatch: int = 2,
                                       min_copies: int = 3) -> List[TandemRepeat]:
         """bwt.py:1891-2001 on the device (records built as bwt.py:1952-1993)."""
-        if max_mismatch != 0:
-            raise NotImplementedError("strict scan with max_mismatch > 0 is not built yet "
-                                      "(the CLI path uses max_mismatch=0, bwt.py:3105)")
         t = self.bwt.text_arr
-        hits = strict_scan_hits(t, min_unit_len, max_unit_len, min_copies)
+        hits = strict_scan_hits(t, min_unit_len, max_unit_len, min_copies, max_mismatch=max_mismatch)
         out = []
         for s, e, L, p, c in hits.tolist():
             motif = bytes(t[s:s + p]).decode("ascii", errors="replace")

@@ -316,7 +316,7 @@ int bwtmi_strict_scan(bwtmi_ctx *ctx, const uint8_t *seq, int64_t n, int32_t min
                       int32_t max_mismatch, int32_t min_copies, bwtmi_hit **hits, int64_t *nhits) {
     return guard([&] {
         CHECK_ARG(ctx && hits && nhits && (seq || n == 0) && n >= 0, "bad argument");
-        CHECK_ARG(max_mismatch == 0, "only max_mismatch == 0 (the CLI path) is implemented on the device");
+        CHECK_ARG(max_mismatch >= 0, "max_mismatch must be >= 0");
         *hits = nullptr;
         *nhits = 0;
         if (n > 0 && seq[n - 1] == '$') --n;   // bwt.py:1915-1916
@@ -324,7 +324,11 @@ int bwtmi_strict_scan(bwtmi_ctx *ctx, const uint8_t *seq, int64_t n, int32_t min
         use(c);
         upload_text(c, c.slot[S_TEXT], seq, n);
         ScanResult r;
-        strict_scan_device(c, c.slot[S_TEXT].as<uint8_t>(), n, min_unit, max_unit, min_copies, r);
+        if (max_mismatch > 0)   // Hamming-tolerant adjacency (library calls)
+            strict_scan_mm_device(c, c.slot[S_TEXT].as<uint8_t>(), n, min_unit, max_unit, max_mismatch, min_copies,
+                                  r.hits);
+        else
+            strict_scan_device(c, c.slot[S_TEXT].as<uint8_t>(), n, min_unit, max_unit, min_copies, r);
         *nhits = (int64_t)r.hits.size();
         auto *out = (bwtmi_hit *)std::malloc(std::max<size_t>(1, r.hits.size()) * sizeof(bwtmi_hit));
         if (!out) fail(BWTMI_E_NOMEM, "malloc");

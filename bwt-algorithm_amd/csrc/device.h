@@ -257,6 +257,9 @@ struct ScanResult {
 // device (nested.hip) and return only the survivors, in that order.
 void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
                         int32_t min_copies, ScanResult &out, bool screen = false);
+// max_mismatch > 0: hits in emission order (host vector)
+void strict_scan_mm_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
+                           int32_t max_mismatch, int32_t min_copies, HitVec &hits);
 
 // ----- nested suppression / sort / dedup of one contig's strict hits (nested.hip)
 void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
@@ -264,7 +267,8 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
 
 // ----- suffix array + BWT of ACGT* '$' texts (sa_dna.hip)
 bool sa_dna_eligible(uint8_t last, int64_t n, const int64_t *totals);
-bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT);
+// also writes the sampled SA (bwt.py:328-333): sampled[j] = SA[j * sample] for j < ceil(n / sample)
+bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, int32_t *sampled, int32_t sample);
 
 // ----- index (index.hip)
 // true when [p, p+n) lies in a host block of mem.h that is (now) registered

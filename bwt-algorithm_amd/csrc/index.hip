@@ -201,6 +201,40 @@ __global__ __launch_bounds__(256) void k_occ_blocks(const uint8_t *__restrict__ 
     }
 }
 
+// The same counts with G = blk / 16 lanes per block (blk a power of two in
+// [16, 1024]): lane j of a group loads bytes [16j, 16j + 16) of its block, so a
+// wave's loads are 64 consecutive 16-byte pieces (1 KB, coalesced) instead of
+// 64 pieces 128 B apart; the group's counts meet by G-lane shuffles and the
+// group's first lane writes them.  SWAR compares as above.
+template <int G>
+__global__ __launch_bounds__(256) void k_occ_groups(const uint8_t *__restrict__ bwt, int64_t n, int64_t nblk,
+                                                    const uint8_t *__restrict__ present, int sigma,
+                                                    uint32_t *__restrict__ cnt /* [sigma][nblk+1] */) {
+    constexpr int kMaxSig = 16;
+    const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t b = gt / G;            // every lane of a group has the same b
+    const int64_t i = gt * 16;           // = b * blk + 16 * (lane in group)
+    uint64_t w0 = 0, w1 = 0, m0 = 0, m1 = 0;
+    if (b < nblk && i < n) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(bwt + i);
+        w0 = ((uint64_t)v.y << 32) | v.x;
+        w1 = ((uint64_t)v.w << 32) | v.z;
+        const int64_t left = n - i;   // bytes past n must not count
+        m0 = left >= 8 ? ~0ull : (~0ull >> (64 - 8 * left));
+        m1 = left >= 16 ? ~0ull : (left <= 8 ? 0ull : (~0ull >> (64 - 8 * (left - 8))));
+    }
+    const int sg = sigma < kMaxSig ? sigma : kMaxSig;
+    for (int c = 0; c < sg; ++c) {
+        const uint64_t pat = 0x0101010101010101ull * present[c];
+        const uint64_t y0 = (w0 ^ pat) | (~m0 & 0x0101010101010101ull);
+        const uint64_t y1 = (w1 ^ pat) | (~m1 & 0x0101010101010101ull);
+        uint32_t s = zero_bytes(y0) + zero_bytes(y1);
+#pragma unroll
+        for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        if (b < nblk && (gt & (G - 1)) == 0) cnt[(int64_t)c * (nblk + 1) + b] = s;
+    }
+}
+
 __global__ void k_sample(const uint32_t *__restrict__ sa, int64_t n, int32_t s, int32_t *__restrict__ out, int64_t m) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
@@ -593,6 +627,7 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     }
     ix->sigma = sigma;
     ix->sa.ensure((size_t)std::max<int64_t>(n, 1) * 4);
+    ix->occ_len = ix->sampled_len = 0;
     if (n == 0) return ix;
     ix->bwt.ensure((size_t)n + 128);
     HIPCHECK(hipMemsetAsync(ix->bwt.p, 0, (size_t)n + 128, st));
@@ -600,8 +635,11 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     HIPCHECK(hipMemcpyAsync(&last, T + n - 1, 1, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     // ACGT* '$' (every CLI contig): string sort over 2-bit words (sa_dna.hip)
+    ix->sampled_len = (n + sa_sample - 1) / sa_sample;
+    ix->sampled.ensure((size_t)ix->sampled_len * 4 + 4);
     const bool dna = sa_dna_eligible(last, n, ix->totals) &&
-                     sa_dna_device(c, T, n, ix->sa.as<uint32_t>(), ix->bwt.as<uint8_t>());
+                     sa_dna_device(c, T, n, ix->sa.as<uint32_t>(), ix->bwt.as<uint8_t>(), ix->sampled.as<int32_t>(),
+                                   sa_sample);
     if (!dna) sa_doubling(c, ix, T, n, sigma, code);
     // scratch of the Occ / k-mer / packed-rank stages
     c.slot[S_IDX0].ensure((size_t)n * 8);
@@ -619,16 +657,35 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     ix->occ.ensure((size_t)sigma * (nblk + 1) * 4);
     HIPCHECK(hipMemsetAsync(ix->occ.p, 0, (size_t)sigma * (nblk + 1) * 4, st));
     HIPCHECK(hipMemcpyAsync(c.slot[S_MISC3].p, present, 256, hipMemcpyHostToDevice, st));
-    KLAUNCH("occ_blocks", (double)n + (double)sigma * (double)(nblk + 1) * 4.0, k_occ_blocks, dim3(blocks(nblk)), dim3(256), 0, st, ix->bwt.as<uint8_t>(), n, nblk,
-                       occ_sample, c.slot[S_MISC3].as<uint8_t>(), sigma, ix->occ.as<uint32_t>());
+    {
+        const double ob = (double)n + (double)sigma * (double)(nblk + 1) * 4.0;   // BWT read + counts written
+        const uint8_t *pres = c.slot[S_MISC3].as<uint8_t>();
+        uint32_t *occ = ix->occ.as<uint32_t>();
+        const uint8_t *B = ix->bwt.as<uint8_t>();
+        const bool pow2 = occ_sample >= 16 && occ_sample <= 1024 && (occ_sample & (occ_sample - 1)) == 0;
+        const unsigned gl = blocks(nblk * (occ_sample / 16));   // one lane per 16 bytes
+        if (pow2 && sigma <= 16) {
+            switch (occ_sample) {
+                case 16: KLAUNCH("occ_blocks", ob, k_occ_groups<1>, dim3(gl), dim3(256), 0, st, B, n, nblk, pres, sigma, occ); break;
+                case 32: KLAUNCH("occ_blocks", ob, k_occ_groups<2>, dim3(gl), dim3(256), 0, st, B, n, nblk, pres, sigma, occ); break;
+                case 64: KLAUNCH("occ_blocks", ob, k_occ_groups<4>, dim3(gl), dim3(256), 0, st, B, n, nblk, pres, sigma, occ); break;
+                case 128: KLAUNCH("occ_blocks", ob, k_occ_groups<8>, dim3(gl), dim3(256), 0, st, B, n, nblk, pres, sigma, occ); break;
+                case 256: KLAUNCH("occ_blocks", ob, k_occ_groups<16>, dim3(gl), dim3(256), 0, st, B, n, nblk, pres, sigma, occ); break;
+                case 512: KLAUNCH("occ_blocks", ob, k_occ_groups<32>, dim3(gl), dim3(256), 0, st, B, n, nblk, pres, sigma, occ); break;
+                default: KLAUNCH("occ_blocks", ob, k_occ_groups<64>, dim3(gl), dim3(256), 0, st, B, n, nblk, pres, sigma, occ); break;
+            }
+        } else {   // other sample rates / alphabets: a thread per block
+            KLAUNCH("occ_blocks", ob, k_occ_blocks, dim3(blocks(nblk)), dim3(256), 0, st, B, n, nblk, occ_sample, pres,
+                    sigma, occ);
+        }
+    }
     for (int cc = 0; cc < sigma; ++cc) {
         uint32_t *row = ix->occ.as<uint32_t>() + (int64_t)cc * (nblk + 1);
         exclusive_scan<uint32_t>(c, row, row, nblk + 1);
     }
-    ix->sampled_len = (n + sa_sample - 1) / sa_sample;
-    ix->sampled.ensure((size_t)ix->sampled_len * 4 + 4);
-    KLAUNCH("k_sample", 0.0, k_sample, dim3(blocks(ix->sampled_len)), dim3(256), 0, st, SA, n, sa_sample,
-                       ix->sampled.as<int32_t>(), ix->sampled_len);
+    if (!dna)   // the DNA sort wrote the samples in its final pass
+        KLAUNCH("k_sample", 0.0, k_sample, dim3(blocks(ix->sampled_len)), dim3(256), 0, st, SA, n, sa_sample,
+                ix->sampled.as<int32_t>(), ix->sampled_len);
 
     // ------------------------------------------------ packed rank (ACGT* '$')
     ix->has_fm2 = false;
@@ -780,14 +837,14 @@ const int32_t *index_lcp_device(Ctx &c, DeviceIndex *ix) {
     uint32_t *isa = c.slot[S_MISC0].as<uint32_t>();
     int32_t *lcp = c.slot[S_MISC1].as<int32_t>();
     HIPCHECK(hipMemsetAsync(lcp, 0, (size_t)n * 4, st));
-    KLAUNCH("k_isa", 0.0, k_isa, dim3(blocks(n)), dim3(256), 0, st, ix->sa.as<uint32_t>(), n, isa);
+    KLAUNCH("k_isa", 8.0 * (double)n, k_isa, dim3(blocks(n)), dim3(256), 0, st, ix->sa.as<uint32_t>(), n, isa);
     uint32_t sa0 = 0;
     HIPCHECK(hipMemcpyAsync(&sa0, ix->sa.p, 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     if ((int64_t)sa0 == n - 1) {
         const int64_t chunk = 64;
         const int64_t nch = (n + chunk - 1) / chunk;
-        KLAUNCH("k_kasai", 0.0, k_kasai, dim3(blocks(nch)), dim3(256), 0, st, ix->text.as<uint8_t>(),
+        KLAUNCH("k_kasai", 13.0 * (double)n, k_kasai, dim3(blocks(nch)), dim3(256), 0, st, ix->text.as<uint8_t>(),
                            ix->sa.as<uint32_t>(), isa, n, chunk, lcp);
     } else {
         // the smallest suffix is not the last one (no unique final sentinel):

@@ -40,7 +40,6 @@ namespace {
 
 constexpr int kB = 256;
 constexpr int kMaxUnit = 9;   // enumerate_motifs range ends at 9 (bwt.py:2052)
-constexpr int kD = 6;         // distinct symbols tracked per column before a host recompute
 
 inline unsigned blocks(int64_t n) { return (unsigned)((n + kB - 1) / kB); }
 
@@ -127,99 +126,138 @@ __device__ __host__ inline int64_t max_mm_for_array(int64_t L, int64_t copies) {
     return max((int64_t)1, (int64_t)ceil(0.08 * (double)total));
 }
 
-struct ColHist {
-    uint8_t sym[kMaxUnit][kD];
-    int32_t cnt[kMaxUnit][kD];
-    uint8_t nd[kMaxUnit];
+// _extend_tandem_fm(text, cs, text[cs:cs+L], L) for every cs and L = 1..Lmax,
+// with every column's symbol counts in registers: 5 bins
+// per column in byte order (A C G N T, so a strict > scan over the bins keeps
+// the smallest byte among the most frequent -- np.unique + argmax), and the
+// copy's mismatches / transversions from the counts alone: a column with
+// majority count b adds tc - b mismatches and the counts of the bins that are
+// transversions of its consensus (count_transversions_array: A<->G and C<->T
+// are transitions, every other pair of distinct symbols in 65..84 -- N
+// included -- is not).  A copy costs O(L), never a re-vote of earlier copies,
+// and nothing spills to scratch.  Any other byte (e.g. the final '$') sends
+// the entry to the host's scalar extension.
+//
+// Output per (start cs, unit L), entry q = (L - 1) n + cs: one 32-bit word =
+// copies added on the left | copies added on the right << 16; 0xffffffff =
+// no extension (cs + L > n); a count past 0xfffe (long homopolymers) or an
+// unbinned symbol writes 0xfffffffe and appends (q, left, right, unbinned) to
+// a side list.  The host reads 4 bytes per entry instead of 13.
+constexpr uint32_t kExtNone = 0xffffffffu, kExtSide = 0xfffffffeu;
+struct ExtSide {
+    int64_t q;
+    uint32_t left, right;
+    uint32_t unbinned, pad;
 };
 
-__device__ inline bool hist_add(ColHist &h, const uint8_t *cp, int L, int32_t d) {
-    for (int p = 0; p < L; ++p) {
-        const uint8_t b = cp[p];
-        int k = 0;
-        while (k < h.nd[p] && h.sym[p][k] != b) ++k;
-        if (k == h.nd[p]) {
-            if (k == kD) return false;
-            h.sym[p][k] = b;
-            h.cnt[p][k] = 0;
-            ++h.nd[p];
-        }
-        h.cnt[p][k] += d;
-    }
-    return true;
-}
-
-// total mismatches and transversions of every copy against the majority consensus
-__device__ inline void hist_eval(const ColHist &h, int L, int64_t tc, int64_t &mm, int64_t &tv) {
-    mm = 0;
-    tv = 0;
-    for (int p = 0; p < L; ++p) {
-        int32_t best = 0;
-        uint8_t cons = 0;
-        for (int k = 0; k < h.nd[p]; ++k) {
-            const int32_t v = h.cnt[p][k];
-            if (v > best || (v == best && v > 0 && h.sym[p][k] < cons)) { best = v; cons = h.sym[p][k]; }
-        }
-        mm += tc - best;
-        for (int k = 0; k < h.nd[p]; ++k)
-            if (h.cnt[p][k] > 0 && transversion(h.sym[p][k], cons)) tv += h.cnt[p][k];
+__device__ __forceinline__ int ext_bin(uint8_t b) {
+    switch (b) {
+        case 'A': return 0;
+        case 'C': return 1;
+        case 'G': return 2;
+        case 'N': return 3;
+        case 'T': return 4;
+        default: return -1;
     }
 }
 
-__device__ inline bool homopolymer(const uint8_t *cp, int L) {
-    for (int p = 1; p < L; ++p)
-        if (cp[p] != cp[0]) return false;
-    return true;
-}
-
-// _extend_tandem_fm(text, cs, text[cs:cs+L], L) for all cs and L = 1..Lmax
-__global__ void k_extend(const uint8_t *__restrict__ t, int64_t n, int Lmax, int32_t *__restrict__ es,
-                         int32_t *__restrict__ ee, int32_t *__restrict__ ec, uint8_t *__restrict__ ovf) {
-    const int64_t tid = (int64_t)blockIdx.x * kB + threadIdx.x;
+__global__ __launch_bounds__(256) void k_extend_cols(const uint8_t *__restrict__ t, int64_t n, int Lmax,
+                                                     uint32_t *__restrict__ word, ExtSide *__restrict__ side,
+                                                     unsigned long long *__restrict__ nside, int64_t side_cap) {
+    // bins of the transversions of consensus bin x (A C G N T)
+    constexpr uint32_t kTv[5] = {0x1au, 0x0du, 0x1au, 0x17u, 0x0du};
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (tid >= (int64_t)Lmax * n) return;
     const int L = (int)(tid / n) + 1;
-    const int64_t cs = tid % n;
-    ovf[tid] = 0;
+    const int64_t cs = tid - (int64_t)(L - 1) * n;
     if (cs + L > n) {
-        es[tid] = -1;
+        word[tid] = kExtNone;
         return;
     }
-    ColHist h;
-    for (int p = 0; p < L; ++p) h.nd[p] = 0;
-    int64_t start = cs, end = cs + L, copies = 1;
-    bool ok = hist_add(h, t + cs, L, 1);
-    while (ok && end + L <= n) {
-        const uint8_t *nx = t + end;
-        if (L > 1 && homopolymer(nx, L)) break;
-        if (!(ok = hist_add(h, nx, L, 1))) break;
-        int64_t mm, tv;
-        hist_eval(h, L, copies + 1, mm, tv);
-        if (mm <= max_mm_for_array(L, copies + 1) && tv == 0) {
+    uint32_t cnt[kMaxUnit][5];
+    bool ok = true;
+#pragma unroll
+    for (int p = 0; p < kMaxUnit; ++p) {
+#pragma unroll
+        for (int b = 0; b < 5; ++b) cnt[p][b] = 0;
+        if (p < L) {
+            const int b = ext_bin(t[cs + p]);
+            if (b < 0) ok = false;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) cnt[p][q] = q == b ? 1u : 0u;   // no dynamic index: registers only
+        }
+    }
+    // try copy at `at`: add it, evaluate, keep or take it back
+    auto try_copy = [&](int64_t at, uint32_t tc) -> bool {
+        int bins[kMaxUnit];
+        bool homo = L > 1;
+        const uint8_t c0 = t[at];
+#pragma unroll
+        for (int p = 0; p < kMaxUnit; ++p) {
+            bins[p] = 0;
+            if (p < L) {
+                const uint8_t c = t[at + p];
+                homo = homo && c == c0;
+                bins[p] = ext_bin(c);
+            }
+        }
+        if (homo) return false;   // the next copy is a homopolymer
+        int64_t mm = 0, tv = 0;
+#pragma unroll
+        for (int p = 0; p < kMaxUnit; ++p) {
+            if (p < L) {
+                if (bins[p] < 0) {
+                    ok = false;
+                    return false;
+                }
+#pragma unroll
+                for (int b = 0; b < 5; ++b) cnt[p][b] += b == bins[p] ? 1u : 0u;
+                uint32_t best = 0;
+                int cb = 0;
+#pragma unroll
+                for (int b = 0; b < 5; ++b)
+                    if (cnt[p][b] > best) {
+                        best = cnt[p][b];
+                        cb = b;
+                    }
+                mm += (int64_t)(tc - best);
+#pragma unroll
+                for (int b = 0; b < 5; ++b)
+                    if ((kTv[cb] >> b) & 1u) tv += cnt[p][b];
+            }
+        }
+        if (mm <= max_mm_for_array(L, tc) && tv == 0) return true;
+#pragma unroll
+        for (int p = 0; p < kMaxUnit; ++p)
+            if (p < L) {
+#pragma unroll
+                for (int b = 0; b < 5; ++b) cnt[p][b] -= b == bins[p] ? 1u : 0u;
+            }
+        return false;
+    };
+    uint32_t copies = 1, right = 0, left = 0;
+    int64_t start = cs, end = cs + L;
+    if (ok) {
+        while (end + L <= n && try_copy(end, copies + 1)) {
             ++copies;
+            ++right;
             end += L;
-        } else {
-            hist_add(h, nx, L, -1);
-            break;
         }
     }
-    while (ok && start - L >= 0) {
-        const uint8_t *pv = t + start - L;
-        if (L > 1 && homopolymer(pv, L)) break;
-        if (!(ok = hist_add(h, pv, L, 1))) break;
-        int64_t mm, tv;
-        hist_eval(h, L, copies + 1, mm, tv);
-        if (mm <= max_mm_for_array(L, copies + 1) && tv == 0) {
+    if (ok) {
+        while (start - L >= 0 && try_copy(start - L, copies + 1)) {
             ++copies;
+            ++left;
             start -= L;
-        } else {
-            hist_add(h, pv, L, -1);
-            break;
         }
     }
-    es[tid] = (int32_t)start;
-    ee[tid] = (int32_t)end;
-    ec[tid] = (int32_t)copies;
-    ovf[tid] = ok ? 0 : 1;
+    if (ok && left < 0xffffu && right < 0xffffu) {
+        word[tid] = left | (right << 16);
+        return;
+    }
+    word[tid] = kExtSide;
+    const unsigned long long k = atomicAdd(nside, 1ull);
+    if ((int64_t)k < side_cap) side[k] = ExtSide{tid, left, right, ok ? 0u : 1u, 0u};
 }
 
 // -------------------------------------------------------------- Tier 1
@@ -606,7 +644,7 @@ void lcp_plateaus_device(Ctx &c, DeviceIndex *ix, const LibParams &p, std::vecto
     c.slot[S_IDX4].ensure((size_t)(n + 1) * 4);
     uint32_t *inrun = c.slot[S_IDX1].as<uint32_t>(), *head = c.slot[S_IDX2].as<uint32_t>();
     uint32_t *hscan = c.slot[S_IDX3].as<uint32_t>(), *cpos = c.slot[S_IDX4].as<uint32_t>();
-    KLAUNCH("k_plateau_flags", 0.0, k_plateau_flags, dim3(blocks(n)), dim3(kB), 0, st, lcp, n, (int32_t)thr, inrun, head);
+    KLAUNCH("k_plateau_flags", 12.0 * (double)n, k_plateau_flags, dim3(blocks(n)), dim3(kB), 0, st, lcp, n, (int32_t)thr, inrun, head);
     HIPCHECK(hipMemsetAsync(inrun + n, 0, 4, st));
     HIPCHECK(hipMemsetAsync(head + n, 0, 4, st));
     exclusive_scan<uint32_t>(c, head, hscan, n + 1);
@@ -659,7 +697,7 @@ void tier1_device(Ctx &c, const uint8_t *d_text, const uint8_t *t, int64_t n, in
     HIPCHECK(hipMemsetAsync(seen, 0, (size_t)n, st));
     std::vector<int64_t> cand, ranges;
     for (int L = std::min(max_motif_length, 9); L >= 1; --L) {   // longest unit first (bwt.py:1451)
-        KLAUNCH("k_t1_flags", 0.0, k_t1_flags, dim3(blocks(n)), dim3(kB), 0, st, d_text, n, L, seen, flag);
+        KLAUNCH("k_t1_flags", 6.0 * (double)n, k_t1_flags, dim3(blocks(n)), dim3(kB), 0, st, d_text, n, L, seen, flag);
         HIPCHECK(hipMemsetAsync(flag + n, 0, 4, st));
         exclusive_scan<uint32_t>(c, flag, pos, n + 1);
         uint32_t m = 0;
@@ -727,32 +765,61 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
     index_get_text(c, ix, text.data());
     const uint8_t *t = text.data();
 
-    // extension table for every start and unit length 1..9
+    // extension table for every start and unit length 1..9 (k_extend_cols)
     const int Lmax = kMaxUnit;
     const int64_t tot = (int64_t)Lmax * n;
     c.slot[S_IDX0].ensure((size_t)tot * 4);
-    c.slot[S_IDX1].ensure((size_t)tot * 4);
-    c.slot[S_IDX2].ensure((size_t)tot * 4);
-    c.slot[S_IDX3].ensure((size_t)tot);
-    KLAUNCH("k_extend", 0.0, k_extend, dim3(blocks(tot)), dim3(kB), 0, st, index_text_device(ix), n, Lmax,
-                       c.slot[S_IDX0].as<int32_t>(), c.slot[S_IDX1].as<int32_t>(), c.slot[S_IDX2].as<int32_t>(),
-                       c.slot[S_IDX3].as<uint8_t>());
-    HIPCHECK(hipGetLastError());
-    std::vector<int32_t> es((size_t)tot), ee((size_t)tot), ec((size_t)tot);
-    std::vector<uint8_t> ovf((size_t)tot);
-    HIPCHECK(hipMemcpyAsync(es.data(), c.slot[S_IDX0].p, (size_t)tot * 4, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipMemcpyAsync(ee.data(), c.slot[S_IDX1].p, (size_t)tot * 4, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipMemcpyAsync(ec.data(), c.slot[S_IDX2].p, (size_t)tot * 4, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipMemcpyAsync(ovf.data(), c.slot[S_IDX3].p, (size_t)tot, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
-    for (int64_t q = 0; q < tot; ++q)
-        if (ovf[(size_t)q]) {
-            int64_t s, e, cc;
-            extend_host(t, n, q % n, q / n + 1, s, e, cc);
-            es[(size_t)q] = (int32_t)s;
-            ee[(size_t)q] = (int32_t)e;
-            ec[(size_t)q] = (int32_t)cc;
+    c.slot[S_COUNTS].ensure(256 * 8);
+    std::vector<uint32_t> ext_word((size_t)tot);
+    std::unordered_map<int64_t, std::array<int64_t, 3>> ext_side;   // q -> (start, end, copies)
+    for (int64_t cap = 1 << 16;;) {
+        c.slot[S_IDX1].ensure((size_t)cap * sizeof(ExtSide));
+        HIPCHECK(hipMemsetAsync(c.slot[S_COUNTS].p, 0, 8, st));
+        KLAUNCH("k_extend", 9.0 * (double)n + 4.0 * (double)tot, k_extend_cols, dim3(blocks(tot)), dim3(kB), 0, st,
+                index_text_device(ix), n, Lmax, c.slot[S_IDX0].as<uint32_t>(), c.slot[S_IDX1].as<ExtSide>(),
+                c.slot[S_COUNTS].as<unsigned long long>(), cap);
+        HIPCHECK(hipGetLastError());
+        unsigned long long ns = 0;
+        HIPCHECK(hipMemcpyAsync(&ns, c.slot[S_COUNTS].p, 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        if ((int64_t)ns > cap) {   // the side list overflowed: again with room for all of it
+            cap = (int64_t)ns;
+            continue;
         }
+        std::vector<ExtSide> side((size_t)ns);
+        HIPCHECK(hipMemcpyAsync(ext_word.data(), c.slot[S_IDX0].p, (size_t)tot * 4, hipMemcpyDeviceToHost, st));
+        if (ns) HIPCHECK(hipMemcpyAsync(side.data(), c.slot[S_IDX1].p, (size_t)ns * sizeof(ExtSide),
+                                        hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        for (const ExtSide &x : side) {
+            const int64_t L = x.q / n + 1, cs = x.q % n;
+            int64_t s0, e0, c0;
+            if (x.unbinned) {   // a symbol outside A C G N T: the scalar extension
+                extend_host(t, n, cs, L, s0, e0, c0);
+            } else {
+                s0 = cs - (int64_t)x.left * L;
+                e0 = cs + L + (int64_t)x.right * L;
+                c0 = 1 + (int64_t)x.left + (int64_t)x.right;
+            }
+            ext_side[x.q] = {s0, e0, c0};
+        }
+        break;
+    }
+    // (start, end, copies) of entry q (cs + L <= n)
+    auto ext_of = [&](int64_t q, int64_t L, int64_t cs, int64_t &s0, int64_t &e0, int64_t &c0) {
+        const uint32_t w = ext_word[(size_t)q];
+        if (w == kExtSide) {
+            const auto &v = ext_side.at(q);
+            s0 = v[0];
+            e0 = v[1];
+            c0 = v[2];
+            return;
+        }
+        const int64_t lf = w & 0xffffu, rt = w >> 16;
+        s0 = cs - lf * L;
+        e0 = cs + L + rt * L;
+        c0 = 1 + lf + rt;
+    };
 
     // seeds: k-mer table (with the reference's short-k lookup, bwt.py:173-193) or FM locate
     std::vector<int64_t> koff;
@@ -836,8 +903,9 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
                 for (int64_t sh = 0; sh < shifts; ++sh) {
                     const int64_t cs = seed - sh;
                     if (cs < 0 || cs + motif_len > n || seen[(size_t)cs]) continue;
-                    const size_t q = (size_t)((motif_len - 1) * n + cs);
-                    const int64_t s = es[q], e = ee[q], cc = ec[q];
+                    const int64_t q = (motif_len - 1) * n + cs;
+                    int64_t s, e, cc;
+                    ext_of(q, motif_len, cs, s, e, cc);
                     if (!(s <= seed && seed < e)) continue;
                     if (cc > bc || (cc == bc && (bs < 0 || s < bs))) { bs = s; be = e; bc = cc; }
                 }

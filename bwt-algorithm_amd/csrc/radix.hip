@@ -114,6 +114,53 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KT *__restrict__ keys, ui
     counts[(int64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
+// The same counts, read as 16-byte vectors (every key of a full tile is loaded
+// before the first LDS atomic, so the loads are all in flight together) and
+// counted into one histogram per wave (no atomics between waves on one bin);
+// the tile's last partial piece takes the scalar path.
+template <int ITEMS, class KT>
+__global__ __launch_bounds__(kBlock) void k_hist_vec(const KT *__restrict__ keys, uint32_t *__restrict__ counts,
+                                                     int64_t n, int shift, int64_t ntiles) {
+    constexpr int VEC = 16 / sizeof(KT);
+    constexpr int NV = ITEMS / VEC;   // 16-byte loads per thread
+    static_assert(ITEMS % VEC == 0, "whole vectors per thread");
+    __shared__ uint32_t h[kWaves][256];
+    for (int i = threadIdx.x; i < kWaves * 256; i += kBlock) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const int wv = threadIdx.x >> 6;
+    const int64_t base = (int64_t)blockIdx.x * (kBlock * ITEMS);
+    if (base + kBlock * ITEMS <= n) {
+        uint4 v[NV];
+        const uint4 *src = reinterpret_cast<const uint4 *>(keys + base);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) v[i] = src[i * kBlock + threadIdx.x];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const KT *k = reinterpret_cast<const KT *>(&v[i]);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) atomicAdd(&h[wv][(k[e] >> shift) & 255u], 1u);
+        }
+    } else {
+        for (int64_t idx = base + threadIdx.x; idx < n; idx += kBlock) atomicAdd(&h[wv][(keys[idx] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) t += h[w][threadIdx.x];
+    counts[(int64_t)threadIdx.x * ntiles + blockIdx.x] = t;
+}
+
+template <int ITEMS, class KT>
+void launch_hist(Ctx &c, const KT *keys, uint32_t *cnt, int64_t n, int sh, int64_t ntiles) {
+    static const int vec = [] { const char *e = std::getenv("BWTMI_HIST_VEC"); return e ? std::atoi(e) : 1; }();
+    if (vec && ((uintptr_t)keys & 15) == 0)
+        KLAUNCH("radix_hist", (double)n * (double)sizeof(KT), (k_hist_vec<ITEMS, KT>), dim3((unsigned)ntiles),
+                dim3(kBlock), 0, c.stream, keys, cnt, n, sh, ntiles);
+    else
+        KLAUNCH("radix_hist", (double)n * (double)sizeof(KT), (k_hist<ITEMS, KT>), dim3((unsigned)ntiles),
+                dim3(kBlock), 0, c.stream, keys, cnt, n, sh, ntiles);
+}
+
 template <bool NT, class T>
 __device__ __forceinline__ void st(T *p, T v) {
     if constexpr (NT) __builtin_nontemporal_store(v, p);
@@ -267,8 +314,7 @@ void radix_sort_cfg(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
     int passes = 0;
     for (int sh = bit0; sh < bit1; sh += 8) {
         // read the keys once
-        KLAUNCH("radix_hist", (double)n * (double)sizeof(KT), (k_hist<kT / kBlock, KT>), dim3((unsigned)ntiles),
-                dim3(kBlock), 0, c.stream, ka, cnt, n, sh, ntiles);
+        launch_hist<kT / kBlock, KT>(c, ka, cnt, n, sh, ntiles);
         exclusive_scan<uint32_t>(c, cnt, cnt, ntiles * 256);
         // read (key, value) once, write it once
         KLAUNCH(sizeof(KT) == 4 ? "radix_scatter_kv8" : sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16",
@@ -347,8 +393,7 @@ void radix_pass_k32(Ctx &c, const uint32_t *kin, const uint32_t *vin, uint32_t *
     const int64_t ntiles = (n + kT - 1) / kT;
     c.slot[S_SORT_HIST].ensure((size_t)ntiles * 256 * sizeof(uint32_t));
     uint32_t *cnt = c.slot[S_SORT_HIST].as<uint32_t>();
-    KLAUNCH("radix_hist", (double)n * 4.0, (k_hist<kT / kBlock, uint32_t>), dim3((unsigned)ntiles), dim3(kBlock), 0,
-            c.stream, kin, cnt, n, shift, ntiles);
+    launch_hist<kT / kBlock, uint32_t>(c, kin, cnt, n, shift, ntiles);
     exclusive_scan<uint32_t>(c, cnt, cnt, ntiles * 256);
     KLAUNCH("radix_partition_kv8", (double)n * 16.0, (k_scatter<uint32_t, uint32_t, BLOCK, ITEMS, false, true>),
             dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, kin, vin, kout, vout, cnt, n, shift, ntiles, 1);

@@ -275,7 +275,10 @@ __global__ __launch_bounds__(kB) void k_grp_apply(const uint32_t *__restrict__ k
 // orders the pairs by the position's top 8 bits, each workgroup's writes stay
 // in one 2^shift-position window that its XCD's L2 holds, so the scattered
 // 4-byte stores reach HBM as whole lines
+// NT: the (position, head) stream is read with nontemporal loads, so it does
+// not displace the window's partly written rank lines from the L2
 constexpr int kPutItems = 16;
+template <bool NT>
 __global__ __launch_bounds__(kB) void k_dna_rank_put(const uint32_t *__restrict__ pv, const uint32_t *__restrict__ hd,
                                                      int64_t n, int64_t ntiles, uint32_t *__restrict__ rank) {
     const int64_t base = xcd_tile(blockIdx.x, ntiles) * (kB * kPutItems) + threadIdx.x;
@@ -283,8 +286,13 @@ __global__ __launch_bounds__(kB) void k_dna_rank_put(const uint32_t *__restrict_
 #pragma unroll
     for (int i = 0; i < kPutItems; ++i) {
         const int64_t r = base + (int64_t)i * kB;
-        p[i] = r < n ? pv[r] : 0u;
-        h[i] = r < n ? hd[r] : 0u;
+        if (NT) {
+            p[i] = r < n ? __builtin_nontemporal_load(pv + r) : 0u;
+            h[i] = r < n ? __builtin_nontemporal_load(hd + r) : 0u;
+        } else {
+            p[i] = r < n ? pv[r] : 0u;
+            h[i] = r < n ? hd[r] : 0u;
+        }
     }
 #pragma unroll
     for (int i = 0; i < kPutItems; ++i)
@@ -718,11 +726,13 @@ __global__ __launch_bounds__(kB) void k_dna_refine_pos(const uint64_t *__restric
 }
 
 __global__ __launch_bounds__(kB) void k_dna_final(const uint32_t *__restrict__ vals, int64_t n, uint32_t *__restrict__ sa,
-                                                  uint8_t *__restrict__ bwt) {
+                                                  uint8_t *__restrict__ bwt, int32_t *__restrict__ sampled,
+                                                  int32_t sample) {
     const int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x;
     if (r >= n) return;
     const uint32_t v = vals[r];
     sa[r] = v & kPosMask;
+    if (r % sample == 0) sampled[r / sample] = (int32_t)(v & kPosMask);   // the SA row is already in hand
     const uint32_t c = v >> 29;
     bwt[r] = c == 4 ? (uint8_t)'$' : (uint8_t)"ACGT"[c];
 }
@@ -737,7 +747,7 @@ bool sa_dna_eligible(const uint8_t last, int64_t n, const int64_t *totals) {
 // SA (uint32[n]) and BWT (uint8[n]) of t[0, n) = ACGT* '$'; false when the
 // refinement needed more than kMaxRounds passes (the caller then runs the
 // general prefix doubling)
-bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT) {
+bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, int32_t *sampled, int32_t sample) {
     hipStream_t st = c.stream;
     const int64_t nw = (n + 31) / 32 + 2;
     c.slot[S_IDX0].ensure((size_t)n * 4 + 64);      // keys, then class lists
@@ -809,8 +819,8 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
     const int64_t nput = (n + kB * kPutItems - 1) / (kB * kPutItems);
     static const int rank0_direct = [] { const char *e = std::getenv("BWTMI_RANK0_DIRECT"); return e && *e == '1'; }();
     if (rank0_direct || n < (1 << 16)) {
-        KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put, dim3((unsigned)nput), dim3(kB), 0, st, vals, hd, n,
-                nput, rank);
+        KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put<false>, dim3((unsigned)nput), dim3(kB), 0, st, vals,
+                hd, n, nput, rank);
     } else {
         // through a position partition (the pass output in the sort's buffers)
         int bits = 0;
@@ -826,8 +836,13 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
         // 1.13-1.36 ms at full occupancy, 0.63 at 2 per CU, 0.55 at 1 per CU
         // (the direct scatter: 2.35)
         static const int put_lds = [] { const char *e = std::getenv("BWTMI_PUT_LDS"); return e ? std::atoi(e) : 128; }();
-        KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put, dim3((unsigned)nput), dim3(kB),
-                (size_t)put_lds * 1024, st, pv, ph, n, nput, rank);
+        static const int put_nt = [] { const char *e = std::getenv("BWTMI_PUT_NT"); return e ? std::atoi(e) : 1; }();
+        if (put_nt)
+            KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put<true>, dim3((unsigned)nput), dim3(kB),
+                    (size_t)put_lds * 1024, st, pv, ph, n, nput, rank);
+        else
+            KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put<false>, dim3((unsigned)nput), dim3(kB),
+                    (size_t)put_lds * 1024, st, pv, ph, n, nput, rank);
     }
     if (G) KLAUNCH("dna_short_fix", 0.0, k_dna_short_fix, dim3(1), dim3(1024), 0, st, vals, rank, gs, ge, G, n);
 
@@ -932,7 +947,8 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
         G = next;
         sl = nsl;
     }
-    KLAUNCH("dna_final", 9.0 * (double)n, k_dna_final, dim3(nblocks(n)), dim3(kB), 0, st, vals, n, SA, BWT);
+    KLAUNCH("dna_final", 9.0 * (double)n + 4.0 * (double)((n + sample - 1) / sample), k_dna_final, dim3(nblocks(n)),
+            dim3(kB), 0, st, vals, n, SA, BWT, sampled, sample);
     HIPCHECK(hipGetLastError());
     return true;
 }

@@ -328,6 +328,96 @@ __global__ void k_mc1(const uint8_t *__restrict__ t, int64_t n, int32_t lmin, in
     nper[row] = k;
 }
 
+// ------------------------------------------------ max_mismatch > 0
+// find_long_unit_repeats_strict with a Hamming tolerance (bwt.py:1929-1944):
+// blocks j and j + L "match" iff D_L(j) = #{x in [j, j + L): t[x] != t[x + L]}
+// <= m.  Row l (L = L0 - l) gets the bit P(j) = (j + 2L <= n and D_L(j) <= m)
+// for every j, each thread sliding the window over kMmSeg positions
+// (D_L(j + 1) = D_L(j) - [t[j] != t[j+L]] + [t[j+L] != t[j+2L]]).
+constexpr int kMmSeg = 1024;
+__global__ __launch_bounds__(256) void k_mm_pbits(const uint8_t *__restrict__ t, int64_t n, int32_t L0, int32_t m,
+                                                  int64_t nw, uint32_t *__restrict__ P) {
+    const int64_t L = L0 - (int64_t)blockIdx.y;
+    const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kMmSeg;
+    if (j0 >= n) return;
+    uint32_t *row = P + (int64_t)blockIdx.y * (nw + 1);
+    const int64_t jend = j0 + kMmSeg < n ? j0 + kMmSeg : n;
+    int64_t D = 0;
+    if (j0 + 2 * L <= n)
+        for (int64_t x = j0; x < j0 + L; ++x) D += t[x] != t[x + L];
+    uint32_t word = 0;
+    for (int64_t j = j0; j < jend; ++j) {
+        const bool p = j + 2 * L <= n && D <= m;
+        word |= (uint32_t)p << (j & 31);
+        if ((j & 31) == 31 || j == jend - 1) {
+            row[j >> 5] = word;
+            word = 0;
+        }
+        if (j + 2 * L < n) D += (int64_t)(t[j + L] != t[j + 2 * L]) - (int64_t)(t[j] != t[j + L]);
+    }
+}
+
+// The scan itself, one wave per unit length: i = the first position >= carry
+// with count >= mc, i.e. Q(i) = (i + L*mc <= n) and P(i), P(i+L), ...,
+// P(i+(mc-2)L) (64 Q words per step, ballot); count = 1 + the run of P along
+// i, i+L, ... (64 copies per step); hit [i, i + count*L); carry = its end.
+// Carry and count are wave-uniform scalars (readfirstlane / ballot), so the
+// loop exits together.  Row l writes (start, count) pairs at out + off[l].
+__device__ __forceinline__ uint32_t pword_at(const uint32_t *row, int64_t bit) {
+    const int64_t w = bit >> 5;
+    const int s = (int)(bit & 31);
+    const uint32_t lo = row[w];
+    return s ? (lo >> s) | (row[w + 1] << (32 - s)) : lo;
+}
+
+__global__ __launch_bounds__(64) void k_mm_walk(const uint32_t *__restrict__ P, int64_t n, int64_t nw, int32_t L0,
+                                                int32_t mc, const int64_t *__restrict__ off,
+                                                int64_t *__restrict__ out, int64_t *__restrict__ nper) {
+    const int64_t L = L0 - (int64_t)blockIdx.x;
+    const int lane = threadIdx.x;
+    const uint32_t *row = P + (int64_t)blockIdx.x * (nw + 1);
+    int64_t *dst = out + 2 * off[blockIdx.x];
+    const int64_t last = n - L * (int64_t)mc;   // the greatest i the loop visits (bwt.py:1923)
+    int64_t carry = 0, k = 0;
+    while (carry <= last) {
+        const int64_t w0 = carry >> 5;
+        const int64_t w = w0 + lane;
+        uint32_t q = 0;
+        if (w <= (last >> 5)) {
+            q = ~0u;
+            if (w == w0) q &= ~0u << (carry & 31);
+            if (w == (last >> 5)) q &= (uint32_t)(~0ull >> (63 - (last & 31))) ;
+            for (int c = 0; c + 1 < mc && q; ++c) q &= pword_at(row, (w << 5) + (int64_t)c * L);
+        }
+        const uint64_t bal = __ballot(q != 0);
+        if (!bal) {
+            carry = (w0 + 64) << 5;
+            continue;
+        }
+        const int f = __ffsll((unsigned long long)bal) - 1;
+        const uint32_t qf = (uint32_t)__builtin_amdgcn_readlane((int)q, f);
+        const int64_t i = ((w0 + f) << 5) + (__ffs(qf) - 1);
+        int64_t cnt = 1;
+        for (;;) {   // the run of P(i + cL) for c = cnt - 1, cnt, ...
+            const int64_t j = i + (cnt - 1 + lane) * L;
+            const bool p = j < n && ((row[j >> 5] >> (j & 31)) & 1u);
+            const uint64_t stop = __ballot(!p);
+            if (stop) {
+                cnt += __ffsll((unsigned long long)stop) - 1;
+                break;
+            }
+            cnt += 64;
+        }
+        if (lane == 0) {
+            dst[2 * k] = i;
+            dst[2 * k + 1] = cnt;
+        }
+        ++k;
+        carry = i + cnt * L;
+    }
+    if (lane == 0) nper[blockIdx.x] = k;
+}
+
 // ---------------------------------------------------------- resolution
 __global__ __launch_bounds__(256) void k_resolve(const uint64_t *__restrict__ keys, const uint64_t *__restrict__ vals,
                                                  int64_t nc, int32_t umax, int sb, int64_t mc,
@@ -520,6 +610,68 @@ void launch_runs(Ctx &c, const uint32_t *P, int64_t n, int32_t lmin, int32_t lma
 }
 
 }  // namespace
+
+// max_mismatch > 0 (library calls; the CLI passes 0, bwt.py:3105): hits in the
+// reference's emission order, prim_len / copies as bwt.py:1956-1961
+void strict_scan_mm_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
+                           int32_t max_mismatch, int32_t min_copies, HitVec &hits) {
+    hits.clear();
+    if (min_copies <= 0) fail(BWTMI_E_ARG, "min_copies must be positive");
+    const int64_t maxL = std::min<int64_t>(max_unit, n / min_copies);   // bwt.py:1920
+    if (n <= 0 || maxL < min_unit || maxL < 1) return;
+    const int64_t lmin = std::max<int32_t>(1, min_unit), lmax = maxL;
+    hipStream_t st = c.stream;
+    const int64_t nw = (n + 31) / 32;
+    // rows per batch: P bits (nw + 1 words per row) and the (start, count) slots
+    // of the row (at most n / (mc L) + 1 hits: a row's hits are disjoint)
+    const int64_t budget = int64_t{1} << 30;
+    std::vector<int64_t> np;
+    for (int64_t L0 = lmax; L0 >= lmin;) {
+        int64_t rows = 0, slots = 0;
+        std::vector<int64_t> off;
+        while (L0 - rows >= lmin) {
+            const int64_t cap = n / (min_copies * (L0 - rows)) + 1;
+            if (rows && (rows + 1) * (nw + 1) * 4 + (slots + cap) * 16 > budget) break;
+            off.push_back(slots);
+            slots += cap;
+            ++rows;
+        }
+        c.slot[S_PACK].ensure((size_t)rows * (nw + 1) * 4);
+        c.slot[S_MISC0].ensure((size_t)slots * 16);
+        c.slot[S_MISC1].ensure((size_t)rows * 8);
+        c.slot[S_MISC2].ensure((size_t)rows * 8);
+        uint32_t *P = c.slot[S_PACK].as<uint32_t>();
+        HIPCHECK(hipMemsetAsync(P, 0, (size_t)rows * (nw + 1) * 4, st));
+        HIPCHECK(hipMemcpyAsync(c.slot[S_MISC1].p, off.data(), (size_t)rows * 8, hipMemcpyHostToDevice, st));
+        const int64_t segs = (n + kMmSeg - 1) / kMmSeg;
+        KLAUNCH("k_mm_pbits", 0.0, k_mm_pbits, dim3((unsigned)((segs + 255) / 256), (unsigned)rows), dim3(256), 0, st,
+                d_text, n, (int32_t)L0, max_mismatch, nw, P);
+        KLAUNCH("k_mm_walk", 0.0, k_mm_walk, dim3((unsigned)rows), dim3(64), 0, st, P, n, nw, (int32_t)L0, min_copies,
+                c.slot[S_MISC1].as<int64_t>(), c.slot[S_MISC0].as<int64_t>(), c.slot[S_MISC2].as<int64_t>());
+        HIPCHECK(hipGetLastError());
+        std::vector<int64_t> cnt((size_t)rows), sc((size_t)slots * 2);
+        HIPCHECK(hipMemcpyAsync(cnt.data(), c.slot[S_MISC2].p, (size_t)rows * 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(sc.data(), c.slot[S_MISC0].p, (size_t)slots * 16, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        for (int64_t r = 0; r < rows; ++r) {
+            const int64_t L = L0 - r;
+            for (int64_t k = 0; k < cnt[(size_t)r]; ++k) {
+                const int64_t i = sc[(size_t)(2 * (off[(size_t)r] + k))], cc = sc[(size_t)(2 * (off[(size_t)r] + k) + 1)];
+                hits.push_back(bwtmi_hit{i, i + cc * L, (int32_t)L, 0, cc});
+            }
+        }
+        L0 -= rows;
+    }
+    const int64_t nh = (int64_t)hits.size();
+    if (!nh) return;
+    c.slot[S_HITS].ensure((size_t)nh * sizeof(bwtmi_hit));
+    HIPCHECK(hipMemcpyAsync(c.slot[S_HITS].p, hits.data(), (size_t)nh * sizeof(bwtmi_hit), hipMemcpyHostToDevice, st));
+    KLAUNCH("k_period", 0.0, k_period, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st, d_text,
+            c.slot[S_HITS].as<bwtmi_hit>(), nh);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(hits.data(), c.slot[S_HITS].p, (size_t)nh * sizeof(bwtmi_hit), hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+}
 
 void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
                         int32_t min_copies, ScanResult &res, bool screen) {

@@ -52,11 +52,11 @@ def _same(seq, min_unit, max_unit, mc):
 def test_strict_scan_reference_raw_hits(gpu_ctx, golden_dir):
     with open(os.path.join(golden_dir, "rawhits.json")) as f:
         raw = json.load(f)
-    for key, case in raw.items():
-        if case.get("max_mismatch", 0):
-            continue
+    from bwtmi.tiers import strict_scan_hits
+    for key, case in raw.items():   # incl. the reference's max_mismatch=2 run ("synth_imperfect.fa|mm2")
         seq = case["seq"].encode()
-        h = _gpu_hits(seq, 1, case["U"], case["min_copies"])
+        h = strict_scan_hits(np.frombuffer(seq, dtype=np.uint8), case.get("min_unit", 1), case["U"],
+                             case["min_copies"], max_mismatch=case.get("max_mismatch", 0))
         got = [[int(s), int(e), seq[s:s + p].decode(), int(c)] for s, e, L, p, c in h.tolist()]
         assert got == case["hits"], key
 
@@ -71,6 +71,21 @@ def test_strict_scan_random_vs_oracle(gpu_ctx, n, alpha, seed):
         U = max(120, min(n // mc, 1000))
         _same(seq, 1, U, mc)
     _same(seq, 3, 40, 3)
+
+
+@pytest.mark.parametrize("n,alpha,seed", [(1, b"ACGT", 1), (60, b"A", 2), (700, b"AC", 3), (5000, b"ACGT", 4),
+                                          (4000, b"ACGTNRY", 5), (30000, b"ACGT", 6)])
+def test_strict_scan_mismatch_vs_oracle(gpu_ctx, n, alpha, seed):
+    """find_long_unit_repeats_strict with max_mismatch > 0 (bwt.py:1929-1944):
+    Hamming-tolerant adjacency on the device against the oracle's direct loop."""
+    from bwtmi.tiers import strict_scan_hits
+    seq = _planted(n, seed, alpha) if n > 100 else _rng_text(n, alpha, seed)
+    t = np.frombuffer(seq, dtype=np.uint8)
+    for mm in (1, 2, 5):
+        for mc, lo, hi in ((3, 1, max(120, min(n // 3, 1000))), (2, 1, 300), (1, 3, 50), (5, 20, 120)):
+            g = strict_scan_hits(t, lo, hi, mc, max_mismatch=mm)
+            o = oracle.strict_scan(seq, lo, hi, mm, mc)
+            assert g.shape == o.shape and (g == o).all(), (n, mm, mc)
 
 
 def test_strict_scan_long_runs_and_streaks(gpu_ctx):

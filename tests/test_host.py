@@ -586,3 +586,57 @@ def test_bench_launches_n_ranks_without_a_launcher(tmp_path):
     finally:
         if env_before is not None:
             os.environ["WORLD_SIZE"] = env_before
+
+
+_DP_SCRIPT = r'''
+import hashlib, sys
+sys.path[:0] = [sys.argv[1], sys.argv[1] + "/bwt-algorithm_amd"]
+import oracle
+from bwtmi import synth, MotifUtils
+from bwtmi.records import Job
+h = hashlib.sha256()
+for idx, sub in ((71, 0.04), (72, 0.08)):
+    seq = synth.generate_contig(200_000, idx, sub)
+    j = Job(min_copies=3, show_progress=True, threads=2)
+    j.add_contig("c%d" % idx, seq, 30, 30)
+    j.add_hits(0, oracle.strict_scan(seq[30:-30], 1, 1000, 0, 3))
+    j.postprocess()
+    h.update(j.render("strfinder"))
+import random
+r = random.Random(5)
+for _ in range(300):
+    m = r.randint(2, 12)
+    motif = "".join(r.choice("ACGT") for _ in range(m))
+    s = list(motif * r.randint(3, 12))
+    for k in range(len(s)):
+        x = r.random()
+        if x < 0.05:
+            s[k] = r.choice("ACGT")
+        elif x < 0.08:
+            s[k] = ""
+        elif x < 0.11:
+            s[k] += r.choice("ACGT")
+    s = "".join(s)
+    res = MotifUtils.align_repeat_region(s, 0, len(s), motif)
+    h.update(repr(None if res is None else (res.copies, res.consensus, res.mismatch_rate, res.variations)).encode())
+print(h.hexdigest())
+'''
+
+
+def test_banded_dp_avx512_and_scalar_paths_agree(tmp_path, built_lib):
+    """The merge/refine banded DP has an AVX-512 path (one register per row)
+    and the scalar path; both run here (BWTMI_NO_AVX512=1 forces the scalar
+    one) on seeded imperfect contigs through post-processing + STRfinder
+    rendering and on 300 random align_repeat_region cases: identical bytes."""
+    import subprocess
+    import sys
+    repo = os.path.abspath(os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    script = tmp_path / "dp.py"
+    script.write_text(_DP_SCRIPT)
+    outs = []
+    for flag in ("0", "1"):
+        env = dict(os.environ, BWTMI_NO_AVX512=flag)
+        r = subprocess.run([sys.executable, str(script), repo], env=env, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(r.stdout.strip())
+    assert outs[0] == outs[1] and len(outs[0]) == 64
