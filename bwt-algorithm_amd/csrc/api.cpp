@@ -288,6 +288,10 @@ int bwtmi_kernel_stats(bwtmi_ctx *ctx, int enable, int reset, char *out, int64_t
         CHECK_ARG(ctx, "null ctx");
         Ctx &c = ctx->c;
         ctx_wait(c);
+        if (!c.pending.empty()) {   // launches of calls that end without resolving their timers
+            HIPCHECK(hipStreamSynchronize(c.stream));
+            c.kresolve();
+        }
         std::string s;
         char line[160];
         for (auto &k : c.kstats) {

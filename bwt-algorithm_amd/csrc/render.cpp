@@ -250,21 +250,26 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
                 const char *rsq = tseq + a;
                 const int64_t rl = b - a;
                 const int64_t k = 3;
+                // Every split point sp (k <= sp < rl - k, a multiple of k) sees whole
+                // copies only: l1 = l2 = k, c1 = the leading copies equal to copy 0,
+                // capped at sp / k, and c2 = the run of copies equal to copy sp/k
+                // (exact equality chains), so both come from one pass over the
+                // copies instead of a rescan per split point (O(copies), not O(copies^2))
+                thread_local std::vector<int32_t> run_from;
+                const int64_t nq = rl / k;   // whole copies
+                int64_t lead = 0;
+                if (rl - k > k) {
+                    while (lead < nq && std::memcmp(rsq + lead * k, rsq, (size_t)k) == 0) ++lead;
+                    run_from.assign((size_t)nq + 1, 0);
+                    for (int64_t q = nq - 1; q >= 0; --q)
+                        run_from[(size_t)q] = 1 + (q + 1 < nq && std::memcmp(rsq + q * k, rsq + (q + 1) * k, (size_t)k) == 0
+                                                       ? run_from[(size_t)q + 1] : 0);
+                }
                 for (int64_t sp = k; sp < rl - k; sp += k) {
-                    const int64_t l1 = std::min<int64_t>(k, rl), l2 = std::min<int64_t>(k, rl - sp);
-                    if (l1 == l2 && std::memcmp(rsq, rsq + sp, (size_t)l1) == 0) continue;
-                    int64_t c1 = 0;
-                    for (int64_t j = 0; j < sp; j += k) {
-                        const int64_t lj = std::min<int64_t>(k, rl - j);
-                        if (lj == l1 && std::memcmp(rsq + j, rsq, (size_t)l1) == 0) ++c1;
-                        else break;
-                    }
-                    int64_t c2 = 0;
-                    for (int64_t j = sp; j < rl; j += k) {
-                        const int64_t lj = std::min<int64_t>(k, rl - j);
-                        if (lj == l2 && std::memcmp(rsq + j, rsq + sp, (size_t)l2) == 0) ++c2;
-                        else break;
-                    }
+                    const int64_t l1 = k, l2 = k;
+                    if (std::memcmp(rsq, rsq + sp, (size_t)k) == 0) continue;
+                    const int64_t c1 = std::min<int64_t>(lead, sp / k);
+                    const int64_t c2 = run_from[(size_t)(sp / k)];
                     if (c1 >= 5 && c2 >= 5 && (double)(c1 * l1 + c2 * l2) >= (double)rl * 0.9) {
                         const int64_t e1 = cur->start + c1 * l1;
                         // actual = repeat_seq[:c1*l1], repeat_seq[c1*l1 : c1*l1 + c2*l2]
@@ -316,25 +321,38 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
         std::vector<Walk> W((size_t)K);
         run_tasks(K, nt, [&](int64_t k) {
             size_t i = cut[(size_t)k];
+            Walk &w = W[(size_t)k];
+            w.rows.reserve(cut[(size_t)k + 1] - i + 16);
+            w.at.reserve(cut[(size_t)k + 1] - i + 16);
             while (i < cut[(size_t)k + 1]) {
                 from[i] = 1;
-                i = step(i, W[(size_t)k]);
+                i = step(i, w);
             }
-            W[(size_t)k].next = i;
+            w.next = i;
         });
+        // the serial repair only decides which rows are taken; they are
+        // copied into place afterwards, in parallel
+        std::vector<Walk> reps((size_t)K);
+        std::vector<std::pair<const Row *, size_t>> seg;
         size_t ti = 0;
         for (int k = 0; k < K; ++k) {
             Walk &sp = W[(size_t)k];
             if (ti >= cut[(size_t)k + 1]) continue;   // the true walk stepped over this chunk
-            Walk rep;
+            Walk &rep = reps[(size_t)k];
             while (ti < cut[(size_t)k + 1] && !from[ti]) ti = step(ti, rep);
-            out.rows.insert(out.rows.end(), rep.rows.begin(), rep.rows.end());
-            out.pools.push_back(std::move(rep.pool));
+            if (!rep.rows.empty()) seg.emplace_back(rep.rows.data(), rep.rows.size());
             if (ti >= cut[(size_t)k + 1]) continue;
             size_t q = (size_t)(std::lower_bound(sp.at.begin(), sp.at.end(), ti) - sp.at.begin());
-            out.rows.insert(out.rows.end(), sp.rows.begin() + (std::ptrdiff_t)q, sp.rows.end());
+            if (q < sp.rows.size()) seg.emplace_back(sp.rows.data() + q, sp.rows.size() - q);
             ti = sp.next;
         }
+        std::vector<size_t> at(seg.size() + 1, out.rows.size());
+        for (size_t q = 0; q < seg.size(); ++q) at[q + 1] = at[q] + seg[q].second;
+        out.rows.resize(at.back());
+        run_tasks((int64_t)seg.size(), nt, [&](int64_t q) {
+            std::copy(seg[(size_t)q].first, seg[(size_t)q].first + seg[(size_t)q].second, out.rows.begin() + (std::ptrdiff_t)at[(size_t)q]);
+        });
+        for (auto &w : reps) out.pools.push_back(std::move(w.pool));
         for (auto &w : W) out.pools.push_back(std::move(w.pool));
     }
     if (const char *e = std::getenv("BWTMI_STATS"); e && *e == '1') {

@@ -20,8 +20,8 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o pmc -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-fm --no-cli > "$OUT/write.json" 2> "$OUT/write.err" || { echo WRITE_FAIL; tail -5 "$OUT/write.err"; exit 1; }
 python3 tools/pmc_traffic.py "$OUT/fetch" "$OUT/write" "$OUT/pmc_traffic.json" && echo PMC_OK
 rm -rf "$OUT/fetch" "$OUT/write"
-timeout -k 10 300 python -u tools/lib_kernels.py "$OUT/lib_kernels.json" 1e6 1e7 > "$OUT/lib_kernels.log" 2>&1 || { echo LIB_FAIL; tail -20 "$OUT/lib_kernels.log"; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/libprof" -o lib -- python3 tools/lib_kernels.py "$OUT/lib_kernels_prof.json" 1e6 1e7 > "$OUT/libprof.log" 2>&1 || { echo LIBPROF_FAIL; tail -20 "$OUT/libprof.log"; exit 1; }
+timeout -k 10 300 python -u tools/lib_kernels.py "$OUT/lib_kernels.json" 999000 1e7 > "$OUT/lib_kernels.log" 2>&1 || { echo LIB_FAIL; tail -20 "$OUT/lib_kernels.log"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/libprof" -o lib -- python3 tools/lib_kernels.py "$OUT/lib_kernels_prof.json" 999000 1e7 > "$OUT/libprof.log" 2>&1 || { echo LIBPROF_FAIL; tail -20 "$OUT/libprof.log"; exit 1; }
 find "$OUT/libprof" -name "*kernel_stats.csv" -exec cp {} "$OUT/lib_kernel_stats.csv" \;
 rm -rf "$OUT/libprof"
 echo ALL_OK

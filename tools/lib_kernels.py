@@ -21,7 +21,7 @@ import numpy as np  # noqa: E402
 
 def main():
     out = sys.argv[1]
-    sizes = [int(float(x)) for x in sys.argv[2:]] or [1_000_000, 10_000_000]
+    sizes = [int(float(x)) for x in sys.argv[2:]] or [999_000, 10_000_000]
     from bwtmi import BWTCore, _lib, synth
     from bwtmi.tiers import Tier1STRFinder, Tier2LCPFinder, Tier3LongReadFinder
     ctx = _lib.ctx(0)
@@ -37,7 +37,7 @@ def main():
                  ("lcp_plateaus", lambda: f._detect_lcp_plateaus(None, "c")),
                  ("tier1", lambda: Tier1STRFinder(np.frombuffer(text, dtype=np.uint8), 9).find_strs("c")),
                  ("tier3", lambda: Tier3LongReadFinder(core).find_very_long_repeats(reads, "c"))]
-        if n <= 1_000_000:   # bwt.py:2048: the reference returns [] above 1 Mbp
+        if n < 1_000_000:   # bwt.py:2048: the reference returns [] above 1 Mbp (text incl. '$')
             calls.append(("short_imperfect", lambda: f.find_short_imperfect_repeats("c", set())))
             calls.append(("long_repeats", lambda: f.find_long_repeats("c", set())))
         for name, fn in calls:
