@@ -216,6 +216,12 @@ struct Job {
     bool postprocessed = false;
     Rendered rendered;                               // last bwtmi_job_render_units result
     double stage_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // the split loader's pass-1 bytes (file range [part_a, part_b) of part_path,
+    // read at the file's size/mtime part_stamp), reused by pass 2 for the own
+    // contigs that lie inside it
+    Seq part;
+    std::string part_path;
+    int64_t part_a = 0, part_b = 0, part_stamp[2] = {-1, -1};
     void assign_units();
 };
 

@@ -85,7 +85,10 @@ struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     // per-kernel HIP-event timing (on the ctx stream), enabled by bwtmi_kernel_stats
-    bool ktiming = false;
+    bool ktiming = [] {   // BWTMI_KTRACE=path: every launch of every call, timed from the start
+        const char *e = std::getenv("BWTMI_KTRACE");
+        return e && *e;
+    }();
     struct Pend {
         std::string name;
         hipEvent_t a, b;

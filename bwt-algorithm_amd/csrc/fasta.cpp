@@ -407,6 +407,12 @@ struct Fd {
         if (::fstat(fd, &st) != 0) fail(BWTMI_E_IO, "cannot stat");
         return (int64_t)st.st_size;
     }
+    void stamp(int64_t out[2]) const {   // size and modification time (ns)
+        struct stat st;
+        if (::fstat(fd, &st) != 0) fail(BWTMI_E_IO, "cannot stat");
+        out[0] = (int64_t)st.st_size;
+        out[1] = (int64_t)st.st_mtim.tv_sec * 1000000000 + (int64_t)st.st_mtim.tv_nsec;
+    }
 };
 
 // [a, b) of the buffer p cut into T chunks at line starts
@@ -431,8 +437,12 @@ void fasta_scan_part(Job &job, const char *path, int32_t world, int32_t rank, st
     Fd f(path);
     const int64_t N = f.size();
     const int64_t A = line_start_from(f.fd, N, N * rank / world), B = line_start_from(f.fd, N, N * (rank + 1) / world);
-    thread_local Seq part;
+    Seq &part = job.part;
     char *p = part.resize_uninit((size_t)std::max<int64_t>(0, B - A));
+    job.part_path = path;
+    job.part_a = A;
+    job.part_b = B;
+    f.stamp(job.part_stamp);
     if (B > A) pread_range(f.fd, p, A, B, nt);
     const int64_t n = B - A;
     const int64_t T = std::max<int64_t>(1, std::min<int64_t>(4 * (int64_t)nt, n / (int64_t(1) << 20) + 1));
@@ -580,9 +590,24 @@ void fasta_load_parts(Job &job, const char *path, int32_t flank_trim, int32_t wo
         own.push_back(Own{cid, a, b, tot, 0, 0});
         tot += b - a;
     }
+    // own contigs inside the range this rank's pass 1 read (the common case:
+    // equal contigs, one per rank) are taken from those bytes in place; only
+    // the others are read again
+    int64_t st_now[2] = {-2, -2};
+    f.stamp(st_now);
+    const bool same_file = job.part_path == path && st_now[0] == job.part_stamp[0] && st_now[1] == job.part_stamp[1] &&
+                           (int64_t)job.part.size() == job.part_b - job.part_a;
+    bool inside = same_file && !own.empty();
+    for (const Own &w : own) inside = inside && w.a >= job.part_a && w.b <= job.part_b;
     thread_local Seq raw;
-    char *p = raw.resize_uninit((size_t)tot);
-    {
+    char *p = nullptr;
+    if (inside) {
+        p = job.part.data();
+        for (Own &w : own) w.off = w.a - job.part_a;
+    } else {
+        p = raw.resize_uninit((size_t)tot);
+    }
+    if (!inside) {
         const int64_t piece = int64_t(4) << 20;
         std::vector<std::pair<size_t, int64_t>> rd;   // (own index, piece start in its range)
         for (size_t u = 0; u < own.size(); ++u)

@@ -573,7 +573,8 @@ std::atomic<int64_t> g_recomputes{0}, g_recompute_ns{0}, g_merges{0}, g_canons{0
 const bool g_stats = [] { const char *e = std::getenv("BWTMI_STATS"); return e && (*e == '1' || *e == '2'); }();
 const bool g_counters = [] { const char *e = std::getenv("BWTMI_STATS"); return e && *e == '2'; }();
 const char *const g_dump = std::getenv("BWTMI_DUMP_RECOMPUTE");
-std::atomic<int64_t> g_hist_n[8][8], g_hist_ns[8][8];   // [log4 motif len][log4 region len]
+std::atomic<int64_t> g_hist_n[8][8], g_hist_ns[8][8];
+std::atomic<int64_t> g_fresh_tests{0}, g_chain_tests{0}, g_fresh_merges{0}, g_chain_merges{0};   // [log4 motif len][log4 region len]
 inline int lg4(int64_t v) { int k = 0; while (v >= 4 && k < 7) { v >>= 2; ++k; } return k; }
 
 // bwt.py:3515-3614 (on the trimmed sequence, before coordinate restore)
@@ -823,7 +824,9 @@ void spec_run(const UnitCtx &u, Pools &pools, int w, const ItemVec &R, int64_t b
     for (int64_t i = b + 1; i < e; ++i) {
         Canon &cc = cb[ci_cur], &ci = cb[ci_cur ^ 1];
         ci.ok = false;
+        if (g_counters) (merged ? g_chain_tests : g_fresh_tests).fetch_add(1, std::memory_order_relaxed);
         if (try_merge(u, pools, w, cur, cc, R[(size_t)i], ci, mg)) {
+            if (g_counters) (merged ? g_chain_merges : g_fresh_merges).fetch_add(1, std::memory_order_relaxed);
             cur = mg;
             merged = true;
             cc.ok = false;
@@ -1370,6 +1373,10 @@ void postprocess(Job &job) {
     if (g_counters)
         std::fprintf(stderr, "[bwtmi] merge tests past the gap test=%lld, same canonical=%lld\n",
                      (long long)g_tests.exchange(0), (long long)g_same.exchange(0));
+    if (g_counters)
+        std::fprintf(stderr, "[bwtmi] fold steps with a fresh current record=%lld (merged %lld), with a merged one=%lld (merged %lld)\n",
+                     (long long)g_fresh_tests.exchange(0), (long long)g_fresh_merges.exchange(0),
+                     (long long)g_chain_tests.exchange(0), (long long)g_chain_merges.exchange(0));
     if (g_counters)
         for (int a = 0; a < 8; ++a)
             for (int b = 0; b < 8; ++b)
