@@ -1353,14 +1353,27 @@ void postprocess(Job &job) {
         }
     }
     job.final_recs.clear();
-    if (job.nunits == 1) {
-        job.final_recs.swap(res[0]);
-    } else {
-        size_t tot = 0;
-        for (auto &v : res) tot += v.size();
-        job.final_recs.reserve(tot);
-        for (auto &v : res)
-            for (auto &r : v) job.final_recs.push_back(std::move(r));
+    size_t tot = 0, nonempty = 0, last = 0;
+    for (size_t k = 0; k < res.size(); ++k)
+        if (!res[k].empty()) {
+            tot += res[k].size();
+            ++nonempty;
+            last = k;
+        }
+    if (nonempty <= 1) {   // one unit with records (one contig, or this rank's only one): no copy
+        if (nonempty) job.final_recs.swap(res[last]);
+    } else {   // the units' records moved into place in parallel
+        std::vector<size_t> at(res.size() + 1, 0);
+        for (size_t k = 0; k < res.size(); ++k) at[k + 1] = at[k] + res[k].size();
+        job.final_recs.resize(tot);
+        run_tasks((int64_t)res.size(), T, [&](int64_t k) {
+            std::move(res[(size_t)k].begin(), res[(size_t)k].end(), job.final_recs.begin() + (std::ptrdiff_t)at[(size_t)k]);
+        });
+    }
+    // the units' emptied vectors are released behind the next stage
+    {
+        auto old = std::make_shared<std::vector<RecVec>>(std::move(res));
+        defer([old] { old->clear(); });
     }
     for (int s = 0; s < 4; ++s) {
         job.stage_ms[2 + s] = 0;
