@@ -381,9 +381,19 @@ int64_t line_start_from(int fd, int64_t N, int64_t x) {
     return N;
 }
 
+// read pieces and line-start chunks of a split load: a rank's share of a
+// file is small (12.5 MB of C4 at 8 ranks), so pieces shrink to keep every
+// thread busy (4 MB pieces gave a 12.7 MB range 4 tasks for 16 threads)
+inline int64_t split_piece(int64_t n, int nt) {
+    return std::max<int64_t>(int64_t(256) << 10, std::min<int64_t>(int64_t(4) << 20, n / (2 * std::max(1, nt)) + 1));
+}
+inline int64_t split_chunks(int64_t n, int nt) {
+    return std::max<int64_t>(1, std::min<int64_t>(4 * (int64_t)nt, n / (int64_t(256) << 10) + 1));
+}
+
 void pread_range(int fd, char *dst, int64_t a, int64_t b, int nt) {
     std::atomic<bool> bad{false};
-    const int64_t piece = int64_t(4) << 20;
+    const int64_t piece = split_piece(b - a, nt);
     run_tasks((b - a + piece - 1) / piece, nt, [&](int64_t k) {
         int64_t o = a + k * piece;
         const int64_t e = std::min(b, o + piece);
@@ -445,7 +455,7 @@ void fasta_scan_part(Job &job, const char *path, int32_t world, int32_t rank, st
     f.stamp(job.part_stamp);
     if (B > A) pread_range(f.fd, p, A, B, nt);
     const int64_t n = B - A;
-    const int64_t T = std::max<int64_t>(1, std::min<int64_t>(4 * (int64_t)nt, n / (int64_t(1) << 20) + 1));
+    const int64_t T = split_chunks(n, nt);
     const std::vector<int64_t> cut = cut_lines(p, 0, n, T, nt);
     std::vector<Chunk> ck((size_t)T);
     run_tasks(T, nt, [&](int64_t t) {
@@ -608,7 +618,7 @@ void fasta_load_parts(Job &job, const char *path, int32_t flank_trim, int32_t wo
         p = raw.resize_uninit((size_t)tot);
     }
     if (!inside) {
-        const int64_t piece = int64_t(4) << 20;
+        const int64_t piece = split_piece(tot, nt);
         std::vector<std::pair<size_t, int64_t>> rd;   // (own index, piece start in its range)
         for (size_t u = 0; u < own.size(); ++u)
             for (int64_t o = 0; o < own[u].b - own[u].a; o += piece) rd.push_back({u, o});
@@ -628,7 +638,7 @@ void fasta_load_parts(Job &job, const char *path, int32_t flank_trim, int32_t wo
     std::vector<int64_t> ca, cb;   // chunk [ca, cb) in the buffer
     for (Own &w : own) {
         const int64_t n = w.b - w.a;
-        const int64_t T = std::max<int64_t>(1, std::min<int64_t>(4 * (int64_t)nt, n / (int64_t(1) << 20) + 1));
+        const int64_t T = split_chunks(n, nt);
         const std::vector<int64_t> cut = cut_lines(p, w.off, w.off + n, T, nt);
         w.c0 = ca.size();
         for (int64_t t = 0; t < T; ++t) {
