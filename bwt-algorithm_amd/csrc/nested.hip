@@ -185,6 +185,114 @@ __global__ void k_buckets(const int64_t *__restrict__ S, int64_t n, int64_t nb, 
     B[b] = (uint32_t)lo;
 }
 
+// the nested test of hit (s0, e0, m) against a kept span (Sk, Ek) of longer
+// motif Mk > m (bwt.py:3460-3490), predicate division for division
+__device__ __forceinline__ bool nested_by(int64_t s0, int64_t e0, int64_t m, int64_t rl, int64_t Sk, int64_t Ek,
+                                          int64_t Mk, double thr) {
+    const int64_t ov = min(e0, Ek) - max(s0, Sk);
+    if (ov <= 0) return false;
+    const double ratio = (double)Mk / (double)m;
+    const double frac = (double)ov / (double)rl;
+    if (m == 1 && Mk > 1 && frac >= 0.8) return true;
+    const double th = ratio >= 10 ? 0.1 : (ratio >= 5 ? 0.3 : thr);
+    return frac >= th;
+}
+
+// All levels in one launch, segment by segment.  Hits overlap only inside a
+// "segment" of the position order (k starts one iff PME[k-1] <= S[k]: no
+// earlier span reaches past it), so segments are independent and the level
+// order only matters inside each.  Workgroup w takes the segments that start
+// in positions [w W, (w+1) W) of the order, copies their spans to LDS and
+// decides them level by level (descending m, a workgroup barrier between
+// levels) -- one launch instead of one per distinct m (119 launches, ~1.5 ms
+// of a 12.5 Mbp scan).  A workgroup whose segments exceed the LDS capacity
+// raises `overflow`, and the caller falls back to the per-level launches.
+constexpr int kSegThreads = 1024;
+constexpr int kSegWin = 2048;   // nominal positions per workgroup
+constexpr int kSegCap = 4096;   // hits a workgroup holds in LDS
+
+__device__ __forceinline__ bool seg_head(const int64_t *__restrict__ S, const int64_t *__restrict__ PME, int64_t k) {
+    return k == 0 || PME[k - 1] <= S[k];
+}
+
+__global__ __launch_bounds__(kSegThreads) void k_seg_levels(const int64_t *__restrict__ S, const int64_t *__restrict__ E,
+                                                            const int32_t *__restrict__ M,
+                                                            const int64_t *__restrict__ PME, int64_t n,
+                                                            uint8_t *__restrict__ kept, unsigned int *__restrict__ overflow,
+                                                            double thr) {
+    __shared__ int64_t sS[kSegCap], sE[kSegCap], sP[kSegCap];
+    __shared__ int32_t sM[kSegCap];
+    __shared__ uint8_t sK[kSegCap];
+    __shared__ unsigned long long found;
+    __shared__ int lvl;
+    const int tid = threadIdx.x;
+    const int64_t w0 = (int64_t)blockIdx.x * kSegWin;
+    const int64_t w1 = w0 + kSegWin < n ? w0 + kSegWin : n;
+    // a = first segment head in [w0, w1): none -> a segment from an earlier window covers it
+    if (tid == 0) found = ~0ull;
+    __syncthreads();
+    for (int64_t k = w0 + tid; k < w1; k += kSegThreads)
+        if (seg_head(S, PME, k)) atomicMin(&found, (unsigned long long)k);
+    __syncthreads();
+    const int64_t a = (int64_t)found;   // uniform
+    if (found == ~0ull) return;
+    __syncthreads();
+    // b = first segment head at or after w1 (n if none), looked for up to a + kSegCap
+    if (tid == 0) found = ~0ull;
+    __syncthreads();
+    const int64_t lim = a + kSegCap < n ? a + kSegCap : n;
+    for (int64_t k = w1 + tid; k < lim + 1 && k <= n; k += kSegThreads)
+        if (k == n || seg_head(S, PME, k)) atomicMin(&found, (unsigned long long)k);
+    __syncthreads();
+    const int64_t b = (int64_t)found;
+    if (found == ~0ull || b - a > kSegCap) {   // segments past the LDS capacity
+        if (tid == 0) atomicOr(overflow, 1u);
+        return;
+    }
+    const int len = (int)(b - a);
+    for (int i = tid; i < len; i += kSegThreads) {
+        sS[i] = S[a + i];
+        sE[i] = E[a + i];
+        sP[i] = PME[a + i];
+        sM[i] = M[a + i];
+        sK[i] = 0;
+    }
+    int cur = 0x7fffffff;   // levels below this one are still undecided
+    for (;;) {
+        if (tid == 0) lvl = -1;
+        __syncthreads();
+        int mx = -1;
+        for (int i = tid; i < len; i += kSegThreads)
+            if (sM[i] < cur && sM[i] > mx) mx = sM[i];
+        if (mx >= 0) atomicMax(&lvl, mx);
+        __syncthreads();
+        const int m = lvl;   // uniform
+        if (m < 0) break;
+        for (int i = tid; i < len; i += kSegThreads) {
+            if (sM[i] != m) continue;
+            const int64_t s0 = sS[i], e0 = sE[i], rl = e0 - s0;
+            bool nested = false;
+            if (rl > 0) {
+                int lo = i + 1, hi = len;   // first local rank with S >= e0 (S[i] = s0 < e0)
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (sS[mid] < e0) lo = mid + 1;
+                    else hi = mid;
+                }
+                for (int k = lo - 1; k >= 0 && sP[k] > s0; --k) {
+                    const int64_t Mk = sM[k];
+                    if (Mk <= m || !sK[k]) continue;   // this level's entries are being written now: never read
+                    if (nested_by(s0, e0, m, rl, sS[k], sE[k], Mk, thr)) { nested = true; break; }
+                }
+            }
+            sK[i] = nested ? 0 : 1;
+        }
+        cur = m;
+        __syncthreads();
+    }
+    for (int i = tid; i < len; i += kSegThreads) kept[a + i] = sK[i];
+}
+
 // one level (all hits of one primitive length m): nested test against the
 // kept spans of longer motif (bwt.py:3460-3490), predicate division for division
 __global__ __launch_bounds__(kB) void k_level(const uint32_t *__restrict__ lvl, int64_t cnt,
@@ -211,13 +319,7 @@ __global__ __launch_bounds__(kB) void k_level(const uint32_t *__restrict__ lvl, 
         for (int64_t k = lo - 1; k >= 0 && PME[k] > s0; --k) {
             const int64_t Mk = M[k];
             if (Mk <= m || !kept[k]) continue;   // same-level entries are being written now: never read
-            const int64_t ov = min(e0, E[k]) - max(s0, S[k]);
-            if (ov <= 0) continue;
-            const double ratio = (double)Mk / (double)m;
-            const double frac = (double)ov / (double)rl;
-            if (m == 1 && Mk > 1 && frac >= 0.8) { nested = true; break; }
-            const double th = ratio >= 10 ? 0.1 : (ratio >= 5 ? 0.3 : thr);
-            if (frac >= th) { nested = true; break; }
+            if (nested_by(s0, e0, m, rl, S[k], E[k], Mk, thr)) { nested = true; break; }
         }
     }
     kept[rank_of[idx]] = nested ? 0 : 1;
@@ -296,6 +398,38 @@ __global__ void k_final_compact(const bwtmi_hit *__restrict__ H, const uint32_t 
 
 }  // namespace
 
+// the per-level path: the hits in level order G (descending m), one launch per
+// level (also the fallback of k_seg_levels when segments exceed its LDS)
+static void screen_levels(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int32_t lmax, int mb, uint64_t *kgrp,
+                          uint32_t *vgrp, const uint32_t *rank_of, const int64_t *S, const int64_t *E, const int32_t *M,
+                          const int64_t *PME, uint8_t *kept, int64_t nb) {
+    hipStream_t st = c.stream;
+    const int gb = ((mb + 7) / 8) * 8;
+    radix_sort_pairs32(c, kgrp, vgrp, n, 0, gb);
+    uint32_t *B = c.slot[S_IDX6].as<uint32_t>();
+    KLAUNCH("k_buckets", 0.0, k_buckets, dim3(blocks(nb)), dim3(kB), 0, st, S, n, nb, B);
+    int64_t *first = c.slot[S_COUNTS].as<int64_t>();
+    HIPCHECK(hipMemsetAsync(first, 0xff, (size_t)(lmax + 2) * 8, st));
+    KLAUNCH("k_bounds", 0.0, k_bounds, dim3(blocks(n)), dim3(kB), 0, st, kgrp, n, first);
+    std::vector<int64_t> fh((size_t)lmax + 2);
+    HIPCHECK(hipMemcpyAsync(fh.data(), first, fh.size() * 8, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(st));
+    // levels in descending m (ascending group key)
+    std::vector<std::pair<int64_t, int64_t>> lv;   // (first, group key)
+    for (int64_t g = 0; g <= lmax; ++g)
+        if (fh[(size_t)g] >= 0) lv.push_back({fh[(size_t)g], g});
+    for (size_t q = 0; q < lv.size(); ++q) {
+        const int64_t a = lv[q].first, b = q + 1 < lv.size() ? lv[q + 1].first : n;
+        if (b - a <= kWaveLevelMax)   // few hits (long motifs, long walks): a wave per hit
+            KLAUNCH("k_level_wave", 0.0, k_level_wave, dim3(blocks((b - a) * 64)), dim3(kB), 0, st, vgrp + a, b - a, d_hits,
+                    rank_of, S, E, M, PME, B, kept, n, 0.5);
+        else
+            KLAUNCH("k_level", 0.0, k_level, dim3(blocks(b - a)), dim3(kB), 0, st, vgrp + a, b - a, d_hits, rank_of, S, E,
+                    M, PME, B, kept, n, 0.5);
+    }
+}
+
 void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
                         ScreenedVec &out) {
     out.clear();
@@ -346,32 +480,20 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     radix_sort_pairs32(c, kpos, vpos, n, 0, round8(lb + mb));
     KLAUNCH("k_keys_start", 0.0, k_keys_start, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, kpos);
     radix_sort_pairs32(c, kpos, vpos, n, 0, round8(std::max(1, bits_for((uint64_t)text_len))));   // start < text_len
-    radix_sort_pairs32(c, kgrp, vgrp, n, 0, round8(mb));
     KLAUNCH("k_gather", 0.0, k_gather, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, S, E, M, rank_of, kept);
     prefix_max(c, E, PME, n, c.slot[S_IDX5].as<int64_t>());
-    uint32_t *B = c.slot[S_IDX6].as<uint32_t>();
-    KLAUNCH("k_buckets", 0.0, k_buckets, dim3(blocks(nb)), dim3(kB), 0, st, S, n, nb, B);
-    int64_t *first = reinterpret_cast<int64_t *>(d_max);
-    HIPCHECK(hipMemsetAsync(first, 0xff, (size_t)(lmax + 2) * 8, st));
-    KLAUNCH("k_bounds", 0.0, k_bounds, dim3(blocks(n)), dim3(kB), 0, st, kgrp, n, first);
-    std::vector<int64_t> fh((size_t)lmax + 2);
-    HIPCHECK(hipMemcpyAsync(fh.data(), first, fh.size() * 8, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipGetLastError());
-    HIPCHECK(hipStreamSynchronize(st));
-
-    // levels in descending m (ascending group key)
-    std::vector<std::pair<int64_t, int64_t>> lv;   // (first, group key)
-    for (int64_t g = 0; g <= lmax; ++g)
-        if (fh[(size_t)g] >= 0) lv.push_back({fh[(size_t)g], g});
-    for (size_t q = 0; q < lv.size(); ++q) {
-        const int64_t a = lv[q].first, b = q + 1 < lv.size() ? lv[q + 1].first : n;
-        if (b - a <= kWaveLevelMax)   // few hits (long motifs, long walks): a wave per hit
-            KLAUNCH("k_level_wave", 0.0, k_level_wave, dim3(blocks((b - a) * 64)), dim3(kB), 0, st, vgrp + a, b - a, d_hits,
-                               rank_of, S, E, M, PME, B, kept, n, 0.5);
-        else
-            KLAUNCH("k_level", 0.0, k_level, dim3(blocks(b - a)), dim3(kB), 0, st, vgrp + a, b - a, d_hits, rank_of, S, E,
-                               M, PME, B, kept, n, 0.5);
+    // every level, segment by segment, in one launch (BWTMI_SEG_LEVELS=0: per-level launches)
+    static const bool seg_levels = [] { const char *e = std::getenv("BWTMI_SEG_LEVELS"); return !(e && *e == '0'); }();
+    unsigned int *d_ovf = reinterpret_cast<unsigned int *>(d_max);
+    unsigned int ovf = 1;
+    if (seg_levels) {
+        HIPCHECK(hipMemsetAsync(d_ovf, 0, 4, st));
+        KLAUNCH("k_seg_levels", 0.0, k_seg_levels, dim3((unsigned)((n + kSegWin - 1) / kSegWin)), dim3(kSegThreads), 0,
+                st, S, E, M, PME, n, kept, d_ovf, 0.5);
+        HIPCHECK(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
     }
+    if (ovf) screen_levels(c, d_hits, n, lmax, mb, kgrp, vgrp, rank_of, S, E, M, PME, kept, nb);
     KLAUNCH("k_final_flags", 0.0, k_final_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, kept, n, flag);
     HIPCHECK(hipMemsetAsync(flag + n, 0, 4, st));
     exclusive_scan<uint32_t>(c, flag, pos, n + 1);
