@@ -201,96 +201,111 @@ __device__ __forceinline__ bool nested_by(int64_t s0, int64_t e0, int64_t m, int
 // All levels in one launch, segment by segment.  Hits overlap only inside a
 // "segment" of the position order (k starts one iff PME[k-1] <= S[k]: no
 // earlier span reaches past it), so segments are independent and the level
-// order only matters inside each.  Workgroup w takes the segments that start
-// in positions [w W, (w+1) W) of the order, copies their spans to LDS and
-// decides them level by level (descending m, a workgroup barrier between
-// levels) -- one launch instead of one per distinct m (119 launches, ~1.5 ms
-// of a 12.5 Mbp scan).  A workgroup whose segments exceed the LDS capacity
-// raises `overflow`, and the caller falls back to the per-level launches.
-constexpr int kSegThreads = 1024;
-constexpr int kSegWin = 2048;   // nominal positions per workgroup
-constexpr int kSegCap = 4096;   // hits a workgroup holds in LDS
+// order only matters inside each.  Window w = the segments that START in
+// positions [w W, (w+1) W) of the order; a workgroup copies its window's spans
+// to LDS and decides them level by level (descending m, a workgroup barrier
+// between levels) -- instead of one launch per distinct m (119 launches, ~1.5
+// ms of a 12.5 Mbp scan).  Two sizes: 256-thread workgroups holding up to
+// kSegCapS hits (many per CU), and for the windows whose segments overflow
+// them (long arrays: chains of overlapping spans) 1024-thread workgroups
+// holding kSegCapL; past that the caller falls back to the per-level launches.
+constexpr int kSegWin = 256;           // nominal positions per window
+constexpr int kSegCapS = 512;          // hits a small workgroup holds
+constexpr int kSegCapL = 4096;         // hits a large workgroup holds
 
 __device__ __forceinline__ bool seg_head(const int64_t *__restrict__ S, const int64_t *__restrict__ PME, int64_t k) {
     return k == 0 || PME[k - 1] <= S[k];
 }
 
-__global__ __launch_bounds__(kSegThreads) void k_seg_levels(const int64_t *__restrict__ S, const int64_t *__restrict__ E,
-                                                            const int32_t *__restrict__ M,
-                                                            const int64_t *__restrict__ PME, int64_t n,
-                                                            uint8_t *__restrict__ kept, unsigned int *__restrict__ overflow,
-                                                            double thr) {
-    __shared__ int64_t sS[kSegCap], sE[kSegCap], sP[kSegCap];
-    __shared__ int32_t sM[kSegCap];
-    __shared__ uint8_t sK[kSegCap];
+// LARGE = false: window blockIdx.x, overflowing windows are appended to ovf_win;
+// LARGE = true: the windows listed in ovf_win (*ovf_n of them), a grid-stride
+// loop; a window past kSegCapL sets *fallback
+template <int T, int CAP, bool LARGE>
+__global__ __launch_bounds__(T) void k_seg_levels(const int64_t *__restrict__ S, const int64_t *__restrict__ E,
+                                                  const int32_t *__restrict__ M, const int64_t *__restrict__ PME,
+                                                  int64_t n, uint8_t *__restrict__ kept, uint32_t *__restrict__ ovf_win,
+                                                  unsigned int *__restrict__ ovf_n, unsigned int *__restrict__ fallback,
+                                                  double thr) {
+    __shared__ int64_t sS[CAP], sE[CAP], sP[CAP];
+    __shared__ int32_t sM[CAP];
+    __shared__ uint8_t sK[CAP];
     __shared__ unsigned long long found;
     __shared__ int lvl;
     const int tid = threadIdx.x;
-    const int64_t w0 = (int64_t)blockIdx.x * kSegWin;
-    const int64_t w1 = w0 + kSegWin < n ? w0 + kSegWin : n;
-    // a = first segment head in [w0, w1): none -> a segment from an earlier window covers it
-    if (tid == 0) found = ~0ull;
-    __syncthreads();
-    for (int64_t k = w0 + tid; k < w1; k += kSegThreads)
-        if (seg_head(S, PME, k)) atomicMin(&found, (unsigned long long)k);
-    __syncthreads();
-    const int64_t a = (int64_t)found;   // uniform
-    if (found == ~0ull) return;
-    __syncthreads();
-    // b = first segment head at or after w1 (n if none), looked for up to a + kSegCap
-    if (tid == 0) found = ~0ull;
-    __syncthreads();
-    const int64_t lim = a + kSegCap < n ? a + kSegCap : n;
-    for (int64_t k = w1 + tid; k < lim + 1 && k <= n; k += kSegThreads)
-        if (k == n || seg_head(S, PME, k)) atomicMin(&found, (unsigned long long)k);
-    __syncthreads();
-    const int64_t b = (int64_t)found;
-    if (found == ~0ull || b - a > kSegCap) {   // segments past the LDS capacity
-        if (tid == 0) atomicOr(overflow, 1u);
-        return;
-    }
-    const int len = (int)(b - a);
-    for (int i = tid; i < len; i += kSegThreads) {
-        sS[i] = S[a + i];
-        sE[i] = E[a + i];
-        sP[i] = PME[a + i];
-        sM[i] = M[a + i];
-        sK[i] = 0;
-    }
-    int cur = 0x7fffffff;   // levels below this one are still undecided
-    for (;;) {
-        if (tid == 0) lvl = -1;
+    const int64_t nwin = LARGE ? (int64_t)*ovf_n : (int64_t)gridDim.x;
+    for (int64_t q = blockIdx.x; q < nwin; q += LARGE ? (int64_t)gridDim.x : nwin) {
+        const int64_t w = LARGE ? (int64_t)ovf_win[q] : q;
+        const int64_t w0 = w * kSegWin;
+        const int64_t w1 = w0 + kSegWin < n ? w0 + kSegWin : n;
+        // a = the window's first segment head (none: a segment from an earlier window covers it)
+        if (tid == 0) found = ~0ull;
         __syncthreads();
-        int mx = -1;
-        for (int i = tid; i < len; i += kSegThreads)
-            if (sM[i] < cur && sM[i] > mx) mx = sM[i];
-        if (mx >= 0) atomicMax(&lvl, mx);
+        for (int64_t k = w0 + tid; k < w1; k += T)
+            if (seg_head(S, PME, k)) atomicMin(&found, (unsigned long long)k);
         __syncthreads();
-        const int m = lvl;   // uniform
-        if (m < 0) break;
-        for (int i = tid; i < len; i += kSegThreads) {
-            if (sM[i] != m) continue;
-            const int64_t s0 = sS[i], e0 = sE[i], rl = e0 - s0;
-            bool nested = false;
-            if (rl > 0) {
-                int lo = i + 1, hi = len;   // first local rank with S >= e0 (S[i] = s0 < e0)
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (sS[mid] < e0) lo = mid + 1;
-                    else hi = mid;
-                }
-                for (int k = lo - 1; k >= 0 && sP[k] > s0; --k) {
-                    const int64_t Mk = sM[k];
-                    if (Mk <= m || !sK[k]) continue;   // this level's entries are being written now: never read
-                    if (nested_by(s0, e0, m, rl, sS[k], sE[k], Mk, thr)) { nested = true; break; }
-                }
+        const int64_t a = (int64_t)found;   // uniform
+        __syncthreads();
+        if (a == (int64_t)~0ull) continue;
+        // b = the first segment head at or after w1 (n if none), looked for up to a + CAP
+        if (tid == 0) found = ~0ull;
+        __syncthreads();
+        const int64_t lim = a + CAP < n ? a + CAP : n;
+        for (int64_t k = w1 + tid; k <= lim; k += T)
+            if (k == n || seg_head(S, PME, k)) atomicMin(&found, (unsigned long long)k);
+        __syncthreads();
+        const int64_t b = (int64_t)found;
+        __syncthreads();
+        if (b == (int64_t)~0ull || b - a > CAP) {   // the window's segments do not fit
+            if (tid == 0) {
+                if (LARGE) atomicOr(fallback, 1u);
+                else ovf_win[atomicAdd(ovf_n, 1u)] = (uint32_t)w;
             }
-            sK[i] = nested ? 0 : 1;
+            continue;
         }
-        cur = m;
-        __syncthreads();
+        const int len = (int)(b - a);
+        for (int i = tid; i < len; i += T) {
+            sS[i] = S[a + i];
+            sE[i] = E[a + i];
+            sP[i] = PME[a + i];
+            sM[i] = M[a + i];
+            sK[i] = 0;
+        }
+        int cur = 0x7fffffff;   // levels below this one are still undecided
+        for (;;) {
+            if (tid == 0) lvl = -1;
+            __syncthreads();
+            int mx = -1;
+            for (int i = tid; i < len; i += T)
+                if (sM[i] < cur && sM[i] > mx) mx = sM[i];
+            if (mx >= 0) atomicMax(&lvl, mx);
+            __syncthreads();
+            const int m = lvl;   // uniform
+            if (m < 0) break;
+            for (int i = tid; i < len; i += T) {
+                if (sM[i] != m) continue;
+                const int64_t s0 = sS[i], e0 = sE[i], rl = e0 - s0;
+                bool nested = false;
+                if (rl > 0) {
+                    int lo = i + 1, hi = len;   // first local rank with S >= e0 (S[i] = s0 < e0)
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (sS[mid] < e0) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    for (int k = lo - 1; k >= 0 && sP[k] > s0; --k) {
+                        const int64_t Mk = sM[k];
+                        if (Mk <= m || !sK[k]) continue;   // this level's entries are being written now: never read
+                        if (nested_by(s0, e0, m, rl, sS[k], sE[k], Mk, thr)) { nested = true; break; }
+                    }
+                }
+                sK[i] = nested ? 0 : 1;
+            }
+            cur = m;
+            __syncthreads();
+        }
+        for (int i = tid; i < len; i += T) kept[a + i] = sK[i];
+        __syncthreads();   // the LDS is refilled by the next window
     }
-    for (int i = tid; i < len; i += kSegThreads) kept[a + i] = sK[i];
 }
 
 // one level (all hits of one primitive length m): nested test against the
@@ -484,12 +499,16 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     prefix_max(c, E, PME, n, c.slot[S_IDX5].as<int64_t>());
     // every level, segment by segment, in one launch (BWTMI_SEG_LEVELS=0: per-level launches)
     static const bool seg_levels = [] { const char *e = std::getenv("BWTMI_SEG_LEVELS"); return !(e && *e == '0'); }();
-    unsigned int *d_ovf = reinterpret_cast<unsigned int *>(d_max);
+    unsigned int *d_ovf = reinterpret_cast<unsigned int *>(d_max);   // [0] fallback flag, [1] overflow windows
     unsigned int ovf = 1;
     if (seg_levels) {
-        HIPCHECK(hipMemsetAsync(d_ovf, 0, 4, st));
-        KLAUNCH("k_seg_levels", 0.0, k_seg_levels, dim3((unsigned)((n + kSegWin - 1) / kSegWin)), dim3(kSegThreads), 0,
-                st, S, E, M, PME, n, kept, d_ovf, 0.5);
+        const int64_t nwin = (n + kSegWin - 1) / kSegWin;
+        uint32_t *ovf_win = pos;   // the final-pass scan buffer is free until then (n + 1 words >= nwin)
+        HIPCHECK(hipMemsetAsync(d_ovf, 0, 8, st));
+        KLAUNCH("k_seg_levels", 0.0, (k_seg_levels<256, kSegCapS, false>), dim3((unsigned)nwin), dim3(256), 0, st, S, E,
+                M, PME, n, kept, ovf_win, d_ovf + 1, d_ovf, 0.5);
+        KLAUNCH("k_seg_levels_l", 0.0, (k_seg_levels<1024, kSegCapL, true>), dim3(256), dim3(1024), 0, st, S, E, M, PME,
+                n, kept, ovf_win, d_ovf + 1, d_ovf, 0.5);
         HIPCHECK(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
     }
