@@ -1263,9 +1263,13 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
             n_collapsed += part[(size_t)t].size();
         }
         t_collapse = clk::now();
-        out.resize((size_t)cnt[(size_t)C]);
+        {
+            DeferConstruct raw;   // constructed below, in parallel
+            out.resize((size_t)cnt[(size_t)C]);
+        }
         parallel_items(C, nt, [&](int64_t t, int) {
             int64_t o = cnt[(size_t)t];
+            for (int64_t q = o; q < cnt[(size_t)t + 1]; ++q) ::new ((void *)&out[(size_t)q]) Rec();
             for (uint32_t i : part[(size_t)t])
                 if (pass(i)) materialize(u, recs[i], shift, out[(size_t)o++]);
         });
@@ -1365,9 +1369,13 @@ void postprocess(Job &job) {
     } else {   // the units' records moved into place in parallel
         std::vector<size_t> at(res.size() + 1, 0);
         for (size_t k = 0; k < res.size(); ++k) at[k + 1] = at[k] + res[k].size();
-        job.final_recs.resize(tot);
+        {
+            DeferConstruct raw;   // move-constructed below, in parallel
+            job.final_recs.resize(tot);
+        }
         run_tasks((int64_t)res.size(), T, [&](int64_t k) {
-            std::move(res[(size_t)k].begin(), res[(size_t)k].end(), job.final_recs.begin() + (std::ptrdiff_t)at[(size_t)k]);
+            Rec *d = job.final_recs.data() + at[(size_t)k];
+            for (Rec &r : res[(size_t)k]) ::new ((void *)d++) Rec(std::move(r));
         });
     }
     // the units' emptied vectors are released behind the next stage
