@@ -159,6 +159,9 @@ char canonical_strand(const char *s, int64_t n);   // the strand of canonical_st
 bool pack2_acgt(const char *s, int64_t n, uint64_t &x);
 uint64_t rc2(uint64_t x, int64_t n);
 uint64_t min_rot2(uint64_t x, int64_t n);
+// canonical word (min over rotations of the motif and its reverse complement)
+// of an ACGT motif of 33..64 bases; false if it has another symbol
+bool canon_key128(const char *s, int64_t n, unsigned __int128 &key);
 int64_t smallest_period(const char *s, int64_t n);
 double entropy_of(const char *s, int64_t n);
 void composition_of(const char *s, int64_t n, double out[4]);

@@ -64,22 +64,34 @@ static inline char comp_base(char c) {       // bwt.py:688-691
     }
 }
 
+// 2-bit code of a byte (A0 C1 G2 T3), 4 for every other byte
+static const struct Code2 {
+    uint8_t v[256];
+    Code2() {
+        for (int b = 0; b < 256; ++b) v[b] = 4;
+        v['A'] = 0;
+        v['C'] = 1;
+        v['G'] = 2;
+        v['T'] = 3;
+    }
+} kCode2;
+
 bool pack2_acgt(const char *s, int64_t n, uint64_t &x) {
     if (n > 32) return false;
-    x = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        uint64_t c;
-        switch (s[i]) {
-            case 'A': c = 0; break;
-            case 'C': c = 1; break;
-            case 'G': c = 2; break;
-            case 'T': c = 3; break;
-            default: return false;
-        }
-        x = (x << 2) | c;
+    uint64_t y = 0;
+    unsigned bad = 0;
+    for (int64_t i = 0; i < n; ++i) {   // branch-free: the invalid bit is checked once
+        const unsigned c = kCode2.v[(uint8_t)s[i]];
+        bad |= c;
+        y = (y << 2) | (c & 3u);
     }
-    return true;
+    x = y;
+    return (bad & 4u) == 0;
 }
+
+// canonical word of an ACGT motif of 33..64 bases (least rotation of the
+// motif and of its reverse complement, as 128-bit 2-bit words)
+bool canon_key128(const char *s, int64_t n, unsigned __int128 &key);
 
 uint64_t rc2(uint64_t x, int64_t n) {
     x = ~x;   // complement: 3 - code
@@ -123,6 +135,14 @@ static u128 min_rot2_128(u128 x, int64_t n) {
         best = r < best ? r : best;
     }
     return best;
+}
+
+bool canon_key128(const char *s, int64_t n, unsigned __int128 &key) {
+    u128 y;
+    if (!pack2_acgt128(s, n, y)) return false;
+    const u128 f = min_rot2_128(y, n), r = min_rot2_128(rc2_128(y, n), n);
+    key = f < r ? f : r;
+    return true;
 }
 
 void canonical_stranded(const std::string &s, std::string &canon, char &strand) {  // 694-716

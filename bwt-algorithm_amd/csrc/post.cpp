@@ -721,7 +721,7 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
 // fail the distance test first.
 struct Canon {
     std::string s;     // canonical string (motifs that do not pack)
-    uint64_t key = 0;  // packed canonical word of an ACGT motif <= 32 bases
+    unsigned __int128 key = 0;  // packed canonical word of an ACGT motif <= 64 bases
     int32_t len = -1;  // motif length; -1 = not computed yet
     bool packed = false;
     bool ok = false;
@@ -740,6 +740,8 @@ inline void canon_fill(const UnitCtx &u, const Item &it, Canon &c) {
     if (c.packed) {
         const uint64_t f = min_rot2(x, (int64_t)mv.size()), r = min_rot2(rc2(x, (int64_t)mv.size()), (int64_t)mv.size());
         c.key = f < r ? f : r;
+    } else if (mv.size() > 32 && mv.size() <= 64 && canon_key128(mv.data(), (int64_t)mv.size(), c.key)) {
+        c.packed = true;   // same length on both sides (same_canonical), so the 64- and 128-bit keys never meet
     } else {
         thread_local std::string tmp;
         tmp.assign(mv.data(), mv.size());

@@ -396,9 +396,10 @@ struct Out {
         *w++ = ch;
     }
     void f(const char *fmt, double x) {   // printf keeps Python's exact-value rounding
-        if (fmt[1] == '.' && fmt[2] == '0' && fmt[3] == 'f' && x == std::floor(x) && std::fabs(x) < 1e15 &&
-            !(x == 0.0 && std::signbit(x))) {
-            i((int64_t)x);   // an integral value prints as that integer under %.0f
+        if (fmt[1] == '.' && fmt[2] == '0' && fmt[3] == 'f' && std::fabs(x) < 1e15 && !std::signbit(x)) {
+            // %.0f rounds the exact binary value to nearest, ties to even --
+            // nearbyint in the default rounding mode, without printf
+            i((int64_t)std::nearbyint(x));
             return;
         }
         char b[64];
