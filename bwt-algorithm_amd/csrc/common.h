@@ -171,7 +171,7 @@ struct AlignSummary {
     bool want_copies = true;                  // fill copy_len / copy_err (bwtmi_align_region)
     std::vector<int64_t> copy_len, copy_err;  // per copy: consumed bases, errors
     std::string consensus;
-    int64_t motif_len = 0, copies = 0, consumed = 0, max_errors = 0, tot_ins = 0, tot_del = 0;
+    int64_t motif_len = 0, copies = 0, consumed = 0, max_errors = 0, tot_ins = 0, tot_del = 0, tot_err = 0;
     double mismatch_rate = 0.0;
     std::string variations;  // ';'-joined
     bool any_variation = false;
@@ -188,6 +188,24 @@ void align_scratch_free(AlignScratch *);
 bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_t end,
                          const std::string &tmpl, int64_t min_copies, AlignSummary &out, double frac,
                          int64_t max_indel_arg, AlignScratch *ws);
+
+// _recompute_repeat's alignment (bwt.py:3530-3534: align_repeat_region with
+// min_copies, then with 1) of a batch of regions on the device (recompute.hip)
+struct RcReq {
+    const char *text;             // device copy of the contig's trimmed sequence
+    int64_t text_len, start, end;  // start / end as align_repeat_region receives them
+    int32_t m, min_copies;         // template = text[start, start + m), 2 <= m <= kRcMaxMotif
+};
+struct RcOut {
+    int32_t status;    // 1 aligned, 0 neither attempt aligned, -1 past a device bound (host recomputes)
+    int32_t str_len;   // consensus (m bytes) then the variations, at arena[str_off]
+    int64_t str_off;
+    int64_t copies, consumed;
+    int32_t tot_err, max_err, tot_ins, tot_del;
+};
+constexpr int32_t kRcMaxMotif = 256;
+// runs a batch to completion: out[k] for every req[k], strings into arena
+using RcBatchFn = std::function<void(const RcReq *, int64_t, RcOut *, std::vector<char> &)>;
 
 // ---------------------------------------------------------------- job
 // formatted text in cached huge-page blocks (mem.h)
@@ -225,6 +243,10 @@ struct Job {
     Seq part;
     std::string part_path;
     int64_t part_a = 0, part_b = 0, part_stamp[2] = {-1, -1};
+    // the merge fold's DP recomputes on the device (set by bwtmi_job_postprocess
+    // when the contigs are resident on a device; rc_text[c] = contig c's copy or null)
+    RcBatchFn rc_batch;
+    std::vector<const char *> rc_text;
     void assign_units();
 };
 

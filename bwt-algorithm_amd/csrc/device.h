@@ -264,6 +264,10 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
 void strict_scan_mm_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
                            int32_t max_mismatch, int32_t min_copies, HitVec &hits);
 
+// ----- the merge fold's DP recomputes, one wavefront per region (recompute.hip);
+// returns after the batch completed (out[] and arena on the host)
+void recompute_batch_device(Ctx &c, const RcReq *req, int64_t nreq, RcOut *out, std::vector<char> &arena);
+
 // ----- nested suppression / sort / dedup of one contig's strict hits (nested.hip)
 void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
                         ScreenedVec &out);

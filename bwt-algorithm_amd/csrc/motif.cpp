@@ -661,6 +661,7 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
         out.consumed = copies;
         out.mismatch_rate = 0.0;
         out.max_errors = 0;
+        out.tot_err = 0;
         out.tot_ins = 0;
         out.tot_del = 0;
         return true;
@@ -761,6 +762,7 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
     out.consumed = consumed;
     out.mismatch_rate = denom > 0 ? (double)tot_err / (double)denom : 0.0;
     out.max_errors = max_err;
+    out.tot_err = tot_err;
     out.tot_ins = tot_ins;
     out.tot_del = tot_del;
     return true;

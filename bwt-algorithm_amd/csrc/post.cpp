@@ -399,10 +399,23 @@ struct Pools {
     }
 };
 
+// the merge fold's recomputes for neighbour pairs (R[i-1], R[i]) met with a
+// fresh current record, run on the device before the fold (merge_fold)
+struct RcTable {
+    std::vector<int32_t> at;   // at[i]: request of the pair (R[i-1], R[i]), -1 none
+    // canonical words the pass computed: kst[i] = 1: key[i] is R[i]'s packed canonical form
+    std::vector<unsigned __int128, BigAlloc<unsigned __int128>> key;
+    std::vector<uint8_t, BigAlloc<uint8_t>> kst;
+    std::vector<RcReq> req;
+    std::vector<RcOut> out;
+    std::vector<char> arena;
+};
+
 struct UnitCtx {
     const Job *job;
     int64_t min_copies;
-    bool restored = false;   // items are in full-sequence coordinates (multi-offset units)
+    bool restored = false;        // items are in full-sequence coordinates (multi-offset units)
+    const RcTable *rc = nullptr;  // merge_fold only
 };
 
 inline std::string_view motif_of(const UnitCtx &u, const Item &it) {
@@ -577,6 +590,17 @@ std::atomic<int64_t> g_hist_n[8][8], g_hist_ns[8][8];
 std::atomic<int64_t> g_fresh_tests{0}, g_chain_tests{0}, g_fresh_merges{0}, g_chain_merges{0};   // [log4 motif len][log4 region len]
 inline int lg4(int64_t v) { int k = 0; while (v >= 4 && k < 7) { v >>= 2; ++k; } return k; }
 
+// align_repeat_region's result as _recompute_repeat reads it (host AlignSummary
+// or a device RcOut)
+struct RcView {
+    bool ok = false;
+    int64_t consumed = 0, copies = 0, motif_len = 0, max_err = 0, tot_ins = 0, tot_del = 0;
+    double mm = 0.0;
+    std::string_view consensus, var;
+};
+Item item_of_alignment(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t start, int64_t end, int64_t m,
+                       int32_t tier, std::string_view tmpl, const RcView &v);
+
 // bwt.py:3515-3614 (on the trimmed sequence, before coordinate restore)
 Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t start, int64_t end,
                int64_t motif_len, int32_t tier) {
@@ -661,32 +685,54 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     s.want_copies = false;
     bool ok = align_repeat_region(seq, L, start, end, tmpl, std::max<int64_t>(1, u.min_copies), s, 0.1, -1, A.as.get());
     if (!ok) ok = align_repeat_region(seq, L, start, end, tmpl, 1, s, 0.1, -1, A.as.get());
+    RcView v;
+    v.ok = ok;
+    if (ok) {
+        v.consumed = s.consumed;
+        v.copies = s.copies;
+        v.motif_len = s.motif_len;
+        v.max_err = s.max_errors;
+        v.tot_ins = s.tot_ins;
+        v.tot_del = s.tot_del;
+        v.mm = s.mismatch_rate;
+        v.consensus = s.consensus;
+        if (s.any_variation) v.var = s.variations;
+    }
+    return item_of_alignment(u, pools, w, chrom, start, end, m, tier, tmpl, v);
+}
+
+// the record _recompute_repeat builds from an alignment (bwt.py:3536-3614)
+Item item_of_alignment(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t start, int64_t end, int64_t m,
+                       int32_t tier, std::string_view tmpl, const RcView &v) {
+    const Contig &c = u.job->contigs[(size_t)chrom];
+    const int64_t L = c.trimmed_len();
+    const int64_t req_end = end;
     Extra x;
     int64_t consumed, cint;
     double mm, pind;
-    const std::string *motif_s = &tmpl;   // never empty
+    std::string_view motif_s = tmpl;   // never empty
     std::string_view var_s;
-    if (!ok) {
+    if (!v.ok) {
         consumed = std::min(L - start, std::max(m, end - start));
         cint = std::max<int64_t>(1, consumed / m);
         mm = 0.0;
         x.max_mm = 0;
         pind = 0.0;
     } else {
-        consumed = s.consumed;
-        cint = s.copies;
-        if (!s.consensus.empty()) motif_s = &s.consensus;
-        mm = s.mismatch_rate;
-        const int64_t tb = s.copies * s.motif_len;
-        const double ir = tb > 0 ? (double)(s.tot_ins + s.tot_del) / (double)tb : 0.0;
+        consumed = v.consumed;
+        cint = v.copies;
+        if (!v.consensus.empty()) motif_s = v.consensus;
+        mm = v.mm;
+        const int64_t tb = v.copies * v.motif_len;
+        const double ir = tb > 0 ? (double)(v.tot_ins + v.tot_del) / (double)tb : 0.0;
         pind = ir * 100.0;
-        x.max_mm = s.max_errors;
-        if (s.any_variation) var_s = s.variations;
+        x.max_mm = v.max_err;
+        var_s = v.var;
     }
     // actual_sequence = sequence[start:start+consumed]
     const int64_t a0 = std::min(start, L), a1 = std::max(a0, std::min(start + consumed, L));
     const int64_t tl = a1 - a0;
-    const int64_t mle = (int64_t)motif_s->size();
+    const int64_t mle = (int64_t)motif_s.size();
     double cf = (double)cint;
     if (tl > 0 && mle > 0) {
         const double fr = (double)tl / (double)mle;
@@ -697,7 +743,7 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     x.confidence = std::max(0.3, 1.0 - mm);
     x.mm = mm;
     x.n_eval = std::max<int64_t>(1, cint);
-    x.strand = canonical_strand(motif_s->data(), (int64_t)motif_s->size());
+    x.strand = canonical_strand(motif_s.data(), (int64_t)motif_s.size());
     x.pmatch = std::max(0.0, 100.0 - mm * 100.0);
     x.pindel = pind;
     x.score = trf_score(tl, mm);
@@ -708,8 +754,8 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     it.start = start;
     it.end = start + tl;
     it.chrom = chrom;
-    it.mlen = (int32_t)motif_s->size();
-    it.x = pools.add(w, x, *motif_s, var_s);
+    it.mlen = (int32_t)motif_s.size();
+    it.x = pools.add(w, x, motif_s, var_s);
     return it;
 }
 
@@ -765,8 +811,41 @@ inline bool same_canonical(const UnitCtx &u, const Item &r1, Canon &c1, const It
     return c1.packed ? c1.key == c2.key : c1.s == c2.s;
 }
 
+// the pair's device result when r1 is the fresh R[pair - 1] and r2 = R[pair]
+// (the request was built from the same two records, so its arguments are this
+// call's), else the host recompute
+inline Item recompute_pair(const UnitCtx &u, Pools &pools, int w, int64_t pair, int32_t chrom, int64_t s, int64_t e,
+                           int64_t m, int32_t tier) {
+    if (pair >= 0 && u.rc) {
+        const int32_t k = u.rc->at[(size_t)pair];
+        if (k >= 0 && u.rc->out[(size_t)k].status >= 0) {
+            const RcReq &q = u.rc->req[(size_t)k];
+            const RcOut &o = u.rc->out[(size_t)k];
+            const Contig &c = u.job->contigs[(size_t)chrom];
+            const std::string_view tmpl(c.trimmed() + q.start, (size_t)q.m);
+            RcView v;
+            v.ok = o.status == 1;
+            if (v.ok) {
+                v.consumed = o.consumed;
+                v.copies = o.copies;
+                v.motif_len = q.m;
+                v.max_err = o.max_err;
+                v.tot_ins = o.tot_ins;
+                v.tot_del = o.tot_del;
+                const int64_t denom = o.copies * (int64_t)q.m;
+                v.mm = denom > 0 ? (double)o.tot_err / (double)denom : 0.0;
+                const char *str = u.rc->arena.data() + o.str_off;
+                v.consensus = std::string_view(str, (size_t)q.m);
+                v.var = std::string_view(str + q.m, (size_t)(o.str_len - q.m));
+            }
+            return item_of_alignment(u, pools, w, chrom, q.start, q.end, m, tier, tmpl, v);
+        }
+    }
+    return recompute(u, pools, w, chrom, s, e, m, tier);
+}
+
 bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, Canon &c1, const Item &r2, Canon &c2,
-               Item &merged) {
+               Item &merged, int64_t pair = -1) {
     if (r1.chrom != r2.chrom) return false;
     if (r1.mlen == 0 || r2.mlen == 0) return false;
     const int64_t ml = std::min(r1.mlen, r2.mlen);
@@ -776,7 +855,7 @@ bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, Canon &c1,
     if (g_counters) g_same.fetch_add(1, std::memory_order_relaxed);
     const int64_t s = std::min(r1.start, r2.start), e = std::max(r1.end, r2.end);
     const int32_t tier = std::min(tier_of(r1), tier_of(r2));
-    Item mg = recompute(u, pools, w, r1.chrom, s, e, std::max<int64_t>(1, ml), tier);
+    Item mg = recompute_pair(u, pools, w, pair, r1.chrom, s, e, std::max<int64_t>(1, ml), tier);
     if (mg.x->copies < (double)u.min_copies) return false;
     const double base = std::max(std::max(mm_of(r1), mm_of(r2)), 0.01);
     if (!(mg.x->mm <= base + 0.2)) return false;
@@ -826,8 +905,12 @@ void spec_run(const UnitCtx &u, Pools &pools, int w, const ItemVec &R, int64_t b
     for (int64_t i = b + 1; i < e; ++i) {
         Canon &cc = cb[ci_cur], &ci = cb[ci_cur ^ 1];
         ci.ok = false;
+        if (u.rc && u.rc->kst[(size_t)i]) {   // computed by rc_prepare
+            ci.key = u.rc->key[(size_t)i];
+            ci.packed = ci.ok = true;
+        }
         if (g_counters) (merged ? g_chain_tests : g_fresh_tests).fetch_add(1, std::memory_order_relaxed);
-        if (try_merge(u, pools, w, cur, cc, R[(size_t)i], ci, mg)) {
+        if (try_merge(u, pools, w, cur, cc, R[(size_t)i], ci, mg, merged ? -1 : i)) {
             if (g_counters) (merged ? g_chain_merges : g_fresh_merges).fetch_add(1, std::memory_order_relaxed);
             cur = mg;
             merged = true;
@@ -867,11 +950,91 @@ inline void refine_one(const UnitCtx &u, Pools &pools, int w, Item &r) {
     r = recompute(u, pools, w, r.chrom, r.start, r.end, m, tier_of(r));
 }
 
+// The requests of every neighbour pair (R[i-1], R[i]) that try_merge would
+// recompute with a fresh current record (same contig, gap test, same canonical
+// motif; bwt.py:3240-3262) and a motif of 2..kRcMaxMotif bases, run as one
+// device batch.  Pairs the fold never tests with a fresh record cost device
+// time only; the one-base motifs keep their closed form on the host.
+void rc_prepare(const UnitCtx &u, const ItemVec &R, int nt, RcTable &T) {
+    const Job &job = *u.job;
+    const int64_t n = (int64_t)R.size();
+    T.at.assign((size_t)n, -1);
+    T.key.resize((size_t)n);
+    T.kst.assign((size_t)n, 0);
+    const int C = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)nt * 4, n / 4096 + 1));
+    std::vector<std::vector<std::pair<int64_t, RcReq>>> part((size_t)C);
+    const int32_t mc = (int32_t)std::max<int64_t>(1, u.min_copies);
+    parallel_items(C, nt, [&](int64_t t, int) {
+        auto &out = part[(size_t)t];
+        Canon cb[2];
+        int64_t have = -1;   // R index whose canonical form is in cb[have & 1]
+        const int64_t lo = n * t / C;
+        auto keep = [&](int64_t k, const Canon &c) {   // records of this chunk only
+            if (k >= lo && c.ok && c.packed && !T.kst[(size_t)k]) {
+                T.key[(size_t)k] = c.key;
+                T.kst[(size_t)k] = 1;
+            }
+        };
+        for (int64_t i = std::max<int64_t>(1, lo); i < n * (t + 1) / C; ++i) {
+            const Item &r1 = R[(size_t)i - 1], &r2 = R[(size_t)i];
+            if (r1.chrom != r2.chrom || r1.mlen == 0 || r2.mlen == 0) continue;
+            const int64_t ml = std::min(r1.mlen, r2.mlen);
+            if (std::max<int64_t>(0, r2.start - r1.end) > ml + 1) continue;
+            const int64_t m = std::max<int64_t>(1, ml);
+            if (m < 2 || m > kRcMaxMotif) continue;
+            const char *text = (size_t)r1.chrom < job.rc_text.size() ? job.rc_text[(size_t)r1.chrom] : nullptr;
+            if (!text) continue;
+            Canon &c1 = cb[(i - 1) & 1], &c2 = cb[i & 1];
+            if (have != i - 1) c1.ok = false;
+            c2.ok = false;
+            have = i;
+            const bool same = same_canonical(u, r1, c1, r2, c2);
+            keep(i - 1, c1);
+            keep(i, c2);
+            if (!same) continue;
+            const Contig &c = job.contigs[(size_t)r1.chrom];
+            const int64_t L = c.trimmed_len();
+            const int64_t start = std::max<int64_t>(0, std::min(r1.start, r2.start));
+            const int64_t e = std::max(r1.end, r2.end);
+            int64_t end = e > 0 ? std::min(L, e) : L;
+            if (end <= start) end = std::min(L, start + m);
+            if (start + m > L) continue;
+            out.push_back({i, RcReq{text, L, start, end, (int32_t)m, mc}});
+        }
+    });
+    size_t tot = 0;
+    for (auto &p : part) tot += p.size();
+    T.req.resize(tot);
+    size_t k = 0;
+    for (auto &p : part)
+        for (auto &e : p) {
+            T.at[(size_t)e.first] = (int32_t)k;
+            T.req[k++] = e.second;
+        }
+    T.out.resize(tot);
+    if (tot) job.rc_batch(T.req.data(), (int64_t)tot, T.out.data(), T.arena);
+}
+
 // the fold's output, refined (the refine pass runs inside the parallel
 // assembly: records are independent there)
-ItemVec merge_fold(const UnitCtx &u, Pools &pools, const ItemVec &R, int nt) {
+ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt) {
     const int64_t n = (int64_t)R.size();
     if (n == 0) return {};
+    // BWTMI_POST_DEVICE_MIN: smallest unit (records) whose fresh-pair recomputes go to the device
+    static const int64_t dev_min = [] {
+        const char *e = std::getenv("BWTMI_POST_DEVICE_MIN");
+        return e && *e ? std::atoll(e) : (int64_t)20000;
+    }();
+    RcTable rc;
+    UnitCtx u = u0;
+    if (u0.job->rc_batch && n >= dev_min) {
+        auto tr0 = std::chrono::steady_clock::now();
+        rc_prepare(u0, R, nt, rc);
+        u.rc = &rc;
+        if (g_stats)
+            std::fprintf(stderr, "  merge device recomputes: %zu in %.1f ms\n", rc.req.size(),
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count());
+    }
     const int64_t K = std::max<int64_t>(1, std::min<int64_t>((int64_t)nt * 8, n / 2048 + 1));
     std::vector<int64_t> cut((size_t)K + 1);
     for (int64_t k = 0; k <= K; ++k) cut[(size_t)k] = n * k / K;
