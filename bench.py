@@ -222,6 +222,8 @@ def main():
     ap.add_argument("--no-fm", action="store_true", help="skip the all-motif FM search report")
     ap.add_argument("--no-cli", action="store_true", help="skip the in-process drop-in CLI timing")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
+    ap.add_argument("--host-load", action="store_true",
+                    help="whole-file load on the host + upload (default: built on the device from the file image)")
     ap.add_argument("--pmc-summary", default=PMC_SUMMARY,
                     help="tools/pmc_traffic.py output giving HBM bytes per launch (roofline.traffic)")
     a = ap.parse_args()
@@ -281,7 +283,10 @@ def main():
     def step():
         timed("reset", job.reset)
         # shared FASTA over N ranks: each scans 1/N of it, the part tables are all-gathered
-        timed("load_fasta", job.load_fasta, fa, FLANK, load_world, load_rank, c if load_world > 1 else None)
+        # one whole file: the sequences are built on the device from the file image
+        # and the host copy is written behind the scan (bwtmi_job_load_fasta_dev)
+        timed("load_fasta", job.load_fasta, fa, FLANK, load_world, load_rank, c if load_world > 1 else None,
+              ctx if load_world == 1 and not a.host_load else None)
         timed("upload", job.upload, ctx)
         timed("scan", job.scan, ctx)
         timed("postprocess", job.postprocess)
@@ -400,7 +405,8 @@ def main():
                        "C5": "one 100 Mbp contig with 0.02 substitutions in the planted arrays, --progress"}[wl_name]
                    + "; FASTA read -> FM index + strict scan + post-processing -> STRfinder repeat.tab closed",
                    "contig_bp": wl["lengths"][0], "contigs": len(wl["lengths"]) * (1 if shared else world),
-                   "parallelism": f"contig-shard x{world}", "index": not a.no_index},
+                   "parallelism": f"contig-shard x{world}", "index": not a.no_index,
+                   "load": "device" if load_world == 1 and not a.host_load else "host"},
         "roofline": roofline,
         "e2e_roofline": {"b_alg_bytes_per_base": B_ALG_PER_BASE, "achieved_gbs": round(e2e_gbs, 2),
                          "peak_gbs": HBM_PEAK_GBS * world, "frac": round(e2e_gbs / (HBM_PEAK_GBS * world), 6)},

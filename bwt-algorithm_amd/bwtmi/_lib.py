@@ -106,6 +106,8 @@ _SIGS = {
     "bwtmi_align_regions": (C.c_int, [_P, C.c_char_p, C.c_int64, _P, C.c_int64, C.c_int64, _P,
                                       C.POINTER(C.c_void_p), _P]),
     "bwtmi_job_load_fasta": (C.c_int, [_P, C.c_char_p, C.c_int32]),
+    "bwtmi_job_load_fasta_dev": (C.c_int, [_P, _P, C.c_char_p, C.c_int32]),
+    "bwtmi_job_device_text": (C.c_int, [_P, _P, C.c_int32, C.c_void_p]),
     "bwtmi_job_contig_count": (C.c_int32, [_P]),
     "bwtmi_job_contig_info": (C.c_int64, [_P, C.c_int32, C.c_char_p, C.c_int64, C.POINTER(C.c_int64),
                                           C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),

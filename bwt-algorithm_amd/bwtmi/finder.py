@@ -131,7 +131,16 @@ class TandemRepeatFinder:
 
     def load_reference(self) -> Dict[str, str]:
         job = self._new_job()
-        job.load_fasta(self.reference_file, self.flank_trim)
+        # with a device the analysed sequences are built there from the file
+        # image and the host copies are written behind the scan
+        # (bwtmi_job_load_fasta_dev); BWTMI_HOST_LOAD=1 loads on the host only
+        dev = None
+        if os.environ.get("BWTMI_HOST_LOAD", "0") != "1":
+            try:
+                dev = _lib.ctx(self.device) if _lib.device_count() > 0 else None
+            except _lib.BwtmiError:
+                dev = None
+        job.load_fasta(self.reference_file, self.flank_trim, dev_ctx=dev)
         self.job = job
         self.full_sequences = _ContigMap(job, trimmed=False)
         self.sequences = _ContigMap(job, trimmed=True)

@@ -126,12 +126,18 @@ class Job:
         self.names.append(name)
         return cid.value
 
-    def load_fasta(self, path: str, flank_trim: int, world: int = 1, rank: int = 0, comm=None) -> None:
+    def load_fasta(self, path: str, flank_trim: int, world: int = 1, rank: int = 0, comm=None,
+                   dev_ctx=None) -> None:
         """load_reference (bwt.py:3713-3756), natively; with world > 1 only this
         rank's fold units get their bases (and the job is restricted to them).
         With a communicator (bwtmi.comm) no rank reads the whole file: each scans
-        its 1/world, the part tables are all-gathered, each reads its own contigs."""
-        if world > 1 and comm is not None:
+        its 1/world, the part tables are all-gathered, each reads its own contigs.
+        With a device context (whole file only) the analysed sequences are built
+        on the device from the file image and the host copies are written behind
+        the next scan (bwtmi_job_load_fasta_dev): upload() has nothing left to do."""
+        if dev_ctx is not None and world <= 1:
+            check(lib().bwtmi_job_load_fasta_dev(dev_ctx, self.h, path.encode(), flank_trim))
+        elif world > 1 and comm is not None:
             from . import comm as _comm
             blob, nw = C.c_void_p(), C.c_int64()
             check(lib().bwtmi_job_fasta_scan_part(self.h, path.encode(), world, rank, C.byref(blob), C.byref(nw)))
@@ -175,6 +181,14 @@ class Job:
         buf = C.create_string_buffer(max(fl, 1))
         check(lib().bwtmi_job_contig_seq(self.h, i, buf))
         return buf.raw[:fl]
+
+    def device_text(self, dev_ctx, i: int) -> bytes:
+        """The device copy of contig i's analysed (trimmed) sequence."""
+        _, fl, tl, tr = self.contig_info(i)
+        n = fl - tl - tr
+        buf = C.create_string_buffer(max(n, 1))
+        check(lib().bwtmi_job_device_text(dev_ctx, self.h, i, buf))
+        return buf.raw[:n]
 
     # pipeline -----------------------------------------------------------
     def upload(self, dev_ctx) -> None:

@@ -181,6 +181,9 @@ struct bwtmi_job {
     JobDev dev;
 };
 
+// readers of contig bytes join a deferred host pass first (bwtmi_job_load_fasta_dev)
+#define TEXT_JOIN(job) const_cast<bwtmi_job *>(job)->j.text_join()
+
 #define CHECK_ARG(cond, msg)                     \
     do {                                         \
         if (!(cond)) fail(BWTMI_E_ARG, "%s", msg); \
@@ -502,6 +505,7 @@ int bwtmi_index_long_repeats(bwtmi_ctx *ctx, bwtmi_index *idx, const bwtmi_lib_p
 int bwtmi_job_tier1(bwtmi_ctx *ctx, bwtmi_job *job, int32_t contig_id, int32_t max_motif_length) {
     return guard([&] {
         CHECK_ARG(ctx && job, "null argument");
+        TEXT_JOIN(job);
         CHECK_ARG(contig_id >= 0 && contig_id < (int32_t)job->j.contigs.size(), "bad contig id");
         Ctx &c = ctx->c;
         use(c);
@@ -528,6 +532,7 @@ int bwtmi_job_create(const bwtmi_params *params, bwtmi_job **out) {
 int bwtmi_job_free(bwtmi_job *job) {
     return guard([&] {
         if (!job) return;
+        if (job->j.text_th.joinable()) job->j.text_th.join();   // its error dies with the job
         if (job->dev.bg_ctx) ctx_join(*job->dev.bg_ctx);   // its error stays for the ctx's next call
         if (job->dev.device >= 0) (void)hipSetDevice(job->dev.device);
         for (auto &d : job->dev.seqs) d.buf.release();
@@ -540,6 +545,7 @@ int bwtmi_job_add_contig(bwtmi_job *job, const char *name, const uint8_t *full, 
                          int64_t trim_left, int64_t trim_right, int32_t *contig_id) {
     return guard([&] {
         CHECK_ARG(job && name && (full || full_len == 0) && full_len >= 0, "bad argument");
+        TEXT_JOIN(job);
         CHECK_ARG(trim_left >= 0 && trim_right >= 0 && trim_left + trim_right <= full_len, "bad trim");
         Contig c;
         c.name = name;
@@ -556,13 +562,125 @@ int bwtmi_job_add_contig(bwtmi_job *job, const char *name, const uint8_t *full, 
 int bwtmi_job_load_fasta(bwtmi_job *job, const char *path, int32_t flank_trim) {
     return guard([&] {
         CHECK_ARG(job && path, "null argument");
+        TEXT_JOIN(job);
         load_fasta(job->j, path, flank_trim);
+    });
+}
+
+// bwtmi_job_load_fasta_dev: the loader's device placement (common.h FastaDev).
+// The file image goes up right after the read (pinned, overlapping the host's
+// first pass), the plain chunks are rebuilt from it on the device
+// (fasta_dev.hip), the host-written pieces follow, and the host pass over the
+// plain chunks runs behind all of it (joined by the scan or any reader).
+namespace {
+struct DevLoad final : FastaDev {
+    Ctx &c;
+    bwtmi_job *job;
+    DevLoad(Ctx &c_, bwtmi_job *j) : c(c_), job(j) {}
+    const char *img = nullptr;
+    void image(const char *p, int64_t n) override {
+        img = p;
+        if (n <= 0) return;
+        ensure_pinned(p, p, (size_t)n);
+        c.slot[S_FASTA].ensure((size_t)n + 64);
+    }
+    void image_part(int64_t off, int64_t n) override {   // from the reading threads
+        HIPCHECK(hipSetDevice(c.device));
+        HIPCHECK(hipMemcpyAsync(c.slot[S_FASTA].as<char>() + off, img + off, (size_t)n, hipMemcpyHostToDevice,
+                                c.stream));
+    }
+    void contigs() override {
+        JobDev &d = job->dev;
+        const Job &J = job->j;
+        if (d.device >= 0 && d.device != c.device) {
+            for (auto &s : d.seqs) s.buf.release();
+            d.seqs.clear();
+        }
+        d.device = c.device;
+        d.seqs.resize(J.contigs.size());
+        for (size_t i = 0; i < J.contigs.size(); ++i) {
+            const Contig &ct = J.contigs[i];
+            DevContig &dc = d.seqs[i];
+            const int64_t tn = ct.trimmed_len();
+            if (dc.n == tn && dc.gen == ct.gen) continue;   // on the device already (not in this file)
+            if (!ct.full.empty()) ensure_pinned(ct.full.data(), ct.full.data(), ct.full.size());
+            dc.buf.ensure((size_t)tn + 128);
+            HIPCHECK(hipMemsetAsync(dc.buf.as<uint8_t>() + tn, 0, 128, c.stream));
+            dc.n = tn;
+            dc.gen = ct.gen;
+        }
+    }
+    void plain(const std::vector<FastaPiece> &ps) override {
+        std::vector<FastaDevPiece> v;
+        v.reserve(ps.size());
+        for (const FastaPiece &p : ps) {
+            const Contig &ct = job->j.contigs[(size_t)p.cid];
+            v.push_back(FastaDevPiece{p.a, p.b, p.off, ct.trim_left, ct.trimmed_len(),
+                                      job->dev.seqs[(size_t)p.cid].buf.as<char>()});
+        }
+        fasta_build_device(c, c.slot[S_FASTA].as<uint8_t>(), v.data(), (int64_t)v.size());
+    }
+    void piece(int32_t cid, int64_t off, const char *host, int64_t n) override {
+        const Contig &ct = job->j.contigs[(size_t)cid];
+        const int64_t tl = ct.trim_left, tn = ct.trimmed_len();
+        const int64_t lo = std::max(off, tl), hi = std::min(off + n, tl + tn);
+        if (hi <= lo) return;
+        HIPCHECK(hipMemcpyAsync(job->dev.seqs[(size_t)cid].buf.as<char>() + (lo - tl), host + (lo - off),
+                                (size_t)(hi - lo), hipMemcpyHostToDevice, c.stream));
+    }
+    void defer(std::function<void()> fn, std::shared_ptr<void> hold) override {
+        hipEvent_t ev;   // every copy out of `hold` (the image) is queued before it
+        HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIPCHECK(hipEventRecord(ev, c.stream));
+        const int dev = c.device;
+        job->j.text_defer([fn = std::move(fn), hold = std::move(hold), ev, dev]() mutable {
+            struct Done {   // also when fn throws: the image outlives its copy
+                hipEvent_t ev;
+                int dev;
+                std::shared_ptr<void> &hold;
+                ~Done() {
+                    (void)hipSetDevice(dev);
+                    (void)hipEventSynchronize(ev);
+                    (void)hipEventDestroy(ev);
+                    hold.reset();
+                }
+            } done{ev, dev, hold};
+            fn();
+        });
+    }
+};
+}  // namespace
+
+int bwtmi_job_load_fasta_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *path, int32_t flank_trim) {
+    return guard([&] {
+        CHECK_ARG(ctx && job && path, "null argument");
+        Ctx &c = ctx->c;
+        job->j.text_join();
+        if (job->dev.bg_ctx && job->dev.bg_ctx != &c) ctx_wait(*job->dev.bg_ctx);   // it reads the old buffers
+        use(c);
+        DevLoad dl(c, job);
+        load_fasta(job->j, path, flank_trim, 1, 0, &dl);
+    });
+}
+
+int bwtmi_job_device_text(bwtmi_ctx *ctx, bwtmi_job *job, int32_t id, uint8_t *dst) {
+    return guard([&] {
+        CHECK_ARG(ctx && job && dst && id >= 0 && id < (int32_t)job->j.contigs.size(), "bad argument");
+        Ctx &c = use(ctx->c);
+        const JobDev &d = job->dev;
+        CHECK_ARG(d.device == c.device && (size_t)id < d.seqs.size() && d.seqs[(size_t)id].n >= 0 &&
+                      d.seqs[(size_t)id].gen == job->j.contigs[(size_t)id].gen,
+                  "contig not resident on this device");
+        const DevContig &dc = d.seqs[(size_t)id];
+        if (dc.n) HIPCHECK(hipMemcpyAsync(dst, dc.buf.p, (size_t)dc.n, hipMemcpyDeviceToHost, c.stream));
+        HIPCHECK(hipStreamSynchronize(c.stream));
     });
 }
 
 int bwtmi_job_load_fasta_shard(bwtmi_job *job, const char *path, int32_t flank_trim, int32_t world, int32_t rank) {
     return guard([&] {
         CHECK_ARG(job && path && world >= 1 && rank >= 0 && rank < world, "bad argument");
+        TEXT_JOIN(job);
         load_fasta(job->j, path, flank_trim, world, rank);
     });
 }
@@ -571,6 +689,7 @@ int bwtmi_job_fasta_scan_part(bwtmi_job *job, const char *path, int32_t world, i
                               int64_t *nwords) {
     return guard([&] {
         CHECK_ARG(job && path && blob && nwords && world >= 1 && rank >= 0 && rank < world, "bad argument");
+        TEXT_JOIN(job);
         std::vector<int64_t> v;
         fasta_scan_part(job->j, path, world, rank, v);
         auto *o = (int64_t *)std::malloc(std::max<size_t>(1, v.size()) * sizeof(int64_t));
@@ -585,6 +704,7 @@ int bwtmi_job_load_fasta_parts(bwtmi_job *job, const char *path, int32_t flank_t
                                const int64_t *blob, int64_t nwords) {
     return guard([&] {
         CHECK_ARG(job && path && blob && nwords >= 6 && world >= 1 && rank >= 0 && rank < world, "bad argument");
+        TEXT_JOIN(job);
         fasta_load_parts(job->j, path, flank_trim, world, rank, blob, nwords);
     });
 }
@@ -592,6 +712,7 @@ int bwtmi_job_load_fasta_parts(bwtmi_job *job, const char *path, int32_t flank_t
 int bwtmi_job_select_shard(bwtmi_job *job, int32_t world, int32_t rank, int32_t *ids, int32_t *n) {
     return guard([&] {
         CHECK_ARG(job && world >= 1 && rank >= 0 && rank < world, "bad argument");
+        TEXT_JOIN(job);
         std::vector<int32_t> v = shard_units(job->j, world, rank);
         Job &J = job->j;
         J.selected.assign(J.contigs.size(), 0);
@@ -636,6 +757,7 @@ int64_t bwtmi_job_contig_info(const bwtmi_job *job, int32_t id, char *name, int6
 int bwtmi_job_contig_seq(const bwtmi_job *job, int32_t id, uint8_t *dst) {
     return guard([&] {
         CHECK_ARG(job && dst && id >= 0 && id < (int32_t)job->j.contigs.size(), "bad argument");
+        TEXT_JOIN(job);
         const Contig &c = job->j.contigs[(size_t)id];
         std::memcpy(dst, c.full.data(), c.full.size());
     });
@@ -657,6 +779,7 @@ static void job_upload(bwtmi_ctx *ctx, bwtmi_job *job) {
         DevContig &dc = d.seqs[i];
         if (!job->j.selected.empty() && !job->j.selected[i]) continue;   // another rank's shard
         if (dc.n == ct.trimmed_len() && dc.gen == ct.gen) continue;
+        job->j.text_join();   // host bytes are read below
         ensure_pinned(ct.full.data(), ct.trimmed(), (size_t)ct.trimmed_len());
         upload_text(c, dc.buf, (const uint8_t *)ct.trimmed(), ct.trimmed_len());
         dc.n = ct.trimmed_len();
@@ -828,6 +951,7 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
             for (auto &e : ex)
                 if (e) std::rethrow_exception(e);
         }
+        J.text_join();   // the host copies written behind this scan (bwtmi_job_load_fasta_dev)
         J.stage_ms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         J.stage_ms[1] = 0;
         if (to_index.empty()) return;
@@ -882,6 +1006,7 @@ int bwtmi_job_wait(bwtmi_ctx *ctx, bwtmi_job *job) {
 int bwtmi_job_add_hits(bwtmi_job *job, int32_t contig_id, const bwtmi_hit *hits, int64_t n) {
     return guard([&] {
         CHECK_ARG(job && (hits || n == 0) && n >= 0, "bad argument");
+        TEXT_JOIN(job);
         Job &J = job->j;
         CHECK_ARG(contig_id >= 0 && contig_id < (int32_t)J.contigs.size(), "bad contig id");
         if (J.hits.size() < J.contigs.size()) J.hits.resize(J.contigs.size());
@@ -915,6 +1040,7 @@ static std::unique_ptr<Ctx> aux_ctx(int device) {
 int bwtmi_job_postprocess(bwtmi_job *job) {
     return guard([&] {
         CHECK_ARG(job, "null argument");
+        TEXT_JOIN(job);
         Job &J = job->j;
         JobDev &d = job->dev;
         // BWTMI_POST_DEVICE=1: the merge fold's fresh-pair recomputes go to the
@@ -958,6 +1084,7 @@ int64_t bwtmi_job_count(const bwtmi_job *job) { return job ? (int64_t)job->j.fin
 int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len) {
     return guard([&] {
         CHECK_ARG(job && out && len, "null argument");
+        TEXT_JOIN(job);
         const std::vector<Text> parts = render_parts(job->j, fmt);
         std::vector<size_t> at(parts.size() + 1, 0);
         for (size_t k = 0; k < parts.size(); ++k) at[k + 1] = at[k] + parts[k].size();
@@ -980,6 +1107,7 @@ int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len) {
 int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path) {
     return guard([&] {
         CHECK_ARG(job && path, "null argument");
+        TEXT_JOIN(job);
         OutFd out(path);
         const int fd = out.fd;
         Rendered R;
@@ -1032,6 +1160,7 @@ int32_t bwtmi_job_unit_count(bwtmi_job *job) {
 int bwtmi_job_unit_rows(bwtmi_job *job, int64_t *unit_rows) {
     return guard([&] {
         CHECK_ARG(job && unit_rows, "null argument");
+        TEXT_JOIN(job);
         Job &J = job->j;
         J.assign_units();
         for (int32_t u = 0; u < J.nunits; ++u) unit_rows[u] = 0;
@@ -1042,6 +1171,7 @@ int bwtmi_job_unit_rows(bwtmi_job *job, int64_t *unit_rows) {
 int bwtmi_job_render_units(bwtmi_job *job, int fmt, const int64_t *row_base, int64_t *bytes) {
     return guard([&] {
         CHECK_ARG(job && bytes, "null argument");
+        TEXT_JOIN(job);
         Job &J = job->j;
         render_rows(J, fmt, row_base, J.rendered);
         for (int32_t u = 0; u <= J.nunits; ++u) bytes[u] = 0;
@@ -1054,6 +1184,7 @@ int bwtmi_job_render_units(bwtmi_job *job, int fmt, const int64_t *row_base, int
 int bwtmi_job_write_units(bwtmi_job *job, const char *path, const int64_t *offsets, int write_header) {
     return guard([&] {
         CHECK_ARG(job && path && offsets, "null argument");
+        TEXT_JOIN(job);
         Job &J = job->j;
         Rendered &R = J.rendered;
         std::vector<Text> parts;
@@ -1077,6 +1208,7 @@ int bwtmi_job_write_units(bwtmi_job *job, const char *path, const int64_t *offse
 int bwtmi_job_get_records(bwtmi_job *job, int64_t *ints9, double *dbls5) {
     return guard([&] {
         CHECK_ARG(job && ints9 && dbls5, "null argument");
+        TEXT_JOIN(job);
         size_t k = 0;
         for (const Rec &r : job->j.final_recs) {
             int64_t *I = ints9 + 9 * k;
@@ -1123,6 +1255,7 @@ struct WireRec {
 int bwtmi_job_export(bwtmi_job *job, uint8_t **buf, int64_t *len) {
     return guard([&] {
         CHECK_ARG(job && buf && len, "null argument");
+        TEXT_JOIN(job);
         std::string s;
         const int64_t n = (int64_t)job->j.final_recs.size();
         s.append((const char *)&n, sizeof n);
@@ -1195,6 +1328,7 @@ int bwtmi_job_import(bwtmi_job *job, const uint8_t *buf, int64_t len) {
 int bwtmi_job_set_records(bwtmi_job *job, const uint8_t *buf, int64_t len) {
     return guard([&] {
         CHECK_ARG(job, "null argument");
+        TEXT_JOIN(job);
         job->j.final_recs.clear();
         import_wire(job, buf, len);
     });

@@ -3,8 +3,11 @@
 
 #include <cstdint>
 #include <cstring>
+#include <exception>
 #include <functional>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/bwtmi.h"
@@ -248,6 +251,53 @@ struct Job {
     RcBatchFn rc_batch;
     std::vector<const char *> rc_text;
     void assign_units();
+    // host text written behind the device work (a whole-file load with device
+    // placement, bwtmi_job_load_fasta_dev): every reader of contig bytes joins it
+    std::thread text_th;
+    std::exception_ptr text_err;
+    void text_defer(std::function<void()> fn) {
+        text_join();
+        text_th = std::thread([this, fn = std::move(fn)] {
+            try {
+                fn();
+            } catch (...) {
+                text_err = std::current_exception();
+            }
+        });
+    }
+    void text_join() {
+        if (text_th.joinable()) text_th.join();
+        if (text_err) {
+            std::exception_ptr e = text_err;
+            text_err = nullptr;
+            std::rethrow_exception(e);
+        }
+    }
+    Job() = default;
+    Job(const Job &) = delete;
+    Job &operator=(const Job &) = delete;
+    ~Job() {
+        if (text_th.joinable()) text_th.join();
+    }
+};
+
+// Device placement of a whole-file load (api.cpp): the loader hands over the
+// file image right after the read, the plain chunks' pieces (file bytes [a, b)
+// minus their newlines, upper-cased, at content offset `off` of contig cid),
+// and the pieces it wrote on the host; defer runs the host pass over the plain
+// chunks behind the device work and keeps `hold` until the copies are done.
+struct FastaPiece {
+    int64_t a, b, off;
+    int32_t cid;
+};
+struct FastaDev {
+    virtual ~FastaDev() = default;
+    virtual void image(const char *img, int64_t n) = 0;         // the image buffer (before the read)
+    virtual void image_part(int64_t off, int64_t n) = 0;         // bytes [off, off + n) are read (any thread)
+    virtual void contigs() = 0;   // names, trims and host buffers are settled
+    virtual void plain(const std::vector<FastaPiece> &pieces) = 0;
+    virtual void piece(int32_t cid, int64_t off, const char *host, int64_t n) = 0;
+    virtual void defer(std::function<void()> fn, std::shared_ptr<void> hold) = 0;
 };
 
 // post.cpp
@@ -261,7 +311,8 @@ std::vector<Text> render_parts(Job &job, int fmt);
 std::string render(Job &job, int fmt);
 // fasta.cpp: load_reference; with world > 1 only this rank's shard (fold units by
 // longest-processing-time over the analysed lengths, shard_units) gets its bases
-void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world = 1, int32_t rank = 0);
+void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world = 1, int32_t rank = 0,
+                FastaDev *dev = nullptr);
 // split multi-rank load: pass 1 over this rank's 1/world of the file -> part
 // table; all ranks' tables (rank order) -> contigs, shard, own bases only
 void fasta_scan_part(Job &job, const char *path, int32_t world, int32_t rank, std::vector<int64_t> &blob);

@@ -66,7 +66,9 @@ struct HBuf {  // pinned host staging
 enum Slot {
     S_TEXT = 0, S_PACK, S_CAND_K, S_CAND_V, S_CAND_K2, S_CAND_V2, S_FLAG, S_SCAN, S_HITS, S_COUNTS,
     S_SORT_TMP0, S_SORT_TMP1, S_SORT_HIST, S_SCAN_TMP, S_MISC0, S_MISC1, S_MISC2, S_MISC3,
-    S_IDX0, S_IDX1, S_IDX2, S_IDX3, S_IDX4, S_IDX5, S_IDX6, S_IDX7, S_IDX8, S_IDX9, S_IDX10, S_IDX11, S_NSLOTS
+    S_IDX0, S_IDX1, S_IDX2, S_IDX3, S_IDX4, S_IDX5, S_IDX6, S_IDX7, S_IDX8, S_IDX9, S_IDX10, S_IDX11,
+    S_FASTA,   // a whole-file load's FASTA image (fasta_dev.hip)
+    S_NSLOTS
 };
 
 struct KernelTimer {
@@ -245,6 +247,15 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t ntiles) {
 // one stable 8-bit pass at `shift` from (kin, vin) into (kout, vout)
 void radix_pass_k32(Ctx &c, const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int64_t n,
                     int shift);
+
+// ----- a FASTA file's plain chunks rebuilt on the device (fasta_dev.hip):
+// image bytes [a, b) minus their newlines, upper-cased, land at content offset
+// `off` of a contig whose trimmed window [tl, tl + tn) is at dst (device)
+struct FastaDevPiece {
+    int64_t a, b, off, tl, tn;
+    char *dst;
+};
+void fasta_build_device(Ctx &c, const uint8_t *d_img, const FastaDevPiece *pieces, int64_t npieces);
 
 // ----- strict scan (strict_scan.hip)
 struct ScanResult {

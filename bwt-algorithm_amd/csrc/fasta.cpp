@@ -53,9 +53,17 @@ struct Chunk {
     int64_t pre = 0;          // content before the chunk's first header
     bool plain = false;       // only '\n' and bytes 0x21..0x7f, no '>': lines need no strip
     std::vector<Hdr> hdrs;
-    // pass 2 destinations (nullptr: not written)
+    // pass 2 destinations (nullptr: not written), with their contig and the
+    // content offset there (the device placement of a whole-file load)
     char *pre_dst = nullptr;
+    int32_t pre_cid = -1;
+    int64_t pre_off = 0;
     std::vector<char *> dst;
+    std::vector<int32_t> dcid;
+    // a chunk with a header (or other irregular lines) whose bytes after the
+    // last '>' line are plain: [tail_a, b) holds tail_len content bytes that
+    // continue the chunk's last destination (-1: no such tail)
+    int64_t tail_a = -1, tail_len = 0;
 };
 
 // calls line(a, b) with the stripped bounds of every non-empty line in [a, e)
@@ -147,7 +155,60 @@ inline void upper_copy(char *__restrict d, const char *__restrict s, int64_t n) 
     }
 }
 
-void read_file(const char *path, Seq &data, int nt) {
+// the content of plain lines [i, e) ('\n' ends every line) upper-cased to d; returns the end
+inline char *plain_copy(const char *p, int64_t i, int64_t e, char *d) {
+    while (i < e) {
+        const char *nl = (const char *)std::memchr(p + i, '\n', (size_t)(e - i));
+        const int64_t j = nl ? (int64_t)(nl - p) : e;
+        upper_copy(d, p + i, j - i);
+        d += j - i;
+        i = j + 1;
+    }
+    return d;
+}
+
+// where the chunk's plain tail goes (host pointer, or nullptr), its contig and content offset
+inline char *tail_dst(const Chunk &C, int32_t &cid, int64_t &off) {
+    if (!C.hdrs.empty()) {
+        cid = C.dcid.back();
+        off = C.hdrs.back().len - C.tail_len;
+        return C.dst.back() ? C.dst.back() + off : nullptr;
+    }
+    cid = C.pre_cid;
+    off = C.pre_off + C.pre - C.tail_len;
+    return C.pre_dst ? C.pre_dst + (C.pre - C.tail_len) : nullptr;
+}
+
+// pass 2 of one chunk: its upper-cased content into place (head: the lines
+// before a plain tail; tail: the plain tail only)
+enum Part { P_ALL, P_HEAD, P_TAIL };
+void pass2(const char *p, const Chunk &C, Part part = P_ALL) {
+    char *d = C.pre_dst;
+    if (C.plain) {   // lines end at '\n' only and need no strip
+        if (d && part != P_HEAD) plain_copy(p, C.a, C.b, d);
+        return;
+    }
+    const int64_t e = C.tail_a >= 0 ? C.tail_a : C.b;
+    if (part != P_TAIL) {
+        size_t h = 0;
+        for_lines(p, C.a, e, [&](int64_t s, int64_t t) {
+            if (p[s] == '>') {
+                d = C.dst[h++];
+                return;
+            }
+            if (!d) return;
+            upper_copy(d, p + s, t - s);
+            d += t - s;
+        });
+    }
+    if (C.tail_a >= 0 && part != P_HEAD) {
+        int32_t cid;
+        int64_t off;
+        if (char *td = tail_dst(C, cid, off)) plain_copy(p, C.tail_a, C.b, td);
+    }
+}
+
+void read_file(const char *path, Seq &data, int nt, FastaDev *dev = nullptr) {
     const int fd = ::open(path, O_RDONLY);
     if (fd < 0) fail(BWTMI_E_IO, "cannot open %s", path);
     struct stat st;
@@ -157,16 +218,19 @@ void read_file(const char *path, Seq &data, int nt) {
     }
     const int64_t n = (int64_t)st.st_size;
     char *buf = data.resize_uninit((size_t)n);
+    if (dev) dev->image(buf, n);   // each piece goes to the device as soon as it is read
     std::atomic<bool> bad{false};
     const int64_t piece = int64_t(4) << 20;
     run_tasks((n + piece - 1) / piece, nt, [&](int64_t k) {
-        int64_t o = k * piece;
+        const int64_t o0 = k * piece;
+        int64_t o = o0;
         const int64_t e = std::min(n, o + piece);
         while (o < e) {
             const ssize_t r = ::pread(fd, buf + o, (size_t)(e - o), (off_t)o);
             if (r <= 0) { bad = true; return; }
             o += r;
         }
+        if (dev) dev->image_part(o0, e - o0);
     });
     ::close(fd);
     if (bad) fail(BWTMI_E_IO, "read error on %s", path);
@@ -174,12 +238,13 @@ void read_file(const char *path, Seq &data, int nt) {
 
 }  // namespace
 
-void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, int32_t rank) {
+void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, int32_t rank, FastaDev *dev) {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
+    job.text_join();   // a deferred pass 2 of the previous load still writes the old buffers
     const int nt = host_threads(job.params);
     thread_local Seq data;   // the file image (kept for the next load)
-    read_file(path, data, nt);
+    read_file(path, data, nt, dev);   // with a device: the image is copied up while it is read
     const auto t1 = clk::now();
     const char *p = data.data();
     const int64_t N = (int64_t)data.size();
@@ -207,7 +272,25 @@ void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, i
             C.pre = (C.b - C.a) - nl;
             return;
         }
-        for_lines(p, C.a, C.b, [&](int64_t s, int64_t e) {
+        // the bytes after the line of the chunk's last '>' may be plain: they
+        // are then content of the last destination, counted without line work
+        int64_t e_lines = C.b;
+        if (!no_plain) {
+            if (const char *gt = (const char *)memrchr(p + C.a, '>', (size_t)(C.b - C.a))) {
+                const int64_t g = (int64_t)(gt - p);
+                const char *nl = (const char *)std::memchr(p + g, '\n', (size_t)(C.b - g));
+                int64_t t = nl ? (int64_t)(nl - p) + 1 : C.b;
+                if (const char *cr = (const char *)std::memchr(p + g, '\r', (size_t)((nl ? t - 1 : C.b) - g)))
+                    t = (int64_t)(cr - p) + 1 + ((int64_t)(cr - p) + 1 < C.b && cr[1] == '\n');
+                if (t < C.b)
+                    if (const int64_t nl2 = plain_newlines(p + t, C.b - t); nl2 >= 0) {
+                        C.tail_a = t;
+                        C.tail_len = (C.b - t) - nl2;
+                        e_lines = t;
+                    }
+            }
+        }
+        for_lines(p, C.a, e_lines, [&](int64_t s, int64_t e) {
             if (p[s] == '>') {
                 int64_t x = s + 1;
                 while (x < e && py_space((unsigned char)p[x])) ++x;
@@ -222,6 +305,7 @@ void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, i
             if (C.hdrs.empty()) C.pre += e - s;
             else C.hdrs.back().len += e - s;
         });
+        if (C.tail_a >= 0) (C.hdrs.empty() ? C.pre : C.hdrs.back().len) += C.tail_len;
     });
 
     // Non-ASCII text: the reference reads the file as UTF-8 str (bwt.py:3719), so an
@@ -311,11 +395,15 @@ void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, i
             Chunk &C = ck[(size_t)t];
             if (have) {
                 C.pre_dst = C.pre ? dst_of(k - 1, off) : nullptr;
+                C.pre_cid = inst[k - 1].contig;
+                C.pre_off = off;
                 off += C.pre;
             }
             C.dst.resize(C.hdrs.size());
+            C.dcid.resize(C.hdrs.size());
             for (size_t h = 0; h < C.hdrs.size(); ++h) {
                 C.dst[h] = C.hdrs[h].len ? dst_of(k, 0) : nullptr;
+                C.dcid[h] = inst[k].contig;
                 off = C.hdrs[h].len;
                 ++k;
                 have = true;
@@ -323,37 +411,63 @@ void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, i
         }
     }
     const auto t2 = clk::now();
-    // pass 2: upper-cased content into place
-    run_tasks(T, nt, [&](int64_t t) {
-        Chunk &C = ck[(size_t)t];
-        char *d = C.pre_dst;
-        if (C.plain) {   // lines end at '\n' only and need no strip
-            if (!d) return;
-            for (int64_t i = C.a; i < C.b;) {
-                const char *nl = (const char *)std::memchr(p + i, '\n', (size_t)(C.b - i));
-                const int64_t j = nl ? (int64_t)(nl - p) : C.b;
-                upper_copy(d, p + i, j - i);
-                d += j - i;
-                i = j + 1;
-            }
-            return;
+    auto stats = [&](const char *what) {
+        if (std::getenv("BWTMI_STATS")) {
+            auto d = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            std::fprintf(stderr, "  load_fasta: read %.1f pass1+stitch %.1f %s %.1f ms (%d threads, %lld chunks)\n",
+                         d(t0, t1), d(t1, t2), what, d(t2, clk::now()), nt, (long long)T);
         }
-        size_t h = 0;
-        for_lines(p, C.a, C.b, [&](int64_t s, int64_t e) {
-            if (p[s] == '>') {
-                d = C.dst[h++];
-                return;
-            }
-            if (!d) return;
-            upper_copy(d, p + s, e - s);
-            d += e - s;
-        });
-    });
-    if (std::getenv("BWTMI_STATS")) {
-        auto d = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        std::fprintf(stderr, "  load_fasta: read %.1f pass1+stitch %.1f pass2 %.1f ms (%d threads, %lld chunks)\n",
-                     d(t0, t1), d(t1, t2), d(t2, clk::now()), nt, (long long)T);
+    };
+    if (!dev) {
+        // pass 2: upper-cased content into place
+        run_tasks(T, nt, [&](int64_t t) { pass2(p, ck[(size_t)t]); });
+        stats("pass2");
+        return;
     }
+    // Device placement: the plain chunks are compacted on the device from the
+    // file image (already on its way); the other chunks (headers, CR, spaces)
+    // are written on the host now and their pieces copied up; the host copy of
+    // the plain chunks is written behind the device work (Job::text_join).
+    dev->contigs();
+    std::vector<int64_t> rest;   // chunks whose head is written now
+    std::vector<FastaPiece> pcs;
+    for (int64_t t = 0; t < T; ++t) {
+        const Chunk &C = ck[(size_t)t];
+        if (!C.plain) rest.push_back(t);
+        else if (C.pre_dst) pcs.push_back(FastaPiece{C.a, C.b, C.pre_off, C.pre_cid});
+        if (C.tail_a >= 0) {
+            int32_t cid;
+            int64_t off;
+            if (tail_dst(C, cid, off)) pcs.push_back(FastaPiece{C.tail_a, C.b, off, cid});
+        }
+    }
+    run_tasks((int64_t)rest.size(), nt, [&](int64_t q) { pass2(p, ck[(size_t)rest[(size_t)q]], P_HEAD); });
+    for (int64_t t : rest) {   // the head's pieces (a plain tail is not among them)
+        const Chunk &C = ck[(size_t)t];
+        const bool tail_pre = C.tail_a >= 0 && C.hdrs.empty();
+        if (C.pre_dst) dev->piece(C.pre_cid, C.pre_off, C.pre_dst, C.pre - (tail_pre ? C.tail_len : 0));
+        for (size_t h = 0; h < C.hdrs.size(); ++h) {
+            const bool tail_here = C.tail_a >= 0 && h + 1 == C.hdrs.size();
+            if (C.dst[h]) dev->piece(C.dcid[h], 0, C.dst[h], C.hdrs[h].len - (tail_here ? C.tail_len : 0));
+        }
+    }
+    dev->plain(pcs);
+    // the deferred pass owns the image (another load on this thread starts a
+    // fresh one); the device layer keeps it until its copy has completed
+    auto img = std::make_shared<Seq>();
+    img->swap(data);
+    auto keep = std::make_shared<std::vector<Chunk>>(std::move(ck));
+    dev->defer(
+        [keep, img, nt] {
+            const std::vector<Chunk> &K = *keep;
+            const char *q = img->data();
+            run_tasks((int64_t)K.size(), nt, [&](int64_t t) {
+                const Chunk &C = K[(size_t)t];
+                if (C.plain || C.tail_a >= 0) pass2(q, C, P_TAIL);
+            });
+        },
+        img);
+    stats("non-plain pass2 + device launch");
 }
 
 // ------------------------------------------------------------------ split load

@@ -598,15 +598,141 @@ __global__ __launch_bounds__(256) void k_present(const uint8_t *__restrict__ t, 
     }
 }
 
+// Long unit lengths, sampled.  When K = (mc-1)L >= 95, every qualifying run
+// (length >= K) holds at least s = floor((K - 31) / 32) >= 2 consecutive full
+// aligned words (a run of length R holds floor((R - 31) / 32) of them at
+// least), so looking at every s-th word finds each such run: the work per
+// group of 32 unit lengths drops from every word to every s-th one (s ~ 2g for
+// group g at min_copies 3).  A sampled lane whose word is full (all 32
+// positions match at distance L) owns the run when one of the s words before
+// it is not full -- the first sample inside the run; the wave then finds the
+// run's start among those s words and its end by scanning forward 64 words a
+// step, for one owner at a time.  Runs and candidates are exactly the dense
+// kernel's (K > 62: only streaks of full words qualify there too).
+constexpr int kSparseMax = 48;   // groups per launch
+struct SparseGroups {
+    int32_t ng;
+    int32_t g[kSparseMax];           // group: L in [32g, 32g+31] (clipped to [lmin, lmax])
+    int32_t s[kSparseMax];           // sample stride in words
+    int64_t woff[kSparseMax + 1];    // first wave of each group in the launch
+};
+
+template <int B>
+__global__ __launch_bounds__(256) void k_runs_sparse(const uint32_t *__restrict__ P, int64_t n, int64_t nwords32,
+                                                     int32_t lmin, int32_t lmax, int64_t mc, SparseGroups sg,
+                                                     CandOut out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);   // wave of the launch
+    int gi = 0;
+    while (gi + 1 < sg.ng && q >= sg.woff[gi + 1]) ++gi;   // uniform
+    if (q >= sg.woff[sg.ng]) return;
+    const int64_t g = sg.g[gi], s = sg.s[gi];
+    const int64_t w = ((q - sg.woff[gi]) * 64 + lane) * s;   // this lane's sampled word
+    const bool inb = w < nwords32;
+    auto word = [&](int64_t x, int p) { return inb && x < nwords32 + 8 ? P[x * B + p] : 0u; };
+    uint32_t a[B], lo[B], hi[B];
+#pragma unroll
+    for (int p = 0; p < B; ++p) {
+        a[p] = inb ? P[w * B + p] : 0u;
+        lo[p] = word(w + g, p);
+        hi[p] = word(w + g + 1, p);
+    }
+    const int64_t Lg = g * 32;
+    const int r_lo = (int)max((int64_t)0, (int64_t)lmin - Lg);
+    const int r_hi = (int)min((int64_t)31, (int64_t)lmax - Lg);
+    const int64_t j0 = w * 32;
+    const bool tail = !inb || j0 + 32 + Lg + 31 >= n;
+    const int seg = (int)(blockIdx.x & (kCandSegs - 1));
+    for (int r = r_lo; r <= r_hi; ++r) {
+        const int64_t L = Lg + r, K = (mc - 1) * L;
+        uint32_t x = 0;
+#pragma unroll
+        for (int p = 0; p < B; ++p) x |= a[p] ^ __builtin_amdgcn_alignbit(hi[p], lo[p], (uint32_t)r);
+        uint32_t M = ~x;
+        if (tail) {
+            const int64_t lim = n - L - j0;
+            if (!inb || lim <= 0) M = 0u;
+            else if (lim < 32) M &= (1u << lim) - 1u;
+        }
+        uint64_t full = __ballot(M == FULL);   // uniform
+        while (full) {
+            const int src = __ffsll((unsigned long long)full) - 1;
+            full &= full - 1;
+            const int64_t ws = (int64_t)__builtin_amdgcn_readlane((int)(w / s), src) * s;   // the owner candidate's word
+            // start: the first non-full word among ws-1 .. ws-s (word ws-s is the
+            // previous sample: all s full means that sample's run, not ours)
+            int64_t start = -1;
+            for (int64_t b0 = 1; b0 <= s; b0 += 64) {
+                const int64_t kk = b0 + lane;
+                const bool look = kk <= s;
+                const uint32_t Mq = look ? eq32<B>(P, ws - kk, L, n) : FULL;   // 0 before the text
+                const uint64_t nb = __ballot(look && Mq != FULL);
+                if (nb) {   // readlane: start (and the `continue` below) stay scalar
+                    const int f = __ffsll((unsigned long long)nb) - 1;
+                    const uint32_t Mf = (uint32_t)__builtin_amdgcn_readlane((int)Mq, f);
+                    start = (ws - (b0 + f) + 1) * 32 - (int64_t)__clz(~Mf);
+                    break;
+                }
+            }
+            if (start < 0) continue;   // not the first sample of its run
+            // end: the first non-full word after ws
+            int64_t end = -1;
+            for (int64_t q0 = ws + 1;; q0 += 64) {
+                const uint32_t Mq = eq32<B>(P, q0 + lane, L, n);   // 0 past the text: ends the scan
+                const uint64_t nb = __ballot(Mq != FULL);
+                if (nb) {
+                    const int f = __ffsll((unsigned long long)nb) - 1;
+                    const uint32_t Mf = (uint32_t)__builtin_amdgcn_readlane((int)Mq, f);
+                    end = (q0 + f) * 32 + (int64_t)__ffs(~Mf) - 1;
+                    break;
+                }
+            }
+            if (end - start >= K && lane == 0) {
+                const unsigned long long at = atomicAdd(out.count + seg, 1ull);
+                put(out, seg, at, L, start, end);
+            }
+        }
+    }
+}
+
+// first group (of 32 unit lengths) whose runs are found by sampling: K >= 95 for its shortest L
+inline int64_t sparse_stride(int64_t g, int32_t lmin, int64_t mc) {
+    const int64_t L = std::max<int64_t>(g * 32, lmin), K = (mc - 1) * L;
+    return K >= 95 ? (K - 31) / 32 : 0;
+}
+
 template <int B>
 void launch_runs(Ctx &c, const uint32_t *P, int64_t n, int32_t lmin, int32_t lmax, int64_t mc, CandOut out) {
     const int64_t nwords32 = (n + 31) / 32;
-    const int64_t tiles = (nwords32 + 4 * kOwn - 1) / (4 * kOwn);
-    const int64_t groups = (int64_t)(lmax >> 5) - (int64_t)(lmin >> 5) + 1;
-    const int32_t gper = 8;   // unit-length groups per workgroup (32 L each)
-    const int64_t gblocks = (groups + gper - 1) / gper;
-    KLAUNCH("k_runs", 0.0, (k_runs<B>), dim3((unsigned)tiles, (unsigned)gblocks), dim3(256), 0, c.stream, P, n, nwords32,
-                       lmin, lmax, mc, gper, out);
+    static const bool dense_only = [] { const char *e = std::getenv("BWTMI_RUNS_DENSE"); return e && *e == '1'; }();
+    int64_t gs = std::max<int64_t>(1, lmin >> 5);   // group 0 (L < 32) stays dense: its short runs
+    while (!dense_only && gs <= (lmax >> 5) && sparse_stride(gs, lmin, mc) < 2) ++gs;
+    if (dense_only) gs = (lmax >> 5) + 1;
+    const int32_t lmax_dense = (int32_t)std::min<int64_t>(lmax, gs * 32 - 1);
+    if (lmin <= lmax_dense) {
+        const int64_t tiles = (nwords32 + 4 * kOwn - 1) / (4 * kOwn);
+        const int64_t groups = (int64_t)(lmax_dense >> 5) - (int64_t)(lmin >> 5) + 1;
+        const int32_t gper = 8;   // unit-length groups per workgroup (32 L each)
+        const int64_t gblocks = (groups + gper - 1) / gper;
+        KLAUNCH("k_runs", 0.0, (k_runs<B>), dim3((unsigned)tiles, (unsigned)gblocks), dim3(256), 0, c.stream, P, n,
+                nwords32, lmin, lmax_dense, mc, gper, out);
+    }
+    for (int64_t g0 = gs; g0 <= (lmax >> 5); g0 += kSparseMax) {
+        SparseGroups sg{};
+        sg.ng = 0;
+        for (int64_t g = g0; g <= (lmax >> 5) && sg.ng < kSparseMax; ++g) {
+            const int64_t s = sparse_stride(g, lmin, mc);
+            sg.g[sg.ng] = (int32_t)g;
+            sg.s[sg.ng] = (int32_t)s;
+            const int64_t samples = (nwords32 + s - 1) / s;
+            sg.woff[sg.ng + 1] = sg.woff[sg.ng] + (samples + 63) / 64;
+            ++sg.ng;
+        }
+        const int64_t waves = sg.woff[sg.ng];
+        if (waves == 0) continue;
+        KLAUNCH("k_runs_sparse", 0.0, (k_runs_sparse<B>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, c.stream,
+                P, n, nwords32, lmin, lmax, mc, sg, out);
+    }
 }
 
 }  // namespace

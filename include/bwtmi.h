@@ -296,6 +296,18 @@ int bwtmi_align_regions(bwtmi_ctx *ctx, const char *seq, int64_t seq_len, const 
  * blank lines skipped, duplicate names overwrite in place.  Registers every
  * contig in job (trim = flank_trim if len > 2*flank_trim). */
 int bwtmi_job_load_fasta(bwtmi_job *job, const char *path, int32_t flank_trim);
+/* bwtmi_job_load_fasta + bwtmi_job_upload for a whole file, with the analysed
+ * sequences built on ctx's device from the file image: its copy to the device
+ * overlaps the loader's first pass, the plain chunks (whole lines of
+ * 0x21..0x7f bytes other than '>') are rebuilt there (fasta_dev.hip), and the
+ * host copies of those chunks are written behind the device work -- complete
+ * when the next bwtmi_job_scan returns, or when any other call on the job
+ * reads contig bytes (bwtmi_job_contig_seq, postprocess, render, ...).
+ * Replaces the same load_reference (bwt.py:3713-3756) as bwtmi_job_load_fasta. */
+int bwtmi_job_load_fasta_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *path, int32_t flank_trim);
+/* the device copy of contig `id`'s analysed (trimmed) sequence into dst
+ * (trimmed_len bytes); fails when it is not resident on ctx's device */
+int bwtmi_job_device_text(bwtmi_ctx *ctx, bwtmi_job *job, int32_t id, uint8_t *dst);
 /* the same for rank `rank` of `world` processes: every contig is registered
  * (names and analysed lengths, for the shard layout), but only the fold units
  * this rank owns (bwtmi_job_select_shard) get their bases, and the job is

@@ -1,0 +1,135 @@
+"""Whole-file loads with the analysed sequences built on the device
+(bwtmi_job_load_fasta_dev, csrc/fasta_dev.hip) against the host loader, which
+the CPU suite pins to load_reference (bwt.py:3713-3756; test_host.py):
+
+* every golden input FASTA (edge cases: CRLF and lone CR, a literal '$',
+  natural-key collisions, contigs of 0-64 bp, lower case);
+* a ~25 MB file mixing plain stretches (LF only, no padding: rebuilt on the
+  device) with messy ones (CR/CRLF, padded and blank lines: written on the
+  host and copied up), lower case, N, duplicate names, tiny and empty contigs,
+  one-base and very long lines;
+* the host copies written behind the device work are complete for every
+  reader (contig_seq right after the load, the scan, a reload).
+Byte work: every comparison is exact."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from oracle import post
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_job_pair(ctx, path, trim=30, threads=None):
+    from bwtmi.records import Job
+    kw = {} if threads is None else {"threads": threads}
+    h = Job(**kw)
+    h.load_fasta(path, trim)
+    d = Job(**kw)
+    d.load_fasta(path, trim, dev_ctx=ctx)
+    assert d.names == h.names
+    for cid in range(h.contig_count()):
+        assert d.contig_info(cid) == h.contig_info(cid)
+        _, fl, tl, tr = h.contig_info(cid)
+        want = h.contig_seq(cid)
+        assert d.contig_seq(cid) == want, h.names[cid]                  # the deferred host copy
+        assert d.device_text(ctx, cid) == want[tl:fl - tr], h.names[cid]  # the device copy
+    return h, d
+
+
+def test_device_load_matches_host_on_golden_inputs(gpu_ctx, golden_dir):
+    from bwtmi import _lib
+    from bwtmi.records import Job
+    paths = sorted(glob.glob(os.path.join(golden_dir, "inputs", "*.fa*")))
+    assert len(paths) > 10
+    failing = 0
+    for p in paths:
+        try:
+            Job().load_fasta(p, 30)
+        except _lib.BwtmiError:   # non-ASCII text: the reference fails, so does every path
+            failing += 1
+            with pytest.raises(_lib.BwtmiError):
+                Job().load_fasta(p, 30, dev_ctx=gpu_ctx)
+            continue
+        seqs, full, offs = post.load_fasta(p, 30)
+        h, d = _check_job_pair(gpu_ctx, p)
+        for cid, nm in enumerate(d.names):
+            assert d.contig_seq(cid).decode() == full[nm], (p, nm)
+    assert failing >= 1
+
+
+def _mixed_fasta(seed: int) -> bytes:
+    r = np.random.default_rng(seed)
+    eols = [b"\n", b"\r\n", b"\r"]
+    out = bytearray()
+    names = [f"chr{k}" for k in range(14)] + ["chr3", "tiny", "chr5"]
+    for i, nm in enumerate(names):
+        plain = i % 3 != 1
+        out += b">" + nm.encode() + b" desc\n"
+        if i % 9 == 4:
+            continue                                  # empty contig
+        total = 17 if nm == "tiny" else int(r.integers(200_000, 3_500_000))
+        width = int(r.choice([60, 80, 1, 7, 2_500_000]))
+        seq = bytes(b"ACGTacgtNn"[k] for k in r.integers(0, 10, total))
+        for a in range(0, total, width):
+            if plain:
+                out += seq[a:a + width] + b"\n"
+            else:
+                pad = b" \t" if r.random() < 0.05 else b""
+                out += pad + seq[a:a + width] + pad + eols[int(r.integers(3))]
+                if r.random() < 0.02:
+                    out += b"   " + eols[int(r.integers(3))]
+    return bytes(out)
+
+
+@pytest.mark.parametrize("threads", [1, 4, 16])
+def test_device_load_plain_tails(gpu_ctx, tmp_path, threads):
+    from test_host import _plain_tail_fasta
+    path = str(tmp_path / "tails.fa")
+    with open(path, "wb") as f:
+        f.write(_plain_tail_fasta(threads))
+    seqs, full, offs = post.load_fasta(path, 30)
+    h, d = _check_job_pair(gpu_ctx, path, threads=threads)
+    for cid, nm in enumerate(d.names):
+        assert d.contig_seq(cid).decode() == full[nm], nm
+
+
+@pytest.mark.parametrize("threads", [1, 5, 16])
+def test_device_load_mixed_plain_and_messy_chunks(gpu_ctx, tmp_path, threads):
+    path = str(tmp_path / "mixed.fa")
+    with open(path, "wb") as f:
+        f.write(_mixed_fasta(threads))
+    seqs, full, offs = post.load_fasta(path, 30)
+    h, d = _check_job_pair(gpu_ctx, path, threads=threads)
+    assert d.names == list(seqs)
+    for cid, nm in enumerate(d.names):
+        assert d.contig_seq(cid).decode() == full[nm], nm
+
+
+def test_device_load_scan_and_reload(gpu_ctx, tmp_path):
+    """Load -> scan -> records equal the host-loaded job's; a second file
+    loaded into the same job replaces the device and host copies."""
+    from bwtmi import synth
+    from bwtmi.records import Job
+    a, b = str(tmp_path / "a.fa"), str(tmp_path / "b.fa")
+    synth.write_fasta(a, [2_000_000, 700_000], 0.0)
+    synth.write_fasta(b, [1_300_000], 0.02, first_index=3)
+    outs = []
+    for dev in (None, gpu_ctx):
+        j = Job(min_copies=3, show_progress=True)
+        for path in (a, b):
+            j.reset()
+            j.load_fasta(path, 30, dev_ctx=dev)
+            j.upload(gpu_ctx)
+            j.scan(gpu_ctx)
+            j.postprocess()
+            outs.append(j.render("strfinder"))
+            j.wait(gpu_ctx)
+            if dev is not None:
+                for cid in range(j.contig_count()):
+                    _, fl, tl, tr = j.contig_info(cid)
+                    assert j.device_text(gpu_ctx, cid) == j.contig_seq(cid)[tl:fl - tr]
+    assert outs[0] == outs[2] and outs[1] == outs[3]
+    assert outs[0] != outs[1]

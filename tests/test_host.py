@@ -107,6 +107,39 @@ def _messy_fasta(seed: int) -> bytes:
     return bytes(out)
 
 
+def _plain_tail_fasta(seed: int) -> bytes:
+    """Headers followed by long LF-only stretches (the loader's plain tails
+    after a chunk's last '>' line), next to CRLF / lone-CR / padded contigs,
+    a '>' inside a sequence line, lower case and N."""
+    r = np.random.default_rng(seed)
+    out = bytearray(b"orphan\n")
+    for i in range(16):
+        eol = [b"\n", b"\r\n", b"\r", b"\n"][i % 4]
+        out += b">c" + str(i).encode() + b" x" + eol
+        total = int(r.integers(1, 1_200_000))
+        width = int(r.choice([60, 1, 13, 900_000]))
+        seq = bytes(b"ACGTacgtNn"[k] for k in r.integers(0, 10, total))
+        for a in range(0, total, width):
+            out += seq[a:a + width] + (b"\n" if i % 4 != 1 else eol)
+        if i == 6:
+            out += b"AC>GT\n" + seq[:5000] + b"\n"
+    return bytes(out)
+
+
+@pytest.mark.parametrize("threads", [1, 4, 16])
+def test_loader_plain_tails(tmp_path, threads):
+    from bwtmi.records import Job
+    path = str(tmp_path / "tails.fa")
+    with open(path, "wb") as f:
+        f.write(_plain_tail_fasta(threads))
+    seqs, full, offs = post.load_fasta(path, 30)
+    j = Job(threads=threads)
+    j.load_fasta(path, 30)
+    assert j.names == list(seqs)
+    for cid, nm in enumerate(j.names):
+        assert j.contig_seq(cid).decode() == full[nm], nm
+
+
 @pytest.mark.parametrize("threads", [1, 3, 16])
 def test_parallel_loader_matches_reference_semantics(tmp_path, threads):
     """The chunked two-pass loader (fasta.cpp) against the line-by-line
