@@ -286,7 +286,7 @@ def main():
         # one whole file: the sequences are built on the device from the file image
         # and the host copy is written behind the scan (bwtmi_job_load_fasta_dev)
         timed("load_fasta", job.load_fasta, fa, FLANK, load_world, load_rank, c if load_world > 1 else None,
-              ctx if load_world == 1 and not a.host_load else None)
+              None if a.host_load else ctx)
         timed("upload", job.upload, ctx)
         timed("scan", job.scan, ctx)
         timed("postprocess", job.postprocess)
@@ -406,7 +406,7 @@ def main():
                    + "; FASTA read -> FM index + strict scan + post-processing -> STRfinder repeat.tab closed",
                    "contig_bp": wl["lengths"][0], "contigs": len(wl["lengths"]) * (1 if shared else world),
                    "parallelism": f"contig-shard x{world}", "index": not a.no_index,
-                   "load": "device" if load_world == 1 and not a.host_load else "host"},
+                   "load": "host" if a.host_load else "device"},
         "roofline": roofline,
         "e2e_roofline": {"b_alg_bytes_per_base": B_ALG_PER_BASE, "achieved_gbs": round(e2e_gbs, 2),
                          "peak_gbs": HBM_PEAK_GBS * world, "frac": round(e2e_gbs / (HBM_PEAK_GBS * world), 6)},

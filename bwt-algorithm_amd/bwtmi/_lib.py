@@ -116,6 +116,7 @@ _SIGS = {
     "bwtmi_job_fasta_scan_part": (C.c_int, [_P, C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p),
                                             C.POINTER(C.c_int64)]),
     "bwtmi_job_load_fasta_parts": (C.c_int, [_P, C.c_char_p, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int64]),
+    "bwtmi_job_load_fasta_parts_dev": (C.c_int, [_P, _P, C.c_char_p, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int64]),
     "bwtmi_job_contig_weight": (C.c_int64, [_P, C.c_int32]),
     "bwtmi_job_select_shard": (C.c_int, [_P, C.c_int32, C.c_int32, _P, _P]),
     "bwtmi_host_info": (C.c_int, [C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),

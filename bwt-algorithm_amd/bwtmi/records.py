@@ -132,9 +132,10 @@ class Job:
         rank's fold units get their bases (and the job is restricted to them).
         With a communicator (bwtmi.comm) no rank reads the whole file: each scans
         its 1/world, the part tables are all-gathered, each reads its own contigs.
-        With a device context (whole file only) the analysed sequences are built
-        on the device from the file image and the host copies are written behind
-        the next scan (bwtmi_job_load_fasta_dev): upload() has nothing left to do."""
+        With a device context (whole file, or the split load) the analysed
+        sequences are built on the device from the file bytes and the host copies
+        are written behind the next scan (bwtmi_job_load_fasta_dev /
+        _parts_dev): upload() has nothing left to do."""
         if dev_ctx is not None and world <= 1:
             check(lib().bwtmi_job_load_fasta_dev(dev_ctx, self.h, path.encode(), flank_trim))
         elif world > 1 and comm is not None:
@@ -146,8 +147,12 @@ class Job:
             finally:
                 lib().bwtmi_free(blob)
             parts = np.frombuffer(b"".join(_comm.allgather_bytes(comm, mine.tobytes())), dtype=np.int64)
-            check(lib().bwtmi_job_load_fasta_parts(self.h, path.encode(), flank_trim, world, rank,
-                                                  parts.ctypes.data_as(C.c_void_p), parts.size))
+            if dev_ctx is not None:
+                check(lib().bwtmi_job_load_fasta_parts_dev(dev_ctx, self.h, path.encode(), flank_trim, world, rank,
+                                                          parts.ctypes.data_as(C.c_void_p), parts.size))
+            else:
+                check(lib().bwtmi_job_load_fasta_parts(self.h, path.encode(), flank_trim, world, rank,
+                                                      parts.ctypes.data_as(C.c_void_p), parts.size))
         elif world > 1:
             check(lib().bwtmi_job_load_fasta_shard(self.h, path.encode(), flank_trim, world, rank))
         else:

@@ -700,6 +700,20 @@ int bwtmi_job_fasta_scan_part(bwtmi_job *job, const char *path, int32_t world, i
     });
 }
 
+int bwtmi_job_load_fasta_parts_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *path, int32_t flank_trim,
+                                   int32_t world, int32_t rank, const int64_t *blob, int64_t nwords) {
+    return guard([&] {
+        CHECK_ARG(ctx && job && path && blob && nwords >= 6 && world >= 1 && rank >= 0 && rank < world,
+                  "bad argument");
+        Ctx &c = ctx->c;
+        job->j.text_join();
+        if (job->dev.bg_ctx && job->dev.bg_ctx != &c) ctx_wait(*job->dev.bg_ctx);
+        use(c);
+        DevLoad dl(c, job);
+        fasta_load_parts(job->j, path, flank_trim, world, rank, blob, nwords, &dl);
+    });
+}
+
 int bwtmi_job_load_fasta_parts(bwtmi_job *job, const char *path, int32_t flank_trim, int32_t world, int32_t rank,
                                const int64_t *blob, int64_t nwords) {
     return guard([&] {

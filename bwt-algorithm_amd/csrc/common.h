@@ -317,7 +317,7 @@ void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world = 
 // table; all ranks' tables (rank order) -> contigs, shard, own bases only
 void fasta_scan_part(Job &job, const char *path, int32_t world, int32_t rank, std::vector<int64_t> &blob);
 void fasta_load_parts(Job &job, const char *path, int32_t flank_trim, int32_t world, int32_t rank,
-                      const int64_t *blob, int64_t nwords);
+                      const int64_t *blob, int64_t nwords, FastaDev *dev = nullptr);
 // fold units -> ranks by longest-processing-time greedy (deterministic; same as
 // bwtmi.dist.assign): returns the contig ids owned by `rank`
 std::vector<int32_t> shard_units(Job &job, int32_t world, int32_t rank);

@@ -624,9 +624,10 @@ void fasta_scan_part(Job &job, const char *path, int32_t world, int32_t rank, st
 }
 
 void fasta_load_parts(Job &job, const char *path, int32_t flank_trim, int32_t world, int32_t rank,
-                      const int64_t *blob, int64_t nwords) {
+                      const int64_t *blob, int64_t nwords, FastaDev *dev) {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
+    job.text_join();
     const int nt = host_threads(job.params);
     struct Inst {
         int32_t contig;
@@ -731,6 +732,9 @@ void fasta_load_parts(Job &job, const char *path, int32_t flank_trim, int32_t wo
     } else {
         p = raw.resize_uninit((size_t)tot);
     }
+    int64_t span = 0;   // own bytes lie in p[0, span)
+    for (const Own &w : own) span = std::max(span, w.off + (w.b - w.a));
+    if (dev) dev->image(p, span);
     if (!inside) {
         const int64_t piece = split_piece(tot, nt);
         std::vector<std::pair<size_t, int64_t>> rd;   // (own index, piece start in its range)
@@ -741,13 +745,17 @@ void fasta_load_parts(Job &job, const char *path, int32_t flank_trim, int32_t wo
             const Own &w = own[rd[(size_t)q].first];
             int64_t o = w.a + rd[(size_t)q].second;
             const int64_t e = std::min(w.b, o + piece);
+            const int64_t o0 = o;
             while (o < e) {
                 const ssize_t r = ::pread(f.fd, p + w.off + (o - w.a), (size_t)(e - o), (off_t)o);
                 if (r <= 0) { bad = true; return; }
                 o += r;
             }
+            if (dev) dev->image_part(w.off + (o0 - w.a), e - o0);
         });
         if (bad) fail(BWTMI_E_IO, "read error");
+    } else if (dev) {
+        for (const Own &w : own) dev->image_part(w.off, w.b - w.a);   // already read by pass 1
     }
     std::vector<int64_t> ca, cb;   // chunk [ca, cb) in the buffer
     for (Own &w : own) {
@@ -790,29 +798,72 @@ void fasta_load_parts(Job &job, const char *path, int32_t flank_trim, int32_t wo
             d += cnt[t];
         }
     }
-    run_tasks((int64_t)NC, nt, [&](int64_t t) {
-        char *d = dst[(size_t)t];
-        const int64_t a0 = ca[(size_t)t], b0 = cb[(size_t)t];
-        if (plain[(size_t)t]) {   // runs between newlines, as load_fasta's pass 2
-            for (int64_t i = a0; i < b0;) {
-                const char *nl = (const char *)std::memchr(p + i, '\n', (size_t)(b0 - i));
-                const int64_t j = nl ? (int64_t)(nl - p) : b0;
-                upper_copy(d, p + i, j - i);
-                d += j - i;
-                i = j + 1;
-            }
+    auto copy_chunk = [](const char *q, int64_t a0, int64_t b0, bool pl, char *d) {
+        if (pl) {   // runs between newlines, as load_fasta's pass 2
+            plain_copy(q, a0, b0, d);
             return;
         }
-        for_lines(p, a0, b0, [&](int64_t s, int64_t e) {
-            if (p[s] == '>') return;
-            upper_copy(d, p + s, e - s);
+        for_lines(q, a0, b0, [&](int64_t s, int64_t e) {
+            if (q[s] == '>') return;
+            upper_copy(d, q + s, e - s);
             d += e - s;
         });
-    });
-    if (std::getenv("BWTMI_STATS")) {
-        auto d = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
-        std::fprintf(stderr, "  load_fasta_parts: stitch %.1f own contigs %.1f ms\n", d(t0, t1), d(t1, clk::now()));
+    };
+    auto stats = [&] {
+        if (std::getenv("BWTMI_STATS")) {
+            auto d = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+            std::fprintf(stderr, "  load_fasta_parts: stitch %.1f own contigs %.1f ms%s\n", d(t0, t1), d(t1, clk::now()),
+                         dev ? " (device placement)" : "");
+        }
+    };
+    if (!dev) {
+        run_tasks((int64_t)NC, nt, [&](int64_t t) { copy_chunk(p, ca[(size_t)t], cb[(size_t)t], plain[(size_t)t], dst[(size_t)t]); });
+        stats();
+        return;
     }
+    // device placement (load_fasta's): plain chunks rebuilt on the device from
+    // the uploaded bytes, the others written here and copied up, the host copy
+    // of the plain chunks written behind the scan
+    dev->contigs();
+    std::vector<int32_t> cid_of(NC, -1);
+    for (const Own &w : own)
+        for (size_t t = w.c0; t < w.c1; ++t) cid_of[t] = (int32_t)w.cid;
+    std::vector<int64_t> rest;
+    std::vector<FastaPiece> pcs;
+    for (size_t t = 0; t < NC; ++t) {
+        if (!dst[t] || !cnt[t]) continue;
+        const int64_t off = dst[t] - job.contigs[(size_t)cid_of[t]].full.data();
+        if (plain[t]) pcs.push_back(FastaPiece{ca[t], cb[t], off, cid_of[t]});
+        else rest.push_back((int64_t)t);
+    }
+    run_tasks((int64_t)rest.size(), nt, [&](int64_t q) {
+        const size_t t = (size_t)rest[(size_t)q];
+        copy_chunk(p, ca[t], cb[t], false, dst[t]);
+    });
+    for (int64_t t : rest) {
+        const Contig &c = job.contigs[(size_t)cid_of[(size_t)t]];
+        dev->piece(cid_of[(size_t)t], dst[(size_t)t] - c.full.data(), dst[(size_t)t], cnt[(size_t)t]);
+    }
+    dev->plain(pcs);
+    // the deferred pass holds the bytes: the thread-local read buffer moves into
+    // it; the pass-1 bytes stay in the job (the next load joins this pass first)
+    std::shared_ptr<Seq> hold = std::make_shared<Seq>();
+    if (!inside) hold->swap(raw);
+    struct Cp {
+        int64_t a, b;
+        char *d;
+    };
+    auto work = std::make_shared<std::vector<Cp>>();
+    for (size_t t = 0; t < NC; ++t)
+        if (plain[t] && dst[t] && cnt[t]) work->push_back(Cp{ca[t], cb[t], dst[t]});
+    const char *src = inside ? p : hold->data();
+    dev->defer(
+        [work, src, nt] {
+            const std::vector<Cp> &W = *work;
+            run_tasks((int64_t)W.size(), nt, [&](int64_t k) { plain_copy(src, W[(size_t)k].a, W[(size_t)k].b, W[(size_t)k].d); });
+        },
+        hold);
+    stats();
 }
 
 }  // namespace bwtmi

@@ -326,6 +326,11 @@ int bwtmi_job_fasta_scan_part(bwtmi_job *job, const char *path, int32_t world, i
                               int64_t *nwords);
 int bwtmi_job_load_fasta_parts(bwtmi_job *job, const char *path, int32_t flank_trim, int32_t world, int32_t rank,
                                const int64_t *blob, int64_t nwords);
+/* the same with this rank's analysed sequences built on ctx's device
+ * (bwtmi_job_load_fasta_dev's placement: plain chunks rebuilt there from the
+ * own contigs' bytes, host copies written behind the next scan) */
+int bwtmi_job_load_fasta_parts_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *path, int32_t flank_trim,
+                                   int32_t world, int32_t rank, const int64_t *blob, int64_t nwords);
 int32_t bwtmi_job_contig_count(const bwtmi_job *job);
 /* analysed length of contig id (its shard weight), also for contigs whose bases
  * live on another rank */

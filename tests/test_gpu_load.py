@@ -133,3 +133,66 @@ def test_device_load_scan_and_reload(gpu_ctx, tmp_path):
                     assert j.device_text(gpu_ctx, cid) == j.contig_seq(cid)[tl:fl - tr]
     assert outs[0] == outs[2] and outs[1] == outs[3]
     assert outs[0] != outs[1]
+
+
+def _scan_part(job, path, world, rank):
+    import ctypes as C
+    from bwtmi._lib import check, lib
+    blob, nw = C.c_void_p(), C.c_int64()
+    check(lib().bwtmi_job_fasta_scan_part(job.h, path.encode(), world, rank, C.byref(blob), C.byref(nw)))
+    try:
+        return np.ctypeslib.as_array(C.cast(blob, C.POINTER(C.c_int64)), shape=(nw.value,)).copy()
+    finally:
+        lib().bwtmi_free(blob)
+
+
+def _split_job(path, world, rank, ctx, threads):
+    """Rank `rank` of a split load, the other ranks' part tables computed here."""
+    import ctypes as C
+    from bwtmi._lib import check, lib
+    from bwtmi.records import Job
+    parts = np.concatenate([_scan_part(Job(threads=threads), path, world, r) for r in range(world)])
+    j = Job(threads=threads)
+    _scan_part(j, path, world, rank)   # this rank's pass-1 bytes, reused by its own contigs
+    args = (j.h, path.encode(), 30, world, rank, parts.ctypes.data_as(C.c_void_p), parts.size)
+    if ctx is None:
+        check(lib().bwtmi_job_load_fasta_parts(*args))
+    else:
+        check(lib().bwtmi_job_load_fasta_parts_dev(ctx, *args))
+    j.names = [j.contig_info(i)[0] for i in range(j.contig_count())]
+    return j
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_device_split_load_matches_host(gpu_ctx, tmp_path, world):
+    """The split multi-rank loader with device placement: every rank's own
+    contigs on the device and on the host equal the host split load's."""
+    from bwtmi import synth
+    path = str(tmp_path / "split.fa")
+    with open(path, "wb") as f:
+        f.write(_plain_tail_fasta_mixed(world))
+    for rank in range(world):
+        h = _split_job(path, world, rank, None, 8)
+        d = _split_job(path, world, rank, gpu_ctx, 8)
+        assert d.names == h.names
+        own = [i for i in range(h.contig_count()) if h.contig_info(i)[1] > 0]
+        for cid in own:
+            assert d.contig_info(cid) == h.contig_info(cid)
+            _, fl, tl, tr = h.contig_info(cid)
+            want = h.contig_seq(cid)
+            assert d.contig_seq(cid) == want, (rank, h.names[cid])
+            assert d.device_text(gpu_ctx, cid) == want[tl:fl - tr], (rank, h.names[cid])
+
+
+def _plain_tail_fasta_mixed(seed: int) -> bytes:
+    from test_host import _plain_tail_fasta
+    from bwtmi import synth
+    r = np.random.default_rng(seed)
+    body = synth.generate_contig(3_000_000, 7)
+    out = bytearray(_plain_tail_fasta(seed))
+    for k in range(4):   # equal synthetic contigs, 60-column lines (the C4 shape)
+        out += b">s" + str(k).encode() + b"\n"
+        a = int(r.integers(0, 1_000_000))
+        seq = body[a:a + 2_000_000]
+        out += b"\n".join(seq[i:i + 60] for i in range(0, len(seq), 60)) + b"\n"
+    return bytes(out)

@@ -59,6 +59,8 @@ def main():
                runs=[])
     split = os.environ.get("C4_SHARD_SPLIT", "1") == "1"   # the split loader (bench / CLI at N > 1)
     res["split_load"] = split
+    devload = os.environ.get("C4_SHARD_DEVLOAD", "1") == "1"   # device placement of the load (bench default)
+    res["device_load"] = devload
     for W, T in [(w, t) for w in worlds for t in tlist]:
         for r in sorted({0, W - 1}):
             job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True, build_index=True,
@@ -75,7 +77,7 @@ def main():
 
             def step():
                 timed("reset", job.reset)
-                timed("load_fasta", job.load_fasta, fa, FLANK, W, r, pc)
+                timed("load_fasta", job.load_fasta, fa, FLANK, W, r, pc, ctx if devload else None)
                 timed("upload", job.upload, ctx)
                 timed("scan", job.scan, ctx)
                 timed("postprocess", job.postprocess)
