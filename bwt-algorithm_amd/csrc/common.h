@@ -211,8 +211,61 @@ constexpr int32_t kRcMaxMotif = 256;
 using RcBatchFn = std::function<void(const RcReq *, int64_t, RcOut *, std::vector<char> &)>;
 
 // ---------------------------------------------------------------- job
-// formatted text in cached huge-page blocks (mem.h)
-using Text = std::basic_string<char, std::char_traits<char>, BigAlloc<char>>;
+// formatted text in cached huge-page blocks (mem.h); the formatters write
+// through a raw cursor into capacity they reserved, so growing never
+// zero-fills (a std::string resize wrote every reserved byte once more)
+class Text {
+public:
+    Text() = default;
+    Text(const char *s, size_t n) {
+        grow(n);
+        if (n) std::memcpy(p_, s, n);
+        n_ = n;
+    }
+    Text(Text &&o) noexcept { swap(o); }
+    Text &operator=(Text &&o) noexcept {
+        swap(o);
+        return *this;
+    }
+    Text(const Text &) = delete;
+    Text &operator=(const Text &) = delete;
+    ~Text() { release(); }
+    const char *data() const { return p_ ? p_ : ""; }
+    char *data() { return p_; }
+    size_t size() const { return n_; }
+    size_t capacity() const { return cap_; }
+    // capacity >= cap, content [0, size) kept
+    void grow(size_t cap) {
+        if (cap <= cap_) return;
+        char *q = (char *)(cap >= kBigMin ? big_alloc(cap) : ::operator new(cap));
+        if (n_) std::memcpy(q, p_, n_);
+        release_keep_size();
+        p_ = q;
+        cap_ = cap;
+    }
+    void set_size(size_t n) { n_ = n; }   // n <= capacity(), bytes written by the caller
+    void swap(Text &o) noexcept {
+        std::swap(p_, o.p_);
+        std::swap(n_, o.n_);
+        std::swap(cap_, o.cap_);
+    }
+
+private:
+    void release_keep_size() {
+        if (p_) {
+            if (cap_ >= kBigMin) big_free(p_, cap_);
+            else ::operator delete(p_);
+        }
+        p_ = nullptr;
+        cap_ = 0;
+    }
+    void release() {
+        release_keep_size();
+        n_ = 0;
+    }
+    char *p_ = nullptr;
+    size_t n_ = 0, cap_ = 0;
+};
 
 // formatted output: header + parts of consecutive rows, each inside one fold unit
 struct Rendered {
