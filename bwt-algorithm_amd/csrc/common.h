@@ -31,16 +31,41 @@ template <class T>
 using NoInit = BigAlloc<T>;
 using HitVec = std::vector<bwtmi_hit, NoInit<bwtmi_hit>>;
 
-// a device-screened strict hit as downloaded (16 B instead of 32): the hit is
-// [start, start + len) with primitive motif length prim, and its copies are
-// len / prim (count after primitive reduction, bwt.py:1957-1961; (end-i)/L
-// otherwise, as end = i + count*L)
-struct ScreenedHit {
-    int64_t start;
-    uint32_t len;
-    uint32_t prim;
+// a device-screened strict hit is [start, start + len) with primitive motif
+// length prim, and its copies are len / prim (count after primitive
+// reduction, bwt.py:1957-1961; (end-i)/L otherwise, as end = i + count*L).
+// Downloaded as one 64-bit word per hit -- start | len << 32 | prim << (32 +
+// lbits), lbits = the bits of the longest span -- when len and prim fit the
+// high half (32 B per hit on the device, 8 B over PCIe), else as two words
+// {start, len | prim << 32}.
+struct ScreenedVec {
+    std::vector<uint64_t, NoInit<uint64_t>> w;
+    int32_t lbits = -1;   // one word per hit when >= 0
+    int64_t size() const { return lbits >= 0 ? (int64_t)w.size() : (int64_t)w.size() / 2; }
+    bool empty() const { return w.empty(); }
+    void clear() {
+        w.clear();
+        lbits = -1;
+    }
+    void swap(ScreenedVec &o) noexcept {
+        w.swap(o.w);
+        std::swap(lbits, o.lbits);
+    }
+    // hit k: start, length, primitive motif length
+    void get(int64_t k, int64_t &start, int64_t &len, int64_t &prim) const {
+        if (lbits >= 0) {
+            const uint64_t x = w[(size_t)k];
+            start = (int64_t)(uint32_t)x;
+            len = (int64_t)((x >> 32) & ((uint64_t(1) << lbits) - 1));
+            prim = (int64_t)(x >> (32 + lbits));
+        } else {
+            start = (int64_t)w[2 * (size_t)k];
+            const uint64_t y = w[2 * (size_t)k + 1];
+            len = (int64_t)(uint32_t)y;
+            prim = (int64_t)(y >> 32);
+        }
+    }
 };
-using ScreenedVec = std::vector<ScreenedHit, NoInit<ScreenedHit>>;
 
 // ---------------------------------------------------------------- contigs
 // contig bases live in cached huge-page blocks (mem.h); the device layer pins

@@ -402,13 +402,21 @@ __global__ void k_final_flags(const int64_t *__restrict__ S, const int64_t *__re
     flag[k] = f ? 1u : 0u;
 }
 
+// kept hits in screen order, one 64-bit word each (lbits >= 0: start | len << 32
+// | prim << (32 + lbits)) or two ({start, len | prim << 32}); common.h ScreenedVec
 __global__ void k_final_compact(const bwtmi_hit *__restrict__ H, const uint32_t *__restrict__ vpos,
                                 const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos, int64_t n,
-                                ScreenedHit *__restrict__ out) {
+                                int lbits, uint64_t *__restrict__ out) {
     const int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x;
     if (k >= n || !flag[k]) return;
     const bwtmi_hit h = H[vpos[k]];
-    out[pos[k]] = ScreenedHit{h.start, (uint32_t)(h.end - h.start), (uint32_t)h.prim_len};
+    const uint64_t len = (uint64_t)(h.end - h.start), prim = (uint64_t)(uint32_t)h.prim_len;
+    if (lbits >= 0) {
+        out[pos[k]] = (uint64_t)(uint32_t)h.start | len << 32 | prim << (32 + lbits);
+    } else {
+        out[2 * (int64_t)pos[k]] = (uint64_t)h.start;
+        out[2 * (int64_t)pos[k] + 1] = (len & 0xFFFFFFFFull) | prim << 32;
+    }
 }
 
 }  // namespace
@@ -476,7 +484,7 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     int32_t *M = c.slot[S_IDX1].as<int32_t>();
     uint32_t *rank_of = c.slot[S_IDX2].as<uint32_t>();
     uint8_t *kept = c.slot[S_IDX3].as<uint8_t>();
-    ScreenedHit *dout = c.slot[S_IDX4].as<ScreenedHit>();
+    uint64_t *dout = c.slot[S_IDX4].as<uint64_t>();   // n * 32 B: room for either layout
     uint32_t *flag = c.slot[S_FLAG].as<uint32_t>(), *pos = c.slot[S_SCAN].as<uint32_t>();
     unsigned long long *d_max = c.slot[S_COUNTS].as<unsigned long long>();
 
@@ -516,15 +524,23 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     KLAUNCH("k_final_flags", 0.0, k_final_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, kept, n, flag);
     HIPCHECK(hipMemsetAsync(flag + n, 0, 4, st));
     exclusive_scan<uint32_t>(c, flag, pos, n + 1);
-    KLAUNCH("k_final_compact", 0.0, k_final_compact, dim3(blocks(n)), dim3(kB), 0, st, d_hits, vpos, flag, pos, n, dout);
+    // one word per kept hit when the longest span and the longest primitive motif
+    // fit the word's high half (BWTMI_SCREEN_WIDE=1: always two)
+    static const bool wide = [] { const char *e = std::getenv("BWTMI_SCREEN_WIDE"); return e && *e == '1'; }();
+    const int lbits = lb;   // bits of the longest span (hit lengths are <= maxlen)
+    const int pbits = std::max(1, bits_for((uint64_t)lmax));
+    out.lbits = !wide && lbits + pbits <= 32 ? lbits : -1;
+    KLAUNCH("k_final_compact", 0.0, k_final_compact, dim3(blocks(n)), dim3(kB), 0, st, d_hits, vpos, flag, pos, n,
+            out.lbits, dout);
     HIPCHECK(hipGetLastError());
     uint32_t nk = 0;
     HIPCHECK(hipMemcpyAsync(&nk, pos + n, 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
-    out.resize(nk);
+    const size_t words = (size_t)nk * (out.lbits >= 0 ? 1 : 2);
+    out.w.resize(words);
     // into a registered block: a pinned DMA instead of a staged pageable copy
-    if (nk) (void)ensure_pinned(out.data(), out.data(), (size_t)nk * sizeof(ScreenedHit));
-    if (nk) HIPCHECK(hipMemcpyAsync(out.data(), dout, (size_t)nk * sizeof(ScreenedHit), hipMemcpyDeviceToHost, st));
+    if (nk) (void)ensure_pinned(out.w.data(), out.w.data(), words * 8);
+    if (nk) HIPCHECK(hipMemcpyAsync(out.w.data(), dout, words * 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
 }
 

@@ -1017,7 +1017,15 @@ void rc_prepare(const UnitCtx &u, const ItemVec &R, int nt, RcTable &T) {
 
 // the fold's output, refined (the refine pass runs inside the parallel
 // assembly: records are independent there)
-ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt) {
+// chunks of the fold's output for the collapse pass: [cut[k], cut[k+1]) with
+// cmax[k] >= the largest end in it (exact unless an equal-start run was
+// reordered across the chunk's edge: then an upper bound, which only moves the
+// collapse's independent cuts later)
+struct OutChunks {
+    std::vector<int64_t> cut, cmax;
+};
+
+ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt, OutChunks *oc = nullptr) {
     const int64_t n = (int64_t)R.size();
     if (n == 0) return {};
     // BWTMI_POST_DEVICE_MIN: smallest unit (records) whose fresh-pair recomputes go to the device
@@ -1112,6 +1120,7 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt) {
     // refine only moves ends, so only runs of equal start need ordering by end
     // -- done here per chunk, then for the runs that cross a chunk edge
     std::vector<uint8_t> by_start((size_t)K, 1);
+    std::vector<int64_t> cm((size_t)K + 1, INT64_MIN);
     auto by_end = [](const Item &x, const Item &y) { return x.end < y.end; };
     parallel_items(K, nt, [&](int64_t k, int w) {
         const SpecOut &sp = spec[(size_t)k];
@@ -1121,7 +1130,12 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt) {
         dst = std::copy(rp.begin(), rp.end(), dst);
         if (synced[(size_t)k])
             for (size_t q = from[(size_t)k]; q < sp.emitted.size(); ++q) *dst++ = sp.record(R, q);
-        for (Item *it = d0; it < dst; ++it) refine_one(u, pools, w, *it);
+        int64_t mx = INT64_MIN;
+        for (Item *it = d0; it < dst; ++it) {
+            refine_one(u, pools, w, *it);
+            mx = std::max(mx, it->end);
+        }
+        cm[(size_t)k] = mx;
         for (Item *it = d0 + 1; it < dst; ++it)
             if (it[-1].start > it->start) { by_start[(size_t)k] = 0; return; }
         for (Item *i = d0; i < dst;) {
@@ -1133,6 +1147,7 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt) {
     });
     out[at[(size_t)K]] = cur;
     refine_one(u, pools, 0, out[at[(size_t)K]]);
+    cm[(size_t)K] = out[at[(size_t)K]].end;   // the last record is chunk K of its own
     bool ordered = true;
     for (int64_t k = 0; k < K; ++k) ordered = ordered && by_start[(size_t)k];
     const size_t N = out.size();
@@ -1145,8 +1160,20 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt) {
         while (i > 0 && out[i - 1].start == out[b].start) --i;
         while (j < N && out[j].start == out[b].start) ++j;
         std::stable_sort(out.begin() + (std::ptrdiff_t)i, out.begin() + (std::ptrdiff_t)j, by_end);
+        // the chunks the run touches share one bound
+        size_t k0 = (size_t)k, k1 = (size_t)k;
+        while (k0 > 0 && at[k0] > i) --k0;
+        while (k1 < (size_t)K && at[k1 + 1] < j) ++k1;
+        int64_t m = INT64_MIN;
+        for (size_t q = k0; q <= k1; ++q) m = std::max(m, cm[q]);
+        for (size_t q = k0; q <= k1; ++q) cm[q] = m;
     }
     if (!ordered) sort_by_pos(out, nt);   // not expected: the general stable sort
+    if (oc && ordered) {
+        oc->cut.assign(at.begin(), at.end());
+        oc->cut.push_back((int64_t)N);
+        oc->cmax.assign(cm.begin(), cm.end());
+    }
     if (g_stats) {
         auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         std::fprintf(stderr, "  merge: repair %.1f assemble %.1f ms\n", d(ts1, ts2),
@@ -1320,9 +1347,9 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
             items.resize(sh.size());
             parallel_for((int64_t)sh.size(), nt, [&](int64_t a, int64_t b) {
                 for (int64_t k = a; k < b; ++k) {
-                    const ScreenedHit &x = sh[(size_t)k];
-                    const int64_t len = x.len, prim = x.prim;
-                    items[(size_t)k] = Item{x.start, x.start + len, nullptr, c, (int32_t)prim};
+                    int64_t s0, len, prim;
+                    sh.get(k, s0, len, prim);
+                    items[(size_t)k] = Item{s0, s0 + len, nullptr, c, (int32_t)prim};
                 }
             });
             ScreenedVec().swap(sh);
@@ -1352,7 +1379,8 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     if (!presorted) dedup_sorted(u, recs);
     auto t2 = clk::now();
     // 3. merge adjacent (bwt.py:3222-3289)
-    recs = merge_fold(u, pools, recs, nt);
+    OutChunks oc;
+    recs = merge_fold(u, pools, recs, nt, &oc);
     auto t3 = clk::now();
     // 4. refine (bwt.py:3291-3314): done inside merge_fold's assembly
     auto r1 = clk::now();   // merge_fold returns its records in (start, end) order
@@ -1390,19 +1418,31 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     size_t n_collapsed = 0;
     {
         const int64_t N = (int64_t)recs.size();
-        const int C = N > 8192 ? 4 * std::max(1, nt) : 1;
-        std::vector<int64_t> cmax((size_t)C, INT64_MIN), sb((size_t)C + 1, N);
-        parallel_items(C, nt, [&](int64_t t, int) {
-            int64_t m = INT64_MIN;
-            for (int64_t k = N * t / C; k < N * (t + 1) / C; ++k) m = std::max(m, recs[(size_t)k].end);
-            cmax[(size_t)t] = m;
-        });
+        // nominal chunks and the largest end in each: the merge fold's output
+        // chunks (it tracked their ends while assembling), else one pass here
+        std::vector<int64_t> nom, cmax;
+        if (one_offset && !oc.cut.empty() && oc.cut.back() == N) {
+            nom = std::move(oc.cut);
+            cmax = std::move(oc.cmax);
+        } else {
+            const int C0 = N > 8192 ? 4 * std::max(1, nt) : 1;
+            nom.resize((size_t)C0 + 1);
+            for (int t = 0; t <= C0; ++t) nom[(size_t)t] = N * t / C0;
+            cmax.assign((size_t)C0, INT64_MIN);
+            parallel_items(C0, nt, [&](int64_t t, int) {
+                int64_t m = INT64_MIN;
+                for (int64_t k = nom[(size_t)t]; k < nom[(size_t)t + 1]; ++k) m = std::max(m, recs[(size_t)k].end);
+                cmax[(size_t)t] = m;
+            });
+        }
+        const int C = (int)cmax.size();
+        std::vector<int64_t> sb((size_t)C + 1, N);
         std::vector<int64_t> pre((size_t)C, INT64_MIN);   // max end before nominal chunk t
         for (int t = 1; t < C; ++t) pre[(size_t)t] = std::max(pre[(size_t)t - 1], cmax[(size_t)t - 1]);
         sb[0] = 0;
         parallel_items(C - 1, nt, [&](int64_t q, int) {
             const int64_t t = q + 1;
-            int64_t i = N * t / C, m = pre[(size_t)t];
+            int64_t i = nom[(size_t)t], m = pre[(size_t)t];
             while (i < N && recs[(size_t)i].start < m) m = std::max(m, recs[(size_t)i++].end);
             sb[(size_t)t] = i;
         });
@@ -1411,16 +1451,17 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
         std::vector<int64_t> cnt((size_t)C + 1, 0);
         parallel_items(C, nt, [&](int64_t t, int) {
             auto &pc = part[(size_t)t];
-            pc.reserve((size_t)(sb[(size_t)t + 1] - sb[(size_t)t]) / 2 + 16);
+            pc.reserve((size_t)(sb[(size_t)t + 1] - sb[(size_t)t]) + 1);   // nearly every record stays
+            int64_t c = 0;   // records passing the final filter, counted as each slot is settled
             for (int64_t k = sb[(size_t)t]; k < sb[(size_t)t + 1]; ++k) {
                 if (!pc.empty() && should_collapse(u, recs[pc.back()], recs[(size_t)k])) {
                     if (!prefer_first(u, recs[pc.back()], recs[(size_t)k])) pc.back() = (uint32_t)k;
                 } else {
+                    if (!pc.empty()) c += pass(pc.back());
                     pc.push_back((uint32_t)k);
                 }
             }
-            int64_t c = 0;
-            for (uint32_t i : pc) c += pass(i);
+            if (!pc.empty()) c += pass(pc.back());
             cnt[(size_t)t + 1] = c;
         });
         for (int t = 0; t < C; ++t) {

@@ -196,3 +196,38 @@ def _plain_tail_fasta_mixed(seed: int) -> bytes:
         seq = body[a:a + 2_000_000]
         out += b"\n".join(seq[i:i + 60] for i in range(0, len(seq), 60)) + b"\n"
     return bytes(out)
+
+
+_SCREEN_SCRIPT = r"""
+import hashlib, os, sys
+sys.path[:0] = [{repo!r}, os.path.join({repo!r}, "bwt-algorithm_amd")]
+from bwtmi import _lib
+from bwtmi.records import Job
+ctx = _lib.ctx(0)
+j = Job(min_copies=3, show_progress=True)
+j.load_fasta({fa!r}, 30, dev_ctx=ctx)
+j.scan(ctx)
+j.postprocess()
+print(hashlib.sha256(j.render("strfinder")).hexdigest(), j.count())
+j.wait(ctx)
+"""
+
+
+def test_screened_hits_one_and_two_word_downloads(tmp_path):
+    """The screened strict hits come down as one 64-bit word each when the
+    longest span and motif fit (the default) or as two (BWTMI_SCREEN_WIDE=1,
+    the layout of spans past 2^32 / (2 * lmax)): same records either way."""
+    import subprocess
+    import sys
+    from bwtmi import synth
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    fa = str(tmp_path / "s.fa")
+    synth.write_fasta(fa, [3_000_000, 1_000_000], 0.02)
+    code = _SCREEN_SCRIPT.format(repo=repo, fa=fa)
+    outs = []
+    for wide in ("0", "1"):
+        env = dict(os.environ, BWTMI_SCREEN_WIDE=wide)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(r.stdout.split()[-2:])
+    assert outs[0] == outs[1] and int(outs[0][1]) > 1000
