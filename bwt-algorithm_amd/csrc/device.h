@@ -214,6 +214,24 @@ struct Ctx {
     } while (0)
 
 // join the context's background device work; rethrows its error
+// The scan's host reads (candidate counts, key widths, hit counts) wait on the
+// stream by polling: a blocking wait (hipDeviceScheduleBlockingSync, kept for
+// the long waits behind host work) sleeps the thread, and its wake-up delays
+// the next dependent launch.  BWTMI_SPIN_SCAN=0: blocking waits here too.
+inline void scan_wait(hipStream_t st) {
+    static const bool spin = [] { const char *e = std::getenv("BWTMI_SPIN_SCAN"); return !(e && *e == '0'); }();
+    if (!spin) {
+        HIPCHECK(hipStreamSynchronize(st));
+        return;
+    }
+    for (;;) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) HIPCHECK(e);
+        __builtin_ia32_pause();
+    }
+}
+
 inline void ctx_join(Ctx &c) {
     if (c.bg.joinable()) c.bg.join();
     if (c.bg_link) *c.bg_link = nullptr;

@@ -437,7 +437,7 @@ static void screen_levels(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int32_t lm
     std::vector<int64_t> fh((size_t)lmax + 2);
     HIPCHECK(hipMemcpyAsync(fh.data(), first, fh.size() * 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipStreamSynchronize(st));
+    scan_wait(st);
     // levels in descending m (ascending group key)
     std::vector<std::pair<int64_t, int64_t>> lv;   // (first, group key)
     for (int64_t g = 0; g <= lmax; ++g)
@@ -493,7 +493,7 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     KLAUNCH("k_maxlen", 0.0, k_maxlen, dim3((unsigned)std::min<int64_t>(1024, blocks(n))), dim3(kB), 0, st, d_hits, n, d_max);
     unsigned long long maxlen = 0;
     HIPCHECK(hipMemcpyAsync(&maxlen, d_max, 8, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
+    scan_wait(st);
     const int mb = std::max(1, bits_for((uint64_t)lmax));
     const int lb = std::max(1, bits_for(maxlen));
     if (lb + mb > 64) fail(BWTMI_E_ARG, "span too long for the screen keys");
@@ -518,7 +518,7 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
         KLAUNCH("k_seg_levels_l", 0.0, (k_seg_levels<1024, kSegCapL, true>), dim3(256), dim3(1024), 0, st, S, E, M, PME,
                 n, kept, ovf_win, d_ovf + 1, d_ovf, 0.5);
         HIPCHECK(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipStreamSynchronize(st));
+        scan_wait(st);
     }
     if (ovf) screen_levels(c, d_hits, n, lmax, mb, kgrp, vgrp, rank_of, S, E, M, PME, kept, nb);
     KLAUNCH("k_final_flags", 0.0, k_final_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, kept, n, flag);
@@ -535,13 +535,13 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     HIPCHECK(hipGetLastError());
     uint32_t nk = 0;
     HIPCHECK(hipMemcpyAsync(&nk, pos + n, 4, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
+    scan_wait(st);
     const size_t words = (size_t)nk * (out.lbits >= 0 ? 1 : 2);
     out.w.resize(words);
     // into a registered block: a pinned DMA instead of a staged pageable copy
     if (nk) (void)ensure_pinned(out.w.data(), out.w.data(), words * 8);
     if (nk) HIPCHECK(hipMemcpyAsync(out.w.data(), dout, words * 8, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
+    scan_wait(st);
 }
 
 }  // namespace bwtmi

@@ -515,14 +515,19 @@ void row_strfinder(Out &o, const Job &job, const Rec &r, const Rec *partner) {
     o.put("%\t-\t");
     o.i(cc); o.c(':'); o.i(r.n_eval); o.c('\t'); o.i(r.n_eval); o.c('\t');
     const int64_t tot = (flanks ? fl.n + fr.n : 0) + core.n;
-    if (tot > 500) {
-        std::string &fc = o.fc;
-        fc.clear();
-        if (flanks) { fc.append(fl.p ? fl.p : "", (size_t)fl.n); fc.append(core.p, (size_t)core.n); fc.append(fr.p ? fr.p : "", (size_t)fr.n); }
-        else fc.assign(core.p, (size_t)core.n);
-        o.put(fc.data(), 250);
+    if (tot > 500) {   // full_seq[:250] + "..." + full_seq[-200:] of fl + core + fr, without building it
+        const View parts[3] = {flanks ? fl : View{}, core, flanks ? fr : View{}};
+        auto put_range = [&](int64_t a, int64_t b) {   // bytes [a, b) of the concatenation
+            int64_t base = 0;
+            for (const View &v : parts) {
+                const int64_t lo = std::max(a, base), hi = std::min(b, base + v.n);
+                if (hi > lo) o.put(v.p + (lo - base), hi - lo);
+                base += v.n;
+            }
+        };
+        put_range(0, 250);
         o.put("...");
-        o.put(fc.data() + fc.size() - 200, 200);
+        put_range(tot - 200, tot);
     } else {
         if (flanks) { o.put(fl); o.put(core); o.put(fr); } else o.put(core);
     }

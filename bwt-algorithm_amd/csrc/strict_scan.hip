@@ -778,7 +778,7 @@ void strict_scan_mm_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min
         std::vector<int64_t> cnt((size_t)rows), sc((size_t)slots * 2);
         HIPCHECK(hipMemcpyAsync(cnt.data(), c.slot[S_MISC2].p, (size_t)rows * 8, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipMemcpyAsync(sc.data(), c.slot[S_MISC0].p, (size_t)slots * 16, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipStreamSynchronize(st));
+        scan_wait(st);
         for (int64_t r = 0; r < rows; ++r) {
             const int64_t L = L0 - r;
             for (int64_t k = 0; k < cnt[(size_t)r]; ++k) {
@@ -796,7 +796,7 @@ void strict_scan_mm_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min
             c.slot[S_HITS].as<bwtmi_hit>(), nh);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipMemcpyAsync(hits.data(), c.slot[S_HITS].p, (size_t)nh * sizeof(bwtmi_hit), hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
+    scan_wait(st);
 }
 
 void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
@@ -830,7 +830,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
         HIPCHECK(hipGetLastError());
         std::vector<int64_t> np((size_t)nL);
         HIPCHECK(hipMemcpyAsync(np.data(), c.slot[S_MISC2].p, np.size() * 8, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipStreamSynchronize(st));
+        scan_wait(st);
         int64_t nh = 0;
         for (auto v : np) nh += v;
         c.slot[S_HITS].ensure((size_t)std::max<int64_t>(nh, 1) * sizeof(bwtmi_hit));
@@ -856,7 +856,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
         if (nh > 0)
             HIPCHECK(hipMemcpyAsync(res.hits.data(), c.slot[S_HITS].p, (size_t)nh * sizeof(bwtmi_hit),
                                     hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipStreamSynchronize(st));
+        scan_wait(st);
         return;
     }
 
@@ -867,7 +867,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
             c.slot[S_COUNTS].as<unsigned long long>());
     unsigned long long present[4];
     HIPCHECK(hipMemcpyAsync(present, c.slot[S_COUNTS].p, sizeof present, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
+    scan_wait(st);
     uint8_t code[256] = {0};
     int sigma = 0;
     for (int b = 0; b < 256; ++b)
@@ -913,7 +913,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
         HIPCHECK(hipGetLastError());
         if (c.timing) HIPCHECK(hipEventRecord(kb, st));
         HIPCHECK(hipMemcpyAsync(segn, d_count, sizeof segn, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipStreamSynchronize(st));
+        scan_wait(st);
         if (c.timing) {
             float ms = 0;
             HIPCHECK(hipEventElapsedTime(&ms, ka, kb));
@@ -978,7 +978,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     HIPCHECK(hipMemcpyAsync(&last_pos, c.slot[S_SCAN].as<uint32_t>() + nc - 1, 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(&last_flag, c.slot[S_FLAG].as<uint32_t>() + nc - 1, 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(&nlong, d_nlong, 8, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
+    scan_wait(st);
     const int64_t nh = (int64_t)last_pos + last_flag;
     c.slot[S_HITS].ensure((size_t)std::max<int64_t>(nh, 1) * sizeof(bwtmi_hit));
     KLAUNCH("k_compact", 0.0, k_compact, dim3(g), dim3(256), 0, st, c.slot[S_CAND_K].as<uint64_t>(), nc, lmax, sb,
@@ -1001,7 +1001,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
             HIPCHECK(hipMemcpyAsync(res.hits.data(), c.slot[S_HITS].p, (size_t)nh * sizeof(bwtmi_hit),
                                     hipMemcpyDeviceToHost, st));
     }
-    HIPCHECK(hipStreamSynchronize(st));
+    scan_wait(st);
     c.kresolve();
     if (c.timing) {
         float ms = 0;
