@@ -90,6 +90,36 @@ int host_threads(const bwtmi_params &p) {
 // runs inline.  Parallel regions go to the calling thread's current pool (the
 // process-wide one unless the thread belongs to a unit group, postprocess).
 namespace {
+// Region hand-off: a region is published by bumping `agen`; workers that
+// finished their last region spin on it for a short while (BWTMI_POOL_SPIN_US,
+// default 60 us) before they block on the condition variable, and the caller
+// spins on `apending` the same way before it blocks.  A step runs dozens of
+// regions separated by short serial parts, so the futex wake-up of 15 sleeping
+// threads (and their serialised re-lock of one mutex) is paid only after a
+// longer pause.  BWTMI_POOL_SPIN_US=0 restores the plain blocking hand-off.
+inline int64_t pool_spin_ns() {
+    static const int64_t ns = [] {
+        const char *e = std::getenv("BWTMI_POOL_SPIN_US");
+        return (int64_t)((e && *e) ? std::atof(e) * 1000.0 : 60000.0);
+    }();
+    return ns;
+}
+inline int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// spin until pred() or the spin window ends; true when pred() held
+template <class P>
+inline bool spin_until(P &&pred) {
+    const int64_t lim = pool_spin_ns();
+    if (lim <= 0) return pred();
+    const int64_t t0 = now_ns();
+    for (int k = 0;; ++k) {
+        if (pred()) return true;
+        __builtin_ia32_pause();
+        if ((k & 63) == 63 && now_ns() - t0 > lim) return pred();
+    }
+}
+
 class Pool {
 public:
     static Pool &global() {
@@ -105,15 +135,17 @@ public:
         }
         std::unique_lock<std::mutex> region(region_mu);   // one region at a time
         grow(nt - 1);
+        bool wake;
         {
             std::lock_guard<std::mutex> lk(mu);
             job = &f;
             want = nt - 1;
-            pending = nt - 1;
             err = nullptr;
-            ++gen;
+            apending.store(nt - 1, std::memory_order_relaxed);
+            agen.store(agen.load(std::memory_order_relaxed) + 1, std::memory_order_release);
+            wake = sleepers > 0;
         }
-        cv.notify_all();
+        if (wake) cv.notify_all();
         Pool *const outer = worker_of;
         worker_of = this;
         try {
@@ -124,8 +156,13 @@ public:
         }
         worker_of = outer;
         // every worker finishes before f (and what it references) goes out of scope
-        std::unique_lock<std::mutex> lk(mu);
-        done.wait(lk, [&] { return pending == 0; });
+        if (!spin_until([&] { return apending.load(std::memory_order_acquire) == 0; })) {
+            std::unique_lock<std::mutex> lk(mu);
+            caller_waits = true;
+            done.wait(lk, [&] { return apending.load(std::memory_order_acquire) == 0; });
+            caller_waits = false;
+        }
+        std::lock_guard<std::mutex> lk(mu);
         job = nullptr;
         if (err) {
             std::exception_ptr e = err;
@@ -137,7 +174,7 @@ public:
         {
             std::lock_guard<std::mutex> lk(mu);
             stop = true;
-            ++gen;
+            agen.store(agen.load(std::memory_order_relaxed) + 1, std::memory_order_release);
         }
         cv.notify_all();
         for (auto &t : th) t.join();
@@ -157,16 +194,21 @@ private:
         int64_t seen = 0;
         {
             std::lock_guard<std::mutex> lk(mu);
-            seen = gen;   // a worker created for the current region still takes part in it
-            if (job && id < want) seen = gen - 1;
+            seen = agen.load(std::memory_order_relaxed);   // a worker created for the current region still takes part in it
+            if (job && id < want) seen -= 1;
         }
         for (;;) {
             const std::function<void(int)> *f;
-            {
+            if (!spin_until([&] { return agen.load(std::memory_order_acquire) != seen; })) {
                 std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return stop || gen != seen; });
+                ++sleepers;
+                cv.wait(lk, [&] { return agen.load(std::memory_order_relaxed) != seen; });
+                --sleepers;
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu);   // job / want / stop of the generation seen
                 if (stop) return;
-                seen = gen;
+                seen = agen.load(std::memory_order_relaxed);
                 if (id >= want) continue;
                 f = job;
             }
@@ -176,8 +218,10 @@ private:
                 std::lock_guard<std::mutex> lk(mu);
                 if (!err) err = std::current_exception();
             }
-            std::lock_guard<std::mutex> lk(mu);
-            if (--pending == 0) done.notify_one();
+            if (apending.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+                std::lock_guard<std::mutex> lk(mu);   // after the decrement: no lost wake-up
+                if (caller_waits) done.notify_one();
+            }
         }
     }
     std::vector<std::thread> th;
@@ -185,8 +229,10 @@ private:
     std::condition_variable cv, done;
     const std::function<void(int)> *job = nullptr;
     std::exception_ptr err;
-    int want = 0, pending = 0;
-    int64_t gen = 0;
+    int want = 0, sleepers = 0;
+    bool caller_waits = false;
+    std::atomic<int64_t> agen{0};
+    std::atomic<int> apending{0};
     bool stop = false;
     static thread_local Pool *worker_of;   // the pool whose region this thread is running
 };

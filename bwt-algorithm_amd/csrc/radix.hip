@@ -58,6 +58,84 @@ __device__ inline T wave_incl_scan(T v) {
     return v;
 }
 
+// Blocked variants of the two chunk kernels: thread t owns the 16 consecutive
+// elements [16t, 16t + 16) of the chunk, read and written as 16-byte vectors
+// (a wave moves 4 KB per 4-8 instructions), scanned in registers; only the
+// 4 wave totals pass through LDS.  The kernels above staged every element in
+// LDS and read it back at a 16-element stride (bank conflicts) -- each of the
+// ~20 scans of a C3 index build over 3.1M tile counts ran at < 1 TB/s.
+template <class T>
+__device__ __forceinline__ bool load_blocked(const T *__restrict__ in, int64_t base, int64_t n, T (&x)[kItems]) {
+    constexpr int NV = kItems * (int)sizeof(T) / 16;
+    if (base + kItems <= n) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(in + base);
+        uint4 v[NV];
+#pragma unroll
+        for (int q = 0; q < NV; ++q) v[q] = p[q];
+        __builtin_memcpy(x, v, sizeof v);
+        return true;
+    }
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) x[i] = base + i < n ? in[base + i] : (T)0;
+    return false;
+}
+
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_chunk_sums_v(const T *__restrict__ in, T *__restrict__ sums, int64_t n) {
+    T x[kItems];
+    load_blocked<T>(in, (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems, n, x);
+    T s = 0;
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) s += x[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    __shared__ T ws[kWaves];
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T t = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) t += ws[w];
+        sums[blockIdx.x] = t;
+    }
+}
+
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_chunk_scan_v(const T *__restrict__ in, T *__restrict__ out,
+                                                         const T *__restrict__ offs, int64_t n) {
+    constexpr int NV = kItems * (int)sizeof(T) / 16;
+    const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems;
+    T x[kItems];
+    const bool full = load_blocked<T>(in, base, n, x);
+    T s = 0;
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        const T t = x[i];
+        x[i] = s;
+        s += t;
+    }
+    const T inc = wave_incl_scan<T>(s);
+    __shared__ T ws[kWaves];
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 63) ws[wv] = inc;
+    __syncthreads();
+    T excl = inc - s + (offs ? offs[blockIdx.x] : (T)0);
+    for (int w = 0; w < wv; ++w) excl += ws[w];
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) x[i] += excl;
+    if (full) {
+        uint4 v[NV];
+        __builtin_memcpy(v, x, sizeof v);
+        uint4 *p = reinterpret_cast<uint4 *>(out + base);
+#pragma unroll
+        for (int q = 0; q < NV; ++q) p[q] = v[q];
+    } else {
+#pragma unroll
+        for (int i = 0; i < kItems; ++i)
+            if (base + i < n) out[base + i] = x[i];
+    }
+}
+
 // exclusive scan of one chunk, adding offs[blockIdx.x] (exclusive chunk prefix)
 template <class T>
 __global__ __launch_bounds__(kBlock) void k_chunk_scan(const T *__restrict__ in, T *__restrict__ out,
@@ -188,13 +266,18 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, c
     static_assert(!SPLIT || sizeof(V) <= sizeof(KT), "values are staged in the key buffer");
     // static LDS: the 256 per-wave digit counters of every wave, the digit bases,
     // the 256/64 wave sums of the digit scan and the key (and value) staging
-    static_assert(sizeof(uint32_t) * (NW * 256 + 256 + 256 / 64) + sizeof(KT) * kT + (SPLIT ? 0 : sizeof(V) * kT) <=
+    static_assert(sizeof(uint32_t) * (NW * 256 + 256 + 256 / 64) + sizeof(KT) * kT + (SPLIT ? (sizeof(KT) == 4 ? kT : 0) : sizeof(V) * kT) <=
                       160 * 1024, "exceeds gfx950's 160 KB of LDS per workgroup");
     __shared__ uint32_t wcnt[NW][256];   // per-wave digit counts, then per-wave digit bases
     __shared__ uint32_t gdelta[256];     // global position of tile slot j = gdelta[digit] + j
     __shared__ uint32_t dsum[256 / 64];  // waves 0-3 own the 256 digits of the scan
     __shared__ KT ks[kT];
     __shared__ V vs_own[SPLIT ? 1 : kT];
+    // 32-bit keys: the digit of tile slot j, from which the value pass re-derives
+    // its global position (no per-item positions held in registers: 80 VGPRs,
+    // 3 workgroups of 8 waves per CU); 64-bit keys keep the positions in registers
+    constexpr bool DG = SPLIT && sizeof(KT) == 4;
+    __shared__ uint8_t dg_s[DG ? kT : 1];
     V *vs = SPLIT ? reinterpret_cast<V *>(ks) : vs_own;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < NW * 256; i += BLOCK) (&wcnt[0][0])[i] = 0;
@@ -203,20 +286,22 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, c
     const int64_t tbase = tile * kT;
     const int64_t wbase = tbase + (int64_t)wv * (ITEMS * 64);
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    // items of this wave that exist: item i of this lane iff i * 64 + lane < lim
+    const int lim = (int)max<int64_t>(0, min<int64_t>(n - wbase, ITEMS * 64));
+    const KT *const kw = kin + wbase + lane;
+    const V *const vw = vin ? vin + wbase + lane : nullptr;
     KT k[ITEMS];
     V v[ITEMS];
-    uint32_t r[ITEMS];   // rank among the wave's earlier keys of the same digit
+    uint32_t slot[ITEMS];   // rank among the wave's earlier keys of the same digit, then the tile slot
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-        const int64_t idx = wbase + i * 64 + lane;
-        const bool valid = idx < n;
-        k[i] = valid ? kin[idx] : (KT)0;
-        if (vin) v[i] = valid ? vin[idx] : (V)0;
+        const bool valid = i * 64 + lane < lim;
+        k[i] = valid ? kw[i * 64] : (KT)0;
+        if (!DG && vin) v[i] = valid ? vw[i * 64] : (V)0;   // DG: loaded once the keys are staged
     }
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-        const int64_t idx = wbase + i * 64 + lane;
-        const bool valid = idx < n;
+        const bool valid = i * 64 + lane < lim;
         const uint32_t d = (uint32_t)((k[i] >> shift) & 255u);
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -226,7 +311,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, c
             peers &= bit ? bal : ~bal;
         }
         const uint32_t before = (uint32_t)__popcll(peers & lt);
-        r[i] = valid ? wcnt[wv][d] + before : 0u;
+        slot[i] = valid ? wcnt[wv][d] + before : 0u;
         __builtin_amdgcn_wave_barrier();
         if (valid && before == 0) wcnt[wv][d] += (uint32_t)__popcll(peers);
         __builtin_amdgcn_wave_barrier();
@@ -258,43 +343,51 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, c
         }
     }
     __syncthreads();
-    uint32_t slot[ITEMS];
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-        const int64_t idx = wbase + i * 64 + lane;
-        slot[i] = 0;
-        if (idx < n) {
+        if (i * 64 + lane < lim) {
             const uint32_t d = (uint32_t)((k[i] >> shift) & 255u);
-            slot[i] = wcnt[wv][d] + r[i];
+            slot[i] += wcnt[wv][d];
             ks[slot[i]] = k[i];
             if (!SPLIT && vin) vs[slot[i]] = v[i];
+        }
+    }
+    if constexpr (DG) {   // the value loads fly while the keys go out (the keys' registers are free now)
+        if (vin) {
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) v[i] = i * 64 + lane < lim ? vw[i * 64] : (V)0;
         }
     }
     __syncthreads();
     const int64_t rem = n - tbase;
     const int cntt = rem < kT ? (int)rem : kT;
-    uint32_t pos[ITEMS];   // global position of tile slot i * BLOCK + t
+    uint32_t pos[DG ? 1 : ITEMS];   // 64-bit keys: global position of tile slot i * BLOCK + t
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const int j = i * BLOCK + threadIdx.x;
-        pos[i] = 0;
         if (j < cntt) {
             const KT key = ks[j];
-            pos[i] = gdelta[(key >> shift) & 255u] + (uint32_t)j;
-            st<NT>(kout + pos[i], key);
-            if (!SPLIT && vout) st<NT>(vout + pos[i], vs[j]);
+            const uint32_t d = (uint32_t)((key >> shift) & 255u);
+            const uint32_t p = gdelta[d] + (uint32_t)j;
+            st<NT>(kout + p, key);
+            if constexpr (DG) dg_s[j] = (uint8_t)d;
+            else pos[i] = p;
+            if (!SPLIT && vout) st<NT>(vout + p, vs[j]);
         }
     }
     if (SPLIT && vin) {
         __syncthreads();   // every key has left the staging buffer
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i)
-            if (wbase + i * 64 + lane < n) vs[slot[i]] = v[i];
+            if (i * 64 + lane < lim) vs[slot[i]] = v[i];
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
             const int j = i * BLOCK + threadIdx.x;
-            if (j < cntt) st<NT>(vout + pos[i], vs[j]);
+            if (j < cntt) {
+                if constexpr (DG) st<NT>(vout + gdelta[dg_s[j]] + (uint32_t)j, vs[j]);
+                else st<NT>(vout + pos[i], vs[j]);
+            }
         }
     }
 }
@@ -349,17 +442,24 @@ void radix_sort_impl(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
 
 }  // namespace
 
+// in place (in == out) is allowed: a chunk's elements are read before any is written
 template <class T>
 static void scan_rec(Ctx &c, const T *in, T *out, int64_t n, T *tmp) {
+    static const int vec = [] { const char *e = std::getenv("BWTMI_SCAN_VEC"); return e ? std::atoi(e) : 1; }();
+    const bool v = vec && (((uintptr_t)in | (uintptr_t)out) & 15) == 0;   // 16-byte vectors need aligned bases
     const int64_t nch = (n + kTile - 1) / kTile;
+    const double bytes = 2.0 * (double)n * (double)sizeof(T);
     if (nch == 1) {
-        KLAUNCH("k_chunk_scan", 0.0, k_chunk_scan<T>, dim3(1), dim3(kBlock), 0, c.stream, in, out, (const T *)nullptr, n);
+        if (v) KLAUNCH("k_chunk_scan", bytes, k_chunk_scan_v<T>, dim3(1), dim3(kBlock), 0, c.stream, in, out, (const T *)nullptr, n);
+        else KLAUNCH("k_chunk_scan", bytes, k_chunk_scan<T>, dim3(1), dim3(kBlock), 0, c.stream, in, out, (const T *)nullptr, n);
         return;
     }
     T *sums = tmp;
-    KLAUNCH("k_chunk_sums", 0.0, k_chunk_sums<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, sums, n);
+    if (v) KLAUNCH("k_chunk_sums", bytes / 2, k_chunk_sums_v<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, sums, n);
+    else KLAUNCH("k_chunk_sums", bytes / 2, k_chunk_sums<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, sums, n);
     scan_rec<T>(c, sums, sums, nch, tmp + nch);
-    KLAUNCH("k_chunk_scan", 0.0, k_chunk_scan<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, out, (const T *)sums, n);
+    if (v) KLAUNCH("k_chunk_scan", bytes, k_chunk_scan_v<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, out, (const T *)sums, n);
+    else KLAUNCH("k_chunk_scan", bytes, k_chunk_scan<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, out, (const T *)sums, n);
 }
 
 template <class T>
