@@ -129,6 +129,7 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
     struct Chunk {
         int32_t first = -1;
         bool mixed = false;
+        std::vector<size_t> bounds;                   // q in the chunk with recs[q].chrom != recs[q - 1].chrom
         std::vector<std::pair<size_t, Rec>> pieces;   // (record index, piece)
     };
     std::vector<Chunk> ck((size_t)CK);
@@ -139,6 +140,7 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
             const Rec &r = recs[q];
             if (C.first < 0) C.first = r.chrom;
             else if (r.chrom != C.first) C.mixed = true;
+            if (q > 0 && r.chrom != recs[q - 1].chrom) C.bounds.push_back(q);
             if (r.motif.size() != 3) continue;
             const Seq &full = job.contigs[(size_t)r.chrom].full;
             if (full.empty()) continue;
@@ -161,10 +163,41 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
         run_tasks(CK, nt, [&](int64_t t) {
             for (size_t q = NR * (size_t)t / (size_t)CK; q < NR * (size_t)(t + 1) / (size_t)CK; ++q) lst[q] = &recs[q];
         });
-    } else {
-        for (const Rec &r : recs) {
-            if (by[(size_t)r.chrom].empty()) chrom_order.push_back(r.chrom);
-            by[(size_t)r.chrom].push_back(&r);
+    } else if (NR > 0) {
+        // the usual multi-contig list: each chromosome's records are one contiguous
+        // run (the fold units are concatenated), so every list is a range, filled in
+        // parallel; otherwise one serial pass
+        std::vector<size_t> runs{0};   // start of each run of equal chromosome
+        for (auto &C : ck) runs.insert(runs.end(), C.bounds.begin(), C.bounds.end());
+        runs.push_back(NR);
+        bool contiguous = true;
+        {
+            std::vector<uint8_t> seen(job.contigs.size(), 0);
+            for (size_t k = 0; k + 1 < runs.size() && contiguous; ++k) {
+                const size_t ch = (size_t)recs[runs[k]].chrom;
+                contiguous = !seen[ch];
+                seen[ch] = 1;
+            }
+        }
+        if (contiguous) {
+            for (size_t k = 0; k + 1 < runs.size(); ++k) {
+                const int32_t ch = recs[runs[k]].chrom;
+                chrom_order.push_back(ch);
+                by[(size_t)ch].resize(runs[k + 1] - runs[k]);
+            }
+            run_tasks(CK, nt, [&](int64_t t) {
+                const size_t a = NR * (size_t)t / (size_t)CK, b = NR * (size_t)(t + 1) / (size_t)CK;
+                size_t k = (size_t)(std::upper_bound(runs.begin(), runs.end(), a) - runs.begin()) - 1;
+                for (size_t q = a; q < b; ++q) {
+                    while (q >= runs[k + 1]) ++k;
+                    by[(size_t)recs[q].chrom][q - runs[k]] = &recs[q];
+                }
+            });
+        } else {
+            for (const Rec &r : recs) {
+                if (by[(size_t)r.chrom].empty()) chrom_order.push_back(r.chrom);
+                by[(size_t)r.chrom].push_back(&r);
+            }
         }
     }
     auto T1 = std::chrono::steady_clock::now();
@@ -647,7 +680,11 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
     for (int64_t a = 0; a < n;) {
         const int32_t un = unit_of(a);
         int64_t e = a;
-        while (e < n && unit_of(e) == un) ++e;
+        if (by_unit_start)   // rows ordered by unit: the unit's run ends at the first larger unit
+            e = (int64_t)(std::partition_point(rows.begin() + (std::ptrdiff_t)a, rows.end(),
+                                               [un](const Row &x) { return x.unit == un; }) - rows.begin());
+        else
+            while (e < n && unit_of(e) == un) ++e;
         const int64_t base = row_base ? row_base[un] : a;
         for (int64_t c = a; c < e; c += CH) chunks.push_back({c, std::min(e, c + CH), base + (c - a), un});
         a = e;

@@ -299,6 +299,45 @@ __global__ __launch_bounds__(kB) void k_dna_rank_put(const uint32_t *__restrict_
         if (base + (int64_t)i * kB < n) rank[p[i] & kPosMask] = h[i];
 }
 
+// The same writes after the pairs are ordered by the top 16 position bits: every
+// position occurs once, so with 2^(bits-16) dividing the 4096-pair tile, tile t
+// holds exactly the positions [4096 t, 4096 t + 4096).  The ranks are placed in
+// an LDS copy of that window and leave as one coalesced 16 KB store (scattered
+// 4-byte stores, even L2-local ones, issue one cache line per lane).  A pair
+// outside the window (not expected) is stored directly.
+template <bool NT>
+__global__ __launch_bounds__(kB) void k_dna_rank_put_tile(const uint32_t *__restrict__ pv, const uint32_t *__restrict__ hd,
+                                                          int64_t n, uint32_t *__restrict__ rank) {
+    constexpr int kT = kB * kPutItems;
+    __shared__ uint32_t win[kT];
+    const int64_t t0 = (int64_t)blockIdx.x * kT;
+    uint32_t p[kPutItems], h[kPutItems];
+#pragma unroll
+    for (int i = 0; i < kPutItems; ++i) {
+        const int64_t r = t0 + (int64_t)i * kB + threadIdx.x;
+        if (NT) {
+            p[i] = r < n ? __builtin_nontemporal_load(pv + r) : 0u;
+            h[i] = r < n ? __builtin_nontemporal_load(hd + r) : 0u;
+        } else {
+            p[i] = r < n ? pv[r] : 0u;
+            h[i] = r < n ? hd[r] : 0u;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kPutItems; ++i) {
+        if (t0 + (int64_t)i * kB + threadIdx.x >= n) continue;
+        const int64_t q = (int64_t)(p[i] & kPosMask) - t0;
+        if (q >= 0 && q < kT) win[q] = h[i];
+        else rank[p[i] & kPosMask] = h[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPutItems; ++i) {
+        const int j = i * kB + threadIdx.x;
+        if (t0 + j < n) rank[t0 + j] = win[j];
+    }
+}
+
 // the <= 16 suffixes with fewer than 16 bases before '$' (their keys are
 // A-padded): each goes to the front of its group, shorter first, and leaves
 // the group; the rest of the group gets the head behind them.  One workgroup.
@@ -828,16 +867,34 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
         c.slot[S_SORT_TMP0].ensure((size_t)n * 4);
         c.slot[S_SORT_TMP1].ensure((size_t)n * 4);
         uint32_t *pv = c.slot[S_SORT_TMP0].as<uint32_t>(), *ph = c.slot[S_SORT_TMP1].as<uint32_t>();
-        radix_pass_k32(c, vals, hd, pv, ph, n, bits - 8);
+        // BWTMI_PUT_PASSES=2 (default): two stable passes order the pairs by the
+        // top 16 position bits, so one workgroup's 4096 pairs cover about 4096
+        // consecutive ranks (16 KB written whole inside the workgroup) instead of
+        // 4096 scattered ranks of a 2^(bits-8) window merged across workgroups in
+        // the XCD's L2 (3.3x write amplification, PMC r03i); 1: one pass
+        static const int put_passes = [] { const char *e = std::getenv("BWTMI_PUT_PASSES"); return e ? std::atoi(e) : 2; }();
+        const bool two = put_passes >= 2 && bits >= 17;
+        if (two) {
+            radix_pass_k32(c, vals, hd, pv, ph, n, bits - 16);
+            radix_pass_k32(c, pv, ph, fe, pe, n, bits - 8);   // fe / pe are free until the refine rounds
+            pv = fe;
+            ph = pe;
+        } else {
+            radix_pass_k32(c, vals, hd, pv, ph, n, bits - 8);
+        }
         // (unused) LDS caps the workgroups per CU, and so the span of positions
         // an XCD writes at once: at 1 workgroup per CU an XCD's 32 x 4096
         // pairs stay within about a quarter of a 2^shift window (2 MB at
         // 100 Mbp) and the L2 merges the stores into whole lines.  r02aj:
         // 1.13-1.36 ms at full occupancy, 0.63 at 2 per CU, 0.55 at 1 per CU
         // (the direct scatter: 2.35)
-        static const int put_lds = [] { const char *e = std::getenv("BWTMI_PUT_LDS"); return e ? std::atoi(e) : 128; }();
+        static const int put_lds_env = [] { const char *e = std::getenv("BWTMI_PUT_LDS"); return e ? std::atoi(e) : -1; }();
+        const int put_lds = put_lds_env >= 0 ? put_lds_env : two ? 0 : 128;   // the occupancy cap serves the one-pass order only
         static const int put_nt = [] { const char *e = std::getenv("BWTMI_PUT_NT"); return e ? std::atoi(e) : 1; }();
-        if (put_nt)
+        if (two && bits - 16 <= 12)   // 2^(bits-16) positions per 16-bit window divide the 4096-pair tile
+            KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put_tile<true>, dim3((unsigned)nput), dim3(kB), 0, st,
+                    pv, ph, n, rank);
+        else if (put_nt)
             KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put<true>, dim3((unsigned)nput), dim3(kB),
                     (size_t)put_lds * 1024, st, pv, ph, n, nput, rank);
         else
