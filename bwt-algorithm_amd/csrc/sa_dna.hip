@@ -12,8 +12,9 @@
 //      of 8 B keys+values instead of 8+ passes of 12 B; the value carries the
 //      suffix start and the code of the base before it (BWT symbol);
 //   3. runs of equal keys (groups): one tiled pass finds them (gs / ge in SA
-//      order) and every suffix's run head; the first ranks go out through a
-//      position partition so the scattered stores stay L2-local;
+//      order) and every suffix's run head; the first ranks go out through two
+//      partition passes by the top 16 position bits, after which each tile of
+//      pairs is one window of positions, written from LDS;
 //   4. groups are finished by prefix doubling over a rank array
 //      (Larsson-Sadakane): rank[i] = SA index of the head of i's group; a
 //      round with h sorts every group by rank[i + h] -- the groups are then
