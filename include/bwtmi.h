@@ -64,7 +64,8 @@ int bwtmi_kernel_stats(bwtmi_ctx *ctx, int enable, int reset, char *out, int64_t
  * (bwt.py:1915-1916).  Hits come out in the reference's emission order
  * (unit_len descending, start ascending).  prim_len = smallest_period_str of
  * the first unit (bwt.py:1956); copies = count after primitive reduction
- * (bwt.py:1957-1961).  max_mismatch must be 0 (the CLI value). */
+ * (bwt.py:1957-1961).  max_mismatch 0 is the CLI value; > 0 compares adjacent
+ * L-blocks by Hamming distance <= max_mismatch (bwt.py:1929-1944, library calls). */
 typedef struct {
     int64_t start;
     int64_t end;
