@@ -91,16 +91,15 @@ int host_threads(const bwtmi_params &p) {
 // process-wide one unless the thread belongs to a unit group, postprocess).
 namespace {
 // Region hand-off: a region is published by bumping `agen`; workers that
-// finished their last region spin on it for a short while (BWTMI_POOL_SPIN_US,
-// default 60 us) before they block on the condition variable, and the caller
-// spins on `apending` the same way before it blocks.  A step runs dozens of
-// regions separated by short serial parts, so the futex wake-up of 15 sleeping
-// threads (and their serialised re-lock of one mutex) is paid only after a
-// longer pause.  BWTMI_POOL_SPIN_US=0 restores the plain blocking hand-off.
+// finished their last region may spin on it for a while (BWTMI_POOL_SPIN_US)
+// before they block on the condition variable, and the caller spins on
+// `apending` the same way before it blocks.  Default 0 (block at once): a
+// 60 us spin sped the W=8 shard step up on one box (r03u) but cost the C3 line
+// ~7 % in an alternating A/B on another (r03z: 2578-2612 vs 2346-2584 Mbp/s).
 inline int64_t pool_spin_ns() {
     static const int64_t ns = [] {
         const char *e = std::getenv("BWTMI_POOL_SPIN_US");
-        return (int64_t)((e && *e) ? std::atof(e) * 1000.0 : 60000.0);
+        return (int64_t)((e && *e) ? std::atof(e) * 1000.0 : 0.0);
     }();
     return ns;
 }
