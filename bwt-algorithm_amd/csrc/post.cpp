@@ -93,13 +93,15 @@ namespace {
 // Region hand-off: a region is published by bumping `agen`; workers that
 // finished their last region may spin on it for a while (BWTMI_POOL_SPIN_US)
 // before they block on the condition variable, and the caller spins on
-// `apending` the same way before it blocks.  Default 0 (block at once): a
-// 60 us spin sped the W=8 shard step up on one box (r03u) but cost the C3 line
-// ~7 % in an alternating A/B on another (r03z: 2578-2612 vs 2346-2584 Mbp/s).
+// `apending` the same way before it blocks.  Default 10 us: it catches the
+// back-to-back regions of a step (C3 2585-2655 vs 2279-2346 Mbp/s and the W=8
+// shard step 8.0-8.1 vs 8.6-8.9 ms, alternating on one box, r03aa), while a
+// 60 us spin, also held through longer serial parts, cost the C3 line ~7 % on
+// another (r03z).  0 = block at once.
 inline int64_t pool_spin_ns() {
     static const int64_t ns = [] {
         const char *e = std::getenv("BWTMI_POOL_SPIN_US");
-        return (int64_t)((e && *e) ? std::atof(e) * 1000.0 : 0.0);
+        return (int64_t)((e && *e) ? std::atof(e) * 1000.0 : 10000.0);
     }();
     return ns;
 }
