@@ -94,10 +94,10 @@ namespace {
 // finished their last region may spin on it for a while (BWTMI_POOL_SPIN_US)
 // before they block on the condition variable, and the caller spins on
 // `apending` the same way before it blocks.  Default 10 us: it catches the
-// back-to-back regions of a step (C3 2585-2655 vs 2279-2346 Mbp/s and the W=8
-// shard step 8.0-8.1 vs 8.6-8.9 ms, alternating on one box, r03aa), while a
-// 60 us spin, also held through longer serial parts, cost the C3 line ~7 % on
-// another (r03z).  0 = block at once.
+// back-to-back regions of a step (alternating A/Bs on two boxes, r03aa/r03ab:
+// C3 +4 % on average, inside the run-to-run spread; W=8 shard step 8.0-8.1 vs
+// 8.6-8.9 ms), while a 60 us spin, also held through longer serial parts, cost
+// the C3 line ~7 % on another box (r03z).  0 = block at once.
 inline int64_t pool_spin_ns() {
     static const int64_t ns = [] {
         const char *e = std::getenv("BWTMI_POOL_SPIN_US");
