@@ -32,9 +32,6 @@ import hashlib
 import json
 import os
 import platform
-import signal
-import socket
-import subprocess
 import sys
 import tempfile
 import time
@@ -48,7 +45,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # VALU issue ceiling: 256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz (MI355X_MICROARCH.md)
 VALU_LANE_OPS_PEAK = 256 * 4 * 32 * 2.4e9
 B_ALG_PER_BASE = 16.7          # compulsory HBM bytes per base, CLI path
-PMC_SUMMARY = os.path.join(REPO, "profiles", "pmc_traffic.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "pmc_traffic.json")            # C3 / C5 kernels
+PMC_SUMMARY_OF = {"C3N": os.path.join(REPO, "profiles", "pmc_traffic_C3N.json")}   # other workloads
 # bench kernel-timer names -> kernel names in the rocprofv3 summaries
 KERNEL_OF = {"radix_scatter_kv8": "k_scatter<u32,u32>", "radix_partition_kv8": "k_scatter<u32,u32>",
              "radix_scatter_kv12": "k_scatter<u64,u32>",
@@ -68,6 +66,9 @@ WORKLOADS = {
     "C3": dict(lengths=[100_000_000], sub_rate=0.0, shared=False, golden="C3p"),
     "C4": dict(lengths=[12_500_000] * 8, sub_rate=0.0, shared=True, golden="C4"),
     "C5": dict(lengths=[100_000_000], sub_rate=0.02, shared=False, golden="C5p"),
+    # C3 with assembly gaps (bwtmi.synth GAP_PROFILES "n2": 3.8 % N in runs of
+    # 10 bp - 958 kbp, ~1e4 single R/Y): the general-alphabet index and scan
+    "C3N": dict(lengths=[100_000_000], sub_rate=0.0, shared=False, golden="C3Np", gaps="n2"),
 }
 
 
@@ -82,14 +83,14 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(sample_bp: int, sub_rate: float, threads: int):
+def cpu_baseline(sample_bp: int, sub_rate: float, threads: int, gaps=None):
     """Native CPU comparator on a bounded sample: the C oracle's index build
     (1 thread) and OpenMP strict scan, then the product's multithreaded host
     post-processing + writer fed through bwtmi_job_add_hits."""
     import oracle
     from bwtmi import synth
     from bwtmi.records import Job
-    seq = synth.generate_contig(sample_bp, 1, sub_rate)
+    seq = synth.generate_contig(sample_bp, 1, sub_rate, gaps=gaps)
     out = os.path.join(tempfile.gettempdir(), f"bwtmi_cpu_{os.getpid()}.tab")
     t0 = time.perf_counter()
     trimmed = seq[FLANK:len(seq) - FLANK]
@@ -163,50 +164,12 @@ def word_compares(n: int, U: int) -> int:
 
 
 def launch_ranks(n: int, argv, script: str = None) -> int:
-    """`bench.py --gpus N` without an external launcher: start N rank processes
-    of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT
-    in their environment, one per GPU) and return the first failing exit code,
-    else 0.  Rank 0 prints the JSON line.  This parent never touches the GPU
-    (no HIP call, nothing loaded from libbwtmi), so starting children is safe;
-    the reference's unit of parallelism is the same: one worker per contig
-    group (bwt.py:3850-3912)."""
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BWTMI_RDZV_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env,
-                                      start_new_session=True))
-    rc = 0
-    try:
-        live = list(procs)
-        while live:
-            time.sleep(0.05)
-            for p in list(live):
-                code = p.poll()
-                if code is None:
-                    continue
-                live.remove(p)
-                if code != 0 and rc == 0:
-                    rc = code if code > 0 else 128 - code
-                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
-                          file=sys.stderr)
-                    for q in live:      # the peers would wait for it in a collective forever
-                        try:
-                            os.killpg(q.pid, signal.SIGTERM)
-                        except ProcessLookupError:
-                            pass
-    finally:
-        for p in procs:
-            if p.poll() is None:
-                try:
-                    os.killpg(p.pid, signal.SIGKILL)
-                except ProcessLookupError:
-                    pass
-                p.wait()
-    return rc
+    """`bench.py --gpus N` without an external launcher: N rank processes of
+    this script, one per GPU (bwtmi.dist.launch_ranks: RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* in their environment, a failing rank stops its
+    peers).  This parent never touches the GPU.  Rank 0 prints the line."""
+    from bwtmi import dist
+    return dist.launch_ranks(n, [sys.executable, script or os.path.abspath(__file__)] + list(argv))
 
 
 def main():
@@ -224,7 +187,7 @@ def main():
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--host-load", action="store_true",
                     help="whole-file load on the host + upload (default: built on the device from the file image)")
-    ap.add_argument("--pmc-summary", default=PMC_SUMMARY,
+    ap.add_argument("--pmc-summary", default=None,
                     help="tools/pmc_traffic.py output giving HBM bytes per launch (roofline.traffic)")
     a = ap.parse_args()
 
@@ -260,11 +223,11 @@ def main():
     if shared:
         fa = os.path.join(tmp, f"bwtmi_bench_{wl_name}_{tag}.fa")
         if rank == 0:
-            synth.write_fasta(fa, wl["lengths"], wl["sub_rate"])
+            synth.write_fasta(fa, wl["lengths"], wl["sub_rate"], gaps=wl.get("gaps"))
         out = os.path.join(tmp, f"bwtmi_bench_{wl_name}_{tag}.tab")
     else:   # one contig (index rank + 1) per rank, own FASTA, own output
         fa = os.path.join(tmp, f"bwtmi_bench_{wl_name}_{tag}_r{rank}.fa")
-        synth.write_fasta(fa, wl["lengths"], wl["sub_rate"], first_index=rank + 1)
+        synth.write_fasta(fa, wl["lengths"], wl["sub_rate"], first_index=rank + 1, gaps=wl.get("gaps"))
         out = os.path.join(tmp, f"bwtmi_bench_{wl_name}_{tag}_r{rank}.tab")
     if c is not None:
         c.barrier()
@@ -360,8 +323,9 @@ def main():
             name, (kms, launches, kbytes) = max(with_bytes.items(), key=lambda kv: kv[1][0])
         achieved = kbytes / (kms / 1e3) / 1e9 if kms > 0 else 0.0
         traffic = None
-        if a.pmc_summary and os.path.exists(a.pmc_summary) and wl_name in ("C3", "C5") and not a.contig_bp:
-            with open(a.pmc_summary) as f:
+        pmc = a.pmc_summary or PMC_SUMMARY_OF.get(wl_name, PMC_SUMMARY)
+        if os.path.exists(pmc) and wl_name in ("C3", "C5", "C3N") and not a.contig_bp:
+            with open(pmc) as f:
                 pk = json.load(f).get("kernels", {}).get(rocprof_name(name))
             if pk:
                 traffic = pk["hbm_bytes_per_launch"]
@@ -381,7 +345,8 @@ def main():
                          gcompares_per_s=round(per_s / 1e9, 1), valu_lane_ops_peak=VALU_LANE_OPS_PEAK,
                          frac_of_valu_issue_at_1_op_per_compare=round(per_s / VALU_LANE_OPS_PEAK, 4))
     e2e_gbs = B_ALG_PER_BASE * total_bp / (elapsed / a.steps) / 1e9
-    cpu = None if a.no_cpu_baseline else cpu_baseline(a.cpu_sample_bp, wl["sub_rate"], host["threads_per_rank"])
+    cpu = None if a.no_cpu_baseline else cpu_baseline(a.cpu_sample_bp, wl["sub_rate"], host["threads_per_rank"],
+                                                        wl.get("gaps"))
     fm = None
     if not a.no_fm:
         first = min(i for i in range(job.contig_count()) if job.contig_info(i)[1] > 0)
@@ -402,7 +367,9 @@ def main():
         "config": {"workload": f"{wl_name}: " + {
                        "C3": "one 100 Mbp synthetic contig per GPU, Tier1+2 defaults with --progress (ungated)",
                        "C4": "8 x 12.5 Mbp contigs in one FASTA, contigs sharded over the GPUs",
-                       "C5": "one 100 Mbp contig with 0.02 substitutions in the planted arrays, --progress"}[wl_name]
+                       "C5": "one 100 Mbp contig with 0.02 substitutions in the planted arrays, --progress",
+                       "C3N": "one 100 Mbp contig with assembly gaps (3.8 % N in runs up to 958 kbp, "
+                              "single R/Y), --progress"}[wl_name]
                    + "; FASTA read -> FM index + strict scan + post-processing -> STRfinder repeat.tab closed",
                    "contig_bp": wl["lengths"][0], "contigs": len(wl["lengths"]) * (1 if shared else world),
                    "parallelism": f"contig-shard x{world}", "index": not a.no_index,

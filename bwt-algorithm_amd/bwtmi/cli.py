@@ -5,6 +5,7 @@ from __future__ import annotations
 import argparse
 import os
 import sys
+from typing import Optional
 
 from .finder import TandemRepeatFinder
 
@@ -56,19 +57,75 @@ def _read_long_reads(path: str):
     return reads
 
 
+# inputs below this size stay in one process: a rank's start-up (interpreter,
+# HIP and RCCL initialisation, ~1-2 s) outweighs what more GPUs save on them
+LAUNCH_MIN_BYTES = 32 << 20
+
+
+def _self_launch(a, argv) -> Optional[int]:
+    """The reference fans contigs out to a Pool of `--jobs` workers (0 = all
+    CPUs, -1 = sequential; bwt.py:3850-3912, 3863-3864, 4336-4358).  Here a
+    worker is a GPU: without an external launcher, `--jobs N|0` starts
+    min(N or #GPUs, #GPUs, #contigs) rank processes of this CLI, one per GPU,
+    that shard the contigs' fold units and write the shared output file
+    (find_and_write_sharded).  Returns their exit code, or None to run in
+    this process: one rank's worth of work, `--jobs -1`, Tier 3 (its records
+    join the scan of every contig in one process), a small input, or
+    BWTMI_CLI_LAUNCH=0.  This process touches no GPU before the launch (the
+    devices are counted in a child).  BWTMI_CLI_RANKS=N forces N ranks over
+    the host transport, rank r on device r mod #GPUs (a rehearsal of an
+    N-GPU node on fewer GPUs)."""
+    from . import dist
+    if dist.is_distributed() or a.jobs == -1 or a.tier3 or os.environ.get("BWTMI_CLI_LAUNCH", "1") == "0":
+        return None
+    forced = int(os.environ.get("BWTMI_CLI_RANKS", "0") or 0)
+    if not forced:
+        try:
+            if os.path.getsize(a.reference) < LAUNCH_MIN_BYTES:
+                return None
+        except OSError:
+            return None
+    cap = forced or (a.jobs if a.jobs > 0 else 1 << 20)
+    n = min(cap, dist.count_fasta_records(a.reference, limit=cap + 1))
+    if n <= 1:
+        return None
+    ndev = dist.count_devices_in_child()
+    if ndev < 1:
+        return None
+    if not forced:
+        n = min(n, ndev)
+        if n <= 1:
+            return None
+    script = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bwt.py")
+
+    def env(r):
+        e = {"BWTMI_CLI_CHILD": "1"}
+        if forced:
+            e.update(BWTMI_COMM="host", BWTMI_DEVICE=str(r % ndev))
+        return e
+    return dist.launch_ranks(n, [sys.executable, script] + list(argv), env)
+
+
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = build_parser().parse_args(argv)
+    child = os.environ.get("BWTMI_CLI_CHILD") == "1"
     tier2 = not a.tier1                                   # bwt.py:4257-4262
     tiers = "Tier 1 (short repeats)" if a.tier1 else "Tier 1 + Tier 2 (short + medium repeats)"
     if a.tier3:
         tiers += " + Tier 3 (very long repeats)"
-    print("BWT-based Tandem Repeat Finder")
-    print("=" * 60)
-    print(f"Reference:    {a.reference}")
-    print(f"Output:       {a.output} ({a.format} format)")
-    print(f"Tiers:        {tiers}")
-    print(f"Engine:       libbwtmi on MI355X (gfx950)")
-    print()
+    if not child:
+        print("BWT-based Tandem Repeat Finder")
+        print("=" * 60)
+        print(f"Reference:    {a.reference}")
+        print(f"Output:       {a.output} ({a.format} format)")
+        print(f"Tiers:        {tiers}")
+        print(f"Engine:       libbwtmi on MI355X (gfx950)")
+        print()
+        sys.stdout.flush()
+        rc = _self_launch(a, argv)
+        if rc is not None:
+            return rc
     finder = TandemRepeatFinder(a.reference, a.sa_sample, show_progress=a.progress,
                                 allow_mismatches=not a.no_mismatches, max_motif_length=a.max_motif_len,
                                 min_period=a.min_period, max_period=a.max_period,

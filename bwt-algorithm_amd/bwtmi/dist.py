@@ -19,7 +19,12 @@ records to rank 0 instead (run_sharded), through the same collective.
 from __future__ import annotations
 
 import os
-from typing import Callable, List, Optional, Sequence
+import signal
+import socket
+import subprocess
+import sys
+import time
+from typing import Callable, Dict, List, Optional, Sequence
 
 import numpy as np
 
@@ -29,6 +34,90 @@ from . import _lib, comm as _comm
 def is_distributed() -> bool:
     """True under a multi-rank launch (WORLD_SIZE > 1)."""
     return int(os.environ.get("WORLD_SIZE", "1")) > 1
+
+
+def launch_ranks(n: int, cmd: Sequence[str], extra_env: Optional[Callable[[int], Dict[str, str]]] = None) -> int:
+    """Start `cmd` as n rank processes of one job on this node (RANK /
+    LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_* in their environment,
+    rank r on GPU r) and wait for them; returns the first failing exit code,
+    else 0.  A failing rank stops its peers (they would wait for it in a
+    collective forever).  The caller must not have touched the GPU: the ranks
+    are fresh processes, as the reference's Pool workers are
+    (bwt.py:3850-3912)."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BWTMI_RDZV_PORT=str(port))
+        if extra_env is not None:
+            env.update(extra_env(r))
+        procs.append(subprocess.Popen(list(cmd), env=env, start_new_session=True))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            time.sleep(0.02)
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bwtmi: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                          file=sys.stderr)
+                    for q in live:
+                        try:
+                            os.killpg(q.pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+    return rc
+
+
+def count_devices_in_child() -> int:
+    """GPUs this process could use, counted in a child process so that the
+    caller never initialises HIP (it may still start rank processes); 0 when
+    there is none or the library cannot be loaded."""
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "try:\n    from bwtmi import _lib; print(_lib.device_count())\n"
+            "except Exception:\n    print(0)\n") % pkg
+    try:
+        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+        return int(out.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError, OSError):
+        return 0
+
+
+def count_fasta_records(path: str, limit: int = 1 << 20) -> int:
+    """Header lines ('>' at a line start) of a FASTA file, counted up to
+    `limit` -- an upper bound on its fold units (bwt.py:3713-3756; natural-key
+    collisions and duplicate names only merge units)."""
+    import mmap
+    try:
+        with open(path, "rb") as f:
+            if os.fstat(f.fileno()).st_size == 0:
+                return 0
+            with mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ) as m:
+                n = 1 if m[:1] == b">" else 0
+                for sep in (b"\n>", b"\r>"):
+                    pos = m.find(sep)
+                    while pos >= 0 and n < limit:
+                        n += 1
+                        pos = m.find(sep, pos + 2)
+                return n
+    except OSError:
+        return 0
 
 
 def init(transport: Optional[str] = None):

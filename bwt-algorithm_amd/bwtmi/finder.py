@@ -35,8 +35,11 @@ class _ContigMap(MutableMapping):
         for i in range(job.contig_count()):
             self._ids[job.contig_info(i)[0]] = i          # a later duplicate wins, in place
         self._vals: Dict[str, str] = {}
+        self._over = set()    # names assigned by the caller (their value replaces the loader's bytes)
 
     def raw(self, name: str) -> bytes:
+        if name in self._over:
+            return self._vals[name].encode("latin-1")
         name_, fl, tl, tr = self._job.contig_info(self._ids[name])
         full = self._job.contig_seq(self._ids[name])
         return full[tl:fl - tr] if self._trimmed else full
@@ -56,10 +59,12 @@ class _ContigMap(MutableMapping):
         if name not in self._ids:
             self._ids[name] = -1
         self._vals[name] = value
+        self._over.add(name)
 
     def __delitem__(self, name: str) -> None:
         del self._ids[name]
         self._vals.pop(name, None)
+        self._over.discard(name)
 
     def __iter__(self):
         return iter(self._ids)

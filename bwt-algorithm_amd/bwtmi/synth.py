@@ -11,6 +11,13 @@ numpy version:
   U{1..6}, 30 % U{7..30}, 10 % U{31..120}; copies U{3..30}; random unit;
 * optional "imperfect" variant: each base inside a planted array is
   substituted with probability `sub_rate` (C5 uses 0.02);
+* optional assembly gaps (`gaps`, a GAP_PROFILES name), laid over the
+  result: runs of `N` after every spacing ~U[a, b], their lengths drawn
+  log-uniformly by decade (a decade d uniform, then a length uniform in
+  [10^d, 10^(d+1)) -- integer arithmetic only), plus single IUPAC `R`/`Y`
+  bases.  Every real assembly carries such runs; they take the index's
+  general-alphabet suffix sort and the scan's 4-plane path (bwt.py:212-264,
+  1921-1999, and the k-mer table's N->A mapping, bwt.py:138-171);
 * output: upper case, 60-column lines, headers ``>contig{k}``.
 """
 from __future__ import annotations
@@ -63,11 +70,51 @@ def _counter_block(seed: int, start: int, count: int) -> np.ndarray:
     return _mix_np(z)
 
 
+# gap profiles: (spacing lo, spacing hi, first decade, last decade) per run
+# class, and the spacing range of single IUPAC bases
+GAP_PROFILES = {
+    # ~1.4 % N in runs of 10 - 999 bp, one R/Y per ~10 kbp
+    "n1": dict(runs=[(2_000, 40_000, 1, 2)], iupac=(1, 20_000)),
+    # n1 plus long gaps of 10 kbp - 1 Mbp every ~10 Mbp (~4-5 % N at 100 Mbp)
+    "n2": dict(runs=[(2_000, 40_000, 1, 2), (3_000_000, 17_000_000, 4, 5)], iupac=(1, 20_000)),
+}
+
+
+def _gap_layout(length: int, seed: int, profile: str) -> Tuple[List[Tuple[int, int]], List[Tuple[int, int]]]:
+    """(start, run length) of every N run and (position, byte) of every IUPAC
+    base of one contig under a GAP_PROFILES profile."""
+    prof = GAP_PROFILES[profile]
+    runs = []
+    for k, (lo, hi, d0, d1) in enumerate(prof["runs"]):
+        rng = _Stream(_mix_int(seed ^ (0x6A90 + k)))
+        cur = 0
+        while True:
+            cur += lo + rng.below(hi - lo + 1)
+            if cur >= length:
+                break
+            d = d0 + rng.below(d1 - d0 + 1)
+            ln = 10 ** d + rng.below(9 * 10 ** d)
+            ln = min(ln, length - cur)
+            runs.append((cur, ln))
+            cur += ln
+    iup = []
+    lo, hi = prof["iupac"]
+    rng = _Stream(_mix_int(seed ^ 0x1A9C))
+    cur = 0
+    while True:
+        cur += lo + rng.below(hi - lo + 1)
+        if cur >= length:
+            break
+        iup.append((cur, b"RY"[rng.below(2)]))
+    return runs, iup
+
+
 def generate_contig(length: int, index: int, sub_rate: float = 0.0,
-                    plants: Optional[List[Tuple[int, int, int]]] = None) -> bytes:
+                    plants: Optional[List[Tuple[int, int, int]]] = None, gaps: Optional[str] = None) -> bytes:
     """Return the sequence bytes of synthetic contig `index`.
 
     `plants`, when given, receives (start, unit_len, copies) per planted array.
+    `gaps` names a GAP_PROFILES entry laid over the contig (None: ACGT only).
     """
     seed = SEED_BASE + index
     bg_seed = _mix_int(seed ^ 0xB6)
@@ -116,6 +163,12 @@ def generate_contig(length: int, index: int, sub_rate: float = 0.0,
         if plants is not None:
             plants.append((cur, unit, copies))
         cur += span
+    if gaps:
+        runs, iup = _gap_layout(length, seed, gaps)
+        for p, b in iup:
+            seq[p] = b
+        for s0, ln in runs:
+            seq[s0:s0 + ln] = ord("N")
     return seq.tobytes()
 
 
@@ -134,13 +187,13 @@ def format_fasta_record(name: str, seq: bytes, width: int = 60) -> bytes:
 
 
 def write_fasta(path: str, lengths: Iterable[int], sub_rate: float = 0.0,
-                first_index: int = 1) -> str:
+                first_index: int = 1, gaps: Optional[str] = None) -> str:
     """Write contigs ``contig{k}`` (k from `first_index`); return sha256 of the file."""
     h = hashlib.sha256()
     tmp = path + ".tmp"
     with open(tmp, "wb") as f:
         for k, n in enumerate(lengths, first_index):
-            rec = format_fasta_record(f"contig{k}", generate_contig(n, k, sub_rate))
+            rec = format_fasta_record(f"contig{k}", generate_contig(n, k, sub_rate, gaps=gaps))
             h.update(rec)
             f.write(rec)
     os.replace(tmp, path)
@@ -153,6 +206,9 @@ CONFIGS = {
     "C3": dict(lengths=[100_000_000], sub_rate=0.0),
     "C4": dict(lengths=[12_500_000] * 8, sub_rate=0.0),
     "C5": dict(lengths=[100_000_000], sub_rate=0.02),
+    # general alphabet: C3 / one C4 contig with assembly gaps (N runs, R/Y)
+    "C3N": dict(lengths=[100_000_000], sub_rate=0.0, gaps="n2"),
+    "G12N": dict(lengths=[12_500_000], sub_rate=0.0, gaps="n2", first_index=2),
 }
 
 
@@ -164,6 +220,7 @@ def main(argv=None) -> int:
     ap.add_argument("--lengths", type=lambda s: [int(x) for x in s.split(",")])
     ap.add_argument("--sub-rate", type=float, default=None)
     ap.add_argument("--first-index", type=int, default=1)
+    ap.add_argument("--gaps", choices=sorted(GAP_PROFILES))
     a = ap.parse_args(argv)
     if a.config:
         cfg = dict(CONFIGS[a.config])
@@ -171,7 +228,9 @@ def main(argv=None) -> int:
         cfg = dict(lengths=a.lengths or [1_000_000], sub_rate=0.0)
     if a.sub_rate is not None:
         cfg["sub_rate"] = a.sub_rate
-    print(write_fasta(a.out, cfg["lengths"], cfg["sub_rate"], a.first_index))
+    if a.gaps:
+        cfg["gaps"] = a.gaps
+    print(write_fasta(a.out, cfg["lengths"], cfg["sub_rate"], a.first_index, cfg.get("gaps")))
     return 0
 
 

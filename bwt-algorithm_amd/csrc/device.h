@@ -48,7 +48,18 @@ struct DBuf {
 struct HBuf {  // pinned host staging
     void *p = nullptr;
     size_t bytes = 0;
+    // async copies still reading the buffer: arm() after queueing them, and
+    // every writer (and ensure / release) settles first
+    hipEvent_t inflight = nullptr;
+    void settle() {
+        if (inflight) HIPCHECK(hipEventSynchronize(inflight));
+    }
+    void arm(hipStream_t st) {
+        if (!inflight) HIPCHECK(hipEventCreateWithFlags(&inflight, hipEventDisableTiming));
+        HIPCHECK(hipEventRecord(inflight, st));
+    }
     void ensure(size_t n) {
+        settle();
         if (n <= bytes) return;
         if (p) HIPCHECK(hipHostFree(p));
         size_t cap = n + n / 8 + 256;
@@ -56,6 +67,11 @@ struct HBuf {  // pinned host staging
         bytes = cap;
     }
     void release() {
+        if (inflight) {
+            (void)hipEventSynchronize(inflight);
+            (void)hipEventDestroy(inflight);
+            inflight = nullptr;
+        }
         if (p) (void)hipHostFree(p);
         p = nullptr;
         bytes = 0;

@@ -132,12 +132,15 @@ void fasta_build_device(Ctx &c, const uint8_t *d_img, const FastaDevPiece *piece
     DPiece *d_pc = (DPiece *)base;
     int32_t *d_segp = (int32_t *)(base + ((tb + 15) & ~size_t(15)));
     uint32_t *d_cnt = (uint32_t *)((char *)d_segp + ((sb + 15) & ~size_t(15)));
-    HBuf &hs = c.host[3];   // pinned staging: the copies run behind this call
-    hs.ensure(tb + sb + 64);
+    // pinned staging: the copies run behind this call, so the previous load's
+    // table copies (another job may share this context) must have read it
+    HBuf &hs = c.host[3];
+    hs.ensure(tb + sb + 64);   // settles the previous copies first
     std::memcpy(hs.p, hp.data(), tb);
     std::memcpy((char *)hs.p + tb, segp.data(), sb);
     HIPCHECK(hipMemcpyAsync(d_pc, hs.p, tb, hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemcpyAsync(d_segp, (char *)hs.p + tb, sb, hipMemcpyHostToDevice, st));
+    hs.arm(st);
     KLAUNCH("k_fa_count", 0.0, k_fa_count, dim3((unsigned)nseg), dim3(kFaThreads), 0, st, d_img, d_pc, d_segp, nseg,
             d_cnt);
     exclusive_scan<uint32_t>(c, d_cnt, d_cnt, nseg);

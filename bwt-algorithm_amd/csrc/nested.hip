@@ -524,12 +524,13 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     KLAUNCH("k_final_flags", 0.0, k_final_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, kept, n, flag);
     HIPCHECK(hipMemsetAsync(flag + n, 0, 4, st));
     exclusive_scan<uint32_t>(c, flag, pos, n + 1);
-    // one word per kept hit when the longest span and the longest primitive motif
-    // fit the word's high half (BWTMI_SCREEN_WIDE=1: always two)
+    // one word per kept hit when the start fits the low half and the longest span
+    // and the longest primitive motif fit the high half (BWTMI_SCREEN_WIDE=1:
+    // always two)
     static const bool wide = [] { const char *e = std::getenv("BWTMI_SCREEN_WIDE"); return e && *e == '1'; }();
     const int lbits = lb;   // bits of the longest span (hit lengths are <= maxlen)
     const int pbits = std::max(1, bits_for((uint64_t)lmax));
-    out.lbits = !wide && lbits + pbits <= 32 ? lbits : -1;
+    out.lbits = !wide && lbits + pbits <= 32 && bits_for((uint64_t)text_len) <= 32 ? lbits : -1;
     KLAUNCH("k_final_compact", 0.0, k_final_compact, dim3(blocks(n)), dim3(kB), 0, st, d_hits, vpos, flag, pos, n,
             out.lbits, dout);
     HIPCHECK(hipGetLastError());

@@ -1520,9 +1520,15 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
             DeferConstruct raw;   // constructed below, in parallel
             out.resize((size_t)cnt[(size_t)C]);
         }
+        // every slot is constructed (a non-throwing pass) before any record is
+        // materialised: a throwing materialize must leave no raw slot behind for
+        // the vector's destructor
+        static_assert(std::is_nothrow_default_constructible<Rec>::value, "Rec() must not throw");
+        parallel_items(C, nt, [&](int64_t t, int) {
+            for (int64_t q = cnt[(size_t)t]; q < cnt[(size_t)t + 1]; ++q) ::new ((void *)&out[(size_t)q]) Rec();
+        });
         parallel_items(C, nt, [&](int64_t t, int) {
             int64_t o = cnt[(size_t)t];
-            for (int64_t q = o; q < cnt[(size_t)t + 1]; ++q) ::new ((void *)&out[(size_t)q]) Rec();
             for (uint32_t i : part[(size_t)t])
                 if (pass(i)) materialize(u, recs[i], shift, out[(size_t)o++]);
         });
@@ -1626,6 +1632,7 @@ void postprocess(Job &job) {
             DeferConstruct raw;   // move-constructed below, in parallel
             job.final_recs.resize(tot);
         }
+        static_assert(std::is_nothrow_move_constructible<Rec>::value, "the parallel moves must not throw");
         run_tasks((int64_t)res.size(), T, [&](int64_t k) {
             Rec *d = job.final_recs.data() + at[(size_t)k];
             for (Rec &r : res[(size_t)k]) ::new ((void *)d++) Rec(std::move(r));

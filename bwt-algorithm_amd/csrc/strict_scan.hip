@@ -755,7 +755,7 @@ void strict_scan_mm_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min
     for (int64_t L0 = lmax; L0 >= lmin;) {
         int64_t rows = 0, slots = 0;
         std::vector<int64_t> off;
-        while (L0 - rows >= lmin) {
+        while (L0 - rows >= lmin && rows < 65535) {   // rows are gridDim.y of k_mm_pbits
             const int64_t cap = n / (min_copies * (L0 - rows)) + 1;
             if (rows && (rows + 1) * (nw + 1) * 4 + (slots + cap) * 16 > budget) break;
             off.push_back(slots);

@@ -27,7 +27,10 @@ here is product code.  Outputs land in tests/golden/ as small data files:
                 O(k^2) nested-suppression loop) swapped for the oracle's
                 restatements -> full-size output SHA-256; the
                 swap is validated against the pure reference on every fixture
-                by `fixtures --check-hybrid`.
+                by `fixtures --check-hybrid`.  Inputs with assembly gaps
+                (N runs) also swap align_repeat_region's one-base case for
+                its closed form, checked against the reference function on
+                20000 random cases before the run.
 """
 from __future__ import annotations
 
@@ -155,7 +158,73 @@ class _StubCore:
         self.text_arr = np.array([], dtype=np.uint8)
 
 
-def install_hybrid(ref, stub_index=True, restate_nested=True):
+def _homopolymer_align(ref):
+    """align_repeat_region (bwt.py:998-1102) for a one-base template and the
+    default indel band, in closed form: a window whose first base differs from
+    the template has the deletion end j = 0 among its best alignments (cost 1,
+    tied with the substitution, first j wins), so _align_unit_to_window fails
+    there and the walk stops; the consensus never changes.  The result is the
+    run of the template base from `start` up to the walk's limit (bwt.py:1033).
+    Validated against the reference function by `_check_homopolymer_align`
+    before every use; it makes assembly gaps (N runs of up to 1 Mbp, each
+    merged ~1000 times) tractable for the hybrid oracle."""
+    orig = ref.MotifUtils.align_repeat_region
+
+    def fast(sequence, start, end, motif_template, mismatch_fraction=0.1, max_indel=None, min_copies=3):
+        if len(motif_template) != 1 or max_indel is not None or len(sequence) == 0:
+            return orig(sequence, start, end, motif_template, mismatch_fraction, max_indel, min_copies)
+        n = len(sequence)
+        start = max(0, start)
+        end = min(n, end if end > start else n)
+        limit = min(n, max(end, start + min_copies) + 4)
+        b = motif_template
+        pos = start
+        while pos < limit:   # run of b, stepping by long slices
+            step = min(limit - pos, 4096)
+            chunk = sequence[pos:pos + step]
+            k = len(chunk) - len(chunk.lstrip(b))
+            pos += k
+            if k < step:
+                break
+        copies = pos - start
+        if copies < min_copies or copies <= 0:
+            return None
+        return ref.RepeatAlignmentSummary(consensus=b, motif_len=1, copies=copies, consumed_length=copies,
+                                          mismatch_rate=0.0, max_errors_per_copy=0, variations=[],
+                                          copy_sequences=[b] * copies, total_insertions=0, total_deletions=0,
+                                          error_counts=[0] * copies)
+    return orig, fast
+
+
+def _check_homopolymer_align(ref, orig, fast, cases=20000):
+    """The closed form equals the reference function on random one-base
+    cases: runs of the template base inside random ACGTNRY text, any start /
+    end (including past the run, at the text's end and end <= start), the
+    callers' min_copies and mismatch fractions."""
+    rng = np.random.default_rng(0x4F11)
+    alpha = "ACGTNRY"
+    for i in range(cases):
+        n = int(rng.integers(1, 120))
+        seq = [alpha[j] for j in rng.integers(0, len(alpha), n)]
+        b = alpha[int(rng.integers(0, len(alpha)))]
+        for _ in range(int(rng.integers(0, 4))):
+            a = int(rng.integers(0, n))
+            seq[a:a + int(rng.integers(1, 40))] = [b] * int(rng.integers(1, 40))
+        seq = "".join(seq)[:n] or b
+        n = len(seq)
+        start = int(rng.integers(-2, n + 2))
+        end = int(rng.integers(-2, n + 6))
+        mc = int(rng.choice([1, 2, 3, 5]))
+        frac = float(rng.choice([0.1, 0.05, 0.2]))
+        tmpl = b if rng.random() < 0.8 else seq[min(max(start, 0), n - 1)]
+        want = orig(seq, start, end, tmpl, mismatch_fraction=frac, min_copies=mc)
+        got = fast(seq, start, end, tmpl, mismatch_fraction=frac, min_copies=mc)
+        if want != got:
+            raise SystemExit(f"homopolymer closed form differs from the reference on case {i}: "
+                             f"{seq!r} {start} {end} {tmpl!r} {frac} {mc}: {want} vs {got}")
+
+
+def install_hybrid(ref, stub_index=True, restate_nested=True, homopolymer=False):
     import oracle
     from oracle import post
 
@@ -182,6 +251,10 @@ def install_hybrid(ref, stub_index=True, restate_nested=True):
         def nested(self, repeats, overlap_threshold=0.5):
             return post.Pipeline({}, {}, {}).suppress_nested(repeats, overlap_threshold)
         ref.TandemRepeatFinder._suppress_nested_short_calls = nested
+    if homopolymer:
+        orig, fast = _homopolymer_align(ref)
+        _check_homopolymer_align(ref, orig, fast)
+        ref.MotifUtils.align_repeat_region = staticmethod(fast)
 
 
 # ------------------------------------------------------------------ commands
@@ -641,20 +714,23 @@ def cmd_hybrid(a):
     """Full-size golden via the validated hybrid oracle."""
     ref = ref_module()
     from bwtmi import synth
-    install_hybrid(ref, stub_index=True, restate_nested=True)
-    work = a.work or tempfile.mkdtemp()
-    fa = os.path.join(work, f"{a.name}.fa")
     cfg = synth.CONFIGS.get(a.config) if a.config else None
     lengths = cfg["lengths"] if cfg else [int(x) for x in a.lengths.split(",")]
     sub = cfg["sub_rate"] if cfg else a.sub_rate
+    gaps = cfg.get("gaps") if cfg else a.gaps
+    first = cfg.get("first_index", 1) if cfg else a.first_index
+    install_hybrid(ref, stub_index=True, restate_nested=True, homopolymer=bool(gaps) or a.homopolymer)
+    work = a.work or tempfile.mkdtemp()
+    fa = os.path.join(work, f"{a.name}.fa")
     t0 = time.time()
-    fa_sha = synth.write_fasta(fa, lengths, sub)
+    fa_sha = synth.write_fasta(fa, lengths, sub, first, gaps)
     args = [os.path.basename(fa), "-o", "out.tab", "--jobs", str(a.jobs)] + a.extra.split()
     run_ref_cli(ref, args, work)
     outp = os.path.join(work, "out.tab")
     with open(outp, "rb") as f:
         data = f.read()
     rec = dict(config=a.config, lengths=lengths, sub_rate=sub, args=a.extra.split(),
+               gaps=gaps, first_index=first, homopolymer_closed_form=bool(gaps) or a.homopolymer,
                fasta_sha256=fa_sha, out_sha256=hashlib.sha256(data).hexdigest(),
                out_rows=data.count(b"\n") - 1, seconds=round(time.time() - t0, 1))
     if a.keep_rows:
@@ -687,6 +763,9 @@ def main():
     p.add_argument("--config")
     p.add_argument("--lengths", default="100000")
     p.add_argument("--sub-rate", type=float, default=0.0)
+    p.add_argument("--gaps", default=None, help="bwtmi.synth GAP_PROFILES name")
+    p.add_argument("--first-index", type=int, default=1)
+    p.add_argument("--homopolymer", action="store_true", help="validated one-base align closed form")
     p.add_argument("--extra", default="")
     p.add_argument("--jobs", type=int, default=-1)
     p.add_argument("--work")

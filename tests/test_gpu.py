@@ -88,6 +88,18 @@ def test_strict_scan_mismatch_vs_oracle(gpu_ctx, n, alpha, seed):
             assert g.shape == o.shape and (g == o).all(), (n, mm, mc)
 
 
+def test_strict_scan_mismatch_many_rows_vs_oracle(gpu_ctx):
+    """max_mismatch > 0 with min_copies 1 and max_unit >= n: more than 65,535
+    unit lengths, so the device batches its rows (gridDim.y of the Hamming
+    pass is at most 65,535)."""
+    from bwtmi.tiers import strict_scan_hits
+    seq = _planted(80_000, 31, b"ACGTN")
+    t = np.frombuffer(seq, dtype=np.uint8)
+    g = strict_scan_hits(t, 1, 80_000, 1, max_mismatch=1)
+    o = oracle.strict_scan(seq, 1, 80_000, 1, 1)
+    assert g.shape == o.shape and (g == o).all()
+
+
 def test_strict_scan_long_runs_and_streaks(gpu_ctx):
     # homopolymers and long periodic arrays: runs spanning many 32-position words
     parts = [b"A" * 5000, b"ACGT" * 700, b"G" * 33, b"CA" * 1000, _rng_text(997, b"ACGT", 3) * 4,
@@ -107,6 +119,16 @@ def test_strict_scan_synthetic_1mbp_vs_oracle(gpu_ctx):
     for sub in (0.0, 0.02):
         seq = synth.generate_contig(1_000_000, 40, sub)
         assert _same(seq, 1, 1000, 3) > 1000
+
+
+def test_strict_scan_10mbp_with_gaps_vs_oracle(gpu_ctx):
+    """A 10 Mbp contig with assembly gaps (4.1 % N in runs of 10 bp - 289 kbp,
+    ~1000 single R/Y; GAP_PROFILES "n2"): raw-byte compares with N == N
+    (bwt.py:1941), so every N run yields one hit per unit length; the text's
+    six symbols take the 4-plane scan.  Against the oracle, bit-exact."""
+    from bwtmi import synth
+    seq = synth.generate_contig(10_000_000, 2, gaps="n2")
+    assert _same(seq, 1, 1000, 3) > 10000
 
 
 # ------------------------------------------------------------------ CLI end to end

@@ -164,6 +164,27 @@ def _split_job(path, world, rank, ctx, threads):
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])
+def test_two_jobs_loaded_back_to_back_on_one_context(gpu_ctx, tmp_path):
+    """Two jobs share one device context (one pinned table-staging buffer):
+    the second load is queued while the first one's image upload and table
+    copies may still be in flight; both jobs' device texts equal their host
+    copies (the staging buffer is settled before it is rewritten)."""
+    from bwtmi import synth
+    from bwtmi.records import Job
+    a, b = str(tmp_path / "a.fa"), str(tmp_path / "b.fa")
+    synth.write_fasta(a, [40_000 + 97 * k for k in range(300)], 0.0, first_index=11)
+    synth.write_fasta(b, [9_000_000, 1_500_000], 0.0, first_index=2, gaps="n2")
+    jobs = []
+    for path in (a, b, a):
+        j = Job()
+        j.load_fasta(path, 30, dev_ctx=gpu_ctx)
+        jobs.append(j)
+    for j in jobs:
+        for cid in range(j.contig_count()):
+            _, fl, tl, tr = j.contig_info(cid)
+            assert j.device_text(gpu_ctx, cid) == j.contig_seq(cid)[tl:fl - tr], (j.names[cid])
+
+
 def test_device_split_load_matches_host(gpu_ctx, tmp_path, world):
     """The split multi-rank loader with device placement: every rank's own
     contigs on the device and on the host equal the host split load's."""

@@ -51,26 +51,55 @@ def test_tier2_gate_boundary_50mbp(gpu_ctx, tmp_path):
         fa.unlink()
 
 
-def _rolling_counts(t2: np.ndarray, k: int) -> np.ndarray:
-    """Occurrences of every k-mer (2-bit code, A<C<G<T) in an ACGT array."""
+def _rolling_counts(t2: np.ndarray, k: int, bad: np.ndarray = None) -> np.ndarray:
+    """Occurrences of every k-mer (2-bit code, A<C<G<T) in an ACGT array;
+    windows holding a position flagged in `bad` (a non-ACGT byte) are not
+    counted."""
     m = t2.size - k + 1
     code = np.zeros(m, dtype=np.uint32)
     for j in range(k):
         code = (code << np.uint32(2)) | t2[j:j + m]
+    if bad is not None:
+        cb = np.concatenate(([0], np.cumsum(bad, dtype=np.int64)))
+        code = code[(cb[k:] - cb[:m]) == 0]
     return np.bincount(code, minlength=4 ** k)
 
 
-def test_index_100mbp_properties(gpu_ctx):
-    """C3's contig (100 Mbp after the trim): SA is a permutation with the
-    sentinel first, sampled adjacent suffixes ascend, BWT = t[SA-1], C/Occ
-    totals, sampled SA = SA[::32], the 8-mer CSR buckets = a bincount of the
-    text's 8-mers (positions ascending inside buckets), and backward search of
-    all 145,338 canonical motifs of 1..10 bp gives intervals whose widths are
-    the motifs' occurrence counts and whose SA rows are occurrences."""
-    from bwtmi import BWTCore, MotifUtils, synth
-    seq = synth.generate_contig(100_000_000, 1)          # C3's contig1
-    body = seq[30:len(seq) - 30]
-    text = body + b"$"
+def _kmer_table(t: np.ndarray, k: int = 8):
+    """The reference's 8-mer table (bwt.py:138-171) restated over arrays: bytes
+    outside ACGTN (either case) are skipped without resetting the rolling
+    window, N counts as A, the window starts at 0 (so the first k-1 valid bases
+    of the text see zero-padded codes), and every valid base at i >= k appends
+    position i-k+1; position 0 only when the first k bytes are all valid.
+    Returns (code, position) of every entry in append order."""
+    lut = np.full(256, 255, dtype=np.uint8)
+    for ch, v in zip(b"ACGTNacgtn", (0, 1, 2, 3, 0, 0, 1, 2, 3, 0)):
+        lut[ch] = v
+    c = lut[t]
+    vpos = np.flatnonzero(c != 255)
+    vc = c[vpos].astype(np.uint32)
+    w = np.zeros(vc.size, dtype=np.uint32)
+    for j in range(k):      # w[i] = codes of valid bases i-k+1..i, zero before the first
+        sh = np.zeros(vc.size, dtype=np.uint32)
+        if j < vc.size:
+            sh[j:] = vc[:vc.size - j]
+        w |= sh << np.uint32(2 * j)
+    keep = vpos >= k
+    code, pos = w[keep], (vpos[keep] - (k - 1)).astype(np.int64)
+    if t.size >= k and (c[:k] != 255).all():
+        code = np.concatenate(([w[k - 1]], code))
+        pos = np.concatenate(([0], pos))
+    return code, pos
+
+
+def _check_index_properties(text: bytes, rng_seed: int = 1):
+    """SA a permutation with the sentinel first, sampled adjacent suffixes
+    ascend (raw byte order, '$' smallest), BWT = t[SA-1], C/Occ totals, sampled
+    SA = SA[::32], the 8-mer CSR equal to the reference's table (bucket sizes
+    and every bucket's positions), and backward search of all 145,338
+    canonical motifs of 1..10 bp giving intervals whose widths are the motifs'
+    occurrence counts and whose SA rows are occurrences."""
+    from bwtmi import BWTCore, MotifUtils
     n = len(text)
     core = BWTCore(text)
     sa = core.suffix_array
@@ -79,7 +108,7 @@ def test_index_100mbp_properties(gpu_ctx):
     seen[sa] = True
     assert seen.all()
     del seen
-    r = np.random.default_rng(1)
+    r = np.random.default_rng(rng_seed)
     for k in r.integers(1, n, 4000).tolist():
         a, b = int(sa[k - 1]), int(sa[k])
         w = 4096
@@ -92,8 +121,9 @@ def test_index_100mbp_properties(gpu_ctx):
     del bwt
     occ = core.occ_checkpoints
     cnt = np.bincount(t, minlength=256)
-    assert sorted(occ) == [36, 65, 67, 71, 84]
-    for c in (36, 65, 67, 71, 84):
+    present = np.flatnonzero(cnt).tolist()
+    assert sorted(occ) == present
+    for c in present:
         assert occ[c][-1] == cnt[c] and core.char_totals[chr(c)] == cnt[c]
         assert core.char_counts[chr(c)] == int(cnt[:c].sum())
     samp = core.sampled_sa
@@ -101,14 +131,15 @@ def test_index_100mbp_properties(gpu_ctx):
     for i in r.integers(0, len(samp), 20000).tolist():
         assert samp[i * 32] == int(sa[i * 32])
     del samp
-    t2 = np.searchsorted(np.frombuffer(b"ACGT", dtype=np.uint8), t[:-1]).astype(np.uint32)
     off, pos = core.kmer_csr()
-    c8 = _rolling_counts(t2, 8)
-    assert np.array_equal(np.diff(off), c8) and off[-1] == n - 8
-    for code in r.integers(0, 65536, 200).tolist():
-        p = pos[off[code]:off[code + 1]]
-        assert (np.diff(p) > 0).all()
-    del off, pos
+    code, kpos = _kmer_table(t)
+    order = np.argsort(code.astype(np.uint16), kind="stable")
+    assert np.array_equal(np.diff(off), np.bincount(code, minlength=65536)) and off[-1] == code.size
+    assert np.array_equal(pos, kpos[order])
+    del off, pos, code, kpos, order
+    bad = ~np.isin(t[:-1], np.frombuffer(b"ACGT", dtype=np.uint8))
+    t2 = np.searchsorted(np.frombuffer(b"ACGT", dtype=np.uint8), t[:-1]).astype(np.uint32) & np.uint32(3)
+    anybad = bool(bad.any())
     pats = [mt for k in range(1, 11) for mt in MotifUtils.enumerate_motifs(k)]
     assert len(pats) == 145338
     got = core.backward_search_batch(pats)
@@ -116,7 +147,7 @@ def test_index_100mbp_properties(gpu_ctx):
     lut = {ord("A"): 0, ord("C"): 1, ord("G"): 2, ord("T"): 3}
     start = 0
     for k in range(1, 11):
-        ck = c8 if k == 8 else _rolling_counts(t2, k)
+        ck = _rolling_counts(t2, k, bad if anybad else None)
         ks = [p for p in pats[start:] if len(p) == k]
         codes = np.array([sum(lut[ord(ch)] << (2 * (k - 1 - j)) for j, ch in enumerate(p)) for p in ks],
                          dtype=np.int64)
@@ -130,6 +161,52 @@ def test_index_100mbp_properties(gpu_ctx):
         for row in range(sp, min(ep + 1, sp + 5)):
             s = int(sa[row])
             assert text[s:s + len(p)] == p, pats[i]
+
+
+def test_index_100mbp_properties(gpu_ctx):
+    """C3's contig (100 Mbp after the trim, ACGT: the DNA suffix sort and the
+    packed-rank search) through _check_index_properties."""
+    from bwtmi import synth
+    seq = synth.generate_contig(100_000_000, 1)          # C3's contig1
+    _check_index_properties(seq[30:len(seq) - 30] + b"$")
+
+
+def test_index_100mbp_properties_with_gaps(gpu_ctx):
+    """C3N's contig: C3 with assembly gaps (3.8 % N in runs of 10 bp - 958
+    kbp, ~1e4 single R/Y; bwtmi.synth GAP_PROFILES "n2").  Non-ACGT text takes
+    the general prefix-doubling suffix sort (ASCII order: N between G and T,
+    bwt.py:212-264), the byte Occ search and the general 8-mer table (N -> A,
+    R/Y skipped, bwt.py:138-171); a 958 kbp N run needs ~16 doubling rounds."""
+    from bwtmi import synth
+    seq = synth.generate_contig(100_000_000, 1, gaps="n2")   # C3N's contig1
+    _check_index_properties(seq[30:len(seq) - 30] + b"$", rng_seed=2)
+
+
+def test_cli_self_launched_ranks_match_one_process(gpu_ctx, tmp_path):
+    """`bwt.py IN.fa --jobs 2` without a launcher starts two rank processes of
+    the CLI (rehearsed on one GPU: BWTMI_CLI_RANKS=2, host transport, both on
+    device 0) that shard the contigs and write the shared file: byte-equal to
+    the one-process output in all five formats (bwt.py:3850-3912, 4141-4198)."""
+    import subprocess
+    import sys
+    from bwtmi import cli, synth
+    fa = tmp_path / "multi.fa"
+    synth.write_fasta(str(fa), [300_000, 120_000, 250_000, 80_000, 200_000], 0.02, first_index=40, gaps="n1")
+    script = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bwt-algorithm_amd", "bwt.py")
+    for fmt in ("strfinder", "bed", "vcf", "trf_table", "trf_dat"):
+        one, many = tmp_path / f"one.{fmt}", tmp_path / f"many.{fmt}"
+        os.environ["BWTMI_CLI_LAUNCH"] = "0"
+        try:
+            assert cli.main([str(fa), "-o", str(one), "--format", fmt, "--jobs", "2"]) == 0
+        finally:
+            del os.environ["BWTMI_CLI_LAUNCH"]
+        env = dict(os.environ, BWTMI_CLI_RANKS="2")
+        r = subprocess.run([sys.executable, script, str(fa), "-o", str(many), "--format", fmt, "--jobs", "2"],
+                           env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert "Completed! Found" in r.stdout
+        assert many.read_bytes() == one.read_bytes(), fmt
+        assert one.read_bytes().count(b"\n") > 100, fmt
 
 
 def test_rccl_one_rank_collectives_and_sharded_write(gpu_ctx, golden_dir, tmp_path):
@@ -193,3 +270,12 @@ def test_cli_deferred_indices_build_on_use(gpu_ctx, golden_dir):
         assert (core.suffix_array == ref.sa).all() and (core.bwt_arr == ref.bwt).all(), name
         assert core.backward_search("AC") == ref.backward_search(b"AC")
         assert core.text == seqs[name] + "$"
+    # a caller's override (and a new name) is what the deferred index is built over
+    names = list(seqs)
+    seqs[names[0]] = "ACGTACGTTTGACCA" * 7
+    seqs["extra"] = "GATTACA" * 9
+    f.build_indices(seqs)
+    for name in (names[0], "extra"):
+        core = f.bwt_cores[name]
+        ref = oracle.Index(seqs[name].encode() + b"$")
+        assert (core.suffix_array == ref.sa).all() and core.text == seqs[name] + "$", name

@@ -276,6 +276,28 @@ def test_save_results_over_plain_record_lists(golden_dir, tmp_path, built_lib):
         assert out.read_text() == post.render(p, [], fmt), fmt
 
 
+def test_sequence_map_overrides(golden_dir, built_lib):
+    """finder.sequences after load_reference: decoded on demand from the
+    loader; a caller's assignment replaces a value (also for what a deferred
+    index is built over, `raw`), a new name is added at the end, a deletion
+    removes it -- the dict semantics of the reference's `sequences`
+    (bwt.py:3713-3756)."""
+    from bwtmi import TandemRepeatFinder
+    fa = os.path.join(golden_dir, "inputs", "test2.fa")
+    f = TandemRepeatFinder(fa)
+    seqs = f.load_reference()
+    want, full, _ = post.load_fasta(fa, 30)
+    assert list(seqs) == list(want) and all(seqs[k] == v for k, v in want.items())
+    names = list(seqs)
+    seqs[names[1]] = "ACGT" * 5
+    seqs["new_contig"] = "GATTACA"
+    assert seqs.raw(names[1]) == b"ACGT" * 5 and seqs[names[1]] == "ACGT" * 5
+    assert seqs.raw("new_contig") == b"GATTACA" and list(seqs)[-1] == "new_contig"
+    assert seqs.raw(names[0]) == want[names[0]].encode()
+    del seqs[names[1]]
+    assert names[1] not in seqs and len(seqs) == len(want)
+
+
 def test_native_postprocess_and_writers_match_goldens(golden_dir, built_lib):
     for name, m, d in _cases(golden_dir):
         j = _native_job(os.path.join(golden_dir, "inputs", m["input"]), d)
@@ -673,3 +695,81 @@ def test_banded_dp_avx512_and_scalar_paths_agree(tmp_path, built_lib):
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(r.stdout.strip())
     assert outs[0] == outs[1] and len(outs[0]) == 64
+
+
+def test_rank_launcher_env_and_failure(tmp_path):
+    """dist.launch_ranks: N fresh processes with RANK / LOCAL_RANK /
+    WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_* set (rank r on GPU r), per-rank
+    extra environment, exit code 0; a failing rank's code comes back and its
+    peers are stopped instead of waiting forever."""
+    import json
+    import sys
+    import time
+    from bwtmi import dist
+    script = tmp_path / "rank.py"
+    script.write_text(
+        "import json, os, sys, time\n"
+        "keys = ['RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'LOCAL_WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT', 'X']\n"
+        "json.dump({k: os.environ.get(k) for k in keys}, open(sys.argv[1] + os.environ['RANK'], 'w'))\n"
+        "if os.environ.get('X') == 'fail':\n    sys.exit(3)\n"
+        "if os.environ.get('X') == 'hang':\n    time.sleep(600)\n")
+    out = str(tmp_path / "env")
+    assert dist.launch_ranks(3, [sys.executable, str(script), out], lambda r: {"X": f"v{r}"}) == 0
+    envs = [json.load(open(out + str(r))) for r in range(3)]
+    assert [e["RANK"] for e in envs] == ["0", "1", "2"] and [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2"]
+    assert {e["WORLD_SIZE"] for e in envs} == {"3"} and {e["LOCAL_WORLD_SIZE"] for e in envs} == {"3"}
+    assert {e["MASTER_ADDR"] for e in envs} == {"127.0.0.1"} and len({e["MASTER_PORT"] for e in envs}) == 1
+    assert [e["X"] for e in envs] == ["v0", "v1", "v2"]
+    t0 = time.time()
+    rc = dist.launch_ranks(2, [sys.executable, str(script), out], lambda r: {"X": "fail" if r == 1 else "hang"})
+    assert rc == 3 and time.time() - t0 < 60
+
+
+def test_cli_self_launch_decisions(tmp_path, monkeypatch):
+    """`bwt.py IN.fa --jobs N|0` without a launcher: min(N or #GPUs, #GPUs,
+    #contigs) ranks of the same CLI (bwt.py:3850-3912, 3863-3864), one per
+    GPU; one process for --jobs -1, Tier 3, one contig, small inputs or no
+    GPU; BWTMI_CLI_RANKS forces a host-transport rehearsal with rank r on
+    device r mod #GPUs.  The launch itself is stubbed."""
+    from bwtmi import cli, dist, synth
+    fa = tmp_path / "in.fa"
+    synth.write_fasta(str(fa), [2000] * 6, 0.0)
+    assert dist.count_fasta_records(str(fa)) == 6 and dist.count_fasta_records(str(fa), limit=3) == 3
+    crlf = tmp_path / "crlf.fa"
+    crlf.write_bytes(b">a\r\nACGT\r\n>b\r\nAC\r\n")
+    lone = tmp_path / "cr.fa"
+    lone.write_bytes(b">a\rACGT\r>b\rAC\r>c\rA")
+    assert dist.count_fasta_records(str(crlf)) == 2 and dist.count_fasta_records(str(lone)) == 3
+    calls = []
+    monkeypatch.setattr(dist, "launch_ranks", lambda n, cmd, env: calls.append((n, cmd, [env(r) for r in range(n)])) or 0)
+    monkeypatch.setattr(cli, "LAUNCH_MIN_BYTES", 0)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("BWTMI_CLI_RANKS", raising=False)
+
+    def decide(args, ndev):
+        calls.clear()
+        monkeypatch.setattr(dist, "count_devices_in_child", lambda: ndev)
+        a = cli.build_parser().parse_args([str(fa)] + args)
+        rc = cli._self_launch(a, [str(fa)] + args)
+        return None if rc is None else calls[0]
+
+    assert decide(["--jobs", "0"], 8)[0] == 6
+    assert decide([], 8)[0] == 4                        # --jobs 4 (the default): 4 workers
+    assert decide(["--jobs", "0"], 2)[0] == 2
+    n, cmd, envs = decide(["--jobs", "3", "--format", "vcf"], 8)
+    assert n == 3 and cmd[1].endswith("bwt.py") and cmd[2:] == [str(fa), "--jobs", "3", "--format", "vcf"]
+    assert envs == [{"BWTMI_CLI_CHILD": "1"}] * 3
+    assert decide(["--jobs", "-1"], 8) is None
+    assert decide(["--jobs", "0", "--tier3"], 8) is None
+    assert decide(["--jobs", "0"], 1) is None
+    assert decide(["--jobs", "0"], 0) is None
+    monkeypatch.setenv("BWTMI_CLI_RANKS", "5")
+    n, cmd, envs = decide(["--jobs", "0"], 2)
+    assert n == 5 and [e["BWTMI_DEVICE"] for e in envs] == ["0", "1", "0", "1", "0"]
+    assert {e["BWTMI_COMM"] for e in envs} == {"host"}
+    monkeypatch.delenv("BWTMI_CLI_RANKS")
+    monkeypatch.setattr(cli, "LAUNCH_MIN_BYTES", 1 << 30)
+    assert decide(["--jobs", "0"], 8) is None
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setattr(cli, "LAUNCH_MIN_BYTES", 0)
+    assert decide(["--jobs", "0"], 8) is None           # already one rank of a launched job
