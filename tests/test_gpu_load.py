@@ -163,7 +163,6 @@ def _split_job(path, world, rank, ctx, threads):
     return j
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
 def test_two_jobs_loaded_back_to_back_on_one_context(gpu_ctx, tmp_path):
     """Two jobs share one device context (one pinned table-staging buffer):
     the second load is queued while the first one's image upload and table
@@ -185,6 +184,7 @@ def test_two_jobs_loaded_back_to_back_on_one_context(gpu_ctx, tmp_path):
             assert j.device_text(gpu_ctx, cid) == j.contig_seq(cid)[tl:fl - tr], (j.names[cid])
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_device_split_load_matches_host(gpu_ctx, tmp_path, world):
     """The split multi-rank loader with device placement: every rank's own
     contigs on the device and on the host equal the host split load's."""
