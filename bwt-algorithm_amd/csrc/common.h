@@ -204,6 +204,10 @@ struct AlignSummary {
     std::string variations;  // ';'-joined
     bool any_variation = false;
 };
+// first position >= pos and < lim whose byte differs from b (lim if none):
+// the end of a homopolymer run, 32 bytes per step (assembly gaps hold N runs
+// of up to megabases, and a run is walked by every recompute merging into it)
+int64_t run_end(const char *s, int64_t pos, int64_t lim, char b);
 // MotifUtils.align_repeat_region (bwt.py:998-1102), max_indel=None, frac=0.1
 bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_t end,
                          const std::string &tmpl, int64_t min_copies, AlignSummary &out,

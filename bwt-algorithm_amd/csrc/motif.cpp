@@ -612,6 +612,18 @@ void consensus_from(const Scratch &S, int64_t m, const std::string &fallback, st
 
 }  // namespace
 
+int64_t run_end(const char *s, int64_t pos, int64_t lim, char b) {
+    const __m256i vb = _mm256_set1_epi8(b);
+    while (pos + 32 <= lim) {
+        const uint32_t eq = (uint32_t)_mm256_movemask_epi8(
+            _mm256_cmpeq_epi8(_mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + pos)), vb));
+        if (eq != 0xFFFFFFFFu) return pos + __builtin_ctz(~eq);
+        pos += 32;
+    }
+    while (pos < lim && s[pos] == b) ++pos;
+    return pos;
+}
+
 struct AlignScratch {
     Scratch S;
     std::string cur;
@@ -645,8 +657,7 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
         const int64_t limit = std::min<int64_t>(
             seq_len, std::max<int64_t>(end, start + min_copies) + std::max<int64_t>(3, max_indel * 4));
         const char b = tmpl[0];
-        int64_t pos = start;
-        while (pos < limit && seq[pos] == b) ++pos;
+        const int64_t pos = start < limit ? run_end(seq, start, limit, b) : start;
         const int64_t copies = pos - start;
         if (copies < min_copies || copies <= 0) return false;
         if (out.want_copies) {

@@ -403,6 +403,11 @@ struct Pools {
         // the worker's DP scratch and summary (recompute)
         std::unique_ptr<AlignScratch, void (*)(AlignScratch *)> as{align_scratch_new(), align_scratch_free};
         AlignSummary sum;
+        // the last maximal homopolymer run this worker walked: [hlo, hhi) of
+        // byte hb in sequence hseq (sequences do not change while the pools live)
+        const char *hseq = nullptr;
+        int64_t hlo = 0, hhi = 0;
+        char hb = 0;
     };
     static constexpr size_t XB = 16384, CB = size_t(2) << 20;   // Extras are trivially destructible
     std::vector<Arena> a;
@@ -680,11 +685,18 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
         // always succeeds (the run holds the template itself).
         const char b = seq[start];
         const int64_t mc = std::max<int64_t>(1, u.min_copies);
-        auto run_to = [&](int64_t limit) {
-            int64_t pos = start;
-            while (pos < limit && seq[pos] == b) ++pos;
-            return pos - start;
-        };
+        // the maximal run of b through start: a merge chain over one long run
+        // (an assembly gap's N run yields a hit per unit length, ~1000 of them,
+        // each merge recomputing the union) walks it once per worker
+        Pools::Arena &HA = pools.a[(size_t)w];
+        if (!(HA.hseq == seq && HA.hb == b && HA.hlo <= start && start < HA.hhi)) {
+            HA.hseq = seq;
+            HA.hb = b;
+            HA.hlo = start;
+            HA.hhi = run_end(seq, start, L, b);
+        }
+        const int64_t hhi = HA.hhi;
+        auto run_to = [&](int64_t limit) { return std::min(hhi, limit) - start; };
         int64_t run = run_to(std::min<int64_t>(L, std::max<int64_t>(end, start + mc) + 4));
         if (run < mc) run = run_to(std::min<int64_t>(L, std::max<int64_t>(end, start + 1) + 4));
         Extra x;

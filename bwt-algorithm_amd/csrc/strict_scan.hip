@@ -103,7 +103,22 @@ struct CandOut {
     int64_t seg_cap;
     int32_t umax;
     int32_t sb;   // key = (umax - L) << sb | s, sb = bits of the text length
+    // streaks whose end lies more than one 64-word step away: (L, start, first
+    // word still to scan) triples, ended by k_streak_end one wave each
+    int64_t *pend;                 // [pend_cap][3]
+    unsigned long long *npend;     // entries pushed (may exceed pend_cap: the host retries)
+    int64_t pend_cap;
 };
+
+// defer the end search of a streak (one lane)
+__device__ __forceinline__ void push_pending(const CandOut &o, int64_t L, int64_t s, int64_t q0) {
+    const unsigned long long at = atomicAdd(o.npend, 1ull);
+    if ((int64_t)at < o.pend_cap) {
+        o.pend[3 * at] = L;
+        o.pend[3 * at + 1] = s;
+        o.pend[3 * at + 2] = q0;
+    }
+}
 
 // candidate at slot idx of segment seg, reserved by the wave (slots past
 // seg_cap are counted, not written: the host retries with larger segments)
@@ -222,15 +237,18 @@ __global__ __launch_bounds__(256) void k_runs(const uint32_t *__restrict__ P, in
         int64_t e_streak = sstart && above ? (w + (src - lane)) * 32 + (int64_t)__ffs(~Mend) - 1 : -1;
         const bool beyond = sstart && !above;
         if (__any(beyond)) {   // at most one lane: the streak runs past lane 63's word
-            for (int64_t q0 = wave_base + 63;; q0 += 64) {
-                const uint32_t Mq = eq32<B>(P, q0 + lane, L, n);   // 0 past the text: ends the scan
-                const uint64_t nb = __ballot(Mq != FULL);
-                if (nb) {
-                    const int f = __ffsll((unsigned long long)nb) - 1;
-                    const uint32_t Mf = (uint32_t)__shfl((int)Mq, f, 64);
-                    if (beyond) e_streak = (q0 + f) * 32 + (int64_t)__ffs(~Mf) - 1;
-                    break;
-                }
+            // one 64-word step here; a streak longer than that (an assembly gap's
+            // N run is one for every unit length) is ended by k_streak_end, so
+            // the unit lengths' walks do not chain through this wave
+            const int64_t q0 = wave_base + 63;
+            const uint32_t Mq = eq32<B>(P, q0 + lane, L, n);   // 0 past the text: ends the scan
+            const uint64_t nb = __ballot(Mq != FULL);
+            if (nb) {
+                const int f = __ffsll((unsigned long long)nb) - 1;
+                const uint32_t Mf = (uint32_t)__shfl((int)Mq, f, 64);
+                if (beyond) e_streak = (q0 + f) * 32 + (int64_t)__ffs(~Mf) - 1;
+            } else if (beyond) {
+                push_pending(out, L, j0 - (int64_t)__clz(~Mp), q0 + 64);
             }
         }
         if (owned) {
@@ -654,43 +672,81 @@ __global__ __launch_bounds__(256) void k_runs_sparse(const uint32_t *__restrict_
             if (!inb || lim <= 0) M = 0u;
             else if (lim < 32) M &= (1u << lim) - 1u;
         }
-        uint64_t full = __ballot(M == FULL);   // uniform
-        while (full) {
-            const int src = __ffsll((unsigned long long)full) - 1;
-            full &= full - 1;
-            const int64_t ws = (int64_t)__builtin_amdgcn_readlane((int)(w / s), src) * s;   // the owner candidate's word
-            // start: the first non-full word among ws-1 .. ws-s (word ws-s is the
-            // previous sample: all s full means that sample's run, not ours)
-            int64_t start = -1;
-            for (int64_t b0 = 1; b0 <= s; b0 += 64) {
-                const int64_t kk = b0 + lane;
-                const bool look = kk <= s;
-                const uint32_t Mq = look ? eq32<B>(P, ws - kk, L, n) : FULL;   // 0 before the text
-                const uint64_t nb = __ballot(look && Mq != FULL);
-                if (nb) {   // readlane: start (and the `continue` below) stay scalar
-                    const int f = __ffsll((unsigned long long)nb) - 1;
-                    const uint32_t Mf = (uint32_t)__builtin_amdgcn_readlane((int)Mq, f);
-                    start = (ws - (b0 + f) + 1) * 32 - (int64_t)__clz(~Mf);
-                    break;
-                }
+        // owner test, every full lane at once: the first non-full word among
+        // w-1 .. w-s gives the run's start (word w-s is the previous sample: all
+        // s full means that sample's run, not ours).  Inside a long streak every
+        // sample is full, so the s words are checked 8 loads at a time per lane
+        // rather than one lane after another for the whole wave.
+        int64_t start = -1;
+        if (__any(M == FULL) && M == FULL) {
+            for (int64_t k0 = 1; k0 <= s && start < 0; k0 += 8) {
+                uint32_t Mq[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) Mq[i] = k0 + i <= s ? eq32<B>(P, w - (k0 + i), L, n) : FULL;   // 0 before the text
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (start < 0 && Mq[i] != FULL) start = (w - (k0 + i) + 1) * 32 - (int64_t)__clz(~Mq[i]);
             }
-            if (start < 0) continue;   // not the first sample of its run
-            // end: the first non-full word after ws
-            int64_t end = -1;
-            for (int64_t q0 = ws + 1;; q0 += 64) {
-                const uint32_t Mq = eq32<B>(P, q0 + lane, L, n);   // 0 past the text: ends the scan
-                const uint64_t nb = __ballot(Mq != FULL);
-                if (nb) {
-                    const int f = __ffsll((unsigned long long)nb) - 1;
-                    const uint32_t Mf = (uint32_t)__builtin_amdgcn_readlane((int)Mq, f);
-                    end = (q0 + f) * 32 + (int64_t)__ffs(~Mf) - 1;
-                    break;
-                }
+        }
+        uint64_t own = __ballot(start >= 0);   // uniform
+        while (own) {
+            const int src = __ffsll((unsigned long long)own) - 1;
+            own &= own - 1;
+            const int64_t ws = (int64_t)__builtin_amdgcn_readlane((int)(w / s), src) * s;   // the owner's word
+            const int64_t st = ((int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)start, src)) |
+                               ((int64_t)__builtin_amdgcn_readlane((int)(start >> 32), src) << 32);
+            // end: the first non-full word after ws -- one 64-word step here, a
+            // longer streak is ended by k_streak_end
+            const int64_t q0 = ws + 1;
+            const uint32_t Mq = eq32<B>(P, q0 + lane, L, n);   // 0 past the text: ends the scan
+            const uint64_t nb = __ballot(Mq != FULL);
+            if (!nb) {
+                if (lane == 0) push_pending(out, L, st, q0 + 64);
+                continue;
             }
-            if (end - start >= K && lane == 0) {
+            const int f = __ffsll((unsigned long long)nb) - 1;
+            const uint32_t Mf = (uint32_t)__builtin_amdgcn_readlane((int)Mq, f);
+            const int64_t end = (q0 + f) * 32 + (int64_t)__ffs(~Mf) - 1;
+            if (end - st >= K && lane == 0) {
                 const unsigned long long at = atomicAdd(out.count + seg, 1ull);
-                put(out, seg, at, L, start, end);
+                put(out, seg, at, L, st, end);
             }
+        }
+    }
+}
+
+// End search of the deferred streaks, one wave per streak (grid-stride over
+// the list; every wave leaves when the list is exhausted): 8 x 64 words per
+// step, their loads issued before any ballot.  A candidate is put when the
+// run is long enough (e - s >= K), exactly as the kernel that found it would.
+constexpr int kWide = 8;
+template <int B>
+__global__ __launch_bounds__(256) void k_streak_end(const uint32_t *__restrict__ P, int64_t n, int64_t mc,
+                                                    CandOut out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int64_t np = min((int64_t)*out.npend, out.pend_cap);
+    for (int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; e < np; e += nw) {   // uniform
+        const int64_t L = out.pend[3 * e], st = out.pend[3 * e + 1];
+        int64_t end = -1;
+        for (int64_t q0 = out.pend[3 * e + 2]; end < 0; q0 += 64 * kWide) {
+            uint32_t Mq[kWide];
+#pragma unroll
+            for (int i = 0; i < kWide; ++i) Mq[i] = eq32<B>(P, q0 + 64 * i + lane, L, n);   // 0 past the text
+#pragma unroll
+            for (int i = 0; i < kWide; ++i) {
+                const uint64_t nb = __ballot(Mq[i] != FULL);
+                if (end < 0 && nb) {
+                    const int f = __ffsll((unsigned long long)nb) - 1;
+                    const uint32_t Mf = (uint32_t)__builtin_amdgcn_readlane((int)Mq[i], f);
+                    end = (q0 + 64 * i + f) * 32 + (int64_t)__ffs(~Mf) - 1;
+                }
+            }
+        }
+        if (end - st >= (mc - 1) * L && lane == 0) {
+            const int seg = (int)(e & (kCandSegs - 1));
+            const unsigned long long at = atomicAdd(out.count + seg, 1ull);
+            put(out, seg, at, L, st, end);
         }
     }
 }
@@ -733,6 +789,7 @@ void launch_runs(Ctx &c, const uint32_t *P, int64_t n, int32_t lmin, int32_t lma
         KLAUNCH("k_runs_sparse", 0.0, (k_runs_sparse<B>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, c.stream,
                 P, n, nwords32, lmin, lmax, mc, sg, out);
     }
+    KLAUNCH("k_streak_end", 0.0, (k_streak_end<B>), dim3(512), dim3(256), 0, c.stream, P, n, mc, out);
 }
 
 }  // namespace
@@ -895,11 +952,17 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     c.slot[S_MISC3].ensure(kCandSegs * (sizeof(unsigned long long) + sizeof(int64_t)) + 64);
     unsigned long long *d_count = c.slot[S_MISC3].as<unsigned long long>();
     int64_t *d_off = reinterpret_cast<int64_t *>(d_count + kCandSegs);
+    // deferred streak ends: the counter sits after the segment counts (both reset per attempt)
+    unsigned long long *d_npend = reinterpret_cast<unsigned long long *>(d_count + kCandSegs + kCandSegs + 2);
+    int64_t pend_cap = 1 << 16;
     for (int attempt = 0;; ++attempt) {
         c.slot[S_CAND_K2].ensure((size_t)(seg_cap * kCandSegs) * sizeof(uint64_t));
         c.slot[S_CAND_V2].ensure((size_t)(seg_cap * kCandSegs) * sizeof(uint64_t));
+        c.slot[S_MISC2].ensure((size_t)pend_cap * 3 * sizeof(int64_t));
         HIPCHECK(hipMemsetAsync(d_count, 0, kCandSegs * sizeof(unsigned long long), st));
-        CandOut co{c.slot[S_CAND_K2].as<uint64_t>(), c.slot[S_CAND_V2].as<uint64_t>(), d_count, seg_cap, lmax, sb};
+        HIPCHECK(hipMemsetAsync(d_npend, 0, sizeof(unsigned long long), st));
+        CandOut co{c.slot[S_CAND_K2].as<uint64_t>(), c.slot[S_CAND_V2].as<uint64_t>(), d_count, seg_cap, lmax, sb,
+                   c.slot[S_MISC2].as<int64_t>(), d_npend, pend_cap};
         hipEvent_t ka = nullptr, kb = nullptr;
         if (c.timing) {
             HIPCHECK(hipEventCreate(&ka));
@@ -913,6 +976,8 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
         HIPCHECK(hipGetLastError());
         if (c.timing) HIPCHECK(hipEventRecord(kb, st));
         HIPCHECK(hipMemcpyAsync(segn, d_count, sizeof segn, hipMemcpyDeviceToHost, st));
+        unsigned long long npend = 0;
+        HIPCHECK(hipMemcpyAsync(&npend, d_npend, sizeof npend, hipMemcpyDeviceToHost, st));
         scan_wait(st);
         if (c.timing) {
             float ms = 0;
@@ -930,9 +995,12 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
             ncand += segn[q];
             mx = std::max(mx, segn[q]);
         }
-        if ((int64_t)mx <= seg_cap) break;
+        if ((int64_t)mx <= seg_cap && (int64_t)npend <= pend_cap) break;
         if (attempt >= 2) fail(BWTMI_E_STATE, "strict scan: candidate segments overflow after %d attempts", attempt + 1);
-        seg_cap = (int64_t)mx + (int64_t)mx / 4 + 1024;   // exact counts: the next attempt fits
+        if ((int64_t)mx > seg_cap) seg_cap = (int64_t)mx + (int64_t)mx / 4 + 1024;   // exact counts: the next attempt fits
+        // (lost streaks were not counted as candidates: the next attempt may find more)
+        if ((int64_t)npend > pend_cap) pend_cap = (int64_t)npend + (int64_t)npend / 4 + 1024;
+        else if ((int64_t)npend > pend_cap / 2) pend_cap *= 2;
     }
     if (ncand > 0) {
         int64_t off[kCandSegs];

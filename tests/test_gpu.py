@@ -306,7 +306,10 @@ def _large_goldens():
 def test_full_size_goldens(gpu_ctx, golden_dir, tmp_path, name):
     """BASELINE configs at full size -- C2 (1 Mbp --tier1), C3 (100 Mbp
     --progress), C4 (8 x 12.5 Mbp), C5 (100 Mbp with 0.02 substitutions inside
-    the planted arrays, --progress, default and --no-mismatches arms) -- run
+    the planted arrays, --progress, default and --no-mismatches arms), and the
+    general alphabet: G12N (12.5 Mbp with assembly gaps: 3.6 % N in runs up to
+    289 kbp, ~1200 single R/Y) and C3Np (C3N, 100 Mbp, 3.8 % N in runs up to
+    958 kbp, --progress) -- run
     through the drop-in CLI (`bwt.py IN.fa -o OUT --jobs -1 ARGS`, bwt.py:4201-4370)
     against repeat.tab hashes of the reference pipeline
     (tests/golden/make_goldens.py hybrid; strict scan and nested suppression
@@ -314,7 +317,8 @@ def test_full_size_goldens(gpu_ctx, golden_dir, tmp_path, name):
     from bwtmi import cli, synth
     g = _large_goldens()[name]
     fa = str(tmp_path / f"{name}.fa")
-    assert synth.write_fasta(fa, g["lengths"], g["sub_rate"]) == g["fasta_sha256"], name
+    assert synth.write_fasta(fa, g["lengths"], g["sub_rate"], g.get("first_index", 1),
+                             g.get("gaps")) == g["fasta_sha256"], name
     out = tmp_path / f"{name}.tab"
     assert cli.main([fa, "-o", str(out), "--jobs", "-1"] + list(g["args"])) == 0
     data = out.read_bytes()

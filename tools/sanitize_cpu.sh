@@ -20,6 +20,6 @@ else
   make -s -j8 -C bwt-algorithm_amd tsan || exit 1
   RT=$(/opt/rocm/llvm/bin/clang++ -print-file-name=libclang_rt.tsan-x86_64.so)
   export BWTMI_LIB=$PWD/bwt-algorithm_amd/build-tsan/libbwtmi_tsan.so
-  export TSAN_OPTIONS=halt_on_error=1:abort_on_error=1:report_signal_unsafe=0:second_deadlock_stack=1:${TSAN_EXTRA:-}
+  export TSAN_OPTIONS=halt_on_error=1:abort_on_error=1:report_signal_unsafe=0:second_deadlock_stack=1:suppressions=$PWD/tools/tsan.supp:${TSAN_EXTRA:-}
 fi
 LD_PRELOAD=$RT${LD_PRELOAD:+:$LD_PRELOAD} timeout -k 10 ${SAN_TIMEOUT:-2400} python -m pytest tests -m "not gpu" -x -q -p no:cacheprovider "$@"
