@@ -321,6 +321,12 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
 bool sa_dna_eligible(uint8_t last, int64_t n, const int64_t *totals);
 // also writes the sampled SA (bwt.py:328-333): sampled[j] = SA[j * sample] for j < ceil(n / sample)
 bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, int32_t *sampled, int32_t sample);
+// texts whose non-'$' symbols are at most 7 bytes above '$' (ACGT with N runs,
+// IUPAC codes): the symbol count (lut: byte -> code 0..6, sym: code -> byte,
+// sym[7] = '$'), else 0
+int sa_small_alphabet(uint8_t last, int64_t n, const int64_t *totals, uint8_t *lut, uint8_t *sym);
+bool sa_small_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, int32_t *sampled, int32_t sample,
+                     const uint8_t *lut, const uint8_t *sym);
 
 // ----- index (index.hip)
 // true when [p, p+n) lies in a host block of mem.h that is (now) registered

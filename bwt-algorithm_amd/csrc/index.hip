@@ -640,7 +640,14 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     const bool dna = sa_dna_eligible(last, n, ix->totals) &&
                      sa_dna_device(c, T, n, ix->sa.as<uint32_t>(), ix->bwt.as<uint8_t>(), ix->sampled.as<int32_t>(),
                                    sa_sample);
-    if (!dna) sa_doubling(c, ix, T, n, sigma, code);
+    // ACGT with assembly gaps (N runs, a few IUPAC codes): the same string sort
+    // over 3-bit symbol codes (BWTMI_SA_SMALL=0: the general doubling instead)
+    static const bool small_ok = [] { const char *e = std::getenv("BWTMI_SA_SMALL"); return !(e && *e == '0'); }();
+    uint8_t slut[256], ssym[8];
+    const bool small = !dna && small_ok && sa_small_alphabet(last, n, ix->totals, slut, ssym) > 0 &&
+                       sa_small_device(c, T, n, ix->sa.as<uint32_t>(), ix->bwt.as<uint8_t>(),
+                                       ix->sampled.as<int32_t>(), sa_sample, slut, ssym);
+    if (!dna && !small) sa_doubling(c, ix, T, n, sigma, code);
     // scratch of the Occ / k-mer / packed-rank stages
     c.slot[S_IDX0].ensure((size_t)n * 8);
     c.slot[S_IDX3].ensure((size_t)std::max<int64_t>(n + 1, 4 * (n / 64 + 2)) * 4);
@@ -683,7 +690,7 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
         uint32_t *row = ix->occ.as<uint32_t>() + (int64_t)cc * (nblk + 1);
         exclusive_scan<uint32_t>(c, row, row, nblk + 1);
     }
-    if (!dna)   // the DNA sort wrote the samples in its final pass
+    if (!dna && !small)   // the string sort wrote the samples in its final pass
         KLAUNCH("k_sample", 0.0, k_sample, dim3(blocks(ix->sampled_len)), dim3(256), 0, st, SA, n, sa_sample,
                 ix->sampled.as<int32_t>(), ix->sampled_len);
 

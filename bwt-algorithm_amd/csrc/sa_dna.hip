@@ -1,8 +1,11 @@
 // sa_dna.hip -- suffix array + BWT of an ACGT text with its single final '$'
 // (BWTCore._build_suffix_array / _build_bwt_array, bwt.py:212-274), the text
-// every CLI contig produces (seq + '$', bwt.py:3053 / 3782).  Any other text
-// (N, IUPAC, lower case, an inner '$') takes index.hip's general prefix
-// doubling.
+// every CLI contig produces (seq + '$', bwt.py:3053 / 3782) -- and of a text
+// over up to 7 other symbols that all sort above '$' (ACGT with assembly gaps:
+// N runs, IUPAC codes), whose first sort key is 16 symbols of 3 bits (48-bit
+// keys, 6 passes) instead of 16 bases of 2 bits; everything after the first
+// sort is the same.  Any other text (an inner '$', more symbols, a byte below
+// '$') takes index.hip's general prefix doubling.
 //
 // The reference orders suffixes by byte value with the unique '$' smallest;
 // 2-bit codes A0 C1 G2 T3 keep that order among bases.  Instead of doubling
@@ -103,6 +106,52 @@ __global__ __launch_bounds__(kB) void k_dna_keys(const uint64_t *__restrict__ P,
     vals[i] = (uint32_t)i | (prev << 29);
 }
 
+// ---- small alphabets (<= 7 symbols above '$'): symbol codes 0..6 by byte
+// order, 4-bit nibbles in the packed words (16 per word, first in the top
+// nibble), '$' and past the end read as code 0 (the end fix-up below serves
+// both paths); the 48-bit key holds 16 codes of 3 bits
+__global__ __launch_bounds__(kB) void k_sym_pack(const uint8_t *__restrict__ t, int64_t n,
+                                                 const uint8_t *__restrict__ lut, uint64_t *__restrict__ P, int64_t nw) {
+    __shared__ uint8_t cm[256];
+    cm[threadIdx.x] = lut[threadIdx.x];
+    __syncthreads();
+    const int64_t w = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (w >= nw) return;
+    const int64_t base = w * 16;
+    uint64_t v = 0;
+    if (base + 16 <= n - 1) {
+        const uint4 a = *reinterpret_cast<const uint4 *>(t + base);
+        const uint32_t ws[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v = (v << 4) | cm[(ws[q] >> (8 * k)) & 255u];
+    } else {
+        for (int k = 0; k < 16; ++k) {
+            const int64_t i = base + k;
+            v = (v << 4) | (i < n - 1 ? cm[t[i]] : 0u);
+        }
+    }
+    P[w] = v;
+}
+
+// key = the 16 symbols from i (3 bits each, first in the top bits of 48);
+// value = i | code of the symbol before i << 29 ('$' = 7 for i == 0)
+__global__ __launch_bounds__(kB) void k_sym_keys(const uint64_t *__restrict__ P, int64_t n, uint64_t *__restrict__ keys,
+                                                 uint32_t *__restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (i >= n) return;
+    const int64_t w = i >> 4;
+    const int sh = (int)(i & 15) * 4;
+    const uint64_t x = sh ? (P[w] << sh) | (P[w + 1] >> (64 - sh)) : P[w];
+    uint64_t k = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) k = (k << 3) | ((x >> (60 - 4 * j)) & 7u);
+    keys[i] = k;
+    const uint32_t prev = i == 0 ? 7u : (uint32_t)((P[(i - 1) >> 4] >> (60 - 4 * ((i - 1) & 15))) & 15u);
+    vals[i] = (uint32_t)i | (prev << 29);
+}
+
 // flags of the multi-member groups (runs of equal keys): S = first member, E = last member
 __global__ __launch_bounds__(kB) void k_dna_compact2(const uint32_t *__restrict__ fs, const uint32_t *__restrict__ ps,
                                                      const uint32_t *__restrict__ fe, const uint32_t *__restrict__ pe,
@@ -127,10 +176,11 @@ struct RunFlags {
 };
 // one coalesced load per key: the neighbours come from the adjacent lanes
 // (lanes 0 and 63 load theirs); every lane of the wave must call it
-__device__ __forceinline__ RunFlags run_flags(const uint32_t *__restrict__ keys, int64_t r, int64_t n) {
+template <class K>
+__device__ __forceinline__ RunFlags run_flags(const K *__restrict__ keys, int64_t r, int64_t n) {
     const int lane = threadIdx.x & 63;
-    const uint32_t k = r < n ? keys[r] : 0u;
-    uint32_t kp = __shfl_up(k, 1, 64), kn = __shfl_down(k, 1, 64);
+    const K k = r < n ? keys[r] : K(0);
+    K kp = __shfl_up(k, 1, 64), kn = __shfl_down(k, 1, 64);
     if (lane == 0 && r > 0 && r < n) kp = keys[r - 1];
     if (lane == 63 && r + 1 < n) kn = keys[r + 1];
     RunFlags f{false, false, false};
@@ -143,7 +193,8 @@ __device__ __forceinline__ RunFlags run_flags(const uint32_t *__restrict__ keys,
     return f;
 }
 
-__global__ __launch_bounds__(kB) void k_grp_count(const uint32_t *__restrict__ keys, int64_t n,
+template <class K>
+__global__ __launch_bounds__(kB) void k_grp_count(const K *__restrict__ keys, int64_t n,
                                                   uint32_t *__restrict__ tcnt) {
     __shared__ uint32_t ws[kB / 64], we[kB / 64], wl[kB / 64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -228,7 +279,8 @@ __global__ __launch_bounds__(1024) void k_grp_scan(uint32_t *__restrict__ tcnt, 
     if (t == 0) tcnt[3 * nt] = carry[0];
 }
 
-__global__ __launch_bounds__(kB) void k_grp_apply(const uint32_t *__restrict__ keys, int64_t n,
+template <class K>
+__global__ __launch_bounds__(kB) void k_grp_apply(const K *__restrict__ keys, int64_t n,
                                                   const uint32_t *__restrict__ tcnt, uint32_t *__restrict__ gs,
                                                   uint32_t *__restrict__ ge, uint32_t *__restrict__ hd) {
     __shared__ uint32_t ws[kB / 64], we[kB / 64], wl[kB / 64];
@@ -765,16 +817,18 @@ __global__ __launch_bounds__(kB) void k_dna_refine_pos(const uint64_t *__restric
     ge[x] = starts[q] + (kl - offs[q]) + 1;
 }
 
+struct Sym8 {
+    uint8_t s[8];   // byte of each BWT code
+};
 __global__ __launch_bounds__(kB) void k_dna_final(const uint32_t *__restrict__ vals, int64_t n, uint32_t *__restrict__ sa,
                                                   uint8_t *__restrict__ bwt, int32_t *__restrict__ sampled,
-                                                  int32_t sample) {
+                                                  int32_t sample, Sym8 sym) {
     const int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x;
     if (r >= n) return;
     const uint32_t v = vals[r];
     sa[r] = v & kPosMask;
     if (r % sample == 0) sampled[r / sample] = (int32_t)(v & kPosMask);   // the SA row is already in hand
-    const uint32_t c = v >> 29;
-    bwt[r] = c == 4 ? (uint8_t)'$' : (uint8_t)"ACGT"[c];
+    bwt[r] = sym.s[v >> 29];
 }
 
 }  // namespace
@@ -784,20 +838,38 @@ bool sa_dna_eligible(const uint8_t last, int64_t n, const int64_t *totals) {
     return totals['A'] + totals['C'] + totals['G'] + totals['T'] + 1 == n;
 }
 
-// SA (uint32[n]) and BWT (uint8[n]) of t[0, n) = ACGT* '$'; false when the
-// refinement needed more than kMaxRounds passes (the caller then runs the
-// general prefix doubling)
-bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, int32_t *sampled, int32_t sample) {
+int sa_small_alphabet(const uint8_t last, int64_t n, const int64_t *totals, uint8_t *lut, uint8_t *sym) {
+    if (n < 2 || n > (int64_t)kPosMask || last != '$' || totals['$'] != 1) return 0;
+    int k = 0;
+    std::memset(lut, 0, 256);
+    for (int b = 0; b < 256; ++b) {
+        if (!totals[b] || b == '$') continue;
+        if (b < '$' || k == 7) return 0;   // '$' must sort first; codes 0..6 (7 is '$' in the values)
+        lut[b] = (uint8_t)k;
+        sym[k++] = (uint8_t)b;
+    }
+    sym[7] = '$';
+    return k;
+}
+
+namespace {
+// SA (uint32[n]) and BWT (uint8[n]) of t[0, n) = the text with its single
+// final '$': ACGT (lut == nullptr: 2-bit bases, 32-bit keys) or a small
+// alphabet (lut: symbol codes, 48-bit keys); false when a round outgrows its
+// lists (the caller then runs the general prefix doubling)
+bool sa_sort(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, int32_t *sampled, int32_t sample,
+             const uint8_t *lut, const uint8_t *symtab) {
     hipStream_t st = c.stream;
-    const int64_t nw = (n + 31) / 32 + 2;
-    c.slot[S_IDX0].ensure((size_t)n * 4 + 64);      // keys, then class lists
+    const bool small = lut != nullptr;
+    const int64_t nw = small ? (n + 15) / 16 + 2 : (n + 31) / 32 + 2;
+    c.slot[S_IDX0].ensure((size_t)n * (small ? 8 : 4) + 64);      // keys, then class lists
     c.slot[S_IDX1].ensure((size_t)n * 4 + 64);      // values
     c.slot[S_IDX2].ensure((size_t)nw * 8 + 64);     // packed text
     c.slot[S_IDX3].ensure((size_t)(n + 1) * 4);     // group-start flags
     c.slot[S_IDX4].ensure((size_t)(n + 1) * 4 + 256);   // their positions (first: the group tiles' counts)
     c.slot[S_IDX5].ensure((size_t)(n + 1) * 4);     // group-end flags
     c.slot[S_IDX6].ensure((size_t)(n + 1) * 4);     // their positions
-    c.slot[S_MISC3].ensure(256);   // 6 class counts | 8 + 1 group-list counters | 8 + 1 change counters
+    c.slot[S_MISC3].ensure(512);   // 6 class counts | 8 + 1 group-list counters | 8 + 1 change counters; symbol lut
     uint32_t *keys = c.slot[S_IDX0].as<uint32_t>();
     uint32_t *vals = c.slot[S_IDX1].as<uint32_t>();
     uint64_t *P = c.slot[S_IDX2].as<uint64_t>();
@@ -805,10 +877,23 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
     uint32_t *fe = c.slot[S_IDX5].as<uint32_t>(), *pe = c.slot[S_IDX6].as<uint32_t>();
     uint32_t *counts = c.slot[S_MISC3].as<uint32_t>();
 
-    KLAUNCH("dna_pack", (double)n + (double)n / 4.0, k_dna_pack, dim3(nblocks(nw)), dim3(kB), 0, st, t, n, P, nw);
-    KLAUNCH("dna_keys", (double)n / 4.0 + 8.0 * (double)n, k_dna_keys, dim3(nblocks(n)), dim3(kB), 0, st, P, n, keys,
-            vals);
-    radix_sort_pairs_k32(c, keys, vals, n, 0, 32);
+    uint64_t *keys64 = c.slot[S_IDX0].as<uint64_t>();
+    Sym8 sym{{'A', 'C', 'G', 'T', '$', 0, 0, 0}};
+    if (small) {
+        std::memcpy(sym.s, symtab, 8);
+        uint8_t *d_lut = reinterpret_cast<uint8_t *>(c.slot[S_MISC3].as<char>() + 256);
+        HIPCHECK(hipMemcpyAsync(d_lut, lut, 256, hipMemcpyHostToDevice, st));
+        KLAUNCH("sym_pack", (double)n + (double)n / 2.0, k_sym_pack, dim3(nblocks(nw)), dim3(kB), 0, st, t, n, d_lut, P,
+                nw);
+        KLAUNCH("sym_keys", (double)n / 2.0 + 12.0 * (double)n, k_sym_keys, dim3(nblocks(n)), dim3(kB), 0, st, P, n,
+                keys64, vals);
+        radix_sort_pairs32(c, keys64, vals, n, 0, 48);
+    } else {
+        KLAUNCH("dna_pack", (double)n + (double)n / 4.0, k_dna_pack, dim3(nblocks(nw)), dim3(kB), 0, st, t, n, P, nw);
+        KLAUNCH("dna_keys", (double)n / 4.0 + 8.0 * (double)n, k_dna_keys, dim3(nblocks(n)), dim3(kB), 0, st, P, n,
+                keys, vals);
+        radix_sort_pairs_k32(c, keys, vals, n, 0, 32);
+    }
 
     // groups of equal 16-base prefixes -> (start, end) lists
     auto groups = [&](const uint32_t *f_s, uint32_t *p_s, const uint32_t *f_e, uint32_t *p_e, int64_t m,
@@ -846,10 +931,19 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
     {
         const int64_t nt = (n + kGTile - 1) / kGTile;
         uint32_t *tcnt = ps;   // 3 nt + 1 words
-        KLAUNCH("dna_grp_count", 4.0 * (double)n, k_grp_count, dim3((unsigned)nt), dim3(kB), 0, st, keys, n, tcnt);
-        KLAUNCH("dna_grp_scan", 0.0, k_grp_scan, dim3(1), dim3(1024), 0, st, tcnt, nt);
-        KLAUNCH("dna_grp_apply", 8.0 * (double)n, k_grp_apply, dim3((unsigned)nt), dim3(kB), 0, st, keys, n, tcnt, gs,
-                ge, hd);
+        if (small) {
+            KLAUNCH("dna_grp_count", 8.0 * (double)n, k_grp_count<uint64_t>, dim3((unsigned)nt), dim3(kB), 0, st,
+                    keys64, n, tcnt);
+            KLAUNCH("dna_grp_scan", 0.0, k_grp_scan, dim3(1), dim3(1024), 0, st, tcnt, nt);
+            KLAUNCH("dna_grp_apply", 12.0 * (double)n, k_grp_apply<uint64_t>, dim3((unsigned)nt), dim3(kB), 0, st,
+                    keys64, n, tcnt, gs, ge, hd);
+        } else {
+            KLAUNCH("dna_grp_count", 4.0 * (double)n, k_grp_count<uint32_t>, dim3((unsigned)nt), dim3(kB), 0, st, keys,
+                    n, tcnt);
+            KLAUNCH("dna_grp_scan", 0.0, k_grp_scan, dim3(1), dim3(1024), 0, st, tcnt, nt);
+            KLAUNCH("dna_grp_apply", 8.0 * (double)n, k_grp_apply<uint32_t>, dim3((unsigned)nt), dim3(kB), 0, st, keys,
+                    n, tcnt, gs, ge, hd);
+        }
         uint32_t g32 = 0;
         HIPCHECK(hipMemcpyAsync(&g32, tcnt + 3 * nt, 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
@@ -1006,9 +1100,19 @@ bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *B
         sl = nsl;
     }
     KLAUNCH("dna_final", 9.0 * (double)n + 4.0 * (double)((n + sample - 1) / sample), k_dna_final, dim3(nblocks(n)),
-            dim3(kB), 0, st, vals, n, SA, BWT, sampled, sample);
+            dim3(kB), 0, st, vals, n, SA, BWT, sampled, sample, sym);
     HIPCHECK(hipGetLastError());
     return true;
+}
+}  // namespace
+
+bool sa_dna_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, int32_t *sampled, int32_t sample) {
+    return sa_sort(c, t, n, SA, BWT, sampled, sample, nullptr, nullptr);
+}
+
+bool sa_small_device(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, int32_t *sampled, int32_t sample,
+                     const uint8_t *lut, const uint8_t *sym) {
+    return sa_sort(c, t, n, SA, BWT, sampled, sample, lut, sym);
 }
 
 }  // namespace bwtmi

@@ -434,6 +434,48 @@ def test_dna_suffix_sort_vs_oracle(gpu_ctx, monkeypatch, case):
     _check_index(t + b"$")
 
 
+@pytest.mark.parametrize("case", ["gaps_300k", "n_only", "n_edges", "seven_symbols", "long_n_run", "groups_with_n",
+                                  "eight_symbols", "byte_below_dollar", "lower_case"])
+def test_small_alphabet_suffix_sort_vs_oracle(gpu_ctx, case):
+    """The string sort over 3-bit symbol codes (sa_dna.hip, up to 7 symbols
+    above '$': ACGT with N runs and IUPAC codes; raw byte order, N between G
+    and T, bwt.py:212-264) against the oracle: assembly gaps, an N-only text,
+    N runs tying with the end's zero-padded keys, all seven symbols, a 70 kbp
+    N run (one group losing h suffixes per doubling round), duplicated
+    N-bearing k-mers; and the texts it must leave to the general doubling
+    (eight symbols, a byte below '$') -- every one bit-exact."""
+    from bwtmi import synth
+    r = np.random.default_rng(sum(map(ord, case)))
+
+    def rnd(k, alpha=b"ACGT"):
+        a = np.frombuffer(alpha, dtype=np.uint8)
+        return a[r.integers(0, len(a), k)].tobytes()
+    if case == "gaps_300k":
+        t = synth.generate_contig(300_000, 14, gaps="n2")
+    elif case == "n_only":
+        t = b"N" * 5000
+    elif case == "n_edges":
+        t = rnd(500, b"ACGTN") + b"N" * 40 + rnd(30) + b"NA" + b"N" * 14
+    elif case == "seven_symbols":
+        t = b"".join(rnd(int(r.integers(3, 30)), b"ACGTNRY") + rnd(3, b"ACGTNRY") * int(r.integers(3, 20))
+                     for _ in range(2000))
+    elif case == "long_n_run":
+        t = rnd(3000) + b"N" * 70_000 + rnd(3000) + b"N" * 17 + rnd(40)
+    elif case == "groups_with_n":
+        parts = []
+        for _ in range(300):
+            w = rnd(int(r.integers(16, 40)), b"ACGTN")
+            parts += [w + rnd(int(r.integers(1, 30)), b"ACGTN") for _ in range(int(r.integers(2, 60)))]
+        t = b"".join(parts)
+    elif case == "eight_symbols":
+        t = _planted(20_000, 9, b"ACGTNRYK")
+    elif case == "byte_below_dollar":
+        t = _planted(20_000, 10, b"ACGT!")
+    else:
+        t = _planted(20_000, 11, b"acgtN")
+    _check_index(t + b"$")
+
+
 @pytest.mark.parametrize("rank", ["packed", "bytes"])
 def test_backward_search_all_short_motifs(gpu_ctx, monkeypatch, rank):
     """Both rank structures: the packed 2-bit blocks of ACGT texts (k_bsearch2)
