@@ -48,7 +48,7 @@ B_ALG_PER_BASE = 16.7          # compulsory HBM bytes per base
 PMC_SUMMARY = os.path.join(REPO, "profiles", "pmc_traffic.json")            # C3 / C5 kernels
 PMC_SUMMARY_OF = {"C3N": os.path.join(REPO, "profiles", "pmc_traffic_C3N.json")}   # other workloads
 # bench kernel-timer names -> kernel names in the rocprofv3 summaries
-KERNEL_OF = {"radix_scatter_kv8": "k_scatter<u32,u32>", "radix_partition_kv8": "k_scatter<u32,u32>",
+KERNEL_OF = {"radix_scatter_kv6": "k_scatter<u16,u32>", "radix_scatter_kv8": "k_scatter<u32,u32>", "radix_partition_kv8": "k_scatter<u32,u32>",
              "radix_scatter_kv12": "k_scatter<u64,u32>",
              "radix_scatter_kv16": "k_scatter<u64,u64>", "bwt_gather": "k_bwt", "occ_blocks": "k_occ_blocks",
              "sa_init_keys": "k_init_keys", "kmer_dna": "k_kmer_dna", "fm2_local": "k_fm2_local",
@@ -61,6 +61,18 @@ def rocprof_name(timer: str) -> str:
         return KERNEL_OF[timer]
     return "k_" + timer if timer.startswith("dna_") else timer
 FLANK = 30
+# The reference itself (bwt.py --jobs 0 --progress, pure Python + numpy, no
+# numba / pydivsufsort), timed in the build container -- it cannot run on the
+# GPU box (tools/time_reference.py, profiles/r02/reference_cpu.json).  A
+# one-contig file uses one core whatever the core count: Pool size
+# min(cores, #contigs), bwt.py:3863-3864.
+REFERENCE_CPU = dict(
+    kind="reference", cores=1, host="build container, 8 vCPU Intel(R) Xeon(R) Processor, Python 3.10.12, numpy 2.2.6",
+    cmd="bwt.py IN.fa -o OUT --jobs 0 --progress",
+    runs=[dict(bp=10_000, seconds=35.8), dict(bp=1_000_000, seconds=5491.6)],
+    value_1mbp=round(1.0 / 5491.6, 7), unit="Mbp/s",
+    extrapolated_100mbp=dict(days=16.6, value=7.0e-5,
+                             basis="5.5 us per strict-scan step x sum_L (n - 3L) + the O(k^2) nested loop"))
 METRIC = "Mbp/s indexed+scanned (Tier1+2) on 100 Mbp synthetic FASTA, 1/2/4/8 GPU"
 WORKLOADS = {
     "C3": dict(lengths=[100_000_000], sub_rate=0.0, shared=False, golden="C3p"),
@@ -113,7 +125,12 @@ def cpu_baseline(sample_bp: int, sub_rate: float, threads: int, gaps=None):
                        f"{dt:.1f} s",
                 phases_s=dict(index=round(t1 - t0, 2), strict_scan=round(t2 - t1, 2),
                               post_and_write=round(t3 - t2, 2)),
-                extrapolated_100mbp_s=round(dt * 100e6 / sample_bp, 1))
+                phase_threads=dict(index=1, strict_scan=threads, post_and_write=threads),
+                # the index phase is the oracle's single-threaded prefix doubling: the
+                # rate of the phases that use every thread, stated on its own
+                value_scan_and_post=round(sample_bp / 1e6 / (t3 - t1), 5),
+                extrapolated_100mbp_s=round(dt * 100e6 / sample_bp, 1),
+                reference_measured=REFERENCE_CPU)
 
 
 def fm_all_motifs(seq: bytes, reps: int = 5):
@@ -158,9 +175,34 @@ def cli_drop_in(fa: str, args, reps: int = 2):
     return dict(argv=["bwt.py", "FA", "-o", "OUT"] + list(args), wall_s=times, output_sha256=digest)
 
 
-def word_compares(n: int, U: int) -> int:
-    """k_runs' 32-position word compares of one contig: sum_L ceil((n - L) / 32)."""
-    return sum((n - L + 31) // 32 for L in range(1, min(U, n // 3) + 1))
+def word_compares(n: int, U: int, mc: int = 3, lmin: int = 1):
+    """32-position word compares of one contig's strict scan, split as
+    strict_scan.hip launch_runs splits the unit lengths (bwt.py:1920):
+      dense   k_runs, unit-length groups (32 L each) whose runs may hold no
+              full aligned word: every word, sum_L ceil((n - L) / 32);
+      sparse  k_runs_sparse, groups with K = (mc - 1) L >= 95: every s-th word
+              with s = (K - 31) // 32 at the group's shortest L;
+      dense_equivalent  every word for every L (what the sampling avoids).
+    The sampled kernel's owner tests and streak-end scans (data-dependent)
+    are not counted, so the rate from these counts is a lower bound."""
+    lmax = min(U, n // mc)
+    nw = (n + 31) // 32
+
+    def stride(g):
+        K = (mc - 1) * max(32 * g, lmin)
+        return (K - 31) // 32 if K >= 95 else 0
+    gs = max(1, lmin >> 5)
+    while gs <= (lmax >> 5) and stride(gs) < 2:
+        gs += 1
+    lmax_dense = min(lmax, gs * 32 - 1)
+    dense = sum((n - L + 31) // 32 for L in range(lmin, lmax_dense + 1))
+    sparse = 0
+    for g in range(gs, (lmax >> 5) + 1):
+        lo, hi = max(32 * g, lmin), min(32 * g + 31, lmax)
+        if hi >= lo:
+            sparse += (hi - lo + 1) * ((nw + stride(g) - 1) // stride(g))
+    every = sum((n - L + 31) // 32 for L in range(lmin, lmax + 1))
+    return dict(dense=dense, sparse=sparse, dense_equivalent=every)
 
 
 def launch_ranks(n: int, argv, script: str = None) -> int:
@@ -334,16 +376,32 @@ def main():
                         alg_bytes_per_launch=round(kbytes / launches), avg_launch_ms=round(kms / launches, 4),
                         launches_per_step=launches / a.steps,
                         share_of_device_time=round(kms / dev_ms, 4) if dev_ms else None)
-    # strict scan: word compares of k_runs against the VALU issue ceiling
+    # strict scan: the word compares k_runs (dense groups) and k_runs_sparse
+    # (sampled groups) perform, over the time of both plus k_streak_end, against
+    # the VALU issue ceiling; the all-words count only as a labelled reference
     mine = job.select_shard(load_world, load_rank) if shared else range(job.contig_count())
-    wc = sum(word_compares(job.contig_weight(i), max(120, min(job.contig_weight(i) // 3, 1000))) for i in mine)
-    kr = kstats.get("k_runs")
+    wc = dict(dense=0, sparse=0, dense_equivalent=0)
+    for i in mine:
+        w = job.contig_weight(i)
+        for k, v in word_compares(w, max(120, min(w // 3, 1000))).items():
+            wc[k] += v
+    scan_names = ("k_runs", "k_runs_sparse", "k_streak_end")
+    scan_ms = sum(kstats[k][0] for k in scan_names if k in kstats) / a.steps
     scan_rate = None
-    if kr and kr[0] > 0:
-        per_s = wc / (kr[0] / a.steps / 1e3)
-        scan_rate = dict(word_compares_per_step=wc, k_runs_ms_per_step=round(kr[0] / a.steps, 3),
-                         gcompares_per_s=round(per_s / 1e9, 1), valu_lane_ops_peak=VALU_LANE_OPS_PEAK,
-                         frac_of_valu_issue_at_1_op_per_compare=round(per_s / VALU_LANE_OPS_PEAK, 4))
+    if scan_ms > 0:
+        done = wc["dense"] + wc["sparse"]
+        per_s = done / (scan_ms / 1e3)
+        scan_rate = dict(word_compares_per_step=done, dense_compares=wc["dense"], sampled_compares=wc["sparse"],
+                         kernels=list(scan_names),
+                         kernels_ms_per_step=round(scan_ms, 3), gcompares_per_s=round(per_s / 1e9, 2),
+                         valu_lane_ops_peak=VALU_LANE_OPS_PEAK,
+                         frac_of_valu_issue_at_1_op_per_compare=round(per_s / VALU_LANE_OPS_PEAK, 5),
+                         note="owner tests and streak-end scans of the sampled groups (data-dependent) are not "
+                              "counted: a lower bound",
+                         dense_equivalent=dict(word_compares=wc["dense_equivalent"],
+                                               gcompares_per_s=round(wc["dense_equivalent"] / (scan_ms / 1e3) / 1e9, 2),
+                                               meaning="every word for every unit length: the work the sampling "
+                                                       "avoids, not work done"))
     e2e_gbs = B_ALG_PER_BASE * total_bp / (elapsed / a.steps) / 1e9
     cpu = None if a.no_cpu_baseline else cpu_baseline(a.cpu_sample_bp, wl["sub_rate"], host["threads_per_rank"],
                                                         wl.get("gaps"))

@@ -203,6 +203,10 @@ struct AlignSummary {
     double mismatch_rate = 0.0;
     std::string variations;  // ';'-joined
     bool any_variation = false;
+    // the walk ended because it reached its safety limit (bwt.py:1033), not at
+    // a copy that failed to align or a window too short: only then can a
+    // larger `end` change the result
+    bool at_limit = false;
 };
 // first position >= pos and < lim whose byte differs from b (lim if none):
 // the end of a homopolymer run, 32 bytes per step (assembly gaps hold N runs

@@ -268,6 +268,7 @@ void exclusive_scan(Ctx &c, const T *in, T *out, int64_t n);   // out may alias 
 void radix_sort_pairs(Ctx &c, uint64_t *keys, uint64_t *vals, int64_t n, int bit0, int bit1);
 void radix_sort_pairs32(Ctx &c, uint64_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1);
 void radix_sort_pairs_k32(Ctx &c, uint32_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1);
+void radix_sort_pairs_k16(Ctx &c, uint16_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1);
 // XCD-aware tile order: blocks b and b + 8 share an XCD (and its L2) under the
 // observed round-robin placement, so each group of blocks b % 8 takes one
 // contiguous range of tiles and neighbouring tiles run on one L2 at about the
@@ -314,8 +315,10 @@ void strict_scan_mm_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min
 void recompute_batch_device(Ctx &c, const RcReq *req, int64_t nreq, RcOut *out, std::vector<char> &arena);
 
 // ----- nested suppression / sort / dedup of one contig's strict hits (nested.hip)
+// d_maxlen: the hits' longest span, already on the device (the strict scan's
+// compaction reduces it); nullptr: reduced here
 void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
-                        ScreenedVec &out);
+                        ScreenedVec &out, const unsigned long long *d_maxlen = nullptr);
 
 // ----- suffix array + BWT of ACGT* '$' texts (sa_dna.hip)
 bool sa_dna_eligible(uint8_t last, int64_t n, const int64_t *totals);

@@ -296,7 +296,7 @@ __global__ void k_kentries(const uint8_t *__restrict__ t, int64_t n, int k, cons
 // position order (p = 0 .. n-9), so the entries need no compaction; codes
 // A0 C1 G2 T3 as kbits.  Four positions per thread from one 12-byte window.
 __global__ __launch_bounds__(256) void k_kmer_dna(const uint8_t *__restrict__ t, int64_t n,
-                                                  uint32_t *__restrict__ keys, uint32_t *__restrict__ pos) {
+                                                  uint16_t *__restrict__ keys, uint32_t *__restrict__ pos) {
     const int64_t p0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
     const int64_t m = n - 8;
     if (p0 >= m) return;
@@ -310,20 +310,26 @@ __global__ __launch_bounds__(256) void k_kmer_dna(const uint8_t *__restrict__ t,
 #pragma unroll
     for (int q = 0; q < 4; ++q)
         if (p0 + q < m) {
-            keys[p0 + q] = (w >> (2 * (3 - q))) & 0xffffu;
+            keys[p0 + q] = (uint16_t)(w >> (2 * (3 - q)));
             pos[p0 + q] = (uint32_t)(p0 + q);
         }
 }
 
-// CSR offsets from the sorted k-mer codes: boundary i (between keys[i-1] and
-// keys[i]) owns the codes (keys[i-1], keys[i]]; every code is written once
+// CSR offsets from the sorted k-mer codes: off[code] = the first entry whose
+// code is >= code (off[65536] = m), one binary search per code -- 65,537
+// searches of ~27 steps whose top levels every thread shares in the cache,
+// instead of a pass over all m sorted codes
 template <typename KT>
 __global__ void k_kbounds(const KT *__restrict__ keys, int64_t m, int64_t *__restrict__ off) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > m) return;
-    const int64_t prev = i == 0 ? -1 : (int64_t)keys[i - 1];
-    const int64_t cur = i == m ? 65536 : (int64_t)keys[i];
-    for (int64_t code = prev + 1; code <= cur; ++code) off[code] = i;
+    const int64_t code = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (code > 65536) return;
+    int64_t lo = 0, hi = m;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)keys[mid] < code) lo = mid + 1;
+        else hi = mid;
+    }
+    off[code] = lo;
 }
 
 // ---- LCP: chunked Kasai (exact while the only rank-0 suffix is the last one)
@@ -724,13 +730,13 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
         // 16-bit radix sort of (code, position)
         ix->has_kmer = true;
         const int64_t nent = n - K;
-        uint32_t *k32 = c.slot[S_IDX0].as<uint32_t>();
+        uint16_t *k16 = c.slot[S_IDX0].as<uint16_t>();   // 16-bit codes: 6 B per entry and pass
         ix->kmer_pos.ensure((size_t)nent * 4);
-        KLAUNCH("kmer_dna", 3.0 * (double)n + 8.0 * (double)nent, k_kmer_dna, dim3(blocks((nent + 3) / 4)), dim3(256),
-                0, st, T, n, k32, ix->kmer_pos.as<uint32_t>());
-        radix_sort_pairs_k32(c, k32, ix->kmer_pos.as<uint32_t>(), nent, 0, 16);
+        KLAUNCH("kmer_dna", (double)n + 6.0 * (double)nent, k_kmer_dna, dim3(blocks((nent + 3) / 4)), dim3(256),
+                0, st, T, n, k16, ix->kmer_pos.as<uint32_t>());
+        radix_sort_pairs_k16(c, k16, ix->kmer_pos.as<uint32_t>(), nent, 0, 16);
         ix->kmer_off.ensure((size_t)(65537) * 8);
-        KLAUNCH("k_kbounds", 0.0, k_kbounds<uint32_t>, dim3(blocks(nent + 1)), dim3(256), 0, st, k32, nent,
+        KLAUNCH("k_kbounds", 0.0, k_kbounds<uint16_t>, dim3(blocks(65537)), dim3(256), 0, st, k16, nent,
                 ix->kmer_off.as<int64_t>());
         ix->kmer_count = nent;
     } else if (!(flags & BWTMI_INDEX_NO_KMER) && n >= K) {
@@ -756,7 +762,7 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
             radix_sort_pairs32(c, keys, ix->kmer_pos.as<uint32_t>(), nent, 0, 16);
         }
         ix->kmer_off.ensure((size_t)(65537) * 8);
-        KLAUNCH("k_kbounds", 0.0, k_kbounds<uint64_t>, dim3(blocks(nent + 1)), dim3(256), 0, st, keys, nent,
+        KLAUNCH("k_kbounds", 0.0, k_kbounds<uint64_t>, dim3(blocks(65537)), dim3(256), 0, st, keys, nent,
                            ix->kmer_off.as<int64_t>());
         ix->kmer_count = nent;
     }

@@ -667,6 +667,7 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
         out.variations.clear();
         out.any_variation = false;
         out.consensus.assign(1, b);
+        out.at_limit = pos >= limit;
         out.motif_len = 1;
         out.copies = copies;
         out.consumed = copies;
@@ -762,6 +763,7 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
         }
         pos += res.consumed;
     }
+    out.at_limit = pos >= limit;
     if (copies < min_copies) return false;
     const int64_t consumed = pos - start;
     if (consumed <= 0) return false;

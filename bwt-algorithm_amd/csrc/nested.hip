@@ -454,7 +454,7 @@ static void screen_levels(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int32_t lm
 }
 
 void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
-                        ScreenedVec &out) {
+                        ScreenedVec &out, const unsigned long long *d_maxlen) {
     out.clear();
     if (n <= 0) return;
     if (n >= (int64_t)UINT32_MAX) fail(BWTMI_E_ARG, "too many strict hits for one contig (%lld)", (long long)n);
@@ -489,10 +489,15 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     unsigned long long *d_max = c.slot[S_COUNTS].as<unsigned long long>();
 
     // longest span -> key widths
-    HIPCHECK(hipMemsetAsync(d_max, 0, 8, st));
-    KLAUNCH("k_maxlen", 0.0, k_maxlen, dim3((unsigned)std::min<int64_t>(1024, blocks(n))), dim3(kB), 0, st, d_hits, n, d_max);
     unsigned long long maxlen = 0;
-    HIPCHECK(hipMemcpyAsync(&maxlen, d_max, 8, hipMemcpyDeviceToHost, st));
+    if (d_maxlen) {
+        HIPCHECK(hipMemcpyAsync(&maxlen, d_maxlen, 8, hipMemcpyDeviceToHost, st));
+    } else {
+        HIPCHECK(hipMemsetAsync(d_max, 0, 8, st));
+        KLAUNCH("k_maxlen", 0.0, k_maxlen, dim3((unsigned)std::min<int64_t>(1024, blocks(n))), dim3(kB), 0, st, d_hits,
+                n, d_max);
+        HIPCHECK(hipMemcpyAsync(&maxlen, d_max, 8, hipMemcpyDeviceToHost, st));
+    }
     scan_wait(st);
     const int mb = std::max(1, bits_for((uint64_t)lmax));
     const int lb = std::max(1, bits_for(maxlen));

@@ -408,6 +408,15 @@ struct Pools {
         const char *hseq = nullptr;
         int64_t hlo = 0, hhi = 0;
         char hb = 0;
+        // the worker's last host recompute whose walk stopped at a copy that
+        // failed (not at its safety limit): from the same start with the same
+        // motif length, any call whose limit lies past that stop walks the same
+        // windows -- a merge chain re-asks this for every record it absorbs
+        bool wk_ok = false;
+        const char *wk_seq = nullptr;
+        int64_t wk_start = 0, wk_m = 0, wk_stop = 0;
+        int wk_phase = 0;   // 1: the min_copies walk succeeded; 2: the min_copies = 1 retry
+        Item wk_item{};
     };
     static constexpr size_t XB = 16384, CB = size_t(2) << 20;   // Extras are trivially destructible
     std::vector<Arena> a;
@@ -435,6 +444,17 @@ struct Pools {
         ::new ((void *)x) Extra(e);
         x->motif = motif;
         x->variations = {};
+        return x;
+    }
+    // a copy of e sharing its strings (the arena keeps them)
+    Extra *clone(int w, const Extra &e) {
+        Arena &A = a[(size_t)w];
+        if (A.xb.empty() || A.xn == XB) {
+            A.xb.emplace_back(XB * sizeof(Extra));
+            A.xn = 0;
+        }
+        Extra *x = (Extra *)A.xb.back().p + A.xn++;
+        ::new ((void *)x) Extra(e);
         return x;
     }
     Extra *add(int w, const Extra &e, std::string_view motif, std::string_view variations) {
@@ -633,7 +653,7 @@ inline char comp_of(char c) {   // bwt.py:688-691
     }
 }
 
-std::atomic<int64_t> g_recomputes{0}, g_recompute_ns{0}, g_merges{0}, g_canons{0}, g_tests{0}, g_same{0};
+std::atomic<int64_t> g_recomputes{0}, g_recompute_ns{0}, g_merges{0}, g_canons{0}, g_tests{0}, g_same{0}, g_walk_reuse{0};
 // BWTMI_STATS=1: stage timers; =2: also per-recompute / per-test counters (slow)
 const bool g_stats = [] { const char *e = std::getenv("BWTMI_STATS"); return e && (*e == '1' || *e == '2'); }();
 const bool g_counters = [] { const char *e = std::getenv("BWTMI_STATS"); return e && *e == '2'; }();
@@ -733,17 +753,40 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
         b = std::min(b, L);
         return b > a ? std::string(seq + a, (size_t)(b - a)) : std::string();
     };
+    Pools::Arena &A = pools.a[(size_t)w];
+    const int64_t mc = std::max<int64_t>(1, u.min_copies);
+    // the walk's safety limit for a min_copies (motif.cpp align_repeat_region, bwt.py:1033)
+    const int64_t mi = std::max<int64_t>(1, std::min<int64_t>(10, m >= 4 ? m / 2 : 1));
+    auto walk_limit = [&](int64_t mcx) {
+        const int64_t e2 = std::min(L, end > start ? end : L);
+        return std::min(L, std::max(e2, start + m * mcx) + std::max(m * 3, mi * 4));
+    };
+    if (A.wk_ok && A.wk_seq == seq && A.wk_start == start && A.wk_m == m &&
+        A.wk_stop < walk_limit(A.wk_phase == 1 ? mc : 1)) {
+        // the same windows up to the same failing copy: the same record, but
+        // for what depends on the call itself (the requested end, the tier)
+        if (g_counters) g_walk_reuse.fetch_add(1, std::memory_order_relaxed);
+        Extra *x = pools.clone(w, *A.wk_item.x);
+        x->req_end = req_end;
+        x->tier = tier;
+        Item it = A.wk_item;
+        it.x = x;
+        return it;
+    }
     std::string tmpl = slice(start, start + m);
     if (tmpl.empty()) {
         const int64_t a = std::max<int64_t>(0, start - m);
         tmpl = slice(a, a + m);
     }
     if (tmpl.empty()) tmpl.assign((size_t)m, 'N');
-    Pools::Arena &A = pools.a[(size_t)w];
     AlignSummary &s = A.sum;
     s.want_copies = false;
-    bool ok = align_repeat_region(seq, L, start, end, tmpl, std::max<int64_t>(1, u.min_copies), s, 0.1, -1, A.as.get());
-    if (!ok) ok = align_repeat_region(seq, L, start, end, tmpl, 1, s, 0.1, -1, A.as.get());
+    int phase = 1;
+    bool ok = align_repeat_region(seq, L, start, end, tmpl, mc, s, 0.1, -1, A.as.get());
+    if (!ok) {
+        phase = 2;
+        ok = align_repeat_region(seq, L, start, end, tmpl, 1, s, 0.1, -1, A.as.get());
+    }
     RcView v;
     v.ok = ok;
     if (ok) {
@@ -757,7 +800,17 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
         v.consensus = s.consensus;
         if (s.any_variation) v.var = s.variations;
     }
-    return item_of_alignment(u, pools, w, chrom, start, end, m, tier, tmpl, v);
+    Item it = item_of_alignment(u, pools, w, chrom, start, end, m, tier, tmpl, v);
+    A.wk_ok = ok && !s.at_limit;
+    if (A.wk_ok) {
+        A.wk_seq = seq;
+        A.wk_start = start;
+        A.wk_m = m;
+        A.wk_stop = start + s.consumed;
+        A.wk_phase = phase;
+        A.wk_item = it;
+    }
+    return it;
 }
 
 // the record _recompute_repeat builds from an alignment (bwt.py:3536-3614)
@@ -1660,9 +1713,10 @@ void postprocess(Job &job) {
         for (int32_t k = 0; k < job.nunits; ++k) job.stage_ms[2 + s] += ms[(size_t)k * 4 + s];
     }
     if (g_counters)
-        std::fprintf(stderr, "[bwtmi] recomputes=%lld (%.1f ms thread-summed) merges=%lld canons=%lld final=%zu\n",
-                     (long long)g_recomputes.exchange(0), g_recompute_ns.exchange(0) / 1e6,
-                     (long long)g_merges.exchange(0), (long long)g_canons.exchange(0), job.final_recs.size());
+        std::fprintf(stderr, "[bwtmi] recomputes=%lld (%.1f ms thread-summed; %lld reused walks) merges=%lld canons=%lld "
+                     "final=%zu\n", (long long)g_recomputes.exchange(0), g_recompute_ns.exchange(0) / 1e6,
+                     (long long)g_walk_reuse.exchange(0), (long long)g_merges.exchange(0),
+                     (long long)g_canons.exchange(0), job.final_recs.size());
     if (g_counters)
         std::fprintf(stderr, "[bwtmi] merge tests past the gap test=%lld, same canonical=%lld\n",
                      (long long)g_tests.exchange(0), (long long)g_same.exchange(0));

@@ -410,7 +410,8 @@ void radix_sort_cfg(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
         launch_hist<kT / kBlock, KT>(c, ka, cnt, n, sh, ntiles);
         exclusive_scan<uint32_t>(c, cnt, cnt, ntiles * 256);
         // read (key, value) once, write it once
-        KLAUNCH(sizeof(KT) == 4 ? "radix_scatter_kv8" : sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16",
+        KLAUNCH(sizeof(KT) == 2 ? "radix_scatter_kv6" : sizeof(KT) == 4 ? "radix_scatter_kv8"
+                : sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16",
                 (double)n * 2.0 * ((double)sizeof(KT) + (vals ? (double)sizeof(V) : 0.0)),
                 (k_scatter<KT, V, BLOCK, ITEMS, NT, SPLIT>), dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, ka, va,
                 kb, vb, cnt, n, sh, ntiles, swz);
@@ -498,6 +499,13 @@ void radix_pass_k32(Ctx &c, const uint32_t *kin, const uint32_t *vin, uint32_t *
     KLAUNCH("radix_partition_kv8", (double)n * 16.0, (k_scatter<uint32_t, uint32_t, BLOCK, ITEMS, false, true>),
             dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, kin, vin, kout, vout, cnt, n, shift, ntiles, 1);
     HIPCHECK(hipGetLastError());
+}
+
+// 16-bit keys (the 8-mer codes), 32-bit values: keys and values staged apart
+// (a value does not fit a key's LDS slot), positions kept in registers
+void radix_sort_pairs_k16(Ctx &c, uint16_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1) {
+    if (n <= 1) return;
+    radix_sort_cfg<uint16_t, uint32_t, 512, 16, false, false>(c, keys, vals, n, bit0, bit1);
 }
 
 void radix_sort_pairs_k32(Ctx &c, uint32_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1) {

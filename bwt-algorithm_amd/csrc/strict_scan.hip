@@ -488,13 +488,28 @@ constexpr int32_t kThreadPeriodL = 32;
 
 // compaction of the resolved hits, with the smallest period of each hit's
 // first unit and the count after primitive reduction (bwt.py:1956-1961)
+// Also the hits' longest span (the screen's key width): a workgroup maximum,
+// and an atomic only when it beats the value already stored (one address for
+// the whole grid: unconditional atomics serialise; maxlen zero before the launch)
 __global__ __launch_bounds__(256) void k_compact(const uint64_t *__restrict__ keys, int64_t nc, int32_t umax, int sb,
                                                  const int64_t *__restrict__ hit_i, const int64_t *__restrict__ hit_c,
                                                  const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
-                                                 const uint8_t *__restrict__ t, bwtmi_hit *__restrict__ hits) {
+                                                 const uint8_t *__restrict__ t, bwtmi_hit *__restrict__ hits,
+                                                 unsigned long long *__restrict__ maxlen) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= nc || !flag[k]) return;
-    const int64_t L = (int64_t)umax - (int64_t)(keys[k] >> sb);
+    const bool live = k < nc && flag[k];
+    const int64_t L = live ? (int64_t)umax - (int64_t)(keys[k] >> sb) : 0;
+    unsigned long long span = live ? (unsigned long long)(hit_c[k] * L) : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) span = max(span, (unsigned long long)__shfl_xor(span, o, 64));
+    __shared__ unsigned long long wmax[4];
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = span;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        if (m > __hip_atomic_load(maxlen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(maxlen, m);
+    }
+    if (!live) return;
     bwtmi_hit h;
     h.start = hit_i[k];
     h.end = hit_i[k] + hit_c[k] * L;
@@ -1049,9 +1064,11 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     scan_wait(st);
     const int64_t nh = (int64_t)last_pos + last_flag;
     c.slot[S_HITS].ensure((size_t)std::max<int64_t>(nh, 1) * sizeof(bwtmi_hit));
+    unsigned long long *d_maxlen = d_npend + 1;   // the hits' longest span, reduced by k_compact
+    HIPCHECK(hipMemsetAsync(d_maxlen, 0, 8, st));
     KLAUNCH("k_compact", 0.0, k_compact, dim3(g), dim3(256), 0, st, c.slot[S_CAND_K].as<uint64_t>(), nc, lmax, sb,
                        c.slot[S_MISC0].as<int64_t>(), c.slot[S_MISC1].as<int64_t>(), c.slot[S_FLAG].as<uint32_t>(),
-                       c.slot[S_SCAN].as<uint32_t>(), d_text, c.slot[S_HITS].as<bwtmi_hit>());
+                       c.slot[S_SCAN].as<uint32_t>(), d_text, c.slot[S_HITS].as<bwtmi_hit>(), d_maxlen);
     if (nlong > 0)
         KLAUNCH("k_period_wave", 0.0, k_period_wave, dim3((unsigned)((nlong * 64 + 255) / 256)), dim3(256), 0, st,
                 c.slot[S_CAND_K].as<uint64_t>(), nlong, lmax, sb, c.slot[S_MISC0].as<int64_t>(),
@@ -1060,7 +1077,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     HIPCHECK(hipGetLastError());
     res.raw = nh;
     if (screen) {
-        screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.shits);
+        screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.shits, d_maxlen);
         if (c.timing) HIPCHECK(hipEventRecord(c.ev1, st));
     } else {
         if (c.timing) HIPCHECK(hipEventRecord(c.ev1, st));
