@@ -338,18 +338,48 @@ __global__ void k_isa(const uint32_t *__restrict__ sa, int64_t n, uint32_t *__re
     if (r < n) isa[sa[r]] = (uint32_t)r;
 }
 
-__global__ void k_kasai(const uint8_t *__restrict__ t, const uint32_t *__restrict__ sa, const uint32_t *__restrict__ isa,
-                        int64_t n, int64_t chunk, int32_t *__restrict__ lcp) {
-    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t i0 = c * chunk;
-    if (i0 >= n) return;
-    const int64_t i1 = i0 + chunk < n ? i0 + chunk : n;
+// bytes p .. p+7 of t (little-endian: byte p lowest), from two aligned words;
+// t is 8-byte aligned and zero-padded by >= 16 bytes past the text
+__device__ __forceinline__ uint64_t load8(const uint8_t *__restrict__ t, int64_t p) {
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(t + (p & ~int64_t{7}));
+    const int sh = (int)(p & 7) * 8;
+    const uint64_t lo = w[0], hi = w[1];
+    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+
+// Chunked Kasai: each thread owns kKasaiChunk consecutive text positions and
+// carries h through them (h restarts at 0 per chunk: exact, only less
+// amortised).  The workgroup's ISA slice is staged in LDS by coalesced loads
+// (a thread's own positions lie kKasaiChunk apart from its neighbours'), and
+// suffixes are compared 8 bytes per step.  The text's unique final '$' ends
+// every comparison before the padding (the caller checks SA[0] == n - 1).
+constexpr int kKasaiChunk = 64;
+__global__ __launch_bounds__(256) void k_kasai(const uint8_t *__restrict__ t, const uint32_t *__restrict__ sa,
+                                               const uint32_t *__restrict__ isa, int64_t n,
+                                               int32_t *__restrict__ lcp) {
+    __shared__ uint32_t ri[256 * (kKasaiChunk + 1)];   // + 1: a thread's slice starts in its own bank
+    const int64_t base = (int64_t)blockIdx.x * 256 * kKasaiChunk;
+    for (int k = threadIdx.x; k < 256 * kKasaiChunk; k += 256) {
+        const int64_t i = base + k;
+        ri[(k / kKasaiChunk) * (kKasaiChunk + 1) + k % kKasaiChunk] = i < n ? isa[i] : 0u;
+    }
+    __syncthreads();
+    const int64_t i0 = base + (int64_t)threadIdx.x * kKasaiChunk;
     int64_t h = 0;
-    for (int64_t i = i0; i < i1; ++i) {
-        const int64_t r = isa[i];
+    for (int q = 0; q < kKasaiChunk; ++q) {
+        const int64_t i = i0 + q;
+        if (i >= n) break;
+        const int64_t r = ri[threadIdx.x * (kKasaiChunk + 1) + q];
         if (r > 0) {
             const int64_t j = sa[r - 1];
-            while (i + h < n && j + h < n && t[i + h] == t[j + h]) ++h;
+            for (;;) {
+                const uint64_t x = load8(t, i + h) ^ load8(t, j + h);
+                if (x) {
+                    h += __builtin_ctzll(x) >> 3;
+                    break;
+                }
+                h += 8;
+            }
             lcp[r] = (int32_t)h;
             if (h > 0) --h;
         }
@@ -854,11 +884,12 @@ const int32_t *index_lcp_device(Ctx &c, DeviceIndex *ix) {
     uint32_t sa0 = 0;
     HIPCHECK(hipMemcpyAsync(&sa0, ix->sa.p, 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
-    if ((int64_t)sa0 == n - 1) {
-        const int64_t chunk = 64;
-        const int64_t nch = (n + chunk - 1) / chunk;
-        KLAUNCH("k_kasai", 13.0 * (double)n, k_kasai, dim3(blocks(nch)), dim3(256), 0, st, ix->text.as<uint8_t>(),
-                           ix->sa.as<uint32_t>(), isa, n, chunk, lcp);
+    uint8_t last = 0;
+    if (n > 0) HIPCHECK(hipMemcpy(&last, ix->text.as<uint8_t>() + n - 1, 1, hipMemcpyDeviceToHost));
+    if ((int64_t)sa0 == n - 1 && ix->totals[last] == 1) {   // a unique smallest last symbol ends every compare
+        const int64_t per = 256 * (int64_t)kKasaiChunk;
+        KLAUNCH("k_kasai", 13.0 * (double)n, k_kasai, dim3((unsigned)((n + per - 1) / per)), dim3(256), 0, st,
+                ix->text.as<uint8_t>(), ix->sa.as<uint32_t>(), isa, n, lcp);
     } else {
         // the smallest suffix is not the last one (no unique final sentinel):
         // Kasai's h then carries over the skipped rank-0 step, so replay it serially

@@ -23,6 +23,9 @@
 // maximality, match-rate filter, variations -- runs on the host over that table.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <mutex>
+
 #include <algorithm>
 #include <array>
 #include <set>
@@ -591,7 +594,7 @@ static bool consensus_array(const uint8_t *t, int64_t n, int64_t start, int64_t 
 }
 
 // canonical (least rotation, forward only) primitive ACGT strings of length k, product order
-static void enumerate_motifs(int k, std::vector<std::string> &out) {
+static void enumerate_motifs_build(int k, std::vector<std::string> &out) {
     out.clear();
     static const char A[4] = {'A', 'C', 'G', 'T'};
     const int64_t total = (int64_t)1 << (2 * k);
@@ -609,6 +612,14 @@ static void enumerate_motifs(int k, std::vector<std::string> &out) {
         }
         if (keep) out.push_back(s);
     }
+}
+
+// the same sets, built once per process (k <= 10: they never change)
+static const std::vector<std::string> &motif_set(int k) {
+    static std::vector<std::string> sets[11];
+    static std::once_flag once[11];
+    std::call_once(once[k], [k] { enumerate_motifs_build(k, sets[k]); });
+    return sets[k];
 }
 
 inline char comp_base(char c) {
@@ -759,6 +770,10 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
                             int32_t chrom, RecVec &out) {
     const int64_t n = index_n(ix);
     if (n > 1000000 || n == 0) return;                    // bwt.py:2048
+    using clk = std::chrono::steady_clock;
+    const bool stats = [] { const char *e = std::getenv("BWTMI_STATS"); return e && *e == '1'; }();
+    const auto T0 = clk::now();
+    auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     const int kmin = std::max(1, p.min_period), kend = std::min(p.max_short_motif + 1, 10);
     hipStream_t st = c.stream;
     std::vector<uint8_t> text((size_t)n);
@@ -770,7 +785,10 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
     const int64_t tot = (int64_t)Lmax * n;
     c.slot[S_IDX0].ensure((size_t)tot * 4);
     c.slot[S_COUNTS].ensure(256 * 8);
-    std::vector<uint32_t> ext_word((size_t)tot);
+    // the table comes down into the context's pinned staging buffer (kept between calls)
+    HBuf &ext_buf = c.host[2];
+    ext_buf.ensure((size_t)tot * 4);
+    uint32_t *const ext_word = ext_buf.as<uint32_t>();
     std::unordered_map<int64_t, std::array<int64_t, 3>> ext_side;   // q -> (start, end, copies)
     for (int64_t cap = 1 << 16;;) {
         c.slot[S_IDX1].ensure((size_t)cap * sizeof(ExtSide));
@@ -787,7 +805,8 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
             continue;
         }
         std::vector<ExtSide> side((size_t)ns);
-        HIPCHECK(hipMemcpyAsync(ext_word.data(), c.slot[S_IDX0].p, (size_t)tot * 4, hipMemcpyDeviceToHost, st));
+        if (stats) std::fprintf(stderr, "    text + extension kernel %.1f ms\n", ms_since(T0));
+        HIPCHECK(hipMemcpyAsync(ext_word, c.slot[S_IDX0].p, (size_t)tot * 4, hipMemcpyDeviceToHost, st));
         if (ns) HIPCHECK(hipMemcpyAsync(side.data(), c.slot[S_IDX1].p, (size_t)ns * sizeof(ExtSide),
                                         hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
@@ -821,6 +840,7 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
         c0 = 1 + lf + rt;
     };
 
+    const double t_ext = ms_since(T0);
     // seeds: k-mer table (with the reference's short-k lookup, bwt.py:173-193) or FM locate
     std::vector<int64_t> koff;
     std::vector<int32_t> kpos;
@@ -829,34 +849,63 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
         koff.resize(65537);
         kpos.resize((size_t)kcount);
         index_get_kmer(c, ix, koff.data(), kpos.data());
+        if (stats) std::fprintf(stderr, "    kmer table down %.1f ms\n", ms_since(T0) - t_ext);
     }
-    std::vector<std::vector<std::string>> motifs(10);
-    std::vector<std::string> pats;            // patterns that go through locate
+    // The motifs in the reference's order (k ascending, enumerate_motifs order,
+    // entropy filter, bwt.py:2053-2095), each with its first locate pattern.
+    struct MotifTask {
+        int k;
+        const std::string *m;
+        size_t pat;
+    };
+    std::vector<MotifTask> tasks;
+    size_t npats = 0;
     for (int k = kmin; k < kend; ++k) {
-        enumerate_motifs(k, motifs[(size_t)k]);
-        if (k <= 8 && kcount > 0) continue;
-        for (auto &m : motifs[(size_t)k]) {
-            if (entropy_of(m.data(), k) < p.min_entropy) continue;
-            std::string rc(m.rbegin(), m.rend());
-            for (auto &ch : rc) ch = comp_base(ch);
-            for (int r = 0; r < k; ++r) {
-                pats.push_back(m.substr((size_t)r) + m.substr(0, (size_t)r));
-                pats.push_back(rc.substr((size_t)r) + rc.substr(0, (size_t)r));
-            }
+        const bool use_hash = k <= 8 && kcount > 0;
+        for (auto &m : motif_set(k)) {
+            if (entropy_of(m.data(), k) < p.min_entropy) continue;   // bwt.py:2058-2060
+            tasks.push_back({k, &m, npats});
+            if (!use_hash) npats += 2 * (size_t)k;
         }
+    }
+    const int nt = std::max(1, host_cpu_budget(nullptr, nullptr));
+    // patterns that go through locate: every rotation of the motif and of its
+    // reverse complement, each motif's 2k patterns written in place (in parallel)
+    std::string blob;
+    std::vector<int64_t> off(npats + 1, 0);
+    if (npats) {
+        std::vector<size_t> at(tasks.size(), 0);
+        size_t bytes = 0;
+        for (size_t ti = 0; ti < tasks.size(); ++ti)
+            if (!(tasks[ti].k <= 8 && kcount > 0)) {
+                at[ti] = bytes;
+                bytes += 2 * (size_t)tasks[ti].k * (size_t)tasks[ti].k;
+            }
+        blob.resize(bytes);
+        run_tasks((int64_t)tasks.size(), nt, [&](int64_t ti) {
+            const MotifTask &mt = tasks[(size_t)ti];
+            const int k = mt.k;
+            if (k <= 8 && kcount > 0) return;
+            const std::string &m = *mt.m;
+            char rc[16];
+            for (int x = 0; x < k; ++x) rc[x] = comp_base(m[(size_t)(k - 1 - x)]);
+            char *w = &blob[at[(size_t)ti]];
+            size_t q = mt.pat;
+            for (int r = 0; r < k; ++r) {
+                for (int x = 0; x < k; ++x) *w++ = m[(size_t)((r + x) % k)];
+                off[++q] = (int64_t)(at[(size_t)ti] + (size_t)(2 * r + 1) * (size_t)k);
+                for (int x = 0; x < k; ++x) *w++ = rc[(r + x) % k];
+                off[++q] = (int64_t)(at[(size_t)ti] + (size_t)(2 * r + 2) * (size_t)k);
+            }
+        });
     }
     std::vector<int64_t> spep;
     std::vector<int32_t> sa;
-    size_t pat_at = 0;
-    if (!pats.empty()) {
-        std::vector<int64_t> off(pats.size() + 1, 0);
-        std::string blob;
-        for (size_t q = 0; q < pats.size(); ++q) {
-            blob += pats[q];
-            off[q + 1] = (int64_t)blob.size();
-        }
-        spep.resize(pats.size() * 2);
-        index_backward_search(c, ix, (const uint8_t *)blob.data(), off.data(), (int64_t)pats.size(), spep.data());
+    if (npats) {
+        spep.resize(npats * 2);
+        if (stats) std::fprintf(stderr, "    motifs + %zu patterns %.1f ms\n", npats, ms_since(T0) - t_ext);
+        index_backward_search(c, ix, (const uint8_t *)blob.data(), off.data(), (int64_t)npats, spep.data());
+        if (stats) std::fprintf(stderr, "    backward search %.1f ms\n", ms_since(T0) - t_ext);
         sa.resize((size_t)n);
         index_get_sa(c, ix, sa.data());
     }
@@ -866,97 +915,213 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
         for (int64_t x = std::max<int64_t>(0, seen_pairs[q]); x < std::min<int64_t>(n, seen_pairs[q + 1]); ++x)
             seen[(size_t)x] = 1;
     const std::string seq((const char *)t, (size_t)n);
-    std::vector<int64_t> positions;
-    AlignSummary summ;
-    for (int k = kmin; k < kend; ++k) {
-        for (auto &m : motifs[(size_t)k]) {
-            if (entropy_of(m.data(), k) < p.min_entropy) continue;   // bwt.py:2058-2060
-            positions.clear();
-            const bool use_hash = k <= 8 && kcount > 0;
-            std::string rc(m.rbegin(), m.rend());
-            for (auto &ch : rc) ch = comp_base(ch);
-            if (use_hash) {
-                for (int r = 0; r < k; ++r)
-                    for (const std::string &rot : {m.substr((size_t)r) + m.substr(0, (size_t)r),
-                                                   rc.substr((size_t)r) + rc.substr(0, (size_t)r)}) {
-                        int64_t w = 0;
-                        for (char ch : rot) w = (w << 2) | (ch == 'C' ? 1 : ch == 'G' ? 2 : ch == 'T' ? 3 : 0);
-                        for (int64_t q = koff[(size_t)w]; q < koff[(size_t)w + 1]; ++q) positions.push_back(kpos[(size_t)q]);
-                    }
-            } else {
-                for (int r = 0; r < 2 * k; ++r, ++pat_at) {
-                    const int64_t sp = spep[2 * pat_at], ep = spep[2 * pat_at + 1];
-                    if (sp < 0) continue;
-                    for (int64_t q = sp; q <= ep; ++q) positions.push_back(sa[(size_t)q]);
+
+    // seed positions of a motif: every rotation of it and of its reverse
+    // complement, through the k-mer table or the FM interval's SA rows; sorted, unique
+    auto seeds_of = [&](const MotifTask &mt, std::vector<int64_t> &positions) {
+        positions.clear();
+        const int k = mt.k;
+        const std::string &m = *mt.m;
+        std::string rc(m.rbegin(), m.rend());
+        for (auto &ch : rc) ch = comp_base(ch);
+        if (k <= 8 && kcount > 0) {
+            for (int r = 0; r < k; ++r)
+                for (const std::string &rot : {m.substr((size_t)r) + m.substr(0, (size_t)r),
+                                               rc.substr((size_t)r) + rc.substr(0, (size_t)r)}) {
+                    int64_t w = 0;
+                    for (char ch : rot) w = (w << 2) | (ch == 'C' ? 1 : ch == 'G' ? 2 : ch == 'T' ? 3 : 0);
+                    for (int64_t q = koff[(size_t)w]; q < koff[(size_t)w + 1]; ++q) positions.push_back(kpos[(size_t)q]);
                 }
+        } else {
+            for (int r = 0; r < 2 * k; ++r) {
+                const int64_t sp = spep[2 * (mt.pat + (size_t)r)], ep = spep[2 * (mt.pat + (size_t)r) + 1];
+                if (sp < 0) continue;
+                for (int64_t q = sp; q <= ep; ++q) positions.push_back(sa[(size_t)q]);
             }
-            std::sort(positions.begin(), positions.end());
-            positions.erase(std::unique(positions.begin(), positions.end()), positions.end());
-            if ((int64_t)positions.size() < p.min_copies || !p.allow_mismatches) continue;
-            // _find_tandems_fm_with_mismatches (bwt.py:2562-2695)
-            int64_t motif_len = k;
-            for (int64_t seed : positions) {
-                if (seen[(size_t)seed]) continue;
-                if (seed + motif_len > n) continue;
-                int64_t bs = -1, be = -1, bc = 0;
-                const int64_t shifts = std::min<int64_t>(motif_len, seed + 1);
-                for (int64_t sh = 0; sh < shifts; ++sh) {
-                    const int64_t cs = seed - sh;
-                    if (cs < 0 || cs + motif_len > n || seen[(size_t)cs]) continue;
-                    const int64_t q = (motif_len - 1) * n + cs;
-                    int64_t s, e, cc;
-                    ext_of(q, motif_len, cs, s, e, cc);
-                    if (!(s <= seed && seed < e)) continue;
-                    if (cc > bc || (cc == bc && (bs < 0 || s < bs))) { bs = s; be = e; bc = cc; }
-                }
-                if (bs < 0) continue;
-                int64_t start = bs, end = be, copies = bc;
-                if (!(copies >= p.min_copies && end - start >= p.min_array_length)) continue;
-                std::string cons;
-                double mm = 0;
-                int64_t maxmm = 0;
-                if (!consensus_array(t, n, start, motif_len, copies, cons, mm, maxmm)) continue;
-                const int64_t prim = smallest_period(cons.data(), (int64_t)cons.size());
-                if (prim < (int64_t)cons.size()) {
-                    motif_len = prim;                    // persists for the later seeds (as in the reference)
-                    copies = std::max<int64_t>(1, (end - start) / motif_len);
-                    end = start + copies * motif_len;
-                    if (!consensus_array(t, n, start, motif_len, copies, cons, mm, maxmm)) continue;
-                }
-                std::string canon;
-                char strand = '+';
-                canonical_stranded(cons, canon, strand);
-                if (start > 0 && t[start - 1] == (uint8_t)cons[(size_t)motif_len - 1]) continue;   // _is_maximal_fm
-                if (end < n && t[end] == (uint8_t)cons[0]) continue;
-                const double pm = (1.0 - mm) * 100.0;
-                if (pm < (motif_len <= 6 ? 90.0 : 85.0)) continue;
+        }
+        std::sort(positions.begin(), positions.end());
+        positions.erase(std::unique(positions.begin(), positions.end()), positions.end());
+    };
+    // the best extension through seed over the shifts whose start is not seen
+    // (seen == nullptr: all shifts) -- most copies, then the leftmost start
+    auto best_of = [&](int64_t seed, int64_t motif_len, const uint8_t *sn, int64_t &bs, int64_t &be, int64_t &bc) {
+        bs = be = -1;
+        bc = 0;
+        const int64_t shifts = std::min<int64_t>(motif_len, seed + 1);
+        for (int64_t sh = 0; sh < shifts; ++sh) {
+            const int64_t cs = seed - sh;
+            if (cs < 0 || cs + motif_len > n || (sn && sn[(size_t)cs])) continue;
+            const int64_t q = (motif_len - 1) * n + cs;
+            int64_t s0, e0, cc;
+            ext_of(q, motif_len, cs, s0, e0, cc);
+            if (!(s0 <= seed && seed < e0)) continue;
+            if (cc > bc || (cc == bc && (bs < 0 || s0 < bs))) { bs = s0; be = e0; bc = cc; }
+        }
+    };
+    // Parallel pass, per motif: its seeds, and the ones that can still become
+    // a record.  `seen` only grows and removes shifts, and a subset's best has
+    // no more copies (and span = copies x unit), so a seed whose best over all
+    // shifts fails min_copies / min_array_length fails in the serial walk too.
+    // The serial walk below then replays the order-dependent state (seen, the
+    // motif length carried from one seed to the next, bwt.py:2655) over the
+    // survivors only -- the consensus, periodicity and maximality work stays there.
+    // The record a seed yields from its extension (start, end, copies) with
+    // motif length L (bwt.py:2641-2690 after the extension): the majority-vote
+    // consensus, the primitive reduction (the new motif length persists for
+    // the motif's later seeds), maximality and the %match floor.  A pure
+    // function of its arguments and the text.
+    struct Decision {
+        int64_t start = 0, end = 0, copies = 0, len_after = 0;   // len_after: the motif length for later seeds
+        bool emit = false;
+        std::string cons;
+        double mm = 0;
+        int64_t maxmm = 0;
+    };
+    auto decide = [&](int64_t start, int64_t end, int64_t copies, int64_t L, Decision &d) {
+        d.emit = false;
+        d.len_after = L;
+        d.cons.clear();
+        if (!consensus_array(t, n, start, L, copies, d.cons, d.mm, d.maxmm)) return;
+        const int64_t prim = smallest_period(d.cons.data(), (int64_t)d.cons.size());
+        if (prim < (int64_t)d.cons.size()) {
+            L = prim;
+            d.len_after = prim;                   // persists for the later seeds (as in the reference)
+            copies = std::max<int64_t>(1, (end - start) / L);
+            end = start + copies * L;
+            if (!consensus_array(t, n, start, L, copies, d.cons, d.mm, d.maxmm)) return;
+        }
+        if (start > 0 && t[start - 1] == (uint8_t)d.cons[(size_t)L - 1]) return;   // _is_maximal_fm
+        if (end < n && t[end] == (uint8_t)d.cons[0]) return;
+        if ((1.0 - d.mm) * 100.0 < (L <= 6 ? 90.0 : 85.0)) return;
+        d.start = start;
+        d.end = end;
+        d.copies = copies;
+        d.emit = true;
+    };
+    struct Cand {
+        int64_t seed, bs, be, bc;   // the best extension over all shifts
+        Decision d;                 // what it yields with the motif's own length
+    };
+    struct TaskOut {
+        bool skip = true;           // fewer than min_copies seeds, or no mismatch search
+        std::vector<Cand> keep;     // candidate seeds, ascending
+    };
+    std::vector<TaskOut> tout(tasks.size());
+    const double t_prep = ms_since(T0);
+    run_tasks((int64_t)tasks.size(), nt, [&](int64_t ti) {
+        thread_local std::vector<int64_t> positions;
+        const MotifTask &mt = tasks[(size_t)ti];
+        seeds_of(mt, positions);
+        TaskOut &o = tout[(size_t)ti];
+        if ((int64_t)positions.size() < p.min_copies || !p.allow_mismatches) return;
+        o.skip = false;
+        for (int64_t seed : positions) {
+            if (seed + mt.k > n) continue;
+            Cand cd;
+            best_of(seed, mt.k, nullptr, cd.bs, cd.be, cd.bc);
+            if (cd.bs < 0 || !(cd.bc >= p.min_copies && cd.be - cd.bs >= p.min_array_length)) continue;
+            cd.seed = seed;
+            decide(cd.bs, cd.be, cd.bc, mt.k, cd.d);
+            o.keep.push_back(std::move(cd));
+        }
+    });
+    const double t_par = ms_since(T0);
+    size_t nkeep = 0;
+    for (const TaskOut &o : tout) nkeep += o.keep.size();
+    const size_t first_new = out.size();
+    struct Report {
+        bool on;
+        clk::time_point t0;
+        double a, b, c;
+        size_t tasks, keep;
+        const RecVec &out;
+        ~Report() {
+            if (on)
+                std::fprintf(stderr, "  short_imperfect: extension table %.1f, seeds/patterns %.1f, parallel seeds %.1f, "
+                             "serial walk + variations %.1f ms (%zu motifs, %zu candidate seeds, %zu records)\n", a,
+                             b - a, c - b, std::chrono::duration<double, std::milli>(clk::now() - t0).count() - c,
+                             tasks, keep, out.size());
+        }
+    } report{stats, T0, t_ext, t_prep, t_par, tasks.size(), nkeep, out};
+    // _find_tandems_fm_with_mismatches (bwt.py:2562-2695) in the reference's
+    // order: only the seen test, the extension over the unseen shifts and the
+    // motif length carried between seeds are order-dependent; a candidate
+    // whose extension is the precomputed one takes its precomputed decision
+    std::vector<int64_t> all;
+    Decision dd;
+    size_t nfull = 0;
+    for (size_t ti = 0; ti < tasks.size(); ++ti) {
+        TaskOut &o = tout[ti];
+        if (o.skip) continue;
+        const MotifTask &mt = tasks[ti];
+        int64_t motif_len = mt.k;
+        bool full = false;   // walking every seed (after a motif length change)
+        const size_t cnt = o.keep.size();
+        for (size_t si = 0; si < (full ? all.size() : cnt); ++si) {
+            const int64_t seed = full ? all[si] : o.keep[si].seed;
+            if (seen[(size_t)seed]) continue;
+            if (seed + motif_len > n) continue;
+            int64_t bs, be, bc;
+            best_of(seed, motif_len, seen.data(), bs, be, bc);
+            if (bs < 0) continue;
+            if (!(bc >= p.min_copies && be - bs >= p.min_array_length)) continue;
+            const Decision *d;
+            if (!full && motif_len == mt.k && bs == o.keep[si].bs && be == o.keep[si].be && bc == o.keep[si].bc) {
+                d = &o.keep[si].d;
+            } else {
+                decide(bs, be, bc, motif_len, dd);
+                d = &dd;
+            }
+            const int64_t len_before = motif_len;
+            motif_len = d->len_after;
+            if (d->emit) {
                 Rec r;
                 r.chrom = chrom;
                 r.tier = 2;
-                r.start = start;
-                r.end = end;
-                r.length = end - start;
-                r.motif = cons;
-                r.copies = (double)copies;
-                r.confidence = std::max(0.5, 1.0 - mm);
-                r.mismatch_rate = mm;
-                r.max_mm = maxmm;
-                r.n_eval = copies;
-                r.strand = strand;
-                r.pmatch = pm;
+                r.start = d->start;
+                r.end = d->end;
+                r.length = d->end - d->start;
+                r.motif = d->cons;
+                r.copies = (double)d->copies;
+                r.confidence = std::max(0.5, 1.0 - d->mm);
+                r.mismatch_rate = d->mm;
+                r.max_mm = d->maxmm;
+                r.n_eval = d->copies;
+                r.pmatch = (1.0 - d->mm) * 100.0;
                 r.pindel = 0.0;
-                r.score = trf_score(end - start, mm);
+                r.score = trf_score(d->end - d->start, d->mm);
                 r.act_kind = ACT_FULL;
-                r.act_off = std::min(start, n);
-                r.act_len = std::max<int64_t>(0, std::min(end, n) - r.act_off);
-                // summarize_variations_array -> align_repeat_region(min_copies=1) (bwt.py:1259-1287)
-                if (align_repeat_region(seq.data(), n, start, end, cons, 1, summ) && summ.any_variation)
-                    r.variations = summ.variations;
+                r.act_off = std::min(d->start, n);
+                r.act_len = std::max<int64_t>(0, std::min(d->end, n) - r.act_off);
+                for (int64_t x = d->start; x < std::min(d->end, n); ++x) seen[(size_t)x] = 1;
                 out.push_back(std::move(r));
-                for (int64_t x = start; x < std::min(end, n); ++x) seen[(size_t)x] = 1;
+            }
+            // a changed motif length changes every later seed's extension: the
+            // candidates of the parallel pass (found with the motif's own length)
+            // no longer cover them, so the walk goes on over all of its seeds
+            if (motif_len != len_before && !full) {
+                seeds_of(mt, all);
+                all.erase(all.begin(), std::upper_bound(all.begin(), all.end(), seed));
+                full = true;
+                ++nfull;
+                si = (size_t)-1;   // ++ -> 0
             }
         }
     }
+    if (stats) std::fprintf(stderr, "    serial walk %.1f ms (%zu motifs walked over all seeds)\n", ms_since(T0) - t_par, nfull);
+    // per record, independent of the walk: the strand of the canonical motif
+    // and the variations (summarize_variations_array -> align_repeat_region
+    // with min_copies 1, bwt.py:1259-1287)
+    run_tasks((int64_t)(out.size() - first_new), nt, [&](int64_t q) {
+        thread_local AlignSummary summ;
+        Rec &r = out[first_new + (size_t)q];
+        std::string canon;
+        char strand = '+';
+        canonical_stranded(r.motif, canon, strand);
+        r.strand = strand;
+        if (align_repeat_region(seq.data(), n, r.start, r.end, r.motif, 1, summ) && summ.any_variation)
+            r.variations = summ.variations;
+    });
 }
 
 
