@@ -730,6 +730,114 @@ __global__ __launch_bounds__(256) void k_runs_sparse(const uint32_t *__restrict_
     }
 }
 
+// The sampled groups of unit lengths over LDS tiles: a workgroup copies its
+// tile of kRunTile words (and the halo the sampled windows and owner tests
+// reach: the largest stride before, one group plus two words after) into LDS
+// once, coalesced, and then examines every sample of every group of the
+// launch inside the tile from there -- the planes are read once per launch
+// instead of three scattered lines per sample and group.  Samples of all
+// groups are flattened over the lanes (the large-stride groups have few).
+// Candidates and their order-free output are exactly k_runs_sparse's.
+template <int B>
+constexpr int run_tile() { return 4096 / B; }   // words per workgroup: <= 64 KB of LDS with a 256-word halo
+constexpr int kRunHaloAfter = 34;
+template <int B>
+__global__ __launch_bounds__(256) void k_runs_tiled(const uint32_t *__restrict__ P, int64_t n, int64_t nwords32,
+                                                    int32_t lmin, int32_t lmax, int64_t mc, SparseGroups sg,
+                                                    int32_t halo, CandOut out) {
+    extern __shared__ uint32_t tl[];   // words base .. base + span - 1, B planes each
+    __shared__ int64_t pre[kSparseMax + 1], first[kSparseMax];
+    constexpr int kRunTile = run_tile<B>();
+    const int64_t w0 = (int64_t)blockIdx.x * kRunTile;
+    const int64_t base = w0 - halo;
+    const int64_t span = halo + kRunTile + kRunHaloAfter;
+    for (int64_t k = threadIdx.x; k < span * B; k += 256) {
+        const int64_t w = base + k / B;
+        tl[k] = w >= 0 && w < nwords32 + 8 ? P[base * B + k] : 0u;
+    }
+    const int64_t wend = min(w0 + (int64_t)kRunTile, nwords32);
+    if (threadIdx.x == 0) {   // samples j * s of group gi in [w0, wend): [first, first + count)
+        pre[0] = 0;
+        for (int gi = 0; gi < sg.ng; ++gi) {
+            const int64_t s = sg.s[gi];
+            first[gi] = (w0 + s - 1) / s;
+            pre[gi + 1] = pre[gi] + max((int64_t)0, (wend + s - 1) / s - first[gi]);
+        }
+    }
+    __syncthreads();
+    // M_L of word w (bit k <-> position 32w + k), from the tile
+    auto eqL = [&](int64_t w, int64_t L) -> uint32_t {
+        const int64_t lim = n - L - w * 32;   // positions 32w + k valid iff k < lim
+        if (w < 0 || lim <= 0) return 0u;
+        const int64_t q = w + (L >> 5) - base;
+        const uint32_t r = (uint32_t)(L & 31);
+        const int64_t a = (w - base) * B;
+        uint32_t x = 0;
+#pragma unroll
+        for (int p = 0; p < B; ++p) x |= tl[a + p] ^ __builtin_amdgcn_alignbit(tl[(q + 1) * B + p], tl[q * B + p], r);
+        uint32_t m = ~x;
+        if (lim < 32) m &= (1u << lim) - 1u;
+        return m;
+    };
+    const int lane = threadIdx.x & 63;
+    const int seg = (int)(blockIdx.x & (kCandSegs - 1));
+    const int64_t total = pre[sg.ng];
+    for (int64_t f0 = 0; f0 < total; f0 += 256) {   // uniform
+        const int64_t f = f0 + threadIdx.x;
+        const bool live = f < total;
+        int gi = 0;
+        while (gi + 1 < sg.ng && f >= pre[gi + 1]) ++gi;
+        const int64_t s = sg.s[gi];
+        const int64_t w = live ? (first[gi] + (f - pre[gi])) * s : w0;
+        const int64_t Lg = (int64_t)sg.g[gi] * 32;
+        for (int r = 0; r < 32; ++r) {   // uniform
+            const int64_t L = Lg + r;
+            const bool ok = live && L >= lmin && L <= lmax;
+            const uint32_t M = ok ? eqL(w, L) : 0u;
+            // owner test: the first non-full word among w-1 .. w-s gives the
+            // run's start (all full: the previous sample owns the run)
+            int64_t start = -1;
+            if (__any(M == FULL) && M == FULL) {
+                for (int64_t k0 = 1; k0 <= s && start < 0; k0 += 8) {
+                    uint32_t Mq[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) Mq[i] = k0 + i <= s ? eqL(w - (k0 + i), L) : FULL;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        if (start < 0 && Mq[i] != FULL) start = (w - (k0 + i) + 1) * 32 - (int64_t)__clz(~Mq[i]);
+                }
+            }
+            uint64_t own = __ballot(start >= 0);   // uniform
+            while (own) {
+                const int src = __ffsll((unsigned long long)own) - 1;
+                own &= own - 1;
+                const int64_t ws = ((int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w, src)) |
+                                   ((int64_t)__builtin_amdgcn_readlane((int)(w >> 32), src) << 32);
+                const int64_t st = ((int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)start, src)) |
+                                   ((int64_t)__builtin_amdgcn_readlane((int)(start >> 32), src) << 32);
+                const int64_t Lo = ((int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)L, src));
+                const int64_t Ko = (mc - 1) * Lo;
+                // end: the first non-full word after ws -- one 64-word step here
+                // (global: it may leave the tile), a longer streak is ended by k_streak_end
+                const int64_t q0 = ws + 1;
+                const uint32_t Mq = eq32<B>(P, q0 + lane, Lo, n);   // 0 past the text: ends the scan
+                const uint64_t nb = __ballot(Mq != FULL);
+                if (!nb) {
+                    if (lane == 0) push_pending(out, Lo, st, q0 + 64);
+                    continue;
+                }
+                const int fb = __ffsll((unsigned long long)nb) - 1;
+                const uint32_t Mf = (uint32_t)__builtin_amdgcn_readlane((int)Mq, fb);
+                const int64_t end = (q0 + fb) * 32 + (int64_t)__ffs(~Mf) - 1;
+                if (end - st >= Ko && lane == 0) {
+                    const unsigned long long at = atomicAdd(out.count + seg, 1ull);
+                    put(out, seg, at, Lo, st, end);
+                }
+            }
+        }
+    }
+}
+
 // End search of the deferred streaks, one wave per streak (grid-stride over
 // the list; every wave leaves when the list is exhausted): 8 x 64 words per
 // step, their loads issued before any ballot.  A candidate is put when the
@@ -801,8 +909,18 @@ void launch_runs(Ctx &c, const uint32_t *P, int64_t n, int32_t lmin, int32_t lma
         }
         const int64_t waves = sg.woff[sg.ng];
         if (waves == 0) continue;
-        KLAUNCH("k_runs_sparse", 0.0, (k_runs_sparse<B>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, c.stream,
-                P, n, nwords32, lmin, lmax, mc, sg, out);
+        int32_t halo = 0;
+        for (int gi = 0; gi < sg.ng; ++gi) halo = std::max(halo, sg.s[gi]);
+        static const bool untiled = [] { const char *e = std::getenv("BWTMI_RUNS_UNTILED"); return e && *e == '1'; }();
+        if (!untiled && halo <= 256) {   // LDS tiles (BWTMI_RUNS_UNTILED=1: the scattered-sample kernel)
+            constexpr int T = run_tile<B>();
+            const size_t lds = (size_t)(halo + T + kRunHaloAfter) * B * 4;
+            KLAUNCH("k_runs_sparse", 0.0, (k_runs_tiled<B>), dim3((unsigned)((nwords32 + T - 1) / T)),
+                    dim3(256), lds, c.stream, P, n, nwords32, lmin, lmax, mc, sg, halo, out);
+        } else {
+            KLAUNCH("k_runs_sparse", 0.0, (k_runs_sparse<B>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, c.stream,
+                    P, n, nwords32, lmin, lmax, mc, sg, out);
+        }
     }
     KLAUNCH("k_streak_end", 0.0, (k_streak_end<B>), dim3(512), dim3(256), 0, c.stream, P, n, mc, out);
 }
