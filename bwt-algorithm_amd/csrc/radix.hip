@@ -443,6 +443,44 @@ void radix_sort_impl(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
 
 }  // namespace
 
+// Mid-size arrays (the radix count tables of short inputs, flag arrays of
+// a few tens of thousands): one workgroup walks the array 4096 elements a step
+// with a running carry -- one launch instead of the sums / scan / scan chain
+// (three launches and their gaps on a launch-bound 12.5 Mbp scan)
+constexpr int64_t kOneBlockScan = 32768;
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_scan_one(const T *__restrict__ in, T *__restrict__ out, int64_t n) {
+    __shared__ T ws[kWaves];
+    __shared__ T carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int64_t c0 = 0; c0 < n; c0 += kTile) {
+        const int64_t base = c0 + (int64_t)threadIdx.x * kItems;
+        T x[kItems];
+#pragma unroll
+        for (int i = 0; i < kItems; ++i) x[i] = base + i < n ? in[base + i] : (T)0;
+        T s = 0;
+#pragma unroll
+        for (int i = 0; i < kItems; ++i) {
+            const T t = x[i];
+            x[i] = s;
+            s += t;
+        }
+        const T inc = wave_incl_scan<T>(s);
+        const int wv = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 63) ws[wv] = inc;
+        __syncthreads();
+        T excl = inc - s + carry;
+        for (int w = 0; w < wv; ++w) excl += ws[w];
+#pragma unroll
+        for (int i = 0; i < kItems; ++i)
+            if (base + i < n) out[base + i] = x[i] + excl;
+        __syncthreads();   // every thread has read carry and ws
+        if (threadIdx.x == kBlock - 1) carry = excl + s;
+        __syncthreads();
+    }
+}
+
 // in place (in == out) is allowed: a chunk's elements are read before any is written
 template <class T>
 static void scan_rec(Ctx &c, const T *in, T *out, int64_t n, T *tmp) {
@@ -450,6 +488,11 @@ static void scan_rec(Ctx &c, const T *in, T *out, int64_t n, T *tmp) {
     const bool v = vec && (((uintptr_t)in | (uintptr_t)out) & 15) == 0;   // 16-byte vectors need aligned bases
     const int64_t nch = (n + kTile - 1) / kTile;
     const double bytes = 2.0 * (double)n * (double)sizeof(T);
+    static const bool one = [] { const char *e = std::getenv("BWTMI_SCAN_ONE"); return !(e && *e == '0'); }();
+    if (nch > 1 && n <= kOneBlockScan && one) {
+        KLAUNCH("k_chunk_scan", bytes, k_scan_one<T>, dim3(1), dim3(kBlock), 0, c.stream, in, out, n);
+        return;
+    }
     if (nch == 1) {
         if (v) KLAUNCH("k_chunk_scan", bytes, k_chunk_scan_v<T>, dim3(1), dim3(kBlock), 0, c.stream, in, out, (const T *)nullptr, n);
         else KLAUNCH("k_chunk_scan", bytes, k_chunk_scan<T>, dim3(1), dim3(kBlock), 0, c.stream, in, out, (const T *)nullptr, n);

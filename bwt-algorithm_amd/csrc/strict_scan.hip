@@ -739,7 +739,9 @@ __global__ __launch_bounds__(256) void k_runs_sparse(const uint32_t *__restrict_
 // groups are flattened over the lanes (the large-stride groups have few).
 // Candidates and their order-free output are exactly k_runs_sparse's.
 template <int B>
-constexpr int run_tile() { return 4096 / B; }   // words per workgroup: <= 64 KB of LDS with a 256-word halo
+constexpr int run_tile() { return 2048 / B; }   // words per workgroup: <= 64 KB of LDS with a 256-word halo
+constexpr int kRunGroupSplit = 2;   // gridDim.y: workgroups share a tile's groups (gi mod 2): 2x the
+                                    // workgroups of a short contig, each tile read twice
 constexpr int kRunHaloAfter = 34;
 template <int B>
 __global__ __launch_bounds__(256) void k_runs_tiled(const uint32_t *__restrict__ P, int64_t n, int64_t nwords32,
@@ -756,12 +758,13 @@ __global__ __launch_bounds__(256) void k_runs_tiled(const uint32_t *__restrict__
         tl[k] = w >= 0 && w < nwords32 + 8 ? P[base * B + k] : 0u;
     }
     const int64_t wend = min(w0 + (int64_t)kRunTile, nwords32);
-    if (threadIdx.x == 0) {   // samples j * s of group gi in [w0, wend): [first, first + count)
+    if (threadIdx.x == 0) {   // samples j * s of this workgroup's groups in [w0, wend): [first, first + count)
         pre[0] = 0;
         for (int gi = 0; gi < sg.ng; ++gi) {
             const int64_t s = sg.s[gi];
             first[gi] = (w0 + s - 1) / s;
-            pre[gi + 1] = pre[gi] + max((int64_t)0, (wend + s - 1) / s - first[gi]);
+            const bool mine = gi % (int)gridDim.y == (int)blockIdx.y;
+            pre[gi + 1] = pre[gi] + (mine ? max((int64_t)0, (wend + s - 1) / s - first[gi]) : 0);
         }
     }
     __syncthreads();
@@ -780,7 +783,7 @@ __global__ __launch_bounds__(256) void k_runs_tiled(const uint32_t *__restrict__
         return m;
     };
     const int lane = threadIdx.x & 63;
-    const int seg = (int)(blockIdx.x & (kCandSegs - 1));
+    const int seg = (int)((blockIdx.x * gridDim.y + blockIdx.y) & (kCandSegs - 1));
     const int64_t total = pre[sg.ng];
     for (int64_t f0 = 0; f0 < total; f0 += 256) {   // uniform
         const int64_t f = f0 + threadIdx.x;
@@ -789,11 +792,29 @@ __global__ __launch_bounds__(256) void k_runs_tiled(const uint32_t *__restrict__
         while (gi + 1 < sg.ng && f >= pre[gi + 1]) ++gi;
         const int64_t s = sg.s[gi];
         const int64_t w = live ? (first[gi] + (f - pre[gi])) * s : w0;
-        const int64_t Lg = (int64_t)sg.g[gi] * 32;
+        const int64_t g = sg.g[gi], Lg = g * 32;
+        // every L of the group compares word w with words w+g, w+g+1: three words
+        // per plane from the tile, once per sample
+        uint32_t a[B], lo[B], hi[B];
+#pragma unroll
+        for (int p = 0; p < B; ++p) {
+            a[p] = tl[(w - base) * B + p];
+            lo[p] = tl[(w + g - base) * B + p];
+            hi[p] = tl[(w + g + 1 - base) * B + p];
+        }
         for (int r = 0; r < 32; ++r) {   // uniform
             const int64_t L = Lg + r;
             const bool ok = live && L >= lmin && L <= lmax;
-            const uint32_t M = ok ? eqL(w, L) : 0u;
+            uint32_t M = 0u;
+            if (ok) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int p = 0; p < B; ++p) x |= a[p] ^ __builtin_amdgcn_alignbit(hi[p], lo[p], (uint32_t)r);
+                M = ~x;
+                const int64_t lim = n - L - w * 32;
+                if (lim <= 0) M = 0u;
+                else if (lim < 32) M &= (1u << lim) - 1u;
+            }
             // owner test: the first non-full word among w-1 .. w-s gives the
             // run's start (all full: the previous sample owns the run)
             int64_t start = -1;
@@ -915,8 +936,9 @@ void launch_runs(Ctx &c, const uint32_t *P, int64_t n, int32_t lmin, int32_t lma
         if (!untiled && halo <= 256) {   // LDS tiles (BWTMI_RUNS_UNTILED=1: the scattered-sample kernel)
             constexpr int T = run_tile<B>();
             const size_t lds = (size_t)(halo + T + kRunHaloAfter) * B * 4;
-            KLAUNCH("k_runs_sparse", 0.0, (k_runs_tiled<B>), dim3((unsigned)((nwords32 + T - 1) / T)),
-                    dim3(256), lds, c.stream, P, n, nwords32, lmin, lmax, mc, sg, halo, out);
+            KLAUNCH("k_runs_sparse", 0.0, (k_runs_tiled<B>),
+                    dim3((unsigned)((nwords32 + T - 1) / T), (unsigned)std::min(kRunGroupSplit, sg.ng)), dim3(256), lds,
+                    c.stream, P, n, nwords32, lmin, lmax, mc, sg, halo, out);
         } else {
             KLAUNCH("k_runs_sparse", 0.0, (k_runs_sparse<B>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, c.stream,
                     P, n, nwords32, lmin, lmax, mc, sg, out);
