@@ -187,6 +187,9 @@ char canonical_strand(const char *s, int64_t n);   // the strand of canonical_st
 bool pack2_acgt(const char *s, int64_t n, uint64_t &x);
 uint64_t rc2(uint64_t x, int64_t n);
 uint64_t min_rot2(uint64_t x, int64_t n);
+// min(min_rot2(x, n), min_rot2(rc2(x, n), n)): the canonical word of a packed
+// ACGT motif; n <= 8 from a table built once (4^n entries per length)
+uint64_t canon2(uint64_t x, int64_t n);
 // canonical word (min over rotations of the motif and its reverse complement)
 // of an ACGT motif of 33..64 bases; false if it has another symbol
 bool canon_key128(const char *s, int64_t n, unsigned __int128 &key);

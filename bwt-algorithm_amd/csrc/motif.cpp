@@ -113,6 +113,23 @@ uint64_t min_rot2(uint64_t x, int64_t n) {
     return best;
 }
 
+uint64_t canon2(uint64_t x, int64_t n) {
+    static const std::vector<uint16_t> *tab = [] {   // [n][x], n = 1..8
+        auto *t = new std::vector<uint16_t>[9];
+        for (int k = 1; k <= 8; ++k) {
+            t[k].resize((size_t)1 << (2 * k));
+            for (uint64_t v = 0; v < t[k].size(); ++v) {
+                const uint64_t f = min_rot2(v, k), r = min_rot2(rc2(v, k), k);
+                t[k][v] = (uint16_t)(f < r ? f : r);
+            }
+        }
+        return t;
+    }();
+    if (n >= 1 && n <= 8) return tab[n][(size_t)x];
+    const uint64_t f = min_rot2(x, n), r = min_rot2(rc2(x, n), n);
+    return f < r ? f : r;
+}
+
 // 33..64 bases: the same over 128-bit words
 typedef unsigned __int128 u128;
 static bool pack2_acgt128(const char *s, int64_t n, u128 &x) {

@@ -896,8 +896,7 @@ inline void canon_fill(const UnitCtx &u, const Item &it, Canon &c) {
     uint64_t x;
     c.packed = mv.size() <= 32 && pack2_acgt(mv.data(), (int64_t)mv.size(), x);
     if (c.packed) {
-        const uint64_t f = min_rot2(x, (int64_t)mv.size()), r = min_rot2(rc2(x, (int64_t)mv.size()), (int64_t)mv.size());
-        c.key = f < r ? f : r;
+        c.key = canon2(x, (int64_t)mv.size());
     } else if (mv.size() > 32 && mv.size() <= 64 && canon_key128(mv.data(), (int64_t)mv.size(), c.key)) {
         c.packed = true;   // same length on both sides (same_canonical), so the 64- and 128-bit keys never meet
     } else {
