@@ -371,6 +371,21 @@ class RepeatList(Sequence):
             check(lib().bwtmi_job_get_records(job.h, self._ints.ctypes.data_as(C.c_void_p),
                                               self._dbls.ctypes.data_as(C.c_void_p)))
         self._cache: Dict[int, TandemRepeat] = {}
+        self._cols: Dict[int, tuple] = {}
+
+    def _str(self, i: int, which: int) -> str:
+        """String `which` of record i from its column, fetched whole on first use
+        (bwtmi_job_get_strings: two C calls per column, not two per record)."""
+        col = self._cols.get(which)
+        if col is None:
+            off = np.zeros(self._n + 1, dtype=np.int64)
+            tot = lib().bwtmi_job_get_strings(self.job.h, which, None, 0, off.ctypes.data_as(C.c_void_p))
+            buf = C.create_string_buffer(max(int(tot), 1))
+            if tot > 0:
+                lib().bwtmi_job_get_strings(self.job.h, which, buf, tot, None)
+            col = self._cols[which] = (buf.raw[:max(int(tot), 0)], off.tolist())
+        raw, off = col
+        return raw[off[i]:off[i + 1]].decode("ascii", errors="replace")
 
     def __len__(self):
         return self._n
@@ -386,9 +401,9 @@ class RepeatList(Sequence):
         if r is None:
             s, e, ln, tier, neval, maxmm, score, flags, chrom = self._ints[i].tolist()
             copies, mm, conf, pmatch, pindel = self._dbls[i].tolist()
-            motif = self.job._string(i, 0)
-            var = self.job._string(i, 2)
-            act = self.job._string(i, 3)
+            motif = self._str(i, 0)
+            var = self._str(i, 2)
+            act = self._str(i, 3)
             if flags & 1:      # a bare consolidated Tier 3 call (bwt.py:3021-3030)
                 cons, comp, ent = None, None, 0.0
             elif flags & 2:    # compound-stage k-mer piece (bwt.py:3980-3987)
@@ -398,7 +413,7 @@ class RepeatList(Sequence):
             r = TandemRepeat(chrom=self.job.names[chrom], start=s, end=e, motif=motif, copies=copies,
                              length=ln, tier=tier, confidence=conf, consensus_motif=cons,
                              mismatch_rate=mm, max_mismatches_per_copy=maxmm,
-                             n_copies_evaluated=neval, strand=self.job._string(i, 4),
+                             n_copies_evaluated=neval, strand=self._str(i, 4),
                              percent_matches=pmatch, percent_indels=pindel, score=score,
                              composition=comp, entropy=ent, actual_sequence=act if act else None,
                              variations=var.split(";") if var else None)

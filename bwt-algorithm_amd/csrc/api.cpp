@@ -658,6 +658,7 @@ int bwtmi_job_load_fasta_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *path, i
         job->j.text_join();
         if (job->dev.bg_ctx && job->dev.bg_ctx != &c) ctx_wait(*job->dev.bg_ctx);   // it reads the old buffers
         use(c);
+        device_wake(c);
         DevLoad dl(c, job);
         load_fasta(job->j, path, flank_trim, 1, 0, &dl);
     });
@@ -709,6 +710,7 @@ int bwtmi_job_load_fasta_parts_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *p
         job->j.text_join();
         if (job->dev.bg_ctx && job->dev.bg_ctx != &c) ctx_wait(*job->dev.bg_ctx);
         use(c);
+        device_wake(c);
         DevLoad dl(c, job);
         fasta_load_parts(job->j, path, flank_trim, world, rank, blob, nwords, &dl);
     });
@@ -1235,26 +1237,54 @@ int bwtmi_job_get_records(bwtmi_job *job, int64_t *ints9, double *dbls5) {
     });
 }
 
-int64_t bwtmi_job_get_string(bwtmi_job *job, int64_t i, int which, char *buf, int64_t cap) {
-    if (!job || i < 0 || i >= (int64_t)job->j.final_recs.size()) return -1;
-    const Rec &r = job->j.final_recs[(size_t)i];
-    std::string s;
+namespace {
+// string `which` of a record (bwtmi_job_get_string); false for an unknown `which`
+bool rec_string(const bwtmi_job *job, const Rec &r, int which, std::string_view &s) {
     switch (which) {
-        case 0: case 1: s = r.motif; break;
-        case 2: s = r.variations; break;
-        case 3: {
+        case 0: case 1: s = r.motif; return true;
+        case 2: s = r.variations; return true;
+        case 3:
+            s = {};
             if (r.act_kind != ACT_NONE) {
                 const Contig &c = job->j.contigs[(size_t)r.chrom];
                 const char *p = (r.act_kind == ACT_FULL ? c.full.data() : c.trimmed()) + r.act_off;
-                s.assign(p, (size_t)r.act_len);
+                s = std::string_view(p, (size_t)r.act_len);
             }
-            break;
-        }
-        case 4: s.assign(1, r.strand); break;
-        default: return -1;
+            return true;
+        case 4: s = std::string_view(&r.strand, 1); return true;
+        default: return false;
     }
+}
+}  // namespace
+
+int64_t bwtmi_job_get_string(bwtmi_job *job, int64_t i, int which, char *buf, int64_t cap) {
+    if (!job || i < 0 || i >= (int64_t)job->j.final_recs.size()) return -1;
+    std::string_view s;
+    if (!rec_string(job, job->j.final_recs[(size_t)i], which, s)) return -1;
     if (buf && cap > 0) std::memcpy(buf, s.data(), std::min<size_t>((size_t)cap, s.size()));
     return (int64_t)s.size();
+}
+
+int64_t bwtmi_job_get_strings(bwtmi_job *job, int which, char *buf, int64_t cap, int64_t *offsets) {
+    if (!job || which < 0 || which > 4) return -1;
+    int64_t tot = 0;
+    std::string_view s;
+    const auto &recs = job->j.final_recs;
+    for (size_t i = 0; i < recs.size(); ++i) {
+        if (offsets) offsets[i] = tot;
+        rec_string(job, recs[i], which, s);
+        tot += (int64_t)s.size();
+    }
+    if (offsets) offsets[recs.size()] = tot;
+    if (buf && cap >= tot) {
+        char *w = buf;
+        for (const Rec &r : recs) {
+            rec_string(job, r, which, s);
+            std::memcpy(w, s.data(), s.size());
+            w += s.size();
+        }
+    }
+    return tot;
 }
 
 // record wire format for the multi-GPU gather: POD header + strings

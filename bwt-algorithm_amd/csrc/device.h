@@ -291,6 +291,12 @@ struct FastaDevPiece {
     char *dst;
 };
 void fasta_build_device(Ctx &c, const uint8_t *d_img, const FastaDevPiece *pieces, int64_t npieces);
+// An empty kernel queued (not waited for) ahead of host work that precedes the
+// first device work of a job: after tens of ms without device work the first
+// operation on the box pays ~5 ms (a 4-byte download 4.5-5.4 ms, the next
+// ones 0.03 ms; r04r), which then elapses behind the host work instead.
+// BWTMI_WAKE=0 disables.
+void device_wake(Ctx &c);
 
 // ----- strict scan (strict_scan.hip)
 struct ScanResult {

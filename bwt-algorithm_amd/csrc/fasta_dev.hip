@@ -15,6 +15,7 @@
 // Image bytes are read once (counts) + once (compact), the text written once.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -102,7 +103,16 @@ __global__ __launch_bounds__(kFaThreads) void k_fa_compact(const uint8_t *__rest
     }
 }
 
+__global__ void k_wake() {}
+
 }  // namespace
+
+void device_wake(Ctx &c) {
+    static const bool on = [] { const char *e = std::getenv("BWTMI_WAKE"); return !(e && *e == '0'); }();
+    if (!on) return;
+    k_wake<<<1, 64, 0, c.stream>>>();
+    HIPCHECK(hipGetLastError());
+}
 
 void fasta_build_device(Ctx &c, const uint8_t *d_img, const FastaDevPiece *pieces, int64_t npieces) {
     if (npieces <= 0) return;

@@ -28,6 +28,8 @@
 
 #include <algorithm>
 #include <array>
+#include <map>
+#include <memory>
 #include <set>
 #include <tuple>
 #include <unordered_map>
@@ -261,6 +263,40 @@ __global__ __launch_bounds__(256) void k_extend_cols(const uint8_t *__restrict__
     word[tid] = kExtSide;
     const unsigned long long k = atomicAdd(nside, 1ull);
     if ((int64_t)k < side_cap) side[k] = ExtSide{tid, left, right, ok ? 0u : 1u, 0u};
+}
+
+// Which seeds can still yield a record (A2-10's parallel pass): seed s with
+// unit L passes the copies / array-length test when the best extension over
+// its shifts cs = s - sh (sh < min(L, s + 1)) does.  Every such window covers
+// s, an entry's span is copies x L, and the best has the most copies, so the
+// test holds iff some window has copies >= thr[L - 1] (= max(min_copies,
+// ceil(min_array_length / L))).  Side entries (the host's own extension)
+// are flagged unconditionally, so the flags are a superset of the passing
+// seeds.  One bit per (L, s): bits[(L - 1) nw + s / 64], nw = ceil(n / 64).
+__global__ void k_probe_nop() {}
+
+struct SeedThr {
+    uint32_t c[kMaxUnit];
+};
+__global__ __launch_bounds__(256) void k_seed_flags(const uint32_t *__restrict__ word, int64_t n, int Lmax, SeedThr thr,
+                                                    uint64_t *__restrict__ bits, int64_t nw) {
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per = nw * 64;
+    const int L = (int)(tid / per) + 1;   // uniform over a wave: per is a multiple of 64
+    if (L > Lmax) return;
+    const int64_t s = tid - (int64_t)(L - 1) * per;
+    bool f = false;
+    if (s + L <= n) {
+        const uint32_t *w = word + (int64_t)(L - 1) * n;
+        const int64_t lo = s - min<int64_t>((int64_t)L, s + 1) + 1;
+        const uint32_t need = thr.c[L - 1];
+        for (int64_t cs = s; cs >= lo && !f; --cs) {
+            const uint32_t x = w[cs];
+            f = x == kExtSide || (x != kExtNone && 1u + (x & 0xffffu) + (x >> 16) >= need);
+        }
+    }
+    const uint64_t b = __ballot(f);
+    if ((threadIdx.x & 63) == 0) bits[tid >> 6] = b;
 }
 
 // -------------------------------------------------------------- Tier 1
@@ -621,8 +657,82 @@ static const std::vector<std::string> &motif_set(int k) {
     std::call_once(once[k], [k] { enumerate_motifs_build(k, sets[k]); });
     return sets[k];
 }
+// entropy_of of every motif of motif_set(k), in its order
+static const std::vector<double> &motif_entropy(int k) {
+    static std::vector<double> ent[11];
+    static std::once_flag once[11];
+    std::call_once(once[k], [k] {
+        for (const std::string &m : motif_set(k)) ent[k].push_back(entropy_of(m.data(), (int64_t)m.size()));
+    });
+    return ent[k];
+}
 
-inline char comp_base(char c) {
+// A2-10's motifs in the reference's order (k ascending, enumerate_motifs
+// order, entropy filter, bwt.py:2053-2095), each with its first locate
+// pattern; the patterns that go through locate (k > 8, or no k-mer table):
+// every rotation of the motif and of its reverse complement.  They depend on
+// the parameters only, so they are built once per process per parameter set.
+struct MotifTask {
+    int k;
+    const std::string *m;
+    size_t pat;
+};
+struct SiPlan {
+    std::vector<MotifTask> tasks;
+    size_t npats = 0;
+    std::string blob;
+    std::vector<int64_t> off;
+};
+char comp_base(char c);
+const SiPlan &si_plan(int kmin, int kend, double min_entropy, bool kmer_table) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, double, bool>, std::unique_ptr<SiPlan>> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    std::unique_ptr<SiPlan> &slot = cache[std::make_tuple(kmin, kend, min_entropy, kmer_table)];
+    if (slot) return *slot;
+    auto pl = std::make_unique<SiPlan>();
+    for (int k = kmin; k < kend; ++k) {
+        const bool use_hash = k <= 8 && kmer_table;
+        const std::vector<std::string> &ms = motif_set(k);
+        const std::vector<double> &me = motif_entropy(k);
+        for (size_t i = 0; i < ms.size(); ++i) {
+            if (me[i] < min_entropy) continue;   // bwt.py:2058-2060
+            pl->tasks.push_back({k, &ms[i], pl->npats});
+            if (!use_hash) pl->npats += 2 * (size_t)k;
+        }
+    }
+    pl->off.assign(pl->npats + 1, 0);
+    if (pl->npats) {
+        std::vector<size_t> at(pl->tasks.size(), 0);
+        size_t bytes = 0;
+        for (size_t ti = 0; ti < pl->tasks.size(); ++ti)
+            if (!(pl->tasks[ti].k <= 8 && kmer_table)) {
+                at[ti] = bytes;
+                bytes += 2 * (size_t)pl->tasks[ti].k * (size_t)pl->tasks[ti].k;
+            }
+        pl->blob.resize(bytes);
+        for (size_t ti = 0; ti < pl->tasks.size(); ++ti) {
+            const MotifTask &mt = pl->tasks[ti];
+            const int k = mt.k;
+            if (k <= 8 && kmer_table) continue;
+            const std::string &m = *mt.m;
+            char rc[16];
+            for (int x = 0; x < k; ++x) rc[x] = comp_base(m[(size_t)(k - 1 - x)]);
+            char *w = &pl->blob[at[ti]];
+            size_t q = mt.pat;
+            for (int r = 0; r < k; ++r) {
+                for (int x = 0; x < k; ++x) *w++ = m[(size_t)((r + x) % k)];
+                pl->off[++q] = (int64_t)(at[ti] + (size_t)(2 * r + 1) * (size_t)k);
+                for (int x = 0; x < k; ++x) *w++ = rc[(r + x) % k];
+                pl->off[++q] = (int64_t)(at[ti] + (size_t)(2 * r + 2) * (size_t)k);
+            }
+        }
+    }
+    slot = std::move(pl);
+    return *slot;
+}
+
+char comp_base(char c) {
     switch (c) {
         case 'A': return 'T';
         case 'T': return 'A';
@@ -776,9 +886,30 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
     auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     const int kmin = std::max(1, p.min_period), kend = std::min(p.max_short_motif + 1, 10);
     hipStream_t st = c.stream;
-    std::vector<uint8_t> text((size_t)n);
-    index_get_text(c, ix, text.data());
+    if (stats) {
+        HIPCHECK(hipStreamSynchronize(st));
+        std::fprintf(stderr, "    stream idle after %.1f ms\n", ms_since(T0));
+        uint32_t probe[4];
+        for (int r = 0; r < 2; ++r) {
+            auto a = clk::now();
+            k_probe_nop<<<1, 64, 0, st>>>();
+            HIPCHECK(hipStreamSynchronize(st));
+            std::fprintf(stderr, "    empty kernel %.3f ms\n", ms_since(a));
+            a = clk::now();
+            HIPCHECK(hipMemcpyAsync(probe, index_text_device(ix), 4, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipStreamSynchronize(st));
+            std::fprintf(stderr, "    4-byte download %.3f ms\n", ms_since(a));
+        }
+    }
+    // the text through the context's pinned staging buffer (a pageable
+    // download of 1 MB took 5-14 ms on the box)
+    HBuf &text_buf = c.host[1];
+    text_buf.ensure((size_t)n);
+    HIPCHECK(hipMemcpyAsync(text_buf.p, index_text_device(ix), (size_t)n, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    std::vector<uint8_t> text(text_buf.as<uint8_t>(), text_buf.as<uint8_t>() + n);
     const uint8_t *t = text.data();
+    if (stats) std::fprintf(stderr, "    text down %.1f ms\n", ms_since(T0));
 
     // extension table for every start and unit length 1..9 (k_extend_cols)
     const int Lmax = kMaxUnit;
@@ -790,6 +921,9 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
     ext_buf.ensure((size_t)tot * 4);
     uint32_t *const ext_word = ext_buf.as<uint32_t>();
     std::unordered_map<int64_t, std::array<int64_t, 3>> ext_side;   // q -> (start, end, copies)
+    const int64_t nw = (n + 63) / 64;
+    std::vector<uint64_t> seed_bits((size_t)Lmax * (size_t)nw);   // k_seed_flags
+    c.slot[S_IDX2].ensure(seed_bits.size() * 8);
     for (int64_t cap = 1 << 16;;) {
         c.slot[S_IDX1].ensure((size_t)cap * sizeof(ExtSide));
         HIPCHECK(hipMemsetAsync(c.slot[S_COUNTS].p, 0, 8, st));
@@ -806,6 +940,16 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
         }
         std::vector<ExtSide> side((size_t)ns);
         if (stats) std::fprintf(stderr, "    text + extension kernel %.1f ms\n", ms_since(T0));
+        SeedThr thr{};
+        for (int L = 1; L <= Lmax; ++L) {
+            const int64_t by_len = (std::max<int64_t>(0, p.min_array_length) + L - 1) / L;
+            thr.c[L - 1] = (uint32_t)std::min<int64_t>(0xffffffffLL, std::max<int64_t>({(int64_t)0, (int64_t)p.min_copies, by_len}));
+        }
+        KLAUNCH("k_seed_flags", 4.0 * (double)tot + (double)Lmax * (double)nw * 8.0, k_seed_flags,
+                dim3((unsigned)(((int64_t)Lmax * nw * 64 + kB - 1) / kB)), dim3(kB), 0, st, c.slot[S_IDX0].as<uint32_t>(), n,
+                Lmax, thr, c.slot[S_IDX2].as<uint64_t>(), nw);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemcpyAsync(seed_bits.data(), c.slot[S_IDX2].p, seed_bits.size() * 8, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipMemcpyAsync(ext_word, c.slot[S_IDX0].p, (size_t)tot * 4, hipMemcpyDeviceToHost, st));
         if (ns) HIPCHECK(hipMemcpyAsync(side.data(), c.slot[S_IDX1].p, (size_t)ns * sizeof(ExtSide),
                                         hipMemcpyDeviceToHost, st));
@@ -851,54 +995,12 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
         index_get_kmer(c, ix, koff.data(), kpos.data());
         if (stats) std::fprintf(stderr, "    kmer table down %.1f ms\n", ms_since(T0) - t_ext);
     }
-    // The motifs in the reference's order (k ascending, enumerate_motifs order,
-    // entropy filter, bwt.py:2053-2095), each with its first locate pattern.
-    struct MotifTask {
-        int k;
-        const std::string *m;
-        size_t pat;
-    };
-    std::vector<MotifTask> tasks;
-    size_t npats = 0;
-    for (int k = kmin; k < kend; ++k) {
-        const bool use_hash = k <= 8 && kcount > 0;
-        for (auto &m : motif_set(k)) {
-            if (entropy_of(m.data(), k) < p.min_entropy) continue;   // bwt.py:2058-2060
-            tasks.push_back({k, &m, npats});
-            if (!use_hash) npats += 2 * (size_t)k;
-        }
-    }
+    const SiPlan &plan = si_plan(kmin, kend, p.min_entropy, kcount > 0);
+    const std::vector<MotifTask> &tasks = plan.tasks;
+    const size_t npats = plan.npats;
+    const std::string &blob = plan.blob;
+    const std::vector<int64_t> &off = plan.off;
     const int nt = std::max(1, host_cpu_budget(nullptr, nullptr));
-    // patterns that go through locate: every rotation of the motif and of its
-    // reverse complement, each motif's 2k patterns written in place (in parallel)
-    std::string blob;
-    std::vector<int64_t> off(npats + 1, 0);
-    if (npats) {
-        std::vector<size_t> at(tasks.size(), 0);
-        size_t bytes = 0;
-        for (size_t ti = 0; ti < tasks.size(); ++ti)
-            if (!(tasks[ti].k <= 8 && kcount > 0)) {
-                at[ti] = bytes;
-                bytes += 2 * (size_t)tasks[ti].k * (size_t)tasks[ti].k;
-            }
-        blob.resize(bytes);
-        run_tasks((int64_t)tasks.size(), nt, [&](int64_t ti) {
-            const MotifTask &mt = tasks[(size_t)ti];
-            const int k = mt.k;
-            if (k <= 8 && kcount > 0) return;
-            const std::string &m = *mt.m;
-            char rc[16];
-            for (int x = 0; x < k; ++x) rc[x] = comp_base(m[(size_t)(k - 1 - x)]);
-            char *w = &blob[at[(size_t)ti]];
-            size_t q = mt.pat;
-            for (int r = 0; r < k; ++r) {
-                for (int x = 0; x < k; ++x) *w++ = m[(size_t)((r + x) % k)];
-                off[++q] = (int64_t)(at[(size_t)ti] + (size_t)(2 * r + 1) * (size_t)k);
-                for (int x = 0; x < k; ++x) *w++ = rc[(r + x) % k];
-                off[++q] = (int64_t)(at[(size_t)ti] + (size_t)(2 * r + 2) * (size_t)k);
-            }
-        });
-    }
     std::vector<int64_t> spep;
     std::vector<int32_t> sa;
     if (npats) {
@@ -916,31 +1018,65 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
             seen[(size_t)x] = 1;
     const std::string seq((const char *)t, (size_t)n);
 
-    // seed positions of a motif: every rotation of it and of its reverse
-    // complement, through the k-mer table or the FM interval's SA rows; sorted, unique
-    auto seeds_of = [&](const MotifTask &mt, std::vector<int64_t> &positions) {
+    // Seed positions of a motif: every rotation of it and of its reverse
+    // complement, through the k-mer table (the reference's short-k lookup) or
+    // the FM interval's SA rows -- restricted to the seeds k_seed_flags marks,
+    // sorted.  Returns the number of unique seeds (flagged or not): distinct
+    // 8-mer keys hold disjoint positions and distinct patterns of one length
+    // disjoint SA intervals, so the count is a sum over the distinct ones.
+    // A seed is kept when it is flagged for some unit length in [1, lmax] (the
+    // parallel pass asks for exactly k: lmin = k).
+    auto seeds_flagged = [&](const MotifTask &mt, int lmin, int lmax, std::vector<int64_t> &positions) -> int64_t {
         positions.clear();
         const int k = mt.k;
+        auto flagged = [&](int64_t s) {
+            uint64_t f = 0;
+            for (int L = lmin; L <= lmax; ++L) f |= seed_bits[(size_t)(L - 1) * (size_t)nw + (size_t)(s >> 6)];
+            return (f >> (s & 63)) & 1u;
+        };
         const std::string &m = *mt.m;
-        std::string rc(m.rbegin(), m.rend());
-        for (auto &ch : rc) ch = comp_base(ch);
+        int64_t total = 0;
         if (k <= 8 && kcount > 0) {
-            for (int r = 0; r < k; ++r)
-                for (const std::string &rot : {m.substr((size_t)r) + m.substr(0, (size_t)r),
-                                               rc.substr((size_t)r) + rc.substr(0, (size_t)r)}) {
-                    int64_t w = 0;
-                    for (char ch : rot) w = (w << 2) | (ch == 'C' ? 1 : ch == 'G' ? 2 : ch == 'T' ? 3 : 0);
-                    for (int64_t q = koff[(size_t)w]; q < koff[(size_t)w + 1]; ++q) positions.push_back(kpos[(size_t)q]);
-                }
+            int64_t keys[16];
+            int nk = 0;
+            int64_t fw = 0, rw = 0;   // packed motif and reverse complement
+            for (int x = 0; x < k; ++x) {
+                const char ch = m[(size_t)x];
+                fw = (fw << 2) | (ch == 'C' ? 1 : ch == 'G' ? 2 : ch == 'T' ? 3 : 0);
+                const char rc = comp_base(m[(size_t)(k - 1 - x)]);
+                rw = (rw << 2) | (rc == 'C' ? 1 : rc == 'G' ? 2 : rc == 'T' ? 3 : 0);
+            }
+            const int64_t mask = (int64_t(1) << (2 * k)) - 1;
+            for (int r = 0; r < k; ++r) {   // rotation r: the word rotated left by r bases
+                const int sh = 2 * (k - r);
+                keys[nk++] = r ? (((fw << (2 * r)) | (fw >> sh)) & mask) : fw;
+                keys[nk++] = r ? (((rw << (2 * r)) | (rw >> sh)) & mask) : rw;
+            }
+            std::sort(keys, keys + nk);
+            nk = (int)(std::unique(keys, keys + nk) - keys);
+            for (int i = 0; i < nk; ++i) {
+                const int64_t a = koff[(size_t)keys[i]], b = koff[(size_t)keys[i] + 1];
+                total += b - a;
+                for (int64_t q = a; q < b; ++q)
+                    if (flagged(kpos[(size_t)q])) positions.push_back(kpos[(size_t)q]);
+            }
         } else {
+            std::pair<int64_t, int64_t> iv[2 * kMaxUnit];
+            int ni = 0;
             for (int r = 0; r < 2 * k; ++r) {
                 const int64_t sp = spep[2 * (mt.pat + (size_t)r)], ep = spep[2 * (mt.pat + (size_t)r) + 1];
-                if (sp < 0) continue;
-                for (int64_t q = sp; q <= ep; ++q) positions.push_back(sa[(size_t)q]);
+                if (sp >= 0) iv[ni++] = {sp, ep};
+            }
+            std::sort(iv, iv + ni);
+            ni = (int)(std::unique(iv, iv + ni) - iv);
+            for (int i = 0; i < ni; ++i) {
+                total += iv[i].second - iv[i].first + 1;
+                for (int64_t q = iv[i].first; q <= iv[i].second; ++q)
+                    if (flagged(sa[(size_t)q])) positions.push_back(sa[(size_t)q]);
             }
         }
         std::sort(positions.begin(), positions.end());
-        positions.erase(std::unique(positions.begin(), positions.end()), positions.end());
+        return total;
     };
     // the best extension through seed over the shifts whose start is not seen
     // (seen == nullptr: all shifts) -- most copies, then the leftmost start
@@ -1011,9 +1147,9 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
     run_tasks((int64_t)tasks.size(), nt, [&](int64_t ti) {
         thread_local std::vector<int64_t> positions;
         const MotifTask &mt = tasks[(size_t)ti];
-        seeds_of(mt, positions);
+        const int64_t total = seeds_flagged(mt, mt.k, mt.k, positions);
         TaskOut &o = tout[(size_t)ti];
-        if ((int64_t)positions.size() < p.min_copies || !p.allow_mismatches) return;
+        if (total < p.min_copies || !p.allow_mismatches) return;
         o.skip = false;
         for (int64_t seed : positions) {
             if (seed + mt.k > n) continue;
@@ -1100,7 +1236,9 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
             // candidates of the parallel pass (found with the motif's own length)
             // no longer cover them, so the walk goes on over all of its seeds
             if (motif_len != len_before && !full) {
-                seeds_of(mt, all);
+                // the motif length only shrinks (a primitive period of the consensus),
+                // and a seed that can pass with some length is flagged for it
+                seeds_flagged(mt, 1, (int)motif_len, all);
                 all.erase(all.begin(), std::upper_bound(all.begin(), all.end(), seed));
                 full = true;
                 ++nfull;
@@ -1464,14 +1602,13 @@ void simple_scan_device(Ctx &c, DeviceIndex *ix, const LibParams &P, const std::
         }
         // device batch
         const int64_t nr = (int64_t)req_w.size();
-        c.slot[S_IDX0].ensure((size_t)nt + 64);
         c.slot[S_IDX1].ensure((size_t)nr * 16);
         c.slot[S_IDX2].ensure((size_t)nr * 40);
         c.slot[S_IDX3].ensure((size_t)nr);
-        HIPCHECK(hipMemcpyAsync(c.slot[S_IDX0].p, t, (size_t)nt, hipMemcpyHostToDevice, st));
         HIPCHECK(hipMemcpyAsync(c.slot[S_IDX1].p, req.data(), (size_t)nr * 16, hipMemcpyHostToDevice, st));
+        // the index's own text (the bytes downloaded above), not a fresh upload per batch
         KLAUNCH("k_simple_extend", 0.0, k_simple_extend, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, st,
-                           c.slot[S_IDX0].as<uint8_t>(), n, c.slot[S_IDX1].as<int64_t>(), nr,
+                           index_text_device(ix), n, c.slot[S_IDX1].as<int64_t>(), nr,
                            c.slot[S_IDX2].as<int64_t>(), c.slot[S_IDX3].as<uint8_t>());
         HIPCHECK(hipGetLastError());
         std::vector<int64_t> res((size_t)nr * 5);

@@ -229,6 +229,27 @@ int64_t smallest_period(const char *s, int64_t n) {   // bwt.py:1125-1133
 
 double entropy_of(const char *s, int64_t n) {         // bwt.py:730-745
     if (n <= 0) return 0.0;
+    if (n <= 64) {   // short motifs: a first-seen list instead of clearing 256 counters per call
+        unsigned char sym[64];
+        int64_t c[64];
+        int m = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            const unsigned char ch = (unsigned char)s[i];
+            int j = 0;
+            while (j < m && sym[j] != ch) ++j;
+            if (j == m) {
+                sym[m] = ch;
+                c[m++] = 0;
+            }
+            ++c[j];
+        }
+        double e = 0.0;
+        for (int k = 0; k < m; ++k) {
+            double p = (double)c[k] / (double)n;
+            e -= p * std::log2(p);
+        }
+        return e;
+    }
     int64_t cnt[256] = {0};
     unsigned char order[256];
     int nord = 0;

@@ -225,6 +225,11 @@ int bwtmi_job_get_records(bwtmi_job *job, int64_t *ints9, double *dbls5);
 /* strings of record i: which = 0 motif, 1 consensus, 2 variations(';'-joined),
  * 3 actual_sequence, 4 strand; returns length, copies up to cap bytes */
 int64_t bwtmi_job_get_string(bwtmi_job *job, int64_t i, int which, char *buf, int64_t cap);
+/* string `which` of every record, concatenated: offsets[0..count] (count + 1
+ * entries, when offsets != NULL) and the bytes into buf when buf != NULL and
+ * cap >= the total; returns the total byte count (-1: bad argument).  One
+ * call per column for the Python record view instead of one per record. */
+int64_t bwtmi_job_get_strings(bwtmi_job *job, int which, char *buf, int64_t cap, int64_t *offsets);
 /* serialise final records for a gather to another rank; import appends them */
 int bwtmi_job_export(bwtmi_job *job, uint8_t **buf, int64_t *len);
 int bwtmi_job_import(bwtmi_job *job, const uint8_t *buf, int64_t len);

@@ -245,6 +245,23 @@ def test_worker_exception_returns_an_error(built_lib, monkeypatch, task):
     assert run() == want
 
 
+def test_record_string_columns_match_per_record_getter(built_lib):
+    """The record view's string columns (bwtmi_job_get_strings, one call per
+    column) hold what the per-record getter returns, for every field."""
+    from bwtmi import synth
+    from bwtmi.records import Job
+    seq = synth.generate_contig(200_000, 6, 0.02)
+    j = Job(min_copies=3, show_progress=True, threads=2)
+    j.add_contig("c", seq, 30, 30)
+    j.add_hits(0, oracle.strict_scan(seq[30:len(seq) - 30], 1, 1000, 0, 3))
+    j.postprocess()
+    recs = j.records()
+    assert len(recs) > 100
+    for which in range(5):
+        assert [recs._str(i, which) for i in range(len(recs))] == [j._string(i, which) for i in range(len(recs))]
+    assert recs[len(recs) - 1].motif == j._string(len(recs) - 1, 0)
+
+
 def test_save_results_over_plain_record_lists(golden_dir, tmp_path, built_lib):
     """save_results(list_of_records) (bwt.py:4141-4198) with a copy of the
     records and with a filtered subset, in all five formats, against the
