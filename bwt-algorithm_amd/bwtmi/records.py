@@ -9,6 +9,7 @@ them natively (bwt.py:4141-4198).
 from __future__ import annotations
 
 import ctypes as C
+import functools
 import math
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
@@ -75,12 +76,18 @@ class TandemRepeat:
 
 
 def _composition(s: str) -> Dict[str, float]:
+    return dict(_composition_of(s))     # a record's own dict (callers may change it)
+
+
+@functools.lru_cache(maxsize=1 << 16)   # motifs recur across records
+def _composition_of(s: str) -> Dict[str, float]:
     if not s:
         return {"A": 0.0, "C": 0.0, "G": 0.0, "T": 0.0}
     u = s.upper()
     return {b: (u.count(b) / len(s)) * 100.0 for b in "ACGT"}
 
 
+@functools.lru_cache(maxsize=1 << 16)
 def _entropy(s: str) -> float:
     if not s:
         return 0.0

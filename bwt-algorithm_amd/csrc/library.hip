@@ -273,8 +273,6 @@ __global__ __launch_bounds__(256) void k_extend_cols(const uint8_t *__restrict__
 // ceil(min_array_length / L))).  Side entries (the host's own extension)
 // are flagged unconditionally, so the flags are a superset of the passing
 // seeds.  One bit per (L, s): bits[(L - 1) nw + s / 64], nw = ceil(n / 64).
-__global__ void k_probe_nop() {}
-
 struct SeedThr {
     uint32_t c[kMaxUnit];
 };
@@ -886,23 +884,7 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
     auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     const int kmin = std::max(1, p.min_period), kend = std::min(p.max_short_motif + 1, 10);
     hipStream_t st = c.stream;
-    if (stats) {
-        HIPCHECK(hipStreamSynchronize(st));
-        std::fprintf(stderr, "    stream idle after %.1f ms\n", ms_since(T0));
-        uint32_t probe[4];
-        for (int r = 0; r < 2; ++r) {
-            auto a = clk::now();
-            k_probe_nop<<<1, 64, 0, st>>>();
-            HIPCHECK(hipStreamSynchronize(st));
-            std::fprintf(stderr, "    empty kernel %.3f ms\n", ms_since(a));
-            a = clk::now();
-            HIPCHECK(hipMemcpyAsync(probe, index_text_device(ix), 4, hipMemcpyDeviceToHost, st));
-            HIPCHECK(hipStreamSynchronize(st));
-            std::fprintf(stderr, "    4-byte download %.3f ms\n", ms_since(a));
-        }
-    }
-    // the text through the context's pinned staging buffer (a pageable
-    // download of 1 MB took 5-14 ms on the box)
+    // the text through the context's pinned staging buffer
     HBuf &text_buf = c.host[1];
     text_buf.ensure((size_t)n);
     HIPCHECK(hipMemcpyAsync(text_buf.p, index_text_device(ix), (size_t)n, hipMemcpyDeviceToHost, st));
@@ -1423,20 +1405,34 @@ inline int64_t max_mm_for_array_host(int64_t L, int64_t c) {
     return std::max<int64_t>(1, (int64_t)std::ceil(f * (double)tot));
 }
 
-// _extend_with_mismatches (bwt.py:2392-2498), exact, any alphabet
+// _extend_with_mismatches (bwt.py:2392-2498), exact, any alphabet.  Each
+// column keeps the symbols it has seen with their counts (a handful); the
+// majority is the largest count, the smallest symbol on ties (the reference's
+// first maximum over symbols in byte order).
 SimRes simple_extend_host(const uint8_t *t, int64_t n, int64_t s0, int64_t p, bool allow) {
-    std::vector<std::array<uint32_t, 256>> cnt((size_t)p);
-    for (auto &a : cnt) a.fill(0);
-    std::string cons((const char *)t + s0, (size_t)p);
-    for (int64_t c = 0; c < p; ++c) ++cnt[(size_t)c][t[s0 + c]];
-    int64_t start = s0, end = s0 + p, copies = 1;
-    auto major = [&](int64_t c, uint32_t &mx) {
-        mx = 0;
-        int sym = 0;
-        for (int b = 0; b < 256; ++b)
-            if (cnt[(size_t)c][(size_t)b] > mx) { mx = cnt[(size_t)c][(size_t)b]; sym = b; }
-        return (char)sym;
+    struct Col {
+        std::vector<std::pair<uint8_t, uint32_t>> v;
+        void add(uint8_t b, int d) {
+            for (auto &e : v)
+                if (e.first == b) { e.second = (uint32_t)((int64_t)e.second + d); return; }
+            v.push_back({b, (uint32_t)d});
+        }
+        char major(uint32_t &mx) const {
+            mx = 0;
+            int sym = 0;
+            for (const auto &e : v)
+                if (e.second > mx || (e.second == mx && e.second > 0 && e.first < sym)) { mx = e.second; sym = e.first; }
+            return (char)sym;
+        }
     };
+    thread_local std::vector<Col> cnt;
+    if ((int64_t)cnt.size() < p) cnt.resize((size_t)p);
+    for (int64_t c = 0; c < p; ++c) {
+        cnt[(size_t)c].v.clear();
+        cnt[(size_t)c].add(t[s0 + c], 1);
+    }
+    std::string cons((const char *)t + s0, (size_t)p);
+    int64_t start = s0, end = s0 + p, copies = 1;
     for (int dir = 0; dir < 2; ++dir) {
         for (;;) {
             if (dir == 0 ? (end + p > n) : (start - p < 0)) break;
@@ -1444,9 +1440,9 @@ SimRes simple_extend_host(const uint8_t *t, int64_t n, int64_t s0, int64_t p, bo
             const int64_t tc = copies + 1;
             int64_t mm = 0;
             for (int64_t c = 0; c < p; ++c) {
-                ++cnt[(size_t)c][t[at + c]];
+                cnt[(size_t)c].add(t[at + c], 1);
                 uint32_t mx;
-                major(c, mx);
+                cnt[(size_t)c].major(mx);
                 mm += tc - mx;
             }
             if (mm <= (allow ? max_mm_for_array_host(p, tc) : 0)) {
@@ -1454,9 +1450,9 @@ SimRes simple_extend_host(const uint8_t *t, int64_t n, int64_t s0, int64_t p, bo
                 if (dir == 0) end += p;
                 else start -= p;
                 uint32_t mx;
-                for (int64_t c = 0; c < p; ++c) cons[(size_t)c] = major(c, mx);
+                for (int64_t c = 0; c < p; ++c) cons[(size_t)c] = cnt[(size_t)c].major(mx);
             } else {
-                for (int64_t c = 0; c < p; ++c) --cnt[(size_t)c][t[at + c]];
+                for (int64_t c = 0; c < p; ++c) cnt[(size_t)c].add(t[at + c], -1);
                 break;
             }
         }
@@ -1472,6 +1468,22 @@ struct SimWalk {
     bool done = false;
     std::vector<int64_t> accepts;   // positions i whose first extension was accepted, in walk order
     std::vector<int64_t> acc_iter;  // iteration number (1-based, within the walk) of each
+    std::vector<SimRes> acc_res;    // and its first extension
+    // first extensions of the current look-ahead, ascending positions: the walk
+    // only moves forward, so a cursor replaces a map
+    std::vector<int64_t> look_pos;
+    std::vector<SimRes> look_res;
+    size_t cur = 0;
+    // the look-ahead's grid: look_start + k step <= look_last, every position
+    // of it tested -- on it, "needs an extension" is membership in look_pos
+    int64_t look_start = -1, look_last = -2, look_len = 0;
+    bool on_grid(int64_t pos, int64_t step) const {
+        return pos >= look_start && pos <= look_last && (pos - look_start) % step == 0;
+    }
+    const SimRes *find(int64_t pos) {
+        while (cur < look_pos.size() && look_pos[cur] < pos) ++cur;
+        return cur < look_pos.size() && look_pos[cur] == pos ? &look_res[cur] : nullptr;
+    }
 };
 }  // namespace
 
@@ -1525,40 +1537,70 @@ void simple_scan_device(Ctx &c, DeviceIndex *ix, const LibParams &P, const std::
         return !(entropy_of((const char *)t + i, p) < P.min_entropy);
     };
     const bool allow_all = P.allow_mismatches != 0;
-    std::vector<std::unordered_map<int64_t, SimRes>> ext(walks.size());
     constexpr int kLook = 512;   // look-ahead positions per walk and round
     hipStream_t st = c.stream;
+    using clk = std::chrono::steady_clock;
+    const bool stats = [] { const char *e = std::getenv("BWTMI_STATS"); return e && *e == '1'; }();
+    double t_host = 0, t_dev = 0;
+    int64_t rounds = 0, nreq = 0;
+    auto T0 = clk::now();
+    std::vector<int64_t> req;        // (i, p | allow << 16)
+    std::vector<int32_t> req_w;
+    std::vector<std::vector<int64_t>> wreq(walks.size());   // each walk's look-ahead requests
+    std::vector<int64_t> lower(walks.size(), 0);
+    const int nthr = std::max(1, host_cpu_budget(nullptr, nullptr));
     for (;;) {
-        // advance every walk until it needs an unknown extension; collect look-ahead requests
-        std::vector<int64_t> req;        // (i, p | allow << 16)
-        std::vector<int32_t> req_w;
-        int64_t lower = 0;               // iterations the earlier walks (period order) take at least
-        for (size_t wi = 0; wi < walks.size(); ++wi) {
+        // advance every walk until it needs an unknown extension; collect look-ahead
+        // requests.  The walks run in parallel; each takes as the iterations of the
+        // earlier walks (period order) their counts after the last round -- a lower
+        // bound, so a walk stops at the global cap no earlier than in a serial pass
+        // and the replay (which applies the cap exactly) sees the same accepts.
+        for (size_t wi = 1; wi < walks.size(); ++wi) lower[wi] = lower[wi - 1] + walks[wi - 1].iters;
+        run_tasks((int64_t)walks.size(), nthr, [&](int64_t wk) {
+            const size_t wi = (size_t)wk;
             SimWalk &w = walks[wi];
+            std::vector<int64_t> &wr = wreq[wi];
+            wr.clear();
             const int64_t p = w.p;
             const bool allow = allow_all && p <= 64;
             while (!w.done) {
                 if (w.i + 2 * p > n) { w.done = true; break; }
-                if (lower + w.iters + 1 > kMaxIter) { w.done = true; break; }   // beyond the global cap
+                if (lower[wi] + w.iters + 1 > kMaxIter) { w.done = true; break; }   // beyond the global cap
                 const int64_t i = w.i;
-                if (!needs_ext(i, p)) { ++w.iters; w.i += step; continue; }
-                auto it = ext[wi].find(i);
-                if (it == ext[wi].end() && p > kSimMaxP) {            // wider than a wave's columns
-                    ext[wi][i] = simple_extend_host(t, n, i, p, allow);
-                    it = ext[wi].find(i);
+                const SimRes *rp;
+                if (w.on_grid(i, step)) {   // tested when the look-ahead was built
+                    rp = w.find(i);
+                    if (!rp) { ++w.iters; w.i += step; continue; }
+                } else {
+                    if (!needs_ext(i, p)) { ++w.iters; w.i += step; continue; }
+                    rp = w.find(i);
                 }
-                if (it == ext[wi].end()) {
-                    for (int64_t q = 0, j = i; q < kLook && j + 2 * p <= n; j += step) {
-                        if (!needs_ext(j, p) || ext[wi].count(j)) continue;
-                        req.push_back(j);
-                        req.push_back(p | (allow ? (1 << 16) : 0));
-                        req_w.push_back((int32_t)wi);
+                SimRes wide;
+                if (!rp && p > kSimMaxP) {            // wider than a wave's columns
+                    wide = simple_extend_host(t, n, i, p, allow);
+                    rp = &wide;
+                }
+                if (!rp) {   // a new look-ahead from i (positions of the old one are behind or off this grid)
+                    // its length adapts: twice what the walk used of the last one
+                    // (a walk that keeps jumping after accepts wastes little), 32..kLook
+                    const int64_t used = (int64_t)w.cur;
+                    w.look_len = w.look_len == 0 ? kLook : std::max<int64_t>(32, std::min<int64_t>(kLook, 2 * used));
+                    w.look_pos.clear();
+                    w.look_res.clear();
+                    w.cur = 0;
+                    w.look_start = i;
+                    int64_t j = i, q = 0;
+                    for (; q < w.look_len && j + 2 * p <= n; j += step) {
+                        if (!needs_ext(j, p)) continue;
+                        wr.push_back(j);
+                        w.look_pos.push_back(j);
                         ++q;
                     }
+                    w.look_last = j - step;
                     break;
                 }
                 ++w.iters;
-                const SimRes &r = it->second;
+                const SimRes &r = *rp;
                 const int64_t alen = r.ae - r.as;
                 bool acc = false;
                 if (alen >= P.min_array_length) {
@@ -1570,6 +1612,7 @@ void simple_scan_device(Ctx &c, DeviceIndex *ix, const LibParams &P, const std::
                 if (!acc) { w.i += step; continue; }
                 w.accepts.push_back(i);
                 w.acc_iter.push_back(w.iters);
+                w.acc_res.push_back(r);
                 // the walk resumes at the (second-extension) array end, decided on the host
                 const int64_t fs = r.fs;
                 const int64_t prim = smallest_period((const char *)t + fs, p);
@@ -1593,40 +1636,62 @@ void simple_scan_device(Ctx &c, DeviceIndex *ix, const LibParams &P, const std::
                 }
                 w.i = ae;
             }
-            lower += w.iters;
+        });
+        req.clear();
+        req_w.clear();
+        for (size_t wi = 0; wi < walks.size(); ++wi) {
+            const int64_t pw = walks[wi].p | (allow_all && walks[wi].p <= 64 ? (1 << 16) : 0);
+            for (int64_t j : wreq[wi]) {
+                req.push_back(j);
+                req.push_back(pw);
+                req_w.push_back((int32_t)wi);
+            }
         }
+        auto T1 = clk::now();
+        t_host += std::chrono::duration<double, std::milli>(T1 - T0).count();
+        T0 = T1;
         if (req.empty()) {
             for (auto &w : walks)
                 if (!w.done) fail(BWTMI_E_STATE, "simple scan: walk of period %lld stalled", (long long)w.p);
             break;
         }
-        // device batch
+        // device batch through the context's pinned staging buffer: requests
+        // in, (5 words + overflow flag) per request out
         const int64_t nr = (int64_t)req_w.size();
+        ++rounds;
+        nreq += nr;
         c.slot[S_IDX1].ensure((size_t)nr * 16);
-        c.slot[S_IDX2].ensure((size_t)nr * 40);
-        c.slot[S_IDX3].ensure((size_t)nr);
-        HIPCHECK(hipMemcpyAsync(c.slot[S_IDX1].p, req.data(), (size_t)nr * 16, hipMemcpyHostToDevice, st));
+        c.slot[S_IDX2].ensure((size_t)nr * 48);
+        HBuf &hb = c.host[0];
+        hb.ensure((size_t)nr * 48);
+        std::memcpy(hb.p, req.data(), (size_t)nr * 16);
+        HIPCHECK(hipMemcpyAsync(c.slot[S_IDX1].p, hb.p, (size_t)nr * 16, hipMemcpyHostToDevice, st));
+        int64_t *d_res = c.slot[S_IDX2].as<int64_t>();
+        uint8_t *d_ovf = reinterpret_cast<uint8_t *>(d_res + 5 * nr);
         // the index's own text (the bytes downloaded above), not a fresh upload per batch
         KLAUNCH("k_simple_extend", 0.0, k_simple_extend, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, st,
-                           index_text_device(ix), n, c.slot[S_IDX1].as<int64_t>(), nr,
-                           c.slot[S_IDX2].as<int64_t>(), c.slot[S_IDX3].as<uint8_t>());
+                index_text_device(ix), n, c.slot[S_IDX1].as<int64_t>(), nr, d_res, d_ovf);
         HIPCHECK(hipGetLastError());
-        std::vector<int64_t> res((size_t)nr * 5);
-        std::vector<uint8_t> ovf((size_t)nr);
-        HIPCHECK(hipMemcpyAsync(res.data(), c.slot[S_IDX2].p, (size_t)nr * 40, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipMemcpyAsync(ovf.data(), c.slot[S_IDX3].p, (size_t)nr, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(hb.p, d_res, (size_t)nr * 41, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
+        const int64_t *res = hb.as<int64_t>();
+        const uint8_t *ovf = reinterpret_cast<const uint8_t *>(res + 5 * nr);
         for (int64_t q = 0; q < nr; ++q) {
             const int64_t i = req[(size_t)(2 * q)], pw = req[(size_t)(2 * q + 1)];
             SimRes r;
-            if (ovf[(size_t)q])
+            if (ovf[q])
                 r = simple_extend_host(t, n, i, pw & 0xFFFF, (pw >> 16) & 1);
             else
-                r = SimRes{res[(size_t)(5 * q)], res[(size_t)(5 * q + 1)], res[(size_t)(5 * q + 2)],
-                           res[(size_t)(5 * q + 3)], res[(size_t)(5 * q + 4)]};
-            ext[(size_t)req_w[(size_t)q]][i] = r;
+                r = SimRes{res[5 * q], res[5 * q + 1], res[5 * q + 2], res[5 * q + 3], res[5 * q + 4]};
+            walks[(size_t)req_w[(size_t)q]].look_res.push_back(r);   // requests of a walk: ascending, in order
         }
+        T1 = clk::now();
+        t_dev += std::chrono::duration<double, std::milli>(T1 - T0).count();
+        T0 = T1;
     }
+    if (stats)
+        std::fprintf(stderr, "  simple scan: %lld walks, %lld rounds, %lld requests, host walk %.1f ms, device batches %.1f ms\n",
+                     (long long)walks.size(), (long long)rounds, (long long)nreq, t_host, t_dev);
     // replay in period order under the global cap: records of the accepted positions
     std::set<std::tuple<int64_t, int64_t, std::string>> seen;
     const std::string seq((const char *)t, (size_t)nt);
@@ -1637,7 +1702,7 @@ void simple_scan_device(Ctx &c, DeviceIndex *ix, const LibParams &P, const std::
         const int64_t p = w.p;
         for (size_t a = 0; a < w.accepts.size(); ++a) {
             if (cum + w.acc_iter[a] > kMaxIter) break;
-            const SimRes &r = ext[wi].at(w.accepts[a]);
+            const SimRes &r = w.acc_res[a];
             const int64_t prim = smallest_period((const char *)t + r.fs, p);
             int64_t pe = prim < p ? prim : p;
             const SimRes r2 = simple_extend_host(t, n, r.fs, pe, allow_all && pe <= 64);
@@ -1688,6 +1753,9 @@ void simple_scan_device(Ctx &c, DeviceIndex *ix, const LibParams &P, const std::
         cum += w.iters;
         if (cum >= kMaxIter) break;
     }
+    if (stats)
+        std::fprintf(stderr, "  simple scan: replay %.1f ms (%zu records)\n",
+                     std::chrono::duration<double, std::milli>(clk::now() - T0).count(), out.size());
 }
 
 }  // namespace bwtmi

@@ -113,19 +113,25 @@ uint64_t min_rot2(uint64_t x, int64_t n) {
     return best;
 }
 
-uint64_t canon2(uint64_t x, int64_t n) {
-    static const std::vector<uint16_t> *tab = [] {   // [n][x], n = 1..8
-        auto *t = new std::vector<uint16_t>[9];
+// [n][x], n = 1..8: the canonical word (low 16 bits) and whether the forward
+// strand holds it (bit 16: min_rot2(x) <= min_rot2(rc2(x)))
+static const std::vector<uint32_t> *canon_table() {
+    static const std::vector<uint32_t> *tab = [] {
+        auto *t = new std::vector<uint32_t>[9];
         for (int k = 1; k <= 8; ++k) {
             t[k].resize((size_t)1 << (2 * k));
             for (uint64_t v = 0; v < t[k].size(); ++v) {
                 const uint64_t f = min_rot2(v, k), r = min_rot2(rc2(v, k), k);
-                t[k][v] = (uint16_t)(f < r ? f : r);
+                t[k][v] = (uint32_t)(f < r ? f : r) | (f <= r ? 1u << 16 : 0u);
             }
         }
         return t;
     }();
-    if (n >= 1 && n <= 8) return tab[n][(size_t)x];
+    return tab;
+}
+
+uint64_t canon2(uint64_t x, int64_t n) {
+    if (n >= 1 && n <= 8) return canon_table()[n][(size_t)x] & 0xffffu;
     const uint64_t f = min_rot2(x, n), r = min_rot2(rc2(x, n), n);
     return f < r ? f : r;
 }
@@ -206,7 +212,10 @@ void canonical_stranded(const std::string &s, std::string &canon, char &strand) 
 
 char canonical_strand(const char *s, int64_t n) {
     uint64_t x;
-    if (n > 0 && pack2_acgt(s, n, x)) return min_rot2(x, n) <= min_rot2(rc2(x, n), n) ? '+' : '-';
+    if (n > 0 && pack2_acgt(s, n, x)) {
+        if (n <= 8) return (canon_table()[n][(size_t)x] >> 16) ? '+' : '-';
+        return min_rot2(x, n) <= min_rot2(rc2(x, n), n) ? '+' : '-';
+    }
     u128 y;
     if (pack2_acgt128(s, n, y)) return min_rot2_128(y, n) <= min_rot2_128(rc2_128(y, n), n) ? '+' : '-';
     thread_local std::string t, c;

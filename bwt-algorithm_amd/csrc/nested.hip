@@ -268,38 +268,44 @@ __global__ __launch_bounds__(T) void k_seg_levels(const int64_t *__restrict__ S,
             sE[i] = E[a + i];
             sP[i] = PME[a + i];
             sM[i] = M[a + i];
-            sK[i] = 0;
         }
+        __syncthreads();
+        // a hit that no span of a longer motif could nest (kept or not) is kept
+        // whatever the levels decide: only the others (kUndecided) take part in
+        // the level loop, whose levels are then the distinct motif lengths among them
+        constexpr uint8_t kUndecided = 2;
+        auto nested_among = [&](int i, bool kept_only) {   // span i nested by a longer motif's span
+            const int64_t s0 = sS[i], e0 = sE[i], rl = e0 - s0;
+            const int64_t m = sM[i];
+            if (rl <= 0) return false;
+            int lo = i + 1, hi = len;   // first local rank with S >= e0 (S[i] = s0 < e0)
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (sS[mid] < e0) lo = mid + 1;
+                else hi = mid;
+            }
+            for (int k = lo - 1; k >= 0 && sP[k] > s0; --k) {
+                const int64_t Mk = sM[k];
+                // this level's entries are being written now: never read (Mk <= m)
+                if (Mk <= m || (kept_only && sK[k] != 1)) continue;
+                if (nested_by(s0, e0, m, rl, sS[k], sE[k], Mk, thr)) return true;
+            }
+            return false;
+        };
+        for (int i = tid; i < len; i += T) sK[i] = nested_among(i, false) ? kUndecided : 1;
         int cur = 0x7fffffff;   // levels below this one are still undecided
         for (;;) {
             if (tid == 0) lvl = -1;
             __syncthreads();
             int mx = -1;
             for (int i = tid; i < len; i += T)
-                if (sM[i] < cur && sM[i] > mx) mx = sM[i];
+                if (sK[i] == kUndecided && sM[i] < cur && sM[i] > mx) mx = sM[i];
             if (mx >= 0) atomicMax(&lvl, mx);
             __syncthreads();
             const int m = lvl;   // uniform
             if (m < 0) break;
-            for (int i = tid; i < len; i += T) {
-                if (sM[i] != m) continue;
-                const int64_t s0 = sS[i], e0 = sE[i], rl = e0 - s0;
-                bool nested = false;
-                if (rl > 0) {
-                    int lo = i + 1, hi = len;   // first local rank with S >= e0 (S[i] = s0 < e0)
-                    while (lo < hi) {
-                        const int mid = (lo + hi) >> 1;
-                        if (sS[mid] < e0) lo = mid + 1;
-                        else hi = mid;
-                    }
-                    for (int k = lo - 1; k >= 0 && sP[k] > s0; --k) {
-                        const int64_t Mk = sM[k];
-                        if (Mk <= m || !sK[k]) continue;   // this level's entries are being written now: never read
-                        if (nested_by(s0, e0, m, rl, sS[k], sE[k], Mk, thr)) { nested = true; break; }
-                    }
-                }
-                sK[i] = nested ? 0 : 1;
-            }
+            for (int i = tid; i < len; i += T)
+                if (sM[i] == m && sK[i] == kUndecided) sK[i] = nested_among(i, true) ? 0 : 1;
             cur = m;
             __syncthreads();
         }
