@@ -7,6 +7,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <cctype>
 #include <cstring>
 #include <exception>
 #include <fcntl.h>
@@ -219,6 +220,24 @@ int bwtmi_open(int device, bwtmi_ctx **out) {
         auto *ctx = new bwtmi_ctx();
         ctx->c.device = device;
         HIPCHECK(hipSetDevice(device));
+        // host threads next to the GPU: a process free to run on both sockets
+        // of a box spread its 16 threads (and their first-touch pages) over
+        // both, and the W = 8 shard step came out at 8.0 or 9.0 ms from run to
+        // run; pinned to either node every run took 7.5-8.3 ms (r04x/r04y)
+        {
+            char bus[64] = {0};
+            if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, device) == hipSuccess) {
+                std::string id(bus);
+                for (auto &ch : id) ch = (char)std::tolower((unsigned char)ch);
+                if (FILE *f = std::fopen(("/sys/bus/pci/devices/" + id + "/numa_node").c_str(), "r")) {
+                    int node = -1;
+                    if (std::fscanf(f, "%d", &node) == 1) bind_host_numa(node);
+                    std::fclose(f);
+                }
+            } else {
+                (void)hipGetLastError();
+            }
+        }
         // how a host thread waits for the device: the background index build
         // waits on the device while every host thread post-processes, so a
         // spinning wait would take a core from them.  Blocking waits by default

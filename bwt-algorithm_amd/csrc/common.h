@@ -416,6 +416,11 @@ std::vector<int32_t> shard_units(Job &job, int32_t world, int32_t rank);
 // LOCAL_WORLD_SIZE ranks of the node), at most 16
 int host_threads(const bwtmi_params &p);
 int host_cpu_budget(int *cpus_visible, int *local_world);
+// Host work (the calling thread now, the worker pools from their next region)
+// moves onto the CPUs of NUMA node `node` that the process may use -- the
+// node of its GPU (bwtmi_open).  False when nothing changed (BWTMI_NUMA_BIND=0,
+// already inside the node, or no such CPUs).
+bool bind_host_numa(int node);
 // fn(task) for task in [0, n) on up to nt threads (dynamic scheduling)
 void run_tasks(int64_t n, int nt, const std::function<void(int64_t)> &fn);
 

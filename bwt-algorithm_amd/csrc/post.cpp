@@ -84,6 +84,73 @@ int host_threads(const bwtmi_params &p) {
     return host_cpu_budget(nullptr, nullptr);
 }
 
+// ------------------------------------------------------------ NUMA placement
+// The CPU set host work runs on (empty: unchanged).  Set once per process by
+// bind_host_numa; the calling thread takes it at once, pool workers at the
+// start of their next region (they may predate the binding).
+namespace {
+std::mutex g_bind_mu;
+cpu_set_t g_bind_set;
+std::atomic<int> g_bind_epoch{0};
+thread_local int tl_bind_epoch = 0;
+inline void apply_binding() {
+    const int e = g_bind_epoch.load(std::memory_order_acquire);
+    if (e == tl_bind_epoch) return;
+    cpu_set_t cs;
+    {
+        std::lock_guard<std::mutex> lk(g_bind_mu);
+        cs = g_bind_set;
+    }
+    (void)sched_setaffinity(0, sizeof cs, &cs);
+    tl_bind_epoch = e;
+}
+bool read_cpulist(const char *path, cpu_set_t &cs) {   // "0-63,128-191"
+    FILE *f = std::fopen(path, "r");
+    if (!f) return false;
+    char buf[4096];
+    const bool ok = std::fgets(buf, sizeof buf, f) != nullptr;
+    std::fclose(f);
+    if (!ok) return false;
+    CPU_ZERO(&cs);
+    for (char *p = buf; *p && *p != '\n';) {
+        char *e;
+        const long a = std::strtol(p, &e, 10);
+        if (e == p) return false;
+        long b = a;
+        p = e;
+        if (*p == '-') {
+            b = std::strtol(p + 1, &e, 10);
+            if (e == p + 1) return false;
+            p = e;
+        }
+        for (long c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET((int)c, &cs);
+        if (*p == ',') ++p;
+    }
+    return CPU_COUNT(&cs) > 0;
+}
+}  // namespace
+
+bool bind_host_numa(int node) {
+    static const bool on = [] { const char *e = std::getenv("BWTMI_NUMA_BIND"); return !(e && *e == '0'); }();
+    if (!on || node < 0) return false;
+    char path[96];
+    std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+    cpu_set_t want, cur, both;
+    if (!read_cpulist(path, want)) return false;
+    if (sched_getaffinity(0, sizeof cur, &cur) != 0) return false;
+    CPU_AND(&both, &want, &cur);
+    // nothing to gain when the process already runs inside the node, nothing
+    // possible when the node holds none of its CPUs
+    if (CPU_COUNT(&both) == 0 || CPU_EQUAL(&both, &cur)) return false;
+    {
+        std::lock_guard<std::mutex> lk(g_bind_mu);
+        g_bind_set = both;
+    }
+    g_bind_epoch.fetch_add(1, std::memory_order_acq_rel);
+    apply_binding();
+    return true;
+}
+
 // Persistent worker pools: parallel regions reuse the same threads (and their
 // thread-local DP scratch) instead of spawning per call.  The caller takes
 // part as worker 0; a region started from inside a worker of the same pool
@@ -213,6 +280,7 @@ private:
                 if (id >= want) continue;
                 f = job;
             }
+            apply_binding();
             try {
                 (*f)(id + 1);
             } catch (...) {   // reported to the caller of run(); never escapes the thread
