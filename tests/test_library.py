@@ -115,6 +115,29 @@ def test_device_short_imperfect_vs_oracle(gpu_ctx, seed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kw", [dict(min_copies=2, min_array_length=4), dict(min_copies=4, min_array_length=20),
+                                dict(min_copies=3, min_array_length=30, min_period=2, max_short_motif=7),
+                                dict(min_copies=2, min_array_length=1, min_entropy=0.5),
+                                dict(allow_mismatches=False)])
+def test_device_short_imperfect_parameters_vs_oracle(gpu_ctx, kw):
+    """The finder's thresholds reach the device seed flags (k_seed_flags keeps a
+    seed when some window through it has >= max(min_copies, ceil(min_array_length
+    / L)) copies): other min_copies / min_array_length / period / entropy
+    settings against the oracle."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_goldens import _crafted_short
+    seq = _crafted_short(17, 40)
+    t = seq + b"$"
+    idx = oracle.Index(t)
+    want = olib.short_imperfect("c", t, idx, **kw)
+    f = _finder(seq.decode())
+    for k, v in kw.items():
+        setattr(f, k, v)
+    _cmp(_as_dicts(f.find_short_imperfect_repeats("c", set())), want, DEV_FIELDS)
+
+
+@pytest.mark.gpu
 def test_device_tier1_matches_reference(gpu_ctx, lib_golden):
     from bwtmi.tiers import Tier1STRFinder
     for name, case in lib_golden.items():
