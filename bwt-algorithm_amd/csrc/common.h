@@ -224,9 +224,12 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
 struct AlignScratch;
 AlignScratch *align_scratch_new();
 void align_scratch_free(AlignScratch *);
+// resume: a walk of the same region start and template that this scratch saw
+// stop at its limit goes on from there when this call's limit is not smaller
+// (and this call's walk is kept in turn when it stops at its limit)
 bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_t end,
                          const std::string &tmpl, int64_t min_copies, AlignSummary &out, double frac,
-                         int64_t max_indel_arg, AlignScratch *ws);
+                         int64_t max_indel_arg, AlignScratch *ws, bool resume = false);
 
 // _recompute_repeat's alignment (bwt.py:3530-3534: align_repeat_region with
 // min_copies, then with 1) of a batch of regions on the device (recompute.hip)

@@ -671,9 +671,30 @@ int64_t run_end(const char *s, int64_t pos, int64_t lim, char b) {
     return pos;
 }
 
+// A walk that stopped at its safety limit, kept for the next call with the
+// same region start and template: the walk's states (positions, consensus
+// counts, variations) do not depend on the limit, only where it stops does,
+// so a call whose limit lies at or past the stop resumes from it instead of
+// re-aligning every copy (the merge fold recomputes a growing region from one
+// start once per chain step).
+struct WalkState {
+    bool valid = false;
+    const char *seq = nullptr;
+    int64_t seq_len = 0, start = 0, max_indel = 0, tol = 0, stop_limit = 0;
+    std::string tmpl, cur, variations;
+    int64_t pos = 0, copies = 0, tot_ins = 0, tot_del = 0, tot_err = 0, max_err = 0;
+    bool any_variation = false, want_copies = false;
+    std::vector<int64_t> copy_len, copy_err;
+    std::vector<char> pc_c;
+    std::vector<int64_t> pc_n;
+    std::vector<uint8_t> pc_k;
+    std::vector<std::vector<std::pair<char, int64_t>>> pc_over;
+};
+
 struct AlignScratch {
     Scratch S;
     std::string cur;
+    WalkState saved;
 };
 AlignScratch *align_scratch_new() { return new AlignScratch(); }
 void align_scratch_free(AlignScratch *w) { delete w; }
@@ -687,7 +708,7 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
 
 bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_t end,
                          const std::string &tmpl, int64_t min_copies, AlignSummary &out, double frac,
-                         int64_t max_indel_arg, AlignScratch *ws) {
+                         int64_t max_indel_arg, AlignScratch *ws, bool resume) {
     if (tmpl.empty() || seq_len == 0) return false;
     start = std::max<int64_t>(0, start);
     end = std::min<int64_t>(seq_len, end > start ? end : seq_len);
@@ -726,19 +747,42 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
         return true;
     }
     Scratch &S = ws->S;
-    pc_reset(S, m);
-    out.copy_len.clear();
-    out.copy_err.clear();
-    out.variations.clear();
-    out.any_variation = false;
     int64_t tot_ins = 0, tot_del = 0, tot_err = 0, max_err = 0;
     std::string &cur = ws->cur;
-    cur = tmpl;
     int64_t pos = start;
     const int64_t limit = std::min<int64_t>(
         seq_len, std::max<int64_t>(end, start + m * min_copies) + std::max<int64_t>(m * 3, max_indel * 4));
     UnitOut res;
     int64_t copies = 0;
+    WalkState &W = ws->saved;
+    if (resume && W.valid && W.seq == seq && W.seq_len == seq_len && W.start == start && W.max_indel == max_indel &&
+        W.tol == tol && W.want_copies == out.want_copies && limit >= W.stop_limit && W.tmpl == tmpl) {
+        // the walk up to W.pos is this call's too; it goes on from there (or
+        // stops at once when the new limit does not pass W.pos)
+        std::swap(S.pc_c, W.pc_c);
+        std::swap(S.pc_n, W.pc_n);
+        std::swap(S.pc_k, W.pc_k);
+        std::swap(S.pc_over, W.pc_over);
+        cur.swap(W.cur);
+        out.variations.swap(W.variations);
+        out.any_variation = W.any_variation;
+        out.copy_len.swap(W.copy_len);
+        out.copy_err.swap(W.copy_err);
+        pos = W.pos;
+        copies = W.copies;
+        tot_ins = W.tot_ins;
+        tot_del = W.tot_del;
+        tot_err = W.tot_err;
+        max_err = W.max_err;
+        W.valid = false;
+    } else {
+        pc_reset(S, m);
+        out.copy_len.clear();
+        out.copy_err.clear();
+        out.variations.clear();
+        out.any_variation = false;
+        cur = tmpl;
+    }
     // exact copies observe cur[p] at every p; they are counted in bulk before
     // the next count update or read, which keeps first-insertion order
     int64_t pend = 0;
@@ -811,10 +855,45 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
         pos += res.consumed;
     }
     out.at_limit = pos >= limit;
-    if (copies < min_copies) return false;
+    flush();   // the pending exact copies' counts (applied before any later update or read)
+    // a walk stopped by its limit is kept for a resume (the counts move, the
+    // strings and per-copy vectors are copied: the result still holds them)
+    auto save = [&]() {
+        if (!resume || !out.at_limit) return;
+        W.valid = true;
+        W.seq = seq;
+        W.seq_len = seq_len;
+        W.start = start;
+        W.max_indel = max_indel;
+        W.tol = tol;
+        W.stop_limit = limit;
+        W.tmpl = tmpl;
+        W.cur = cur;
+        W.variations = out.variations;
+        W.any_variation = out.any_variation;
+        W.want_copies = out.want_copies;
+        W.copy_len = out.copy_len;
+        W.copy_err = out.copy_err;
+        W.pos = pos;
+        W.copies = copies;
+        W.tot_ins = tot_ins;
+        W.tot_del = tot_del;
+        W.tot_err = tot_err;
+        W.max_err = max_err;
+        std::swap(S.pc_c, W.pc_c);
+        std::swap(S.pc_n, W.pc_n);
+        std::swap(S.pc_k, W.pc_k);
+        std::swap(S.pc_over, W.pc_over);
+    };
+    if (copies < min_copies) {
+        save();
+        return false;
+    }
     const int64_t consumed = pos - start;
-    if (consumed <= 0) return false;
-    flush();
+    if (consumed <= 0) {
+        save();
+        return false;
+    }
     consensus_from(S, m, cur, out.consensus);
     const int64_t denom = copies * m;
     out.motif_len = m;
@@ -825,6 +904,7 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
     out.tot_err = tot_err;
     out.tot_ins = tot_ins;
     out.tot_del = tot_del;
+    save();
     return true;
 }
 

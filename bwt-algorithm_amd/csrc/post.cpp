@@ -850,10 +850,13 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     AlignSummary &s = A.sum;
     s.want_copies = false;
     int phase = 1;
-    bool ok = align_repeat_region(seq, L, start, end, tmpl, mc, s, 0.1, -1, A.as.get());
+    // resume: a chain of merges recomputes a growing region from one start,
+    // and each walk that stopped at its limit goes on from where it stopped
+    static const bool resume = [] { const char *e = std::getenv("BWTMI_WALK_RESUME"); return !(e && *e == '0'); }();
+    bool ok = align_repeat_region(seq, L, start, end, tmpl, mc, s, 0.1, -1, A.as.get(), resume);
     if (!ok) {
         phase = 2;
-        ok = align_repeat_region(seq, L, start, end, tmpl, 1, s, 0.1, -1, A.as.get());
+        ok = align_repeat_region(seq, L, start, end, tmpl, 1, s, 0.1, -1, A.as.get(), resume);
     }
     RcView v;
     v.ok = ok;
