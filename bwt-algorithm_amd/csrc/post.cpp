@@ -139,9 +139,10 @@ bool bind_host_numa(int node) {
     if (!read_cpulist(path, want)) return false;
     if (sched_getaffinity(0, sizeof cur, &cur) != 0) return false;
     CPU_AND(&both, &want, &cur);
-    // nothing to gain when the process already runs inside the node, nothing
-    // possible when the node holds none of its CPUs
-    if (CPU_COUNT(&both) == 0 || CPU_EQUAL(&both, &cur)) return false;
+    // nothing to gain when the process already runs inside the node; no
+    // binding that leaves fewer CPUs than the host threads of a rank (a small
+    // cpuset split over both nodes)
+    if (CPU_EQUAL(&both, &cur) || CPU_COUNT(&both) < host_cpu_budget(nullptr, nullptr)) return false;
     {
         std::lock_guard<std::mutex> lk(g_bind_mu);
         g_bind_set = both;
