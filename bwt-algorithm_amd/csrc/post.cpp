@@ -339,6 +339,26 @@ static void parallel_items(int64_t n, int nt, F &&fn) {
     Pool::current().run(nt, work);
 }
 
+// static blocks: worker w takes items [n w / nt, n (w + 1) / nt) -- for the
+// memory-bound passes over the fold's chunks, so that a chunk is read by the
+// worker (and the core's cache) that wrote it in the pass before
+// (BWTMI_STATIC_PASSES=0: dynamic, as parallel_items)
+template <class F>
+static void parallel_blocks(int64_t n, int nt, F &&fn) {
+    static const bool on = [] { const char *e = std::getenv("BWTMI_STATIC_PASSES"); return !(e && *e == '0'); }();
+    if (!on) {
+        parallel_items(n, nt, fn);
+        return;
+    }
+    if (n <= 0) return;
+    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n));
+    auto work = [&](int w) {
+        for (int64_t k = n * w / nt; k < n * (w + 1) / nt; ++k) fn(k, w);
+    };
+    if (nt == 1) { work(0); return; }
+    Pool::current().run(nt, work);
+}
+
 void run_tasks(int64_t n, int nt, const std::function<void(int64_t)> &fn) {
     parallel_items(n, nt, [&](int64_t k, int) { fn(k); });
 }
@@ -1237,12 +1257,15 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt, Ou
     // task) -- the pool must hand the error back through the C ABI (tests/test_host.py)
     const char *inj_e = std::getenv("BWTMI_FAIL_MERGE_CHUNK");
     const int64_t inj = inj_e ? (std::atoll(inj_e) < 0 ? K - 1 : std::atoll(inj_e)) : -1;
-    parallel_items(K, nt, [&](int64_t k, int w) {
+    static const bool static_spec = [] { const char *e = std::getenv("BWTMI_STATIC_SPEC"); return e && *e == '1'; }();
+    auto spec_task = [&](int64_t k, int w) {
         if (k == inj) fail(BWTMI_E_STATE, "injected failure in merge task %lld", (long long)k);
         auto a = std::chrono::steady_clock::now();
         spec_run(u, pools, w, R, cut[(size_t)k], cut[(size_t)k + 1], fresh, spec[(size_t)k]);
         if (g_stats) cms[(size_t)k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
-    });
+    };
+    if (static_spec) parallel_blocks(K, nt, spec_task);
+    else parallel_items(K, nt, spec_task);
     auto ts1 = std::chrono::steady_clock::now();
     if (g_stats) {
         double sum = 0, mx = 0;
@@ -1305,7 +1328,7 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt, Ou
     std::vector<uint8_t> by_start((size_t)K, 1);
     std::vector<int64_t> cm((size_t)K + 1, INT64_MIN);
     auto by_end = [](const Item &x, const Item &y) { return x.end < y.end; };
-    parallel_items(K, nt, [&](int64_t k, int w) {
+    parallel_blocks(K, nt, [&](int64_t k, int w) {
         const SpecOut &sp = spec[(size_t)k];
         Item *const d0 = out.data() + at[(size_t)k];
         Item *dst = d0;
@@ -1623,7 +1646,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
         std::vector<int64_t> pre((size_t)C, INT64_MIN);   // max end before nominal chunk t
         for (int t = 1; t < C; ++t) pre[(size_t)t] = std::max(pre[(size_t)t - 1], cmax[(size_t)t - 1]);
         sb[0] = 0;
-        parallel_items(C - 1, nt, [&](int64_t q, int) {
+        parallel_blocks(C - 1, nt, [&](int64_t q, int) {
             const int64_t t = q + 1;
             int64_t i = nom[(size_t)t], m = pre[(size_t)t];
             while (i < N && recs[(size_t)i].start < m) m = std::max(m, recs[(size_t)i++].end);
@@ -1632,7 +1655,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
         for (int t = 1; t <= C; ++t) sb[(size_t)t] = std::max(sb[(size_t)t], sb[(size_t)t - 1]);
         std::vector<std::vector<uint32_t>> part((size_t)C);
         std::vector<int64_t> cnt((size_t)C + 1, 0);
-        parallel_items(C, nt, [&](int64_t t, int) {
+        parallel_blocks(C, nt, [&](int64_t t, int) {
             auto &pc = part[(size_t)t];
             pc.reserve((size_t)(sb[(size_t)t + 1] - sb[(size_t)t]) + 1);   // nearly every record stays
             int64_t c = 0;   // records passing the final filter, counted as each slot is settled
@@ -1660,10 +1683,10 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
         // materialised: a throwing materialize must leave no raw slot behind for
         // the vector's destructor
         static_assert(std::is_nothrow_default_constructible<Rec>::value, "Rec() must not throw");
-        parallel_items(C, nt, [&](int64_t t, int) {
+        parallel_blocks(C, nt, [&](int64_t t, int) {
             for (int64_t q = cnt[(size_t)t]; q < cnt[(size_t)t + 1]; ++q) ::new ((void *)&out[(size_t)q]) Rec();
         });
-        parallel_items(C, nt, [&](int64_t t, int) {
+        parallel_blocks(C, nt, [&](int64_t t, int) {
             int64_t o = cnt[(size_t)t];
             for (uint32_t i : part[(size_t)t])
                 if (pass(i)) materialize(u, recs[i], shift, out[(size_t)o++]);
