@@ -152,6 +152,24 @@ def fm_all_motifs(seq: bytes, reps: int = 5):
                 mpatterns_per_s=round(len(pats) / dt / 1e6, 2))
 
 
+def host_counters():
+    """Process page faults / context switches and the cgroup's CPU-quota
+    throttling (cpu.stat), read around the timed region: a host stage slowed by
+    the quota or by page faulting shows here, not in the kernel times."""
+    import resource
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    d = dict(minflt=ru.ru_minflt, majflt=ru.ru_majflt, nvcsw=ru.ru_nvcsw, nivcsw=ru.ru_nivcsw)
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, v = line.split()
+                if k in ("nr_throttled", "throttled_usec", "usage_usec"):
+                    d["cg_" + k] = int(v)
+    except (OSError, ValueError):
+        pass
+    return d
+
+
 def cli_drop_in(fa: str, args, reps: int = 2):
     """The drop-in CLI (`bwt.py FA -o OUT ARGS`, bwt.py:4201-4370) run
     in-process on the workload's FASTA: wall time of each run (a fresh
@@ -313,11 +331,13 @@ def main():
     calls.clear()
     _lib.kernel_stats(ctx, enable=True, reset=True)
     sync()
+    host0 = host_counters()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
     sync()
     elapsed = time.perf_counter() - t0
+    host1 = host_counters()
     kstats = _lib.kernel_stats(ctx, enable=False, reset=True)
     stages = job.stage_ms()
     if c is not None:
@@ -449,6 +469,7 @@ def main():
         "kernels_ms_per_step": {k: round(v[0] / a.steps, 3) for k, v in
                                 sorted(kstats.items(), key=lambda kv: -kv[1][0])},
         "calls_ms_per_step": {k: round(v, 2) for k, v in per_call.items()},
+        "host_per_step": {k: round((host1[k] - host0[k]) / a.steps, 1) for k in host1 if k in host0},
         "value_resident_text": round(total_bp / 1e6 / ((ms_step - load_up) / 1e3), 3) if ms_step > load_up else None,
         "fm_all_motifs_1_10": fm,
         "cli_drop_in": cli,

@@ -142,7 +142,33 @@ bool bind_host_numa(int node) {
     // nothing to gain when the process already runs inside the node; no
     // binding that leaves fewer CPUs than the host threads of a rank (a small
     // cpuset split over both nodes)
-    if (CPU_EQUAL(&both, &cur) || CPU_COUNT(&both) < host_cpu_budget(nullptr, nullptr)) return false;
+    int lw = 1;
+    const int budget = host_cpu_budget(nullptr, &lw);
+    if (CPU_EQUAL(&both, &cur) || CPU_COUNT(&both) < budget) return false;
+    // one hardware thread per physical core when the node's cores can hold
+    // every rank's threads (host workers + runtime threads) without sharing a
+    // core: two workers on the siblings of one core run the memory-bound host
+    // passes at well under half speed each (BWTMI_NUMA_SMT=1 keeps siblings)
+    static const bool smt = [] { const char *e = std::getenv("BWTMI_NUMA_SMT"); return e && *e == '1'; }();
+    if (!smt) {
+        cpu_set_t one;
+        CPU_ZERO(&one);
+        std::vector<std::pair<int, int>> seen;   // (package, core) taken
+        for (int c = 0; c < CPU_SETSIZE; ++c) {
+            if (!CPU_ISSET(c, &both)) continue;
+            int pkg = -1, core = -1;
+            char q[128];
+            std::snprintf(q, sizeof q, "/sys/devices/system/cpu/cpu%d/topology/physical_package_id", c);
+            if (FILE *f = std::fopen(q, "r")) { if (std::fscanf(f, "%d", &pkg) != 1) pkg = -1; std::fclose(f); }
+            std::snprintf(q, sizeof q, "/sys/devices/system/cpu/cpu%d/topology/core_id", c);
+            if (FILE *f = std::fopen(q, "r")) { if (std::fscanf(f, "%d", &core) != 1) core = -1; std::fclose(f); }
+            if (pkg < 0 || core < 0) { CPU_ZERO(&one); break; }   // no topology: keep the node set
+            if (std::find(seen.begin(), seen.end(), std::make_pair(pkg, core)) != seen.end()) continue;
+            seen.emplace_back(pkg, core);
+            CPU_SET(c, &one);
+        }
+        if (CPU_COUNT(&one) >= lw * (budget + 4)) both = one;
+    }
     {
         std::lock_guard<std::mutex> lk(g_bind_mu);
         g_bind_set = both;
