@@ -1364,6 +1364,7 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt, Ou
             for (size_t q = from[(size_t)k]; q < sp.emitted.size(); ++q) *dst++ = sp.record(R, q);
         int64_t mx = INT64_MIN;
         for (Item *it = d0; it < dst; ++it) {
+            if (it + 8 < dst && it[8].x) __builtin_prefetch(it[8].x);   // refine reads x->mm
             refine_one(u, pools, w, *it);
             mx = std::max(mx, it->end);
         }
@@ -1705,18 +1706,42 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
             DeferConstruct raw;   // constructed below, in parallel
             out.resize((size_t)cnt[(size_t)C]);
         }
-        // every slot is constructed (a non-throwing pass) before any record is
-        // materialised: a throwing materialize must leave no raw slot behind for
-        // the vector's destructor
+        // each chunk constructs its slots and materialises them in one pass (the
+        // record is still in cache).  Every slot is constructed whatever throws:
+        // a chunk whose materialize throws constructs the rest of its slots
+        // before it reports, and the chunks after it only construct theirs, so
+        // the vector's destructor never meets a raw slot.
         static_assert(std::is_nothrow_default_constructible<Rec>::value, "Rec() must not throw");
+        std::atomic<bool> failed{false};
+        std::exception_ptr err;
+        std::mutex err_mu;
         parallel_blocks(C, nt, [&](int64_t t, int) {
-            for (int64_t q = cnt[(size_t)t]; q < cnt[(size_t)t + 1]; ++q) ::new ((void *)&out[(size_t)q]) Rec();
+            const int64_t q0 = cnt[(size_t)t], q1 = cnt[(size_t)t + 1];
+            int64_t o = q0;   // slots [q0, o) are constructed
+            if (!failed.load(std::memory_order_relaxed)) {
+                try {
+                    const std::vector<uint32_t> &pt = part[(size_t)t];
+                    for (size_t j = 0; j < pt.size(); ++j) {
+                        if (j + 8 < pt.size()) {   // the record data of a later slot (written by other workers)
+                            const Item &ahead = recs[pt[j + 8]];
+                            if (ahead.x) __builtin_prefetch(ahead.x);
+                        }
+                        const uint32_t i = pt[j];
+                        if (pass(i)) {
+                            ::new ((void *)&out[(size_t)o]) Rec();
+                            ++o;
+                            materialize(u, recs[i], shift, out[(size_t)o - 1]);
+                        }
+                    }
+                } catch (...) {
+                    failed.store(true, std::memory_order_relaxed);
+                    std::lock_guard<std::mutex> lk(err_mu);
+                    if (!err) err = std::current_exception();
+                }
+            }
+            for (; o < q1; ++o) ::new ((void *)&out[(size_t)o]) Rec();
         });
-        parallel_blocks(C, nt, [&](int64_t t, int) {
-            int64_t o = cnt[(size_t)t];
-            for (uint32_t i : part[(size_t)t])
-                if (pass(i)) materialize(u, recs[i], shift, out[(size_t)o++]);
-        });
+        if (err) std::rethrow_exception(err);
     }
     auto t4 = clk::now();
     if (std::getenv("BWTMI_STATS")) {
