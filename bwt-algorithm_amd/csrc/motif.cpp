@@ -611,9 +611,12 @@ bool finish_unit(const char *motif, int64_t m, const char *win, int64_t n, int64
     return true;
 }
 
+// only the entry counts need clearing: entries at or past pc_k[p] are never read
 inline void pc_reset(Scratch &S, int64_t m) {
-    S.pc_c.assign((size_t)(m * KIN), 0);
-    S.pc_n.assign((size_t)(m * KIN), 0);
+    if (S.pc_c.size() < (size_t)(m * KIN)) {
+        S.pc_c.resize((size_t)(m * KIN));
+        S.pc_n.resize((size_t)(m * KIN));
+    }
     S.pc_k.assign((size_t)m, 0);
     if ((int64_t)S.pc_over.size() < m) S.pc_over.resize((size_t)m);
     for (int64_t p = 0; p < m; ++p) S.pc_over[(size_t)p].clear();
