@@ -1002,18 +1002,64 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
             auto ti = std::chrono::steady_clock::now();
             try {
                 c.activate();
-                for (const auto &tx : to_index) {
+                // one build on context x (its own stream, slots and scratch index)
+                auto build = [sa_sample](Ctx &x, const std::pair<const uint8_t *, int64_t> &tx) {
                     const int64_t len = tx.second;
                     // (S_CAND_K2 is free after the scan; index_build_device uses the MISC/IDX slots)
-                    DBuf &tb = c.slot[S_CAND_K2];
+                    DBuf &tb = x.slot[S_CAND_K2];
                     tb.ensure((size_t)len + 1 + 128);
-                    HIPCHECK(hipMemcpyAsync(tb.p, tx.first, (size_t)len, hipMemcpyDeviceToDevice, c.stream));
-                    HIPCHECK(hipMemsetAsync(tb.as<uint8_t>() + len, '$', 1, c.stream));
-                    HIPCHECK(hipMemsetAsync(tb.as<uint8_t>() + len + 1, 0, 127, c.stream));
-                    c.scratch_index = index_build_device(c, tb.as<uint8_t>(), len + 1, sa_sample, 128, 0u,
-                                                         c.scratch_index);
+                    HIPCHECK(hipMemcpyAsync(tb.p, tx.first, (size_t)len, hipMemcpyDeviceToDevice, x.stream));
+                    HIPCHECK(hipMemsetAsync(tb.as<uint8_t>() + len, '$', 1, x.stream));
+                    HIPCHECK(hipMemsetAsync(tb.as<uint8_t>() + len + 1, 0, 127, x.stream));
+                    x.scratch_index = index_build_device(x, tb.as<uint8_t>(), len + 1, sa_sample, 128, 0u,
+                                                         x.scratch_index);
+                };
+                // several contigs: the builds go to the scan lanes (longest first, each
+                // to the least loaded lane), each lane's builds on its own stream and
+                // host thread -- a 12.5 Mbp build is a chain of small launches and host
+                // reads that leaves the device mostly idle, and eight of them in a row
+                // outlasted the host stages of the 8-contig step (C4: 35 ms, r04final)
+                static const int kIndexLanes = [] {
+                    const char *e = std::getenv("BWTMI_INDEX_LANES");
+                    return e && *e ? std::max(1, std::min(8, std::atoi(e))) : 4;
+                }();
+                const size_t nl = std::min<size_t>((size_t)kIndexLanes, to_index.size());
+                if (nl <= 1) {
+                    for (const auto &tx : to_index) build(c, tx);
+                    HIPCHECK(hipStreamSynchronize(c.stream));
+                } else {
+                    std::vector<size_t> ord(to_index.size());
+                    for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
+                    std::stable_sort(ord.begin(), ord.end(),
+                                     [&](size_t x, size_t y) { return to_index[x].second > to_index[y].second; });
+                    std::vector<std::vector<size_t>> part(nl);
+                    std::vector<int64_t> load(nl, 0);
+                    for (size_t i : ord) {
+                        const size_t k = (size_t)(std::min_element(load.begin(), load.end()) - load.begin());
+                        part[k].push_back(i);
+                        load[k] += to_index[i].second;
+                    }
+                    std::vector<Ctx *> lc(nl);
+                    lc[0] = &c;
+                    for (size_t k = 1; k < nl; ++k) lc[k] = &scan_lane(c, k);
+                    std::vector<std::exception_ptr> ex(nl);
+                    auto run = [&](size_t k) {
+                        try {
+                            if (k) lc[k]->activate();
+                            for (size_t i : part[k]) build(*lc[k], to_index[i]);
+                            HIPCHECK(hipStreamSynchronize(lc[k]->stream));
+                        } catch (...) {
+                            ex[k] = std::current_exception();
+                        }
+                    };
+                    std::vector<std::thread> th;
+                    for (size_t k = 1; k < nl; ++k) th.emplace_back(run, k);
+                    run(0);
+                    for (auto &t : th) t.join();
+                    for (size_t k = 1; k < nl; ++k) c.absorb_kstats(*lc[k]);
+                    for (auto &e : ex)
+                        if (e) std::rethrow_exception(e);
                 }
-                HIPCHECK(hipStreamSynchronize(c.stream));
             } catch (const Error &e) {
                 c.bg_code = e.code;
                 c.bg_err = "background index build: " + e.msg;
