@@ -84,6 +84,7 @@ enum Slot {
     S_SORT_TMP0, S_SORT_TMP1, S_SORT_HIST, S_SCAN_TMP, S_MISC0, S_MISC1, S_MISC2, S_MISC3,
     S_IDX0, S_IDX1, S_IDX2, S_IDX3, S_IDX4, S_IDX5, S_IDX6, S_IDX7, S_IDX8, S_IDX9, S_IDX10, S_IDX11,
     S_FASTA,   // a whole-file load's FASTA image (fasta_dev.hip)
+    S_SORT_DIG,   // the next pass's digit of every key, written by a radix pass (radix.hip)
     S_NSLOTS
 };
 

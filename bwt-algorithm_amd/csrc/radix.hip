@@ -259,7 +259,8 @@ template <class KT, class V, int BLOCK, int ITEMS, bool NT, bool SPLIT>
 __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, const V *__restrict__ vin,
                                                    KT *__restrict__ kout, V *__restrict__ vout,
                                                    const uint32_t *__restrict__ offs, int64_t n, int shift,
-                                                   int64_t ntiles, int swz) {
+                                                   int64_t ntiles, int swz, uint8_t *__restrict__ dnext = nullptr,
+                                                   int nshift = 0) {
     constexpr int kT = BLOCK * ITEMS;
     constexpr int NW = BLOCK / 64;
     static_assert(BLOCK >= 256 && BLOCK % 64 == 0, "threads 0..255 own one digit each");
@@ -370,6 +371,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, c
             const uint32_t d = (uint32_t)((key >> shift) & 255u);
             const uint32_t p = gdelta[d] + (uint32_t)j;
             st<NT>(kout + p, key);
+            if (dnext) dnext[p] = (uint8_t)((key >> nshift) & 255u);   // the next pass's histogram input
             if constexpr (DG) dg_s[j] = (uint8_t)d;
             else pos[i] = p;
             if (!SPLIT && vout) st<NT>(vout + p, vs[j]);
@@ -404,17 +406,33 @@ void radix_sort_cfg(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
     V *va = vals, *vb = vals ? c.slot[S_SORT_TMP1].as<V>() : nullptr;
     uint32_t *cnt = c.slot[S_SORT_HIST].as<uint32_t>();
     static const int swz = [] { const char *e = std::getenv("BWTMI_RADIX_SWZ"); return e ? std::atoi(e) : 1; }();
+    // 64-bit keys: each pass but the last also writes the next pass's digit of
+    // every key it places (one byte, at the key's new position), and the next
+    // histogram reads n bytes instead of 8n (C3N: histograms 3.34 -> 2.56 ms,
+    // the kv12 scatters +0.3 ms for their byte stores, r04zo).  For 32- and
+    // 16-bit keys the byte stores cost the scatter more than the histogram
+    // saves (C3: kv8 1.54 -> 1.86 ms for 1.21 -> 0.97), so they read the keys.
+    // BWTMI_RADIX_DIGITS=0: never, =2: every key width.
+    static const int digits = [] { const char *e = std::getenv("BWTMI_RADIX_DIGITS"); return e && *e ? std::atoi(e) : 1; }();
+    const bool dig = (digits == 2 || (digits == 1 && sizeof(KT) == 8)) && bit0 + 8 < bit1;
+    uint8_t *dg = nullptr;
+    if (dig) {
+        c.slot[S_SORT_DIG].ensure((size_t)n + 64);
+        dg = c.slot[S_SORT_DIG].as<uint8_t>();
+    }
     int passes = 0;
     for (int sh = bit0; sh < bit1; sh += 8) {
-        // read the keys once
-        launch_hist<kT / kBlock, KT>(c, ka, cnt, n, sh, ntiles);
+        // read the keys (the first pass) or their digit bytes once
+        if (dig && sh > bit0) launch_hist<kT / kBlock, uint8_t>(c, dg, cnt, n, 0, ntiles);
+        else launch_hist<kT / kBlock, KT>(c, ka, cnt, n, sh, ntiles);
         exclusive_scan<uint32_t>(c, cnt, cnt, ntiles * 256);
         // read (key, value) once, write it once
+        const bool more = dig && sh + 8 < bit1;
         KLAUNCH(sizeof(KT) == 2 ? "radix_scatter_kv6" : sizeof(KT) == 4 ? "radix_scatter_kv8"
                 : sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16",
                 (double)n * 2.0 * ((double)sizeof(KT) + (vals ? (double)sizeof(V) : 0.0)),
                 (k_scatter<KT, V, BLOCK, ITEMS, NT, SPLIT>), dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, ka, va,
-                kb, vb, cnt, n, sh, ntiles, swz);
+                kb, vb, cnt, n, sh, ntiles, swz, more ? dg : nullptr, sh + 8);
         std::swap(ka, kb);
         std::swap(va, vb);
         ++passes;
