@@ -98,6 +98,7 @@ _SIGS = {
     "bwtmi_job_get_records": (C.c_int, [_P, _P, _P]),
     "bwtmi_job_get_string": (C.c_int64, [_P, C.c_int64, C.c_int, _P, C.c_int64]),
     "bwtmi_job_get_strings": (C.c_int64, [_P, C.c_int, _P, C.c_int64, _P]),
+    "bwtmi_fasta_count_records": (C.c_int64, [C.c_char_p, C.c_int64]),
     "bwtmi_job_export": (C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
     "bwtmi_job_import": (C.c_int, [_P, _P, C.c_int64]),
     "bwtmi_job_stage_ms": (C.c_int, [_P, C.POINTER(C.c_double)]),

@@ -72,7 +72,9 @@ def _self_launch(a, argv) -> Optional[int]:
     this process: one rank's worth of work, `--jobs -1`, Tier 3 (its records
     join the scan of every contig in one process), a small input, or
     BWTMI_CLI_LAUNCH=0.  This process touches no GPU before the launch (the
-    devices are counted in a child).  BWTMI_CLI_RANKS=N forces N ranks over
+    devices are counted in a child; the records by the library's host-only
+    bwtmi_fasta_count_records -- loading the library and that call leave no
+    /dev/kfd or DRM descriptor open, checked on the box).  BWTMI_CLI_RANKS=N forces N ranks over
     the host transport, rank r on device r mod #GPUs (a rehearsal of an
     N-GPU node on fewer GPUs)."""
     from . import dist

@@ -102,7 +102,15 @@ def count_devices_in_child() -> int:
 def count_fasta_records(path: str, limit: int = 1 << 20) -> int:
     """Header lines ('>' at a line start) of a FASTA file, counted up to
     `limit` -- an upper bound on its fold units (bwt.py:3713-3756; natural-key
-    collisions and duplicate names only merge units)."""
+    collisions and duplicate names only merge units).  The native parallel
+    count (bwtmi_fasta_count_records, host only); 0 for an unreadable file."""
+    from ._lib import lib
+    n = int(lib().bwtmi_fasta_count_records(os.fsencode(path), int(limit)))
+    return max(n, 0)
+
+
+def _count_fasta_records_py(path: str, limit: int = 1 << 20) -> int:
+    """The same count in Python (two mmap scans) -- the tests' cross-check."""
     import mmap
     try:
         with open(path, "rb") as f:

@@ -720,6 +720,15 @@ int bwtmi_job_fasta_scan_part(bwtmi_job *job, const char *path, int32_t world, i
     });
 }
 
+int64_t bwtmi_fasta_count_records(const char *path, int64_t limit) {
+    if (!path || limit < 0) return -1;
+    try {
+        return fasta_count_records(path, limit);
+    } catch (...) {
+        return -1;
+    }
+}
+
 int bwtmi_job_load_fasta_parts_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *path, int32_t flank_trim,
                                    int32_t world, int32_t rank, const int64_t *blob, int64_t nwords) {
     return guard([&] {

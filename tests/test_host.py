@@ -757,6 +757,15 @@ def test_cli_self_launch_decisions(tmp_path, monkeypatch):
     lone = tmp_path / "cr.fa"
     lone.write_bytes(b">a\rACGT\r>b\rAC\r>c\rA")
     assert dist.count_fasta_records(str(crlf)) == 2 and dist.count_fasta_records(str(lone)) == 3
+    # the native parallel count (8 MiB pieces: headers right at a piece edge) against the Python one
+    big = tmp_path / "big.fa"
+    body = bytearray(b"ACGT" * ((20 << 20) // 4))
+    for k, at in enumerate([(8 << 20), (8 << 20) + 1, (16 << 20) - 1, (16 << 20) + 5]):
+        body[at - 1:at + 1] = b"\n>"
+    big.write_bytes(b">first\n" + bytes(body) + b"\n")
+    for lim in (1, 2, 4, 100):
+        assert dist.count_fasta_records(str(big), limit=lim) == dist._count_fasta_records_py(str(big), limit=lim)
+    assert dist.count_fasta_records(str(tmp_path / "missing.fa")) == 0
     calls = []
     monkeypatch.setattr(dist, "launch_ranks", lambda n, cmd, env: calls.append((n, cmd, [env(r) for r in range(n)])) or 0)
     monkeypatch.setattr(cli, "LAUNCH_MIN_BYTES", 0)
