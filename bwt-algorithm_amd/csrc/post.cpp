@@ -1254,7 +1254,11 @@ struct OutChunks {
     std::vector<int64_t> cut, cmax;
 };
 
-ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt, OutChunks *oc = nullptr) {
+// fill (optional): writes R[a, b) -- the records are converted by the
+// speculative task that reads them first (device-screened hits), not by a pass
+// of their own
+ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt, OutChunks *oc = nullptr,
+                   const std::function<void(int64_t, int64_t)> *fill = nullptr) {
     const int64_t n = (int64_t)R.size();
     if (n == 0) return {};
     // BWTMI_POST_DEVICE_MIN: smallest unit (records) whose fresh-pair recomputes go to the device
@@ -1264,6 +1268,10 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt, Ou
     }();
     RcTable rc;
     UnitCtx u = u0;
+    if (fill && u0.job->rc_batch && n >= dev_min) {   // the request pass reads every record first
+        parallel_for(n, nt, [&](int64_t a, int64_t b) { (*fill)(a, b); });
+        fill = nullptr;
+    }
     if (u0.job->rc_batch && n >= dev_min) {
         auto tr0 = std::chrono::steady_clock::now();
         rc_prepare(u0, R, nt, rc);
@@ -1287,6 +1295,7 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt, Ou
     auto spec_task = [&](int64_t k, int w) {
         if (k == inj) fail(BWTMI_E_STATE, "injected failure in merge task %lld", (long long)k);
         auto a = std::chrono::steady_clock::now();
+        if (fill) (*fill)(cut[(size_t)k], cut[(size_t)k + 1]);
         spec_run(u, pools, w, R, cut[(size_t)k], cut[(size_t)k + 1], fresh, spec[(size_t)k]);
         if (g_stats) cms[(size_t)k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
     };
@@ -1570,7 +1579,29 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     //    deduplicated per chromosome; a one-chromosome unit then skips 1-2.
     ItemVec recs;
     bool presorted = chroms.size() == 1;
+    // one device-screened contig (the usual unit): its compact hits become
+    // records inside the merge fold's speculative tasks, chunk by chunk
+    std::function<void(int64_t, int64_t)> fill_fn;
+    static const bool fused_fill = [] { const char *e = std::getenv("BWTMI_FUSED_ITEMS"); return !(e && *e == '0'); }();
+    if (fused_fill && chroms.size() == 1) {
+        const int32_t c = chroms[0];
+        const bool scr = (size_t)c < job.screened.size() && job.screened[(size_t)c] && (size_t)c < shits.size();
+        const bool mine = job.selected.empty() || ((size_t)c < job.selected.size() && job.selected[(size_t)c]);
+        const bool t3 = mine && (size_t)c < job.t3.size() && !job.t3[(size_t)c].empty();
+        if (scr && !t3) {
+            const ScreenedVec &sh = shits[(size_t)c];
+            recs.resize(sh.size());   // NoInit: filled by fill_fn
+            fill_fn = [&recs, &sh, c](int64_t a, int64_t b) {
+                for (int64_t k = a; k < b; ++k) {
+                    int64_t s0, len, prim;
+                    sh.get(k, s0, len, prim);
+                    recs[(size_t)k] = Item{s0, s0 + len, nullptr, c, (int32_t)prim};
+                }
+            };
+        }
+    }
     for (int32_t c : chroms) {
+        if (fill_fn) break;   // the fused path above
         auto &h = raw[(size_t)c];
         const bool scr = (size_t)c < job.screened.size() && job.screened[(size_t)c];
         presorted = presorted && scr;
@@ -1613,7 +1644,11 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     auto t2 = clk::now();
     // 3. merge adjacent (bwt.py:3222-3289)
     OutChunks oc;
-    recs = merge_fold(u, pools, recs, nt, &oc);
+    recs = merge_fold(u, pools, recs, nt, &oc, fill_fn ? &fill_fn : nullptr);
+    if (fill_fn) {
+        ScreenedVec().swap(shits[(size_t)chroms[0]]);
+        HitVec().swap(raw[(size_t)chroms[0]]);
+    }
     auto t3 = clk::now();
     // 4. refine (bwt.py:3291-3314): done inside merge_fold's assembly
     auto r1 = clk::now();   // merge_fold returns its records in (start, end) order
