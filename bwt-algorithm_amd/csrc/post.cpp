@@ -1291,7 +1291,6 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt, Ou
     // task) -- the pool must hand the error back through the C ABI (tests/test_host.py)
     const char *inj_e = std::getenv("BWTMI_FAIL_MERGE_CHUNK");
     const int64_t inj = inj_e ? (std::atoll(inj_e) < 0 ? K - 1 : std::atoll(inj_e)) : -1;
-    static const bool static_spec = [] { const char *e = std::getenv("BWTMI_STATIC_SPEC"); return e && *e == '1'; }();
     auto spec_task = [&](int64_t k, int w) {
         if (k == inj) fail(BWTMI_E_STATE, "injected failure in merge task %lld", (long long)k);
         auto a = std::chrono::steady_clock::now();
@@ -1299,8 +1298,7 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt, Ou
         spec_run(u, pools, w, R, cut[(size_t)k], cut[(size_t)k + 1], fresh, spec[(size_t)k]);
         if (g_stats) cms[(size_t)k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
     };
-    if (static_spec) parallel_blocks(K, nt, spec_task);
-    else parallel_items(K, nt, spec_task);
+    parallel_items(K, nt, spec_task);   // dynamic: the chunks' costs are uneven (r04ze: static blocks no better)
     auto ts1 = std::chrono::steady_clock::now();
     if (g_stats) {
         double sum = 0, mx = 0;
