@@ -275,6 +275,7 @@ def main():
     if rehearsal:
         local = local % max(1, _lib.device_count())
     ctx = _lib.ctx(local)
+    _lib.bind_host(ctx)        # host threads next to the GPU (the library never does it by itself)
     host = _lib.host_info()
 
     # input FASTA on local disk, written once before timing

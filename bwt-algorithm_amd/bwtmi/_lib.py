@@ -130,6 +130,14 @@ _SIGS = {
     "bwtmi_job_set_records": (C.c_int, [_P, _P, C.c_int64]),
     "bwtmi_wire_record_size": (C.c_int, []),
     "bwtmi_job_contig_error": (C.c_int64, [_P, C.c_int32, C.c_char_p, C.c_int64]),
+    "bwtmi_source_hash": (C.c_char_p, []),
+    "bwtmi_knob_set": (C.c_int, [C.c_char_p, C.c_int64]),
+    "bwtmi_knob_get": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64)]),
+    "bwtmi_knob_default": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64)]),
+    "bwtmi_knob_names": (C.c_char_p, []),
+    "bwtmi_bind_host": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int)]),
+    "bwtmi_host_binding_plan": (C.c_int, [C.c_char_p, C.c_int, C.c_char_p, C.c_int, C.c_int, C.c_char_p,
+                                          C.c_char_p, C.c_int64, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -188,6 +196,88 @@ def _close_all():
     for h in list(_ctxs.values()):
         _lib.bwtmi_close(h)
     _ctxs.clear()
+
+
+def source_hash() -> str:
+    """sha256 of csrc/* and include/bwtmi.h embedded when libbwtmi.so was built."""
+    return lib().bwtmi_source_hash().decode()
+
+
+def tree_source_hash() -> str:
+    """The same hash computed from the sources in this tree (Makefile SRC_HASH):
+    the files in byte order of their paths, concatenated."""
+    import glob
+    import hashlib
+    csrc = os.path.join(_PKG_ROOT, "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.cpp")) + glob.glob(os.path.join(csrc, "*.h")) +
+                   glob.glob(os.path.join(csrc, "*.hip")))
+    files.append(os.path.join(os.path.dirname(_PKG_ROOT), "include", "bwtmi.h"))
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def check_build() -> str:
+    """Fails loudly when the loaded library was built from other sources than
+    this tree's (a stale or foreign libbwtmi.so); returns the hash."""
+    got, want = source_hash(), tree_source_hash()
+    if got != want:
+        raise BwtmiError(f"{LIB_PATH} was built from sources {got[:16]}..., this tree holds {want[:16]}...: "
+                         f"rebuild with `make -C {_PKG_ROOT}`")
+    return got
+
+
+def knob(name: str, value: Optional[int] = None) -> int:
+    """Read (and with value, set) a run-time switch BWTMI_<name> (INTEGRATION.md);
+    returns the value before the call."""
+    v = C.c_int64()
+    check(lib().bwtmi_knob_get(name.encode(), C.byref(v)))
+    if value is not None:
+        check(lib().bwtmi_knob_set(name.encode(), int(value)))
+    return v.value
+
+
+def knob_names() -> list:
+    return lib().bwtmi_knob_names().decode().split(",")
+
+
+class knobs:
+    """with knobs(RUNS_DENSE=1, ...): set switches for the block, restore after."""
+
+    def __init__(self, **kv):
+        self.kv = kv
+        self.old = {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = knob(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            knob(k, v)
+        return False
+
+
+def bind_host(h, on: bool = True) -> bool:
+    """Move this process's host work onto the CPUs of its GPU's NUMA node (the
+    CLI, bench and rank launcher ask for it; the library never does on its own);
+    on=False restores the affinity the binding replaced.  True when it changed."""
+    b = C.c_int(0)
+    check(lib().bwtmi_bind_host(h, int(on), C.byref(b)))
+    return bool(b.value)
+
+
+def binding_plan(sysroot: str, local_rank: int, rank_pci, threads: int, allowed: str, smt: bool = False):
+    """(cpulist or '', node, local ranks on that node) the binding would choose,
+    from a sysfs tree under sysroot; no affinity change."""
+    out = C.create_string_buffer(8192)
+    node, peers = C.c_int(-1), C.c_int(0)
+    check(lib().bwtmi_host_binding_plan(sysroot.encode(), local_rank, ",".join(rank_pci).encode(), threads, int(smt),
+                                        allowed.encode(), out, len(out), C.byref(node), C.byref(peers)))
+    return out.value.decode(), node.value, peers.value
 
 
 def kernel_stats(h, enable: bool = True, reset: bool = True) -> dict:

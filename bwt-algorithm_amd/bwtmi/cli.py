@@ -128,6 +128,10 @@ def main(argv=None) -> int:
         rc = _self_launch(a, argv)
         if rc is not None:
             return rc
+    # the process that does the work binds its host threads next to its GPU
+    # (bwtmi_open reads the switch; a library user's affinity is never touched)
+    from . import _lib
+    _lib.knob("NUMA_BIND", 1)
     finder = TandemRepeatFinder(a.reference, a.sa_sample, show_progress=a.progress,
                                 allow_mismatches=not a.no_mismatches, max_motif_length=a.max_motif_len,
                                 min_period=a.min_period, max_period=a.max_period,

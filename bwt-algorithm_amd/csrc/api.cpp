@@ -105,10 +105,6 @@ struct JobDev {
     int device = -1;
     std::vector<DevContig> seqs;
     Ctx *bg_ctx = nullptr;   // context whose background work reads these buffers (cleared by its join)
-    // the post-processing's device work (merge fold recomputes): a context of its
-    // own, so it never shares a stream or scratch with the background index build
-    std::unique_ptr<Ctx> post;
-    std::mutex post_mu;   // fold units run in parallel threads
 };
 
 // every entry point that touches a context: join its background work, select the device
@@ -193,7 +189,14 @@ struct bwtmi_job {
 extern "C" {
 
 const char *bwtmi_last_error(void) { return g_err.c_str(); }
-const char *bwtmi_version(void) { return "bwtmi 0.1 (gfx950)"; }
+// sha256 of the sources the library was built from (csrc/*.cpp *.h *.hip and
+// include/bwtmi.h in path order; generated by the Makefile into build/srchash.c)
+extern "C" const char bwtmi_src_sha256[];
+const char *bwtmi_source_hash(void) { return bwtmi_src_sha256; }
+const char *bwtmi_version(void) {
+    static const std::string v = std::string("bwtmi 0.5 (gfx950) src ") + bwtmi_src_sha256;
+    return v.c_str();
+}
 void bwtmi_free(void *p) { std::free(p); }
 
 int bwtmi_device_count(int *count) {
@@ -203,6 +206,36 @@ int bwtmi_device_count(int *count) {
         hipError_t e = hipGetDeviceCount(&n);
         *count = (e == hipSuccess) ? n : 0;
     });
+}
+
+// Host threads next to the GPU: a process free to run on both sockets of a
+// box spread its 16 threads (and their first-touch pages) over both, and the
+// W = 8 shard step came out at 8.0 or 9.0 ms from run to run; pinned to either
+// node every run took 7.5-8.3 ms (r04x/r04y).  Local rank r drives device
+// r mod (visible devices) -- LOCAL_RANK / LOCAL_WORLD_SIZE of the launcher --
+// so the ranks sharing this GPU's node are counted from their own GPUs.
+static bool bind_host_for(int device) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const char *lw_e = std::getenv("LOCAL_WORLD_SIZE");
+    const char *lr_e = std::getenv("LOCAL_RANK");
+    const int lw = std::max(1, lw_e ? std::atoi(lw_e) : 1);
+    int lr = lr_e ? std::atoi(lr_e) : device;
+    if (lr < 0 || lr >= lw) lr = 0;
+    std::vector<std::string> pci((size_t)lw);
+    for (int r = 0; r < lw; ++r) {
+        const int d = r == lr ? device : r % ndev;
+        char bus[64] = {0};
+        if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, d) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        pci[(size_t)r] = bus;
+    }
+    return bind_host_numa(lr, pci);
 }
 
 int bwtmi_open(int device, bwtmi_ctx **out) {
@@ -220,37 +253,16 @@ int bwtmi_open(int device, bwtmi_ctx **out) {
         auto *ctx = new bwtmi_ctx();
         ctx->c.device = device;
         HIPCHECK(hipSetDevice(device));
-        // host threads next to the GPU: a process free to run on both sockets
-        // of a box spread its 16 threads (and their first-touch pages) over
-        // both, and the W = 8 shard step came out at 8.0 or 9.0 ms from run to
-        // run; pinned to either node every run took 7.5-8.3 ms (r04x/r04y)
-        {
-            char bus[64] = {0};
-            if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, device) == hipSuccess) {
-                std::string id(bus);
-                for (auto &ch : id) ch = (char)std::tolower((unsigned char)ch);
-                if (FILE *f = std::fopen(("/sys/bus/pci/devices/" + id + "/numa_node").c_str(), "r")) {
-                    int node = -1;
-                    if (std::fscanf(f, "%d", &node) == 1) bind_host_numa(node);
-                    std::fclose(f);
-                }
-            } else {
-                (void)hipGetLastError();
-            }
-        }
+        // host threads next to the GPU only when asked for (bwtmi_bind_host, or
+        // BWTMI_NUMA_BIND=1 here): a library call never changes the caller's
+        // affinity on its own
+        if (knob(KN_NUMA_BIND)) bind_host_for(device);
         // how a host thread waits for the device: the background index build
         // waits on the device while every host thread post-processes, so a
-        // spinning wait would take a core from them.  Blocking waits by default
-        // (r02az, C3: 1949 vs 1895 Mbp/s over 3 runs each; BWTMI_SYNC=spin|yield|
-        // block|auto overrides)
-        {
-            const char *e = std::getenv("BWTMI_SYNC");
-            const std::string m = e ? e : "block";
-            const unsigned f = m == "yield" ? hipDeviceScheduleYield
-                               : m == "block" ? hipDeviceScheduleBlockingSync
-                               : m == "spin" ? hipDeviceScheduleSpin : hipDeviceScheduleAuto;
-            if (hipSetDeviceFlags(f) != hipSuccess) (void)hipGetLastError();   // context already active: keep its mode
-        }
+        // spinning wait would take a core from them -- blocking waits (r02az, C3:
+        // 1949 vs 1895 Mbp/s over 3 runs each); the scan's short waits poll
+        // (scan_wait)
+        if (hipSetDeviceFlags(hipDeviceScheduleBlockingSync) != hipSuccess) (void)hipGetLastError();
         HIPCHECK(hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking));
         HIPCHECK(hipEventCreate(&ctx->c.ev0));
         HIPCHECK(hipEventCreate(&ctx->c.ev1));
@@ -265,6 +277,7 @@ static void ctx_release(Ctx &c) {
     if (c.scratch_index) index_free(c.scratch_index);
     c.scratch_index = nullptr;
     for (auto &s : c.slot) s.release();
+    c.lb_ticket.release();
     for (auto &h : c.host) h.release();
     for (hipEvent_t e : c.evpool) (void)hipEventDestroy(e);
     c.evpool.clear();
@@ -287,6 +300,36 @@ static Ctx &scan_lane(Ctx &c, size_t k) {
     l.ktiming = c.ktiming;
     l.timing = c.timing;
     return l;
+}
+
+int bwtmi_bind_host(bwtmi_ctx *ctx, int on, int *changed) {
+    return guard([&] {
+        CHECK_ARG(ctx, "null argument");
+        const bool b = on ? bind_host_for(ctx->c.device) : unbind_host();
+        if (changed) *changed = b ? 1 : 0;
+    });
+}
+
+int bwtmi_host_binding_plan(const char *sysroot, int local_rank, const char *rank_pci, int threads, int smt,
+                            const char *allowed, char *out, int64_t cap, int *node, int *ranks_on_node) {
+    return guard([&] {
+        CHECK_ARG(sysroot && rank_pci && allowed && out && cap > 0, "null argument");
+        std::vector<std::string> pci;
+        for (const char *p = rank_pci; *p;) {
+            const char *e = std::strchr(p, ',');
+            pci.emplace_back(p, e ? (size_t)(e - p) : std::strlen(p));
+            p = e ? e + 1 : p + std::strlen(p);
+        }
+        cpu_set_t al, cs;
+        if (!parse_cpulist(allowed, al)) fail(BWTMI_E_ARG, "bad cpulist '%s'", allowed);
+        int nd = -1, peers = 0;
+        const bool b = plan_host_binding(sysroot, local_rank, pci, threads, smt != 0, al, cs, &nd, &peers);
+        const std::string str = b ? cpulist_str(cs) : std::string();
+        if ((int64_t)str.size() + 1 > cap) fail(BWTMI_E_ARG, "output buffer too small");
+        std::memcpy(out, str.c_str(), str.size() + 1);
+        if (node) *node = nd;
+        if (ranks_on_node) *ranks_on_node = peers;
+    });
 }
 
 int bwtmi_close(bwtmi_ctx *ctx) {
@@ -555,7 +598,6 @@ int bwtmi_job_free(bwtmi_job *job) {
         if (job->dev.bg_ctx) ctx_join(*job->dev.bg_ctx);   // its error stays for the ctx's next call
         if (job->dev.device >= 0) (void)hipSetDevice(job->dev.device);
         for (auto &d : job->dev.seqs) d.buf.release();
-        if (job->dev.post) ctx_release(*job->dev.post);
         delete job;
     });
 }
@@ -894,8 +936,7 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
         const char *fail_contig = std::getenv("BWTMI_FAIL_CONTIG");   // test hook: this contig's worker fails
         const char *fail_kind = std::getenv("BWTMI_FAIL_KIND");       // "hip": as a device fault
         // nested suppression + sort + dedup on the device (BWTMI_HOST_SCREEN=1: on the host)
-        const char *hs = std::getenv("BWTMI_HOST_SCREEN");
-        const bool screen = !(hs && *hs == '1');
+        const bool screen = knob(KN_HOST_SCREEN) == 0;
         J.final_recs.clear();
         J.postprocessed = false;
         const bwtmi_params &P = J.params;
@@ -952,10 +993,7 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
         // scan is a chain of small dependent launches and host reads, so one
         // stream leaves the device idle between them); contigs go to lanes
         // longest first, each to the least loaded lane
-        static const int kLanes = [] {
-            const char *e = std::getenv("BWTMI_SCAN_LANES");
-            return e && *e ? std::max(1, std::min(8, std::atoi(e))) : 4;
-        }();
+        const int kLanes = (int)std::max<int64_t>(1, std::min<int64_t>(8, knob(KN_SCAN_LANES)));
         const size_t nl = std::min<size_t>((size_t)kLanes, todo.size());
         if (nl <= 1) {
             for (size_t i : todo) scan_one(c, i);
@@ -1028,10 +1066,7 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
                 // host thread -- a 12.5 Mbp build is a chain of small launches and host
                 // reads that leaves the device mostly idle, and eight of them in a row
                 // outlasted the host stages of the 8-contig step (C4: 35 ms, r04final)
-                static const int kIndexLanes = [] {
-                    const char *e = std::getenv("BWTMI_INDEX_LANES");
-                    return e && *e ? std::max(1, std::min(8, std::atoi(e))) : 4;
-                }();
+                const int kIndexLanes = (int)std::max<int64_t>(1, std::min<int64_t>(8, knob(KN_INDEX_LANES)));
                 const size_t nl = std::min<size_t>((size_t)kIndexLanes, to_index.size());
                 if (nl <= 1) {
                     for (const auto &tx : to_index) build(c, tx);
@@ -1116,55 +1151,11 @@ int64_t bwtmi_job_raw_count(const bwtmi_job *job) {
     return n;
 }
 
-// a context of its own on `device` (stream, events; slots on first use)
-static std::unique_ptr<Ctx> aux_ctx(int device) {
-    auto l = std::make_unique<Ctx>();
-    l->device = device;
-    HIPCHECK(hipSetDevice(device));
-    HIPCHECK(hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking));
-    HIPCHECK(hipEventCreate(&l->ev0));
-    HIPCHECK(hipEventCreate(&l->ev1));
-    return l;
-}
-
 int bwtmi_job_postprocess(bwtmi_job *job) {
     return guard([&] {
         CHECK_ARG(job, "null argument");
         TEXT_JOIN(job);
         Job &J = job->j;
-        JobDev &d = job->dev;
-        // BWTMI_POST_DEVICE=1: the merge fold's fresh-pair recomputes go to the
-        // device when the contigs are resident there (after a scan or upload).
-        // Off by default: on the C3 step the batch (7.7 ms for 112k regions,
-        // request pass included) costs more than the host threads it relieves
-        // (spec 11.7 -> 10.6 ms; r03j A/B)
-        const char *pe = std::getenv("BWTMI_POST_DEVICE");
-        const bool on = pe && *pe == '1' && d.device >= 0;
-        J.rc_text.assign(J.contigs.size(), nullptr);
-        bool any = false;
-        if (on)
-            for (size_t i = 0; i < J.contigs.size() && i < d.seqs.size(); ++i) {
-                const DevContig &dc = d.seqs[i];
-                if (dc.buf.p && dc.n == J.contigs[i].trimmed_len() && dc.gen == J.contigs[i].gen) {
-                    J.rc_text[i] = dc.buf.as<char>();
-                    any = true;
-                }
-            }
-        if (any) {
-            if (!d.post) d.post = aux_ctx(d.device);
-            J.rc_batch = [&d](const RcReq *req, int64_t n, RcOut *out, std::vector<char> &arena) {
-                std::lock_guard<std::mutex> lk(d.post_mu);
-                d.post->activate();
-                recompute_batch_device(*d.post, req, n, out, arena);
-            };
-        }
-        struct Reset {
-            Job &J;
-            ~Reset() {
-                J.rc_batch = nullptr;
-                J.rc_text.clear();
-            }
-        } reset{J};
         postprocess(J);
     });
 }

@@ -1,6 +1,9 @@
 // common.h -- internal declarations shared by the libbwtmi translation units.
 #pragma once
 
+#include <sched.h>
+
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <exception>
@@ -247,7 +250,6 @@ struct RcOut {
 };
 constexpr int32_t kRcMaxMotif = 256;
 // runs a batch to completion: out[k] for every req[k], strings into arena
-using RcBatchFn = std::function<void(const RcReq *, int64_t, RcOut *, std::vector<char> &)>;
 
 // ---------------------------------------------------------------- job
 // formatted text in cached huge-page blocks (mem.h); the formatters write
@@ -338,10 +340,6 @@ struct Job {
     Seq part;
     std::string part_path;
     int64_t part_a = 0, part_b = 0, part_stamp[2] = {-1, -1};
-    // the merge fold's DP recomputes on the device (set by bwtmi_job_postprocess
-    // when the contigs are resident on a device; rc_text[c] = contig c's copy or null)
-    RcBatchFn rc_batch;
-    std::vector<const char *> rc_text;
     void assign_units();
     // host text written behind the device work (a whole-file load with device
     // placement, bwtmi_job_load_fasta_dev): every reader of contig bytes joins it
@@ -420,10 +418,28 @@ std::vector<int32_t> shard_units(Job &job, int32_t world, int32_t rank);
 int host_threads(const bwtmi_params &p);
 int host_cpu_budget(int *cpus_visible, int *local_world);
 // Host work (the calling thread now, the worker pools from their next region)
-// moves onto the CPUs of NUMA node `node` that the process may use -- the
-// node of its GPU (bwtmi_open).  False when nothing changed (BWTMI_NUMA_BIND=0,
-// already inside the node, or no such CPUs).
-bool bind_host_numa(int node);
+// moves onto the CPUs of the NUMA node of local rank `local_rank`'s GPU
+// (rank r drives the GPU at PCI address rank_pci[r]); asked for explicitly
+// (bwtmi_bind_host: the CLI, bench and rank launcher), never by bwtmi_open.
+// False when nothing changed (see plan_host_binding, post.cpp).
+bool bind_host_numa(int local_rank, const std::vector<std::string> &rank_pci);
+bool unbind_host();   // back to the affinity the binding replaced (calling thread now, workers at their next region)
+int gpu_numa_node(const char *sysroot, const char *pci);
+bool plan_host_binding(const char *sysroot, int local_rank, const std::vector<std::string> &rank_pci, int threads,
+                       bool smt, const cpu_set_t &allowed, cpu_set_t &out, int *node_out, int *ranks_on_node);
+std::string cpulist_str(const cpu_set_t &cs);
+bool parse_cpulist(const char *txt, cpu_set_t &cs);
+
+// ----- run-time switches (knobs.cpp): BWTMI_<NAME> read once from the
+// environment, changeable in-process through bwtmi_knob_set
+enum Knob {
+    KN_RUNS_DENSE, KN_RUNS_UNTILED, KN_SA_SMALL, KN_SEG_LEVELS, KN_SCREEN_WIDE, KN_FM_BYTES, KN_LS_CAP,
+    KN_HOST_SCREEN, KN_NO_PLAIN, KN_INDEX_LANES, KN_SCAN_LANES, KN_NO_AVX512, KN_POOL_SPIN_US,
+    KN_UNIT_GROUP_THREADS, KN_STATS, KN_NUMA_BIND, KN_NUMA_SMT, KN_FAIL_MERGE_CHUNK, KN_COUNT
+};
+extern std::atomic<int64_t> g_knobs[KN_COUNT];
+inline int64_t knob(Knob k) { return g_knobs[k].load(std::memory_order_relaxed); }
+inline bool stats_on(int level = 1) { return knob(KN_STATS) >= level; }
 int64_t fasta_count_records(const char *path, int64_t limit);   // fasta.cpp
 // fn(task) for task in [0, n) on up to nt threads (dynamic scheduling)
 void run_tasks(int64_t n, int nt, const std::function<void(int64_t)> &fn);

@@ -85,6 +85,7 @@ enum Slot {
     S_IDX0, S_IDX1, S_IDX2, S_IDX3, S_IDX4, S_IDX5, S_IDX6, S_IDX7, S_IDX8, S_IDX9, S_IDX10, S_IDX11,
     S_FASTA,   // a whole-file load's FASTA image (fasta_dev.hip)
     S_SORT_DIG,   // the next pass's digit of every key, written by a radix pass (radix.hip)
+    S_LB,         // look-back granules of the single-pass scans and radix histograms (radix.hip)
     S_NSLOTS
 };
 
@@ -185,6 +186,8 @@ struct Ctx {
         evused = 0;
     }
     DBuf slot[S_NSLOTS];
+    DBuf lb_ticket;          // the look-back launches' tile ticket (radix.hip)
+    uint32_t lb_epoch = 0;   // the last look-back launch's epoch
     HBuf host[4];
     struct DeviceIndex *scratch_index = nullptr;   // reused by the worker-path index builds
     // device work that runs behind host work (the worker-path index builds):
@@ -234,13 +237,8 @@ struct Ctx {
 // The scan's host reads (candidate counts, key widths, hit counts) wait on the
 // stream by polling: a blocking wait (hipDeviceScheduleBlockingSync, kept for
 // the long waits behind host work) sleeps the thread, and its wake-up delays
-// the next dependent launch.  BWTMI_SPIN_SCAN=0: blocking waits here too.
+// the next dependent launch.
 inline void scan_wait(hipStream_t st) {
-    static const bool spin = [] { const char *e = std::getenv("BWTMI_SPIN_SCAN"); return !(e && *e == '0'); }();
-    if (!spin) {
-        HIPCHECK(hipStreamSynchronize(st));
-        return;
-    }
     for (;;) {
         const hipError_t e = hipStreamQuery(st);
         if (e == hipSuccess) return;
@@ -296,7 +294,7 @@ void fasta_build_device(Ctx &c, const uint8_t *d_img, const FastaDevPiece *piece
 // first device work of a job: after tens of ms without device work the first
 // operation on the box pays ~5 ms (a 4-byte download 4.5-5.4 ms, the next
 // ones 0.03 ms; r04r), which then elapses behind the host work instead.
-// BWTMI_WAKE=0 disables.
+
 void device_wake(Ctx &c);
 
 // ----- strict scan (strict_scan.hip)

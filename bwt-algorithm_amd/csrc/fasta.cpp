@@ -266,7 +266,7 @@ void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, i
         Chunk &C = ck[(size_t)t];
         C.a = cut[(size_t)t];
         C.b = cut[(size_t)t + 1];
-        static const bool no_plain = std::getenv("BWTMI_NO_PLAIN") != nullptr;   // A/B switch
+        const bool no_plain = knob(KN_NO_PLAIN) != 0;   // A/B switch: every chunk line by line
         if (const int64_t nl = no_plain ? -1 : plain_newlines(p + C.a, C.b - C.a); nl >= 0) {   // no header: all content
             C.plain = true;
             C.pre = (C.b - C.a) - nl;
@@ -412,7 +412,7 @@ void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, i
     }
     const auto t2 = clk::now();
     auto stats = [&](const char *what) {
-        if (std::getenv("BWTMI_STATS")) {
+        if (stats_on()) {
             auto d = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
             std::fprintf(stderr, "  load_fasta: read %.1f pass1+stitch %.1f %s %.1f ms (%d threads, %lld chunks)\n",
                          d(t0, t1), d(t1, t2), what, d(t2, clk::now()), nt, (long long)T);
@@ -859,7 +859,7 @@ void fasta_load_parts(Job &job, const char *path, int32_t flank_trim, int32_t wo
         });
     };
     auto stats = [&] {
-        if (std::getenv("BWTMI_STATS")) {
+        if (stats_on()) {
             auto d = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
             std::fprintf(stderr, "  load_fasta_parts: stitch %.1f own contigs %.1f ms%s\n", d(t0, t1), d(t1, clk::now()),
                          dev ? " (device placement)" : "");

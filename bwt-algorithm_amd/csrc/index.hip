@@ -678,7 +678,7 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
                                    sa_sample);
     // ACGT with assembly gaps (N runs, a few IUPAC codes): the same string sort
     // over 3-bit symbol codes (BWTMI_SA_SMALL=0: the general doubling instead)
-    static const bool small_ok = [] { const char *e = std::getenv("BWTMI_SA_SMALL"); return !(e && *e == '0'); }();
+    const bool small_ok = knob(KN_SA_SMALL) != 0;
     uint8_t slut[256], ssym[8];
     const bool small = !dna && small_ok && sa_small_alphabet(last, n, ix->totals, slut, ssym) > 0 &&
                        sa_small_device(c, T, n, ix->sa.as<uint32_t>(), ix->bwt.as<uint8_t>(),
@@ -939,7 +939,7 @@ void index_backward_search(Ctx &c, DeviceIndex *ix, const uint8_t *pats, const i
     HIPCHECK(hipMemcpyAsync(tabs, ix->C, 256 * 8, hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemcpyAsync(tabs + 256, ix->totals, 256 * 8, hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemcpyAsync(tabs + 512, ix->code_of, 256, hipMemcpyHostToDevice, st));
-    if (ix->has_fm2 && !std::getenv("BWTMI_FM_BYTES")) {
+    if (ix->has_fm2 && !knob(KN_FM_BYTES)) {
         FM2View g;
         g.blk = ix->fm2.as<uint4>();
         const char sym[5] = {'A', 'C', 'G', 'T', '$'};

@@ -879,7 +879,7 @@ void short_imperfect_device(Ctx &c, DeviceIndex *ix, const LibParams &p, const s
     const int64_t n = index_n(ix);
     if (n > 1000000 || n == 0) return;                    // bwt.py:2048
     using clk = std::chrono::steady_clock;
-    const bool stats = [] { const char *e = std::getenv("BWTMI_STATS"); return e && *e == '1'; }();
+    const bool stats = stats_on();
     const auto T0 = clk::now();
     auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     const int kmin = std::max(1, p.min_period), kend = std::min(p.max_short_motif + 1, 10);
@@ -1540,7 +1540,7 @@ void simple_scan_device(Ctx &c, DeviceIndex *ix, const LibParams &P, const std::
     constexpr int kLook = 512;   // look-ahead positions per walk and round
     hipStream_t st = c.stream;
     using clk = std::chrono::steady_clock;
-    const bool stats = [] { const char *e = std::getenv("BWTMI_STATS"); return e && *e == '1'; }();
+    const bool stats = stats_on();
     double t_host = 0, t_dev = 0;
     int64_t rounds = 0, nreq = 0;
     auto T0 = clk::now();

@@ -423,8 +423,7 @@ __attribute__((target("avx512f,avx512bw,avx512vl"))) static int dp_rows_avx512(
 
 static const bool g_avx512 = [] {
     __builtin_cpu_init();
-    const char *e = std::getenv("BWTMI_NO_AVX512");
-    return !(e && *e == '1') && __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+    return !knob(KN_NO_AVX512) && __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
            __builtin_cpu_supports("avx512vl");
 }();
 

@@ -517,7 +517,7 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     KLAUNCH("k_gather", 0.0, k_gather, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, S, E, M, rank_of, kept);
     prefix_max(c, E, PME, n, c.slot[S_IDX5].as<int64_t>());
     // every level, segment by segment, in one launch (BWTMI_SEG_LEVELS=0: per-level launches)
-    static const bool seg_levels = [] { const char *e = std::getenv("BWTMI_SEG_LEVELS"); return !(e && *e == '0'); }();
+    const bool seg_levels = knob(KN_SEG_LEVELS) != 0;
     unsigned int *d_ovf = reinterpret_cast<unsigned int *>(d_max);   // [0] fallback flag, [1] overflow windows
     unsigned int ovf = 1;
     if (seg_levels) {
@@ -538,7 +538,7 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     // one word per kept hit when the start fits the low half and the longest span
     // and the longest primitive motif fit the high half (BWTMI_SCREEN_WIDE=1:
     // always two)
-    static const bool wide = [] { const char *e = std::getenv("BWTMI_SCREEN_WIDE"); return e && *e == '1'; }();
+    const bool wide = knob(KN_SCREEN_WIDE) != 0;
     const int lbits = lb;   // bits of the longest span (hit lengths are <= maxlen)
     const int pbits = std::max(1, bits_for((uint64_t)lmax));
     out.lbits = !wide && lbits + pbits <= 32 && bits_for((uint64_t)text_len) <= 32 ? lbits : -1;

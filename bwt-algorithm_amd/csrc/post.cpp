@@ -104,15 +104,24 @@ inline void apply_binding() {
     (void)sched_setaffinity(0, sizeof cs, &cs);
     tl_bind_epoch = e;
 }
-bool read_cpulist(const char *path, cpu_set_t &cs) {   // "0-63,128-191"
-    FILE *f = std::fopen(path, "r");
-    if (!f) return false;
-    char buf[4096];
-    const bool ok = std::fgets(buf, sizeof buf, f) != nullptr;
-    std::fclose(f);
-    if (!ok) return false;
+}  // namespace
+
+std::string cpulist_str(const cpu_set_t &cs) {
+    std::string s;
+    for (int c = 0; c < CPU_SETSIZE; ++c) {
+        if (!CPU_ISSET(c, &cs)) continue;
+        int e = c;
+        while (e + 1 < CPU_SETSIZE && CPU_ISSET(e + 1, &cs)) ++e;
+        if (!s.empty()) s += ',';
+        s += std::to_string(c);
+        if (e > c) s += '-' + std::to_string(e);
+        c = e;
+    }
+    return s;
+}
+bool parse_cpulist(const char *txt, cpu_set_t &cs) {
     CPU_ZERO(&cs);
-    for (char *p = buf; *p && *p != '\n';) {
+    for (const char *p = txt; p && *p && *p != '\n';) {
         char *e;
         const long a = std::strtol(p, &e, 10);
         if (e == p) return false;
@@ -126,52 +135,100 @@ bool read_cpulist(const char *path, cpu_set_t &cs) {   // "0-63,128-191"
         for (long c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET((int)c, &cs);
         if (*p == ',') ++p;
     }
-    return CPU_COUNT(&cs) > 0;
+    return true;
 }
+namespace {
+int read_int(const std::string &path, int def) {
+    int v = def;
+    if (FILE *f = std::fopen(path.c_str(), "r")) {
+        if (std::fscanf(f, "%d", &v) != 1) v = def;
+        std::fclose(f);
+    }
+    return v;
+}
+int g_bound_node = -1;   // the node host work is bound to (under g_bind_mu)
+cpu_set_t g_orig_set;    // the affinity the first binding replaced
 }  // namespace
 
-bool bind_host_numa(int node) {
-    static const bool on = [] { const char *e = std::getenv("BWTMI_NUMA_BIND"); return !(e && *e == '0'); }();
-    if (!on || node < 0) return false;
-    char path[96];
-    std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
-    cpu_set_t want, cur, both;
-    if (!read_cpulist(path, want)) return false;
-    if (sched_getaffinity(0, sizeof cur, &cur) != 0) return false;
-    CPU_AND(&both, &want, &cur);
-    // nothing to gain when the process already runs inside the node; no
-    // binding that leaves fewer CPUs than the host threads of a rank (a small
-    // cpuset split over both nodes)
-    int lw = 1;
-    const int budget = host_cpu_budget(nullptr, &lw);
-    if (CPU_EQUAL(&both, &cur) || CPU_COUNT(&both) < budget) return false;
-    // one hardware thread per physical core when the node's cores can hold
-    // every rank's threads (host workers + runtime threads) without sharing a
-    // core: two workers on the siblings of one core run the memory-bound host
-    // passes at well under half speed each (BWTMI_NUMA_SMT=1 keeps siblings)
-    static const bool smt = [] { const char *e = std::getenv("BWTMI_NUMA_SMT"); return e && *e == '1'; }();
+// The NUMA node of a GPU from its PCI address ("0000:75:00.0"), -1 unknown
+int gpu_numa_node(const char *sysroot, const char *pci) {
+    std::string id(pci ? pci : "");
+    for (auto &ch : id) ch = (char)std::tolower((unsigned char)ch);
+    return read_int(std::string(sysroot) + "/bus/pci/devices/" + id + "/numa_node", -1);
+}
+
+// Pure planner (no affinity change; sysfs read under `sysroot`, "/sys" on a
+// host, a faked tree in the tests).  Local rank r of the node drives the GPU
+// at rank_pci[r]; this rank's GPU is rank_pci[local_rank].  The set: the
+// `allowed` CPUs of this GPU's NUMA node; with one hardware thread per
+// physical core when those cores can hold every local rank WHOSE GPU SITS ON
+// THAT NODE with `threads` workers + 4 runtime threads each (two workers on
+// the siblings of one core run the memory-bound host passes at well under
+// half speed each; smt keeps the siblings).  False (no binding): unknown
+// node, the process already runs inside the node, or fewer allowed CPUs there
+// than `threads` (a small cpuset split over both nodes).
+bool plan_host_binding(const char *sysroot, int local_rank, const std::vector<std::string> &rank_pci, int threads,
+                       bool smt, const cpu_set_t &allowed, cpu_set_t &out, int *node_out, int *ranks_on_node) {
+    if (local_rank < 0 || local_rank >= (int)rank_pci.size()) return false;
+    const int node = gpu_numa_node(sysroot, rank_pci[(size_t)local_rank].c_str());
+    if (node_out) *node_out = node;
+    if (node < 0) return false;
+    int peers = 0;
+    for (const auto &p : rank_pci) peers += gpu_numa_node(sysroot, p.c_str()) == node;
+    if (ranks_on_node) *ranks_on_node = peers;
+    cpu_set_t want, both;
+    FILE *f = std::fopen((std::string(sysroot) + "/devices/system/node/node" + std::to_string(node) + "/cpulist").c_str(), "r");
+    if (!f) return false;
+    char buf[4096];
+    const bool ok = std::fgets(buf, sizeof buf, f) != nullptr;
+    std::fclose(f);
+    if (!ok || !parse_cpulist(buf, want)) return false;
+    CPU_AND(&both, &want, &allowed);
+    if (CPU_EQUAL(&both, &allowed) || CPU_COUNT(&both) < threads) return false;
     if (!smt) {
         cpu_set_t one;
         CPU_ZERO(&one);
         std::vector<std::pair<int, int>> seen;   // (package, core) taken
         for (int c = 0; c < CPU_SETSIZE; ++c) {
             if (!CPU_ISSET(c, &both)) continue;
-            int pkg = -1, core = -1;
-            char q[128];
-            std::snprintf(q, sizeof q, "/sys/devices/system/cpu/cpu%d/topology/physical_package_id", c);
-            if (FILE *f = std::fopen(q, "r")) { if (std::fscanf(f, "%d", &pkg) != 1) pkg = -1; std::fclose(f); }
-            std::snprintf(q, sizeof q, "/sys/devices/system/cpu/cpu%d/topology/core_id", c);
-            if (FILE *f = std::fopen(q, "r")) { if (std::fscanf(f, "%d", &core) != 1) core = -1; std::fclose(f); }
+            const std::string t = std::string(sysroot) + "/devices/system/cpu/cpu" + std::to_string(c) + "/topology/";
+            const int pkg = read_int(t + "physical_package_id", -1), core = read_int(t + "core_id", -1);
             if (pkg < 0 || core < 0) { CPU_ZERO(&one); break; }   // no topology: keep the node set
             if (std::find(seen.begin(), seen.end(), std::make_pair(pkg, core)) != seen.end()) continue;
             seen.emplace_back(pkg, core);
             CPU_SET(c, &one);
         }
-        if (CPU_COUNT(&one) >= lw * (budget + 4)) both = one;
+        if (CPU_COUNT(&one) >= peers * (threads + 4)) both = one;
     }
+    out = both;
+    return true;
+}
+
+bool bind_host_numa(int local_rank, const std::vector<std::string> &rank_pci) {
+    cpu_set_t cur, want;
+    if (sched_getaffinity(0, sizeof cur, &cur) != 0) return false;
+    int node = -1;
+    if (!plan_host_binding("/sys", local_rank, rank_pci, host_cpu_budget(nullptr, nullptr), knob(KN_NUMA_SMT) != 0, cur,
+                           want, &node, nullptr))
+        return false;
     {
         std::lock_guard<std::mutex> lk(g_bind_mu);
-        g_bind_set = both;
+        if (g_bound_node >= 0 && g_bound_node != node) return false;   // contexts on two nodes: keep the first
+        if (g_bound_node < 0) g_orig_set = cur;
+        g_bound_node = node;
+        g_bind_set = want;
+    }
+    g_bind_epoch.fetch_add(1, std::memory_order_acq_rel);
+    apply_binding();
+    return true;
+}
+
+bool unbind_host() {
+    {
+        std::lock_guard<std::mutex> lk(g_bind_mu);
+        if (g_bound_node < 0) return false;
+        g_bound_node = -1;
+        g_bind_set = g_orig_set;
     }
     g_bind_epoch.fetch_add(1, std::memory_order_acq_rel);
     apply_binding();
@@ -192,13 +249,7 @@ namespace {
 // C3 +4 % on average, inside the run-to-run spread; W=8 shard step 8.0-8.1 vs
 // 8.6-8.9 ms), while a 60 us spin, also held through longer serial parts, cost
 // the C3 line ~7 % on another box (r03z).  0 = block at once.
-inline int64_t pool_spin_ns() {
-    static const int64_t ns = [] {
-        const char *e = std::getenv("BWTMI_POOL_SPIN_US");
-        return (int64_t)((e && *e) ? std::atof(e) * 1000.0 : 10000.0);
-    }();
-    return ns;
-}
+inline int64_t pool_spin_ns() { return knob(KN_POOL_SPIN_US) * 1000; }
 inline int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -368,14 +419,8 @@ static void parallel_items(int64_t n, int nt, F &&fn) {
 // static blocks: worker w takes items [n w / nt, n (w + 1) / nt) -- for the
 // memory-bound passes over the fold's chunks, so that a chunk is read by the
 // worker (and the core's cache) that wrote it in the pass before
-// (BWTMI_STATIC_PASSES=0: dynamic, as parallel_items)
 template <class F>
 static void parallel_blocks(int64_t n, int nt, F &&fn) {
-    static const bool on = [] { const char *e = std::getenv("BWTMI_STATIC_PASSES"); return !(e && *e == '0'); }();
-    if (!on) {
-        parallel_items(n, nt, fn);
-        return;
-    }
     if (n <= 0) return;
     nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n));
     auto work = [&](int w) {
@@ -586,23 +631,10 @@ struct Pools {
     }
 };
 
-// the merge fold's recomputes for neighbour pairs (R[i-1], R[i]) met with a
-// fresh current record, run on the device before the fold (merge_fold)
-struct RcTable {
-    std::vector<int32_t> at;   // at[i]: request of the pair (R[i-1], R[i]), -1 none
-    // canonical words the pass computed: kst[i] = 1: key[i] is R[i]'s packed canonical form
-    std::vector<unsigned __int128, BigAlloc<unsigned __int128>> key;
-    std::vector<uint8_t, BigAlloc<uint8_t>> kst;
-    std::vector<RcReq> req;
-    std::vector<RcOut> out;
-    std::vector<char> arena;
-};
-
 struct UnitCtx {
     const Job *job;
     int64_t min_copies;
     bool restored = false;        // items are in full-sequence coordinates (multi-offset units)
-    const RcTable *rc = nullptr;  // merge_fold only
 };
 
 inline std::string_view motif_of(const UnitCtx &u, const Item &it) {
@@ -770,8 +802,6 @@ inline char comp_of(char c) {   // bwt.py:688-691
 
 std::atomic<int64_t> g_recomputes{0}, g_recompute_ns{0}, g_merges{0}, g_canons{0}, g_tests{0}, g_same{0}, g_walk_reuse{0};
 // BWTMI_STATS=1: stage timers; =2: also per-recompute / per-test counters (slow)
-const bool g_stats = [] { const char *e = std::getenv("BWTMI_STATS"); return e && (*e == '1' || *e == '2'); }();
-const bool g_counters = [] { const char *e = std::getenv("BWTMI_STATS"); return e && *e == '2'; }();
 const char *const g_dump = std::getenv("BWTMI_DUMP_RECOMPUTE");
 std::atomic<int64_t> g_hist_n[8][8], g_hist_ns[8][8];
 std::atomic<int64_t> g_fresh_tests{0}, g_chain_tests{0}, g_fresh_merges{0}, g_chain_merges{0};   // [log4 motif len][log4 region len]
@@ -794,9 +824,9 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     struct Tick {   // BWTMI_STATS=2 only
         int a, b;
         std::chrono::steady_clock::time_point t;
-        Tick(int a_, int b_) : a(a_), b(b_) { if (g_counters) t = std::chrono::steady_clock::now(); }
+        Tick(int a_, int b_) : a(a_), b(b_) { if (stats_on(2)) t = std::chrono::steady_clock::now(); }
         ~Tick() {
-            if (!g_counters) return;
+            if (!stats_on(2)) return;
             const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t).count();
             g_recomputes.fetch_add(1, std::memory_order_relaxed);
             g_recompute_ns.fetch_add(ns, std::memory_order_relaxed);
@@ -880,7 +910,7 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
         A.wk_stop < walk_limit(A.wk_phase == 1 ? mc : 1)) {
         // the same windows up to the same failing copy: the same record, but
         // for what depends on the call itself (the requested end, the tier)
-        if (g_counters) g_walk_reuse.fetch_add(1, std::memory_order_relaxed);
+        if (stats_on(2)) g_walk_reuse.fetch_add(1, std::memory_order_relaxed);
         Extra *x = pools.clone(w, *A.wk_item.x);
         x->req_end = req_end;
         x->tier = tier;
@@ -899,7 +929,7 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     int phase = 1;
     // resume: a chain of merges recomputes a growing region from one start,
     // and each walk that stopped at its limit goes on from where it stopped
-    static const bool resume = [] { const char *e = std::getenv("BWTMI_WALK_RESUME"); return !(e && *e == '0'); }();
+    constexpr bool resume = true;
     bool ok = align_repeat_region(seq, L, start, end, tmpl, mc, s, 0.1, -1, A.as.get(), resume);
     if (!ok) {
         phase = 2;
@@ -1008,7 +1038,7 @@ struct Canon {
 // and of its reverse complement (the packed word orders like the string)
 inline void canon_fill(const UnitCtx &u, const Item &it, Canon &c) {
     if (c.ok) return;
-    if (g_counters) g_canons.fetch_add(1, std::memory_order_relaxed);
+    if (stats_on(2)) g_canons.fetch_add(1, std::memory_order_relaxed);
     const std::string_view mv = motif_of(u, it);
     c.len = (int32_t)mv.size();
     uint64_t x;
@@ -1040,55 +1070,23 @@ inline bool same_canonical(const UnitCtx &u, const Item &r1, Canon &c1, const It
     return c1.packed ? c1.key == c2.key : c1.s == c2.s;
 }
 
-// the pair's device result when r1 is the fresh R[pair - 1] and r2 = R[pair]
-// (the request was built from the same two records, so its arguments are this
-// call's), else the host recompute
-inline Item recompute_pair(const UnitCtx &u, Pools &pools, int w, int64_t pair, int32_t chrom, int64_t s, int64_t e,
-                           int64_t m, int32_t tier) {
-    if (pair >= 0 && u.rc) {
-        const int32_t k = u.rc->at[(size_t)pair];
-        if (k >= 0 && u.rc->out[(size_t)k].status >= 0) {
-            const RcReq &q = u.rc->req[(size_t)k];
-            const RcOut &o = u.rc->out[(size_t)k];
-            const Contig &c = u.job->contigs[(size_t)chrom];
-            const std::string_view tmpl(c.trimmed() + q.start, (size_t)q.m);
-            RcView v;
-            v.ok = o.status == 1;
-            if (v.ok) {
-                v.consumed = o.consumed;
-                v.copies = o.copies;
-                v.motif_len = q.m;
-                v.max_err = o.max_err;
-                v.tot_ins = o.tot_ins;
-                v.tot_del = o.tot_del;
-                const int64_t denom = o.copies * (int64_t)q.m;
-                v.mm = denom > 0 ? (double)o.tot_err / (double)denom : 0.0;
-                const char *str = u.rc->arena.data() + o.str_off;
-                v.consensus = std::string_view(str, (size_t)q.m);
-                v.var = std::string_view(str + q.m, (size_t)(o.str_len - q.m));
-            }
-            return item_of_alignment(u, pools, w, chrom, q.start, q.end, m, tier, tmpl, v);
-        }
-    }
-    return recompute(u, pools, w, chrom, s, e, m, tier);
-}
 
 bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, Canon &c1, const Item &r2, Canon &c2,
-               Item &merged, int64_t pair = -1) {
+               Item &merged) {
     if (r1.chrom != r2.chrom) return false;
     if (r1.mlen == 0 || r2.mlen == 0) return false;
     const int64_t ml = std::min(r1.mlen, r2.mlen);
     if (std::max<int64_t>(0, r2.start - r1.end) > ml + 1) return false;   // cheap test first
-    if (g_counters) g_tests.fetch_add(1, std::memory_order_relaxed);
+    if (stats_on(2)) g_tests.fetch_add(1, std::memory_order_relaxed);
     if (!same_canonical(u, r1, c1, r2, c2)) return false;
-    if (g_counters) g_same.fetch_add(1, std::memory_order_relaxed);
+    if (stats_on(2)) g_same.fetch_add(1, std::memory_order_relaxed);
     const int64_t s = std::min(r1.start, r2.start), e = std::max(r1.end, r2.end);
     const int32_t tier = std::min(tier_of(r1), tier_of(r2));
-    Item mg = recompute_pair(u, pools, w, pair, r1.chrom, s, e, std::max<int64_t>(1, ml), tier);
+    Item mg = recompute(u, pools, w, r1.chrom, s, e, std::max<int64_t>(1, ml), tier);
     if (mg.x->copies < (double)u.min_copies) return false;
     const double base = std::max(std::max(mm_of(r1), mm_of(r2)), 0.01);
     if (!(mg.x->mm <= base + 0.2)) return false;
-    if (g_counters) g_merges.fetch_add(1, std::memory_order_relaxed);
+    if (stats_on(2)) g_merges.fetch_add(1, std::memory_order_relaxed);
     if ((int64_t)r1.mlen == std::max<int64_t>(1, ml)) merged = mg;   // len(r1.consensus_motif)
     else merged = recompute(u, pools, w, r1.chrom, s, e, r1.mlen, tier);
     return true;
@@ -1134,13 +1132,9 @@ void spec_run(const UnitCtx &u, Pools &pools, int w, const ItemVec &R, int64_t b
     for (int64_t i = b + 1; i < e; ++i) {
         Canon &cc = cb[ci_cur], &ci = cb[ci_cur ^ 1];
         ci.ok = false;
-        if (u.rc && u.rc->kst[(size_t)i]) {   // computed by rc_prepare
-            ci.key = u.rc->key[(size_t)i];
-            ci.packed = ci.ok = true;
-        }
-        if (g_counters) (merged ? g_chain_tests : g_fresh_tests).fetch_add(1, std::memory_order_relaxed);
-        if (try_merge(u, pools, w, cur, cc, R[(size_t)i], ci, mg, merged ? -1 : i)) {
-            if (g_counters) (merged ? g_chain_merges : g_fresh_merges).fetch_add(1, std::memory_order_relaxed);
+        if (stats_on(2)) (merged ? g_chain_tests : g_fresh_tests).fetch_add(1, std::memory_order_relaxed);
+        if (try_merge(u, pools, w, cur, cc, R[(size_t)i], ci, mg)) {
+            if (stats_on(2)) (merged ? g_chain_merges : g_fresh_merges).fetch_add(1, std::memory_order_relaxed);
             cur = mg;
             merged = true;
             cc.ok = false;
@@ -1179,71 +1173,6 @@ inline void refine_one(const UnitCtx &u, Pools &pools, int w, Item &r) {
     r = recompute(u, pools, w, r.chrom, r.start, r.end, m, tier_of(r));
 }
 
-// The requests of every neighbour pair (R[i-1], R[i]) that try_merge would
-// recompute with a fresh current record (same contig, gap test, same canonical
-// motif; bwt.py:3240-3262) and a motif of 2..kRcMaxMotif bases, run as one
-// device batch.  Pairs the fold never tests with a fresh record cost device
-// time only; the one-base motifs keep their closed form on the host.
-void rc_prepare(const UnitCtx &u, const ItemVec &R, int nt, RcTable &T) {
-    const Job &job = *u.job;
-    const int64_t n = (int64_t)R.size();
-    T.at.assign((size_t)n, -1);
-    T.key.resize((size_t)n);
-    T.kst.assign((size_t)n, 0);
-    const int C = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)nt * 4, n / 4096 + 1));
-    std::vector<std::vector<std::pair<int64_t, RcReq>>> part((size_t)C);
-    const int32_t mc = (int32_t)std::max<int64_t>(1, u.min_copies);
-    parallel_items(C, nt, [&](int64_t t, int) {
-        auto &out = part[(size_t)t];
-        Canon cb[2];
-        int64_t have = -1;   // R index whose canonical form is in cb[have & 1]
-        const int64_t lo = n * t / C;
-        auto keep = [&](int64_t k, const Canon &c) {   // records of this chunk only
-            if (k >= lo && c.ok && c.packed && !T.kst[(size_t)k]) {
-                T.key[(size_t)k] = c.key;
-                T.kst[(size_t)k] = 1;
-            }
-        };
-        for (int64_t i = std::max<int64_t>(1, lo); i < n * (t + 1) / C; ++i) {
-            const Item &r1 = R[(size_t)i - 1], &r2 = R[(size_t)i];
-            if (r1.chrom != r2.chrom || r1.mlen == 0 || r2.mlen == 0) continue;
-            const int64_t ml = std::min(r1.mlen, r2.mlen);
-            if (std::max<int64_t>(0, r2.start - r1.end) > ml + 1) continue;
-            const int64_t m = std::max<int64_t>(1, ml);
-            if (m < 2 || m > kRcMaxMotif) continue;
-            const char *text = (size_t)r1.chrom < job.rc_text.size() ? job.rc_text[(size_t)r1.chrom] : nullptr;
-            if (!text) continue;
-            Canon &c1 = cb[(i - 1) & 1], &c2 = cb[i & 1];
-            if (have != i - 1) c1.ok = false;
-            c2.ok = false;
-            have = i;
-            const bool same = same_canonical(u, r1, c1, r2, c2);
-            keep(i - 1, c1);
-            keep(i, c2);
-            if (!same) continue;
-            const Contig &c = job.contigs[(size_t)r1.chrom];
-            const int64_t L = c.trimmed_len();
-            const int64_t start = std::max<int64_t>(0, std::min(r1.start, r2.start));
-            const int64_t e = std::max(r1.end, r2.end);
-            int64_t end = e > 0 ? std::min(L, e) : L;
-            if (end <= start) end = std::min(L, start + m);
-            if (start + m > L) continue;
-            out.push_back({i, RcReq{text, L, start, end, (int32_t)m, mc}});
-        }
-    });
-    size_t tot = 0;
-    for (auto &p : part) tot += p.size();
-    T.req.resize(tot);
-    size_t k = 0;
-    for (auto &p : part)
-        for (auto &e : p) {
-            T.at[(size_t)e.first] = (int32_t)k;
-            T.req[k++] = e.second;
-        }
-    T.out.resize(tot);
-    if (tot) job.rc_batch(T.req.data(), (int64_t)tot, T.out.data(), T.arena);
-}
-
 // the fold's output, refined (the refine pass runs inside the parallel
 // assembly: records are independent there)
 // chunks of the fold's output for the collapse pass: [cut[k], cut[k+1]) with
@@ -1261,46 +1190,28 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt, Ou
                    const std::function<void(int64_t, int64_t)> *fill = nullptr) {
     const int64_t n = (int64_t)R.size();
     if (n == 0) return {};
-    // BWTMI_POST_DEVICE_MIN: smallest unit (records) whose fresh-pair recomputes go to the device
-    static const int64_t dev_min = [] {
-        const char *e = std::getenv("BWTMI_POST_DEVICE_MIN");
-        return e && *e ? std::atoll(e) : (int64_t)20000;
-    }();
-    RcTable rc;
-    UnitCtx u = u0;
-    if (fill && u0.job->rc_batch && n >= dev_min) {   // the request pass reads every record first
-        parallel_for(n, nt, [&](int64_t a, int64_t b) { (*fill)(a, b); });
-        fill = nullptr;
-    }
-    if (u0.job->rc_batch && n >= dev_min) {
-        auto tr0 = std::chrono::steady_clock::now();
-        rc_prepare(u0, R, nt, rc);
-        u.rc = &rc;
-        if (g_stats)
-            std::fprintf(stderr, "  merge device recomputes: %zu in %.1f ms\n", rc.req.size(),
-                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count());
-    }
+    const UnitCtx &u = u0;
     const int64_t K = std::max<int64_t>(1, std::min<int64_t>((int64_t)nt * 8, n / 2048 + 1));
     std::vector<int64_t> cut((size_t)K + 1);
     for (int64_t k = 0; k <= K; ++k) cut[(size_t)k] = n * k / K;
     std::vector<uint8_t, BigAlloc<uint8_t>> fresh((size_t)n, 0);
     std::vector<SpecOut> spec((size_t)K);
     auto ts0 = std::chrono::steady_clock::now();
-    std::vector<double> cms(g_stats ? (size_t)K : 0);
-    // test hook: BWTMI_FAIL_MERGE_CHUNK=k throws inside worker task k (k < 0: the last
+    std::vector<double> cms(stats_on() ? (size_t)K : 0);
+    // test hook: BWTMI_FAIL_MERGE_CHUNK=k throws inside worker task k (-2: the last
     // task) -- the pool must hand the error back through the C ABI (tests/test_host.py)
-    const char *inj_e = std::getenv("BWTMI_FAIL_MERGE_CHUNK");
-    const int64_t inj = inj_e ? (std::atoll(inj_e) < 0 ? K - 1 : std::atoll(inj_e)) : -1;
+    const int64_t inj_k = knob(KN_FAIL_MERGE_CHUNK);
+    const int64_t inj = inj_k == -1 ? -1 : inj_k < 0 ? K - 1 : inj_k;
     auto spec_task = [&](int64_t k, int w) {
         if (k == inj) fail(BWTMI_E_STATE, "injected failure in merge task %lld", (long long)k);
         auto a = std::chrono::steady_clock::now();
         if (fill) (*fill)(cut[(size_t)k], cut[(size_t)k + 1]);
         spec_run(u, pools, w, R, cut[(size_t)k], cut[(size_t)k + 1], fresh, spec[(size_t)k]);
-        if (g_stats) cms[(size_t)k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+        if (stats_on()) cms[(size_t)k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
     };
     parallel_items(K, nt, spec_task);   // dynamic: the chunks' costs are uneven (r04ze: static blocks no better)
     auto ts1 = std::chrono::steady_clock::now();
-    if (g_stats) {
+    if (stats_on()) {
         double sum = 0, mx = 0;
         for (double v : cms) { sum += v; mx = std::max(mx, v); }
         std::fprintf(stderr, "  merge spec %.1f ms (K=%lld, chunk sum %.1f max %.1f ms)\n",
@@ -1414,7 +1325,7 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt, Ou
         oc->cut.push_back((int64_t)N);
         oc->cmax.assign(cm.begin(), cm.end());
     }
-    if (g_stats) {
+    if (stats_on()) {
         auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         std::fprintf(stderr, "  merge: repair %.1f assemble %.1f ms\n", d(ts1, ts2),
                      d(ts2, std::chrono::steady_clock::now()));
@@ -1580,8 +1491,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     // one device-screened contig (the usual unit): its compact hits become
     // records inside the merge fold's speculative tasks, chunk by chunk
     std::function<void(int64_t, int64_t)> fill_fn;
-    static const bool fused_fill = [] { const char *e = std::getenv("BWTMI_FUSED_ITEMS"); return !(e && *e == '0'); }();
-    if (fused_fill && chroms.size() == 1) {
+    if (chroms.size() == 1) {
         const int32_t c = chroms[0];
         const bool scr = (size_t)c < job.screened.size() && job.screened[(size_t)c] && (size_t)c < shits.size();
         const bool mine = job.selected.empty() || ((size_t)c < job.selected.size() && job.selected[(size_t)c]);
@@ -1777,7 +1687,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
         if (err) std::rethrow_exception(err);
     }
     auto t4 = clk::now();
-    if (std::getenv("BWTMI_STATS")) {
+    if (stats_on()) {
         auto d = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         std::fprintf(stderr, "  merge %.1f (-> %zu) refine %.1f sort %.1f restore+sort %.1f collapse %.1f (%zu -> %zu) filter+mat %.1f ms\n",
                      d(t2, t3), n_before_collapse, d(t3, r1), d(r1, r2), d(r2, r3), d(r3, t_collapse), n_before_collapse,
@@ -1808,10 +1718,7 @@ void postprocess(Job &job) {
     // a few units and threads to spare: G groups of T / G threads, each its own
     // pool, take units longest first (a unit's parallel regions carry serial
     // parts and joins that one 16-thread region per unit paid unit by unit)
-    static const int kGroupThreads = [] {
-        const char *e = std::getenv("BWTMI_UNIT_GROUP_THREADS");
-        return e && *e ? std::max(1, std::atoi(e)) : 4;
-    }();
+    const int kGroupThreads = (int)std::max<int64_t>(1, knob(KN_UNIT_GROUP_THREADS));
     const int G = (int)std::min<int64_t>(busy, T / kGroupThreads);
     if (busy >= T) {
         parallel_items(job.nunits, T, [&](int64_t k, int) {
@@ -1853,7 +1760,7 @@ void postprocess(Job &job) {
         for (int32_t k = 0; k < job.nunits; ++k) {
             auto a = std::chrono::steady_clock::now();
             process_unit(job, units[(size_t)k], job.hits, job.shits, res[(size_t)k], &ms[(size_t)k * 4], T);
-            if (g_stats)
+            if (stats_on())
                 std::fprintf(stderr, "  unit %d: %.1f ms total\n", k,
                              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count());
         }
@@ -1890,19 +1797,19 @@ void postprocess(Job &job) {
         job.stage_ms[2 + s] = 0;
         for (int32_t k = 0; k < job.nunits; ++k) job.stage_ms[2 + s] += ms[(size_t)k * 4 + s];
     }
-    if (g_counters)
+    if (stats_on(2))
         std::fprintf(stderr, "[bwtmi] recomputes=%lld (%.1f ms thread-summed; %lld reused walks) merges=%lld canons=%lld "
                      "final=%zu\n", (long long)g_recomputes.exchange(0), g_recompute_ns.exchange(0) / 1e6,
                      (long long)g_walk_reuse.exchange(0), (long long)g_merges.exchange(0),
                      (long long)g_canons.exchange(0), job.final_recs.size());
-    if (g_counters)
+    if (stats_on(2))
         std::fprintf(stderr, "[bwtmi] merge tests past the gap test=%lld, same canonical=%lld\n",
                      (long long)g_tests.exchange(0), (long long)g_same.exchange(0));
-    if (g_counters)
+    if (stats_on(2))
         std::fprintf(stderr, "[bwtmi] fold steps with a fresh current record=%lld (merged %lld), with a merged one=%lld (merged %lld)\n",
                      (long long)g_fresh_tests.exchange(0), (long long)g_fresh_merges.exchange(0),
                      (long long)g_chain_tests.exchange(0), (long long)g_chain_merges.exchange(0));
-    if (g_counters)
+    if (stats_on(2))
         for (int a = 0; a < 8; ++a)
             for (int b = 0; b < 8; ++b)
                 if (int64_t c = g_hist_n[a][b].exchange(0))

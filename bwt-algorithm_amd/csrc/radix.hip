@@ -1,10 +1,12 @@
-// radix.hip -- hand-written device primitives for gfx950: exclusive scan and a
-// stable LSD radix sort (8-bit digits) over 64- or 32-bit keys with 32/64-bit
-// values.
+// radix.hip -- hand-written device primitives for gfx950: a single-pass
+// exclusive scan and a stable LSD radix sort (8-bit digits) over 16-, 32- or
+// 64-bit keys with 32/64-bit values.
 //
-// Radix pass = three launches:
-//   hist    : one workgroup per 8192-key tile, LDS histogram -> counts[d][tile]
-//   scan    : exclusive scan of counts (digit-major) -> global offsets
+// Radix pass = two launches:
+//   hist    : k_hist_lb -- per-wave LDS histograms of 1-4 scatter tiles per
+//             workgroup, then a decoupled look-back per digit gives every
+//             tile's exclusive prefix of each digit (tile-major rows) and the
+//             last workgroup the digit bases; no count table scan
 //   scatter : each of the 8 waves owns 1024 consecutive keys of the tile; it
 //             ranks keys of equal digit with 8 ballots (wave64 match-any) in
 //             index order, so the pass is stable; the tile is reordered by
@@ -27,26 +29,6 @@ constexpr int kItems = 16;
 constexpr int kTile = kBlock * kItems;  // 4096
 constexpr int kWaves = kBlock / 64;
 
-// ------------------------------------------------------------------ scan
-template <class T>
-__global__ __launch_bounds__(kBlock) void k_chunk_sums(const T *__restrict__ in, T *__restrict__ sums, int64_t n) {
-    const int64_t base = (int64_t)blockIdx.x * kTile;
-    T s = 0;
-#pragma unroll
-    for (int i = 0; i < kItems; ++i) {
-        const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
-        if (idx < n) s += in[idx];
-    }
-    __shared__ T red[kBlock];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = kBlock / 2; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) sums[blockIdx.x] = red[0];
-}
-
 template <class T>
 __device__ inline T wave_incl_scan(T v) {
     const int lane = threadIdx.x & 63;
@@ -58,77 +40,123 @@ __device__ inline T wave_incl_scan(T v) {
     return v;
 }
 
-// Blocked variants of the two chunk kernels: thread t owns the 16 consecutive
-// elements [16t, 16t + 16) of the chunk, read and written as 16-byte vectors
-// (a wave moves 4 KB per 4-8 instructions), scanned in registers; only the
-// 4 wave totals pass through LDS.  The kernels above staged every element in
-// LDS and read it back at a 16-element stride (bank conflicts) -- each of the
-// ~20 scans of a C3 index build over 3.1M tile counts ran at < 1 TB/s.
-template <class T>
-__device__ __forceinline__ bool load_blocked(const T *__restrict__ in, int64_t base, int64_t n, T (&x)[kItems]) {
-    constexpr int NV = kItems * (int)sizeof(T) / 16;
-    if (base + kItems <= n) {
-        const uint4 *p = reinterpret_cast<const uint4 *>(in + base);
-        uint4 v[NV];
+__device__ inline uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
-        for (int q = 0; q < NV; ++q) v[q] = p[q];
-        __builtin_memcpy(x, v, sizeof v);
-        return true;
-    }
-#pragma unroll
-    for (int i = 0; i < kItems; ++i) x[i] = base + i < n ? in[base + i] : (T)0;
-    return false;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
 }
 
-template <class T>
-__global__ __launch_bounds__(kBlock) void k_chunk_sums_v(const T *__restrict__ in, T *__restrict__ sums, int64_t n) {
-    T x[kItems];
-    load_blocked<T>(in, (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems, n, x);
-    T s = 0;
-#pragma unroll
-    for (int i = 0; i < kItems; ++i) s += x[i];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    __shared__ T ws[kWaves];
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
-    __syncthreads();
+// ------------------------------------------------------------ look-back
+// Single-pass prefix sums (decoupled look-back): the workgroups of a launch
+// take their tile in ticket order (an agent-scope atomic counter, so a
+// workgroup only ever waits on tiles whose owners are already running),
+// publish their tile's aggregate, then walk back over the predecessors'
+// published values until one carries an inclusive prefix.  Each published
+// value is ONE 8-byte granule written and read with agent-scope (sc1)
+// atomics -- {value:32, flag:2, epoch:30} -- so it needs no fence: a reader
+// accepts a granule only when its epoch is this launch's (every launch on a
+// context draws a fresh one, so the buffer never needs clearing between
+// launches) and its flag is set.  The last ticket holder resets the counter
+// for the next launch.
+constexpr uint64_t kLbA = 1, kLbP = 2;   // aggregate / inclusive prefix
+__device__ __forceinline__ uint64_t lb_pack(uint32_t epoch, uint64_t flag, uint32_t v) {
+    return ((uint64_t)epoch << 34) | (flag << 32) | v;
+}
+__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_load(uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool lb_ready(uint64_t s, uint32_t epoch) {
+    return (uint32_t)(s >> 34) == epoch && ((s >> 32) & 3u) != 0;
+}
+// the tile of this workgroup (thread 0 draws it; every thread returns it)
+__device__ __forceinline__ int64_t lb_ticket(unsigned *ticket, int64_t ntickets) {
+    __shared__ unsigned tk;
     if (threadIdx.x == 0) {
-        T t = 0;
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) t += ws[w];
-        sums[blockIdx.x] = t;
+        tk = atomicAdd(ticket, 1u);
+        if ((int64_t)tk == ntickets - 1) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    __syncthreads();
+    return (int64_t)tk;
 }
 
-template <class T>
-__global__ __launch_bounds__(kBlock) void k_chunk_scan_v(const T *__restrict__ in, T *__restrict__ out,
-                                                         const T *__restrict__ offs, int64_t n) {
-    constexpr int NV = kItems * (int)sizeof(T) / 16;
-    const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems;
-    T x[kItems];
-    const bool full = load_blocked<T>(in, base, n, x);
-    T s = 0;
+// exclusive scan of uint32 in one launch: 4096 elements per workgroup (16
+// consecutive ones per thread, 16-byte loads when aligned), wave 0 walks the
+// predecessors 64 tiles per step (lane l reads tile t - 1 - l; the ballot of
+// inclusive flags says where to stop, the ballot of unready lanes whether to
+// wait).  In place (in == out) is allowed: a tile reads its elements before
+// it writes them and no other tile touches them.
+__global__ __launch_bounds__(kBlock) void k_scan_lb(const uint32_t *__restrict__ in, uint32_t *out, int64_t n,
+                                                    int64_t ntiles, uint64_t *status, unsigned *ticket,
+                                                    uint32_t epoch, int vec) {
+    const int64_t tile = lb_ticket(ticket, ntiles);
+    const int64_t base = tile * kTile + (int64_t)threadIdx.x * kItems;
+    uint32_t x[kItems];
+    const bool full = vec && base + kItems <= n;
+    if (full) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(in + base);
+        uint4 v[kItems / 4];
+#pragma unroll
+        for (int q = 0; q < kItems / 4; ++q) v[q] = p[q];
+        __builtin_memcpy(x, v, sizeof v);
+    } else {
+#pragma unroll
+        for (int i = 0; i < kItems; ++i) x[i] = base + i < n ? in[base + i] : 0u;
+    }
+    uint32_t s = 0;
 #pragma unroll
     for (int i = 0; i < kItems; ++i) {
-        const T t = x[i];
+        const uint32_t t = x[i];
         x[i] = s;
         s += t;
     }
-    const T inc = wave_incl_scan<T>(s);
-    __shared__ T ws[kWaves];
-    const int wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 63) ws[wv] = inc;
+    const uint32_t inc = wave_incl_scan<uint32_t>(s);
+    __shared__ uint32_t ws[kWaves];
+    __shared__ uint32_t tile_excl;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 63) ws[wv] = inc;
     __syncthreads();
-    T excl = inc - s + (offs ? offs[blockIdx.x] : (T)0);
-    for (int w = 0; w < wv; ++w) excl += ws[w];
+    if (wv == 0) {
+        uint32_t agg = 0;
 #pragma unroll
-    for (int i = 0; i < kItems; ++i) x[i] += excl;
+        for (int w = 0; w < kWaves; ++w) agg += ws[w];
+        uint32_t excl = 0;
+        if (tile == 0) {
+            if (lane == 0) lb_store(status, lb_pack(epoch, kLbP, agg));
+        } else {
+            if (lane == 0) lb_store(status + tile, lb_pack(epoch, kLbA, agg));
+            for (int64_t top = tile - 1;;) {   // every exit and wait is decided by a ballot (uniform)
+                const int64_t idx = top - lane;
+                const uint64_t v = idx >= 0 ? lb_load(status + idx) : lb_pack(epoch, kLbP, 0);
+                const bool ready = lb_ready(v, epoch);
+                const uint64_t nr = __ballot(!ready);
+                const uint64_t pm = __ballot(ready && ((v >> 32) & 3u) == kLbP);
+                const int fp = pm ? __ffsll((unsigned long long)pm) - 1 : 64;
+                if (nr && __ffsll((unsigned long long)nr) - 1 <= fp) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += wave_sum_u32(lane <= fp ? (uint32_t)v : 0u);
+                if (fp < 64) break;
+                top -= 64;
+            }
+            if (lane == 0) lb_store(status + tile, lb_pack(epoch, kLbP, excl + agg));
+        }
+        if (lane == 0) tile_excl = excl;
+    }
+    __syncthreads();
+    uint32_t e = inc - s + tile_excl;
+    for (int w = 0; w < wv; ++w) e += ws[w];
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) x[i] += e;
     if (full) {
-        uint4 v[NV];
+        uint4 v[kItems / 4];
         __builtin_memcpy(v, x, sizeof v);
         uint4 *p = reinterpret_cast<uint4 *>(out + base);
 #pragma unroll
-        for (int q = 0; q < NV; ++q) p[q] = v[q];
+        for (int q = 0; q < kItems / 4; ++q) p[q] = v[q];
     } else {
 #pragma unroll
         for (int i = 0; i < kItems; ++i)
@@ -136,107 +164,99 @@ __global__ __launch_bounds__(kBlock) void k_chunk_scan_v(const T *__restrict__ i
     }
 }
 
-// exclusive scan of one chunk, adding offs[blockIdx.x] (exclusive chunk prefix)
-template <class T>
-__global__ __launch_bounds__(kBlock) void k_chunk_scan(const T *__restrict__ in, T *__restrict__ out,
-                                                       const T *__restrict__ offs, int64_t n) {
-    __shared__ T buf[kTile];
-    __shared__ T wsum[kWaves];
-    const int64_t base = (int64_t)blockIdx.x * kTile;
-#pragma unroll
-    for (int i = 0; i < kItems; ++i) {
-        const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
-        buf[i * kBlock + threadIdx.x] = idx < n ? in[idx] : (T)0;
-    }
-    __syncthreads();
-    T loc[kItems];
-    T s = 0;
-#pragma unroll
-    for (int i = 0; i < kItems; ++i) {
-        loc[i] = s;
-        s += buf[threadIdx.x * kItems + i];
-    }
-    const T inc = wave_incl_scan<T>(s);
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 63) wsum[wv] = inc;
-    __syncthreads();
-    T wpre = 0;
-    for (int w = 0; w < wv; ++w) wpre += wsum[w];
-    const T excl = inc - s + wpre + (offs ? offs[blockIdx.x] : (T)0);
-#pragma unroll
-    for (int i = 0; i < kItems; ++i) buf[threadIdx.x * kItems + i] = loc[i] + excl;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kItems; ++i) {
-        const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
-        if (idx < n) out[idx] = buf[i * kBlock + threadIdx.x];
-    }
-}
-
 // ------------------------------------------------------------------ radix
-// Pass geometry: 256-thread workgroups (thread t owns digit t in the tile
-// scan), ITEMS keys per thread, tile = 256 * ITEMS.
-template <int ITEMS, class KT>
-__global__ __launch_bounds__(kBlock) void k_hist(const KT *__restrict__ keys, uint32_t *__restrict__ counts,
-                                                 int64_t n, int shift, int64_t ntiles) {
-    __shared__ uint32_t h[256];
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * (kBlock * ITEMS);
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
-        if (idx < n) atomicAdd(&h[(keys[idx] >> shift) & 255u], 1u);
-    }
-    __syncthreads();
-    counts[(int64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
-}
-
-// The same counts, read as 16-byte vectors (every key of a full tile is loaded
-// before the first LDS atomic, so the loads are all in flight together) and
-// counted into one histogram per wave (no atomics between waves on one bin);
-// the tile's last partial piece takes the scalar path.
-template <int ITEMS, class KT>
-__global__ __launch_bounds__(kBlock) void k_hist_vec(const KT *__restrict__ keys, uint32_t *__restrict__ counts,
-                                                     int64_t n, int shift, int64_t ntiles) {
+// Histogram + offsets of one pass in one launch.  Scatter tiles hold kSub
+// keys; a histogram workgroup counts S consecutive scatter tiles (S = 1..4:
+// fewer, longer look-back chains on large inputs), one LDS histogram per wave,
+// and thread d owns digit d: it publishes the workgroup's count of d, walks
+// back for the count of d in all earlier workgroups, and writes every scatter
+// tile's exclusive prefix of d -- tile-major rows prefix[tile][256], one
+// coalesced 1 KB row per tile.  The workgroup holding the last ticket also
+// knows every digit's total and writes the digit bases (exclusive scan over
+// the 256 totals).  The scatter's global slot of a key of digit d in tile t is
+// then base[d] + prefix[t][d] + its rank in the tile.
+constexpr int kSub = 8192;   // keys per scatter tile (512 threads x 16)
+constexpr int kMaxSub = 4;
+template <class KT>
+__global__ __launch_bounds__(kBlock) void k_hist_lb(const KT *__restrict__ keys, int64_t n, int shift, int64_t ntiles,
+                                                    int S, int64_t nhist, uint64_t *status,
+                                                    uint32_t *__restrict__ prefix, uint32_t *__restrict__ base,
+                                                    unsigned *ticket, uint32_t epoch, int vec) {
     constexpr int VEC = 16 / sizeof(KT);
-    constexpr int NV = ITEMS / VEC;   // 16-byte loads per thread
-    static_assert(ITEMS % VEC == 0, "whole vectors per thread");
+    constexpr int NV = kSub / kBlock / VEC;   // 16-byte loads per thread and scatter tile
     __shared__ uint32_t h[kWaves][256];
-    for (int i = threadIdx.x; i < kWaves * 256; i += kBlock) (&h[0][0])[i] = 0;
+    const int64_t ht = lb_ticket(ticket, nhist);
+    const int wv = threadIdx.x >> 6, d = threadIdx.x, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) h[w][d] = 0;
     __syncthreads();
-    const int wv = threadIdx.x >> 6;
-    const int64_t base = (int64_t)blockIdx.x * (kBlock * ITEMS);
-    if (base + kBlock * ITEMS <= n) {
-        uint4 v[NV];
-        const uint4 *src = reinterpret_cast<const uint4 *>(keys + base);
+    uint32_t cnt[kMaxSub];
+    uint32_t total = 0;
 #pragma unroll
-        for (int i = 0; i < NV; ++i) v[i] = src[i * kBlock + threadIdx.x];
+    for (int s = 0; s < kMaxSub; ++s) {
+        cnt[s] = 0;
+        const int64_t tile = ht * S + s;
+        if (s >= S || tile >= ntiles) continue;   // uniform
+        const int64_t b0 = tile * kSub;
+        if (vec && b0 + kSub <= n) {
+            uint4 v[NV];
+            const uint4 *src = reinterpret_cast<const uint4 *>(keys + b0);
 #pragma unroll
-        for (int i = 0; i < NV; ++i) {
-            const KT *k = reinterpret_cast<const KT *>(&v[i]);
+            for (int i = 0; i < NV; ++i) v[i] = src[i * kBlock + threadIdx.x];
 #pragma unroll
-            for (int e = 0; e < VEC; ++e) atomicAdd(&h[wv][(k[e] >> shift) & 255u], 1u);
+            for (int i = 0; i < NV; ++i) {
+                const KT *k = reinterpret_cast<const KT *>(&v[i]);
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) atomicAdd(&h[wv][(uint32_t)(k[e] >> shift) & 255u], 1u);
+            }
+        } else {
+            const int64_t e1 = min(n, b0 + (int64_t)kSub);
+            for (int64_t i = b0 + threadIdx.x; i < e1; i += kBlock) atomicAdd(&h[wv][(uint32_t)(keys[i] >> shift) & 255u], 1u);
         }
-    } else {
-        for (int64_t idx = base + threadIdx.x; idx < n; idx += kBlock) atomicAdd(&h[wv][(keys[idx] >> shift) & 255u], 1u);
-    }
-    __syncthreads();
-    uint32_t t = 0;
+        __syncthreads();
+        uint32_t c = 0;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) t += h[w][threadIdx.x];
-    counts[(int64_t)threadIdx.x * ntiles + blockIdx.x] = t;
-}
-
-template <int ITEMS, class KT>
-void launch_hist(Ctx &c, const KT *keys, uint32_t *cnt, int64_t n, int sh, int64_t ntiles) {
-    static const int vec = [] { const char *e = std::getenv("BWTMI_HIST_VEC"); return e ? std::atoi(e) : 1; }();
-    if (vec && ((uintptr_t)keys & 15) == 0)
-        KLAUNCH("radix_hist", (double)n * (double)sizeof(KT), (k_hist_vec<ITEMS, KT>), dim3((unsigned)ntiles),
-                dim3(kBlock), 0, c.stream, keys, cnt, n, sh, ntiles);
-    else
-        KLAUNCH("radix_hist", (double)n * (double)sizeof(KT), (k_hist<ITEMS, KT>), dim3((unsigned)ntiles),
-                dim3(kBlock), 0, c.stream, keys, cnt, n, sh, ntiles);
+        for (int w = 0; w < kWaves; ++w) {
+            c += h[w][d];
+            h[w][d] = 0;   // thread d alone touches column d until the next barrier
+        }
+        cnt[s] = c;
+        total += c;
+        __syncthreads();
+    }
+    uint32_t excl = 0;
+    if (ht == 0) {
+        lb_store(status + d, lb_pack(epoch, kLbP, total));
+    } else {
+        lb_store(status + ht * 256 + d, lb_pack(epoch, kLbA, total));
+        for (int64_t j = ht - 1;;) {   // this lane's digit only
+            const uint64_t v = lb_load(status + j * 256 + d);
+            if (!lb_ready(v, epoch)) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            excl += (uint32_t)v;
+            if (((v >> 32) & 3u) == kLbP) break;
+            --j;
+        }
+        lb_store(status + ht * 256 + d, lb_pack(epoch, kLbP, excl + total));
+    }
+    uint32_t run = excl;
+#pragma unroll
+    for (int s = 0; s < kMaxSub; ++s) {
+        const int64_t tile = ht * S + s;
+        if (s < S && tile < ntiles) prefix[tile * 256 + d] = run;
+        run += cnt[s];
+    }
+    if (ht == nhist - 1) {   // run = the total of digit d
+        __shared__ uint32_t dsum[kWaves];
+        const uint32_t inc = wave_incl_scan<uint32_t>(run);
+        if (lane == 63) dsum[wv] = inc;
+        __syncthreads();
+        uint32_t b = inc - run;
+        for (int w = 0; w < wv; ++w) b += dsum[w];
+        base[d] = b;
+    }
 }
 
 template <bool NT, class T>
@@ -258,8 +278,9 @@ __device__ __forceinline__ void st(T *p, T v) {
 template <class KT, class V, int BLOCK, int ITEMS, bool NT, bool SPLIT>
 __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, const V *__restrict__ vin,
                                                    KT *__restrict__ kout, V *__restrict__ vout,
-                                                   const uint32_t *__restrict__ offs, int64_t n, int shift,
-                                                   int64_t ntiles, int swz, uint8_t *__restrict__ dnext = nullptr,
+                                                   const uint32_t *__restrict__ prefix,
+                                                   const uint32_t *__restrict__ dbase, int64_t n, int shift,
+                                                   int64_t ntiles, uint8_t *__restrict__ dnext = nullptr,
                                                    int nshift = 0) {
     constexpr int kT = BLOCK * ITEMS;
     constexpr int NW = BLOCK / 64;
@@ -283,7 +304,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, c
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < NW * 256; i += BLOCK) (&wcnt[0][0])[i] = 0;
     __syncthreads();
-    const int64_t tile = swz ? xcd_tile(blockIdx.x, ntiles) : (int64_t)blockIdx.x;
+    const int64_t tile = xcd_tile(blockIdx.x, ntiles);
     const int64_t tbase = tile * kT;
     const int64_t wbase = tbase + (int64_t)wv * (ITEMS * 64);
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -335,7 +356,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, c
     if (dg < 256) {
         uint32_t toff = inc - tot;
         for (int w = 0; w < wv; ++w) toff += dsum[w];
-        gdelta[dg] = offs[(int64_t)dg * ntiles + tile] - toff;
+        gdelta[dg] = dbase[dg] + prefix[tile * 256 + dg] - toff;
         uint32_t b = toff;
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
@@ -394,27 +415,60 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, c
     }
 }
 
+// The look-back state of a context: the granule buffer (shared by the
+// histogram and scan launches, which never overlap on one stream), the ticket
+// counter and a fresh epoch per launch.  A (re)allocated granule buffer is
+// cleared once, so no stale granule can carry a future epoch.
+struct LbState {
+    uint64_t *status;
+    unsigned *ticket;
+    uint32_t epoch;
+};
+LbState lb_prepare(Ctx &c, int64_t granules) {
+    DBuf &g = c.slot[S_LB];
+    const void *p0 = g.p;
+    const size_t b0 = g.bytes;
+    g.ensure((size_t)granules * 8 + 64);
+    const bool fresh = g.p != p0 || g.bytes != b0;
+    if (++c.lb_epoch >= (1u << 30)) c.lb_epoch = 1;   // epochs wrap: clear again
+    if (fresh || c.lb_epoch == 1) HIPCHECK(hipMemsetAsync(g.p, 0, g.bytes, c.stream));
+    if (!c.lb_ticket.p) {
+        c.lb_ticket.ensure(64);
+        HIPCHECK(hipMemsetAsync(c.lb_ticket.p, 0, c.lb_ticket.bytes, c.stream));
+    }
+    return {g.as<uint64_t>(), c.lb_ticket.as<unsigned>(), c.lb_epoch};
+}
+
+// one pass's histogram and offsets: prefix rows in S_SORT_HIST, digit bases after them
+template <class KT>
+void launch_hist(Ctx &c, const KT *keys, int64_t n, int shift, int64_t ntiles, uint32_t **prefix, uint32_t **base) {
+    const int S = ntiles >= 4096 ? 4 : ntiles >= 1024 ? 2 : 1;   // scatter tiles per histogram workgroup
+    const int64_t nhist = (ntiles + S - 1) / S;
+    c.slot[S_SORT_HIST].ensure((size_t)(ntiles + 1) * 256 * sizeof(uint32_t));
+    *prefix = c.slot[S_SORT_HIST].as<uint32_t>();
+    *base = *prefix + ntiles * 256;
+    const LbState lb = lb_prepare(c, nhist * 256);
+    KLAUNCH("radix_hist", (double)n * (double)sizeof(KT), k_hist_lb<KT>, dim3((unsigned)nhist), dim3(kBlock), 0,
+            c.stream, keys, n, shift, ntiles, S, nhist, lb.status, *prefix, *base, lb.ticket, lb.epoch,
+            ((uintptr_t)keys & 15) == 0 ? 1 : 0);
+}
+
 template <class KT, class V, int BLOCK, int ITEMS, bool NT, bool SPLIT>
 void radix_sort_cfg(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
     constexpr int kT = BLOCK * ITEMS;
-    static_assert(kT % kBlock == 0, "histogram tiles are 256-thread tiles");
+    static_assert(kT == kSub, "the histogram counts the scatter's tiles");
     const int64_t ntiles = (n + kT - 1) / kT;
     c.slot[S_SORT_TMP0].ensure((size_t)n * sizeof(KT));
     if (vals) c.slot[S_SORT_TMP1].ensure((size_t)n * sizeof(V));
-    c.slot[S_SORT_HIST].ensure((size_t)ntiles * 256 * sizeof(uint32_t));
     KT *ka = keys, *kb = c.slot[S_SORT_TMP0].as<KT>();
     V *va = vals, *vb = vals ? c.slot[S_SORT_TMP1].as<V>() : nullptr;
-    uint32_t *cnt = c.slot[S_SORT_HIST].as<uint32_t>();
-    static const int swz = [] { const char *e = std::getenv("BWTMI_RADIX_SWZ"); return e ? std::atoi(e) : 1; }();
     // 64-bit keys: each pass but the last also writes the next pass's digit of
     // every key it places (one byte, at the key's new position), and the next
     // histogram reads n bytes instead of 8n (C3N: histograms 3.34 -> 2.56 ms,
     // the kv12 scatters +0.3 ms for their byte stores, r04zo).  For 32- and
     // 16-bit keys the byte stores cost the scatter more than the histogram
     // saves (C3: kv8 1.54 -> 1.86 ms for 1.21 -> 0.97), so they read the keys.
-    // BWTMI_RADIX_DIGITS=0: never, =2: every key width.
-    static const int digits = [] { const char *e = std::getenv("BWTMI_RADIX_DIGITS"); return e && *e ? std::atoi(e) : 1; }();
-    const bool dig = (digits == 2 || (digits == 1 && sizeof(KT) == 8)) && bit0 + 8 < bit1;
+    const bool dig = sizeof(KT) == 8 && bit0 + 8 < bit1;
     uint8_t *dg = nullptr;
     if (dig) {
         c.slot[S_SORT_DIG].ensure((size_t)n + 64);
@@ -422,17 +476,17 @@ void radix_sort_cfg(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
     }
     int passes = 0;
     for (int sh = bit0; sh < bit1; sh += 8) {
+        uint32_t *prefix, *base;
         // read the keys (the first pass) or their digit bytes once
-        if (dig && sh > bit0) launch_hist<kT / kBlock, uint8_t>(c, dg, cnt, n, 0, ntiles);
-        else launch_hist<kT / kBlock, KT>(c, ka, cnt, n, sh, ntiles);
-        exclusive_scan<uint32_t>(c, cnt, cnt, ntiles * 256);
+        if (dig && sh > bit0) launch_hist<uint8_t>(c, dg, n, 0, ntiles, &prefix, &base);
+        else launch_hist<KT>(c, ka, n, sh, ntiles, &prefix, &base);
         // read (key, value) once, write it once
         const bool more = dig && sh + 8 < bit1;
         KLAUNCH(sizeof(KT) == 2 ? "radix_scatter_kv6" : sizeof(KT) == 4 ? "radix_scatter_kv8"
                 : sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16",
                 (double)n * 2.0 * ((double)sizeof(KT) + (vals ? (double)sizeof(V) : 0.0)),
                 (k_scatter<KT, V, BLOCK, ITEMS, NT, SPLIT>), dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, ka, va,
-                kb, vb, cnt, n, sh, ntiles, swz, more ? dg : nullptr, sh + 8);
+                kb, vb, prefix, base, n, sh, ntiles, more ? dg : nullptr, sh + 8);
         std::swap(ka, kb);
         std::swap(va, vb);
         ++passes;
@@ -449,10 +503,12 @@ void radix_sort_cfg(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
 // staging 0.50-0.51 (20 items 0.52, 12 items 0.50, 8 items 0.47); separate key
 // and value staging 0.44-0.45; nontemporal stores 0.34-0.41 in every geometry.
 // r01ak, same box session for every variant: 512x16 0.50, 256x16 0.47, 512x8
-// 0.47, 1024x4 0.47, 256x20 0.48, 1024x8 0.44, 256x32 0.43.
+// 0.47, 1024x4 0.47, 256x20 0.48, 1024x8 0.44, 256x32 0.43; r02w (32-bit keys):
+// 512x32, 256x32, 1024x16, 512x24 within 5 % of 512x16.
 template <class KT, class V>
 void radix_sort_impl(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
     if (n <= 1) return;
+    if (n >= (int64_t{1} << 32)) fail(BWTMI_E_ARG, "radix sort: %lld keys exceed the 32-bit offsets", (long long)n);
     // 512 threads x 16 keys: 8192-key tiles, 8 waves per workgroup, ~75 KB of
     // LDS with 64-bit keys (64 KB staging + 8 KB wave counters + digit tables),
     // ~43 KB with 32-bit keys; 2 (3) workgroups per CU within gfx950's 160 KB
@@ -461,85 +517,19 @@ void radix_sort_impl(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
 
 }  // namespace
 
-// Mid-size arrays (the radix count tables of short inputs, flag arrays of
-// a few tens of thousands): one workgroup walks the array 4096 elements a step
-// with a running carry -- one launch instead of the sums / scan / scan chain
-// (three launches and their gaps on a launch-bound 12.5 Mbp scan)
-constexpr int64_t kOneBlockScan = 32768;
-template <class T>
-__global__ __launch_bounds__(kBlock) void k_scan_one(const T *__restrict__ in, T *__restrict__ out, int64_t n) {
-    __shared__ T ws[kWaves];
-    __shared__ T carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int64_t c0 = 0; c0 < n; c0 += kTile) {
-        const int64_t base = c0 + (int64_t)threadIdx.x * kItems;
-        T x[kItems];
-#pragma unroll
-        for (int i = 0; i < kItems; ++i) x[i] = base + i < n ? in[base + i] : (T)0;
-        T s = 0;
-#pragma unroll
-        for (int i = 0; i < kItems; ++i) {
-            const T t = x[i];
-            x[i] = s;
-            s += t;
-        }
-        const T inc = wave_incl_scan<T>(s);
-        const int wv = threadIdx.x >> 6;
-        if ((threadIdx.x & 63) == 63) ws[wv] = inc;
-        __syncthreads();
-        T excl = inc - s + carry;
-        for (int w = 0; w < wv; ++w) excl += ws[w];
-#pragma unroll
-        for (int i = 0; i < kItems; ++i)
-            if (base + i < n) out[base + i] = x[i] + excl;
-        __syncthreads();   // every thread has read carry and ws
-        if (threadIdx.x == kBlock - 1) carry = excl + s;
-        __syncthreads();
-    }
-}
-
-// in place (in == out) is allowed: a chunk's elements are read before any is written
-template <class T>
-static void scan_rec(Ctx &c, const T *in, T *out, int64_t n, T *tmp) {
-    static const int vec = [] { const char *e = std::getenv("BWTMI_SCAN_VEC"); return e ? std::atoi(e) : 1; }();
-    const bool v = vec && (((uintptr_t)in | (uintptr_t)out) & 15) == 0;   // 16-byte vectors need aligned bases
-    const int64_t nch = (n + kTile - 1) / kTile;
-    const double bytes = 2.0 * (double)n * (double)sizeof(T);
-    static const bool one = [] { const char *e = std::getenv("BWTMI_SCAN_ONE"); return !(e && *e == '0'); }();
-    if (nch > 1 && n <= kOneBlockScan && one) {
-        KLAUNCH("k_chunk_scan", bytes, k_scan_one<T>, dim3(1), dim3(kBlock), 0, c.stream, in, out, n);
-        return;
-    }
-    if (nch == 1) {
-        if (v) KLAUNCH("k_chunk_scan", bytes, k_chunk_scan_v<T>, dim3(1), dim3(kBlock), 0, c.stream, in, out, (const T *)nullptr, n);
-        else KLAUNCH("k_chunk_scan", bytes, k_chunk_scan<T>, dim3(1), dim3(kBlock), 0, c.stream, in, out, (const T *)nullptr, n);
-        return;
-    }
-    T *sums = tmp;
-    if (v) KLAUNCH("k_chunk_sums", bytes / 2, k_chunk_sums_v<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, sums, n);
-    else KLAUNCH("k_chunk_sums", bytes / 2, k_chunk_sums<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, sums, n);
-    scan_rec<T>(c, sums, sums, nch, tmp + nch);
-    if (v) KLAUNCH("k_chunk_scan", bytes, k_chunk_scan_v<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, out, (const T *)sums, n);
-    else KLAUNCH("k_chunk_scan", bytes, k_chunk_scan<T>, dim3((unsigned)nch), dim3(kBlock), 0, c.stream, in, out, (const T *)sums, n);
-}
-
 template <class T>
 void exclusive_scan(Ctx &c, const T *in, T *out, int64_t n) {
+    static_assert(sizeof(T) == 4, "32-bit scans");
     if (n <= 0) return;
-    int64_t need = 0;
-    for (int64_t m = n; m > kTile;) {
-        m = (m + kTile - 1) / kTile;
-        need += m;
-    }
-    c.slot[S_SCAN_TMP].ensure((size_t)(need + 1) * sizeof(T));
-    scan_rec<T>(c, in, out, n, c.slot[S_SCAN_TMP].as<T>());
+    const int64_t ntiles = (n + kTile - 1) / kTile;
+    const LbState lb = lb_prepare(c, ntiles);
+    const int vec = (((uintptr_t)in | (uintptr_t)out) & 15) == 0 ? 1 : 0;   // 16-byte vectors need aligned bases
+    KLAUNCH("k_scan", 2.0 * (double)n * (double)sizeof(T), k_scan_lb, dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream,
+            (const uint32_t *)in, (uint32_t *)out, n, ntiles, lb.status, lb.ticket, lb.epoch, vec);
     HIPCHECK(hipGetLastError());
 }
 
 template void exclusive_scan<uint32_t>(Ctx &, const uint32_t *, uint32_t *, int64_t);
-template void exclusive_scan<uint64_t>(Ctx &, const uint64_t *, uint64_t *, int64_t);
-template void exclusive_scan<int64_t>(Ctx &, const int64_t *, int64_t *, int64_t);
 
 void radix_sort_pairs(Ctx &c, uint64_t *keys, uint64_t *vals, int64_t n, int bit0, int bit1) {
     radix_sort_impl<uint64_t, uint64_t>(c, keys, vals, n, bit0, bit1);
@@ -553,12 +543,10 @@ void radix_pass_k32(Ctx &c, const uint32_t *kin, const uint32_t *vin, uint32_t *
     if (n <= 0) return;
     constexpr int BLOCK = 512, ITEMS = 16, kT = BLOCK * ITEMS;
     const int64_t ntiles = (n + kT - 1) / kT;
-    c.slot[S_SORT_HIST].ensure((size_t)ntiles * 256 * sizeof(uint32_t));
-    uint32_t *cnt = c.slot[S_SORT_HIST].as<uint32_t>();
-    launch_hist<kT / kBlock, uint32_t>(c, kin, cnt, n, shift, ntiles);
-    exclusive_scan<uint32_t>(c, cnt, cnt, ntiles * 256);
+    uint32_t *prefix, *base;
+    launch_hist<uint32_t>(c, kin, n, shift, ntiles, &prefix, &base);
     KLAUNCH("radix_partition_kv8", (double)n * 16.0, (k_scatter<uint32_t, uint32_t, BLOCK, ITEMS, false, true>),
-            dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, kin, vin, kout, vout, cnt, n, shift, ntiles, 1);
+            dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, kin, vin, kout, vout, prefix, base, n, shift, ntiles);
     HIPCHECK(hipGetLastError());
 }
 
@@ -566,18 +554,12 @@ void radix_pass_k32(Ctx &c, const uint32_t *kin, const uint32_t *vin, uint32_t *
 // (a value does not fit a key's LDS slot), positions kept in registers
 void radix_sort_pairs_k16(Ctx &c, uint16_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1) {
     if (n <= 1) return;
+    if (n >= (int64_t{1} << 32)) fail(BWTMI_E_ARG, "radix sort: %lld keys exceed the 32-bit offsets", (long long)n);
     radix_sort_cfg<uint16_t, uint32_t, 512, 16, false, false>(c, keys, vals, n, bit0, bit1);
 }
 
 void radix_sort_pairs_k32(Ctx &c, uint32_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1) {
-    static const int v = [] { const char *e = std::getenv("BWTMI_RADIX32"); return e ? std::atoi(e) : 0; }();
-    switch (v) {   // geometry A/B (tools/gpu_radix_ab.sh)
-        case 1: radix_sort_cfg<uint32_t, uint32_t, 512, 32, false, true>(c, keys, vals, n, bit0, bit1); return;
-        case 2: radix_sort_cfg<uint32_t, uint32_t, 256, 32, false, true>(c, keys, vals, n, bit0, bit1); return;
-        case 3: radix_sort_cfg<uint32_t, uint32_t, 1024, 16, false, true>(c, keys, vals, n, bit0, bit1); return;
-        case 4: radix_sort_cfg<uint32_t, uint32_t, 512, 24, false, true>(c, keys, vals, n, bit0, bit1); return;
-        default: radix_sort_impl<uint32_t, uint32_t>(c, keys, vals, n, bit0, bit1);
-    }
+    radix_sort_impl<uint32_t, uint32_t>(c, keys, vals, n, bit0, bit1);
 }
 
 }  // namespace bwtmi

@@ -389,7 +389,7 @@ void detect_compounds(const Job &job, const RecVec &recs, Compound &out, int nt)
         for (auto &w : reps) out.pools.push_back(std::move(w.pool));
         for (auto &w : W) out.pools.push_back(std::move(w.pool));
     }
-    if (const char *e = std::getenv("BWTMI_STATS"); e && *e == '1') {
+    if (stats_on()) {
         auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         std::fprintf(stderr, "  compounds: group+kmer %.1f sort %.1f walk %.1f ms (%zu pieces)\n", d(T0, T1), tsort,
                      d(T2, std::chrono::steady_clock::now()) - tsort, out.pool.size());
@@ -749,7 +749,7 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
     });
     auto t3 = std::chrono::steady_clock::now();
     job.stage_ms[6] = std::chrono::duration<double, std::milli>(t3 - t0).count();
-    if (const char *e = std::getenv("BWTMI_STATS"); e && *e == '1') {
+    if (stats_on()) {
         auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         std::fprintf(stderr, "  render: compounds+sort %.1f chunking %.1f format %.1f ms (%zu rows)\n", d(t0, t1),
                      d(t1, t2), d(t2, t3), rows.size());

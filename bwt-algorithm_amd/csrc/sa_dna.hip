@@ -913,13 +913,13 @@ bool sa_sort(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, in
     const int64_t lalloc = n / 2 + n / 8 + 16 * (int64_t)kCH + 64;
     for (int q : {S_MISC0, S_MISC1, S_IDX9, S_IDX10}) c.slot[q].ensure((size_t)lalloc * 4);
     int64_t lcap = lalloc;
-    if (const char *e = std::getenv("BWTMI_LS_CAP")) lcap = std::min<int64_t>(lcap, std::atoll(e));   // test hook
+    if (knob(KN_LS_CAP) >= 0) lcap = std::min<int64_t>(lcap, knob(KN_LS_CAP));   // test hook
     c.slot[S_IDX8].ensure((size_t)n * 4 + 64);
     // a round's rank changes (<= its members; holes and uneven shards as above)
     const int64_t calloc_ = n + n / 4 + 16 * (int64_t)kCH + 64;
     c.slot[S_IDX11].ensure((size_t)calloc_ * 8);
     int64_t ccap = calloc_;
-    if (const char *e = std::getenv("BWTMI_LS_CAP")) ccap = std::min<int64_t>(ccap, 2 * std::atoll(e));
+    if (knob(KN_LS_CAP) >= 0) ccap = std::min<int64_t>(ccap, 2 * knob(KN_LS_CAP));
     uint64_t *chg = c.slot[S_IDX11].as<uint64_t>();
     uint32_t *gs = c.slot[S_MISC0].as<uint32_t>(), *ge = c.slot[S_MISC1].as<uint32_t>();
     uint32_t *xs = c.slot[S_IDX9].as<uint32_t>(), *xe = c.slot[S_IDX10].as<uint32_t>();
@@ -951,50 +951,29 @@ bool sa_sort(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, in
     }
     // rank[pos] = head
     const int64_t nput = (n + kB * kPutItems - 1) / (kB * kPutItems);
-    static const int rank0_direct = [] { const char *e = std::getenv("BWTMI_RANK0_DIRECT"); return e && *e == '1'; }();
-    if (rank0_direct || n < (1 << 16)) {
+    if (n <= (1 << 16)) {
         KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put<false>, dim3((unsigned)nput), dim3(kB), 0, st, vals,
                 hd, n, nput, rank);
     } else {
-        // through a position partition (the pass output in the sort's buffers)
+        // through a position partition (the pass output in the sort's buffers):
+        // two stable passes order the pairs by the top 16 position bits, so one
+        // workgroup's 4096 pairs cover about 4096 consecutive ranks (16 KB written
+        // whole inside the workgroup) instead of 4096 scattered ranks of a
+        // 2^(bits-8) window merged across workgroups in the XCD's L2 (one pass:
+        // 3.3x write amplification, PMC r03i; the direct scatter 2.35 ms at C3)
         int bits = 0;
         while ((int64_t{1} << bits) < n) ++bits;
         c.slot[S_SORT_TMP0].ensure((size_t)n * 4);
         c.slot[S_SORT_TMP1].ensure((size_t)n * 4);
         uint32_t *pv = c.slot[S_SORT_TMP0].as<uint32_t>(), *ph = c.slot[S_SORT_TMP1].as<uint32_t>();
-        // BWTMI_PUT_PASSES=2 (default): two stable passes order the pairs by the
-        // top 16 position bits, so one workgroup's 4096 pairs cover about 4096
-        // consecutive ranks (16 KB written whole inside the workgroup) instead of
-        // 4096 scattered ranks of a 2^(bits-8) window merged across workgroups in
-        // the XCD's L2 (3.3x write amplification, PMC r03i); 1: one pass
-        static const int put_passes = [] { const char *e = std::getenv("BWTMI_PUT_PASSES"); return e ? std::atoi(e) : 2; }();
-        const bool two = put_passes >= 2 && bits >= 17;
-        if (two) {
-            radix_pass_k32(c, vals, hd, pv, ph, n, bits - 16);
-            radix_pass_k32(c, pv, ph, fe, pe, n, bits - 8);   // fe / pe are free until the refine rounds
-            pv = fe;
-            ph = pe;
-        } else {
-            radix_pass_k32(c, vals, hd, pv, ph, n, bits - 8);
-        }
-        // (unused) LDS caps the workgroups per CU, and so the span of positions
-        // an XCD writes at once: at 1 workgroup per CU an XCD's 32 x 4096
-        // pairs stay within about a quarter of a 2^shift window (2 MB at
-        // 100 Mbp) and the L2 merges the stores into whole lines.  r02aj:
-        // 1.13-1.36 ms at full occupancy, 0.63 at 2 per CU, 0.55 at 1 per CU
-        // (the direct scatter: 2.35)
-        static const int put_lds_env = [] { const char *e = std::getenv("BWTMI_PUT_LDS"); return e ? std::atoi(e) : -1; }();
-        const int put_lds = put_lds_env >= 0 ? put_lds_env : two ? 0 : 128;   // the occupancy cap serves the one-pass order only
-        static const int put_nt = [] { const char *e = std::getenv("BWTMI_PUT_NT"); return e ? std::atoi(e) : 1; }();
-        if (two && bits - 16 <= 12)   // 2^(bits-16) positions per 16-bit window divide the 4096-pair tile
+        radix_pass_k32(c, vals, hd, pv, ph, n, bits - 16);
+        radix_pass_k32(c, pv, ph, fe, pe, n, bits - 8);   // fe / pe are free until the refine rounds
+        if (bits - 16 <= 12)   // 2^(bits-16) positions per 16-bit window divide the 4096-pair tile
             KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put_tile<true>, dim3((unsigned)nput), dim3(kB), 0, st,
-                    pv, ph, n, rank);
-        else if (put_nt)
-            KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put<true>, dim3((unsigned)nput), dim3(kB),
-                    (size_t)put_lds * 1024, st, pv, ph, n, nput, rank);
-        else
-            KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put<false>, dim3((unsigned)nput), dim3(kB),
-                    (size_t)put_lds * 1024, st, pv, ph, n, nput, rank);
+                    fe, pe, n, rank);
+        else   // texts past 2^28 bases: streaming stores into the 2^(bits-16) windows
+            KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put<true>, dim3((unsigned)nput), dim3(kB), 0, st, fe,
+                    pe, n, nput, rank);
     }
     if (G) KLAUNCH("dna_short_fix", 0.0, k_dna_short_fix, dim3(1), dim3(1024), 0, st, vals, rank, gs, ge, G, n);
 

@@ -742,17 +742,16 @@ template <int B>
 constexpr int run_tile() { return 2048 / B; }   // words per workgroup: <= 64 KB of LDS with a 256-word halo
 constexpr int kRunGroupSplit = 2;   // gridDim.y: workgroups share a tile's groups (gi mod 2): 2x the
                                     // workgroups of a short contig, each tile read twice
-constexpr int kRunHaloAfter = 34;
 template <int B>
 __global__ __launch_bounds__(256) void k_runs_tiled(const uint32_t *__restrict__ P, int64_t n, int64_t nwords32,
                                                     int32_t lmin, int32_t lmax, int64_t mc, SparseGroups sg,
-                                                    int32_t halo, CandOut out) {
+                                                    int32_t halo, int32_t after, CandOut out) {
     extern __shared__ uint32_t tl[];   // words base .. base + span - 1, B planes each
     __shared__ int64_t pre[kSparseMax + 1], first[kSparseMax];
     constexpr int kRunTile = run_tile<B>();
     const int64_t w0 = (int64_t)blockIdx.x * kRunTile;
     const int64_t base = w0 - halo;
-    const int64_t span = halo + kRunTile + kRunHaloAfter;
+    const int64_t span = halo + kRunTile + after;   // a sample w < w0 + kRunTile reads up to word w + g + 1
     for (int64_t k = threadIdx.x; k < span * B; k += 256) {
         const int64_t w = base + k / B;
         tl[k] = w >= 0 && w < nwords32 + 8 ? P[base * B + k] : 0u;
@@ -904,7 +903,7 @@ inline int64_t sparse_stride(int64_t g, int32_t lmin, int64_t mc) {
 template <int B>
 void launch_runs(Ctx &c, const uint32_t *P, int64_t n, int32_t lmin, int32_t lmax, int64_t mc, CandOut out) {
     const int64_t nwords32 = (n + 31) / 32;
-    static const bool dense_only = [] { const char *e = std::getenv("BWTMI_RUNS_DENSE"); return e && *e == '1'; }();
+    const bool dense_only = knob(KN_RUNS_DENSE) != 0;   // A/B and parity cross-check: every group dense
     int64_t gs = std::max<int64_t>(1, lmin >> 5);   // group 0 (L < 32) stays dense: its short runs
     while (!dense_only && gs <= (lmax >> 5) && sparse_stride(gs, lmin, mc) < 2) ++gs;
     if (dense_only) gs = (lmax >> 5) + 1;
@@ -930,15 +929,20 @@ void launch_runs(Ctx &c, const uint32_t *P, int64_t n, int32_t lmin, int32_t lma
         }
         const int64_t waves = sg.woff[sg.ng];
         if (waves == 0) continue;
-        int32_t halo = 0;
-        for (int gi = 0; gi < sg.ng; ++gi) halo = std::max(halo, sg.s[gi]);
-        static const bool untiled = [] { const char *e = std::getenv("BWTMI_RUNS_UNTILED"); return e && *e == '1'; }();
-        if (!untiled && halo <= 256) {   // LDS tiles (BWTMI_RUNS_UNTILED=1: the scattered-sample kernel)
-            constexpr int T = run_tile<B>();
-            const size_t lds = (size_t)(halo + T + kRunHaloAfter) * B * 4;
+        // the tile's halo: the largest stride before it (owner tests), the
+        // largest group + 2 words after it (words w + g and w + g + 1 of its last sample)
+        int32_t halo = 0, after = 0;
+        for (int gi = 0; gi < sg.ng; ++gi) {
+            halo = std::max(halo, sg.s[gi]);
+            after = std::max(after, sg.g[gi] + 2);
+        }
+        const bool untiled = knob(KN_RUNS_UNTILED) != 0;
+        constexpr int T = run_tile<B>();
+        const size_t lds = (size_t)(halo + T + after) * B * 4;
+        if (!untiled && halo <= 256 && lds <= 64 * 1024) {   // LDS tiles (BWTMI_RUNS_UNTILED=1: the scattered-sample kernel)
             KLAUNCH("k_runs_sparse", 0.0, (k_runs_tiled<B>),
                     dim3((unsigned)((nwords32 + T - 1) / T), (unsigned)std::min(kRunGroupSplit, sg.ng)), dim3(256), lds,
-                    c.stream, P, n, nwords32, lmin, lmax, mc, sg, halo, out);
+                    c.stream, P, n, nwords32, lmin, lmax, mc, sg, halo, after, out);
         } else {
             KLAUNCH("k_runs_sparse", 0.0, (k_runs_sparse<B>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, c.stream,
                     P, n, nwords32, lmin, lmax, mc, sg, out);

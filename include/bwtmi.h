@@ -43,10 +43,42 @@ typedef struct bwtmi_job bwtmi_job;
 
 /* ------------------------------------------------------------ context */
 const char *bwtmi_last_error(void);
+/* "bwtmi 0.5 (gfx950) src <sha256>": the sources the library was built from */
 const char *bwtmi_version(void);
+/* sha256 (hex) of the csrc sources (.cpp, .h, .hip) and include/bwtmi.h, concatenated in
+ * byte order of their paths, computed by the Makefile at build time: a test
+ * or launcher compares it with the tree it runs from (bwtmi._lib.check_build) */
+const char *bwtmi_source_hash(void);
 int bwtmi_device_count(int *count);
 int bwtmi_open(int device, bwtmi_ctx **out);
 int bwtmi_close(bwtmi_ctx *ctx);
+/* Host placement, asked for explicitly (the CLI, bench.py and the rank
+ * launcher do; bwtmi_open never does unless BWTMI_NUMA_BIND=1): on=1 moves
+ * this process's host work -- the calling thread now, the library's worker
+ * threads at their next parallel region -- onto the CPUs of the NUMA node of
+ * ctx's GPU; on=0 restores the affinity the binding replaced.  *changed = 1
+ * when the placement changed.  Local rank r (LOCAL_RANK / LOCAL_WORLD_SIZE)
+ * drives device r mod (visible devices); the ranks whose GPUs share this
+ * node decide whether one hardware thread per core is taken.  A second
+ * context on another node leaves the first binding in place. */
+int bwtmi_bind_host(bwtmi_ctx *ctx, int on, int *changed);
+/* The CPU set bwtmi_bind_host would choose, without changing anything: sysfs
+ * read under `sysroot` ("/sys" on a host; a faked tree in the tests), local
+ * rank `local_rank` of the ranks whose GPUs have the comma-separated PCI
+ * addresses `rank_pci` (rank order), `threads` host threads per rank, `smt`
+ * = keep sibling hardware threads, `allowed` = the process's affinity as a
+ * cpulist.  out = the chosen cpulist ("" = no binding); *node = this GPU's
+ * NUMA node, *ranks_on_node = local ranks whose GPUs sit on it. */
+int bwtmi_host_binding_plan(const char *sysroot, int local_rank, const char *rank_pci, int threads, int smt,
+                            const char *allowed, char *out, int64_t cap, int *node, int *ranks_on_node);
+/* Run-time switches (INTEGRATION.md "Run-time switches"): BWTMI_<NAME> read
+ * once from the environment; get/set in-process by NAME (with or without the
+ * BWTMI_ prefix).  Unknown names: BWTMI_E_ARG.  bwtmi_knob_names(): all names,
+ * comma-separated. */
+int bwtmi_knob_set(const char *name, int64_t value);
+int bwtmi_knob_get(const char *name, int64_t *value);
+int bwtmi_knob_default(const char *name, int64_t *value);
+const char *bwtmi_knob_names(void);
 void bwtmi_free(void *p);
 /* time (ms) of the kernels of the last call on ctx, measured with HIP events
  * on the ctx stream: [0]=total device, [1]=dominant kernel, [2]=its launches */

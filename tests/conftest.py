@@ -29,6 +29,7 @@ def built_lib():
         import subprocess
         subprocess.run(["make", "-s", "-j8", "-C", PKG], check=True)
     from bwtmi import _lib
+    _lib.check_build()     # the library was built from this tree's sources (embedded hash)
     return _lib.lib()
 
 

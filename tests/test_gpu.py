@@ -109,6 +109,44 @@ def test_strict_scan_long_runs_and_streaks(gpu_ctx):
         _same(seq, 1, 1000, mc)
 
 
+def test_strict_scan_long_units_tile_halo(gpu_ctx):
+    """--max-unit-len beyond 1000: the sampled groups of unit
+    lengths >= 1088 read words w + g + 1 past the LDS tile's owned words, so the
+    halo after the tile is sized from the launch's largest group.  Arrays of
+    unit 1050-2000 planted across tile ends (2048/B words), against the oracle."""
+    r = np.random.default_rng(77)
+    t = bytearray(_rng_text(400_000, b"ACGT", 77))
+    pos = 500
+    while pos < len(t) - 9000:
+        L = int(r.integers(1050, 2001))
+        unit = _rng_text(L, b"ACGT", int(r.integers(1 << 30)))
+        arr = unit * int(r.integers(2, 5))
+        t[pos:pos + len(arr)] = arr
+        pos += len(arr) + int(r.integers(50, 3000))
+    seq = bytes(t)
+    for mc in (2, 3):
+        assert _same(seq, 1, 2000, mc) > 0
+    _same(seq, 1100, 1900, 2)
+    four = _planted(150_000, 78, b"ACGTNR", max_unit=1500)   # 4 bit planes: a shorter tile
+    _same(four, 1, 1500, 2)
+
+
+@pytest.mark.parametrize("kv", [{"RUNS_DENSE": 1}, {"RUNS_UNTILED": 1}])
+def test_strict_scan_alternate_kernels_vs_oracle(gpu_ctx, kv):
+    """The strict scan's alternate paths (BWTMI_RUNS_DENSE: every group in the
+    dense kernel; BWTMI_RUNS_UNTILED: sampled groups straight from the planes)
+    find the same hits: planted arrays on 2- and 4-plane texts, long units
+    across tile ends, homopolymers."""
+    from bwtmi import _lib
+    texts = [_planted(120_000, 91), _planted(60_000, 92, b"ACGTNR", max_unit=700),
+             b"A" * 4000 + _rng_text(3000, b"ACGT", 93) + b"CAG" * 900]
+    with _lib.knobs(**kv):
+        for seq in texts:
+            for mc in (2, 3, 5):
+                _same(seq, 1, 1000, mc)
+        _same(_planted(200_000, 94, max_unit=1700), 1, 1800, 2)
+
+
 def test_strict_scan_min_copies_one(gpu_ctx):
     seq = _planted(600, 21)
     _same(seq, 1, 200, 1)
@@ -212,9 +250,7 @@ def _job_output(contigs, screen: bool, mc=3, fmt="strfinder"):
     device (nested.hip) or the host nested/sort/dedup stage."""
     from bwtmi import _lib
     from bwtmi.records import Job
-    old = os.environ.get("BWTMI_HOST_SCREEN")
-    os.environ["BWTMI_HOST_SCREEN"] = "0" if screen else "1"
-    try:
+    with _lib.knobs(HOST_SCREEN=0 if screen else 1):
         j = Job(min_copies=mc, show_progress=True)
         for name, seq in contigs:
             j.add_contig(name, seq, 30 if len(seq) > 60 else 0, 30 if len(seq) > 60 else 0)
@@ -222,16 +258,14 @@ def _job_output(contigs, screen: bool, mc=3, fmt="strfinder"):
         raw = j.raw_count()
         j.postprocess()
         return raw, j.render(fmt)
-    finally:
-        if old is None:
-            os.environ.pop("BWTMI_HOST_SCREEN", None)
-        else:
-            os.environ["BWTMI_HOST_SCREEN"] = old
 
 
 @pytest.mark.parametrize("case", ["planted", "synthetic", "imperfect", "same_unit", "tiny"])
 def test_device_screen_matches_host(gpu_ctx, case):
-    """nested suppression + sort + dedup on the device == the host restatement."""
+    """nested suppression + sort + dedup on the device == the host restatement,
+    for the segmented single-launch screen and the per-level launches
+    (BWTMI_SEG_LEVELS=0)."""
+    from bwtmi import _lib
     from bwtmi import synth
     if case == "planted":
         contigs = [("p1", _planted(300_000, 5, max_unit=400, density=0.5)), ("p2", _planted(50_000, 6))]
@@ -248,6 +282,8 @@ def test_device_screen_matches_host(gpu_ctx, case):
         rh, h = _job_output(contigs, False, fmt=fmt)
         assert rd == rh
         assert d == h, (case, fmt)
+    with _lib.knobs(SEG_LEVELS=0):
+        assert _job_output(contigs, True, fmt="strfinder")[1] == _job_output(contigs, False, fmt="strfinder")[1]
 
 
 def test_failing_contig_yields_error_and_no_records(gpu_ctx, golden_dir, tmp_path, capsys, monkeypatch):
@@ -427,11 +463,11 @@ def test_dna_suffix_sort_vs_oracle(gpu_ctx, monkeypatch, case):
             parts.append([b"AC", b"G", b"CAG", b"TTA", b"GATC"][int(r.integers(0, 5))] * int(r.integers(3, 12)))
         t = b"".join(parts)
         assert len(t) > 1 << 16
-        if case.endswith("small_lists"):
-            monkeypatch.setenv("BWTMI_LS_CAP", "3000")
     else:   # one base repeated: a large group that loses 16 suffixes per round
         t = rnd(300) + b"G" * 2500 + rnd(300)
-    _check_index(t + b"$")
+    from bwtmi import _lib
+    with _lib.knobs(LS_CAP=3000 if case.endswith("small_lists") else -1):
+        _check_index(t + b"$")
 
 
 @pytest.mark.parametrize("case", ["gaps_300k", "n_only", "n_edges", "seven_symbols", "long_n_run", "groups_with_n",
@@ -476,20 +512,28 @@ def test_small_alphabet_suffix_sort_vs_oracle(gpu_ctx, case):
     _check_index(t + b"$")
 
 
+def test_small_alphabet_texts_through_general_doubling(gpu_ctx):
+    """BWTMI_SA_SMALL=0: gap texts take the general prefix doubling (index.hip)
+    instead of the 3-bit string sort; the same arrays as the oracle."""
+    from bwtmi import _lib, synth
+    with _lib.knobs(SA_SMALL=0):
+        _check_index(synth.generate_contig(200_000, 15, gaps="n2") + b"$")
+        _check_index(_planted(20_000, 16, b"ACGTNRY") + b"$")
+
+
 @pytest.mark.parametrize("rank", ["packed", "bytes"])
-def test_backward_search_all_short_motifs(gpu_ctx, monkeypatch, rank):
+def test_backward_search_all_short_motifs(gpu_ctx, rank):
     """Both rank structures: the packed 2-bit blocks of ACGT texts (k_bsearch2)
     and the byte BWT + sampled Occ (k_bsearch, BWTMI_FM_BYTES=1)."""
-    from bwtmi import BWTCore, MotifUtils, synth
-    if rank == "bytes":
-        monkeypatch.setenv("BWTMI_FM_BYTES", "1")
+    from bwtmi import BWTCore, MotifUtils, _lib, synth
     text = synth.generate_contig(50000, 77) + b"$"
     core = BWTCore(text.decode())
     ref = oracle.Index(text)
     pats = [m for k in range(1, 7) for m in MotifUtils.enumerate_motifs(k)]
     pats += ["ACGTACGTAC", "N", "", "TTTTTTTTTT", "GATTACA", "$", "A$", "$A", "C$", text[-9:].decode(),
              text[:12].decode(), text[100:164].decode(), "ACGN"]
-    got = core.backward_search_batch(pats)
+    with _lib.knobs(FM_BYTES=int(rank == "bytes")):
+        got = core.backward_search_batch(pats)
     for p, (sp, ep) in zip(pats, got.tolist()):
         assert (sp, ep) == ref.backward_search(p.encode()), p
 

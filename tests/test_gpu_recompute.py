@@ -128,38 +128,3 @@ def test_device_recompute_reference_fixtures(gpu_ctx, golden_dir):
             assert (got[6], got[0], got[1]) == (want["consensus"], want["copies"], want["consumed"])
         n += 1
     assert n > 0
-
-
-_CLI_LOOP = """
-import hashlib, json, os, sys
-sys.path[:0] = [sys.argv[1], os.path.join(sys.argv[1], "bwt-algorithm_amd")]
-from bwtmi import cli
-cases, out = json.loads(sys.argv[2]), sys.argv[3]
-got = {}
-for key, fa, args in cases:
-    assert cli.main([fa, "-o", out, "--jobs", "0"] + args) == 0, key
-    got[key] = hashlib.sha256(open(out, "rb").read()).hexdigest()
-print(json.dumps(got))
-"""
-
-
-def test_merge_fold_with_device_recomputes_matches_goldens(golden_dir, tmp_path):
-    """The drop-in CLI with the fold's fresh-pair recomputes on the device for
-    every unit (BWTMI_POST_DEVICE=1, BWTMI_POST_DEVICE_MIN=0), in a fresh
-    process: the reference goldens of every fixture FASTA and format, byte for
-    byte."""
-    import subprocess
-    import sys
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    with open(os.path.join(golden_dir, "expected_cli.json")) as f:
-        exp = json.load(f)
-    cases = [(k, os.path.join(golden_dir, "inputs", v["input"]), list(v["args"])) for k, v in sorted(exp.items())
-             if "--jobs" not in v["args"]]
-    env = dict(os.environ, BWTMI_POST_DEVICE="1", BWTMI_POST_DEVICE_MIN="0")
-    r = subprocess.run([sys.executable, "-c", _CLI_LOOP, repo, json.dumps(cases), str(tmp_path / "o.out")], env=env,
-                       capture_output=True, timeout=600)
-    assert r.returncode == 0, r.stderr.decode()[-2000:]
-    got = json.loads(r.stdout.decode().strip().splitlines()[-1])
-    assert len(got) == len(cases) >= 30
-    for k, sha in got.items():
-        assert sha == exp[k]["sha256"], k

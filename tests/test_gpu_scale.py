@@ -209,6 +209,95 @@ def test_cli_self_launched_ranks_match_one_process(gpu_ctx, tmp_path):
         assert one.read_bytes().count(b"\n") > 100, fmt
 
 
+def test_cli_eight_self_launched_ranks_match_c4_golden(gpu_ctx, golden_dir, tmp_path):
+    """C4 (8 x 12.5 Mbp, BASELINE configs[3]) through `bwt.py C4.fa --jobs 8`
+    with 8 self-launched ranks (rehearsed on one GPU: BWTMI_CLI_RANKS=8, host
+    transport): each rank loads its share of the file (split loader), scans,
+    post-processes and writes its rows into the shared file; the file must
+    equal the C4 golden of the reference pipeline (bwt.py:3850-3912)."""
+    import hashlib
+    import json
+    import subprocess
+    import sys
+    from bwtmi import synth
+    with open(os.path.join(golden_dir, "expected_large.json")) as f:
+        g = json.load(f)["C4"]
+    fa = str(tmp_path / "C4.fa")
+    assert synth.write_fasta(fa, g["lengths"], g["sub_rate"], g.get("first_index", 1), g.get("gaps")) == \
+        g["fasta_sha256"]
+    out = tmp_path / "C4.tab"
+    script = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bwt-algorithm_amd", "bwt.py")
+    env = dict(os.environ, BWTMI_CLI_RANKS="8")
+    r = subprocess.run([sys.executable, script, fa, "-o", str(out), "--jobs", "8"] + list(g["args"]),
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    data = out.read_bytes()
+    assert data.count(b"\n") - 1 == g["out_rows"]
+    assert hashlib.sha256(data).hexdigest() == g["out_sha256"]
+
+
+def test_scan_and_index_lanes_switches(gpu_ctx):
+    """A multi-contig job's strict scans and background index builds on 1 lane
+    (BWTMI_SCAN_LANES=1, BWTMI_INDEX_LANES=1) or 8: the same records."""
+    from bwtmi import _lib, synth
+    from bwtmi.records import Job
+    seqs = [synth.generate_contig(150_000 + 40_000 * i, 70 + i, 0.02, gaps="n1" if i % 3 == 0 else None)
+            for i in range(7)]
+
+    def run():
+        j = Job(min_copies=3, show_progress=True, build_index=True, threads=8)
+        for i, s in enumerate(seqs):
+            j.add_contig(f"chr{i + 1}", s, 30, 30)
+        j.scan(gpu_ctx)
+        j.postprocess()
+        j.wait(gpu_ctx)
+        return j.render("strfinder")
+    want = run()
+    assert want.count(b"\n") > 1000
+    for kv in ({"SCAN_LANES": 1, "INDEX_LANES": 1}, {"SCAN_LANES": 8, "INDEX_LANES": 8}):
+        with _lib.knobs(**kv):
+            assert run() == want, kv
+
+
+def test_bind_host_moves_and_restores_affinity(gpu_ctx):
+    """bwtmi_bind_host: host work onto the GPU's NUMA node (a subset of that
+    node's CPUs; with BWTMI_NUMA_SMT=1 the node's allowed CPUs), and back."""
+    from bwtmi import _lib
+    before = os.sched_getaffinity(0)
+    for smt in (0, 1):
+        with _lib.knobs(NUMA_SMT=smt):
+            changed = _lib.bind_host(gpu_ctx)
+            now = os.sched_getaffinity(0)
+            if changed:
+                assert now < before, (smt, sorted(now)[:8])
+            else:
+                assert now == before
+            _lib.bind_host(gpu_ctx, False)
+            assert os.sched_getaffinity(0) == before
+
+
+def test_ktrace_records_every_launch(gpu_ctx, tmp_path):
+    """BWTMI_KTRACE=path: one line per kernel launch (name, ms, idle ms) and a
+    marker per resolved batch, appended to the file."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path[:0] = [%r, %r]\n"
+            "import numpy as np\n"
+            "from bwtmi import synth\n"
+            "from bwtmi.tiers import strict_scan_hits\n"
+            "print(len(strict_scan_hits(np.frombuffer(synth.generate_contig(200000, 3), dtype=np.uint8), 1, 1000, 3)))\n"
+            % (repo, os.path.join(repo, "bwt-algorithm_amd")))
+    trace = tmp_path / "k.txt"
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, BWTMI_KTRACE=str(trace)),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = trace.read_text().splitlines()
+    names = [ln.split()[0] for ln in lines if not ln.startswith("--")]
+    assert "k_runs" in names and "radix_hist" in names and any(ln.startswith("-- resolve") for ln in lines)
+    assert all(len(ln.split()) == 3 for ln in lines if not ln.startswith("--"))
+
+
 def test_rccl_one_rank_collectives_and_sharded_write(gpu_ctx, golden_dir, tmp_path):
     """The RCCL transport on one rank (ncclCommInitRank with nranks = 1):
     int64 SUM / MAX with negative values and float64 MAX come back exactly,

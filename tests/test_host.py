@@ -220,8 +220,8 @@ def test_edge_inputs_match_reference_goldens(golden_dir, built_lib):
         assert hashlib.sha256(j.render(d["fmt"])).hexdigest() == m["sha256"], name
 
 
-@pytest.mark.parametrize("task", ["0", "-1"])
-def test_worker_exception_returns_an_error(built_lib, monkeypatch, task):
+@pytest.mark.parametrize("task", [0, -2])
+def test_worker_exception_returns_an_error(built_lib, task):
     """An exception inside a pooled worker task (the first, run by the caller
     thread, and the last, run by a pool thread) comes back through the C ABI as
     an error; the pool stays usable and the next call gives the normal result."""
@@ -238,10 +238,9 @@ def test_worker_exception_returns_an_error(built_lib, monkeypatch, task):
         j.postprocess()
         return j.render("strfinder")
     want = run()
-    monkeypatch.setenv("BWTMI_FAIL_MERGE_CHUNK", task)
-    with pytest.raises(_lib.BwtmiError, match="injected failure"):
-        run()
-    monkeypatch.delenv("BWTMI_FAIL_MERGE_CHUNK")
+    with _lib.knobs(FAIL_MERGE_CHUNK=task):   # -2: the last task
+        with pytest.raises(_lib.BwtmiError, match="injected failure"):
+            run()
     assert run() == want
 
 

@@ -1,0 +1,229 @@
+"""Build provenance, run-time switches and host placement (CPU only).
+
+- the loaded libbwtmi.so was built from this tree's sources (embedded hash);
+- every BWTMI_* variable the library reads is a documented switch
+  (INTEGRATION.md "Run-time switches") that some test sets;
+- the host switches select paths with the same results;
+- the NUMA placement planner on a faked sysfs tree (2 nodes x 4 GPUs, 8 ranks).
+"""
+import glob
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(REPO, "bwt-algorithm_amd", "csrc")
+
+
+def _integration_switches():
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    sec = text[text.index("## Run-time switches"):]
+    nxt = sec.find("\n## ", 3)
+    sec = sec if nxt < 0 else sec[:nxt]
+    return set(re.findall(r"`BWTMI_([A-Z0-9_]+)`", sec))
+
+
+def test_library_built_from_this_tree(built_lib):
+    from bwtmi import _lib
+    h = _lib.check_build()
+    assert re.fullmatch(r"[0-9a-f]{64}", h)
+    assert h in built_lib.bwtmi_version().decode()
+
+
+def test_knob_registry_get_set_restore(built_lib):
+    from bwtmi import _lib
+    import ctypes as C
+    names = _lib.knob_names()
+    assert len(names) == len(set(names)) >= 15
+    for n in names:
+        d = C.c_int64()
+        _lib.check(built_lib.bwtmi_knob_default(n.encode(), C.byref(d)))
+        old = _lib.knob(n)
+        with _lib.knobs(**{n: old + 7}):
+            assert _lib.knob(n) == old + 7
+            assert _lib.knob("BWTMI_" + n) == old + 7    # the prefix is accepted
+        assert _lib.knob(n) == old
+    with pytest.raises(_lib.BwtmiError):
+        _lib.knob("NO_SUCH_SWITCH")
+
+
+def test_every_switch_is_documented_and_tested(built_lib):
+    """Every getenv("BWTMI_...") left in csrc/ and every registry switch is listed
+    in INTEGRATION.md and set by at least one test (verdict r4 #6)."""
+    from bwtmi import _lib
+    src = ""
+    for f in glob.glob(os.path.join(CSRC, "*")):
+        src += open(f, errors="replace").read()
+    env = set(re.findall(r'getenv\("BWTMI_([A-Z0-9_]+)"\)', src))
+    every = env | set(_lib.knob_names())
+    documented = _integration_switches()
+    assert every <= documented, sorted(every - documented)
+    tests = ""
+    for f in glob.glob(os.path.join(REPO, "tests", "*.py")):
+        if os.path.basename(f) != "test_knobs.py":
+            tests += open(f).read()
+    tests += open(__file__).read().split("# ---- switch " + "exercisers")[-1]
+    untested = [n for n in sorted(every) if not re.search(r"\b(BWTMI_)?%s\b" % n, tests)]
+    assert not untested, untested
+
+
+# ---- switch exercisers (the host paths they select give the same results)
+def _post(contigs, threads):
+    from bwtmi.records import Job
+    j = Job(min_copies=3, show_progress=True, threads=threads)
+    for i, seq in enumerate(contigs):
+        j.add_contig(f"chr{i + 1}", seq, 30, 30)
+        j.add_hits(i, oracle.strict_scan(seq[30:len(seq) - 30], 1, 1000, 0, 3))
+    j.postprocess()
+    return j.render("strfinder")
+
+
+def test_unit_groups_and_pool_spin_switches(built_lib):
+    """BWTMI_UNIT_GROUP_THREADS (threads per unit group of a multi-contig job)
+    and BWTMI_POOL_SPIN_US (0: workers block at once) change only the schedule."""
+    from bwtmi import _lib, synth
+    contigs = [synth.generate_contig(60_000 + 7_000 * i, 50 + i, 0.02) for i in range(6)]
+    want = _post(contigs, 8)
+    for kv in ({"UNIT_GROUP_THREADS": 1}, {"UNIT_GROUP_THREADS": 16}, {"POOL_SPIN_US": 0},
+               {"POOL_SPIN_US": 500, "UNIT_GROUP_THREADS": 2}):
+        with _lib.knobs(**kv):
+            assert _post(contigs, 8) == want, kv
+
+
+def test_stats_switch_reports_stages(built_lib, capfd):
+    """BWTMI_STATS=1 prints the post-processing and writer stage timers on stderr
+    (and =2 the per-recompute counters); the output is unchanged."""
+    from bwtmi import _lib, synth
+    contigs = [synth.generate_contig(80_000, 61, 0.02)]
+    want = _post(contigs, 4)
+    capfd.readouterr()
+    for level in (1, 2):
+        with _lib.knobs(STATS=level):
+            assert _post(contigs, 4) == want
+        err = capfd.readouterr().err
+        assert "merge" in err and "collapse" in err, err[-500:]
+
+
+def test_no_plain_loader_switch(tmp_path, built_lib):
+    """BWTMI_NO_PLAIN=1: every chunk of the FASTA goes line by line (no plain-chunk
+    fast path): the same contigs as the default loader and as load_reference."""
+    from bwtmi import _lib
+    from bwtmi.records import Job
+    from oracle import post
+    r = np.random.default_rng(5)
+    parts = []
+    for i in range(7):
+        seq = bytes(r.choice(np.frombuffer(b"ACGTNacgt", dtype=np.uint8), int(r.integers(50, 300_000))))
+        w = int(r.integers(1, 200))
+        parts.append(b">c%d desc\n" % i + b"\n".join(seq[k:k + w] for k in range(0, len(seq), w)) + b"\n")
+    path = str(tmp_path / "p.fa")
+    open(path, "wb").write(b"".join(parts))
+    seqs, full, offs = post.load_fasta(path, 30)
+    for flag in (0, 1):
+        with _lib.knobs(NO_PLAIN=flag):
+            j = Job(threads=5)
+            j.load_fasta(path, 30)
+            assert j.names == list(seqs)
+            for cid, nm in enumerate(j.names):
+                assert j.contig_seq(cid).decode() == full[nm], (flag, nm)
+
+
+_DUMP = """
+import sys
+sys.path[:0] = [{repo!r}, {pkg!r}]
+import oracle
+from bwtmi import synth
+from bwtmi.records import Job
+seq = synth.generate_contig(60_000, 9, 0.03)
+j = Job(min_copies=3, show_progress=True, threads=2)
+j.add_contig("c", seq, 30, 30)
+j.add_hits(0, oracle.strict_scan(seq[30:len(seq) - 30], 1, 1000, 0, 3))
+j.postprocess()
+print(j.count())
+"""
+
+
+def test_dump_recompute_hook_writes_the_dp_arguments(tmp_path, built_lib):
+    """BWTMI_DUMP_RECOMPUTE=path (tools/recompute_bench.cpp input): the merge
+    fold's DP recomputes are appended to the file; the records are unchanged."""
+    code = _DUMP.format(repo=REPO, pkg=os.path.join(REPO, "bwt-algorithm_amd"))
+    base = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert base.returncode == 0, base.stderr[-2000:]
+    dump = tmp_path / "rc.bin"
+    env = dict(os.environ, BWTMI_DUMP_RECOMPUTE=str(dump))
+    got = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert got.returncode == 0, got.stderr[-2000:]
+    assert got.stdout == base.stdout
+    assert dump.exists() and dump.stat().st_size > 0
+
+
+# ---- NUMA placement planner
+def _fake_sysfs(root, gpus_per_node=4, nodes=2, cores_per_node=32):
+    """2 sockets x 32 cores x 2 hardware threads: node k holds cores
+    [32k, 32k + 32) and their siblings + 64; GPU g sits on node g // 4."""
+    total = nodes * cores_per_node
+    for k in range(nodes):
+        d = root / "devices/system/node" / f"node{k}"
+        d.mkdir(parents=True)
+        lo = k * cores_per_node
+        (d / "cpulist").write_text(f"{lo}-{lo + cores_per_node - 1},{lo + total}-{lo + total + cores_per_node - 1}\n")
+    for c in range(2 * total):
+        t = root / "devices/system/cpu" / f"cpu{c}" / "topology"
+        t.mkdir(parents=True)
+        core = c % total
+        (t / "physical_package_id").write_text(f"{core // cores_per_node}\n")
+        (t / "core_id").write_text(f"{core % cores_per_node}\n")
+    pci = []
+    for g in range(nodes * gpus_per_node):
+        addr = f"0000:{0x10 + 0x20 * g:02x}:00.0"
+        d = root / "bus/pci/devices" / addr
+        d.mkdir(parents=True)
+        (d / "numa_node").write_text(f"{g // gpus_per_node}\n")
+        pci.append(addr.upper())     # HIP reports upper-case hex
+    return pci
+
+
+def test_binding_plan_two_nodes_four_gpus_each(tmp_path, built_lib):
+    from bwtmi import _lib
+    pci = _fake_sysfs(tmp_path)
+    root = str(tmp_path)
+    allowed = "0-127"
+    node0_all, node1_all = "0-31,64-95", "32-63,96-127"
+    for r in range(8):
+        # 16 threads per rank: 4 ranks x 20 > 32 cores -> the node's hardware threads, siblings kept
+        got, node, peers = _lib.binding_plan(root, r, pci, 16, allowed)
+        assert (node, peers) == (r // 4, 4)
+        assert got == (node0_all if r < 4 else node1_all), (r, got)
+        # 4 threads per rank: the 4 ranks ON THIS NODE x 8 = 32 cores -> one thread per core
+        # (counting all 8 local ranks, 64 > 32, kept the siblings: the round-4 bug)
+        got, node, peers = _lib.binding_plan(root, r, pci, 4, allowed)
+        assert got == ("0-31" if r < 4 else "32-63"), (r, got)
+        # smt keeps the siblings
+        got, _, _ = _lib.binding_plan(root, r, pci, 4, allowed, smt=True)
+        assert got == (node0_all if r < 4 else node1_all)
+    # all 8 ranks' GPUs on node 0 (e.g. one visible device): 8 x 8 > 32 -> siblings kept
+    same = [pci[0]] * 8
+    got, node, peers = _lib.binding_plan(root, 3, same, 4, allowed)
+    assert (got, node, peers) == (node0_all, 0, 8)
+    # already inside the node: nothing to change
+    assert _lib.binding_plan(root, 0, pci, 4, "0-15")[0] == ""
+    # the node's allowed CPUs cannot hold the rank's threads: no binding
+    assert _lib.binding_plan(root, 0, pci, 16, "0-7,32-63")[0] == ""
+    # allowed set limits the choice
+    assert _lib.binding_plan(root, 5, pci, 4, "0-127")[0] == "32-63"
+    assert _lib.binding_plan(root, 5, pci, 2, "20-47,84-111")[0] == "32-47,96-111"   # 16 cores < 4 x 6
+    # unknown GPU node
+    assert _lib.binding_plan(root, 0, ["0000:ff:00.0"] + pci[1:], 4, allowed)[1] == -1
+
+
+def test_library_does_not_bind_by_default(built_lib):
+    """bwtmi_open leaves the caller's affinity alone unless asked (the CLI sets
+    BWTMI_NUMA_BIND, bench.py calls bwtmi_bind_host)."""
+    from bwtmi import _lib
+    assert _lib.knob("NUMA_BIND") == 0 or os.environ.get("BWTMI_NUMA_BIND") == "1"
