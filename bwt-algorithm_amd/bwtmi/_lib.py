@@ -131,6 +131,8 @@ _SIGS = {
     "bwtmi_wire_record_size": (C.c_int, []),
     "bwtmi_job_contig_error": (C.c_int64, [_P, C.c_int32, C.c_char_p, C.c_int64]),
     "bwtmi_source_hash": (C.c_char_p, []),
+    "bwtmi_trace_push": (C.c_int, [C.c_char_p]),
+    "bwtmi_trace_pop": (C.c_int, []),
     "bwtmi_knob_set": (C.c_int, [C.c_char_p, C.c_int64]),
     "bwtmi_knob_get": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64)]),
     "bwtmi_knob_default": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64)]),

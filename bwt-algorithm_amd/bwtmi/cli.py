@@ -36,6 +36,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--min-copies", type=int, default=3, help="Minimum number of copies required (default: 3)")
     p.add_argument("--min-entropy", type=float, default=1.0,
                    help="Minimum Shannon entropy to avoid low-complexity (default: 1.0)")
+    p.add_argument("--profile", metavar="JSON", default=None,
+                   help="write per-stage wall ms / calls / bytes of this run to JSON (rank r of N: JSON.rankR)")
     p.add_argument("--flank-trim", type=int, default=30,
                    help="Trim N bp from each end before analysis (default: 30, use 0 to disable)")
     return p
@@ -132,6 +134,16 @@ def main(argv=None) -> int:
     # (bwtmi_open reads the switch; a library user's affinity is never touched)
     from . import _lib
     _lib.knob("NUMA_BIND", 1)
+    from . import profile
+    prof = profile.start() if a.profile else None
+    rc = _run(a, tier2)
+    if prof is not None:
+        path = a.profile if int(os.environ.get("WORLD_SIZE", "1")) == 1 else f"{a.profile}.rank{os.environ.get('RANK', '0')}"
+        prof.write(path)
+    return rc
+
+
+def _run(a, tier2) -> int:
     finder = TandemRepeatFinder(a.reference, a.sa_sample, show_progress=a.progress,
                                 allow_mismatches=not a.no_mismatches, max_motif_length=a.max_motif_len,
                                 min_period=a.min_period, max_period=a.max_period,

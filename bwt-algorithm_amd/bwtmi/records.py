@@ -9,6 +9,7 @@ them natively (bwt.py:4141-4198).
 from __future__ import annotations
 
 import ctypes as C
+import os
 import functools
 import math
 from dataclasses import dataclass
@@ -143,6 +144,13 @@ class Job:
         sequences are built on the device from the file bytes and the host copies
         are written behind the next scan (bwtmi_job_load_fasta_dev /
         _parts_dev): upload() has nothing left to do."""
+        from . import profile
+        with profile.stage("load", os.path.getsize(path) if os.path.exists(path) else 0):
+            self._load_fasta(path, flank_trim, world, rank, comm, dev_ctx)
+        if profile.active() is not None:
+            profile.active().info["bases"] = int(sum(self.contig_weight(i) for i in range(self.contig_count())))
+
+    def _load_fasta(self, path, flank_trim, world, rank, comm, dev_ctx) -> None:
         if dev_ctx is not None and world <= 1:
             check(lib().bwtmi_job_load_fasta_dev(dev_ctx, self.h, path.encode(), flank_trim))
         elif world > 1 and comm is not None:
@@ -204,14 +212,22 @@ class Job:
 
     # pipeline -----------------------------------------------------------
     def upload(self, dev_ctx) -> None:
-        check(lib().bwtmi_job_upload(dev_ctx, self.h))
+        from . import profile
+        with profile.stage("upload"):
+            check(lib().bwtmi_job_upload(dev_ctx, self.h))
 
     def scan(self, dev_ctx) -> None:
-        check(lib().bwtmi_job_scan(dev_ctx, self.h))
+        from . import profile
+        with profile.stage("scan"):
+            check(lib().bwtmi_job_scan(dev_ctx, self.h))
 
     def wait(self, dev_ctx) -> None:
         """Join the background FM index builds started by scan()."""
-        check(lib().bwtmi_job_wait(dev_ctx, self.h))
+        from . import profile
+        with profile.stage("index_wait"):
+            check(lib().bwtmi_job_wait(dev_ctx, self.h))
+        if profile.active() is not None:
+            profile.active().job_split(self)
 
     def reset(self) -> None:
         check(lib().bwtmi_job_reset(self.h))
@@ -245,7 +261,11 @@ class Job:
         return lib().bwtmi_job_raw_count(self.h)
 
     def postprocess(self) -> None:
-        check(lib().bwtmi_job_postprocess(self.h))
+        from . import profile
+        with profile.stage("postprocess"):
+            check(lib().bwtmi_job_postprocess(self.h))
+        if profile.active() is not None:
+            profile.active().info["records"] = self.count()
 
     def count(self) -> int:
         return lib().bwtmi_job_count(self.h)
@@ -259,7 +279,11 @@ class Job:
             lib().bwtmi_free(p)
 
     def write(self, fmt: str, path: str) -> None:
-        check(lib().bwtmi_job_write(self.h, _lib.FMT[fmt], path.encode()))
+        from . import profile
+        with profile.stage("write"):
+            check(lib().bwtmi_job_write(self.h, _lib.FMT[fmt], path.encode()))
+        if profile.active() is not None:
+            profile.active().add_bytes("write", os.path.getsize(path))
 
     # ---- sharded output (bwtmi.dist.write_sharded)
     def unit_count(self) -> int:
@@ -277,12 +301,16 @@ class Job:
         if row_base is not None:
             row_base = np.ascontiguousarray(row_base, dtype=np.int64)
             rb = row_base.ctypes.data
-        check(lib().bwtmi_job_render_units(self.h, _lib.FMT[fmt], rb, out.ctypes.data))
+        from . import profile
+        with profile.stage("write"):
+            check(lib().bwtmi_job_render_units(self.h, _lib.FMT[fmt], rb, out.ctypes.data))
         return out
 
     def write_units(self, path: str, offsets: np.ndarray, write_header: bool) -> None:
         offsets = np.ascontiguousarray(offsets, dtype=np.int64)
-        check(lib().bwtmi_job_write_units(self.h, path.encode(), offsets.ctypes.data, int(write_header)))
+        from . import profile
+        with profile.stage("write"):
+            check(lib().bwtmi_job_write_units(self.h, path.encode(), offsets.ctypes.data, int(write_header)))
 
     def export(self) -> bytes:
         p, n = C.c_void_p(), C.c_int64()

@@ -77,6 +77,8 @@ GAP_PROFILES = {
     "n1": dict(runs=[(2_000, 40_000, 1, 2)], iupac=(1, 20_000)),
     # n1 plus long gaps of 10 kbp - 1 Mbp every ~10 Mbp (~4-5 % N at 100 Mbp)
     "n2": dict(runs=[(2_000, 40_000, 1, 2), (3_000_000, 17_000_000, 4, 5)], iupac=(1, 20_000)),
+    # n1 plus runs of 5 - 20 kbp (uniform) every 20-60 kbp: the pure-reference gap golden (G300Np)
+    "n3": dict(runs=[(2_000, 40_000, 1, 2), (20_000, 60_000, 5_000, 20_000, "uniform")], iupac=(1, 20_000)),
 }
 
 
@@ -85,15 +87,20 @@ def _gap_layout(length: int, seed: int, profile: str) -> Tuple[List[Tuple[int, i
     base of one contig under a GAP_PROFILES profile."""
     prof = GAP_PROFILES[profile]
     runs = []
-    for k, (lo, hi, d0, d1) in enumerate(prof["runs"]):
+    for k, spec in enumerate(prof["runs"]):
+        lo, hi, d0, d1 = spec[:4]
+        uniform = len(spec) > 4   # (spacing lo, hi, length lo, hi, "uniform")
         rng = _Stream(_mix_int(seed ^ (0x6A90 + k)))
         cur = 0
         while True:
             cur += lo + rng.below(hi - lo + 1)
             if cur >= length:
                 break
-            d = d0 + rng.below(d1 - d0 + 1)
-            ln = 10 ** d + rng.below(9 * 10 ** d)
+            if uniform:
+                ln = d0 + rng.below(d1 - d0 + 1)
+            else:
+                d = d0 + rng.below(d1 - d0 + 1)
+                ln = 10 ** d + rng.below(9 * 10 ** d)
             ln = min(ln, length - cur)
             runs.append((cur, ln))
             cur += ln

@@ -414,6 +414,7 @@ int bwtmi_strict_scan(bwtmi_ctx *ctx, const uint8_t *seq, int64_t n, int32_t min
 int bwtmi_index_build(bwtmi_ctx *ctx, const uint8_t *text, int64_t n, int32_t sa_sample, int32_t occ_sample,
                       uint32_t flags, bwtmi_index **out) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:index");
         CHECK_ARG(ctx && out && (text || n == 0) && n >= 0 && sa_sample > 0 && occ_sample > 0, "bad argument");
         *out = nullptr;
         Ctx &c = ctx->c;
@@ -622,6 +623,7 @@ int bwtmi_job_add_contig(bwtmi_job *job, const char *name, const uint8_t *full, 
 
 int bwtmi_job_load_fasta(bwtmi_job *job, const char *path, int32_t flank_trim) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:load");
         CHECK_ARG(job && path, "null argument");
         TEXT_JOIN(job);
         load_fasta(job->j, path, flank_trim);
@@ -714,6 +716,7 @@ struct DevLoad final : FastaDev {
 
 int bwtmi_job_load_fasta_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *path, int32_t flank_trim) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:load");
         CHECK_ARG(ctx && job && path, "null argument");
         Ctx &c = ctx->c;
         job->j.text_join();
@@ -741,6 +744,7 @@ int bwtmi_job_device_text(bwtmi_ctx *ctx, bwtmi_job *job, int32_t id, uint8_t *d
 
 int bwtmi_job_load_fasta_shard(bwtmi_job *job, const char *path, int32_t flank_trim, int32_t world, int32_t rank) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:load");
         CHECK_ARG(job && path && world >= 1 && rank >= 0 && rank < world, "bad argument");
         TEXT_JOIN(job);
         load_fasta(job->j, path, flank_trim, world, rank);
@@ -750,6 +754,7 @@ int bwtmi_job_load_fasta_shard(bwtmi_job *job, const char *path, int32_t flank_t
 int bwtmi_job_fasta_scan_part(bwtmi_job *job, const char *path, int32_t world, int32_t rank, int64_t **blob,
                               int64_t *nwords) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:load");
         CHECK_ARG(job && path && blob && nwords && world >= 1 && rank >= 0 && rank < world, "bad argument");
         TEXT_JOIN(job);
         std::vector<int64_t> v;
@@ -774,6 +779,7 @@ int64_t bwtmi_fasta_count_records(const char *path, int64_t limit) {
 int bwtmi_job_load_fasta_parts_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *path, int32_t flank_trim,
                                    int32_t world, int32_t rank, const int64_t *blob, int64_t nwords) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:load");
         CHECK_ARG(ctx && job && path && blob && nwords >= 6 && world >= 1 && rank >= 0 && rank < world,
                   "bad argument");
         Ctx &c = ctx->c;
@@ -789,6 +795,7 @@ int bwtmi_job_load_fasta_parts_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *p
 int bwtmi_job_load_fasta_parts(bwtmi_job *job, const char *path, int32_t flank_trim, int32_t world, int32_t rank,
                                const int64_t *blob, int64_t nwords) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:load");
         CHECK_ARG(job && path && blob && nwords >= 6 && world >= 1 && rank >= 0 && rank < world, "bad argument");
         TEXT_JOIN(job);
         fasta_load_parts(job->j, path, flank_trim, world, rank, blob, nwords);
@@ -876,6 +883,7 @@ static void job_upload(bwtmi_ctx *ctx, bwtmi_job *job) {
 
 int bwtmi_job_upload(bwtmi_ctx *ctx, bwtmi_job *job) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:upload");
         CHECK_ARG(ctx && job, "null argument");
         job_upload(ctx, job);
     });
@@ -923,6 +931,7 @@ int bwtmi_job_select(bwtmi_job *job, const int32_t *ids, int32_t n) {
 
 int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:scan");
         CHECK_ARG(ctx && job, "null argument");
         auto t0 = std::chrono::steady_clock::now();
         job_upload(ctx, job);
@@ -1046,6 +1055,7 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
         job->dev.bg_ctx = &c;
         c.bg_link = &job->dev.bg_ctx;
         c.bg = std::thread([&c, sa_sample, to_index] {
+            BWTMI_STAGE("bwtmi:index");
             auto ti = std::chrono::steady_clock::now();
             try {
                 c.activate();
@@ -1121,6 +1131,7 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
 
 int bwtmi_job_wait(bwtmi_ctx *ctx, bwtmi_job *job) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:index_wait");
         CHECK_ARG(ctx && job, "null argument");
         const bool ran = ctx->c.bg.joinable();
         ctx_wait(ctx->c);
@@ -1153,6 +1164,7 @@ int64_t bwtmi_job_raw_count(const bwtmi_job *job) {
 
 int bwtmi_job_postprocess(bwtmi_job *job) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:postprocess");
         CHECK_ARG(job, "null argument");
         TEXT_JOIN(job);
         Job &J = job->j;
@@ -1164,6 +1176,7 @@ int64_t bwtmi_job_count(const bwtmi_job *job) { return job ? (int64_t)job->j.fin
 
 int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:write");
         CHECK_ARG(job && out && len, "null argument");
         TEXT_JOIN(job);
         const std::vector<Text> parts = render_parts(job->j, fmt);
@@ -1187,6 +1200,7 @@ int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len) {
 // open(path, 'w') + write (the file is overwritten in place, then cut).
 int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:write");
         CHECK_ARG(job && path, "null argument");
         TEXT_JOIN(job);
         OutFd out(path);
@@ -1251,6 +1265,7 @@ int bwtmi_job_unit_rows(bwtmi_job *job, int64_t *unit_rows) {
 
 int bwtmi_job_render_units(bwtmi_job *job, int fmt, const int64_t *row_base, int64_t *bytes) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:write");
         CHECK_ARG(job && bytes, "null argument");
         TEXT_JOIN(job);
         Job &J = job->j;
@@ -1264,6 +1279,7 @@ int bwtmi_job_render_units(bwtmi_job *job, int fmt, const int64_t *row_base, int
 
 int bwtmi_job_write_units(bwtmi_job *job, const char *path, const int64_t *offsets, int write_header) {
     return guard([&] {
+        BWTMI_STAGE("bwtmi:write");
         CHECK_ARG(job && path && offsets, "null argument");
         TEXT_JOIN(job);
         Job &J = job->j;

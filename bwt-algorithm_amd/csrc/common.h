@@ -437,6 +437,15 @@ enum Knob {
     KN_HOST_SCREEN, KN_NO_PLAIN, KN_INDEX_LANES, KN_SCAN_LANES, KN_NO_AVX512, KN_POOL_SPIN_US,
     KN_UNIT_GROUP_THREADS, KN_STATS, KN_NUMA_BIND, KN_NUMA_SMT, KN_FAIL_MERGE_CHUNK, KN_COUNT
 };
+// a roctx range for the lifetime of the object (trace.cpp); names "bwtmi:<stage>"
+struct StageRange {
+    explicit StageRange(const char *name);
+    ~StageRange();
+    StageRange(const StageRange &) = delete;
+    StageRange &operator=(const StageRange &) = delete;
+};
+#define BWTMI_STAGE(name) ::bwtmi::StageRange bwtmi_stage_range_(name)
+
 extern std::atomic<int64_t> g_knobs[KN_COUNT];
 inline int64_t knob(Knob k) { return g_knobs[k].load(std::memory_order_relaxed); }
 inline bool stats_on(int level = 1) { return knob(KN_STATS) >= level; }

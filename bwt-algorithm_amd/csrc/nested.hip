@@ -230,7 +230,7 @@ __global__ __launch_bounds__(T) void k_seg_levels(const int64_t *__restrict__ S,
     __shared__ int32_t sM[CAP];
     __shared__ uint8_t sK[CAP];
     __shared__ unsigned long long found;
-    __shared__ int lvl;
+    __shared__ int pend[3];
     const int tid = threadIdx.x;
     const int64_t nwin = LARGE ? (int64_t)*ovf_n : (int64_t)gridDim.x;
     for (int64_t q = blockIdx.x; q < nwin; q += LARGE ? (int64_t)gridDim.x : nwin) {
@@ -293,21 +293,49 @@ __global__ __launch_bounds__(T) void k_seg_levels(const int64_t *__restrict__ S,
             return false;
         };
         for (int i = tid; i < len; i += T) sK[i] = nested_among(i, false) ? kUndecided : 1;
-        int cur = 0x7fffffff;   // levels below this one are still undecided
-        for (;;) {
-            if (tid == 0) lvl = -1;
+        // Rounds instead of levels: an undecided hit is decided as soon as the
+        // longer-motif spans that would nest it are decided -- suppressed by the
+        // first KEPT one (final, whatever else is pending), kept when none is
+        // kept and none is pending.  That is the reference's level order's
+        // outcome (a hit only ever reads decisions of strictly longer motifs),
+        // reached in as many rounds as the longest chain of such dependencies
+        // (a handful) instead of one barrier pair per distinct motif length.
+        volatile uint8_t *vK = sK;   // entries of other hits change during a round
+        auto decide = [&](int i) -> uint8_t {   // 0 nested, 1 kept, kUndecided: wait
+            const int64_t s0 = sS[i], e0 = sE[i], rl = e0 - s0;
+            const int64_t m = sM[i];
+            int lo = i + 1, hi = len;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (sS[mid] < e0) lo = mid + 1;
+                else hi = mid;
+            }
+            bool wait = false;
+            for (int k = lo - 1; k >= 0 && sP[k] > s0; --k) {
+                const int64_t Mk = sM[k];
+                if (Mk <= m) continue;
+                const uint8_t dk = vK[k];
+                if (dk == 0) continue;
+                if (nested_by(s0, e0, m, rl, sS[k], sE[k], Mk, thr)) {
+                    if (dk == 1) return 0;
+                    wait = true;
+                }
+            }
+            return wait ? kUndecided : 1;
+        };
+        if (tid == 0) pend[0] = pend[1] = pend[2] = 0;
+        __syncthreads();
+        for (int r = 0;; ++r) {
+            for (int i = tid; i < len; i += T) {
+                if (vK[i] != kUndecided) continue;
+                const uint8_t res = decide(i);
+                if (res == kUndecided) pend[r % 3] = 1;
+                else vK[i] = res;
+            }
+            // the flag of round r + 1: last read after round r - 2's barrier
+            if (tid == 0) pend[(r + 1) % 3] = 0;
             __syncthreads();
-            int mx = -1;
-            for (int i = tid; i < len; i += T)
-                if (sK[i] == kUndecided && sM[i] < cur && sM[i] > mx) mx = sM[i];
-            if (mx >= 0) atomicMax(&lvl, mx);
-            __syncthreads();
-            const int m = lvl;   // uniform
-            if (m < 0) break;
-            for (int i = tid; i < len; i += T)
-                if (sM[i] == m && sK[i] == kUndecided) sK[i] = nested_among(i, true) ? 0 : 1;
-            cur = m;
-            __syncthreads();
+            if (!pend[r % 3]) break;   // uniform: not reset before round r + 2
         }
         for (int i = tid; i < len; i += T) kept[a + i] = sK[i];
         __syncthreads();   // the LDS is refilled by the next window

@@ -16,6 +16,7 @@
 // always the current frame's slice [start, end) (trimmed before
 // _restore_reference_coordinates, full after), so it is never stored.
 #include <algorithm>
+#include <optional>
 #include <array>
 #include <atomic>
 #include <chrono>
@@ -1552,12 +1553,17 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
     auto t2 = clk::now();
     // 3. merge adjacent (bwt.py:3222-3289)
     OutChunks oc;
-    recs = merge_fold(u, pools, recs, nt, &oc, fill_fn ? &fill_fn : nullptr);
+    {
+        BWTMI_STAGE("bwtmi:merge");
+        recs = merge_fold(u, pools, recs, nt, &oc, fill_fn ? &fill_fn : nullptr);
+    }
     if (fill_fn) {
         ScreenedVec().swap(shits[(size_t)chroms[0]]);
         HitVec().swap(raw[(size_t)chroms[0]]);
     }
     auto t3 = clk::now();
+    std::optional<StageRange> rf;
+    rf.emplace("bwtmi:refine..filter");
     // 4. refine (bwt.py:3291-3314): done inside merge_fold's assembly
     auto r1 = clk::now();   // merge_fold returns its records in (start, end) order
     auto r2 = clk::now();
@@ -1687,6 +1693,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
         if (err) std::rethrow_exception(err);
     }
     auto t4 = clk::now();
+    rf.reset();
     if (stats_on()) {
         auto d = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         std::fprintf(stderr, "  merge %.1f (-> %zu) refine %.1f sort %.1f restore+sort %.1f collapse %.1f (%zu -> %zu) filter+mat %.1f ms\n",

@@ -177,6 +177,18 @@ __global__ __launch_bounds__(kBlock) void k_scan_lb(const uint32_t *__restrict__
 // then base[d] + prefix[t][d] + its rank in the tile.
 constexpr int kSub = 8192;   // keys per scatter tile (512 threads x 16)
 constexpr int kMaxSub = 4;
+constexpr int kLbWin = 16;   // predecessors a digit's look-back reads per step (loads in flight)
+template <class KT>
+__device__ __forceinline__ void hist_load(const KT *__restrict__ keys, int64_t tile, int64_t n, int vec,
+                                          uint4 (&v)[kSub / kBlock / (16 / sizeof(KT))]) {
+    constexpr int NV = kSub / kBlock / (16 / sizeof(KT));
+    const int64_t b0 = tile * kSub;
+    if (vec && b0 + kSub <= n) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(keys + b0);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) v[i] = src[i * kBlock + threadIdx.x];
+    }
+}
 template <class KT>
 __global__ __launch_bounds__(kBlock) void k_hist_lb(const KT *__restrict__ keys, int64_t n, int shift, int64_t ntiles,
                                                     int S, int64_t nhist, uint64_t *status,
@@ -189,6 +201,8 @@ __global__ __launch_bounds__(kBlock) void k_hist_lb(const KT *__restrict__ keys,
     const int wv = threadIdx.x >> 6, d = threadIdx.x, lane = threadIdx.x & 63;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) h[w][d] = 0;
+    uint4 cur[NV], nxt[NV];
+    hist_load<KT>(keys, ht * S, n, vec, cur);
     __syncthreads();
     uint32_t cnt[kMaxSub];
     uint32_t total = 0;
@@ -197,15 +211,13 @@ __global__ __launch_bounds__(kBlock) void k_hist_lb(const KT *__restrict__ keys,
         cnt[s] = 0;
         const int64_t tile = ht * S + s;
         if (s >= S || tile >= ntiles) continue;   // uniform
+        // the next sub-tile's keys are in flight while this one is counted
+        if (s + 1 < S && tile + 1 < ntiles) hist_load<KT>(keys, tile + 1, n, vec, nxt);
         const int64_t b0 = tile * kSub;
         if (vec && b0 + kSub <= n) {
-            uint4 v[NV];
-            const uint4 *src = reinterpret_cast<const uint4 *>(keys + b0);
-#pragma unroll
-            for (int i = 0; i < NV; ++i) v[i] = src[i * kBlock + threadIdx.x];
 #pragma unroll
             for (int i = 0; i < NV; ++i) {
-                const KT *k = reinterpret_cast<const KT *>(&v[i]);
+                const KT *k = reinterpret_cast<const KT *>(&cur[i]);
 #pragma unroll
                 for (int e = 0; e < VEC; ++e) atomicAdd(&h[wv][(uint32_t)(k[e] >> shift) & 255u], 1u);
             }
@@ -222,6 +234,8 @@ __global__ __launch_bounds__(kBlock) void k_hist_lb(const KT *__restrict__ keys,
         }
         cnt[s] = c;
         total += c;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) cur[i] = nxt[i];
         __syncthreads();
     }
     uint32_t excl = 0;
@@ -229,15 +243,25 @@ __global__ __launch_bounds__(kBlock) void k_hist_lb(const KT *__restrict__ keys,
         lb_store(status + d, lb_pack(epoch, kLbP, total));
     } else {
         lb_store(status + ht * 256 + d, lb_pack(epoch, kLbA, total));
-        for (int64_t j = ht - 1;;) {   // this lane's digit only
-            const uint64_t v = lb_load(status + j * 256 + d);
-            if (!lb_ready(v, epoch)) {
-                __builtin_amdgcn_s_sleep(1);
-                continue;
+        // this lane's digit: kLbWin predecessors per step, their loads in flight
+        // together; the ready ones in order are consumed, a step stops at the
+        // first inclusive prefix or the first unready granule (re-read next step)
+        for (int64_t j = ht - 1;;) {
+            uint64_t v[kLbWin];
+#pragma unroll
+            for (int i = 0; i < kLbWin; ++i) v[i] = j - i >= 0 ? lb_load(status + (j - i) * 256 + d) : lb_pack(epoch, kLbP, 0);
+            bool done = false;
+            int used = 0;
+#pragma unroll
+            for (int i = 0; i < kLbWin; ++i) {
+                if (done || used < i || !lb_ready(v[i], epoch)) continue;
+                excl += (uint32_t)v[i];
+                used = i + 1;
+                done = ((v[i] >> 32) & 3u) == kLbP;
             }
-            excl += (uint32_t)v;
-            if (((v >> 32) & 3u) == kLbP) break;
-            --j;
+            if (done) break;
+            j -= used;
+            if (used < kLbWin) __builtin_amdgcn_s_sleep(1);
         }
         lb_store(status + ht * 256 + d, lb_pack(epoch, kLbP, excl + total));
     }

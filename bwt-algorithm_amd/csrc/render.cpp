@@ -4,6 +4,7 @@
 // Python's "{x:.Nf}" and C's "%.Nf" both print the exact binary value rounded
 // half-to-even, so numeric columns are byte-identical.
 #include <algorithm>
+#include <optional>
 #include <chrono>
 #include <cinttypes>
 #include <cmath>
@@ -593,6 +594,7 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
     Compound comp;
     std::vector<Row> rows;
     if (fmt == BWTMI_FMT_STRFINDER) {
+        BWTMI_STAGE("bwtmi:compounds");
         detect_compounds(job, job.final_recs, comp, host_threads(job.params));
         rows.swap(comp.rows);
     } else {
@@ -695,6 +697,8 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
     out.part_unit.resize(chunks.size());
     for (size_t q = 0; q < chunks.size(); ++q) out.part_unit[q] = chunks[q].unit;
     auto t2 = std::chrono::steady_clock::now();
+    std::optional<StageRange> fr;
+    fr.emplace("bwtmi:format");
     run_tasks((int64_t)chunks.size(), host_threads(job.params), [&](int64_t ck) {
         Out o;
         const Chunk &C = chunks[(size_t)ck];
@@ -747,6 +751,7 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
         out.parts[(size_t)ck] = o.finish();
         if (on_part) (*on_part)((size_t)ck);
     });
+    fr.reset();
     auto t3 = std::chrono::steady_clock::now();
     job.stage_ms[6] = std::chrono::duration<double, std::milli>(t3 - t0).count();
     if (stats_on()) {

@@ -75,6 +75,11 @@ int bwtmi_host_binding_plan(const char *sysroot, int local_rank, const char *ran
  * once from the environment; get/set in-process by NAME (with or without the
  * BWTMI_ prefix).  Unknown names: BWTMI_E_ARG.  bwtmi_knob_names(): all names,
  * comma-separated. */
+/* roctx ranges (rocprofv3 --marker-trace): the library opens "bwtmi:<stage>"
+ * around load, upload, scan, index, merge, refine..filter, compounds, format,
+ * write and index_wait; a host application can nest its own with these. */
+int bwtmi_trace_push(const char *name);
+int bwtmi_trace_pop(void);
 int bwtmi_knob_set(const char *name, int64_t value);
 int bwtmi_knob_get(const char *name, int64_t *value);
 int bwtmi_knob_default(const char *name, int64_t *value);

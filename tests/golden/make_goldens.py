@@ -224,6 +224,50 @@ def _check_homopolymer_align(ref, orig, fast, cases=20000):
                              f"{seq!r} {start} {end} {tmpl!r} {frac} {mc}: {want} vs {got}")
 
 
+def _long_homopolymer_cases():
+    """Long one-base cases (verdict r4 #2): runs of 1 kbp - 200 kbp of the
+    template base inside ACGTNRY text, the walk starting before, at and inside
+    the run, its requested end inside, at and past the run (and end <= start),
+    every caller's arguments: _recompute_repeat's two attempts (bwt.py:3535-
+    3551: mismatch_fraction 0.1, min_copies max(1, min_copies) then 1) and
+    the variation scan (bwt.py:1277: 0.1, min_copies 1), min_copies 3 and 5 of
+    the CLI's --min-copies, and mismatch fractions 0.05 / 0.2."""
+    rng = np.random.default_rng(0x10C6)
+    alpha = "ACGTNRY"
+    cases = []
+    for run in (1_000, 4_999, 20_000, 75_000, 200_000):
+        for b in ("N", "A", "T"):
+            left = "".join(alpha[j] for j in rng.integers(0, len(alpha), int(rng.integers(0, 300))))
+            right = "".join(alpha[j] for j in rng.integers(0, len(alpha), int(rng.integers(0, 300))))
+            left = left.rstrip(b)
+            right = right.lstrip(b)
+            seq = left + b * run + right
+            r0, r1 = len(left), len(left) + run
+            starts = [max(0, r0 - 7), r0, r0 + int(rng.integers(1, run))]
+            for st in starts:
+                ends = [st, st - 3, min(len(seq), st + int(rng.integers(1, 40))), r1 - int(rng.integers(0, 5)), r1,
+                        min(len(seq) + 10, r1 + int(rng.integers(1, 50)))]
+                for en in ends:
+                    mc = int(rng.choice([1, 2, 3, 5]))
+                    frac = float(rng.choice([0.1, 0.1, 0.05, 0.2]))
+                    cases.append(dict(left=left, base=b, run=run, right=right, start=st, end=en, min_copies=mc,
+                                      mismatch_fraction=frac))
+    return cases
+
+
+def _check_homopolymer_align_long(ref, orig, fast):
+    """The closed form against the reference function on _long_homopolymer_cases."""
+    for i, c in enumerate(_long_homopolymer_cases()):
+        seq = c["left"] + c["base"] * c["run"] + c["right"]
+        want = orig(seq, c["start"], c["end"], c["base"], mismatch_fraction=c["mismatch_fraction"],
+                    min_copies=c["min_copies"])
+        got = fast(seq, c["start"], c["end"], c["base"], mismatch_fraction=c["mismatch_fraction"],
+                   min_copies=c["min_copies"])
+        if want != got:
+            raise SystemExit(f"homopolymer closed form differs from the reference on long case {i}: "
+                             f"{ {k: v for k, v in c.items() if k not in ('left', 'right')} }")
+
+
 def install_hybrid(ref, stub_index=True, restate_nested=True, homopolymer=False):
     import oracle
     from oracle import post
@@ -254,6 +298,7 @@ def install_hybrid(ref, stub_index=True, restate_nested=True, homopolymer=False)
     if homopolymer:
         orig, fast = _homopolymer_align(ref)
         _check_homopolymer_align(ref, orig, fast)
+        _check_homopolymer_align_long(ref, orig, fast)
         ref.MotifUtils.align_repeat_region = staticmethod(fast)
 
 
@@ -710,8 +755,34 @@ def cmd_edge(a):
         json.dump(man, f, indent=1, sort_keys=True)
 
 
+def cmd_homopolymer(a):
+    """The reference's align_repeat_region on the long one-base cases, as
+    fixtures (tests/golden/homopolymer_long.json: the case and the reference's
+    copies / consumed length, or null), and the closed form checked on them."""
+    ref = ref_module()
+    orig, fast = _homopolymer_align(ref)
+    t0 = time.time()
+    out = []
+    for c in _long_homopolymer_cases():
+        seq = c["left"] + c["base"] * c["run"] + c["right"]
+        r = orig(seq, c["start"], c["end"], c["base"], mismatch_fraction=c["mismatch_fraction"],
+                 min_copies=c["min_copies"])
+        rec = dict(c)
+        rec["want"] = None if r is None else dict(copies=r.copies, consumed=r.consumed_length,
+                                                   consensus=r.consensus, mismatch_rate=r.mismatch_rate,
+                                                   max_errors=r.max_errors_per_copy,
+                                                   ins=r.total_insertions, dels=r.total_deletions,
+                                                   variations=list(r.variations))
+        out.append(rec)
+    _check_homopolymer_align_long(ref, orig, fast)
+    with open(os.path.join(HERE, "homopolymer_long.json"), "w") as f:
+        json.dump(dict(seconds=round(time.time() - t0, 1), cases=out), f, indent=0)
+    print(len(out), "cases", round(time.time() - t0, 1), "s")
+
+
 def cmd_hybrid(a):
-    """Full-size golden via the validated hybrid oracle."""
+    """Full-size golden via the validated hybrid oracle (--pure: the reference
+    itself, nothing swapped)."""
     ref = ref_module()
     from bwtmi import synth
     cfg = synth.CONFIGS.get(a.config) if a.config else None
@@ -719,7 +790,8 @@ def cmd_hybrid(a):
     sub = cfg["sub_rate"] if cfg else a.sub_rate
     gaps = cfg.get("gaps") if cfg else a.gaps
     first = cfg.get("first_index", 1) if cfg else a.first_index
-    install_hybrid(ref, stub_index=True, restate_nested=True, homopolymer=bool(gaps) or a.homopolymer)
+    if not a.pure:
+        install_hybrid(ref, stub_index=True, restate_nested=True, homopolymer=bool(gaps) or a.homopolymer)
     work = a.work or tempfile.mkdtemp()
     fa = os.path.join(work, f"{a.name}.fa")
     t0 = time.time()
@@ -730,7 +802,8 @@ def cmd_hybrid(a):
     with open(outp, "rb") as f:
         data = f.read()
     rec = dict(config=a.config, lengths=lengths, sub_rate=sub, args=a.extra.split(),
-               gaps=gaps, first_index=first, homopolymer_closed_form=bool(gaps) or a.homopolymer,
+               gaps=gaps, first_index=first, pure_reference=bool(a.pure),
+               homopolymer_closed_form=(bool(gaps) or a.homopolymer) and not a.pure,
                fasta_sha256=fa_sha, out_sha256=hashlib.sha256(data).hexdigest(),
                out_rows=data.count(b"\n") - 1, seconds=round(time.time() - t0, 1))
     if a.keep_rows:
@@ -758,6 +831,7 @@ def main():
     sp.add_parser("tier3")
     sp.add_parser("simple")
     sp.add_parser("edge")
+    sp.add_parser("homopolymer")
     p = sp.add_parser("hybrid")
     p.add_argument("name")
     p.add_argument("--config")
@@ -766,6 +840,7 @@ def main():
     p.add_argument("--gaps", default=None, help="bwtmi.synth GAP_PROFILES name")
     p.add_argument("--first-index", type=int, default=1)
     p.add_argument("--homopolymer", action="store_true", help="validated one-base align closed form")
+    p.add_argument("--pure", action="store_true", help="the reference itself, nothing swapped")
     p.add_argument("--extra", default="")
     p.add_argument("--jobs", type=int, default=-1)
     p.add_argument("--work")
@@ -773,7 +848,7 @@ def main():
     p.add_argument("--save-out", action="store_true")
     a = ap.parse_args()
     dict(fixtures=cmd_fixtures, rawhits=cmd_rawhits, index=cmd_index, motif=cmd_motif,
-         hybrid=cmd_hybrid, library=cmd_library, tier3=cmd_tier3, simple=cmd_simple, edge=cmd_edge)[a.cmd](a)
+         hybrid=cmd_hybrid, homopolymer=cmd_homopolymer, library=cmd_library, tier3=cmd_tier3, simple=cmd_simple, edge=cmd_edge)[a.cmd](a)
 
 
 if __name__ == "__main__":

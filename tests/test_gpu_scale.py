@@ -276,6 +276,28 @@ def test_bind_host_moves_and_restores_affinity(gpu_ctx):
             assert os.sched_getaffinity(0) == before
 
 
+def test_cli_profile_json(gpu_ctx, golden_dir, tmp_path):
+    """`bwt.py IN.fa --profile P.json`: wall ms, calls and bytes of every stage
+    the CLI runs (load, scan, postprocess, write, index_wait) and the library's
+    own split (scan, index, merge, refine..filter, render); the output file is
+    the golden one."""
+    import json
+    from bwtmi import cli
+    with open(os.path.join(golden_dir, "expected_cli.json")) as f:
+        want = json.load(f)["synthetic_test.fa.strfinder"]["sha256"]
+    out, prof = tmp_path / "o.tab", tmp_path / "p.json"
+    fa = os.path.join(golden_dir, "inputs", "synthetic_test.fa")
+    assert cli.main([fa, "-o", str(out), "--format", "strfinder", "--profile", str(prof)]) == 0
+    import hashlib
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == want
+    d = json.loads(prof.read_text())
+    assert set(d["stages"]) >= {"load", "scan", "postprocess", "write", "index_wait"}
+    assert d["stages"]["load"]["bytes"] == os.path.getsize(fa)
+    assert d["stages"]["write"]["bytes"] == out.stat().st_size
+    assert set(d["library_stage_ms"]) >= {"scan", "index", "merge", "refine..filter", "render"}
+    assert d["records"] > 0 and d["bases"] > 0
+
+
 def test_ktrace_records_every_launch(gpu_ctx, tmp_path):
     """BWTMI_KTRACE=path: one line per kernel launch (name, ms, idle ms) and a
     marker per resolved batch, appended to the file."""

@@ -227,3 +227,37 @@ def test_library_does_not_bind_by_default(built_lib):
     BWTMI_NUMA_BIND, bench.py calls bwtmi_bind_host)."""
     from bwtmi import _lib
     assert _lib.knob("NUMA_BIND") == 0 or os.environ.get("BWTMI_NUMA_BIND") == "1"
+
+
+# ---- stage profile (CLI --profile) and roctx ranges
+def test_stage_profile_of_host_calls(tmp_path, built_lib):
+    """bwtmi.profile times the job calls the CLI makes (load, postprocess, write)
+    with their bytes; the trace entry points take nested ranges."""
+    import json
+    from bwtmi import _lib, profile, synth
+    from bwtmi.records import Job
+    fa = str(tmp_path / "p.fa")
+    synth.write_fasta(fa, [120_000, 80_000], 0.02)
+    prof = profile.start()
+    try:
+        j = Job(min_copies=3, show_progress=True, threads=4)
+        j.load_fasta(fa, 30)
+        for cid in range(j.contig_count()):
+            seq = j.contig_seq(cid)
+            _, fl, tl, tr = j.contig_info(cid)
+            j.add_hits(cid, oracle.strict_scan(seq[tl:len(seq) - tr], 1, 1000, 0, 3))
+        j.postprocess()
+        out = str(tmp_path / "o.tab")
+        j.write("strfinder", out)
+        path = str(tmp_path / "prof.json")
+        prof.write(path)
+    finally:
+        profile._active = None
+    d = json.load(open(path))
+    st = d["stages"]
+    assert set(st) >= {"load", "postprocess", "write"}
+    assert st["load"]["bytes"] == os.path.getsize(fa) and st["write"]["bytes"] == os.path.getsize(out)
+    assert all(v["ms"] > 0 and v["calls"] == 1 for v in st.values())
+    assert d["bases"] == 200_000 - 4 * 30 and d["records"] == j.count()
+    assert built_lib.bwtmi_trace_push(b"outer") == 0 and built_lib.bwtmi_trace_push(b"inner") == 0
+    assert built_lib.bwtmi_trace_pop() == 0 and built_lib.bwtmi_trace_pop() == 0

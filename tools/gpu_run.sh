@@ -9,6 +9,7 @@
 #   "bench NAME [bench.py args]"    one bench line -> NAME.json (+ NAME.err)
 #   "prof NAME [bench.py args]"     rocprofv3 --kernel-trace --stats of a bench run -> kernel_stats_NAME.csv
 #   "pmc NAME [bench.py args]"      FETCH_SIZE and WRITE_SIZE passes (one counter block per run) -> pmc_traffic_NAME.json
+#   "mtrace NAME FASTA [args]"      rocprofv3 --marker-trace --kernel-trace of the CLI (+ --profile JSON)
 #   "py NAME script [args]"         any python tool (tools/c4_shard.py, tools/lib_kernels.py, ...) -> NAME.log
 # Every step runs under its own time limit; the first failing step ends the call.
 set -o pipefail
@@ -66,6 +67,15 @@ for step in "$@"; do
       python3 tools/pmc_traffic.py "$OUT/pmc_${name}_FETCH_SIZE" "$OUT/pmc_${name}_WRITE_SIZE" "$OUT/pmc_traffic_$name.json" \
         || { echo PMC_PARSE_FAIL; exit 1; }
       rm -rf "$OUT/pmc_${name}_FETCH_SIZE" "$OUT/pmc_${name}_WRITE_SIZE" ;;
+    mtrace)   # roctx stage ranges + kernels of one CLI run: "mtrace NAME FASTA [bwt.py args]"
+      timeout -k 10 600 rocprofv3 --marker-trace --kernel-trace --output-format csv -d "$OUT/mt_$name" -o run -- \
+        python3 bwt-algorithm_amd/bwt.py "${args[@]}" -o "$OUT/mt_$name.tab" --profile "$OUT/profile_$name.json" \
+        > "$OUT/mt_$name.log" 2>&1 || { echo MTRACE_FAIL; tail -5 "$OUT/mt_$name.log"; exit 1; }
+      find "$OUT/mt_$name" -name "*marker_api_trace.csv" -exec cp {} "$OUT/marker_trace_$name.csv" \;
+      find "$OUT/mt_$name" -name "*kernel_trace.csv" -exec cp {} "$OUT/kernel_trace_$name.csv" \;
+      rm -rf "$OUT/mt_$name" "$OUT/mt_$name.tab"
+      python3 tools/stage_ranges.py "$OUT/marker_trace_$name.csv" "$OUT/kernel_trace_$name.csv" > "$OUT/stage_ranges_$name.txt" \
+        && cat "$OUT/stage_ranges_$name.txt" ;;
     py)
       timeout -k 10 600 python -u "${args[@]}" > "$OUT/$name.log" 2>&1 || { echo PY_FAIL; tail -30 "$OUT/$name.log"; exit 1; }
       tail -15 "$OUT/$name.log" ;;
