@@ -82,7 +82,7 @@ struct HBuf {  // pinned host staging
 enum Slot {
     S_TEXT = 0, S_PACK, S_CAND_K, S_CAND_V, S_CAND_K2, S_CAND_V2, S_FLAG, S_SCAN, S_HITS, S_COUNTS,
     S_SORT_TMP0, S_SORT_TMP1, S_SORT_HIST, S_SCAN_TMP, S_MISC0, S_MISC1, S_MISC2, S_MISC3,
-    S_IDX0, S_IDX1, S_IDX2, S_IDX3, S_IDX4, S_IDX5, S_IDX6, S_IDX7, S_IDX8, S_IDX9, S_IDX10, S_IDX11,
+    S_IDX0, S_IDX1, S_IDX2, S_IDX3, S_IDX4, S_IDX5, S_IDX6, S_IDX7, S_IDX8, S_IDX9, S_IDX10, S_IDX11, S_IDX12,
     S_FASTA,   // a whole-file load's FASTA image (fasta_dev.hip)
     S_SORT_DIG,   // the next pass's digit of every key, written by a radix pass (radix.hip)
     S_LB,         // look-back granules of the single-pass scans and radix histograms (radix.hip)

@@ -186,16 +186,20 @@ __global__ void k_buckets(const int64_t *__restrict__ S, int64_t n, int64_t nb, 
 }
 
 // the nested test of hit (s0, e0, m) against a kept span (Sk, Ek) of longer
-// motif Mk > m (bwt.py:3460-3490), predicate division for division
+// motif Mk > m (bwt.py:3460-3490, overlap_threshold 0.5 as both CLI call
+// sites pass it, bwt.py:3829 / 3928), in integers: for the thresholds t =
+// p / q in {0.1, 0.3, 0.5, 0.8} the reference's float test ov / rl >= t holds
+// exactly when q ov >= p rl (a ratio below p / q differs from it by at least
+// 1 / (q rl), far above the rounding of either double), and Mk / m >= 10 / 5
+// exactly when Mk >= 10 m / 5 m.  No division in the walks.
 __device__ __forceinline__ bool nested_by(int64_t s0, int64_t e0, int64_t m, int64_t rl, int64_t Sk, int64_t Ek,
-                                          int64_t Mk, double thr) {
+                                          int64_t Mk) {
     const int64_t ov = min(e0, Ek) - max(s0, Sk);
     if (ov <= 0) return false;
-    const double ratio = (double)Mk / (double)m;
-    const double frac = (double)ov / (double)rl;
-    if (m == 1 && Mk > 1 && frac >= 0.8) return true;
-    const double th = ratio >= 10 ? 0.1 : (ratio >= 5 ? 0.3 : thr);
-    return frac >= th;
+    if (m == 1 && Mk > 1 && 5 * ov >= 4 * rl) return true;   // frac >= 0.8
+    if (Mk >= 10 * m) return 10 * ov >= rl;                    // >= 0.1
+    if (Mk >= 5 * m) return 10 * ov >= 3 * rl;                 // >= 0.3
+    return 2 * ov >= rl;                                       // >= 0.5
 }
 
 // All levels in one launch, segment by segment.  Hits overlap only inside a
@@ -220,23 +224,23 @@ __device__ __forceinline__ bool seg_head(const int64_t *__restrict__ S, const in
 // LARGE = false: window blockIdx.x, overflowing windows are appended to ovf_win;
 // LARGE = true: the windows listed in ovf_win (*ovf_n of them), a grid-stride
 // loop; a window past kSegCapL sets *fallback
-template <int T, int CAP, bool LARGE>
+template <int T, int CAP, int WIN, bool LARGE>
 __global__ __launch_bounds__(T) void k_seg_levels(const int64_t *__restrict__ S, const int64_t *__restrict__ E,
                                                   const int32_t *__restrict__ M, const int64_t *__restrict__ PME,
                                                   int64_t n, uint8_t *__restrict__ kept, uint32_t *__restrict__ ovf_win,
-                                                  unsigned int *__restrict__ ovf_n, unsigned int *__restrict__ fallback,
-                                                  double thr) {
+                                                  unsigned int *__restrict__ ovf_n, unsigned int *__restrict__ fallback) {
     __shared__ int64_t sS[CAP], sE[CAP], sP[CAP];
     __shared__ int32_t sM[CAP];
     __shared__ uint8_t sK[CAP];
+    __shared__ int16_t sF[CAP];
     __shared__ unsigned long long found;
     __shared__ int pend[3];
     const int tid = threadIdx.x;
     const int64_t nwin = LARGE ? (int64_t)*ovf_n : (int64_t)gridDim.x;
     for (int64_t q = blockIdx.x; q < nwin; q += LARGE ? (int64_t)gridDim.x : nwin) {
         const int64_t w = LARGE ? (int64_t)ovf_win[q] : q;
-        const int64_t w0 = w * kSegWin;
-        const int64_t w1 = w0 + kSegWin < n ? w0 + kSegWin : n;
+        const int64_t w0 = w * WIN;
+        const int64_t w1 = w0 + WIN < n ? w0 + WIN : n;
         // a = the window's first segment head (none: a segment from an earlier window covers it)
         if (tid == 0) found = ~0ull;
         __syncthreads();
@@ -274,10 +278,14 @@ __global__ __launch_bounds__(T) void k_seg_levels(const int64_t *__restrict__ S,
         // whatever the levels decide: only the others (kUndecided) take part in
         // the level loop, whose levels are then the distinct motif lengths among them
         constexpr uint8_t kUndecided = 2;
-        auto nested_among = [&](int i, bool kept_only) {   // span i nested by a longer motif's span
+        // the first pass walks each hit's window back from its end to the first
+        // span of a longer motif that would nest it (kept or not) and remembers
+        // where: a hit with none is kept whatever the others decide, the rest
+        // (kUndecided) resume their walk there -- no nester lies above it
+        auto first_nester = [&](int i) -> int {   // local rank of the first possible nester, -1 none
             const int64_t s0 = sS[i], e0 = sE[i], rl = e0 - s0;
             const int64_t m = sM[i];
-            if (rl <= 0) return false;
+            if (rl <= 0) return -1;
             int lo = i + 1, hi = len;   // first local rank with S >= e0 (S[i] = s0 < e0)
             while (lo < hi) {
                 const int mid = (lo + hi) >> 1;
@@ -286,13 +294,15 @@ __global__ __launch_bounds__(T) void k_seg_levels(const int64_t *__restrict__ S,
             }
             for (int k = lo - 1; k >= 0 && sP[k] > s0; --k) {
                 const int64_t Mk = sM[k];
-                // this level's entries are being written now: never read (Mk <= m)
-                if (Mk <= m || (kept_only && sK[k] != 1)) continue;
-                if (nested_by(s0, e0, m, rl, sS[k], sE[k], Mk, thr)) return true;
+                if (Mk > m && nested_by(s0, e0, m, rl, sS[k], sE[k], Mk)) return k;
             }
-            return false;
+            return -1;
         };
-        for (int i = tid; i < len; i += T) sK[i] = nested_among(i, false) ? kUndecided : 1;
+        for (int i = tid; i < len; i += T) {
+            const int k = first_nester(i);
+            sK[i] = k >= 0 ? kUndecided : 1;
+            sF[i] = (int16_t)k;
+        }
         // Rounds instead of levels: an undecided hit is decided as soon as the
         // longer-motif spans that would nest it are decided -- suppressed by the
         // first KEPT one (final, whatever else is pending), kept when none is
@@ -304,19 +314,13 @@ __global__ __launch_bounds__(T) void k_seg_levels(const int64_t *__restrict__ S,
         auto decide = [&](int i) -> uint8_t {   // 0 nested, 1 kept, kUndecided: wait
             const int64_t s0 = sS[i], e0 = sE[i], rl = e0 - s0;
             const int64_t m = sM[i];
-            int lo = i + 1, hi = len;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (sS[mid] < e0) lo = mid + 1;
-                else hi = mid;
-            }
             bool wait = false;
-            for (int k = lo - 1; k >= 0 && sP[k] > s0; --k) {
+            for (int k = sF[i]; k >= 0 && sP[k] > s0; --k) {
                 const int64_t Mk = sM[k];
                 if (Mk <= m) continue;
                 const uint8_t dk = vK[k];
                 if (dk == 0) continue;
-                if (nested_by(s0, e0, m, rl, sS[k], sE[k], Mk, thr)) {
+                if (nested_by(s0, e0, m, rl, sS[k], sE[k], Mk)) {
                     if (dk == 1) return 0;
                     wait = true;
                 }
@@ -348,8 +352,7 @@ __global__ __launch_bounds__(kB) void k_level(const uint32_t *__restrict__ lvl, 
                                               const bwtmi_hit *__restrict__ H, const uint32_t *__restrict__ rank_of,
                                               const int64_t *__restrict__ S, const int64_t *__restrict__ E,
                                               const int32_t *__restrict__ M, const int64_t *__restrict__ PME,
-                                              const uint32_t *__restrict__ B, uint8_t *__restrict__ kept, int64_t n,
-                                              double thr) {
+                                              const uint32_t *__restrict__ B, uint8_t *__restrict__ kept, int64_t n) {
     const int64_t t = (int64_t)blockIdx.x * kB + threadIdx.x;
     if (t >= cnt) return;
     const uint32_t idx = lvl[t];
@@ -368,7 +371,7 @@ __global__ __launch_bounds__(kB) void k_level(const uint32_t *__restrict__ lvl, 
         for (int64_t k = lo - 1; k >= 0 && PME[k] > s0; --k) {
             const int64_t Mk = M[k];
             if (Mk <= m || !kept[k]) continue;   // same-level entries are being written now: never read
-            if (nested_by(s0, e0, m, rl, S[k], E[k], Mk, thr)) { nested = true; break; }
+            if (nested_by(s0, e0, m, rl, S[k], E[k], Mk)) { nested = true; break; }
         }
     }
     kept[rank_of[idx]] = nested ? 0 : 1;
@@ -384,7 +387,7 @@ __global__ __launch_bounds__(kB) void k_level_wave(const uint32_t *__restrict__ 
                                                    const int64_t *__restrict__ S, const int64_t *__restrict__ E,
                                                    const int32_t *__restrict__ M, const int64_t *__restrict__ PME,
                                                    const uint32_t *__restrict__ B, uint8_t *__restrict__ kept,
-                                                   int64_t n, double thr) {
+                                                   int64_t n) {
     const int lane = threadIdx.x & 63;
     const int64_t t = ((int64_t)blockIdx.x * kB + threadIdx.x) >> 6;
     if (t >= cnt) return;   // wave-uniform
@@ -406,15 +409,8 @@ __global__ __launch_bounds__(kB) void k_level_wave(const uint32_t *__restrict__ 
             bool hit = false;
             if (live) {
                 const int64_t Mk = M[k];
-                if (Mk > m && kept[k]) {   // same-level entries are being written now: never read
-                    const int64_t ov = min(e0, E[k]) - max(s0, S[k]);
-                    if (ov > 0) {
-                        const double ratio = (double)Mk / (double)m;
-                        const double frac = (double)ov / (double)rl;
-                        const double th = ratio >= 10 ? 0.1 : (ratio >= 5 ? 0.3 : thr);
-                        hit = (m == 1 && Mk > 1 && frac >= 0.8) || frac >= th;
-                    }
-                }
+                if (Mk > m && kept[k])   // same-level entries are being written now: never read
+                    hit = nested_by(s0, e0, m, rl, S[k], E[k], Mk);
             }
             if (__any(hit)) {
                 nested = true;
@@ -480,10 +476,10 @@ static void screen_levels(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int32_t lm
         const int64_t a = lv[q].first, b = q + 1 < lv.size() ? lv[q + 1].first : n;
         if (b - a <= kWaveLevelMax)   // few hits (long motifs, long walks): a wave per hit
             KLAUNCH("k_level_wave", 0.0, k_level_wave, dim3(blocks((b - a) * 64)), dim3(kB), 0, st, vgrp + a, b - a, d_hits,
-                    rank_of, S, E, M, PME, B, kept, n, 0.5);
+                    rank_of, S, E, M, PME, B, kept, n);
         else
             KLAUNCH("k_level", 0.0, k_level, dim3(blocks(b - a)), dim3(kB), 0, st, vgrp + a, b - a, d_hits, rank_of, S, E,
-                    M, PME, B, kept, n, 0.5);
+                    M, PME, B, kept, n);
     }
 }
 
@@ -549,13 +545,31 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     unsigned int *d_ovf = reinterpret_cast<unsigned int *>(d_max);   // [0] fallback flag, [1] overflow windows
     unsigned int ovf = 1;
     if (seg_levels) {
-        const int64_t nwin = (n + kSegWin - 1) / kSegWin;
         uint32_t *ovf_win = pos;   // the final-pass scan buffer is free until then (n + 1 words >= nwin)
         HIPCHECK(hipMemsetAsync(d_ovf, 0, 8, st));
-        KLAUNCH("k_seg_levels", 0.0, (k_seg_levels<256, kSegCapS, false>), dim3((unsigned)nwin), dim3(256), 0, st, S, E,
-                M, PME, n, kept, ovf_win, d_ovf + 1, d_ovf, 0.5);
-        KLAUNCH("k_seg_levels_l", 0.0, (k_seg_levels<1024, kSegCapL, true>), dim3(256), dim3(1024), 0, st, S, E, M, PME,
-                n, kept, ovf_win, d_ovf + 1, d_ovf, 0.5);
+        const int64_t var = knob(KN_SEG_VARIANT);
+        auto run = [&](auto small, auto large, int win, int ts, int tl) {
+            const int64_t nwin = (n + win - 1) / win;
+            KLAUNCH("k_seg_levels", 0.0, small, dim3((unsigned)nwin), dim3(ts), 0, st, S, E, M, PME, n, kept, ovf_win,
+                    d_ovf + 1, d_ovf);
+            KLAUNCH("k_seg_levels_l", 0.0, large, dim3(256), dim3(tl), 0, st, S, E, M, PME, n, kept, ovf_win, d_ovf + 1,
+                    d_ovf);
+        };
+        if (var == 1)
+            run(k_seg_levels<256, 1024, 512, false>, k_seg_levels<1024, kSegCapL, 512, true>, 512, 256, 1024);
+        else if (var == 2)
+            run(k_seg_levels<512, 2048, 1024, false>, k_seg_levels<1024, kSegCapL, 1024, true>, 1024, 512, 1024);
+        else if (var == 3)
+            run(k_seg_levels<128, 256, 128, false>, k_seg_levels<1024, kSegCapL, 128, true>, 128, 128, 1024);
+        else
+            run(k_seg_levels<256, kSegCapS, kSegWin, false>, k_seg_levels<1024, kSegCapL, kSegWin, true>, kSegWin, 256,
+                1024);
+        if (stats_on()) {
+            unsigned int o2[2] = {0, 0};
+            HIPCHECK(hipMemcpyAsync(o2, d_ovf, 8, hipMemcpyDeviceToHost, st));
+            scan_wait(st);
+            std::fprintf(stderr, "  screen: %lld hits, %u overflow windows, fallback %u\n", (long long)n, o2[1], o2[0]);
+        }
         HIPCHECK(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, st));
         scan_wait(st);
     }

@@ -635,11 +635,99 @@ __global__ __launch_bounds__(kB) void k_dna_classify(const uint32_t *__restrict_
         }
 }
 
+// Long runs of one symbol ("deep" suffixes: the first 16 symbols all equal c).
+// A run of R copies of c puts R - 15 suffixes into one 16-symbol group that
+// plain doubling resolves only h symbols per round (16 rounds for the 958 kbp
+// N runs of an assembly).  Their order is known in closed form instead: a
+// deep suffix is c^r X with X[0] != c (r = symbols to the run's end); every
+// one whose X[0] < c sorts before every one whose X[0] > c (b = 0 / 1), then
+// b = 0 by r ascending, b = 1 by r descending, then by X.  So the first round
+// (h = 16) sorts deep groups by (b, +-r) and every later round by rank[a + r]
+// -- the current rank of X, a coarsening of its final rank -- instead of
+// rank[a + h]; deep groups hold only deep suffixes (their 16-prefix is c^16),
+// so every group is keyed one way.  re[a >> 4] = the end of the run holding
+// position 16 (a >> 4) + 15, which lies inside a's run whenever a is deep.
+struct Deep {
+    const uint64_t *P;    // packed text (2-bit bases, or 4-bit symbol codes when small)
+    const uint32_t *re;   // run end per 16-position block (valid for deep suffixes' blocks)
+    int small;            // symbol codes of the small-alphabet path
+    int on;               // any run of >= 16 equal symbols
+};
+
+// the 16 symbols from a (the packed words are padded): c when all equal, else -1
+__device__ __forceinline__ int homopolymer16(const Deep &d, int64_t a) {
+    if (d.small) {
+        const int64_t w = a >> 4;
+        const int sh = (int)(a & 15) * 4;
+        const uint64_t x = sh ? (d.P[w] << sh) | (d.P[w + 1] >> (64 - sh)) : d.P[w];
+        const uint64_t c = x >> 60;
+        return x == c * 0x1111111111111111ull ? (int)c : -1;
+    }
+    const uint64_t w = window(d.P, a) >> 32;   // 16 bases, 2 bits each
+    const uint64_t c = w >> 30;
+    return w == c * 0x55555555ull ? (int)c : -1;
+}
+__device__ __forceinline__ int sym_at(const Deep &d, int64_t i) {
+    return d.small ? (int)((d.P[i >> 4] >> (60 - 4 * (i & 15))) & 15u) : (int)base_code(d.P, i);
+}
+
 // the doubling key of member v: rank of the suffix h bases on (a group member
-// always has more than h bases before '$': its h-prefix is shared)
-__device__ __forceinline__ uint32_t ls_key(const uint32_t *__restrict__ rank, uint32_t v, int64_t n, int64_t h) {
+// always has more than h bases before '$': its h-prefix is shared); deep
+// suffixes: (b, +-r) in the first round, then the rank of their run's end
+__device__ __forceinline__ uint32_t ls_key(const uint32_t *__restrict__ rank, uint32_t v, int64_t n, int64_t h,
+                                          const Deep &d) {
     const int64_t a = v & kPosMask;
+    if (d.on && a + 16 < n) {
+        const int c = homopolymer16(d, a);
+        if (c >= 0) {
+            const int64_t e = d.re[a >> 4];   // first position past the run (<= n - 1: '$' ends every run)
+            const int64_t r = e - a;
+            if (h == 16) {
+                const bool b = e < n - 1 && sym_at(d, e) > c;
+                return b ? (1u << 29) | (uint32_t)(kPosMask - r) : (uint32_t)r;
+            }
+            return rank[e];
+        }
+    }
     return a + h < n ? rank[a + h] : 0u;
+}
+
+// runs of >= 16 equal symbols in t[0, n - 1): flags at their first position
+// and at the position past their last one
+__global__ __launch_bounds__(kB) void k_run_marks(Deep d, int64_t n, uint32_t *__restrict__ fst, uint32_t *__restrict__ fen) {
+    const int64_t p = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (p >= n) return;
+    bool st = false, en = false;
+    if (p + 16 < n) {   // 16 real symbols from p
+        const int c = homopolymer16(d, p);
+        st = c >= 0 && (p == 0 || sym_at(d, p - 1) != c);
+    }
+    if (p >= 16 && p <= n - 1) {   // p is past a run whose last 16 symbols are p-16 .. p-1
+        const int c = homopolymer16(d, p - 16);
+        en = c >= 0 && (p == n - 1 || sym_at(d, p) != c);
+    }
+    fst[p] = st;
+    fen[p] = en;
+}
+
+// run k = [starts[k], ends[k]): re[b] = ends[k] for every block b whose last
+// position 16 b + 15 lies in the run
+__global__ __launch_bounds__(kB) void k_run_fill(const uint32_t *__restrict__ fst, const uint32_t *__restrict__ pst,
+                                                 const uint32_t *__restrict__ fen, const uint32_t *__restrict__ pen,
+                                                 int64_t n, uint32_t *__restrict__ rs, uint32_t *__restrict__ rend) {
+    const int64_t p = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (p >= n) return;
+    if (fst[p]) rs[pst[p]] = (uint32_t)p;
+    if (fen[p]) rend[pen[p]] = (uint32_t)p;
+}
+__global__ __launch_bounds__(kB) void k_run_blocks(const uint32_t *__restrict__ rs, const uint32_t *__restrict__ rend,
+                                                   const uint32_t *__restrict__ kcount, uint32_t *__restrict__ re) {
+    const uint32_t K = *kcount;
+    for (uint32_t k = blockIdx.x; k < K; k += gridDim.x) {
+        const int64_t s0 = rs[k], e0 = rend[k];
+        const int64_t b0 = s0 >= 15 ? (s0 - 15 + 15) / 16 : 0, b1 = (e0 - 1 - 15) / 16;   // 16 b + 15 in [s0, e0)
+        for (int64_t b = b0 + threadIdx.x; b <= b1; b += kB) re[b] = (uint32_t)e0;
+    }
 }
 
 // one doubling pass over groups of <= W members, 64/W groups per wave: bitonic
@@ -650,7 +738,8 @@ constexpr int kLB = 1024;   // threads per workgroup of the wave-sort passes
 template <int W>
 __global__ __launch_bounds__(kLB) void k_ls_wave(const uint32_t *__restrict__ starts, const uint32_t *__restrict__ sizes,
                                                 int64_t cnt, uint32_t *__restrict__ vals,
-                                                const uint32_t *__restrict__ rank, int64_t n, int64_t h, LsOut o) {
+                                                const uint32_t *__restrict__ rank, int64_t n, int64_t h, LsOut o,
+                                                Deep dp) {
     const int lane = threadIdx.x & 63, kk = lane & (W - 1);
     const int64_t g = (((int64_t)blockIdx.x * kLB + threadIdx.x) >> 6) * (64 / W) + lane / W;
     uint32_t s = 0, sz = 0;
@@ -660,7 +749,7 @@ __global__ __launch_bounds__(kLB) void k_ls_wave(const uint32_t *__restrict__ st
     }
     const bool live = kk < (int)sz;
     const uint32_t orig = live ? vals[s + kk] : 0u;
-    uint64_t x = live ? ((uint64_t)ls_key(rank, orig, n, h) << 32) | orig : ~0ull;
+    uint64_t x = live ? ((uint64_t)ls_key(rank, orig, n, h, dp) << 32) | orig : ~0ull;
 #pragma unroll
     for (int k2 = 2; k2 <= W; k2 <<= 1)
 #pragma unroll
@@ -692,7 +781,7 @@ __global__ __launch_bounds__(kLB) void k_ls_wave(const uint32_t *__restrict__ st
 constexpr int kWB = 1024;
 __global__ __launch_bounds__(kWB) void k_ls_block(const uint32_t *__restrict__ starts, const uint32_t *__restrict__ sizes,
                                                   uint32_t *__restrict__ vals, const uint32_t *__restrict__ rank,
-                                                  int64_t n, int64_t h, LsOut o) {
+                                                  int64_t n, int64_t h, LsOut o, Deep dp) {
     __shared__ uint64_t x[kMedium];
     __shared__ int wl[kWB / 64], wf[kWB / 64];
     const uint32_t s = starts[blockIdx.x], sz = sizes[blockIdx.x];
@@ -700,7 +789,7 @@ __global__ __launch_bounds__(kWB) void k_ls_block(const uint32_t *__restrict__ s
     uint32_t p2 = 1;
     while (p2 < sz) p2 <<= 1;
     const uint32_t orig = t < (int)sz ? vals[s + t] : 0u;
-    if (t < (int)p2) x[t] = t < (int)sz ? ((uint64_t)ls_key(rank, orig, n, h) << 32) | orig : ~0ull;
+    if (t < (int)p2) x[t] = t < (int)sz ? ((uint64_t)ls_key(rank, orig, n, h, dp) << 32) | orig : ~0ull;
     __syncthreads();
     for (uint32_t k2 = 2; k2 <= p2; k2 <<= 1)
         for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
@@ -748,10 +837,11 @@ __global__ __launch_bounds__(kWB) void k_ls_block(const uint32_t *__restrict__ s
 // one wave-class pass over the cnt groups of a class list
 template <int W>
 void ls_wave_pass(Ctx &c, const char *name, const uint32_t *cs, const uint32_t *cz, uint32_t cnt, uint32_t *vals,
-                  const uint32_t *rank, int64_t n, int64_t h, const LsOut &o) {
+                  const uint32_t *rank, int64_t n, int64_t h, const LsOut &o, const Deep &dp) {
     if (!cnt) return;
     const unsigned grid = (unsigned)((cnt + (kLB / 64) * (64 / W) - 1) / ((kLB / 64) * (64 / W)));
-    KLAUNCH(name, 0.0, (k_ls_wave<W>), dim3(grid), dim3(kLB), 0, c.stream, cs, cz, (int64_t)cnt, vals, rank, n, h, o);
+    KLAUNCH(name, 0.0, (k_ls_wave<W>), dim3(grid), dim3(kLB), 0, c.stream, cs, cz, (int64_t)cnt, vals, rank, n, h, o,
+            dp);
 }
 
 // groups larger than kMedium: (group index << 30 | rank[a+h]) keys gathered
@@ -759,12 +849,12 @@ void ls_wave_pass(Ctx &c, const char *name, const uint32_t *cs, const uint32_t *
 __global__ __launch_bounds__(kB) void k_dna_refine_keys(const uint32_t *__restrict__ starts, const uint32_t *__restrict__ sizes,
                                                         const uint32_t *__restrict__ offs, const uint32_t *__restrict__ vals,
                                                         const uint32_t *__restrict__ rank, int64_t n, int64_t h,
-                                                        uint64_t *__restrict__ rk, uint32_t *__restrict__ rv) {
+                                                        uint64_t *__restrict__ rk, uint32_t *__restrict__ rv, Deep dp) {
     const uint32_t q = blockIdx.y;
     const uint32_t s = starts[q], sz = sizes[q], at = offs[q];
     for (uint32_t k = blockIdx.x * kB + threadIdx.x; k < sz; k += gridDim.x * kB) {
         const uint32_t v = vals[s + k];
-        rk[at + k] = ((uint64_t)q << 30) | ls_key(rank, v, n, h);
+        rk[at + k] = ((uint64_t)q << 30) | ls_key(rank, v, n, h, dp);
         rv[at + k] = v;
     }
 }
@@ -977,6 +1067,29 @@ bool sa_sort(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, in
     }
     if (G) KLAUNCH("dna_short_fix", 0.0, k_dna_short_fix, dim3(1), dim3(1024), 0, st, vals, rank, gs, ge, G, n);
 
+    // runs of >= 16 equal symbols: their blocks' run ends (Deep); the flag
+    // buffers are free until the large-group rounds
+    Deep dp{P, nullptr, small ? 1 : 0, 0};
+    if (G > 0) {
+        c.slot[S_IDX12].ensure((size_t)(n / 16 + 2) * 4 + 64);
+        uint32_t *re = c.slot[S_IDX12].as<uint32_t>();
+        KLAUNCH("dna_run_marks", 0.0, k_run_marks, dim3(nblocks(n)), dim3(kB), 0, st, dp, n, fs, fe);
+        HIPCHECK(hipMemsetAsync(fs + n, 0, 4, st));
+        exclusive_scan<uint32_t>(c, fs, ps, n + 1);
+        uint32_t K = 0;
+        HIPCHECK(hipMemcpyAsync(&K, ps + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        if (K) {
+            exclusive_scan<uint32_t>(c, fe, pe, n);
+            uint32_t *rs = keys, *rend = keys + K + 16;   // the keys are dead until the class lists
+            KLAUNCH("dna_run_fill", 0.0, k_run_fill, dim3(nblocks(n)), dim3(kB), 0, st, fs, ps, fe, pe, n, rs, rend);
+            KLAUNCH("dna_run_blocks", 0.0, k_run_blocks, dim3((unsigned)std::min<int64_t>(K, 4096)), dim3(kB), 0, st, rs,
+                    rend, ps + n, re);
+            dp.re = re;
+            dp.on = 1;
+        }
+    }
+
     std::vector<uint32_t> lstart, lsize, loff;
     ShardedList sl{};   // the first list is plain
     for (int64_t h = 16; G > 0; h *= 2) {
@@ -1026,17 +1139,17 @@ bool sa_sort(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, in
             HIPCHECK(hipMemcpyAsync(tab + 2 * L, loff.data(), (size_t)L * 4, hipMemcpyHostToDevice, st));
             grid2 = dim3((unsigned)std::min<int64_t>(64, (mx + kB - 1) / kB), (unsigned)L);
             KLAUNCH("dna_refine_keys", 0.0, k_dna_refine_keys, grid2, dim3(kB), 0, st, tab, tab + L, tab + 2 * L, vals,
-                    rank, n, h, rk, rv);
+                    rank, n, h, rk, rv, dp);
         }
         // the sorts read rank[a + h] as the round found it (the large groups'
         // keys are gathered above); their rank changes are stored after them
-        ls_wave_pass<4>(c, "dna_ls_w4", cs, cz, cnt[0], vals, rank, n, h, o);
-        ls_wave_pass<16>(c, "dna_ls_w16", cs + G, cz + G, cnt[1], vals, rank, n, h, o);
-        ls_wave_pass<32>(c, "dna_ls_w32", cs + 2 * G, cz + 2 * G, cnt[2], vals, rank, n, h, o);
-        ls_wave_pass<64>(c, "dna_ls_w64", cs + 3 * G, cz + 3 * G, cnt[3], vals, rank, n, h, o);
+        ls_wave_pass<4>(c, "dna_ls_w4", cs, cz, cnt[0], vals, rank, n, h, o, dp);
+        ls_wave_pass<16>(c, "dna_ls_w16", cs + G, cz + G, cnt[1], vals, rank, n, h, o, dp);
+        ls_wave_pass<32>(c, "dna_ls_w32", cs + 2 * G, cz + 2 * G, cnt[2], vals, rank, n, h, o, dp);
+        ls_wave_pass<64>(c, "dna_ls_w64", cs + 3 * G, cz + 3 * G, cnt[3], vals, rank, n, h, o, dp);
         if (cnt[4])
             KLAUNCH("dna_ls_block", 0.0, k_ls_block, dim3(cnt[4]), dim3(kWB), 0, st, cs + 4 * G, cz + 4 * G, vals,
-                    rank, n, h, o);
+                    rank, n, h, o, dp);
         uint32_t sc[25];   // group shards, overflow | 7 unused | change shards, overflow
         HIPCHECK(hipMemcpyAsync(sc, ncnt, sizeof sc, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));

@@ -512,6 +512,34 @@ def test_small_alphabet_suffix_sort_vs_oracle(gpu_ctx, case):
     _check_index(t + b"$")
 
 
+@pytest.mark.parametrize("alpha", [b"ACGT", b"ACGTNRY"])
+def test_long_runs_ordered_in_closed_form_vs_oracle(gpu_ctx, alpha):
+    """Suffixes inside runs of >= 16 equal symbols (sa_dna.hip Deep: first round
+    by (next symbol above / below the run's, +-remaining run), later rounds by
+    the rank of the run's end): runs of every symbol and of lengths 15-17, 31-33
+    and up to 40 kbp, followed by smaller and larger symbols, back to back,
+    at the start, running into '$', and many runs of equal length (ties broken
+    by what follows them) -- against the oracle."""
+    r = np.random.default_rng(len(alpha))
+
+    def rnd(k):
+        a = np.frombuffer(alpha, dtype=np.uint8)
+        return a[r.integers(0, len(a), k)].tobytes()
+    parts = [alpha[:1] * 40]   # a run at the start
+    for i in range(600):
+        c = alpha[int(r.integers(0, len(alpha)))]
+        ln = int(r.choice([15, 16, 17, 31, 32, 33, 48, 64, 100, 257, 1000]))
+        parts.append(bytes([c]) * ln + rnd(int(r.integers(0, 6))))
+    parts.append(b"".join(bytes([alpha[k % len(alpha)]]) * 20 for k in range(50)))   # runs back to back
+    parts.append(rnd(50) + bytes([alpha[-1]]) * 40_000 + rnd(30))
+    for k in range(40):   # equal runs, ties broken by the following text
+        parts.append(bytes([alpha[0]]) * 37 + rnd(25))
+    t = b"".join(parts) + bytes([alpha[1]]) * 50    # a run into '$'
+    _check_index(t + b"$")
+    _check_index(bytes([alpha[0]]) * 5000 + b"$")
+    _check_index(bytes([alpha[2]]) * 17 + bytes([alpha[0]]) * 33 + b"$")
+
+
 def test_small_alphabet_texts_through_general_doubling(gpu_ctx):
     """BWTMI_SA_SMALL=0: gap texts take the general prefix doubling (index.hip)
     instead of the 3-bit string sort; the same arrays as the oracle."""

@@ -63,7 +63,8 @@ def main():
     devload = os.environ.get("C4_SHARD_DEVLOAD", "1") == "1"   # device placement of the load (bench default)
     res["device_load"] = devload
     for W, T in [(w, t) for w in worlds for t in tlist]:
-        for r in range(W):          # every rank of the world: the worst one sets the projection
+        ranks = [int(x) for x in os.environ["C4_SHARD_RANKS"].split(",")] if os.environ.get("C4_SHARD_RANKS") else range(W)
+        for r in ranks:             # every rank of the world: the worst one sets the projection
             job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True, build_index=True,
                       sa_sample=32, threads=T)
 

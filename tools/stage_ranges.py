@@ -12,7 +12,7 @@ def main():
     ranges = []
     with open(sys.argv[1]) as f:
         for r in csv.DictReader(f):
-            msg = r.get("Message") or r.get("Marker_Message") or ""
+            msg = r.get("Function") or r.get("Message") or r.get("Marker_Message") or ""
             if not msg.startswith("bwtmi"):
                 continue
             ranges.append((msg, int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Thread_Id", "")))
