@@ -52,7 +52,9 @@ KERNEL_OF = {"radix_scatter_kv6": "k_scatter<u16,u32>", "radix_scatter_kv8": "k_
              "radix_scatter_kv12": "k_scatter<u64,u32>",
              "radix_scatter_kv16": "k_scatter<u64,u64>", "bwt_gather": "k_bwt", "occ_blocks": "k_occ_blocks",
              "sa_init_keys": "k_init_keys", "kmer_dna": "k_kmer_dna", "fm2_local": "k_fm2_local",
-             "fm2_counts": "k_fm2_counts", "dna_ls_keys": "k_ls_wave"}
+             "fm2_counts": "k_fm2_counts", "dna_ls_keys": "k_ls_wave",
+             "radix_hist_k1": "k_hist_lb<u8>", "radix_hist_k2": "k_hist_lb<u16>", "radix_hist_k4": "k_hist_lb<u32>",
+             "radix_hist_k8": "k_hist_lb<u64>", "k_scan": "k_scan_lb"}
 
 
 def rocprof_name(timer: str) -> str:

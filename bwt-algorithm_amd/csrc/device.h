@@ -264,6 +264,8 @@ inline void ctx_wait(Ctx &c) {
 // ----- primitives (radix.hip)
 template <class T>
 void exclusive_scan(Ctx &c, const T *in, T *out, int64_t n);   // out may alias in
+// `rows` independent scans of n uint32 each, row r at in / out + r * stride, in one launch
+void exclusive_scan_rows(Ctx &c, const uint32_t *in, uint32_t *out, int64_t n, int rows, int64_t stride);
 void radix_sort_pairs(Ctx &c, uint64_t *keys, uint64_t *vals, int64_t n, int bit0, int bit1);
 void radix_sort_pairs32(Ctx &c, uint64_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1);
 void radix_sort_pairs_k32(Ctx &c, uint32_t *keys, uint32_t *vals, int64_t n, int bit0, int bit1);

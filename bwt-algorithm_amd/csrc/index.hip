@@ -431,6 +431,8 @@ __global__ __launch_bounds__(256) void k_fm2_local(const uint8_t *__restrict__ b
     fm2[4 * b + 2] = lo;
     fm2[4 * b + 3] = hi;
     for (int q = 0; q < 4; ++q) cnt4[(int64_t)q * (nb + 1) + b] = c[q];
+    if (b == nb - 1)
+        for (int q = 0; q < 4; ++q) cnt4[(int64_t)q * (nb + 1) + nb] = 0;   // the rows' last word (scanned to the total)
 }
 
 __global__ __launch_bounds__(256) void k_fm2_counts(const uint32_t *__restrict__ cnt4, int64_t nb,
@@ -722,10 +724,8 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
                     sigma, occ);
         }
     }
-    for (int cc = 0; cc < sigma; ++cc) {
-        uint32_t *row = ix->occ.as<uint32_t>() + (int64_t)cc * (nblk + 1);
-        exclusive_scan<uint32_t>(c, row, row, nblk + 1);
-    }
+    // the sigma rows of nblk + 1 counts, one launch
+    exclusive_scan_rows(c, ix->occ.as<uint32_t>(), ix->occ.as<uint32_t>(), nblk + 1, sigma, nblk + 1);
     if (!dna && !small)   // the string sort wrote the samples in its final pass
         KLAUNCH("k_sample", 0.0, k_sample, dim3(blocks(ix->sampled_len)), dim3(256), 0, st, SA, n, sa_sample,
                 ix->sampled.as<int32_t>(), ix->sampled_len);
@@ -740,10 +740,8 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
         HIPCHECK(hipMemsetAsync(d_dollar, 0, 8, st));
         KLAUNCH("fm2_local", (double)n + 16.0 * (double)nb + 16.0 * (double)nb, k_fm2_local, dim3(blocks(nb)),
                 dim3(256), 0, st, ix->bwt.as<uint8_t>(), n, nb, ix->fm2.as<uint64_t>(), cnt4, d_dollar);
-        for (int q = 0; q < 4; ++q) {
-            HIPCHECK(hipMemsetAsync(cnt4 + (int64_t)q * (nb + 1) + nb, 0, 4, st));
-            exclusive_scan<uint32_t>(c, cnt4 + (int64_t)q * (nb + 1), cnt4 + (int64_t)q * (nb + 1), nb + 1);
-        }
+        // k_fm2_local zeroed each row's last word: 4 rows of nb + 1, one launch
+        exclusive_scan_rows(c, cnt4, cnt4, nb + 1, 4, nb + 1);
         KLAUNCH("fm2_counts", 32.0 * (double)nb, k_fm2_counts, dim3(blocks(nb)), dim3(256), 0, st, cnt4, nb,
                 ix->fm2.as<uint32_t>());
         unsigned long long dr = 0;

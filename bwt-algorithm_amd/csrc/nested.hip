@@ -213,8 +213,8 @@ __device__ __forceinline__ bool nested_by(int64_t s0, int64_t e0, int64_t m, int
 // kSegCapS hits (many per CU), and for the windows whose segments overflow
 // them (long arrays: chains of overlapping spans) 1024-thread workgroups
 // holding kSegCapL; past that the caller falls back to the per-level launches.
-constexpr int kSegWin = 256;           // nominal positions per window
-constexpr int kSegCapS = 512;          // hits a small workgroup holds
+constexpr int kSegWin = 512;           // nominal positions per window
+constexpr int kSegCapS = 1024;         // hits a small workgroup holds
 constexpr int kSegCapL = 4096;         // hits a large workgroup holds
 
 __device__ __forceinline__ bool seg_head(const int64_t *__restrict__ S, const int64_t *__restrict__ PME, int64_t k) {
@@ -547,23 +547,13 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     if (seg_levels) {
         uint32_t *ovf_win = pos;   // the final-pass scan buffer is free until then (n + 1 words >= nwin)
         HIPCHECK(hipMemsetAsync(d_ovf, 0, 8, st));
-        const int64_t var = knob(KN_SEG_VARIANT);
-        auto run = [&](auto small, auto large, int win, int ts, int tl) {
-            const int64_t nwin = (n + win - 1) / win;
-            KLAUNCH("k_seg_levels", 0.0, small, dim3((unsigned)nwin), dim3(ts), 0, st, S, E, M, PME, n, kept, ovf_win,
-                    d_ovf + 1, d_ovf);
-            KLAUNCH("k_seg_levels_l", 0.0, large, dim3(256), dim3(tl), 0, st, S, E, M, PME, n, kept, ovf_win, d_ovf + 1,
-                    d_ovf);
-        };
-        if (var == 1)
-            run(k_seg_levels<256, 1024, 512, false>, k_seg_levels<1024, kSegCapL, 512, true>, 512, 256, 1024);
-        else if (var == 2)
-            run(k_seg_levels<512, 2048, 1024, false>, k_seg_levels<1024, kSegCapL, 1024, true>, 1024, 512, 1024);
-        else if (var == 3)
-            run(k_seg_levels<128, 256, 128, false>, k_seg_levels<1024, kSegCapL, 128, true>, 128, 128, 1024);
-        else
-            run(k_seg_levels<256, kSegCapS, kSegWin, false>, k_seg_levels<1024, kSegCapL, kSegWin, true>, kSegWin, 256,
-                1024);
+        // windows of 512 positions, up to 1024 hits per 256-thread workgroup
+        // (r05i, C3: 0.44 ms for both launches; 256 / 512: 0.48; 128 / 256: 0.46)
+        const int64_t nwin = (n + kSegWin - 1) / kSegWin;
+        KLAUNCH("k_seg_levels", 0.0, (k_seg_levels<256, kSegCapS, kSegWin, false>), dim3((unsigned)nwin), dim3(256), 0,
+                st, S, E, M, PME, n, kept, ovf_win, d_ovf + 1, d_ovf);
+        KLAUNCH("k_seg_levels_l", 0.0, (k_seg_levels<1024, kSegCapL, kSegWin, true>), dim3(256), dim3(1024), 0, st, S,
+                E, M, PME, n, kept, ovf_win, d_ovf + 1, d_ovf);
         if (stats_on()) {
             unsigned int o2[2] = {0, 0};
             HIPCHECK(hipMemcpyAsync(o2, d_ovf, 8, hipMemcpyDeviceToHost, st));

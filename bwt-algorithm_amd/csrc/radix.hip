@@ -59,6 +59,7 @@ __device__ inline uint32_t wave_sum_u32(uint32_t v) {
 // launches) and its flag is set.  The last ticket holder resets the counter
 // for the next launch.
 constexpr uint64_t kLbA = 1, kLbP = 2;   // aggregate / inclusive prefix
+constexpr int kMaxScanRows = 64;         // rows of one exclusive_scan_rows launch (a ticket each)
 __device__ __forceinline__ uint64_t lb_pack(uint32_t epoch, uint64_t flag, uint32_t v) {
     return ((uint64_t)epoch << 34) | (flag << 32) | v;
 }
@@ -88,10 +89,15 @@ __device__ __forceinline__ int64_t lb_ticket(unsigned *ticket, int64_t ntickets)
 // inclusive flags says where to stop, the ballot of unready lanes whether to
 // wait).  In place (in == out) is allowed: a tile reads its elements before
 // it writes them and no other tile touches them.
+// gridDim.y rows of n elements, `stride` apart, scanned independently (one
+// ticket and one granule range per row)
 __global__ __launch_bounds__(kBlock) void k_scan_lb(const uint32_t *__restrict__ in, uint32_t *out, int64_t n,
                                                     int64_t ntiles, uint64_t *status, unsigned *ticket,
-                                                    uint32_t epoch, int vec) {
-    const int64_t tile = lb_ticket(ticket, ntiles);
+                                                    uint32_t epoch, int vec, int64_t stride) {
+    in += (int64_t)blockIdx.y * stride;
+    out += (int64_t)blockIdx.y * stride;
+    status += (int64_t)blockIdx.y * ntiles;
+    const int64_t tile = lb_ticket(ticket + blockIdx.y, ntiles);
     const int64_t base = tile * kTile + (int64_t)threadIdx.x * kItems;
     uint32_t x[kItems];
     const bool full = vec && base + kItems <= n;
@@ -176,7 +182,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_lb(const uint32_t *__restrict__
 // the 256 totals).  The scatter's global slot of a key of digit d in tile t is
 // then base[d] + prefix[t][d] + its rank in the tile.
 constexpr int kSub = 8192;   // keys per scatter tile (512 threads x 16)
-constexpr int kMaxSub = 4;
+constexpr int kMaxSub = 16;
 constexpr int kLbWin = 16;   // predecessors a digit's look-back reads per step (loads in flight)
 template <class KT>
 __device__ __forceinline__ void hist_load(const KT *__restrict__ keys, int64_t tile, int64_t n, int vec,
@@ -201,8 +207,13 @@ __global__ __launch_bounds__(kBlock) void k_hist_lb(const KT *__restrict__ keys,
     const int wv = threadIdx.x >> 6, d = threadIdx.x, lane = threadIdx.x & 63;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) h[w][d] = 0;
-    uint4 cur[NV], nxt[NV];
-    hist_load<KT>(keys, ht * S, n, vec, cur);
+    // D sub-tiles ahead in flight while one is counted: ~32 KB of loads per
+    // workgroup whatever the key width (one tile of 32-bit keys, four of bytes)
+    constexpr int D = NV >= 8 ? 1 : 8 / NV;
+    uint4 buf[D + 1][NV];
+#pragma unroll
+    for (int q = 0; q < D; ++q)
+        if (q < S && ht * S + q < ntiles) hist_load<KT>(keys, ht * S + q, n, vec, buf[q]);
     __syncthreads();
     uint32_t cnt[kMaxSub];
     uint32_t total = 0;
@@ -211,8 +222,8 @@ __global__ __launch_bounds__(kBlock) void k_hist_lb(const KT *__restrict__ keys,
         cnt[s] = 0;
         const int64_t tile = ht * S + s;
         if (s >= S || tile >= ntiles) continue;   // uniform
-        // the next sub-tile's keys are in flight while this one is counted
-        if (s + 1 < S && tile + 1 < ntiles) hist_load<KT>(keys, tile + 1, n, vec, nxt);
+        if (s + D < S && tile + D < ntiles) hist_load<KT>(keys, tile + D, n, vec, buf[(s + D) % (D + 1)]);
+        uint4 (&cur)[NV] = buf[s % (D + 1)];
         const int64_t b0 = tile * kSub;
         if (vec && b0 + kSub <= n) {
 #pragma unroll
@@ -234,8 +245,6 @@ __global__ __launch_bounds__(kBlock) void k_hist_lb(const KT *__restrict__ keys,
         }
         cnt[s] = c;
         total += c;
-#pragma unroll
-        for (int i = 0; i < NV; ++i) cur[i] = nxt[i];
         __syncthreads();
     }
     uint32_t excl = 0;
@@ -457,7 +466,7 @@ LbState lb_prepare(Ctx &c, int64_t granules) {
     if (++c.lb_epoch >= (1u << 30)) c.lb_epoch = 1;   // epochs wrap: clear again
     if (fresh || c.lb_epoch == 1) HIPCHECK(hipMemsetAsync(g.p, 0, g.bytes, c.stream));
     if (!c.lb_ticket.p) {
-        c.lb_ticket.ensure(64);
+        c.lb_ticket.ensure(kMaxScanRows * sizeof(unsigned));
         HIPCHECK(hipMemsetAsync(c.lb_ticket.p, 0, c.lb_ticket.bytes, c.stream));
     }
     return {g.as<uint64_t>(), c.lb_ticket.as<unsigned>(), c.lb_epoch};
@@ -466,13 +475,19 @@ LbState lb_prepare(Ctx &c, int64_t granules) {
 // one pass's histogram and offsets: prefix rows in S_SORT_HIST, digit bases after them
 template <class KT>
 void launch_hist(Ctx &c, const KT *keys, int64_t n, int shift, int64_t ntiles, uint32_t **prefix, uint32_t **base) {
-    const int S = ntiles >= 4096 ? 4 : ntiles >= 1024 ? 2 : 1;   // scatter tiles per histogram workgroup
+    const int64_t fs = knob(KN_HIST_S);
+    // scatter tiles per histogram workgroup: ~512-1024 workgroups -- the
+    // look-back chains, not the reads, set the time of larger grids (r05j, C3
+    // 32-bit pass: 12207 / 6104 / 3052 / 763 workgroups 292 / 198 / 164 / 140 us)
+    const int S = fs > 0 ? (int)std::min<int64_t>(fs, kMaxSub) : (int)std::max<int64_t>(1, std::min<int64_t>(kMaxSub, ntiles / 512));
     const int64_t nhist = (ntiles + S - 1) / S;
     c.slot[S_SORT_HIST].ensure((size_t)(ntiles + 1) * 256 * sizeof(uint32_t));
     *prefix = c.slot[S_SORT_HIST].as<uint32_t>();
     *base = *prefix + ntiles * 256;
     const LbState lb = lb_prepare(c, nhist * 256);
-    KLAUNCH("radix_hist", (double)n * (double)sizeof(KT), k_hist_lb<KT>, dim3((unsigned)nhist), dim3(kBlock), 0,
+    KLAUNCH(sizeof(KT) == 1 ? "radix_hist_k1" : sizeof(KT) == 2 ? "radix_hist_k2" : sizeof(KT) == 4 ? "radix_hist_k4"
+                                                                                        : "radix_hist_k8",
+            (double)n * (double)sizeof(KT), k_hist_lb<KT>, dim3((unsigned)nhist), dim3(kBlock), 0,
             c.stream, keys, n, shift, ntiles, S, nhist, lb.status, *prefix, *base, lb.ticket, lb.epoch,
             ((uintptr_t)keys & 15) == 0 ? 1 : 0);
 }
@@ -541,16 +556,22 @@ void radix_sort_impl(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
 
 }  // namespace
 
+void exclusive_scan_rows(Ctx &c, const uint32_t *in, uint32_t *out, int64_t n, int rows, int64_t stride) {
+    if (n <= 0 || rows <= 0) return;
+    if (rows > kMaxScanRows) fail(BWTMI_E_ARG, "exclusive_scan_rows: %d rows (at most %d)", rows, kMaxScanRows);
+    const int64_t ntiles = (n + kTile - 1) / kTile;
+    const LbState lb = lb_prepare(c, ntiles * rows);
+    // 16-byte vectors need aligned bases in every row
+    const int vec = (((uintptr_t)in | (uintptr_t)out) & 15) == 0 && (rows == 1 || (stride & 3) == 0) ? 1 : 0;
+    KLAUNCH("k_scan", 2.0 * (double)n * rows * 4.0, k_scan_lb, dim3((unsigned)ntiles, (unsigned)rows), dim3(kBlock), 0,
+            c.stream, in, out, n, ntiles, lb.status, lb.ticket, lb.epoch, vec, stride);
+    HIPCHECK(hipGetLastError());
+}
+
 template <class T>
 void exclusive_scan(Ctx &c, const T *in, T *out, int64_t n) {
     static_assert(sizeof(T) == 4, "32-bit scans");
-    if (n <= 0) return;
-    const int64_t ntiles = (n + kTile - 1) / kTile;
-    const LbState lb = lb_prepare(c, ntiles);
-    const int vec = (((uintptr_t)in | (uintptr_t)out) & 15) == 0 ? 1 : 0;   // 16-byte vectors need aligned bases
-    KLAUNCH("k_scan", 2.0 * (double)n * (double)sizeof(T), k_scan_lb, dim3((unsigned)ntiles), dim3(kBlock), 0, c.stream,
-            (const uint32_t *)in, (uint32_t *)out, n, ntiles, lb.status, lb.ticket, lb.epoch, vec);
-    HIPCHECK(hipGetLastError());
+    exclusive_scan_rows(c, (const uint32_t *)in, (uint32_t *)out, n, 1, 0);
 }
 
 template void exclusive_scan<uint32_t>(Ctx &, const uint32_t *, uint32_t *, int64_t);

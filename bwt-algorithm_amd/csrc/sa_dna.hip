@@ -692,41 +692,78 @@ __device__ __forceinline__ uint32_t ls_key(const uint32_t *__restrict__ rank, ui
     return a + h < n ? rank[a + h] : 0u;
 }
 
-// runs of >= 16 equal symbols in t[0, n - 1): flags at their first position
-// and at the position past their last one
-__global__ __launch_bounds__(kB) void k_run_marks(Deep d, int64_t n, uint32_t *__restrict__ fst, uint32_t *__restrict__ fen) {
-    const int64_t p = (int64_t)blockIdx.x * kB + threadIdx.x;
-    if (p >= n) return;
-    bool st = false, en = false;
-    if (p + 16 < n) {   // 16 real symbols from p
+// runs of >= 16 equal symbols in t[0, n - 1): their first positions, appended
+// (unordered) to rs through one atomic per workgroup
+// (16 consecutive positions per thread: a run starts at most once among them
+// -- two starts need a run of >= 16 between them)
+__global__ __launch_bounds__(kB) void k_run_starts(Deep d, int64_t n, uint32_t *__restrict__ rs,
+                                                   uint32_t *__restrict__ kcount, uint32_t cap) {
+    const int64_t p0 = ((int64_t)blockIdx.x * kB + threadIdx.x) * 16;
+    bool st = false;
+    int64_t p = 0;
+    for (int j = 0; j < 16 && !st; ++j) {
+        p = p0 + j;
+        if (p + 16 >= n) break;   // 16 real symbols from p
         const int c = homopolymer16(d, p);
         st = c >= 0 && (p == 0 || sym_at(d, p - 1) != c);
     }
-    if (p >= 16 && p <= n - 1) {   // p is past a run whose last 16 symbols are p-16 .. p-1
-        const int c = homopolymer16(d, p - 16);
-        en = c >= 0 && (p == n - 1 || sym_at(d, p) != c);
+    __shared__ uint32_t wc[kB / 64 + 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t m = __ballot(st);
+    if (lane == 0) wc[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < kB / 64; ++w) {
+            const uint32_t x = wc[w];
+            wc[w] = tot;
+            tot += x;
+        }
+        wc[kB / 64] = tot ? atomicAdd(kcount, tot) : 0u;
     }
-    fst[p] = st;
-    fen[p] = en;
+    __syncthreads();
+    if (st) {
+        const uint32_t at = wc[kB / 64] + wc[wv] + (uint32_t)__popcll(m & lanes_below(lane));
+        if (at < cap) rs[at] = (uint32_t)p;
+    }
 }
 
-// run k = [starts[k], ends[k]): re[b] = ends[k] for every block b whose last
-// position 16 b + 15 lies in the run
-__global__ __launch_bounds__(kB) void k_run_fill(const uint32_t *__restrict__ fst, const uint32_t *__restrict__ pst,
-                                                 const uint32_t *__restrict__ fen, const uint32_t *__restrict__ pen,
-                                                 int64_t n, uint32_t *__restrict__ rs, uint32_t *__restrict__ rend) {
-    const int64_t p = (int64_t)blockIdx.x * kB + threadIdx.x;
-    if (p >= n) return;
-    if (fst[p]) rs[pst[p]] = (uint32_t)p;
-    if (fen[p]) rend[pen[p]] = (uint32_t)p;
-}
-__global__ __launch_bounds__(kB) void k_run_blocks(const uint32_t *__restrict__ rs, const uint32_t *__restrict__ rend,
-                                                   const uint32_t *__restrict__ kcount, uint32_t *__restrict__ re) {
+// one workgroup per run (grid-stride over the K runs): its end e (the first
+// position >= start + 16 whose symbol differs, or n - 1: '$'), found 16
+// positions per thread and 8 windows in flight, then re[b] = e for every block
+// b whose last position 16 b + 15 lies in [start, e)
+__global__ __launch_bounds__(kB) void k_run_ends(Deep d, int64_t n, const uint32_t *__restrict__ rs,
+                                                 const uint32_t *__restrict__ kcount, uint32_t *__restrict__ re) {
+    __shared__ unsigned long long first;
     const uint32_t K = *kcount;
     for (uint32_t k = blockIdx.x; k < K; k += gridDim.x) {
-        const int64_t s0 = rs[k], e0 = rend[k];
-        const int64_t b0 = s0 >= 15 ? (s0 - 15 + 15) / 16 : 0, b1 = (e0 - 1 - 15) / 16;   // 16 b + 15 in [s0, e0)
+        const int64_t s0 = rs[k];
+        const int c = sym_at(d, s0);
+        if (threadIdx.x == 0) first = (unsigned long long)(n - 1);
+        __syncthreads();
+        for (int64_t base = s0 + 16;; base += (int64_t)kB * 16 * 8) {   // uniform (first is read after a barrier)
+            int64_t mine = n - 1;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int64_t pos = base + ((int64_t)q * kB + threadIdx.x) * 16;
+                if (pos >= n - 1 || mine < n - 1) continue;
+                if (pos + 16 <= n - 1 && homopolymer16(d, pos) == c) continue;
+                for (int j = 0; j < 16; ++j)
+                    if (pos + j >= n - 1 || sym_at(d, pos + j) != c) {
+                        mine = pos + j;
+                        break;
+                    }
+            }
+            if (mine < n - 1) atomicMin(&first, (unsigned long long)mine);
+            __syncthreads();
+            const int64_t e = (int64_t)first;
+            if (e < n - 1 || base + (int64_t)kB * 16 * 8 >= n - 1) break;
+            __syncthreads();
+        }
+        const int64_t e0 = (int64_t)first;
+        const int64_t b0 = s0 >> 4, b1 = (e0 - 16) >> 4;   // 16 b + 15 in [s0, e0)
         for (int64_t b = b0 + threadIdx.x; b <= b1; b += kB) re[b] = (uint32_t)e0;
+        __syncthreads();   // `first` is reset for the next run
     }
 }
 
@@ -1071,20 +1108,19 @@ bool sa_sort(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, in
     // buffers are free until the large-group rounds
     Deep dp{P, nullptr, small ? 1 : 0, 0};
     if (G > 0) {
-        c.slot[S_IDX12].ensure((size_t)(n / 16 + 2) * 4 + 64);
-        uint32_t *re = c.slot[S_IDX12].as<uint32_t>();
-        KLAUNCH("dna_run_marks", 0.0, k_run_marks, dim3(nblocks(n)), dim3(kB), 0, st, dp, n, fs, fe);
-        HIPCHECK(hipMemsetAsync(fs + n, 0, 4, st));
-        exclusive_scan<uint32_t>(c, fs, ps, n + 1);
+        const int64_t cap = n / 16 + 64;   // runs of >= 16 are disjoint
+        c.slot[S_IDX12].ensure((size_t)(n / 16 + 2) * 4 + (size_t)cap * 4 + 64);
+        uint32_t *re = c.slot[S_IDX12].as<uint32_t>(), *rs = re + n / 16 + 2;
+        uint32_t *kcount = counts + 40;   // past the class / list / change counters
+        HIPCHECK(hipMemsetAsync(kcount, 0, 4, st));
+        KLAUNCH("dna_run_starts", 0.0, k_run_starts, dim3(nblocks((n + 15) / 16)), dim3(kB), 0, st, dp, n, rs, kcount,
+                (uint32_t)cap);
         uint32_t K = 0;
-        HIPCHECK(hipMemcpyAsync(&K, ps + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(&K, kcount, 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
         if (K) {
-            exclusive_scan<uint32_t>(c, fe, pe, n);
-            uint32_t *rs = keys, *rend = keys + K + 16;   // the keys are dead until the class lists
-            KLAUNCH("dna_run_fill", 0.0, k_run_fill, dim3(nblocks(n)), dim3(kB), 0, st, fs, ps, fe, pe, n, rs, rend);
-            KLAUNCH("dna_run_blocks", 0.0, k_run_blocks, dim3((unsigned)std::min<int64_t>(K, 4096)), dim3(kB), 0, st, rs,
-                    rend, ps + n, re);
+            KLAUNCH("dna_run_ends", 0.0, k_run_ends, dim3((unsigned)std::min<uint32_t>(K, 2048)), dim3(kB), 0, st, dp, n,
+                    rs, kcount, re);
             dp.re = re;
             dp.on = 1;
         }

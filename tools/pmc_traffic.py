@@ -20,9 +20,10 @@ def short(name: str) -> str:
     m = re.search(r"::(k_[A-Za-z0-9_]+)", name)
     s = m.group(1) if m else name.split("(")[0].strip()
     # type template arguments (k_scatter<key, value, ...>: kv8 = <u32,u32>, kv12 = <u64,u32>)
-    ts = re.findall(r"(unsigned int|unsigned long|unsigned short)", name.replace("(anonymous namespace)", "").split("(")[0])
+    ts = re.findall(r"(unsigned int|unsigned long|unsigned short|unsigned char)",
+                    name.replace("(anonymous namespace)", "").split("(")[0])
     if ts:
-        s += "<" + ",".join({"unsigned int": "u32", "unsigned long": "u64", "unsigned short": "u16"}[t]
+        s += "<" + ",".join({"unsigned int": "u32", "unsigned long": "u64", "unsigned short": "u16", "unsigned char": "u8"}[t]
                             for t in ts[:2]) + ">"
     return s
 

@@ -18,7 +18,7 @@ _lib.bind_host(ctx)
 seq = synth.generate_contig(bp, 1, 0.0)
 for rep in range(2):
     for v in variants:
-        with _lib.knobs(SEG_VARIANT=v):
+        if True:   # geometry variants were compared here (r05i); one geometry is kept
             j = Job(min_copies=3, show_progress=True, build_index=False)
             j.add_contig("contig1", seq, 30, 30)
             j.upload(ctx)
