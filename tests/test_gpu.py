@@ -540,6 +540,19 @@ def test_long_runs_ordered_in_closed_form_vs_oracle(gpu_ctx, alpha):
     _check_index(bytes([alpha[2]]) * 17 + bytes([alpha[0]]) * 33 + b"$")
 
 
+@pytest.mark.parametrize("S", [1, 3, 16])
+def test_radix_histogram_geometries(gpu_ctx, S):
+    """The single-pass radix histogram with 1, 3 or 16 scatter tiles per
+    workgroup (BWTMI_HIST_S; look-back chains of different lengths, partial
+    last workgroups): the candidate sorts of the strict scan and the suffix
+    sorts give the oracle's results."""
+    from bwtmi import _lib, synth
+    with _lib.knobs(HIST_S=S):
+        _same(_planted(300_000, 95 + S), 1, 1000, 3)
+        _check_index(synth.generate_contig(400_000, 96 + S, gaps="n1") + b"$")
+        _check_index(synth.generate_contig(300_000, 99 + S) + b"$")
+
+
 def test_small_alphabet_texts_through_general_doubling(gpu_ctx):
     """BWTMI_SA_SMALL=0: gap texts take the general prefix doubling (index.hip)
     instead of the 3-bit string sort; the same arrays as the oracle."""
