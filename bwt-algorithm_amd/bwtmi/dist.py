@@ -55,6 +55,23 @@ def launch_ranks(n: int, cmd: Sequence[str], extra_env: Optional[Callable[[int],
             env.update(extra_env(r))
         procs.append(subprocess.Popen(list(cmd), env=env, start_new_session=True))
     rc = 0
+    # a SIGTERM / SIGHUP to this launcher (kill, a scheduler's soft stop) reaches
+    # the ranks too: they run in sessions of their own and would outlive it
+    forwarded = {}
+
+    def forward(signum, frame):
+        for q in procs:
+            if q.poll() is None:
+                try:
+                    os.killpg(q.pid, signum)
+                except ProcessLookupError:
+                    pass
+        raise SystemExit(128 + signum)
+    for sig in (signal.SIGTERM, signal.SIGHUP):
+        try:
+            forwarded[sig] = signal.signal(sig, forward)
+        except ValueError:   # not the main thread: no handlers
+            pass
     try:
         live = list(procs)
         while live:
@@ -74,6 +91,8 @@ def launch_ranks(n: int, cmd: Sequence[str], extra_env: Optional[Callable[[int],
                         except ProcessLookupError:
                             pass
     finally:
+        for sig, old in forwarded.items():
+            signal.signal(sig, old)
         for p in procs:
             if p.poll() is None:
                 try:

@@ -577,8 +577,7 @@ int64_t fasta_count_records(const char *path, int64_t limit) {
         if (bad.load(std::memory_order_relaxed) || total.load(std::memory_order_relaxed) >= limit) return;
         const int64_t a = k * kPiece, b = std::min(size, a + kPiece);
         const int64_t from = a > 0 ? a - 1 : 0;   // the byte before the piece decides its first '>'
-        thread_local std::vector<char> buf;
-        buf.resize((size_t)(b - from));
+        std::vector<char> buf((size_t)(b - from));   // this call's only: freed when the task ends
         int64_t got = 0;
         while (got < b - from) {
             const ssize_t r = ::pread(fd, buf.data() + got, (size_t)(b - from - got), (off_t)(from + got));

@@ -741,6 +741,47 @@ def test_rank_launcher_env_and_failure(tmp_path):
     assert rc == 3 and time.time() - t0 < 60
 
 
+def test_rank_launcher_forwards_sigterm(tmp_path):
+    """A SIGTERM to the launcher (dist.launch_ranks in the CLI parent) reaches
+    the rank processes, which run in sessions of their own: none outlives it
+    (ADVICE r4)."""
+    import signal
+    import subprocess
+    import sys
+    import time
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bwt-algorithm_amd")
+    rank = tmp_path / "rank.py"
+    rank.write_text("import os, sys, time\nopen(sys.argv[1] + os.environ['RANK'], 'w').write(str(os.getpid()))\n"
+                    "time.sleep(600)\n")
+    out = str(tmp_path / "pid")
+    launcher = subprocess.Popen([sys.executable, "-c",
+                                 "import sys; sys.path.insert(0, %r)\nfrom bwtmi import dist\n"
+                                 "sys.exit(dist.launch_ranks(2, [sys.executable, %r, %r]))" % (pkg, str(rank), out)])
+    pids = []
+    for _ in range(300):
+        if all(os.path.exists(out + str(r)) and open(out + str(r)).read() for r in range(2)):
+            pids = [int(open(out + str(r)).read()) for r in range(2)]
+            break
+        time.sleep(0.05)
+    assert len(pids) == 2
+    launcher.send_signal(signal.SIGTERM)
+    assert launcher.wait(timeout=30) != 0
+    for _ in range(200):
+        alive = []
+        for p in pids:
+            try:
+                os.kill(p, 0)
+                with open(f"/proc/{p}/stat") as f:
+                    if f.read().split()[2] != "Z":
+                        alive.append(p)
+            except (ProcessLookupError, FileNotFoundError):
+                pass
+        if not alive:
+            break
+        time.sleep(0.05)
+    assert not alive, alive
+
+
 def test_cli_self_launch_decisions(tmp_path, monkeypatch):
     """`bwt.py IN.fa --jobs N|0` without a launcher: min(N or #GPUs, #GPUs,
     #contigs) ranks of the same CLI (bwt.py:3850-3912, 3863-3864), one per
