@@ -51,6 +51,7 @@ def lib():
                                       C.c_int32, C.POINTER(C.POINTER(C.c_int64))]
         L.orc_free.argtypes = [p]
         L.orc_suffix_array.argtypes = [p, C.c_int64, p]
+        L.orc_set_sa_threads.argtypes = [C.c_int32]
         L.orc_bwt.argtypes = [p, C.c_int64, p, p]
         L.orc_char_counts.argtypes = [p, C.c_int64, p, p]
         L.orc_occ_len.restype = C.c_int64
@@ -104,14 +105,21 @@ def effective_max_unit(seq_len: int, min_copies: int = 3, max_unit_len: int = 12
 class Index:
     """Reference-equivalent BWTCore arrays (text must include the sentinel)."""
 
-    def __init__(self, text, sa_sample_rate: int = 32, occ_sample_rate: int = 128, k: int = 8):
+    def __init__(self, text, sa_sample_rate: int = 32, occ_sample_rate: int = 128, k: int = 8,
+                 threads: int = 1):
+        """threads > 1 sorts each prefix-doubling round on that many threads
+        (same order: the sort key is a total order)."""
         t = _u8(text)
         self.text = t
         n = len(t)
         self.n = n
         L = lib()
         self.sa = np.zeros(n, dtype=np.int32)
-        L.orc_suffix_array(_ptr(t), n, _ptr(self.sa))
+        L.orc_set_sa_threads(threads)
+        try:
+            L.orc_suffix_array(_ptr(t), n, _ptr(self.sa))
+        finally:
+            L.orc_set_sa_threads(1)
         self.bwt = np.zeros(n, dtype=np.uint8)
         L.orc_bwt(_ptr(t), n, _ptr(self.sa), _ptr(self.bwt))
         self.totals = np.zeros(256, dtype=np.int64)

@@ -85,6 +85,23 @@ def test_index_arrays_match_reference(golden_dir):
             assert list(ix.backward_search(p.encode())) == iv, (key, p)
 
 
+def test_threaded_suffix_array_equals_serial(golden_dir):
+    """The baseline's threaded prefix doubling (chunk sorts + co-rank merges +
+    chunked re-rank) returns the reference's suffix array: on every golden
+    text, and equal to the 1-thread sort on texts large enough to take the
+    parallel path (runs, repeats, N blocks, odd thread counts)."""
+    arrs = np.load(os.path.join(golden_dir, "index_arrays.npz"))
+    for key in _load(golden_dir, "index_meta.json"):
+        assert (oracle.Index(arrs[key + "__text"].tobytes(), threads=4).sa == arrs[key + "__sa"]).all(), key
+    rng = np.random.default_rng(5)
+    for n, th in [(4096, 2), (50_001, 3), (200_000, 8)]:
+        t = rng.choice(np.frombuffer(b"ACGTN", np.uint8), n - 1)
+        t[100:2100] = ord("A")
+        t[3000:3600] = np.tile(t[2900:2906], 100)
+        text = np.append(t, np.uint8(36)).tobytes()
+        assert (oracle.Index(text, threads=th).sa == oracle.Index(text).sa).all(), (n, th)
+
+
 def test_motif_helpers_match_reference(golden_dir):
     k = _load(golden_dir, "motif_known.json")
     for w, v in k["canonical"].items():
