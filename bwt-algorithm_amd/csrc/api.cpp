@@ -279,6 +279,7 @@ static void ctx_release(Ctx &c) {
     for (auto &s : c.slot) s.release();
     c.lb_ticket.release();
     for (auto &h : c.host) h.release();
+    c.mbox.release();
     for (hipEvent_t e : c.evpool) (void)hipEventDestroy(e);
     c.evpool.clear();
     (void)hipEventDestroy(c.ev0);

@@ -189,6 +189,15 @@ struct Ctx {
     DBuf lb_ticket;          // the look-back launches' tile ticket (radix.hip)
     uint32_t lb_epoch = 0;   // the last look-back launch's epoch
     HBuf host[4];
+    // pinned mailbox of the scan's small device->host reads: the reads of one
+    // step are queued into it and share one stream wait (a copy into pageable
+    // memory is staged synchronously -- one host round trip per value, ~20 us)
+    HBuf mbox;
+    template <class T>
+    T *mailbox(size_t n) {
+        mbox.ensure(std::max<size_t>(n * sizeof(T), 4096));
+        return mbox.as<T>();
+    }
     struct DeviceIndex *scratch_index = nullptr;   // reused by the worker-path index builds
     // device work that runs behind host work (the worker-path index builds):
     // every entry point that uses this context joins it first (ctx_wait)
@@ -322,10 +331,10 @@ void strict_scan_mm_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min
 void recompute_batch_device(Ctx &c, const RcReq *req, int64_t nreq, RcOut *out, std::vector<char> &arena);
 
 // ----- nested suppression / sort / dedup of one contig's strict hits (nested.hip)
-// d_maxlen: the hits' longest span, already on the device (the strict scan's
-// compaction reduces it); nullptr: reduced here
+// maxlen: the hits' longest span, when the caller knows it (the strict scan's
+// compaction reduces it and reads it with the hit count); -1: reduced here
 void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
-                        ScreenedVec &out, const unsigned long long *d_maxlen = nullptr);
+                        ScreenedVec &out, int64_t maxlen = -1);
 
 // ----- suffix array + BWT of ACGT* '$' texts (sa_dna.hip)
 bool sa_dna_eligible(uint8_t last, int64_t n, const int64_t *totals);

@@ -484,7 +484,7 @@ static void screen_levels(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int32_t lm
 }
 
 void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
-                        ScreenedVec &out, const unsigned long long *d_maxlen) {
+                        ScreenedVec &out, int64_t maxlen_known) {
     out.clear();
     if (n <= 0) return;
     if (n >= (int64_t)UINT32_MAX) fail(BWTMI_E_ARG, "too many strict hits for one contig (%lld)", (long long)n);
@@ -519,23 +519,26 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     unsigned long long *d_max = c.slot[S_COUNTS].as<unsigned long long>();
 
     // longest span -> key widths
+    unsigned long long *mb = c.mailbox<unsigned long long>(4);
     unsigned long long maxlen = 0;
-    if (d_maxlen) {
-        HIPCHECK(hipMemcpyAsync(&maxlen, d_maxlen, 8, hipMemcpyDeviceToHost, st));
+    if (maxlen_known >= 0) {
+        maxlen = (unsigned long long)maxlen_known;
     } else {
         HIPCHECK(hipMemsetAsync(d_max, 0, 8, st));
         KLAUNCH("k_maxlen", 0.0, k_maxlen, dim3((unsigned)std::min<int64_t>(1024, blocks(n))), dim3(kB), 0, st, d_hits,
                 n, d_max);
-        HIPCHECK(hipMemcpyAsync(&maxlen, d_max, 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(mb, d_max, 8, hipMemcpyDeviceToHost, st));
+        scan_wait(st);
+        maxlen = mb[0];
     }
-    scan_wait(st);
-    const int mb = std::max(1, bits_for((uint64_t)lmax));
+    const int mb_bits = std::max(1, bits_for((uint64_t)lmax));
     const int lb = std::max(1, bits_for(maxlen));
-    if (lb + mb > 64) fail(BWTMI_E_ARG, "span too long for the screen keys");
+    if (lb + mb_bits > 64) fail(BWTMI_E_ARG, "span too long for the screen keys");
     auto round8 = [](int b) { return ((b + 7) / 8) * 8; };
 
-    KLAUNCH("k_keys", 0.0, k_keys, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, mb, (int64_t)lmax, kpos, vpos, kgrp, vgrp);
-    radix_sort_pairs32(c, kpos, vpos, n, 0, round8(lb + mb));
+    KLAUNCH("k_keys", 0.0, k_keys, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, mb_bits, (int64_t)lmax, kpos, vpos, kgrp,
+            vgrp);
+    radix_sort_pairs32(c, kpos, vpos, n, 0, round8(lb + mb_bits));
     KLAUNCH("k_keys_start", 0.0, k_keys_start, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, kpos);
     radix_sort_pairs32(c, kpos, vpos, n, 0, round8(std::max(1, bits_for((uint64_t)text_len))));   // start < text_len
     KLAUNCH("k_gather", 0.0, k_gather, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, S, E, M, rank_of, kept);
@@ -543,6 +546,24 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     // every level, segment by segment, in one launch (BWTMI_SEG_LEVELS=0: per-level launches)
     const bool seg_levels = knob(KN_SEG_LEVELS) != 0;
     unsigned int *d_ovf = reinterpret_cast<unsigned int *>(d_max);   // [0] fallback flag, [1] overflow windows
+    // one word per kept hit when the start fits the low half and the longest span
+    // and the longest primitive motif fit the high half (BWTMI_SCREEN_WIDE=1:
+    // always two)
+    const bool wide = knob(KN_SCREEN_WIDE) != 0;
+    const int lbits = lb;   // bits of the longest span (hit lengths are <= maxlen)
+    const int pbits = std::max(1, bits_for((uint64_t)lmax));
+    out.lbits = !wide && lbits + pbits <= 32 && bits_for((uint64_t)text_len) <= 32 ? lbits : -1;
+    // the kept flags -> their order -> the packed records, and the kept count
+    // with the screen's overflow flag (mb[1]) in the same stream wait
+    auto final_pass = [&] {
+        KLAUNCH("k_final_flags", 0.0, k_final_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, kept, n, flag);
+        HIPCHECK(hipMemsetAsync(flag + n, 0, 4, st));
+        exclusive_scan<uint32_t>(c, flag, pos, n + 1);
+        KLAUNCH("k_final_compact", 0.0, k_final_compact, dim3(blocks(n)), dim3(kB), 0, st, d_hits, vpos, flag, pos, n,
+                out.lbits, dout);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemcpyAsync(reinterpret_cast<uint32_t *>(mb), pos + n, 4, hipMemcpyDeviceToHost, st));
+    };
     unsigned int ovf = 1;
     if (seg_levels) {
         uint32_t *ovf_win = pos;   // the final-pass scan buffer is free until then (n + 1 words >= nwin)
@@ -554,32 +575,22 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
                 st, S, E, M, PME, n, kept, ovf_win, d_ovf + 1, d_ovf);
         KLAUNCH("k_seg_levels_l", 0.0, (k_seg_levels<1024, kSegCapL, kSegWin, true>), dim3(256), dim3(1024), 0, st, S,
                 E, M, PME, n, kept, ovf_win, d_ovf + 1, d_ovf);
-        if (stats_on()) {
-            unsigned int o2[2] = {0, 0};
-            HIPCHECK(hipMemcpyAsync(o2, d_ovf, 8, hipMemcpyDeviceToHost, st));
-            scan_wait(st);
+        // the window list (ovf_win) is spent: the final pass runs before the
+        // host sees the fallback flag, and runs again after a fallback (rare)
+        final_pass();
+        HIPCHECK(hipMemcpyAsync(mb + 1, d_ovf, 8, hipMemcpyDeviceToHost, st));
+        scan_wait(st);
+        const unsigned int *o2 = reinterpret_cast<const unsigned int *>(mb + 1);
+        ovf = o2[0];
+        if (stats_on())
             std::fprintf(stderr, "  screen: %lld hits, %u overflow windows, fallback %u\n", (long long)n, o2[1], o2[0]);
-        }
-        HIPCHECK(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, st));
+    }
+    if (ovf) {
+        screen_levels(c, d_hits, n, lmax, mb_bits, kgrp, vgrp, rank_of, S, E, M, PME, kept, nb);
+        final_pass();
         scan_wait(st);
     }
-    if (ovf) screen_levels(c, d_hits, n, lmax, mb, kgrp, vgrp, rank_of, S, E, M, PME, kept, nb);
-    KLAUNCH("k_final_flags", 0.0, k_final_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, kept, n, flag);
-    HIPCHECK(hipMemsetAsync(flag + n, 0, 4, st));
-    exclusive_scan<uint32_t>(c, flag, pos, n + 1);
-    // one word per kept hit when the start fits the low half and the longest span
-    // and the longest primitive motif fit the high half (BWTMI_SCREEN_WIDE=1:
-    // always two)
-    const bool wide = knob(KN_SCREEN_WIDE) != 0;
-    const int lbits = lb;   // bits of the longest span (hit lengths are <= maxlen)
-    const int pbits = std::max(1, bits_for((uint64_t)lmax));
-    out.lbits = !wide && lbits + pbits <= 32 && bits_for((uint64_t)text_len) <= 32 ? lbits : -1;
-    KLAUNCH("k_final_compact", 0.0, k_final_compact, dim3(blocks(n)), dim3(kB), 0, st, d_hits, vpos, flag, pos, n,
-            out.lbits, dout);
-    HIPCHECK(hipGetLastError());
-    uint32_t nk = 0;
-    HIPCHECK(hipMemcpyAsync(&nk, pos + n, 4, hipMemcpyDeviceToHost, st));
-    scan_wait(st);
+    const uint32_t nk = *reinterpret_cast<const uint32_t *>(mb);
     const size_t words = (size_t)nk * (out.lbits >= 0 ? 1 : 2);
     out.w.resize(words);
     // into a registered block: a pinned DMA instead of a staged pageable copy

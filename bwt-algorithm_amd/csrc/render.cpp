@@ -705,7 +705,23 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
         const int64_t a = C.a, b = C.b;
         o.reserve((size_t)(b - a) * 256);
         double cp[4], ent;
+        // a row's flanks and core are bytes of its contig at random distances
+        // from the last row's: their lines are requested a few rows ahead
+        constexpr int64_t kAhead = 6;
+        auto prefetch_row = [&](int64_t k) {
+            const Rec &r = *rows[(size_t)k].r;
+            const Seq &full = job.contigs[(size_t)r.chrom].full;
+            if (full.empty()) return;
+            const int64_t FL = (int64_t)full.size();
+            const int64_t s0 = std::min(std::max<int64_t>(0, r.start - 30), FL - 1), e0 = std::min(std::max<int64_t>(0, r.end), FL - 1);
+            __builtin_prefetch(full.data() + s0);
+            __builtin_prefetch(full.data() + s0 + 64);
+            __builtin_prefetch(full.data() + e0);
+        };
+        if (fmt == BWTMI_FMT_STRFINDER)
+            for (int64_t k = a; k < std::min(b, a + kAhead); ++k) prefetch_row(k);
         for (int64_t k = a; k < b; ++k) {
+            if (fmt == BWTMI_FMT_STRFINDER && k + kAhead < b) prefetch_row(k + kAhead);
             const Rec &r = *rows[(size_t)k].r;
             const int64_t row_id = C.id0 + (k - a);
             switch (fmt) {

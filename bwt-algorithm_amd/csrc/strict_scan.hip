@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstring>
 #include <vector>
 
 #include "device.h"
@@ -543,13 +544,11 @@ __global__ void k_count_long(const uint64_t *__restrict__ keys, int64_t nc, int3
 // lanes mark which of 64 consecutive d divide L (ballot), each divisor in
 // ascending order is tested over the unit 64 bytes at a time (coalesced), the
 // first one without a mismatch is the period
-__global__ __launch_bounds__(256) void k_period_wave(const uint64_t *__restrict__ keys, int64_t nlong, int32_t umax, int sb,
-                                                     const int64_t *__restrict__ hit_i, const int64_t *__restrict__ hit_c,
-                                                     const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
-                                                     const uint8_t *__restrict__ t, bwtmi_hit *__restrict__ hits) {
+__device__ __forceinline__ void period_wave_one(const uint64_t *__restrict__ keys, int64_t k, int32_t umax, int sb,
+                                                const int64_t *__restrict__ hit_i, const int64_t *__restrict__ hit_c,
+                                                const uint32_t *__restrict__ pos, const uint8_t *__restrict__ t,
+                                                bwtmi_hit *__restrict__ hits) {
     const int lane = threadIdx.x & 63;
-    const int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (k >= nlong || !flag[k]) return;   // wave-uniform
     const int32_t L = (int32_t)((int64_t)umax - (int64_t)(keys[k] >> sb));
     const uint8_t *s = t + hit_i[k];
     int32_t p = L;
@@ -572,6 +571,19 @@ __global__ __launch_bounds__(256) void k_period_wave(const uint64_t *__restrict_
         h.prim_len = p;
         h.copies = p < L ? (h.end - h.start) / p : hit_c[k];
     }
+}
+
+// The count of long units comes from the device (k_count_long): the launch
+// is sized from the candidate count, and each wave takes units nwaves apart.
+__global__ __launch_bounds__(256) void k_period_wave(const uint64_t *__restrict__ keys, const int64_t *__restrict__ d_nlong,
+                                                     int32_t umax, int sb,
+                                                     const int64_t *__restrict__ hit_i, const int64_t *__restrict__ hit_c,
+                                                     const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
+                                                     const uint8_t *__restrict__ t, bwtmi_hit *__restrict__ hits) {
+    const int64_t nlong = *d_nlong;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; k < nlong; k += nwaves)
+        if (flag[k]) period_wave_one(keys, k, umax, sb, hit_i, hit_c, pos, t, hits);   // wave-uniform
 }
 
 // smallest_period_str of text[i : i+L] (bwt.py:1125-1133), then
@@ -623,12 +635,20 @@ __global__ __launch_bounds__(256) void k_present(const uint8_t *__restrict__ t, 
         for (int64_t i = 0; i < head; ++i) mark(m, t[i]);
         for (int64_t i = head + nv * 16; i < n; ++i) mark(m, t[i]);
     }
+    // OR-reduced per wave, then per workgroup in LDS: one global atomic per
+    // workgroup and word (per-wave atomics on the same few addresses serialised
+    // at L2: 53 us on a 12.5 Mbp text, r05r)
+    __shared__ unsigned long long bm[4];
+    if (threadIdx.x < 4) bm[threadIdx.x] = 0;
+    __syncthreads();
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         uint64_t x = m[j];
         for (int o = 32; o > 0; o >>= 1) x |= __shfl_xor(x, o, 64);
-        if ((threadIdx.x & 63) == 0 && x) atomicOr(mask + j, (unsigned long long)x);
+        if ((threadIdx.x & 63) == 0 && x) atomicOr(&bm[j], (unsigned long long)x);
     }
+    __syncthreads();
+    if (threadIdx.x < 4 && bm[threadIdx.x]) atomicOr(mask + threadIdx.x, bm[threadIdx.x]);
 }
 
 // Long unit lengths, sampled.  When K = (mc-1)L >= 95, every qualifying run
@@ -1081,9 +1101,12 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     HIPCHECK(hipMemsetAsync(c.slot[S_COUNTS].p, 0, 256 * sizeof(unsigned long long), st));
     KLAUNCH("k_present", (double)n, k_present, dim3(1024), dim3(256), 0, st, d_text, n,
             c.slot[S_COUNTS].as<unsigned long long>());
+    // the small host reads below go through the pinned mailbox, one wait per step
+    unsigned long long *mb = c.mailbox<unsigned long long>(kCandSegs + 8);
     unsigned long long present[4];
-    HIPCHECK(hipMemcpyAsync(present, c.slot[S_COUNTS].p, sizeof present, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(mb, c.slot[S_COUNTS].p, sizeof present, hipMemcpyDeviceToHost, st));
     scan_wait(st);
+    std::memcpy(present, mb, sizeof present);
     uint8_t code[256] = {0};
     int sigma = 0;
     for (int b = 0; b < 256; ++b)
@@ -1134,10 +1157,11 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
         else launch_runs<8>(c, P, n, lmin, lmax, min_copies, co);
         HIPCHECK(hipGetLastError());
         if (c.timing) HIPCHECK(hipEventRecord(kb, st));
-        HIPCHECK(hipMemcpyAsync(segn, d_count, sizeof segn, hipMemcpyDeviceToHost, st));
-        unsigned long long npend = 0;
-        HIPCHECK(hipMemcpyAsync(&npend, d_npend, sizeof npend, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(mb, d_count, sizeof segn, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(mb + kCandSegs, d_npend, 8, hipMemcpyDeviceToHost, st));
         scan_wait(st);
+        std::memcpy(segn, mb, sizeof segn);
+        const unsigned long long npend = mb[kCandSegs];
         if (c.timing) {
             float ms = 0;
             HIPCHECK(hipEventElapsedTime(&ms, ka, kb));
@@ -1197,31 +1221,33 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
                        c.slot[S_MISC1].as<int64_t>(), c.slot[S_FLAG].as<uint32_t>());
     HIPCHECK(hipMemsetAsync(c.slot[S_SCAN].as<uint32_t>() + nc, 0, sizeof(uint32_t), st));
     exclusive_scan<uint32_t>(c, c.slot[S_FLAG].as<uint32_t>(), c.slot[S_SCAN].as<uint32_t>(), nc);
-    uint32_t last_pos = 0, last_flag = 0;
-    int64_t nlong = 0;
     int64_t *d_nlong = d_off + kCandSegs;   // after the segment offsets
     KLAUNCH("k_count_long", 0.0, k_count_long, dim3(1), dim3(64), 0, st, c.slot[S_CAND_K].as<uint64_t>(), nc, lmax,
             sb, kThreadPeriodL, d_nlong);
-    HIPCHECK(hipMemcpyAsync(&last_pos, c.slot[S_SCAN].as<uint32_t>() + nc - 1, 4, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipMemcpyAsync(&last_flag, c.slot[S_FLAG].as<uint32_t>() + nc - 1, 4, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipMemcpyAsync(&nlong, d_nlong, 8, hipMemcpyDeviceToHost, st));
-    scan_wait(st);
-    const int64_t nh = (int64_t)last_pos + last_flag;
-    c.slot[S_HITS].ensure((size_t)std::max<int64_t>(nh, 1) * sizeof(bwtmi_hit));
+    // hits are a subset of the candidates: the compaction and the long units'
+    // periods run before the host learns the hit count, which it reads with the
+    // longest span in one wait
+    c.slot[S_HITS].ensure((size_t)nc * sizeof(bwtmi_hit));
     unsigned long long *d_maxlen = d_npend + 1;   // the hits' longest span, reduced by k_compact
     HIPCHECK(hipMemsetAsync(d_maxlen, 0, 8, st));
     KLAUNCH("k_compact", 0.0, k_compact, dim3(g), dim3(256), 0, st, c.slot[S_CAND_K].as<uint64_t>(), nc, lmax, sb,
                        c.slot[S_MISC0].as<int64_t>(), c.slot[S_MISC1].as<int64_t>(), c.slot[S_FLAG].as<uint32_t>(),
                        c.slot[S_SCAN].as<uint32_t>(), d_text, c.slot[S_HITS].as<bwtmi_hit>(), d_maxlen);
-    if (nlong > 0)
-        KLAUNCH("k_period_wave", 0.0, k_period_wave, dim3((unsigned)((nlong * 64 + 255) / 256)), dim3(256), 0, st,
-                c.slot[S_CAND_K].as<uint64_t>(), nlong, lmax, sb, c.slot[S_MISC0].as<int64_t>(),
-                c.slot[S_MISC1].as<int64_t>(), c.slot[S_FLAG].as<uint32_t>(), c.slot[S_SCAN].as<uint32_t>(), d_text,
-                c.slot[S_HITS].as<bwtmi_hit>());
+    KLAUNCH("k_period_wave", 0.0, k_period_wave, dim3((unsigned)std::min<int64_t>(2048, (nc * 64 + 255) / 256)),
+            dim3(256), 0, st, c.slot[S_CAND_K].as<uint64_t>(), d_nlong, lmax, sb, c.slot[S_MISC0].as<int64_t>(),
+            c.slot[S_MISC1].as<int64_t>(), c.slot[S_FLAG].as<uint32_t>(), c.slot[S_SCAN].as<uint32_t>(), d_text,
+            c.slot[S_HITS].as<bwtmi_hit>());
     HIPCHECK(hipGetLastError());
+    uint32_t *mb32 = reinterpret_cast<uint32_t *>(mb);
+    HIPCHECK(hipMemcpyAsync(mb32, c.slot[S_SCAN].as<uint32_t>() + nc - 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(mb32 + 1, c.slot[S_FLAG].as<uint32_t>() + nc - 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(mb + 1, d_maxlen, 8, hipMemcpyDeviceToHost, st));
+    scan_wait(st);
+    const int64_t nh = (int64_t)mb32[0] + mb32[1];
+    const int64_t maxlen = (int64_t)mb[1];
     res.raw = nh;
     if (screen) {
-        screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.shits, d_maxlen);
+        screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.shits, maxlen);
         if (c.timing) HIPCHECK(hipEventRecord(c.ev1, st));
     } else {
         if (c.timing) HIPCHECK(hipEventRecord(c.ev1, st));
