@@ -3,10 +3,12 @@
 // 64-bit keys with 32/64-bit values.
 //
 // Radix pass = two launches:
-//   hist    : k_hist_lb -- per-wave LDS histograms of 1-4 scatter tiles per
-//             workgroup, then a decoupled look-back per digit gives every
-//             tile's exclusive prefix of each digit (tile-major rows) and the
-//             last workgroup the digit bases; no count table scan
+//   hist    : k_hist_lb -- per-wave LDS histograms of 1-16 scatter tiles per
+//             workgroup (a run of equal digits in a 16-byte load is one add),
+//             then a two-level look-back per digit (this block of 16 tickets,
+//             then the earlier blocks' aggregates) gives every tile's
+//             exclusive prefix of each digit (tile-major rows) and the last
+//             workgroup the digit bases; no count table scan
 //   scatter : each of the 8 waves owns 1024 consecutive keys of the tile; it
 //             ranks keys of equal digit with 8 ballots (wave64 match-any) in
 //             index order, so the pass is stable; the tile is reordered by
@@ -18,6 +20,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
+#include <vector>
 
 #include "device.h"
 
@@ -172,10 +176,10 @@ __global__ __launch_bounds__(kBlock) void k_scan_lb(const uint32_t *__restrict__
 
 // ------------------------------------------------------------------ radix
 // Histogram + offsets of one pass in one launch.  Scatter tiles hold kSub
-// keys; a histogram workgroup counts S consecutive scatter tiles (S = 1..4:
-// fewer, longer look-back chains on large inputs), one LDS histogram per wave,
-// and thread d owns digit d: it publishes the workgroup's count of d, walks
-// back for the count of d in all earlier workgroups, and writes every scatter
+// keys; a histogram workgroup counts S consecutive scatter tiles (S = 1..16:
+// fewer workgroups on large inputs), one LDS histogram per wave,
+// and thread d owns digit d: it publishes the workgroup's count of d, sums
+// the count of d in all earlier workgroups, and writes every scatter
 // tile's exclusive prefix of d -- tile-major rows prefix[tile][256], one
 // coalesced 1 KB row per tile.  The workgroup holding the last ticket also
 // knows every digit's total and writes the digit bases (exclusive scan over
@@ -183,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_lb(const uint32_t *__restrict__
 // then base[d] + prefix[t][d] + its rank in the tile.
 constexpr int kSub = 8192;   // keys per scatter tile (512 threads x 16)
 constexpr int kMaxSub = 16;
-constexpr int kLbWin = 16;   // predecessors a digit's look-back reads per step (loads in flight)
+constexpr int kLbBlk = 16;   // tickets per look-back block (and granules a digit's look-back reads per step)
 template <class KT>
 __device__ __forceinline__ void hist_load(const KT *__restrict__ keys, int64_t tile, int64_t n, int vec,
                                           uint4 (&v)[kSub / kBlock / (16 / sizeof(KT))]) {
@@ -228,9 +232,25 @@ __global__ __launch_bounds__(kBlock) void k_hist_lb(const KT *__restrict__ keys,
         if (vec && b0 + kSub <= n) {
 #pragma unroll
             for (int i = 0; i < NV; ++i) {
+                // a run of equal digits among the load's VEC consecutive keys is
+                // one add: same-digit lanes serialise an LDS atomic, and partly
+                // ordered keys (the later passes, the refine rounds' digit bytes)
+                // have long runs (tools/hist_bench: 100M bytes in runs of 8-263,
+                // 145 -> 32 us; random 32-bit keys 99 -> 79 us, the read floor)
                 const KT *k = reinterpret_cast<const KT *>(&cur[i]);
+                uint32_t run = (uint32_t)(k[0] >> shift) & 255u, rc = 1;
 #pragma unroll
-                for (int e = 0; e < VEC; ++e) atomicAdd(&h[wv][(uint32_t)(k[e] >> shift) & 255u], 1u);
+                for (int e = 1; e < VEC; ++e) {
+                    const uint32_t dg = (uint32_t)(k[e] >> shift) & 255u;
+                    if (dg != run) {
+                        atomicAdd(&h[wv][run], rc);
+                        run = dg;
+                        rc = 1;
+                    } else {
+                        ++rc;
+                    }
+                }
+                atomicAdd(&h[wv][run], rc);
             }
         } else {
             const int64_t e1 = min(n, b0 + (int64_t)kSub);
@@ -247,33 +267,38 @@ __global__ __launch_bounds__(kBlock) void k_hist_lb(const KT *__restrict__ keys,
         total += c;
         __syncthreads();
     }
-    uint32_t excl = 0;
-    if (ht == 0) {
-        lb_store(status + d, lb_pack(epoch, kLbP, total));
-    } else {
-        lb_store(status + ht * 256 + d, lb_pack(epoch, kLbA, total));
-        // this lane's digit: kLbWin predecessors per step, their loads in flight
-        // together; the ready ones in order are consumed, a step stops at the
-        // first inclusive prefix or the first unready granule (re-read next step)
-        for (int64_t j = ht - 1;;) {
-            uint64_t v[kLbWin];
+    // two-level look-back: the workgroups of a launch count at the same time,
+    // so a one-level chain of inclusive prefixes would advance a window of
+    // predecessors per round trip (~48 round trips for 763 workgroups).
+    // Instead: the sum of the earlier workgroups of this block of kLbBlk
+    // tickets, then of the earlier blocks' aggregates, which the last
+    // workgroup of each block publishes -- about 4 round trips.  Every wait is
+    // on lower tickets (running or done).
+    const int64_t blk = ht / kLbBlk, b0 = blk * kLbBlk;
+    lb_store(status + ht * 256 + d, lb_pack(epoch, kLbA, total));
+    auto sum_ready = [&](int64_t first, int cntw) -> uint32_t {   // granules [first, first + cntw) of digit d, waited for
+        uint32_t acc = 0;
+        uint32_t have = 0;   // bit i: granule i already summed
+        const uint32_t want = cntw >= 32 ? 0xffffffffu : ((1u << cntw) - 1u);
+        while (have != want) {
+            uint64_t v[kLbBlk];
 #pragma unroll
-            for (int i = 0; i < kLbWin; ++i) v[i] = j - i >= 0 ? lb_load(status + (j - i) * 256 + d) : lb_pack(epoch, kLbP, 0);
-            bool done = false;
-            int used = 0;
+            for (int i = 0; i < kLbBlk; ++i)
+                v[i] = i < cntw && !((have >> i) & 1u) ? lb_load(status + (first + i) * 256 + d) : 0ull;
 #pragma unroll
-            for (int i = 0; i < kLbWin; ++i) {
-                if (done || used < i || !lb_ready(v[i], epoch)) continue;
-                excl += (uint32_t)v[i];
-                used = i + 1;
-                done = ((v[i] >> 32) & 3u) == kLbP;
-            }
-            if (done) break;
-            j -= used;
-            if (used < kLbWin) __builtin_amdgcn_s_sleep(1);
+            for (int i = 0; i < kLbBlk; ++i)
+                if (i < cntw && !((have >> i) & 1u) && lb_ready(v[i], epoch)) {
+                    acc += (uint32_t)v[i];
+                    have |= 1u << i;
+                }
+            if (have != want) __builtin_amdgcn_s_sleep(1);
         }
-        lb_store(status + ht * 256 + d, lb_pack(epoch, kLbP, excl + total));
-    }
+        return acc;
+    };
+    const uint32_t local = sum_ready(b0, (int)(ht - b0));
+    if (ht - b0 == kLbBlk - 1) lb_store(status + (nhist + blk) * 256 + d, lb_pack(epoch, kLbA, local + total));
+    uint32_t excl = local;
+    for (int64_t q = 0; q < blk; q += kLbBlk) excl += sum_ready(nhist + q, (int)min<int64_t>(kLbBlk, blk - q));
     uint32_t run = excl;
 #pragma unroll
     for (int s = 0; s < kMaxSub; ++s) {
@@ -484,7 +509,7 @@ void launch_hist(Ctx &c, const KT *keys, int64_t n, int shift, int64_t ntiles, u
     c.slot[S_SORT_HIST].ensure((size_t)(ntiles + 1) * 256 * sizeof(uint32_t));
     *prefix = c.slot[S_SORT_HIST].as<uint32_t>();
     *base = *prefix + ntiles * 256;
-    const LbState lb = lb_prepare(c, nhist * 256);
+    const LbState lb = lb_prepare(c, (nhist + (nhist + kLbBlk - 1) / kLbBlk) * 256);
     KLAUNCH(sizeof(KT) == 1 ? "radix_hist_k1" : sizeof(KT) == 2 ? "radix_hist_k2" : sizeof(KT) == 4 ? "radix_hist_k4"
                                                                                         : "radix_hist_k8",
             (double)n * (double)sizeof(KT), k_hist_lb<KT>, dim3((unsigned)nhist), dim3(kBlock), 0,
