@@ -211,13 +211,8 @@ __global__ __launch_bounds__(kBlock) void k_hist_lb(const KT *__restrict__ keys,
     const int wv = threadIdx.x >> 6, d = threadIdx.x, lane = threadIdx.x & 63;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) h[w][d] = 0;
-    // D sub-tiles ahead in flight while one is counted: ~32 KB of loads per
-    // workgroup whatever the key width (one tile of 32-bit keys, four of bytes)
-    constexpr int D = NV >= 8 ? 1 : 8 / NV;
-    uint4 buf[D + 1][NV];
-#pragma unroll
-    for (int q = 0; q < D; ++q)
-        if (q < S && ht * S + q < ntiles) hist_load<KT>(keys, ht * S + q, n, vec, buf[q]);
+    // each sub-tile is loaded right before it is counted: a ring of
+    // prefetched sub-tiles ran slower (tools/hist_bench: 100M bytes 31 -> 50 us)
     __syncthreads();
     uint32_t cnt[kMaxSub];
     uint32_t total = 0;
@@ -226,8 +221,8 @@ __global__ __launch_bounds__(kBlock) void k_hist_lb(const KT *__restrict__ keys,
         cnt[s] = 0;
         const int64_t tile = ht * S + s;
         if (s >= S || tile >= ntiles) continue;   // uniform
-        if (s + D < S && tile + D < ntiles) hist_load<KT>(keys, tile + D, n, vec, buf[(s + D) % (D + 1)]);
-        uint4 (&cur)[NV] = buf[s % (D + 1)];
+        uint4 cur[NV];
+        hist_load<KT>(keys, tile, n, vec, cur);
         const int64_t b0 = tile * kSub;
         if (vec && b0 + kSub <= n) {
 #pragma unroll

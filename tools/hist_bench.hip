@@ -9,6 +9,7 @@
 //            the other lanes one by one
 //   run16 / runslice: runs of equal digits among a thread's consecutive keys
 //            (per 16-byte load / over the thread's contiguous slice) added once
+//   ring_run16: run16 with k_hist_lb's prefetch ring (one tile ahead)
 //   none   : the same loads, keys summed in a register (no counting): the
 //            read floor of this loop
 // Inputs: random bytes, and "runs" (bytes constant over runs of 4096 keys --
@@ -41,6 +42,52 @@ __global__ __launch_bounds__(kB) void k_count(const KT *__restrict__ keys, int64
     for (int w = 0; w < 4; ++w) h[w][d] = 0;
     __syncthreads();
     uint32_t acc = 0;
+    if constexpr (MODE == 7) {   // k_hist_lb's loop: one tile prefetched while one is counted
+        constexpr int D = NV >= 8 ? 1 : 8 / NV;
+        uint4 buf[D + 1][NV];
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(keys + ((int64_t)blockIdx.x * kS + q) * kSub);
+#pragma unroll
+            for (int i = 0; i < NV; ++i) buf[q][i] = src[i * kB + threadIdx.x];
+        }
+#pragma unroll
+        for (int s = 0; s < kS; ++s) {
+            const int64_t tile = (int64_t)blockIdx.x * kS + s;
+            if (tile >= ntiles) continue;
+            if (s + D < kS && tile + D < ntiles) {
+                const uint4 *src = reinterpret_cast<const uint4 *>(keys + (tile + D) * kSub);
+#pragma unroll
+                for (int i = 0; i < NV; ++i) buf[(s + D) % (D + 1)][i] = src[i * kB + threadIdx.x];
+            }
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                const KT *k = reinterpret_cast<const KT *>(&buf[s % (D + 1)][i]);
+                uint32_t run = (uint32_t)k[0] & 255u, rc = 1;
+#pragma unroll
+                for (int e = 1; e < VEC; ++e) {
+                    const uint32_t dg = (uint32_t)k[e] & 255u;
+                    if (dg != run) {
+                        atomicAdd(&h[wv][run], rc);
+                        run = dg;
+                        rc = 1;
+                    } else {
+                        ++rc;
+                    }
+                }
+                atomicAdd(&h[wv][run], rc);
+            }
+            __syncthreads();
+            uint32_t c = 0;
+            for (int w = 0; w < 4; ++w) {
+                c += h[w][d];
+                h[w][d] = 0;
+            }
+            out[tile * 256 + d] = c;
+            __syncthreads();
+        }
+        return;
+    }
     for (int s = 0; s < kS; ++s) {
         const int64_t tile = (int64_t)blockIdx.x * kS + s;
         if (tile >= ntiles) break;
@@ -158,10 +205,10 @@ void run(const char *tag, int64_t n, int runs, uint32_t *out, uint32_t *sink) {
     };
     const double ta = time(k_count<0, KT>), tm = time(k_count<1, KT>), tn = time(k_count<2, KT>),
                  tp1 = time(k_count<3, KT>), tp2 = time(k_count<4, KT>), tr5 = time(k_count<5, KT>),
-                 tr6 = time(k_count<6, KT>);
+                 tr6 = time(k_count<6, KT>), tr7 = time(k_count<7, KT>);
     std::printf("{\"keys\": \"%s\", \"n\": %lld, \"atom_us\": %.1f, \"match_us\": %.1f, \"none_us\": %.1f, "
-                "\"peel1_us\": %.1f, \"peel2_us\": %.1f, \"run16_us\": %.1f, \"runslice_us\": %.1f}\n",
-                tag, (long long)n, ta, tm, tn, tp1, tp2, tr5, tr6);
+                "\"peel1_us\": %.1f, \"peel2_us\": %.1f, \"run16_us\": %.1f, \"runslice_us\": %.1f, \"ring_run16_us\": %.1f}\n",
+                tag, (long long)n, ta, tm, tn, tp1, tp2, tr5, tr6, tr7);
     CK(hipFree(d));
 }
 
