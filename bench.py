@@ -240,7 +240,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=["auto"] + sorted(WORKLOADS), default="auto")
     ap.add_argument("--contig-bp", type=int, default=0, help="override every contig length (tests)")
-    ap.add_argument("--cpu-sample-bp", type=int, default=5_000_000)
+    ap.add_argument("--cpu-sample-bp", type=int, default=30_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-index", action="store_true", help="skip the FM index (scan-only step)")
     ap.add_argument("--no-fm", action="store_true", help="skip the all-motif FM search report")
