@@ -398,6 +398,16 @@ def main():
                         alg_bytes_per_launch=round(kbytes / launches), avg_launch_ms=round(kms / launches, 4),
                         launches_per_step=launches / a.steps,
                         share_of_device_time=round(kms / dev_ms, 4) if dev_ms else None)
+        # the write pattern's own ceiling, measured apart (tools/scatter_ceiling.hip): context for
+        # frac, which stays against the 8 TB/s HBM peak
+        ceil = os.path.join(REPO, "profiles", "r05", "scatter_ceiling_r05x.json")
+        if name in ("radix_scatter_kv8", "radix_partition_kv8") and os.path.exists(ceil):
+            with open(ceil) as f:
+                cj = json.load(f)
+            roofline["pattern_ceiling"] = dict(
+                unit="GB/s", copy=round(cj["copy_tbs"] * 1e3), runs32_xcd=round(cj["runs_skew_xcd_tbs"] * 1e3),
+                source="profiles/r05/scatter_ceiling_r05x.json: 1.6 GB per launch as a streaming copy, and as "
+                       "256 misaligned runs of 32 pairs per 8192-pair tile in the product's XCD tile order")
     # strict scan: the word compares k_runs (dense groups) and k_runs_sparse
     # (sampled groups) perform, over the time of both plus k_streak_end, against
     # the VALU issue ceiling; the all-words count only as a labelled reference

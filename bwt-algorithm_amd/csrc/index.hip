@@ -269,26 +269,28 @@ __global__ void k_kcompact(const uint8_t *__restrict__ t, int64_t n, const uint3
 
 // entries in position order: [first window at 0 if all k leading chars valid]
 // then every valid i >= k -> (window of the last k valid codes, i-k+1)
+// 16-bit codes (k <= 8): 6 bytes per entry written and per radix pass moved
+// (64-bit codes: 12), the layout of the ACGT path's k_kmer_dna
 __global__ void k_kentries(const uint8_t *__restrict__ t, int64_t n, int k, const uint32_t *__restrict__ vpos,
-                           const uint8_t *__restrict__ V, int first, uint64_t *__restrict__ keys,
+                           const uint8_t *__restrict__ V, int first, uint16_t *__restrict__ keys,
                            uint32_t *__restrict__ vals, uint32_t vbase_k) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     if (i == k - 1 && first) {
-        uint64_t w = 0;
+        uint32_t w = 0;
         for (int q = 0; q < k; ++q) w = (w << 2) | V[q];
-        keys[0] = w;
+        keys[0] = (uint16_t)w;
         vals[0] = 0;
     }
     if (i < k || kbits(t[i]) < 0) return;
     const int64_t v = vpos[i];
-    uint64_t w = 0;
+    uint32_t w = 0;
     for (int q = k - 1; q >= 0; --q) {
         const int64_t x = v - q;
         w = (w << 2) | (x >= 0 ? V[x] : 0u);
     }
     const int64_t e = (int64_t)first + (v - vbase_k);
-    keys[e] = w;
+    keys[e] = (uint16_t)w;
     vals[e] = (uint32_t)(i - k + 1);
 }
 
@@ -771,12 +773,13 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
         ix->has_kmer = true;
         KLAUNCH("k_kvalid", 0.0, k_kvalid, dim3(blocks(n)), dim3(256), 0, st, T, n, flag);
         exclusive_scan<uint32_t>(c, flag, head, n);   // head = vpos
-        uint32_t vk = 0, vkf = 0, vlast = 0, vlastf = 0;
-        HIPCHECK(hipMemcpyAsync(&vk, head + K - 1, 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipMemcpyAsync(&vkf, flag + K - 1, 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipMemcpyAsync(&vlast, head + n - 1, 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipMemcpyAsync(&vlastf, flag + n - 1, 4, hipMemcpyDeviceToHost, st));
+        uint32_t *mb = c.mailbox<uint32_t>(4);          // four reads, one wait
+        HIPCHECK(hipMemcpyAsync(mb + 0, head + K - 1, 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(mb + 1, flag + K - 1, 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(mb + 2, head + n - 1, 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(mb + 3, flag + n - 1, 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
+        const uint32_t vk = mb[0], vkf = mb[1], vlast = mb[2], vlastf = mb[3];
         const int64_t nvalid = (int64_t)vlast + vlastf;
         const int64_t valid_first = (int64_t)vk + vkf;   // valid among the first K chars
         const int first = valid_first == K ? 1 : 0;
@@ -784,13 +787,14 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
         uint8_t *V = (uint8_t *)gid;   // reuse: nvalid bytes <= 4n
         KLAUNCH("k_kcompact", 0.0, k_kcompact, dim3(blocks(n)), dim3(256), 0, st, T, n, head, V);
         ix->kmer_pos.ensure((size_t)std::max<int64_t>(nent, 1) * 4);
+        uint16_t *k16 = reinterpret_cast<uint16_t *>(keys);
         if (nent > 0) {
-            KLAUNCH("k_kentries", 0.0, k_kentries, dim3(blocks(n)), dim3(256), 0, st, T, n, K, head, V, first, keys,
+            KLAUNCH("k_kentries", 0.0, k_kentries, dim3(blocks(n)), dim3(256), 0, st, T, n, K, head, V, first, k16,
                                ix->kmer_pos.as<uint32_t>(), (uint32_t)valid_first);
-            radix_sort_pairs32(c, keys, ix->kmer_pos.as<uint32_t>(), nent, 0, 16);
+            radix_sort_pairs_k16(c, k16, ix->kmer_pos.as<uint32_t>(), nent, 0, 16);
         }
         ix->kmer_off.ensure((size_t)(65537) * 8);
-        KLAUNCH("k_kbounds", 0.0, k_kbounds<uint64_t>, dim3(blocks(65537)), dim3(256), 0, st, keys, nent,
+        KLAUNCH("k_kbounds", 0.0, k_kbounds<uint16_t>, dim3(blocks(65537)), dim3(256), 0, st, k16, nent,
                            ix->kmer_off.as<int64_t>());
         ix->kmer_count = nent;
     }

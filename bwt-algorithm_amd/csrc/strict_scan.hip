@@ -481,11 +481,59 @@ __device__ __forceinline__ int32_t smallest_period(const uint8_t *__restrict__ s
     return L;
 }
 
+// smallest_period of s[0, L) for L <= 32 in registers: the 32 bytes from
+// three aligned 16-byte loads (every device text carries 128 zero bytes of
+// padding: upload_text, the device loader),
+// and each divisor d <= 16 of L tested as one comparison of the byte string
+// with itself shifted by d (compile-time shifts): no chain of dependent byte
+// loads per divisor
+template <int D>
+__device__ __forceinline__ bool shift_equal(const uint64_t (&w)[6], int32_t L) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int32_t lo = 8 * q;   // bytes [lo, lo + 8) of s[D..] against the same of s[0..]
+        if (lo >= L - D) break;
+        constexpr int W = D / 8, B = 8 * (D % 8);
+        const uint64_t sh = B == 0 ? w[q + W] : (w[q + W] >> B) | (w[q + W + 1] << (64 - B));
+        const int32_t nb = min(8, L - D - lo);
+        const uint64_t m = nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1ull);
+        if ((sh ^ w[q]) & m) return false;
+    }
+    return true;
+}
+__device__ __forceinline__ int32_t period_le32(const uint8_t *__restrict__ t, int64_t start, int32_t L) {
+    const uintptr_t addr = (uintptr_t)(t + start);
+    const uint4 *a = reinterpret_cast<const uint4 *>(addr & ~(uintptr_t)15);
+    const int off = (int)(addr & 15);
+    const uint4 x0 = a[0], x1 = a[1], x2 = a[2];
+    const uint64_t v[6] = {(uint64_t)x0.x | (uint64_t)x0.y << 32, (uint64_t)x0.z | (uint64_t)x0.w << 32,
+                           (uint64_t)x1.x | (uint64_t)x1.y << 32, (uint64_t)x1.z | (uint64_t)x1.w << 32,
+                           (uint64_t)x2.x | (uint64_t)x2.y << 32, (uint64_t)x2.z | (uint64_t)x2.w << 32};
+    const int ws = off >> 3, bs = 8 * (off & 7);
+    uint64_t w[6];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {   // bytes [8q, 8q + 8) of s
+        const uint64_t lo = ws ? v[q + 1] : v[q], hi = ws ? v[q + 2] : v[q + 1];
+        w[q] = bs ? (lo >> bs) | (hi << (64 - bs)) : lo;
+    }
+    w[4] = w[5] = 0;
+    // bytes at or past L are not compared (masks), so what follows the unit is irrelevant
+#define BWTMI_PERIOD_TRY(D) \
+    if (D < L && L % D == 0 && shift_equal<D>(w, L)) return D;
+    BWTMI_PERIOD_TRY(1) BWTMI_PERIOD_TRY(2) BWTMI_PERIOD_TRY(3) BWTMI_PERIOD_TRY(4)
+    BWTMI_PERIOD_TRY(5) BWTMI_PERIOD_TRY(6) BWTMI_PERIOD_TRY(7) BWTMI_PERIOD_TRY(8)
+    BWTMI_PERIOD_TRY(9) BWTMI_PERIOD_TRY(10) BWTMI_PERIOD_TRY(11) BWTMI_PERIOD_TRY(12)
+    BWTMI_PERIOD_TRY(13) BWTMI_PERIOD_TRY(14) BWTMI_PERIOD_TRY(15) BWTMI_PERIOD_TRY(16)
+#undef BWTMI_PERIOD_TRY
+    return L;
+}
+
 // hits of unit length up to kThreadPeriodL get their period from one thread
 // (at most kThreadPeriodL - 1 divisor candidates over a few cached bytes);
 // longer units from one wave (k_period_wave): a thread walking a 1000-byte unit
 // byte by byte is a serial chain of loads that held every launch for ~2.6 ms
 constexpr int32_t kThreadPeriodL = 32;
+static_assert(kThreadPeriodL <= 32, "period_le32 holds 32 bytes of the unit");
 
 // compaction of the resolved hits, with the smallest period of each hit's
 // first unit and the count after primitive reduction (bwt.py:1956-1961)
@@ -521,7 +569,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t *__restrict__ ke
         hits[pos[k]] = h;
         return;
     }
-    const int32_t p = smallest_period(t + h.start, (int32_t)L);
+    const int32_t p = period_le32(t, h.start, (int32_t)L);
     h.prim_len = p;
     h.copies = p < L ? (h.end - h.start) / p : hit_c[k];
     hits[pos[k]] = h;
