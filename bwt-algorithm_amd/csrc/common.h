@@ -41,18 +41,34 @@ using HitVec = std::vector<bwtmi_hit, NoInit<bwtmi_hit>>;
 // lbits), lbits = the bits of the longest span -- when len and prim fit the
 // high half (32 B per hit on the device, 8 B over PCIe), else as two words
 // {start, len | prim << 32}.
+// a device download still landing in host memory (nested.hip): wait(k) returns
+// once hits [0, k) are there; the destructor waits for all of it
+struct Landing {
+    virtual ~Landing() = default;
+    virtual void wait(int64_t k) = 0;
+};
+
 struct ScreenedVec {
     std::vector<uint64_t, NoInit<uint64_t>> w;
     int32_t lbits = -1;   // one word per hit when >= 0
+    // the download into w, when it is still in flight: declared after w, so it
+    // is destroyed (and waited for) before w is freed
+    std::shared_ptr<Landing> landing;
     int64_t size() const { return lbits >= 0 ? (int64_t)w.size() : (int64_t)w.size() / 2; }
     bool empty() const { return w.empty(); }
+    // hits [0, k) readable
+    void wait(int64_t k) const {
+        if (landing) landing->wait(k);
+    }
     void clear() {
+        landing.reset();
         w.clear();
         lbits = -1;
     }
     void swap(ScreenedVec &o) noexcept {
         w.swap(o.w);
         std::swap(lbits, o.lbits);
+        landing.swap(o.landing);
     }
     // hit k: start, length, primitive motif length
     void get(int64_t k, int64_t &start, int64_t &len, int64_t &prim) const {

@@ -1501,6 +1501,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
             const ScreenedVec &sh = shits[(size_t)c];
             recs.resize(sh.size());   // NoInit: filled by fill_fn
             fill_fn = [&recs, &sh, c](int64_t a, int64_t b) {
+                sh.wait(b);   // the scan's download of these hits may still be landing
                 for (int64_t k = a; k < b; ++k) {
                     int64_t s0, len, prim;
                     sh.get(k, s0, len, prim);
@@ -1518,6 +1519,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
         if (scr && (size_t)c < shits.size()) {   // device-screened: compact records
             auto &sh = shits[(size_t)c];
             items.resize(sh.size());
+            sh.wait(sh.size());
             parallel_for((int64_t)sh.size(), nt, [&](int64_t a, int64_t b) {
                 for (int64_t k = a; k < b; ++k) {
                     int64_t s0, len, prim;

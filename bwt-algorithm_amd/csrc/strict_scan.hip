@@ -1295,16 +1295,20 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     const int64_t maxlen = (int64_t)mb[1];
     res.raw = nh;
     if (screen) {
+        // records c.ev1 behind its kernels; its hits download may still be landing
+        // (res.shits.wait), every kernel has finished
         screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.shits, maxlen);
-        if (c.timing) HIPCHECK(hipEventRecord(c.ev1, st));
+        if (c.timing && !res.shits.landing) HIPCHECK(hipEventRecord(c.ev1, st));
+        if (!res.shits.landing) scan_wait(st);
+        else if (c.timing) while (hipEventQuery(c.ev1) == hipErrorNotReady) __builtin_ia32_pause();
     } else {
         if (c.timing) HIPCHECK(hipEventRecord(c.ev1, st));
         res.hits.resize((size_t)nh);
         if (nh > 0)
             HIPCHECK(hipMemcpyAsync(res.hits.data(), c.slot[S_HITS].p, (size_t)nh * sizeof(bwtmi_hit),
                                     hipMemcpyDeviceToHost, st));
+        scan_wait(st);
     }
-    scan_wait(st);
     c.kresolve();
     if (c.timing) {
         float ms = 0;
