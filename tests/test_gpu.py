@@ -286,6 +286,32 @@ def test_device_screen_matches_host(gpu_ctx, case):
         assert _job_output(contigs, True, fmt="strfinder")[1] == _job_output(contigs, False, fmt="strfinder")[1]
 
 
+def test_screened_hits_landing_in_pieces(gpu_ctx):
+    """The scan returns while its screened-hit download is still landing (in
+    pieces, an event behind each; nested.hip).  A job reset or a rescan right
+    after the scan waits for it before the host buffer goes, and the
+    post-processing reads each piece only after it has landed: the output
+    equals the host screen's whatever happens in between."""
+    from bwtmi import _lib, synth
+    from bwtmi.records import Job
+    seq = synth.generate_contig(3_000_000, 11, 0.0)   # ~40 k kept hits: several pieces
+    want = _job_output([("contig1", seq)], False)[1]
+    j = Job(min_copies=3, show_progress=True)
+    j.add_contig("contig1", seq, 30, 30)
+    ctx = _lib.ctx()
+    j.scan(ctx)
+    j.reset()          # drops the landing buffer at once
+    j.scan(ctx)
+    j.scan(ctx)        # the second scan replaces a buffer still landing
+    j.postprocess()
+    assert j.render("strfinder") == want
+    del j              # a job freed right after its scan
+    j2 = Job(min_copies=3, show_progress=True)
+    j2.add_contig("contig1", seq, 30, 30)
+    j2.scan(ctx)
+    del j2
+
+
 def test_failing_contig_yields_error_and_no_records(gpu_ctx, golden_dir, tmp_path, capsys, monkeypatch):
     """The worker's failure convention (bwt.py:3137-3141): a contig whose device
     work fails is reported as `ERROR processing chromosome NAME: ...` and
