@@ -628,6 +628,7 @@ int bwtmi_job_load_fasta(bwtmi_job *job, const char *path, int32_t flank_trim) {
         CHECK_ARG(job && path, "null argument");
         TEXT_JOIN(job);
         load_fasta(job->j, path, flank_trim);
+        pool_spin_for_job(job->j);
     });
 }
 
@@ -726,6 +727,7 @@ int bwtmi_job_load_fasta_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *path, i
         device_wake(c);
         DevLoad dl(c, job);
         load_fasta(job->j, path, flank_trim, 1, 0, &dl);
+        pool_spin_for_job(job->j);
     });
 }
 
@@ -749,6 +751,7 @@ int bwtmi_job_load_fasta_shard(bwtmi_job *job, const char *path, int32_t flank_t
         CHECK_ARG(job && path && world >= 1 && rank >= 0 && rank < world, "bad argument");
         TEXT_JOIN(job);
         load_fasta(job->j, path, flank_trim, world, rank);
+        pool_spin_for_job(job->j);
     });
 }
 
@@ -790,6 +793,7 @@ int bwtmi_job_load_fasta_parts_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *p
         device_wake(c);
         DevLoad dl(c, job);
         fasta_load_parts(job->j, path, flank_trim, world, rank, blob, nwords, &dl);
+        pool_spin_for_job(job->j);
     });
 }
 
@@ -800,6 +804,7 @@ int bwtmi_job_load_fasta_parts(bwtmi_job *job, const char *path, int32_t flank_t
         CHECK_ARG(job && path && blob && nwords >= 6 && world >= 1 && rank >= 0 && rank < world, "bad argument");
         TEXT_JOIN(job);
         fasta_load_parts(job->j, path, flank_trim, world, rank, blob, nwords);
+        pool_spin_for_job(job->j);
     });
 }
 
@@ -934,6 +939,7 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
     return guard([&] {
         BWTMI_STAGE("bwtmi:scan");
         CHECK_ARG(ctx && job, "null argument");
+        pool_spin_for_job(job->j);
         auto t0 = std::chrono::steady_clock::now();
         job_upload(ctx, job);
         Job &J = job->j;
@@ -1167,6 +1173,7 @@ int bwtmi_job_postprocess(bwtmi_job *job) {
     return guard([&] {
         BWTMI_STAGE("bwtmi:postprocess");
         CHECK_ARG(job, "null argument");
+        pool_spin_for_job(job->j);
         TEXT_JOIN(job);
         Job &J = job->j;
         postprocess(J);
@@ -1179,6 +1186,7 @@ int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len) {
     return guard([&] {
         BWTMI_STAGE("bwtmi:write");
         CHECK_ARG(job && out && len, "null argument");
+        pool_spin_for_job(job->j);
         TEXT_JOIN(job);
         const std::vector<Text> parts = render_parts(job->j, fmt);
         std::vector<size_t> at(parts.size() + 1, 0);
@@ -1203,6 +1211,7 @@ int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path) {
     return guard([&] {
         BWTMI_STAGE("bwtmi:write");
         CHECK_ARG(job && path, "null argument");
+        pool_spin_for_job(job->j);
         TEXT_JOIN(job);
         OutFd out(path);
         const int fd = out.fd;
@@ -1268,6 +1277,7 @@ int bwtmi_job_render_units(bwtmi_job *job, int fmt, const int64_t *row_base, int
     return guard([&] {
         BWTMI_STAGE("bwtmi:write");
         CHECK_ARG(job && bytes, "null argument");
+        pool_spin_for_job(job->j);
         TEXT_JOIN(job);
         Job &J = job->j;
         render_rows(J, fmt, row_base, J.rendered);
@@ -1282,6 +1292,7 @@ int bwtmi_job_write_units(bwtmi_job *job, const char *path, const int64_t *offse
     return guard([&] {
         BWTMI_STAGE("bwtmi:write");
         CHECK_ARG(job && path && offsets, "null argument");
+        pool_spin_for_job(job->j);
         TEXT_JOIN(job);
         Job &J = job->j;
         Rendered &R = J.rendered;

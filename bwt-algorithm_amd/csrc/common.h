@@ -465,6 +465,10 @@ struct StageRange {
 extern std::atomic<int64_t> g_knobs[KN_COUNT];
 inline int64_t knob(Knob k) { return g_knobs[k].load(std::memory_order_relaxed); }
 inline bool stats_on(int level = 1) { return knob(KN_STATS) >= level; }
+// the pool's spin window when BWTMI_POOL_SPIN_US is -1 (auto), set from the
+// size of the job that calls in (post.cpp): short regions with short serial
+// gaps between them (a shard) keep their workers spinning longer
+void pool_spin_for_job(const Job &job);
 int64_t fasta_count_records(const char *path, int64_t limit);   // fasta.cpp
 // fn(task) for task in [0, n) on up to nt threads (dynamic scheduling)
 void run_tasks(int64_t n, int nt, const std::function<void(int64_t)> &fn);

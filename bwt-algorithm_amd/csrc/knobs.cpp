@@ -25,7 +25,7 @@ constexpr KnobDef kDefs[KN_COUNT] = {
     {"RUNS_DENSE", 0},          {"RUNS_UNTILED", 0},     {"SA_SMALL", 1},       {"SEG_LEVELS", 1},
     {"SCREEN_WIDE", 0},         {"FM_BYTES", 0},         {"LS_CAP", -1},        {"HOST_SCREEN", 0},
     {"NO_PLAIN", 0},            {"INDEX_LANES", 4},      {"SCAN_LANES", 4},     {"NO_AVX512", 0},
-    {"POOL_SPIN_US", 10},       {"UNIT_GROUP_THREADS", 4}, {"STATS", 0},        {"NUMA_BIND", 0},
+    {"POOL_SPIN_US", -1},       {"UNIT_GROUP_THREADS", 4}, {"STATS", 0},        {"NUMA_BIND", 0},
     {"NUMA_SMT", 0},            {"FAIL_MERGE_CHUNK", -1}, {"HIST_S", 0},
 };
 

@@ -245,12 +245,18 @@ namespace {
 // Region hand-off: a region is published by bumping `agen`; workers that
 // finished their last region may spin on it for a while (BWTMI_POOL_SPIN_US)
 // before they block on the condition variable, and the caller spins on
-// `apending` the same way before it blocks.  Default 10 us: it catches the
-// back-to-back regions of a step (alternating A/Bs on two boxes, r03aa/r03ab:
-// C3 +4 % on average, inside the run-to-run spread; W=8 shard step 8.0-8.1 vs
-// 8.6-8.9 ms), while a 60 us spin, also held through longer serial parts, cost
-// the C3 line ~7 % on another box (r03z).  0 = block at once.
-inline int64_t pool_spin_ns() { return knob(KN_POOL_SPIN_US) * 1000; }
+// `apending` the same way before it blocks.  10 us catches the back-to-back
+// regions of a step (r03aa/r03ab: C3 +4 %, W=8 shard step 8.0-8.1 vs 8.6-8.9
+// ms), while a 60 us spin, also held through longer serial parts, cost the C3
+// line ~7 % on another box (r03z).  Auto (-1, the default): 200 us while the
+// calling job holds <= 32 Mbp (its regions are short and come back to back:
+// W=8 shard 6.3-6.6 vs 6.8-7.3 ms at 10 us, r05gd), else 10 us (C3 within
+// its run-to-run spread either way).  0 = block at once.
+std::atomic<int64_t> g_auto_spin_ns{10000};
+inline int64_t pool_spin_ns() {
+    const int64_t k = knob(KN_POOL_SPIN_US);
+    return k >= 0 ? k * 1000 : g_auto_spin_ns.load(std::memory_order_relaxed);
+}
 inline int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -387,6 +393,13 @@ private:
 thread_local Pool *Pool::worker_of = nullptr;
 thread_local Pool *Pool::tl_pool = nullptr;
 }  // namespace
+
+void pool_spin_for_job(const Job &job) {
+    int64_t bases = 0;
+    for (size_t i = 0; i < job.contigs.size(); ++i)
+        if (job.selected.empty() || (i < job.selected.size() && job.selected[i])) bases += job.contigs[i].trimmed_len();
+    g_auto_spin_ns.store(bases <= 32000000 ? 200000 : 10000, std::memory_order_relaxed);
+}
 
 // fn(begin, end) over [0, n) in contiguous chunks
 template <class F>

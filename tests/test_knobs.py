@@ -86,12 +86,13 @@ def _post(contigs, threads):
 
 def test_unit_groups_and_pool_spin_switches(built_lib):
     """BWTMI_UNIT_GROUP_THREADS (threads per unit group of a multi-contig job)
-    and BWTMI_POOL_SPIN_US (0: workers block at once) change only the schedule."""
+    and BWTMI_POOL_SPIN_US (0: workers block at once; -1: by job size) change only
+    the schedule."""
     from bwtmi import _lib, synth
     contigs = [synth.generate_contig(60_000 + 7_000 * i, 50 + i, 0.02) for i in range(6)]
     want = _post(contigs, 8)
     for kv in ({"UNIT_GROUP_THREADS": 1}, {"UNIT_GROUP_THREADS": 16}, {"POOL_SPIN_US": 0},
-               {"POOL_SPIN_US": 500, "UNIT_GROUP_THREADS": 2}):
+               {"POOL_SPIN_US": 500, "UNIT_GROUP_THREADS": 2}, {"POOL_SPIN_US": -1}):
         with _lib.knobs(**kv):
             assert _post(contigs, 8) == want, kv
 
