@@ -117,6 +117,8 @@ _SIGS = {
     "bwtmi_job_load_fasta_shard": (C.c_int, [_P, C.c_char_p, C.c_int32, C.c_int32, C.c_int32]),
     "bwtmi_job_fasta_scan_part": (C.c_int, [_P, C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p),
                                             C.POINTER(C.c_int64)]),
+    "bwtmi_job_fasta_scan_part_dev": (C.c_int, [_P, _P, C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p),
+                                                C.POINTER(C.c_int64)]),
     "bwtmi_job_load_fasta_parts": (C.c_int, [_P, C.c_char_p, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int64]),
     "bwtmi_job_load_fasta_parts_dev": (C.c_int, [_P, _P, C.c_char_p, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int64]),
     "bwtmi_job_contig_weight": (C.c_int64, [_P, C.c_int32]),

@@ -156,7 +156,12 @@ class Job:
         elif world > 1 and comm is not None:
             from . import comm as _comm
             blob, nw = C.c_void_p(), C.c_int64()
-            check(lib().bwtmi_job_fasta_scan_part(self.h, path.encode(), world, rank, C.byref(blob), C.byref(nw)))
+            if dev_ctx is not None:   # the part's bytes go up to the device during the exchange
+                check(lib().bwtmi_job_fasta_scan_part_dev(dev_ctx, self.h, path.encode(), world, rank, C.byref(blob),
+                                                          C.byref(nw)))
+            else:
+                check(lib().bwtmi_job_fasta_scan_part(self.h, path.encode(), world, rank, C.byref(blob),
+                                                      C.byref(nw)))
             try:
                 mine = np.ctypeslib.as_array(C.cast(blob, C.POINTER(C.c_int64)), shape=(nw.value,)).copy()
             finally:

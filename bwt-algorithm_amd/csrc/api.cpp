@@ -643,13 +643,19 @@ struct DevLoad final : FastaDev {
     bwtmi_job *job;
     DevLoad(Ctx &c_, bwtmi_job *j) : c(c_), job(j) {}
     const char *img = nullptr;
+    bool preloaded = false;   // the image is the pass-1 part already queued to S_FASTA
     void image(const char *p, int64_t n) override {
         img = p;
-        if (n <= 0) return;
+        const Job &J = job->j;
+        preloaded = J.part_dev_tag != 0 && c.fasta_tag == J.part_dev_tag && p == J.part.data() &&
+                    n <= (int64_t)J.part.size();
+        if (!preloaded) c.fasta_tag = 0;   // S_FASTA gets other bytes
+        if (n <= 0 || preloaded) return;
         ensure_pinned(p, p, (size_t)n);
         c.slot[S_FASTA].ensure((size_t)n + 64);
     }
     void image_part(int64_t off, int64_t n) override {   // from the reading threads
+        if (preloaded) return;
         HIPCHECK(hipSetDevice(c.device));
         HIPCHECK(hipMemcpyAsync(c.slot[S_FASTA].as<char>() + off, img + off, (size_t)n, hipMemcpyHostToDevice,
                                 c.stream));
@@ -763,6 +769,42 @@ int bwtmi_job_fasta_scan_part(bwtmi_job *job, const char *path, int32_t world, i
         TEXT_JOIN(job);
         std::vector<int64_t> v;
         fasta_scan_part(job->j, path, world, rank, v);
+        auto *o = (int64_t *)std::malloc(std::max<size_t>(1, v.size()) * sizeof(int64_t));
+        if (!o) fail(BWTMI_E_NOMEM, "malloc");
+        std::memcpy(o, v.data(), v.size() * sizeof(int64_t));
+        *blob = o;
+        *nwords = (int64_t)v.size();
+    });
+}
+
+// pass 1 as above, and the part's bytes queued to ctx's FASTA image slot right
+// away: when this rank's contigs lie inside its part (equal contigs, one per
+// rank), pass 2 (bwtmi_job_load_fasta_parts_dev on the same ctx) finds its
+// image on the device and the copy has overlapped the part-table exchange
+int bwtmi_job_fasta_scan_part_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *path, int32_t world, int32_t rank,
+                                  int64_t **blob, int64_t *nwords) {
+    return guard([&] {
+        BWTMI_STAGE("bwtmi:load");
+        CHECK_ARG(ctx && job && path && blob && nwords && world >= 1 && rank >= 0 && rank < world, "bad argument");
+        TEXT_JOIN(job);
+        Ctx &c = ctx->c;
+        if (job->dev.bg_ctx && job->dev.bg_ctx != &c) ctx_wait(*job->dev.bg_ctx);
+        use(c);
+        // the previous part's copy (if any) has left job->j.part before it is overwritten
+        HIPCHECK(hipStreamSynchronize(c.stream));
+        std::vector<int64_t> v;
+        job->j.part_dev_tag = 0;
+        fasta_scan_part(job->j, path, world, rank, v);
+        const Seq &part = job->j.part;
+        if (!part.empty()) {
+            static std::atomic<uint64_t> tags{0};
+            const uint64_t tag = ++tags;
+            ensure_pinned(part.data(), part.data(), part.size());
+            c.slot[S_FASTA].ensure(part.size() + 64);
+            HIPCHECK(hipMemcpyAsync(c.slot[S_FASTA].p, part.data(), part.size(), hipMemcpyHostToDevice, c.stream));
+            c.fasta_tag = tag;
+            job->j.part_dev_tag = tag;
+        }
         auto *o = (int64_t *)std::malloc(std::max<size_t>(1, v.size()) * sizeof(int64_t));
         if (!o) fail(BWTMI_E_NOMEM, "malloc");
         std::memcpy(o, v.data(), v.size() * sizeof(int64_t));

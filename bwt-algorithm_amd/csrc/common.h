@@ -356,6 +356,9 @@ struct Job {
     Seq part;
     std::string part_path;
     int64_t part_a = 0, part_b = 0, part_stamp[2] = {-1, -1};
+    // pass 1 with a device (bwtmi_job_fasta_scan_part_dev): the part's bytes
+    // were queued to that context's FASTA image slot under this tag (0: not)
+    uint64_t part_dev_tag = 0;
     void assign_units();
     // host text written behind the device work (a whole-file load with device
     // placement, bwtmi_job_load_fasta_dev): every reader of contig bytes joins it

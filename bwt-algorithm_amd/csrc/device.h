@@ -187,6 +187,7 @@ struct Ctx {
     }
     DBuf slot[S_NSLOTS];
     DBuf lb_ticket;          // the look-back launches' tile ticket (radix.hip)
+    uint64_t fasta_tag = 0;  // what S_FASTA holds: a split loader's pass-1 part (its job's tag), 0 anything else
     uint32_t lb_epoch = 0;   // the last look-back launch's epoch
     HBuf host[4];
     // pinned mailbox of the scan's small device->host reads: the reads of one

@@ -367,6 +367,11 @@ int bwtmi_job_load_fasta_shard(bwtmi_job *job, const char *path, int32_t flank_t
  * Replaces load_reference (bwt.py:3713-3756) + the contig split of 3850-3912. */
 int bwtmi_job_fasta_scan_part(bwtmi_job *job, const char *path, int32_t world, int32_t rank, int64_t **blob,
                               int64_t *nwords);
+/* the same, and the part's bytes go up to ctx's device at once: a following
+ * bwtmi_job_load_fasta_parts_dev on that ctx whose contigs lie inside the part
+ * skips their copy (it overlapped the part-table exchange) */
+int bwtmi_job_fasta_scan_part_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *path, int32_t world, int32_t rank,
+                                  int64_t **blob, int64_t *nwords);
 /* header lines of a FASTA file ('>' at the start or after a line break),
  * counted up to limit; -1 if it cannot be read.  Host only (no device is
  * touched): the CLI's decision to launch one rank per GPU (bwt.py:3863-3864's

@@ -135,25 +135,33 @@ def test_device_load_scan_and_reload(gpu_ctx, tmp_path):
     assert outs[0] != outs[1]
 
 
-def _scan_part(job, path, world, rank):
+def _scan_part(job, path, world, rank, ctx=None):
     import ctypes as C
     from bwtmi._lib import check, lib
     blob, nw = C.c_void_p(), C.c_int64()
-    check(lib().bwtmi_job_fasta_scan_part(job.h, path.encode(), world, rank, C.byref(blob), C.byref(nw)))
+    if ctx is None:
+        check(lib().bwtmi_job_fasta_scan_part(job.h, path.encode(), world, rank, C.byref(blob), C.byref(nw)))
+    else:   # the part's bytes queued to ctx's device too
+        check(lib().bwtmi_job_fasta_scan_part_dev(ctx, job.h, path.encode(), world, rank, C.byref(blob),
+                                                  C.byref(nw)))
     try:
         return np.ctypeslib.as_array(C.cast(blob, C.POINTER(C.c_int64)), shape=(nw.value,)).copy()
     finally:
         lib().bwtmi_free(blob)
 
 
-def _split_job(path, world, rank, ctx, threads):
-    """Rank `rank` of a split load, the other ranks' part tables computed here."""
+def _split_job(path, world, rank, ctx, threads, pre_ctx=None, between=None):
+    """Rank `rank` of a split load, the other ranks' part tables computed here.
+    pre_ctx: pass 1 also queues the part to that context's device; between():
+    runs between the two passes (another load on the same context)."""
     import ctypes as C
     from bwtmi._lib import check, lib
     from bwtmi.records import Job
     parts = np.concatenate([_scan_part(Job(threads=threads), path, world, r) for r in range(world)])
     j = Job(threads=threads)
-    _scan_part(j, path, world, rank)   # this rank's pass-1 bytes, reused by its own contigs
+    _scan_part(j, path, world, rank, pre_ctx)   # this rank's pass-1 bytes, reused by its own contigs
+    if between is not None:
+        between()
     args = (j.h, path.encode(), 30, world, rank, parts.ctypes.data_as(C.c_void_p), parts.size)
     if ctx is None:
         check(lib().bwtmi_job_load_fasta_parts(*args))
@@ -182,6 +190,35 @@ def test_two_jobs_loaded_back_to_back_on_one_context(gpu_ctx, tmp_path):
         for cid in range(j.contig_count()):
             _, fl, tl, tr = j.contig_info(cid)
             assert j.device_text(gpu_ctx, cid) == j.contig_seq(cid)[tl:fl - tr], (j.names[cid])
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_split_load_part_preloaded_on_device(gpu_ctx, tmp_path, world):
+    """Pass 1 with a device queues the part's bytes to the context's FASTA image
+    slot, and pass 2 on that context skips their copy when its contigs lie
+    inside the part (equal contigs, one per rank) -- also when another job's
+    load on the same context overwrote the slot in between (pass 2 copies
+    again): the device texts equal the host split load's."""
+    from bwtmi import synth
+    from bwtmi.records import Job
+    path = str(tmp_path / "eq.fa")
+    synth.write_fasta(path, [300_000] * world, 0.0, first_index=3)
+    other = str(tmp_path / "other.fa")
+    synth.write_fasta(other, [200_000, 50_000], 0.0, first_index=40, gaps="n2")
+
+    def clobber():
+        Job().load_fasta(other, 30, dev_ctx=gpu_ctx)
+
+    for rank in range(world):
+        h = _split_job(path, world, rank, None, 8)
+        for between in (None, clobber):
+            d = _split_job(path, world, rank, gpu_ctx, 8, pre_ctx=gpu_ctx, between=between)
+            assert d.names == h.names
+            own = [i for i in range(h.contig_count()) if h.contig_info(i)[1] > 0]
+            assert own
+            for cid in own:
+                _, fl, tl, tr = d.contig_info(cid)
+                assert d.device_text(gpu_ctx, cid) == h.contig_seq(cid)[tl:fl - tr], (rank, cid, between)
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])
