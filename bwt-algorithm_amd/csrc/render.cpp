@@ -673,9 +673,10 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
     // ids are row_base[unit] + rank within the unit (global index when the
     // caller renders only its own shard), else the local index
     const int64_t n = (int64_t)rows.size();
-    // >= 4 chunks per thread while that keeps them >= 1024 rows (a 40k-row shard
-    // in 8192-row chunks kept 5 of 16 threads busy)
-    const int64_t CH = std::max<int64_t>(1024, std::min<int64_t>(8192, n / (4 * (int64_t)host_threads(job.params)) + 1));
+    // >= 8 chunks per thread while that keeps them >= 256 rows (a 40k-row shard
+    // in 8192-row chunks kept 5 of 16 threads busy; in 1024-row chunks, 2 or 3
+    // chunks a thread, the last wave left threads idle)
+    const int64_t CH = std::max<int64_t>(256, std::min<int64_t>(8192, n / (8 * (int64_t)host_threads(job.params)) + 1));
     auto unit_of = [&](int64_t k) { return rows[(size_t)k].unit; };
     struct Chunk { int64_t a, b, id0; int32_t unit; };
     std::vector<Chunk> chunks;
