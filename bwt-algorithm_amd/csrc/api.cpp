@@ -672,6 +672,7 @@ struct DevLoad final : FastaDev {
         for (size_t i = 0; i < J.contigs.size(); ++i) {
             const Contig &ct = J.contigs[i];
             DevContig &dc = d.seqs[i];
+            if (!J.selected.empty() && (i >= J.selected.size() || !J.selected[i])) continue;   // another rank's contig
             const int64_t tn = ct.trimmed_len();
             if (dc.n == tn && dc.gen == ct.gen) continue;   // on the device already (not in this file)
             if (!ct.full.empty()) ensure_pinned(ct.full.data(), ct.full.data(), ct.full.size());

@@ -367,6 +367,8 @@ void load_fasta(Job &job, const char *path, int32_t flank_trim, int32_t world, i
         std::fill(mine.begin(), mine.end(), 0);
         for (int32_t c : shard_units(job, world, rank)) mine[(size_t)c] = 1;
         job.selected.assign(mine.begin(), mine.end());
+    } else {
+        job.selected.clear();   // a whole load: every contig (a restriction from an earlier shard load goes)
     }
     // buffers (allocation only; pass 2 fills them in parallel)
     std::vector<char *> base(job.contigs.size(), nullptr);
@@ -735,6 +737,8 @@ void fasta_load_parts(Job &job, const char *path, int32_t flank_trim, int32_t wo
         std::fill(mine.begin(), mine.end(), 0);
         for (int32_t c : shard_units(job, world, rank)) mine[(size_t)c] = 1;
         job.selected.assign(mine.begin(), mine.end());
+    } else {
+        job.selected.clear();   // a whole load: every contig (a restriction from an earlier shard load goes)
     }
     const auto t1 = clk::now();
     Fd f(path);

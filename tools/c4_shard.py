@@ -65,7 +65,8 @@ def main():
     for W, T in [(w, t) for w in worlds for t in tlist]:
         ranks = [int(x) for x in os.environ["C4_SHARD_RANKS"].split(",")] if os.environ.get("C4_SHARD_RANKS") else range(W)
         for r in ranks:             # every rank of the world: the worst one sets the projection
-            job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True, build_index=True,
+            job = Job(min_copies=3, max_unit_len=120, show_progress=True, tier2=True,
+                      build_index=os.environ.get("C4_SHARD_INDEX", "1") == "1",   # 0: what the index costs the host stages
                       sa_sample=32, threads=T)
 
             calls = {}
