@@ -179,6 +179,36 @@ def generate_contig(length: int, index: int, sub_rate: float = 0.0,
     return seq.tobytes()
 
 
+def shared_prefix_runs(alphabet: bytes = b"ACGT", seed: int = 1,
+                       run_lengths: Iterable[int] = tuple(range(16, 34)) + (40, 48, 63, 64, 65, 100),
+                       prefix_lengths: Iterable[int] = (16, 32, 48, 64)) -> bytes:
+    """A suffix-sort stress text: for every run symbol c, run length r and
+    prefix length p, one random p-base prefix Z (not ending in c) is repeated
+    with c^r and then every other symbol x, each copy followed by its own
+    random tail -- Z c^r x W.  Two such suffixes share p + r symbols, differ at
+    x, and their tails W order them the other way about half of the time, so a
+    sort that treats the run's rank as resolving more symbols than it does
+    (h-prefix claims of the doubling rounds) orders them by W.  Real genomes
+    hold the same pattern: near-identical repeat copies followed by poly-A
+    tails of equal length."""
+    rng = _Stream(_mix_int(SEED_BASE ^ 0x5A11 ^ seed))
+
+    def rnd(k: int, avoid_last: int = -1) -> bytes:
+        b = bytearray(alphabet[rng.below(len(alphabet))] for _ in range(k))
+        while k and b[-1] == avoid_last:
+            b[-1] = alphabet[rng.below(len(alphabet))]
+        return bytes(b)
+    parts = [rnd(64)]
+    for c in alphabet:
+        for r in run_lengths:
+            for p in prefix_lengths:
+                z = rnd(p, c)
+                for x in alphabet:
+                    if x != c:
+                        parts.append(z + bytes([c]) * r + bytes([x]) + rnd(24))
+    return b"".join(parts)
+
+
 def format_fasta_record(name: str, seq: bytes, width: int = 60) -> bytes:
     arr = np.frombuffer(seq, dtype=np.uint8)
     full = len(arr) // width

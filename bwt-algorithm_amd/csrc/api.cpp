@@ -791,10 +791,9 @@ int bwtmi_job_fasta_scan_part_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *pa
         Ctx &c = ctx->c;
         if (job->dev.bg_ctx && job->dev.bg_ctx != &c) ctx_wait(*job->dev.bg_ctx);
         use(c);
-        // the previous part's copy (if any) has left job->j.part before it is overwritten
-        HIPCHECK(hipStreamSynchronize(c.stream));
+        // the previous part's copy (if any, on whichever context) has left
+        // job->j.part before pass 1 overwrites it (fasta_scan_part settles it)
         std::vector<int64_t> v;
-        job->j.part_dev_tag = 0;
         fasta_scan_part(job->j, path, world, rank, v);
         const Seq &part = job->j.part;
         if (!part.empty()) {
@@ -803,6 +802,13 @@ int bwtmi_job_fasta_scan_part_dev(bwtmi_ctx *ctx, bwtmi_job *job, const char *pa
             ensure_pinned(part.data(), part.data(), part.size());
             c.slot[S_FASTA].ensure(part.size() + 64);
             HIPCHECK(hipMemcpyAsync(c.slot[S_FASTA].p, part.data(), part.size(), hipMemcpyHostToDevice, c.stream));
+            hipEvent_t ev;
+            HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            HIPCHECK(hipEventRecord(ev, c.stream));
+            job->j.part_inflight = [ev] {   // an event wait needs no current device
+                (void)hipEventSynchronize(ev);
+                (void)hipEventDestroy(ev);
+            };
             c.fasta_tag = tag;
             job->j.part_dev_tag = tag;
         }

@@ -357,8 +357,20 @@ struct Job {
     std::string part_path;
     int64_t part_a = 0, part_b = 0, part_stamp[2] = {-1, -1};
     // pass 1 with a device (bwtmi_job_fasta_scan_part_dev): the part's bytes
-    // were queued to that context's FASTA image slot under this tag (0: not)
+    // were queued to that context's FASTA image slot under this tag (0: not),
+    // and part_inflight waits for that copy; every path that rewrites or frees
+    // `part` settles first (a host pass 1 on another file or rank
+    // kept the tag, and the copy could still be reading the old bytes)
     uint64_t part_dev_tag = 0;
+    std::function<void()> part_inflight;
+    void part_settle() {
+        part_dev_tag = 0;
+        if (part_inflight) {
+            std::function<void()> f = std::move(part_inflight);
+            part_inflight = nullptr;
+            f();
+        }
+    }
     void assign_units();
     // host text written behind the device work (a whole-file load with device
     // placement, bwtmi_job_load_fasta_dev): every reader of contig bytes joins it
@@ -387,6 +399,7 @@ struct Job {
     Job &operator=(const Job &) = delete;
     ~Job() {
         if (text_th.joinable()) text_th.join();
+        part_settle();   // `part` is freed with the job
     }
 };
 

@@ -612,6 +612,7 @@ void fasta_scan_part(Job &job, const char *path, int32_t world, int32_t rank, st
     const int64_t N = f.size();
     const int64_t A = line_start_from(f.fd, N, N * rank / world), B = line_start_from(f.fd, N, N * (rank + 1) / world);
     Seq &part = job.part;
+    job.part_settle();   // a device copy of the previous part has left it; its tag no longer names these bytes
     char *p = part.resize_uninit((size_t)std::max<int64_t>(0, B - A));
     job.part_path = path;
     job.part_a = A;

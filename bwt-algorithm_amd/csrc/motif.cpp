@@ -421,11 +421,15 @@ __attribute__((target("avx512f,avx512bw,avx512vl"))) static int dp_rows_avx512(
     return 1;
 }
 
-static const bool g_avx512 = [] {
+// the CPU feature test is cached; the switch is read at every call (a
+// namespace-scope initialiser could run before knobs.cpp has read the
+// environment, and bwtmi_knob_set must take effect in-process)
+static const bool g_cpu_avx512 = [] {
     __builtin_cpu_init();
-    return !knob(KN_NO_AVX512) && __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+    return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
            __builtin_cpu_supports("avx512vl");
 }();
+static inline bool use_avx512() { return g_cpu_avx512 && !knob(KN_NO_AVX512); }
 
 // ops of one copy are formatted with a placeholder-free prefix; the copy index
 // is prepended when the copy is accepted (ops hold "pos:..." pieces)
@@ -447,7 +451,7 @@ bool align_unit(const char *motif, int64_t m, const char *win, int64_t n, int64_
     const size_t cells = (size_t)((m + 1) * W) + 32;
     if (S.ptr.size() < cells) S.ptr.resize(cells);
     const int32_t reject = (int32_t)(tol + 2 * max_indel);
-    if (g_avx512 && W <= 31 && INF < 30000) {
+    if (use_avx512() && W <= 31 && INF < 30000) {
         // 64 bytes of never-matching padding on both sides of the window
         if (S.wpad.size() < (size_t)(n + 128)) S.wpad.resize((size_t)(n + 128));
         std::memset(S.wpad.data(), 0xff, 64);

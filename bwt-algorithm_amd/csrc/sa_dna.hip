@@ -641,12 +641,26 @@ __global__ __launch_bounds__(kB) void k_dna_classify(const uint32_t *__restrict_
 // N runs of an assembly).  Their order is known in closed form instead: a
 // deep suffix is c^r X with X[0] != c (r = symbols to the run's end); every
 // one whose X[0] < c sorts before every one whose X[0] > c (b = 0 / 1), then
-// b = 0 by r ascending, b = 1 by r descending, then by X.  So the first round
-// (h = 16) sorts deep groups by (b, +-r) and every later round by rank[a + r]
-// -- the current rank of X, a coarsening of its final rank -- instead of
-// rank[a + h]; deep groups hold only deep suffixes (their 16-prefix is c^16),
-// so every group is keyed one way.  re[a >> 4] = the end of the run holding
-// position 16 (a >> 4) + 15, which lies inside a's run whenever a is deep.
+// b = 0 by r ascending, b = 1 by r descending, then by X.
+// The doubling invariant must hold for every group, deep or not: after the
+// round with h, the members of a group share their first 2h symbols, because
+// other suffixes read a group's rank through rank[a + h] as standing for h
+// symbols in the next round.  A (b, r) group shares exactly r symbols, so:
+//   round h = 16 (the c^16 group [gs, gs + gsz)): members with r >= 32 get
+//     gs + (r - 32) (b = 0) or gs + gsz - 1 - (r - 32) (b = 1) -- inside the
+//     group's own SA range, b = 0 below b = 1 (the group holds R - 15 members
+//     per run of length R, so the two ranges never meet); members with
+//     r < 32 keep rank[a + 16], which already falls below gs (b = 0) or at or
+//     after gs + gsz (b = 1);
+//   rounds h >= 32 (groups are uniform in r from here on): rank[a + r] -- the
+//     rank of X, h symbols of it -- while r >= h (r + h >= 2h symbols), and
+//     rank[a + h] once r < h.
+// (Round 5 keyed every run member by (b, r) and then rank[a + r] whatever r
+// was: a (b, r) group with r < 2h then claimed 2h symbols, and Z c^r x W
+// against Z c^r y V with |Z| = h tied and skipped x)
+// Deep groups hold only deep suffixes (their 16-prefix is c^16), so every
+// group is keyed one way.  re[a >> 4] = the end of the run holding position
+// 16 (a >> 4) + 15, which lies inside a's run whenever a is deep.
 struct Deep {
     const uint64_t *P;    // packed text (2-bit bases, or 4-bit symbol codes when small)
     const uint32_t *re;   // run end per 16-position block (valid for deep suffixes' blocks)
@@ -671,11 +685,11 @@ __device__ __forceinline__ int sym_at(const Deep &d, int64_t i) {
     return d.small ? (int)((d.P[i >> 4] >> (60 - 4 * (i & 15))) & 15u) : (int)base_code(d.P, i);
 }
 
-// the doubling key of member v: rank of the suffix h bases on (a group member
-// always has more than h bases before '$': its h-prefix is shared); deep
-// suffixes: (b, +-r) in the first round, then the rank of their run's end
+// the doubling key of member v of the group [gs, gs + gsz): rank of the suffix
+// h bases on (a group member always has more than h bases before '$': its
+// h-prefix is shared); deep suffixes as above
 __device__ __forceinline__ uint32_t ls_key(const uint32_t *__restrict__ rank, uint32_t v, int64_t n, int64_t h,
-                                          const Deep &d) {
+                                          const Deep &d, uint32_t gs, uint32_t gsz) {
     const int64_t a = v & kPosMask;
     if (d.on && a + 16 < n) {
         const int c = homopolymer16(d, a);
@@ -683,10 +697,13 @@ __device__ __forceinline__ uint32_t ls_key(const uint32_t *__restrict__ rank, ui
             const int64_t e = d.re[a >> 4];   // first position past the run (<= n - 1: '$' ends every run)
             const int64_t r = e - a;
             if (h == 16) {
-                const bool b = e < n - 1 && sym_at(d, e) > c;
-                return b ? (1u << 29) | (uint32_t)(kPosMask - r) : (uint32_t)r;
+                if (r >= 32) {
+                    const bool b = e < n - 1 && sym_at(d, e) > c;
+                    return b ? gs + gsz - 1u - (uint32_t)(r - 32) : gs + (uint32_t)(r - 32);
+                }
+            } else if (r >= h) {
+                return rank[e];
             }
-            return rank[e];
         }
     }
     return a + h < n ? rank[a + h] : 0u;
@@ -786,7 +803,7 @@ __global__ __launch_bounds__(kLB) void k_ls_wave(const uint32_t *__restrict__ st
     }
     const bool live = kk < (int)sz;
     const uint32_t orig = live ? vals[s + kk] : 0u;
-    uint64_t x = live ? ((uint64_t)ls_key(rank, orig, n, h, dp) << 32) | orig : ~0ull;
+    uint64_t x = live ? ((uint64_t)ls_key(rank, orig, n, h, dp, s, sz) << 32) | orig : ~0ull;
 #pragma unroll
     for (int k2 = 2; k2 <= W; k2 <<= 1)
 #pragma unroll
@@ -826,7 +843,7 @@ __global__ __launch_bounds__(kWB) void k_ls_block(const uint32_t *__restrict__ s
     uint32_t p2 = 1;
     while (p2 < sz) p2 <<= 1;
     const uint32_t orig = t < (int)sz ? vals[s + t] : 0u;
-    if (t < (int)p2) x[t] = t < (int)sz ? ((uint64_t)ls_key(rank, orig, n, h, dp) << 32) | orig : ~0ull;
+    if (t < (int)p2) x[t] = t < (int)sz ? ((uint64_t)ls_key(rank, orig, n, h, dp, s, sz) << 32) | orig : ~0ull;
     __syncthreads();
     for (uint32_t k2 = 2; k2 <= p2; k2 <<= 1)
         for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
@@ -891,7 +908,7 @@ __global__ __launch_bounds__(kB) void k_dna_refine_keys(const uint32_t *__restri
     const uint32_t s = starts[q], sz = sizes[q], at = offs[q];
     for (uint32_t k = blockIdx.x * kB + threadIdx.x; k < sz; k += gridDim.x * kB) {
         const uint32_t v = vals[s + k];
-        rk[at + k] = ((uint64_t)q << 30) | ls_key(rank, v, n, h, dp);
+        rk[at + k] = ((uint64_t)q << 30) | ls_key(rank, v, n, h, dp, s, sz);
         rv[at + k] = v;
     }
 }

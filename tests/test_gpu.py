@@ -566,6 +566,25 @@ def test_long_runs_ordered_in_closed_form_vs_oracle(gpu_ctx, alpha):
     _check_index(bytes([alpha[2]]) * 17 + bytes([alpha[0]]) * 33 + b"$")
 
 
+@pytest.mark.parametrize("alpha", [b"ACGT", b"ACGTNRY"])
+def test_runs_after_shared_prefixes_vs_oracle(gpu_ctx, alpha):
+    """Repeated 16-64-symbol prefixes followed by equal runs of 16-100 symbols
+    and different next symbols on the same side of the run's symbol
+    (bwtmi.synth.shared_prefix_runs): Z c^r x W.  The run's closed-form rank
+    must never stand for more symbols than a doubling round claims -- with
+    r < 2h a (b, r) group holds suffixes that differ inside the 2h-prefix, and
+    a suffix Z... reading it through rank[a + h] would tie with its twin and
+    skip x (sa_dna.hip ls_key).  Against the oracle; the 1 Mbp copy
+    takes the partitioned first ranks and the segmented refinement rounds."""
+    from bwtmi import synth
+    _check_index(synth.shared_prefix_runs(alpha, 1) + b"$")
+    _check_index(synth.shared_prefix_runs(alpha, 2, run_lengths=(16, 17, 20, 31, 32, 33),
+                                          prefix_lengths=(32, 64)) * 3 + b"$")
+    big = b"".join(synth.shared_prefix_runs(alpha, s, run_lengths=(16, 24, 31, 40, 63), prefix_lengths=(32, 64))
+                   for s in range(3, 40))
+    _check_index(big[:1_000_000] + b"$")
+
+
 @pytest.mark.parametrize("S", [1, 3, 16])
 def test_radix_histogram_geometries(gpu_ctx, S):
     """The single-pass radix histogram with 1, 3 or 16 scatter tiles per
