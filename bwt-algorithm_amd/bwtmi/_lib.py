@@ -102,11 +102,9 @@ _SIGS = {
     "bwtmi_job_export": (C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
     "bwtmi_job_import": (C.c_int, [_P, _P, C.c_int64]),
     "bwtmi_job_stage_ms": (C.c_int, [_P, C.POINTER(C.c_double)]),
-"bwtmi_align_region": (C.c_int, [C.c_char_p, C.c_int64, C.c_int64, C.c_int64, C.c_char_p, C.c_int64,
+    "bwtmi_align_region": (C.c_int, [C.c_char_p, C.c_int64, C.c_int64, C.c_int64, C.c_char_p, C.c_int64,
                                      C.c_double, C.c_int64, C.c_int64, _P, C.POINTER(C.c_double), _P,
                                      C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
-    "bwtmi_align_regions": (C.c_int, [_P, C.c_char_p, C.c_int64, _P, C.c_int64, C.c_int64, _P,
-                                      C.POINTER(C.c_void_p), _P]),
     "bwtmi_job_load_fasta": (C.c_int, [_P, C.c_char_p, C.c_int32]),
     "bwtmi_job_load_fasta_dev": (C.c_int, [_P, _P, C.c_char_p, C.c_int32]),
     "bwtmi_job_device_text": (C.c_int, [_P, _P, C.c_int32, C.c_void_p]),
@@ -292,36 +290,6 @@ def kernel_stats(h, enable: bool = True, reset: bool = True) -> dict:
     for line in buf.value.decode().splitlines():
         name, ms, n, b = line.split()
         out[name] = (float(ms), int(n), float(b))
-    return out
-
-
-def align_regions(h, seq: bytes, regions, min_copies: int):
-    """_recompute_repeat's alignment (bwt.py:3530-3534) of (start, end, m) regions of
-    seq on the device (csrc/recompute.hip): per region None or (copies, consumed,
-    max_errors, tot_ins, tot_del, tot_err, consensus, variations, on_device)."""
-    import numpy as np
-    args = np.ascontiguousarray(np.asarray(regions, dtype=np.int64).reshape(-1, 3))
-    n = args.shape[0]
-    ints = np.zeros((n, 8), dtype=np.int64)
-    off = np.zeros(n + 1, dtype=np.int64)
-    strs = C.c_void_p()
-    check(lib().bwtmi_align_regions(h, seq, len(seq), args.ctypes.data, n, min_copies, ints.ctypes.data,
-                                    C.byref(strs), off.ctypes.data))
-    try:
-        blob = C.string_at(strs, int(off[-1])) if off[-1] else b""
-    finally:
-        if strs:
-            lib().bwtmi_free(strs)
-    out = []
-    for k in range(n):
-        r = ints[k].tolist()
-        if not r[0]:
-            out.append(None)
-            continue
-        m = int(args[k, 2])
-        s = blob[off[k]:off[k + 1]]
-        out.append((r[1], r[2], r[3], r[4], r[5], r[6], s[:m].decode("latin-1"), s[m:].decode("latin-1"),
-                    bool(r[7])))
     return out
 
 

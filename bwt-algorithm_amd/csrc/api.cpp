@@ -1572,62 +1572,4 @@ int bwtmi_align_region(const char *seq, int64_t seq_len, int64_t start, int64_t 
     return rc ? rc : found;
 }
 
-int bwtmi_align_regions(bwtmi_ctx *ctx, const char *seq, int64_t seq_len, const int64_t *args, int64_t nreq,
-                        int64_t min_copies, int64_t *ints8, char **strings, int64_t *str_off) {
-    return guard([&] {
-        CHECK_ARG(ctx && (seq || seq_len == 0) && seq_len >= 0 && (args || nreq == 0) && nreq >= 0 && ints8 &&
-                      strings && str_off, "bad argument");
-        *strings = nullptr;
-        Ctx &c = use(ctx->c);
-        DBuf &tb = c.slot[S_MISC3];
-        tb.ensure((size_t)seq_len + 64);
-        if (seq_len) HIPCHECK(hipMemcpyAsync(tb.p, seq, (size_t)seq_len, hipMemcpyHostToDevice, c.stream));
-        std::vector<RcReq> req((size_t)nreq);
-        const int32_t mc = (int32_t)std::max<int64_t>(1, min_copies);
-        for (int64_t k = 0; k < nreq; ++k) {
-            const int64_t m = args[3 * k + 2];
-            CHECK_ARG(m >= 1 && m <= INT32_MAX, "bad motif length");
-            req[(size_t)k] = RcReq{tb.as<char>(), seq_len, args[3 * k], args[3 * k + 1], (int32_t)m, mc};
-        }
-        std::vector<RcOut> out((size_t)nreq);
-        std::vector<char> arena;
-        recompute_batch_device(c, req.data(), nreq, out.data(), arena);
-        std::string all;
-        str_off[0] = 0;
-        AlignSummary s;
-        s.want_copies = false;
-        for (int64_t k = 0; k < nreq; ++k) {
-            const RcOut &o = out[(size_t)k];
-            int64_t *r = ints8 + 8 * k;
-            std::fill(r, r + 8, 0);
-            if (o.status >= 0) {
-                r[7] = 1;
-                if (o.status == 1) {
-                    r[0] = 1; r[1] = o.copies; r[2] = o.consumed; r[3] = o.max_err;
-                    r[4] = o.tot_ins; r[5] = o.tot_del; r[6] = o.tot_err;
-                    all.append(arena.data() + o.str_off, (size_t)o.str_len);
-                }
-            } else {   // past a device bound: the host alignment, both attempts
-                const RcReq &q = req[(size_t)k];
-                const int64_t a = std::max<int64_t>(0, q.start);
-                const std::string tmpl(seq + std::min(a, seq_len), (size_t)std::max<int64_t>(0, std::min<int64_t>(q.m, seq_len - a)));
-                bool ok = align_repeat_region(seq, seq_len, q.start, q.end, tmpl, mc, s);
-                if (!ok) ok = align_repeat_region(seq, seq_len, q.start, q.end, tmpl, 1, s);
-                if (ok) {
-                    r[0] = 1; r[1] = s.copies; r[2] = s.consumed; r[3] = s.max_errors;
-                    r[4] = s.tot_ins; r[5] = s.tot_del; r[6] = s.tot_err;
-                    all += s.consensus;
-                    all += s.variations;
-                }
-            }
-            str_off[k + 1] = (int64_t)all.size();
-        }
-        char *v = (char *)std::malloc(all.size() + 1);
-        if (!v) fail(BWTMI_E_NOMEM, "out of host memory");
-        std::memcpy(v, all.data(), all.size());
-        v[all.size()] = 0;
-        *strings = v;
-    });
-}
-
 }  // extern "C"

@@ -250,22 +250,6 @@ bool align_repeat_region(const char *seq, int64_t seq_len, int64_t start, int64_
                          const std::string &tmpl, int64_t min_copies, AlignSummary &out, double frac,
                          int64_t max_indel_arg, AlignScratch *ws, bool resume = false);
 
-// _recompute_repeat's alignment (bwt.py:3530-3534: align_repeat_region with
-// min_copies, then with 1) of a batch of regions on the device (recompute.hip)
-struct RcReq {
-    const char *text;             // device copy of the contig's trimmed sequence
-    int64_t text_len, start, end;  // start / end as align_repeat_region receives them
-    int32_t m, min_copies;         // template = text[start, start + m), 2 <= m <= kRcMaxMotif
-};
-struct RcOut {
-    int32_t status;    // 1 aligned, 0 neither attempt aligned, -1 past a device bound (host recomputes)
-    int32_t str_len;   // consensus (m bytes) then the variations, at arena[str_off]
-    int64_t str_off;
-    int64_t copies, consumed;
-    int32_t tot_err, max_err, tot_ins, tot_del;
-};
-constexpr int32_t kRcMaxMotif = 256;
-// runs a batch to completion: out[k] for every req[k], strings into arena
 
 // ---------------------------------------------------------------- job
 // formatted text in cached huge-page blocks (mem.h); the formatters write

@@ -327,10 +327,6 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
 void strict_scan_mm_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
                            int32_t max_mismatch, int32_t min_copies, HitVec &hits);
 
-// ----- the merge fold's DP recomputes, one wavefront per region (recompute.hip);
-// returns after the batch completed (out[] and arena on the host)
-void recompute_batch_device(Ctx &c, const RcReq *req, int64_t nreq, RcOut *out, std::vector<char> &arena);
-
 // ----- nested suppression / sort / dedup of one contig's strict hits (nested.hip)
 // maxlen: the hits' longest span, when the caller knows it (the strict scan's
 // compaction reduces it and reads it with the hit count); -1: reduced here

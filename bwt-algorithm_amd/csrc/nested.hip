@@ -618,11 +618,12 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     // standing between the scan and the post-processing
     (void)ensure_pinned(out.w.data(), out.w.data(), words * 8);
     struct Pieces final : Landing {
-        int dev = 0;
         std::vector<hipEvent_t> ev;
         std::vector<int64_t> end;   // hits landed once ev[p] has completed: [0, end[p])
+        // runs on whichever thread drops the hits (job reset, rescan, job_free, a
+        // post-processing worker): event waits need no current device, so the
+        // thread's device is left alone
         ~Pieces() override {
-            (void)hipSetDevice(dev);
             for (hipEvent_t e : ev) {
                 (void)hipEventSynchronize(e);
                 (void)hipEventDestroy(e);
@@ -641,7 +642,6 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
         }
     };
     auto pc = std::make_shared<Pieces>();
-    pc->dev = c.device;
     const int P = (int)std::max<int64_t>(1, std::min<int64_t>(8, (int64_t)words / (1 << 16)));   // >= 512 KB pieces
     for (int q = 0; q < P; ++q) {
         const int64_t h0 = (int64_t)nk * q / P, h1 = (int64_t)nk * (q + 1) / P;

@@ -821,8 +821,7 @@ std::atomic<int64_t> g_hist_n[8][8], g_hist_ns[8][8];
 std::atomic<int64_t> g_fresh_tests{0}, g_chain_tests{0}, g_fresh_merges{0}, g_chain_merges{0};   // [log4 motif len][log4 region len]
 inline int lg4(int64_t v) { int k = 0; while (v >= 4 && k < 7) { v >>= 2; ++k; } return k; }
 
-// align_repeat_region's result as _recompute_repeat reads it (host AlignSummary
-// or a device RcOut)
+// align_repeat_region's result as _recompute_repeat reads it (a host AlignSummary)
 struct RcView {
     bool ok = false;
     int64_t consumed = 0, copies = 0, motif_len = 0, max_err = 0, tot_ins = 0, tot_del = 0;

@@ -321,18 +321,6 @@ int bwtmi_align_region(const char *seq, int64_t seq_len, int64_t start, int64_t 
                        int64_t tmpl_len, double frac, int64_t max_indel, int64_t min_copies,
                        int64_t *ints8, double *mismatch_rate, char *consensus, char **variations,
                        int64_t **copy_len, int64_t **copy_err);
-/* _recompute_repeat's alignment (bwt.py:3530-3534: align_repeat_region with
- * min_copies, then with 1; frac 0.1, max_indel None, template
- * seq[start:start+m]) of a batch of regions of one sequence on the device,
- * one wavefront per region -- the kernel the merge fold uses for its
- * fresh-pair recomputes (bwt.py:3222-3289).  args: nreq x (start, end, m);
- * per region ints8: found (1/0), copies, consumed, max_errors, tot_ins,
- * tot_del, tot_err, on_device (0: past a device bound, aligned on the host);
- * *strings (malloc'd, free with bwtmi_free): consensus (m bytes) then the
- * variations of region k at [str_off[k], str_off[k + 1]) (empty when not found). */
-int bwtmi_align_regions(bwtmi_ctx *ctx, const char *seq, int64_t seq_len, const int64_t *args, int64_t nreq,
-                        int64_t min_copies, int64_t *ints8, char **strings, int64_t *str_off);
-
 /* ------------------------------------------------------------ FASTA
  * TandemRepeatFinder.load_reference (bwt.py:3713-3756) natively: strip,
  * '>' headers (name = first whitespace token), upper-case sequence lines,
