@@ -186,6 +186,21 @@ struct Ctx {
         evused = 0;
     }
     DBuf slot[S_NSLOTS];
+    // BWTMI_DEVICE_CHECKS=1: the radix passes and the suffix sort's kernels test
+    // the bounds of their tickets, list slots and scattered writes, skip a
+    // store that would leave its array and set a bit here (kChk*); the host
+    // reads the word at the sort's stream waits (checks_verify) and fails
+    // naming what was hit.  Off (nullptr): nothing is tested.
+    DBuf chk;
+    uint32_t *checks() {
+        if (!knob(KN_DEVICE_CHECKS)) return nullptr;
+        if (!chk.p) {
+            chk.ensure(64);
+            HIPCHECK(hipMemsetAsync(chk.p, 0, 64, stream));
+        }
+        return chk.as<uint32_t>();
+    }
+    void checks_verify(const char *where);   // after a wait on `stream` (radix.hip)
     DBuf lb_ticket;          // the look-back launches' tile ticket (radix.hip)
     uint64_t fasta_tag = 0;  // what S_FASTA holds: a split loader's pass-1 part (its job's tag), 0 anything else
     uint32_t lb_epoch = 0;   // the last look-back launch's epoch
@@ -270,6 +285,15 @@ inline void ctx_wait(Ctx &c) {
         fail(code, "%s", c.bg_err.c_str());
     }
 }
+
+// device check bits (Ctx::checks)
+constexpr uint32_t kChkHistTicket = 1;   // a histogram workgroup drew a ticket >= its launch's workgroups
+constexpr uint32_t kChkScatter = 2;      // a radix scatter slot outside [0, n)
+constexpr uint32_t kChkRankPut = 4;      // a first-rank position outside [0, n)
+constexpr uint32_t kChkShortFix = 8;     // the end fix-up: a group or a short suffix not where it must be
+constexpr uint32_t kChkRunList = 16;     // more runs of >= 16 equal symbols than the run list holds
+constexpr uint32_t kChkRunEnd = 32;      // a run end / run-end block outside the text
+constexpr uint32_t kChkDeepEnd = 64;     // a deep suffix whose run end is not inside the text
 
 // ----- primitives (radix.hip)
 template <class T>

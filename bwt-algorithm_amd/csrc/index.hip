@@ -800,6 +800,7 @@ DeviceIndex *index_build_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_
     }
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipStreamSynchronize(st));
+    c.checks_verify("the end of the index build");
     c.kresolve();
     return ix;
 }

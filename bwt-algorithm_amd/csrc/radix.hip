@@ -203,11 +203,15 @@ template <class KT>
 __global__ __launch_bounds__(kBlock) void k_hist_lb(const KT *__restrict__ keys, int64_t n, int shift, int64_t ntiles,
                                                     int S, int64_t nhist, uint64_t *status,
                                                     uint32_t *__restrict__ prefix, uint32_t *__restrict__ base,
-                                                    unsigned *ticket, uint32_t epoch, int vec) {
+                                                    unsigned *ticket, uint32_t epoch, int vec, uint32_t *chk) {
     constexpr int VEC = 16 / sizeof(KT);
     constexpr int NV = kSub / kBlock / VEC;   // 16-byte loads per thread and scatter tile
     __shared__ uint32_t h[kWaves][256];
     const int64_t ht = lb_ticket(ticket, nhist);
+    if (chk && ht >= nhist) {   // (uniform: the ticket is shared) a counter left non-zero by an earlier launch
+        if (threadIdx.x == 0) atomicOr(chk, kChkHistTicket);
+        return;
+    }
     const int wv = threadIdx.x >> 6, d = threadIdx.x, lane = threadIdx.x & 63;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) h[w][d] = 0;
@@ -333,7 +337,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, c
                                                    KT *__restrict__ kout, V *__restrict__ vout,
                                                    const uint32_t *__restrict__ prefix,
                                                    const uint32_t *__restrict__ dbase, int64_t n, int shift,
-                                                   int64_t ntiles, uint8_t *__restrict__ dnext = nullptr,
+                                                   int64_t ntiles, uint32_t *chk, uint8_t *__restrict__ dnext = nullptr,
                                                    int nshift = 0) {
     constexpr int kT = BLOCK * ITEMS;
     constexpr int NW = BLOCK / 64;
@@ -444,10 +448,14 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, c
             const KT key = ks[j];
             const uint32_t d = (uint32_t)((key >> shift) & 255u);
             const uint32_t p = gdelta[d] + (uint32_t)j;
-            st<NT>(kout + p, key);
-            if (dnext) dnext[p] = (uint8_t)((key >> nshift) & 255u);   // the next pass's histogram input
             if constexpr (DG) dg_s[j] = (uint8_t)d;
             else pos[i] = p;
+            if (chk && (int64_t)p >= n) {   // a count table that does not match the keys
+                atomicOr(chk, kChkScatter);
+                continue;
+            }
+            st<NT>(kout + p, key);
+            if (dnext) dnext[p] = (uint8_t)((key >> nshift) & 255u);   // the next pass's histogram input
             if (!SPLIT && vout) st<NT>(vout + p, vs[j]);
         }
     }
@@ -461,8 +469,12 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, c
         for (int i = 0; i < ITEMS; ++i) {
             const int j = i * BLOCK + threadIdx.x;
             if (j < cntt) {
-                if constexpr (DG) st<NT>(vout + gdelta[dg_s[j]] + (uint32_t)j, vs[j]);
-                else st<NT>(vout + pos[i], vs[j]);
+                if constexpr (DG) {
+                    const uint32_t p = gdelta[dg_s[j]] + (uint32_t)j;
+                    if (!chk || (int64_t)p < n) st<NT>(vout + p, vs[j]);
+                } else if (!chk || (int64_t)pos[i] < n) {
+                    st<NT>(vout + pos[i], vs[j]);
+                }
             }
         }
     }
@@ -509,7 +521,7 @@ void launch_hist(Ctx &c, const KT *keys, int64_t n, int shift, int64_t ntiles, u
                                                                                         : "radix_hist_k8",
             (double)n * (double)sizeof(KT), k_hist_lb<KT>, dim3((unsigned)nhist), dim3(kBlock), 0,
             c.stream, keys, n, shift, ntiles, S, nhist, lb.status, *prefix, *base, lb.ticket, lb.epoch,
-            ((uintptr_t)keys & 15) == 0 ? 1 : 0);
+            ((uintptr_t)keys & 15) == 0 ? 1 : 0, c.checks());
 }
 
 template <class KT, class V, int BLOCK, int ITEMS, bool NT, bool SPLIT>
@@ -545,7 +557,7 @@ void radix_sort_cfg(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
                 : sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16",
                 (double)n * 2.0 * ((double)sizeof(KT) + (vals ? (double)sizeof(V) : 0.0)),
                 (k_scatter<KT, V, BLOCK, ITEMS, NT, SPLIT>), dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, ka, va,
-                kb, vb, prefix, base, n, sh, ntiles, more ? dg : nullptr, sh + 8);
+                kb, vb, prefix, base, n, sh, ntiles, c.checks(), more ? dg : nullptr, sh + 8);
         std::swap(ka, kb);
         std::swap(va, vb);
         ++passes;
@@ -575,6 +587,21 @@ void radix_sort_impl(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
 }
 
 }  // namespace
+
+void Ctx::checks_verify(const char *where) {
+    if (!chk.p || !knob(KN_DEVICE_CHECKS)) return;
+    uint32_t v = 0;
+    HIPCHECK(hipMemcpyAsync(&v, chk.p, 4, hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+    if (!v) return;
+    HIPCHECK(hipMemsetAsync(chk.p, 0, 4, stream));
+    static const char *const names[] = {"histogram ticket", "scatter slot", "first-rank position", "end fix-up",
+                                        "run list", "run end", "deep run end"};
+    std::string what;
+    for (int b = 0; b < 7; ++b)
+        if (v >> b & 1u) what += std::string(what.empty() ? "" : ", ") + names[b];
+    fail(BWTMI_E_STATE, "device check failed before %s: %s (BWTMI_DEVICE_CHECKS)", where, what.c_str());
+}
 
 void exclusive_scan_rows(Ctx &c, const uint32_t *in, uint32_t *out, int64_t n, int rows, int64_t stride) {
     if (n <= 0 || rows <= 0) return;
@@ -611,7 +638,8 @@ void radix_pass_k32(Ctx &c, const uint32_t *kin, const uint32_t *vin, uint32_t *
     uint32_t *prefix, *base;
     launch_hist<uint32_t>(c, kin, n, shift, ntiles, &prefix, &base);
     KLAUNCH("radix_partition_kv8", (double)n * 16.0, (k_scatter<uint32_t, uint32_t, BLOCK, ITEMS, false, true>),
-            dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, kin, vin, kout, vout, prefix, base, n, shift, ntiles);
+            dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, kin, vin, kout, vout, prefix, base, n, shift, ntiles,
+            c.checks());
     HIPCHECK(hipGetLastError());
 }
 

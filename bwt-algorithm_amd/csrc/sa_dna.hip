@@ -333,7 +333,8 @@ __global__ __launch_bounds__(kB) void k_grp_apply(const K *__restrict__ keys, in
 constexpr int kPutItems = 16;
 template <bool NT>
 __global__ __launch_bounds__(kB) void k_dna_rank_put(const uint32_t *__restrict__ pv, const uint32_t *__restrict__ hd,
-                                                     int64_t n, int64_t ntiles, uint32_t *__restrict__ rank) {
+                                                     int64_t n, int64_t ntiles, uint32_t *__restrict__ rank,
+                                                     uint32_t *chk) {
     const int64_t base = xcd_tile(blockIdx.x, ntiles) * (kB * kPutItems) + threadIdx.x;
     uint32_t p[kPutItems], h[kPutItems];
 #pragma unroll
@@ -349,7 +350,10 @@ __global__ __launch_bounds__(kB) void k_dna_rank_put(const uint32_t *__restrict_
     }
 #pragma unroll
     for (int i = 0; i < kPutItems; ++i)
-        if (base + (int64_t)i * kB < n) rank[p[i] & kPosMask] = h[i];
+        if (base + (int64_t)i * kB < n) {
+            if (chk && (int64_t)(p[i] & kPosMask) >= n) atomicOr(chk, kChkRankPut);
+            else rank[p[i] & kPosMask] = h[i];
+        }
 }
 
 // The same writes after the pairs are ordered by the top 16 position bits: every
@@ -360,7 +364,7 @@ __global__ __launch_bounds__(kB) void k_dna_rank_put(const uint32_t *__restrict_
 // outside the window (not expected) is stored directly.
 template <bool NT>
 __global__ __launch_bounds__(kB) void k_dna_rank_put_tile(const uint32_t *__restrict__ pv, const uint32_t *__restrict__ hd,
-                                                          int64_t n, uint32_t *__restrict__ rank) {
+                                                          int64_t n, uint32_t *__restrict__ rank, uint32_t *chk) {
     constexpr int kT = kB * kPutItems;
     __shared__ uint32_t win[kT];
     const int64_t t0 = (int64_t)blockIdx.x * kT;
@@ -381,6 +385,7 @@ __global__ __launch_bounds__(kB) void k_dna_rank_put_tile(const uint32_t *__rest
         if (t0 + (int64_t)i * kB + threadIdx.x >= n) continue;
         const int64_t q = (int64_t)(p[i] & kPosMask) - t0;
         if (q >= 0 && q < kT) win[q] = h[i];
+        else if (chk && (int64_t)(p[i] & kPosMask) >= n) atomicOr(chk, kChkRankPut);
         else rank[p[i] & kPosMask] = h[i];
     }
     __syncthreads();
@@ -396,12 +401,13 @@ __global__ __launch_bounds__(kB) void k_dna_rank_put_tile(const uint32_t *__rest
 // the group; the rest of the group gets the head behind them.  One workgroup.
 __global__ __launch_bounds__(1024) void k_dna_short_fix(uint32_t *__restrict__ vals, uint32_t *__restrict__ rank,
                                                         uint32_t *__restrict__ gs, const uint32_t *__restrict__ ge,
-                                                        int64_t G, int64_t n) {
+                                                        int64_t G, int64_t n, uint32_t *chk) {
     __shared__ int64_t grp[16];      // group index of the short suffix with r bases left, or -1
     __shared__ uint32_t where[16];   // its index in vals
     const int ns = (int)min<int64_t>(16, n);
     if (threadIdx.x < 16) {
         grp[threadIdx.x] = -1;
+        where[threadIdx.x] = ~0u;
         if ((int)threadIdx.x < ns) {
             const uint32_t hd = rank[n - 1 - threadIdx.x];
             int64_t lo = 0, hi = G;   // gs ascends: find gs[x] == hd
@@ -431,6 +437,10 @@ __global__ __launch_bounds__(1024) void k_dna_short_fix(uint32_t *__restrict__ v
             for (int r = 0; r < ns; ++r) {
                 if (grp[r] != g) continue;
                 const uint32_t t = s + k, from = where[r];
+                if (chk && (from < s || from >= e || t >= e)) {   // the short suffix was not found in its group
+                    atomicOr(chk, kChkShortFix);
+                    continue;
+                }
                 const uint32_t moved = vals[t];
                 vals[t] = vals[from];
                 vals[from] = moved;
@@ -666,6 +676,7 @@ struct Deep {
     const uint32_t *re;   // run end per 16-position block (valid for deep suffixes' blocks)
     int small;            // symbol codes of the small-alphabet path
     int on;               // any run of >= 16 equal symbols
+    uint32_t *chk;        // Ctx::checks (nullptr: off)
 };
 
 // the 16 symbols from a (the packed words are padded): c when all equal, else -1
@@ -696,6 +707,10 @@ __device__ __forceinline__ uint32_t ls_key(const uint32_t *__restrict__ rank, ui
         if (c >= 0) {
             const int64_t e = d.re[a >> 4];   // first position past the run (<= n - 1: '$' ends every run)
             const int64_t r = e - a;
+            if (d.chk && (e < a + 16 || e >= n)) {   // a run-end block the run-end pass did not write
+                atomicOr(d.chk, kChkDeepEnd);
+                return 0u;
+            }
             if (h == 16) {
                 if (r >= 32) {
                     const bool b = e < n - 1 && sym_at(d, e) > c;
@@ -742,6 +757,7 @@ __global__ __launch_bounds__(kB) void k_run_starts(Deep d, int64_t n, uint32_t *
     if (st) {
         const uint32_t at = wc[kB / 64] + wc[wv] + (uint32_t)__popcll(m & lanes_below(lane));
         if (at < cap) rs[at] = (uint32_t)p;
+        else if (d.chk) atomicOr(d.chk, kChkRunList);
     }
 }
 
@@ -779,7 +795,11 @@ __global__ __launch_bounds__(kB) void k_run_ends(Deep d, int64_t n, const uint32
         }
         const int64_t e0 = (int64_t)first;
         const int64_t b0 = s0 >> 4, b1 = (e0 - 16) >> 4;   // 16 b + 15 in [s0, e0)
-        for (int64_t b = b0 + threadIdx.x; b <= b1; b += kB) re[b] = (uint32_t)e0;
+        if (d.chk && (e0 < s0 + 16 || e0 > n - 1 || b1 > (n - 1) / 16)) {
+            if (threadIdx.x == 0) atomicOr(d.chk, kChkRunEnd);
+        } else {
+            for (int64_t b = b0 + threadIdx.x; b <= b1; b += kB) re[b] = (uint32_t)e0;
+        }
         __syncthreads();   // `first` is reset for the next run
     }
 }
@@ -1091,13 +1111,14 @@ bool sa_sort(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, in
         uint32_t g32 = 0;
         HIPCHECK(hipMemcpyAsync(&g32, tcnt + 3 * nt, 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
+        c.checks_verify("the suffix sort's 16-symbol groups");
         G = g32;
     }
     // rank[pos] = head
     const int64_t nput = (n + kB * kPutItems - 1) / (kB * kPutItems);
     if (n <= (1 << 16)) {
         KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put<false>, dim3((unsigned)nput), dim3(kB), 0, st, vals,
-                hd, n, nput, rank);
+                hd, n, nput, rank, c.checks());
     } else {
         // through a position partition (the pass output in the sort's buffers):
         // two stable passes order the pairs by the top 16 position bits, so one
@@ -1114,16 +1135,17 @@ bool sa_sort(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, in
         radix_pass_k32(c, pv, ph, fe, pe, n, bits - 8);   // fe / pe are free until the refine rounds
         if (bits - 16 <= 12)   // 2^(bits-16) positions per 16-bit window divide the 4096-pair tile
             KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put_tile<true>, dim3((unsigned)nput), dim3(kB), 0, st,
-                    fe, pe, n, rank);
+                    fe, pe, n, rank, c.checks());
         else   // texts past 2^28 bases: streaming stores into the 2^(bits-16) windows
             KLAUNCH("dna_rank_put", 12.0 * (double)n, k_dna_rank_put<true>, dim3((unsigned)nput), dim3(kB), 0, st, fe,
-                    pe, n, nput, rank);
+                    pe, n, nput, rank, c.checks());
     }
-    if (G) KLAUNCH("dna_short_fix", 0.0, k_dna_short_fix, dim3(1), dim3(1024), 0, st, vals, rank, gs, ge, G, n);
+    if (G) KLAUNCH("dna_short_fix", 0.0, k_dna_short_fix, dim3(1), dim3(1024), 0, st, vals, rank, gs, ge, G, n,
+                   c.checks());
 
     // runs of >= 16 equal symbols: their blocks' run ends (Deep); the flag
     // buffers are free until the large-group rounds
-    Deep dp{P, nullptr, small ? 1 : 0, 0};
+    Deep dp{P, nullptr, small ? 1 : 0, 0, c.checks()};
     if (G > 0) {
         const int64_t cap = n / 16 + 64;   // runs of >= 16 are disjoint
         c.slot[S_IDX12].ensure((size_t)(n / 16 + 2) * 4 + (size_t)cap * 4 + 64);
@@ -1135,6 +1157,7 @@ bool sa_sort(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, in
         uint32_t K = 0;
         HIPCHECK(hipMemcpyAsync(&K, kcount, 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
+        c.checks_verify("the suffix sort's first ranks and run starts");
         if (K) {
             KLAUNCH("dna_run_ends", 0.0, k_run_ends, dim3((unsigned)std::min<uint32_t>(K, 2048)), dim3(kB), 0, st, dp, n,
                     rs, kcount, re);
@@ -1158,6 +1181,7 @@ bool sa_sort(Ctx &c, const uint8_t *t, int64_t n, uint32_t *SA, uint8_t *BWT, in
         uint32_t cnt[kClasses];
         HIPCHECK(hipMemcpyAsync(cnt, counts, sizeof cnt, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
+        c.checks_verify("a doubling round");
         if (FILE *tf = Ctx::ktrace_file())
             std::fprintf(tf, "# round h=%lld G=%lld classes %u %u %u %u %u %u\n", (long long)h, (long long)G, cnt[0],
                          cnt[1], cnt[2], cnt[3], cnt[4], cnt[5]);

@@ -1311,6 +1311,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     HIPCHECK(hipMemcpyAsync(mb32 + 1, c.slot[S_FLAG].as<uint32_t>() + nc - 1, 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(mb + 1, d_maxlen, 8, hipMemcpyDeviceToHost, st));
     scan_wait(st);
+    c.checks_verify("the strict scan's hit count");
     const int64_t nh = (int64_t)mb32[0] + mb32[1];
     const int64_t maxlen = (int64_t)mb[1];
     res.raw = nh;
