@@ -232,10 +232,6 @@ constexpr int kSegWin = 512;           // nominal positions per window
 constexpr int kSegCapS = 1024;         // hits a small workgroup holds
 constexpr int kSegCapL = 4096;         // hits a large workgroup holds
 
-__device__ __forceinline__ bool seg_head(const int64_t *__restrict__ S, const int64_t *__restrict__ PME, int64_t k) {
-    return k == 0 || PME[k - 1] <= S[k];
-}
-
 // LARGE = false: window blockIdx.x, overflowing windows are appended to ovf_win;
 // LARGE = true: the windows listed in ovf_win (*ovf_n of them), a grid-stride
 // loop; a window past kSegCapL sets *fallback
@@ -249,6 +245,7 @@ __global__ __launch_bounds__(T) void k_seg_levels(const int64_t *__restrict__ S,
     __shared__ uint8_t sK[CAP];
     __shared__ int16_t sF[CAP];
     __shared__ unsigned long long found;
+    __shared__ int64_t pm1;   // PME[w0 - 1]
     __shared__ int pend[3];
     const int tid = threadIdx.x;
     const int64_t nwin = LARGE ? (int64_t)*ovf_n : (int64_t)gridDim.x;
@@ -256,11 +253,33 @@ __global__ __launch_bounds__(T) void k_seg_levels(const int64_t *__restrict__ S,
         const int64_t w = LARGE ? (int64_t)ovf_win[q] : q;
         const int64_t w0 = w * WIN;
         const int64_t w1 = w0 + WIN < n ? w0 + WIN : n;
-        // a = the window's first segment head (none: a segment from an earlier window covers it)
-        if (tid == 0) found = ~0ull;
+        // The window's entries from w0 on, up to CAP of them, go to LDS in one
+        // pass: its segments start at a >= w0 and end at b <= a + CAP, so that
+        // copy is the window's whenever a == w0 (nearly always), and the two
+        // head searches below read LDS -- one round trip to memory per window
+        // instead of three (head search, end search, copy).
+        const int64_t L0 = w0 + CAP < n ? CAP : n - w0;
+        for (int i = tid; i < L0; i += T) {
+            sS[i] = S[w0 + i];
+            sE[i] = E[w0 + i];
+            sP[i] = PME[w0 + i];
+            sM[i] = M[w0 + i];
+        }
+        if (tid == 0) {
+            found = ~0ull;
+            pm1 = w0 > 0 ? PME[w0 - 1] : INT64_MIN;
+        }
         __syncthreads();
+        // k >= w0 starts a segment: k == 0 or PME[k - 1] <= S[k] (LDS where loaded)
+        auto head_at = [&](int64_t k) -> bool {
+            if (k == 0) return true;
+            const int64_t j = k - w0;
+            const int64_t pp = j == 0 ? pm1 : (j - 1 < L0 ? sP[j - 1] : PME[k - 1]);
+            return pp <= (j < L0 ? sS[j] : S[k]);
+        };
+        // a = the window's first segment head (none: a segment from an earlier window covers it)
         for (int64_t k = w0 + tid; k < w1; k += T)
-            if (seg_head(S, PME, k)) atomicMin(&found, (unsigned long long)k);
+            if (head_at(k)) atomicMin(&found, (unsigned long long)k);
         __syncthreads();
         const int64_t a = (int64_t)found;   // uniform
         __syncthreads();
@@ -270,7 +289,7 @@ __global__ __launch_bounds__(T) void k_seg_levels(const int64_t *__restrict__ S,
         __syncthreads();
         const int64_t lim = a + CAP < n ? a + CAP : n;
         for (int64_t k = w1 + tid; k <= lim; k += T)
-            if (k == n || seg_head(S, PME, k)) atomicMin(&found, (unsigned long long)k);
+            if (k == n || head_at(k)) atomicMin(&found, (unsigned long long)k);
         __syncthreads();
         const int64_t b = (int64_t)found;
         __syncthreads();
@@ -282,13 +301,15 @@ __global__ __launch_bounds__(T) void k_seg_levels(const int64_t *__restrict__ S,
             continue;
         }
         const int len = (int)(b - a);
-        for (int i = tid; i < len; i += T) {
-            sS[i] = S[a + i];
-            sE[i] = E[a + i];
-            sP[i] = PME[a + i];
-            sM[i] = M[a + i];
+        if (a != w0 || b - w0 > L0) {   // not the loaded range: the window's own copy
+            for (int i = tid; i < len; i += T) {
+                sS[i] = S[a + i];
+                sE[i] = E[a + i];
+                sP[i] = PME[a + i];
+                sM[i] = M[a + i];
+            }
+            __syncthreads();
         }
-        __syncthreads();
         // a hit that no span of a longer motif could nest (kept or not) is kept
         // whatever the levels decide: only the others (kUndecided) take part in
         // the level loop, whose levels are then the distinct motif lengths among them

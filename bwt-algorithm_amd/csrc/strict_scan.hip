@@ -231,25 +231,28 @@ __global__ __launch_bounds__(256) void k_runs(const uint32_t *__restrict__ P, in
         // scanning 64 words per step (long exact arrays repeat for many L, and
         // one lane walking them word by word stalls its wave on dependent loads).
         const bool sstart = owned && M == FULL && Mp != FULL;
-        const uint64_t nf = __ballot(M != FULL);
-        const uint64_t above = lane == 63 ? 0ull : (nf & (~0ull << (lane + 1)));
-        const int src = above ? __ffsll((unsigned long long)above) - 1 : lane;
-        const uint32_t Mend = (uint32_t)__shfl((int)M, src, 64);
-        int64_t e_streak = sstart && above ? (w + (src - lane)) * 32 + (int64_t)__ffs(~Mend) - 1 : -1;
-        const bool beyond = sstart && !above;
-        if (__any(beyond)) {   // at most one lane: the streak runs past lane 63's word
-            // one 64-word step here; a streak longer than that (an assembly gap's
-            // N run is one for every unit length) is ended by k_streak_end, so
-            // the unit lengths' walks do not chain through this wave
-            const int64_t q0 = wave_base + 63;
-            const uint32_t Mq = eq32<B>(P, q0 + lane, L, n);   // 0 past the text: ends the scan
-            const uint64_t nb = __ballot(Mq != FULL);
-            if (nb) {
-                const int f = __ffsll((unsigned long long)nb) - 1;
-                const uint32_t Mf = (uint32_t)__shfl((int)Mq, f, 64);
-                if (beyond) e_streak = (q0 + f) * 32 + (int64_t)__ffs(~Mf) - 1;
-            } else if (beyond) {
-                push_pending(out, L, j0 - (int64_t)__clz(~Mp), q0 + 64);
+        int64_t e_streak = -1;
+        if (__any(sstart)) {   // (short unit lengths: rarely) the streak ends
+            const uint64_t nf = __ballot(M != FULL);
+            const uint64_t above = lane == 63 ? 0ull : (nf & (~0ull << (lane + 1)));
+            const int src = above ? __ffsll((unsigned long long)above) - 1 : lane;
+            const uint32_t Mend = (uint32_t)__shfl((int)M, src, 64);
+            if (sstart && above) e_streak = (w + (src - lane)) * 32 + (int64_t)__ffs(~Mend) - 1;
+            const bool beyond = sstart && !above;
+            if (__any(beyond)) {   // at most one lane: the streak runs past lane 63's word
+                // one 64-word step here; a streak longer than that (an assembly gap's
+                // N run is one for every unit length) is ended by k_streak_end, so
+                // the unit lengths' walks do not chain through this wave
+                const int64_t q0 = wave_base + 63;
+                const uint32_t Mq = eq32<B>(P, q0 + lane, L, n);   // 0 past the text: ends the scan
+                const uint64_t nb = __ballot(Mq != FULL);
+                if (nb) {
+                    const int f = __ffsll((unsigned long long)nb) - 1;
+                    const uint32_t Mf = (uint32_t)__shfl((int)Mq, f, 64);
+                    if (beyond) e_streak = (q0 + f) * 32 + (int64_t)__ffs(~Mf) - 1;
+                } else if (beyond) {
+                    push_pending(out, L, j0 - (int64_t)__clz(~Mp), q0 + 64);
+                }
             }
         }
         if (owned) {
@@ -285,6 +288,7 @@ __global__ __launch_bounds__(256) void k_runs(const uint32_t *__restrict__ P, in
                 }
             }
         }
+        if (!__any(cnt != 0)) continue;   // most (unit length, word) steps: no candidate, no prefix scan
         int incl = cnt;   // wave inclusive prefix of the counts
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {

@@ -125,6 +125,19 @@ def main():
                 fn(*args)
                 calls[name] = calls.get(name, 0.0) + (time.perf_counter() - t) * 1e3
 
+            # the sharded write's pieces, timed apart (render / exchange / pwrite)
+            def timed_method(nm, f):
+                def g(*a, **kw):
+                    t0 = time.perf_counter()
+                    r = f(*a, **kw)
+                    calls["w_" + nm] = calls.get("w_" + nm, 0.0) + (time.perf_counter() - t0) * 1e3
+                    return r
+                return g
+            for meth in ("unit_rows", "render_units", "write_units"):
+                if not hasattr(job, "_orig_" + meth):
+                    setattr(job, "_orig_" + meth, getattr(job, meth))
+                setattr(job, meth, timed_method(meth, getattr(job, "_orig_" + meth)))
+
             def step():
                 pc.begin_step()
                 timed("reset", job.reset)

@@ -67,6 +67,14 @@ for step in "$@"; do
       python3 tools/pmc_traffic.py "$OUT/pmc_${name}_FETCH_SIZE" "$OUT/pmc_${name}_WRITE_SIZE" "$OUT/pmc_traffic_$name.json" \
         || { echo PMC_PARSE_FAIL; exit 1; }
       rm -rf "$OUT/pmc_${name}_FETCH_SIZE" "$OUT/pmc_${name}_WRITE_SIZE" ;;
+    sq)   # one SQ counter pass over the kernels matching a regex ('+' stands for '|'): "sq NAME CTR,CTR,... REGEX [bench.py args]"
+      IFS=',' read -r -a CTRS <<< "${args[0]}"
+      RX=${args[1]//+/|}
+      timeout -k 10 -s KILL 180 rocprofv3 --pmc "${CTRS[@]}" --kernel-include-regex "$RX" --output-format csv \
+        -d "$OUT/sq_$name" -o sq -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-fm --no-cli "${args[@]:2}" \
+        > "$OUT/sq_$name.json" 2> "$OUT/sq_$name.err" || { echo SQ_FAIL; tail -5 "$OUT/sq_$name.err"; exit 1; }
+      python3 tools/pmc_sq.py "$OUT/sq_$name" > "$OUT/sq_$name.txt" && cat "$OUT/sq_$name.txt"
+      rm -rf "$OUT/sq_$name" ;;
     mtrace)   # roctx stage ranges + kernels of one CLI run: "mtrace NAME FASTA [bwt.py args]"
       timeout -k 10 600 rocprofv3 --marker-trace --kernel-trace --output-format csv -d "$OUT/mt_$name" -o run -- \
         python3 bwt-algorithm_amd/bwt.py "${args[@]}" -o "$OUT/mt_$name.tab" --profile "$OUT/profile_$name.json" \
