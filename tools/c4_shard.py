@@ -77,6 +77,19 @@ class StandInComm:
         self._wire(np.zeros(1, dtype=np.int64))
 
 
+def cgroup_cpu_us():
+    """CPU time of this cgroup (all its threads) in microseconds, or None"""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, v = line.split()
+                if k == "usage_usec":
+                    return int(v)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def main():
     out_json = sys.argv[1]
     tlist = [int(x) for x in sys.argv[2:]] or [2, 16]
@@ -150,15 +163,19 @@ def main():
             step()
             calls.clear()
             ts = []
+            cpu0 = cgroup_cpu_us()
             for _ in range(3):
                 t = time.perf_counter()
                 step()
                 ts.append((time.perf_counter() - t) * 1e3)
+            cpu1 = cgroup_cpu_us()
             bp = sum(job.contig_weight(i) for i in job.select_shard(W, r))
             res["runs"].append(dict(world=W, threads=T, rank=r, shard_bp=bp, step_ms=round(max(ts), 2),
                                     median_ms=round(sorted(ts)[1], 2),
                                     steps_ms=[round(x, 2) for x in ts], stage_ms=[round(x, 2) for x in job.stage_ms()],
-                                    calls_ms={k: round(v / 3, 2) for k, v in calls.items()}))
+                                    calls_ms={k: round(v / 3, 2) for k, v in calls.items()},
+                                    cpu_ms_per_step=round((cpu1 - cpu0) / 3e3, 2) if cpu0 is not None and cpu1 is not None
+                                    else None))
             print(json.dumps(res["runs"][-1]), flush=True)
     for W, T in [(w, t) for w in worlds for t in tlist]:
         worst = max(x["step_ms"] for x in res["runs"] if x["threads"] == T and x["world"] == W)
