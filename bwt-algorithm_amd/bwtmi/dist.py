@@ -185,23 +185,30 @@ def assign(units: List[List[int]], weights: Sequence[int], world: int) -> List[L
 def write_sharded(comm, job, fmt: str, path: str) -> int:
     """Write the output file from every rank's own fold units, without moving
     records between ranks.  The file is the units' rows in unit (natural-key)
-    order (bwt.py:4147-4150) and each unit lives on exactly one rank, so two
-    all-reduces of per-unit counts (rows for VCF ids, then bytes) give every
-    rank its byte offsets; rank 0 sizes the file and writes the header.
-    Returns the file size."""
-    rows = comm.allreduce(job.unit_rows())
-    row_base = np.concatenate([[0], np.cumsum(rows)[:-1]]).astype(np.int64)
+    order (bwt.py:4147-4150) and each unit lives on exactly one rank, so an
+    all-reduce of per-unit byte counts gives every rank its byte offsets (VCF
+    also needs the rows before each unit for its TR ids: one all-reduce of
+    per-unit row counts first); rank 0 writes the header and sizes the file.
+    Sizing commutes with the writes -- every rank writes inside [0, total), and
+    ftruncate to total neither moves nor drops those bytes whenever it lands --
+    so only the end of the write needs a barrier.  Returns the file size."""
+    row_base = None
+    if fmt == "vcf":
+        rows = comm.allreduce(job.unit_rows())
+        row_base = np.concatenate([[0], np.cumsum(rows)[:-1]]).astype(np.int64)
     local = job.render_units(fmt, row_base)
     sizes = comm.allreduce(np.ascontiguousarray(local[1:]))
     header = int(local[0])
     offsets = np.concatenate([[0, header], header + np.cumsum(sizes)[:-1]]).astype(np.int64)
     total = header + int(sizes.sum())
     if comm.rank == 0:
-        # sized in place: every byte of [0, total) is written below, so an
-        # existing file is overwritten (reusing its page-cache pages) and cut
-        with open(path, "r+b" if os.path.isfile(path) else "wb") as f:
-            f.truncate(total)
-    comm.barrier()
+        # sized in place: every byte of [0, total) is written, so an existing file
+        # is overwritten (reusing its page-cache pages) and cut
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
+        try:
+            os.ftruncate(fd, total)
+        finally:
+            os.close(fd)
     job.write_units(path, offsets, write_header=(comm.rank == 0))
     comm.barrier()
     return total

@@ -578,8 +578,11 @@ def _sharded_write_worker(rank, world, port, fa, outdir):
 @pytest.mark.parametrize("world,name", [(2, "test_all_12.fa"), (3, "edge_mixed.fa")])
 def test_sharded_write_matches_single_process(tmp_path, golden_dir, built_lib, world, name):
     """Each rank writes its own fold units at exchanged offsets; the file equals
-    the single-process output in every format (incl. global VCF row ids)."""
+    the single-process output in every format (incl. global VCF row ids), also
+    over a longer stale file (rank 0 sizes it while the others write)."""
     fa = os.path.join(golden_dir, "inputs", name)
+    for fmt in ("strfinder", "bed", "vcf", "trf_table", "trf_dat"):
+        (tmp_path / f"{fmt}.out").write_bytes(b"stale\n" * 200_000)
     _spawn(_sharded_write_worker, (world, _free_port(), fa, str(tmp_path)), world)
     for fmt in ("strfinder", "bed", "vcf", "trf_table", "trf_dat"):
         assert (tmp_path / f"{fmt}.out").read_text() == post.run_file(fa, fmt), fmt
