@@ -539,6 +539,12 @@ struct Extra {                  // trivially destructible: strings live in the P
     int32_t tier = 2;
     char strand = '+';
     bool stats_none = false;    // Rec::stats_none
+    // the DP walk stopped at a copy that failed (not at its safety limit):
+    // where, and with which min_copies (1: min_copies, 2: the retry with 1).
+    // A later call with the same start and motif length whose limit lies past
+    // wk_stop walks the same windows (recompute's reuse; refine's calls)
+    int8_t wk_phase = 0;
+    int64_t wk_stop = -1;
 };
 
 static_assert(std::is_trivially_destructible<Extra>::value, "Extras live in raw arena blocks");
@@ -549,8 +555,17 @@ static_assert(std::is_trivially_destructible<Extra>::value, "Extras live in raw 
 // unit is primitive), tier 2; every other record carries an Extra
 struct Item {
     int64_t start, end;   // current frame (trimmed, then full after restore)
-    const Extra *x;       // recomputed record, nullptr for a strict hit
+    // recomputed record (nullptr for a strict hit), tagged in bit 0 when its
+    // mismatch rate is non-zero: the refine pass tests every fold output and
+    // only those records, so it reads no Extra for the others (each read a
+    // cache miss: the C3 assembly pass 6.0 -> ~2 ms)
+    const Extra *xp;
     int32_t chrom, mlen;
+    const Extra *x() const { return reinterpret_cast<const Extra *>(reinterpret_cast<uintptr_t>(xp) & ~uintptr_t(1)); }
+    bool imperfect() const { return (reinterpret_cast<uintptr_t>(xp) & 1u) != 0; }
+    void set_x(const Extra *e) {   // after e->mm is final
+        xp = reinterpret_cast<const Extra *>(reinterpret_cast<uintptr_t>(e) | (e && e->mm != 0.0 ? 1u : 0u));
+    }
 };
 static_assert(sizeof(Item) == 32, "fold items stay 32 bytes");
 
@@ -652,15 +667,15 @@ struct UnitCtx {
 };
 
 inline std::string_view motif_of(const UnitCtx &u, const Item &it) {
-    if (it.x) return it.x->motif;
+    if (it.xp) return it.x()->motif;
     const Contig &c = u.job->contigs[(size_t)it.chrom];
     return std::string_view((u.restored ? c.full.data() : c.trimmed()) + it.start, (size_t)it.mlen);
 }
 inline int64_t strict_copies(const Item &it) { return (it.end - it.start) / it.mlen; }
-inline int32_t tier_of(const Item &it) { return it.x ? it.x->tier : 2; }
-inline double copies_of(const Item &it) { return it.x ? it.x->copies : (double)strict_copies(it); }
-inline double mm_of(const Item &it) { return it.x ? it.x->mm : 0.0; }
-inline double conf_of(const Item &it) { return it.x ? it.x->confidence : 0.95; }
+inline int32_t tier_of(const Item &it) { return it.xp ? it.x()->tier : 2; }
+inline double copies_of(const Item &it) { return it.xp ? it.x()->copies : (double)strict_copies(it); }
+inline double mm_of(const Item &it) { return it.xp ? it.x()->mm : 0.0; }
+inline double conf_of(const Item &it) { return it.xp ? it.x()->confidence : 0.95; }
 
 // stable sort of items by (start, end)
 void sort_by_pos(ItemVec &v, int nt) {
@@ -832,8 +847,11 @@ Item item_of_alignment(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int
                        int32_t tier, std::string_view tmpl, const RcView &v);
 
 // bwt.py:3515-3614 (on the trimmed sequence, before coordinate restore)
+// prev (optional): an earlier record from the same start (refine passes the
+// record it refines) -- reused when its walk stopped at a failing copy inside
+// this call's limit
 Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t start, int64_t end,
-               int64_t motif_len, int32_t tier) {
+               int64_t motif_len, int32_t tier, const Item *prev = nullptr) {
     struct Tick {   // BWTMI_STATS=2 only
         int a, b;
         std::chrono::steady_clock::time_point t;
@@ -896,7 +914,7 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
         it.end = start + run;
         it.chrom = chrom;
         it.mlen = 1;
-        it.x = pools.add_static(w, x, std::string_view(&kByteChars[(uint8_t)b], 1));
+        it.set_x(pools.add_static(w, x, std::string_view(&kByteChars[(uint8_t)b], 1)));
         return it;
     }
     if (g_dump) {   // BWTMI_DUMP_RECOMPUTE=path: the DP recomputes' arguments (tools/recompute_bench.cpp)
@@ -919,16 +937,28 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
         const int64_t e2 = std::min(L, end > start ? end : L);
         return std::min(L, std::max(e2, start + m * mcx) + std::max(m * 3, mi * 4));
     };
+    if (prev && prev->xp && prev->start == start && prev->chrom == chrom) {
+        const Extra &px = *prev->x();
+        if (px.wk_stop >= 0 && px.req_m == m && px.wk_stop < walk_limit(px.wk_phase == 1 ? mc : 1)) {
+            if (stats_on(2)) g_walk_reuse.fetch_add(1, std::memory_order_relaxed);
+            Extra *x = pools.clone(w, px);
+            x->req_end = req_end;
+            x->tier = tier;
+            Item it = *prev;
+            it.set_x(x);
+            return it;
+        }
+    }
     if (A.wk_ok && A.wk_seq == seq && A.wk_start == start && A.wk_m == m &&
         A.wk_stop < walk_limit(A.wk_phase == 1 ? mc : 1)) {
         // the same windows up to the same failing copy: the same record, but
         // for what depends on the call itself (the requested end, the tier)
         if (stats_on(2)) g_walk_reuse.fetch_add(1, std::memory_order_relaxed);
-        Extra *x = pools.clone(w, *A.wk_item.x);
+        Extra *x = pools.clone(w, *A.wk_item.x());
         x->req_end = req_end;
         x->tier = tier;
         Item it = A.wk_item;
-        it.x = x;
+        it.set_x(x);
         return it;
     }
     std::string tmpl = slice(start, start + m);
@@ -963,6 +993,11 @@ Item recompute(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int64_t sta
     }
     Item it = item_of_alignment(u, pools, w, chrom, start, end, m, tier, tmpl, v);
     A.wk_ok = ok && !s.at_limit;
+    if (A.wk_ok) {   // this worker's new Extra: the record carries its walk's stop for later calls
+        Extra *xe = const_cast<Extra *>(it.x());
+        xe->wk_stop = start + s.consumed;
+        xe->wk_phase = (int8_t)phase;
+    }
     if (A.wk_ok) {
         A.wk_seq = seq;
         A.wk_start = start;
@@ -1028,7 +1063,7 @@ Item item_of_alignment(const UnitCtx &u, Pools &pools, int w, int32_t chrom, int
     it.end = start + tl;
     it.chrom = chrom;
     it.mlen = (int32_t)motif_s.size();
-    it.x = pools.add(w, x, motif_s, var_s);
+    it.set_x(pools.add(w, x, motif_s, var_s));
     return it;
 }
 
@@ -1074,7 +1109,7 @@ inline void canon_fill(const UnitCtx &u, const Item &it, Canon &c) {
 // share a canonical form (rotations and the reverse complement keep non-ACGT
 // symbols), so mixed pairs are unequal without building strings.
 inline bool same_canonical(const UnitCtx &u, const Item &r1, Canon &c1, const Item &r2, Canon &c2) {
-    const int64_t m1 = r1.x ? (int64_t)r1.x->motif.size() : r1.mlen, m2 = r2.x ? (int64_t)r2.x->motif.size() : r2.mlen;
+    const int64_t m1 = r1.xp ? (int64_t)r1.x()->motif.size() : r1.mlen, m2 = r2.xp ? (int64_t)r2.x()->motif.size() : r2.mlen;
     if (m1 != m2) return false;
     if (m1 == 0) return true;
     canon_fill(u, r1, c1);
@@ -1096,9 +1131,9 @@ bool try_merge(const UnitCtx &u, Pools &pools, int w, const Item &r1, Canon &c1,
     const int64_t s = std::min(r1.start, r2.start), e = std::max(r1.end, r2.end);
     const int32_t tier = std::min(tier_of(r1), tier_of(r2));
     Item mg = recompute(u, pools, w, r1.chrom, s, e, std::max<int64_t>(1, ml), tier);
-    if (mg.x->copies < (double)u.min_copies) return false;
+    if (mg.x()->copies < (double)u.min_copies) return false;
     const double base = std::max(std::max(mm_of(r1), mm_of(r2)), 0.01);
-    if (!(mg.x->mm <= base + 0.2)) return false;
+    if (!(mg.x()->mm <= base + 0.2)) return false;
     if (stats_on(2)) g_merges.fetch_add(1, std::memory_order_relaxed);
     if ((int64_t)r1.mlen == std::max<int64_t>(1, ml)) merged = mg;   // len(r1.consensus_motif)
     else merged = recompute(u, pools, w, r1.chrom, s, e, r1.mlen, tier);
@@ -1176,14 +1211,14 @@ void spec_run(const UnitCtx &u, Pools &pools, int w, const ItemVec &R, int64_t b
 // [start, end) with this motif length would be recomputed with the same
 // arguments (same result)
 inline void refine_one(const UnitCtx &u, Pools &pools, int w, Item &r) {
-    if (!r.x || r.x->mm == 0.0) return;
-    if (r.mlen > 0 && r.mlen == r.x->req_m && r.x->req_end == r.end) return;
+    if (!r.imperfect()) return;   // a strict hit, or mismatch rate 0
+    if (r.mlen > 0 && r.mlen == r.x()->req_m && r.x()->req_end == r.end) return;
     int64_t m = r.mlen;
     if (m <= 0) {
         const int64_t rc = (int64_t)std::nearbyint(copies_of(r));
         m = std::max<int64_t>(1, (r.end - r.start) / std::max<int64_t>(1, rc ? rc : 1));
     }
-    r = recompute(u, pools, w, r.chrom, r.start, r.end, m, tier_of(r));
+    r = recompute(u, pools, w, r.chrom, r.start, r.end, m, tier_of(r), &r);
 }
 
 // the fold's output, refined (the refine pass runs inside the parallel
@@ -1285,20 +1320,11 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt, Ou
     std::vector<uint8_t> by_start((size_t)K, 1);
     std::vector<int64_t> cm((size_t)K + 1, INT64_MIN);
     auto by_end = [](const Item &x, const Item &y) { return x.end < y.end; };
-    parallel_blocks(K, nt, [&](int64_t k, int w) {
-        const SpecOut &sp = spec[(size_t)k];
-        Item *const d0 = out.data() + at[(size_t)k];
-        Item *dst = d0;
-        const ItemVec &rp = rep[(size_t)k];
-        dst = std::copy(rp.begin(), rp.end(), dst);
-        if (synced[(size_t)k])
-            for (size_t q = from[(size_t)k]; q < sp.emitted.size(); ++q) *dst++ = sp.record(R, q);
+    // a chunk's largest end, its order check and its equal-start runs ordered by end
+    auto finish_chunk = [&](int64_t k) {
+        Item *const d0 = out.data() + at[(size_t)k], *const dst = out.data() + at[(size_t)k + 1];
         int64_t mx = INT64_MIN;
-        for (Item *it = d0; it < dst; ++it) {
-            if (it + 8 < dst && it[8].x) __builtin_prefetch(it[8].x);   // refine reads x->mm
-            refine_one(u, pools, w, *it);
-            mx = std::max(mx, it->end);
-        }
+        for (Item *it = d0; it < dst; ++it) mx = std::max(mx, it->end);
         cm[(size_t)k] = mx;
         for (Item *it = d0 + 1; it < dst; ++it)
             if (it[-1].start > it->start) { by_start[(size_t)k] = 0; return; }
@@ -1308,7 +1334,39 @@ ItemVec merge_fold(const UnitCtx &u0, Pools &pools, const ItemVec &R, int nt, Ou
             if (j - i > 1) std::stable_sort(i, j, by_end);
             i = j;
         }
+    };
+    // The imperfect records (the only ones refine recomputes) are few and
+    // clustered along the contig: refined inside the assembly, a chunk holding
+    // hundreds of them held its worker for milliseconds while the others idled
+    // (20 Mbp: 4.5k imperfect of 767k, 2.6k recomputes; the pass 3-6 ms, 1.5-2
+    // without them).  So the assembly copies and lists them, they are refined
+    // as one dynamic task list, and only the chunks holding them are finished
+    // after that.
+    std::vector<std::vector<int64_t>> imp((size_t)K);
+    parallel_items(K, nt, [&](int64_t k, int) {
+        const SpecOut &sp = spec[(size_t)k];
+        Item *const d0 = out.data() + at[(size_t)k];
+        Item *dst = d0;
+        const ItemVec &rp = rep[(size_t)k];
+        dst = std::copy(rp.begin(), rp.end(), dst);
+        if (synced[(size_t)k])
+            for (size_t q = from[(size_t)k]; q < sp.emitted.size(); ++q) *dst++ = sp.record(R, q);
+        for (Item *it = d0; it < dst; ++it)
+            if (it->imperfect()) imp[(size_t)k].push_back(it - out.data());
+        if (imp[(size_t)k].empty()) finish_chunk(k);
     });
+    std::vector<int64_t> todo;
+    for (auto &v : imp) todo.insert(todo.end(), v.begin(), v.end());
+    if (!todo.empty()) {
+        constexpr int64_t kPer = 8;   // records per task
+        parallel_items(((int64_t)todo.size() + kPer - 1) / kPer, nt, [&](int64_t q, int w) {
+            const int64_t a = q * kPer, b = std::min<int64_t>((int64_t)todo.size(), a + kPer);
+            for (int64_t i = a; i < b; ++i) refine_one(u, pools, w, out[(size_t)todo[(size_t)i]]);
+        });
+        parallel_items(K, nt, [&](int64_t k, int) {
+            if (!imp[(size_t)k].empty()) finish_chunk(k);
+        });
+    }
     out[at[(size_t)K]] = cur;
     refine_one(u, pools, 0, out[at[(size_t)K]]);
     cm[(size_t)K] = out[at[(size_t)K]].end;   // the last record is chunk K of its own
@@ -1440,7 +1498,7 @@ Item item_of_rec(Pools &pools, const Rec &r) {
     it.end = r.end;
     it.chrom = r.chrom;
     it.mlen = (int32_t)r.motif.size();
-    it.x = pools.add(0, x, r.motif, r.variations);
+    it.set_x(pools.add(0, x, r.motif, r.variations));
     return it;
 }
 
@@ -1452,8 +1510,8 @@ void materialize(const UnitCtx &u, const Item &it, int64_t shift, Rec &r) {   //
     r.start = it.start + shift;
     r.end = it.end + shift;
     r.length = it.end - it.start;
-    if (it.x) {
-        const Extra &x = *it.x;
+    if (it.xp) {
+        const Extra &x = *it.x();
         r.motif = x.motif;
         r.copies = x.copies;
         r.confidence = x.confidence;
@@ -1687,7 +1745,7 @@ void process_unit(const Job &job, const std::vector<int32_t> &chroms, std::vecto
                     for (size_t j = 0; j < pt.size(); ++j) {
                         if (j + 8 < pt.size()) {   // the record data of a later slot (written by other workers)
                             const Item &ahead = recs[pt[j + 8]];
-                            if (ahead.x) __builtin_prefetch(ahead.x);
+                            if (ahead.xp) __builtin_prefetch(ahead.x());
                         }
                         const uint32_t i = pt[j];
                         if (pass(i)) {
