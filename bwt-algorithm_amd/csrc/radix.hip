@@ -480,160 +480,6 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const KT *__restrict__ kin, c
     }
 }
 
-// Scatter of one large tile (BLOCK x ITEMS keys = HT histogram tiles of kSub
-// keys) in R staging rounds.  The pass's writes go out as one run per digit
-// and tile, 32 pairs long on average in an 8192-key tile: runs that short, at
-// the misaligned positions a real pass has, cap a pattern-only kernel at 3.8
-// TB/s, runs of 64 / 128 pairs at 4.25 / 4.61 TB/s (profiles/r05/
-// scatter_ceiling_r05x.json).  Ranking as in k_scatter; then round r stages
-// the pairs whose tile slot lies in [r S, (r + 1) S) -- keys and values side
-// by side, S = kT / R -- and streams that slice of the tile-sorted order out,
-// so the LDS holds S pairs however large the tile.  The histogram is not
-// changed: tile t's digit base is the prefix row of its first histogram tile
-// (HT consecutive histogram tiles are one scatter tile, in order).
-//   LATE : the values are loaded once the keys have left (the keys' registers
-//          are free then; 32 K-key tiles would spill holding both), keys and
-//          values take turns in one staging buffer, and the value rounds find a
-//          slot's global position from its digit, kept per slot in LDS
-template <class KT, class V, int BLOCK, int ITEMS, int R, bool LATE>
-__global__ __launch_bounds__(BLOCK, BLOCK == 512 ? 4 : 1) void k_scatter_big(const KT *__restrict__ kin, const V *__restrict__ vin,
-                                                       KT *__restrict__ kout, V *__restrict__ vout,
-                                                       const uint32_t *__restrict__ prefix,
-                                                       const uint32_t *__restrict__ dbase, int64_t n, int shift,
-                                                       int64_t ntiles, uint32_t *chk) {
-    constexpr int kT = BLOCK * ITEMS, NW = BLOCK / 64, S = kT / R, HT = kT / kSub;
-    static_assert(BLOCK >= 256 && BLOCK % 64 == 0, "threads 0..255 own one digit each");
-    static_assert(kT % kSub == 0 && kT % R == 0 && S % BLOCK == 0, "whole histogram tiles, whole rounds");
-    constexpr int SB = LATE ? (int)std::max(sizeof(KT), sizeof(V)) * S : (int)(sizeof(KT) + sizeof(V)) * S;
-    static_assert(sizeof(uint32_t) * (NW * 256 + 256 + 256 / 64) + SB + (LATE ? kT : 0) <= 160 * 1024,
-                  "exceeds gfx950's 160 KB of LDS per workgroup");
-    __shared__ uint32_t wcnt[NW][256];
-    __shared__ uint32_t gdelta[256];
-    __shared__ uint32_t dsum[256 / 64];
-    __shared__ __attribute__((aligned(16))) unsigned char stage[SB];
-    __shared__ uint8_t dg_s[LATE ? kT : 1];
-    KT *const ks = reinterpret_cast<KT *>(stage);
-    V *const vs = reinterpret_cast<V *>(LATE ? stage : stage + sizeof(KT) * S);
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int i = threadIdx.x; i < NW * 256; i += BLOCK) (&wcnt[0][0])[i] = 0;
-    __syncthreads();
-    const int64_t tile = xcd_tile(blockIdx.x, ntiles);
-    const int64_t tbase = tile * kT;
-    const int64_t wbase = tbase + (int64_t)wv * (ITEMS * 64);
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int lim = (int)max<int64_t>(0, min<int64_t>(n - wbase, ITEMS * 64));
-    const KT *const kw = kin + wbase + lane;
-    const V *const vw = vin ? vin + wbase + lane : nullptr;
-    KT k[ITEMS];
-    V v[ITEMS];
-    uint32_t slot[ITEMS];
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        const bool valid = i * 64 + lane < lim;
-        k[i] = valid ? kw[i * 64] : (KT)0;
-        if (!LATE && vin) v[i] = valid ? vw[i * 64] : (V)0;
-    }
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        const bool valid = i * 64 + lane < lim;
-        const uint32_t d = (uint32_t)((k[i] >> shift) & 255u);
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int bt = 0; bt < 8; ++bt) {
-            const bool bit = (d >> bt) & 1u;
-            const uint64_t bal = __ballot(bit);
-            peers &= bit ? bal : ~bal;
-        }
-        const uint32_t before = (uint32_t)__popcll(peers & lt);
-        slot[i] = valid ? wcnt[wv][d] + before : 0u;
-        __builtin_amdgcn_wave_barrier();
-        if (valid && before == 0) wcnt[wv][d] += (uint32_t)__popcll(peers);
-        __builtin_amdgcn_wave_barrier();
-    }
-    __syncthreads();
-    const int dg = threadIdx.x;
-    uint32_t cnt[NW], tot = 0, inc = 0;
-    if (dg < 256) {
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            cnt[w] = wcnt[w][dg];
-            tot += cnt[w];
-        }
-        inc = wave_incl_scan<uint32_t>(tot);
-        if (lane == 63) dsum[wv] = inc;
-    }
-    __syncthreads();
-    if (dg < 256) {
-        uint32_t toff = inc - tot;
-        for (int w = 0; w < wv; ++w) toff += dsum[w];
-        gdelta[dg] = dbase[dg] + prefix[tile * HT * 256 + dg] - toff;
-        uint32_t b = toff;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            wcnt[w][dg] = b;
-            b += cnt[w];
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i)
-        if (i * 64 + lane < lim) slot[i] += wcnt[wv][(uint32_t)((k[i] >> shift) & 255u)];
-    const int64_t rem = n - tbase;
-    const int cntt = rem < kT ? (int)rem : kT;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        if (r) __syncthreads();   // the previous slice has left the staging buffers
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i) {
-            const uint32_t s = slot[i] - (uint32_t)(r * S);   // (wraps below the slice)
-            if (i * 64 + lane < lim && s < (uint32_t)S) {
-                ks[s] = k[i];
-                if (!LATE && vin) vs[s] = v[i];
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < S / BLOCK; ++q) {
-            const int jl = q * BLOCK + threadIdx.x, j = r * S + jl;
-            if (j < cntt) {
-                const KT key = ks[jl];
-                const uint32_t d = (uint32_t)((key >> shift) & 255u);
-                const uint32_t p = gdelta[d] + (uint32_t)j;
-                if constexpr (LATE) dg_s[j] = (uint8_t)d;
-                if (chk && (int64_t)p >= n) {
-                    atomicOr(chk, kChkScatter);
-                    continue;
-                }
-                kout[p] = key;
-                if (!LATE && vout) vout[p] = vs[jl];
-            }
-        }
-    }
-    if constexpr (LATE) {
-        if (!vin) return;   // (uniform)
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i) v[i] = i * 64 + lane < lim ? vw[i * 64] : (V)0;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            __syncthreads();   // the staging buffer's last readers are done
-#pragma unroll
-            for (int i = 0; i < ITEMS; ++i) {
-                const uint32_t s = slot[i] - (uint32_t)(r * S);
-                if (i * 64 + lane < lim && s < (uint32_t)S) vs[s] = v[i];
-            }
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < S / BLOCK; ++q) {
-                const int jl = q * BLOCK + threadIdx.x, j = r * S + jl;
-                if (j < cntt) {
-                    const uint32_t p = gdelta[dg_s[j]] + (uint32_t)j;
-                    if (!chk || (int64_t)p < n) vout[p] = vs[jl];
-                }
-            }
-        }
-    }
-}
-
 // The look-back state of a context: the granule buffer (shared by the
 // histogram and scan launches, which never overlap on one stream), the ticket
 // counter and a fresh epoch per launch.  A (re)allocated granule buffer is
@@ -678,43 +524,6 @@ void launch_hist(Ctx &c, const KT *keys, int64_t n, int shift, int64_t ntiles, u
             ((uintptr_t)keys & 15) == 0 ? 1 : 0, c.checks());
 }
 
-// The scatter of one 16- or 32-bit-key pass in tiles of 16 K or 32 K keys
-// (BWTMI_RADIX_TILE = 16 / 32, 17 = 16 with the values loaded beside the keys;
-// 8 or 0: the 8 K-key k_scatter); false when the
-// caller's k_scatter runs instead.
-template <class KT, class V>
-bool launch_scatter_big(Ctx &c, const char *name, double bytes, const KT *kin, const V *vin, KT *kout, V *vout,
-                        const uint32_t *prefix, const uint32_t *base, int64_t n, int sh) {
-    static_assert(sizeof(KT) <= 4 && sizeof(V) == 4, "16- and 32-bit keys, 32-bit values");
-    const int64_t t = knob(KN_RADIX_TILE);
-    if constexpr (sizeof(KT) == 4) {   // 512 x 32 staged in 2 rounds: 2 workgroups per CU
-        if (t == 18) {
-            const int64_t nt = (n + 16383) / 16384;
-            KLAUNCH(name, bytes, (k_scatter_big<KT, V, 512, 32, 2, true>), dim3((unsigned)nt), dim3(512), 0, c.stream,
-                    kin, vin, kout, vout, prefix, base, n, sh, nt, c.checks());
-            return true;
-        }
-    }
-    if (t == 16 || t == 17) {   // 17: values loaded with the keys
-        const int64_t nt = (n + 16383) / 16384;
-        if (t == 16)
-            KLAUNCH(name, bytes, (k_scatter_big<KT, V, 1024, 16, 1, true>), dim3((unsigned)nt), dim3(1024), 0, c.stream,
-                    kin, vin, kout, vout, prefix, base, n, sh, nt, c.checks());
-        else
-            KLAUNCH(name, bytes, (k_scatter_big<KT, V, 1024, 16, 1, false>), dim3((unsigned)nt), dim3(1024), 0, c.stream,
-                    kin, vin, kout, vout, prefix, base, n, sh, nt, c.checks());
-        return true;
-    }
-    if constexpr (sizeof(KT) == 4) {   // (16-bit keys spill at 32 items a thread)
-        if (t != 32) return false;
-        const int64_t nt = (n + 32767) / 32768;
-        KLAUNCH(name, bytes, (k_scatter_big<KT, V, 1024, 32, 2, true>), dim3((unsigned)nt), dim3(1024), 0, c.stream, kin,
-                vin, kout, vout, prefix, base, n, sh, nt, c.checks());
-        return true;
-    }
-    return false;
-}
-
 template <class KT, class V, int BLOCK, int ITEMS, bool NT, bool SPLIT>
 void radix_sort_cfg(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
     constexpr int kT = BLOCK * ITEMS;
@@ -747,12 +556,8 @@ void radix_sort_cfg(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
         const char *name = sizeof(KT) == 2 ? "radix_scatter_kv6" : sizeof(KT) == 4 ? "radix_scatter_kv8"
                            : sizeof(V) == 4 ? "radix_scatter_kv12" : "radix_scatter_kv16";
         const double bytes = (double)n * 2.0 * ((double)sizeof(KT) + (vals ? (double)sizeof(V) : 0.0));
-        bool big = false;
-        if constexpr (sizeof(KT) <= 4 && sizeof(V) == 4)
-            big = vals && launch_scatter_big<KT, V>(c, name, bytes, ka, va, kb, vb, prefix, base, n, sh);
-        if (!big)
-            KLAUNCH(name, bytes, (k_scatter<KT, V, BLOCK, ITEMS, NT, SPLIT>), dim3((unsigned)ntiles), dim3(BLOCK), 0,
-                    c.stream, ka, va, kb, vb, prefix, base, n, sh, ntiles, c.checks(), more ? dg : nullptr, sh + 8);
+        KLAUNCH(name, bytes, (k_scatter<KT, V, BLOCK, ITEMS, NT, SPLIT>), dim3((unsigned)ntiles), dim3(BLOCK), 0,
+                c.stream, ka, va, kb, vb, prefix, base, n, sh, ntiles, c.checks(), more ? dg : nullptr, sh + 8);
         std::swap(ka, kb);
         std::swap(va, vb);
         ++passes;
@@ -770,7 +575,12 @@ void radix_sort_cfg(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
 // and value staging 0.44-0.45; nontemporal stores 0.34-0.41 in every geometry.
 // r01ak, same box session for every variant: 512x16 0.50, 256x16 0.47, 512x8
 // 0.47, 1024x4 0.47, 256x20 0.48, 1024x8 0.44, 256x32 0.43; r02w (32-bit keys):
-// 512x32, 256x32, 1024x16, 512x24 within 5 % of 512x16.
+// 512x32, 256x32, 1024x16, 512x24 within 5 % of 512x16.  r06l/r06m (C3, same
+// box): 16 K / 32 K-key tiles staged in LDS rounds, which lengthen each digit's
+// written run 2-4x, are slower -- 1024x16 2.05-2.17 ms per step, 1024x32 2.33,
+// 512x32 in two rounds (2 workgroups per CU) 1.80, against 1.54-1.56 for 512x16:
+// with one or two workgroups per CU the ranking and the streaming phases of a
+// CU's workgroups no longer overlap (profiles/r06/radix_tiles).
 template <class KT, class V>
 void radix_sort_impl(Ctx &c, KT *keys, V *vals, int64_t n, int bit0, int bit1) {
     if (n <= 1) return;
@@ -832,11 +642,9 @@ void radix_pass_k32(Ctx &c, const uint32_t *kin, const uint32_t *vin, uint32_t *
     const int64_t ntiles = (n + kT - 1) / kT;
     uint32_t *prefix, *base;
     launch_hist<uint32_t>(c, kin, n, shift, ntiles, &prefix, &base);
-    if (!launch_scatter_big<uint32_t, uint32_t>(c, "radix_partition_kv8", (double)n * 16.0, kin, vin, kout, vout,
-                                                prefix, base, n, shift))
-        KLAUNCH("radix_partition_kv8", (double)n * 16.0, (k_scatter<uint32_t, uint32_t, BLOCK, ITEMS, false, true>),
-                dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, kin, vin, kout, vout, prefix, base, n, shift, ntiles,
-                c.checks());
+    KLAUNCH("radix_partition_kv8", (double)n * 16.0, (k_scatter<uint32_t, uint32_t, BLOCK, ITEMS, false, true>),
+            dim3((unsigned)ntiles), dim3(BLOCK), 0, c.stream, kin, vin, kout, vout, prefix, base, n, shift, ntiles,
+            c.checks());
     HIPCHECK(hipGetLastError());
 }
 

@@ -598,21 +598,6 @@ def test_radix_histogram_geometries(gpu_ctx, S):
         _check_index(synth.generate_contig(300_000, 99 + S) + b"$")
 
 
-@pytest.mark.parametrize("T", [16, 17, 18, 32])
-def test_radix_scatter_tiles(gpu_ctx, T):
-    """16 K- and 32 K-key scatter tiles (BWTMI_RADIX_TILE; 17 = values loaded
-    with the keys): the 32-bit and 16-bit key passes of the candidate sorts,
-    the 8-mer hash and the suffix sorts give the oracle's results, with partial
-    last tiles and the device checks on."""
-    from bwtmi import _lib, synth
-    with _lib.knobs(RADIX_TILE=T, DEVICE_CHECKS=1):
-        _same(_planted(300_000, 195 + T), 1, 1000, 3)
-        _same(_planted(40_000, 17 + T, b"ACGTNRY"), 1, 200, 2)
-        _check_index(synth.generate_contig(400_000, 196 + T, gaps="n1") + b"$")
-        _check_index(synth.generate_contig(300_001, 199 + T) + b"$")
-        _check_index(synth.shared_prefix_runs(b"ACGT", 5 + T) + b"$")
-
-
 def test_small_alphabet_texts_through_general_doubling(gpu_ctx):
     """BWTMI_SA_SMALL=0: gap texts take the general prefix doubling (index.hip)
     instead of the 3-bit string sort; the same arrays as the oracle."""
