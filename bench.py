@@ -248,6 +248,8 @@ def main():
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--host-load", action="store_true",
                     help="whole-file load on the host + upload (default: built on the device from the file image)")
+    ap.add_argument("--sync-write", action="store_true",
+                    help="write each step's file before the step ends (bwtmi_job_write) instead of behind the next step")
     ap.add_argument("--pmc-summary", default=None,
                     help="tools/pmc_traffic.py output giving HBM bytes per launch (roofline.traffic)")
     a = ap.parse_args()
@@ -320,10 +322,17 @@ def main():
             # all-reduces of per-unit sizes; no record leaves its GPU
             timed("write", dist.write_sharded, c, job, "strfinder", out)
         else:
-            timed("write", job.write, "strfinder", out)     # repeat.tab, as the CLI writes it
+            # repeat.tab, as the CLI writes it; the call returns once the rows are
+            # formatted and the job's writer finishes the file behind the next
+            # step's load and scan (bwtmi_job_write_async).  The next step joins it
+            # before rewriting the file ("write_join"), and sync() joins the last
+            # one inside the timed region, so every step's file is whole in it.
+            timed("write_join", job.write_join)
+            timed("write", job.write, "strfinder", out, not a.sync_write)
         timed("index_wait", job.wait, ctx)    # the FM index build ran behind the host work
 
     def sync():
+        job.write_join()
         _lib.lib().bwtmi_device_sync(local)
         if c is not None:
             c.barrier()
@@ -463,7 +472,11 @@ def main():
                    + "; FASTA read -> FM index + strict scan + post-processing -> STRfinder repeat.tab closed",
                    "contig_bp": wl["lengths"][0], "contigs": len(wl["lengths"]) * (1 if shared else world),
                    "parallelism": f"contig-shard x{world}", "index": not a.no_index,
-                   "load": "host" if a.host_load else "device"},
+                   "load": "host" if a.host_load else "device",
+                   "write": ("sharded pwrite in the step" if shared and world > 1 else
+                             "in the step" if a.sync_write else
+                             "finished behind the next step's load and scan, joined before the file "
+                             "is rewritten and before the timed region ends")},
         "roofline": roofline,
         "e2e_roofline": {"b_alg_bytes_per_base": B_ALG_PER_BASE, "achieved_gbs": round(e2e_gbs, 2),
                          "peak_gbs": HBM_PEAK_GBS * world, "frac": round(e2e_gbs / (HBM_PEAK_GBS * world), 6)},

@@ -91,6 +91,8 @@ _SIGS = {
     "bwtmi_job_count": (C.c_int64, [_P]),
     "bwtmi_job_render": (C.c_int, [_P, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
     "bwtmi_job_write": (C.c_int, [_P, C.c_int, C.c_char_p]),
+    "bwtmi_job_write_async": (C.c_int, [_P, C.c_int, C.c_char_p]),
+    "bwtmi_job_write_join": (C.c_int, [_P]),
     "bwtmi_job_unit_count": (C.c_int32, [_P]),
     "bwtmi_job_unit_rows": (C.c_int, [_P, _P]),
     "bwtmi_job_render_units": (C.c_int, [_P, C.c_int, _P, _P]),

@@ -283,12 +283,20 @@ class Job:
         finally:
             lib().bwtmi_free(p)
 
-    def write(self, fmt: str, path: str) -> None:
+    def write(self, fmt: str, path: str, background: bool = False) -> None:
+        """Write the file (bwtmi_job_write).  background=True returns once the
+        rows are formatted and the job's writer finishes the file behind the
+        caller (bwtmi_job_write_async): write_join() waits for it and raises
+        its error; the next write and the job's release join it first."""
         from . import profile
         with profile.stage("write"):
-            check(lib().bwtmi_job_write(self.h, _lib.FMT[fmt], path.encode()))
-        if profile.active() is not None:
+            fn = lib().bwtmi_job_write_async if background else lib().bwtmi_job_write
+            check(fn(self.h, _lib.FMT[fmt], path.encode()))
+        if profile.active() is not None and not background:
             profile.active().add_bytes("write", os.path.getsize(path))
+
+    def write_join(self) -> None:
+        check(lib().bwtmi_job_write_join(self.h))
 
     # ---- sharded output (bwtmi.dist.write_sharded)
     def unit_count(self) -> int:

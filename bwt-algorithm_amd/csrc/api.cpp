@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cctype>
+#include <condition_variable>
 #include <cstring>
 #include <exception>
 #include <fcntl.h>
@@ -203,6 +204,98 @@ static void pwrite_parts(const char *path, bool whole, const std::vector<Text> &
     if (!out.finish(whole, at.back())) fail(BWTMI_E_IO, "short write to %s", path);
 }
 
+// One output file written by its own writer thread while the rows are being
+// formatted (bwtmi_job_write, bwtmi_job_write_async).  The formatting tasks
+// mark their part done; the writer pwritev's every run of consecutive done
+// parts in file order, the header first -- ONE writer, since buffered writes
+// to one file serialise on its inode lock (pwrite_run).  The content is that
+// of one open(path, 'w') + write: the file is overwritten in place and cut to
+// its size at the end (a short write or an error cuts it to 0).
+struct FileWrite {
+    OutFd out;
+    std::string path;
+    Rendered R;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<uint8_t> done;
+    size_t next = 0, off = 0;
+    bool started = false, rendered = false, aborted = false, header_done = false, bad = false;
+    std::thread th;
+    explicit FileWrite(const char *p) : out(p), path(p) {}
+    ~FileWrite() {
+        if (th.joinable()) {
+            abort();
+            th.join();
+        }
+    }
+    void part_done(size_t k) {   // (render_rows sized R.parts before the first part)
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!started) {
+                done.assign(R.parts.size(), 0);
+                started = true;
+            }
+            done[k] = 1;
+        }
+        cv.notify_one();
+    }
+    void render_done() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            rendered = true;
+        }
+        cv.notify_one();
+    }
+    void abort() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            rendered = aborted = true;
+        }
+        cv.notify_one();
+    }
+    void run() {
+        std::unique_lock<std::mutex> lk(mu);
+        std::vector<const char *> wp;
+        std::vector<size_t> wn;
+        auto ready = [&] { return started && next < done.size() && done[next]; };
+        for (;;) {
+            cv.wait(lk, [&] { return aborted || rendered || (started && !header_done) || ready(); });
+            if (aborted) return;
+            if (!header_done) {   // the header exists once a part or the whole render is done
+                header_done = true;
+                const char *hp = R.header.data();
+                const size_t hn = R.header.size();
+                off = hn;
+                lk.unlock();
+                if (!pwrite_run(out.fd, &hp, &hn, 1, 0)) bad = true;
+                lk.lock();
+                continue;
+            }
+            if (ready()) {
+                const size_t at = off;
+                wp.clear();
+                wn.clear();
+                while (ready()) {
+                    wp.push_back(R.parts[next].data());
+                    wn.push_back(R.parts[next].size());
+                    off += R.parts[next].size();
+                    ++next;
+                }
+                lk.unlock();
+                if (!pwrite_run(out.fd, wp.data(), wn.data(), wp.size(), at)) bad = true;
+                lk.lock();
+                continue;
+            }
+            if (rendered) return;   // every part is done and written
+        }
+    }
+    // wait for the writer, cut the file to its size and close it; false on a short write
+    bool finish() {
+        if (th.joinable()) th.join();
+        return !bad && !aborted && out.finish(true, off);
+    }
+};
+
 }  // namespace bwtmi
 
 using namespace bwtmi;
@@ -217,7 +310,30 @@ struct bwtmi_index {
 struct bwtmi_job {
     Job j;
     JobDev dev;
+    std::unique_ptr<FileWrite> wr;   // a file still being written (bwtmi_job_write_async)
 };
+
+namespace {
+// the job's file write in flight, if any: wait for it and report its error
+void write_join(bwtmi_job *job) {
+    if (!job->wr) return;
+    std::unique_ptr<FileWrite> w = std::move(job->wr);
+    if (!w->finish()) fail(BWTMI_E_IO, "short write to %s", w->path.c_str());
+}
+// format the job's rows into `path`, the writer thread writing behind the
+// formatting; returns with the writer still running (job->wr)
+void write_start(bwtmi_job *job, int fmt, const char *path) {
+    pool_spin_for_job(job->j);
+    job->j.text_join();
+    auto w = std::make_unique<FileWrite>(path);
+    FileWrite *f = w.get();
+    f->th = std::thread([f] { f->run(); });
+    const std::function<void(size_t)> on_part = [f](size_t k) { f->part_done(k); };
+    render_rows(job->j, fmt, nullptr, f->R, &on_part);   // (throws: ~FileWrite stops the writer, cuts the file)
+    f->render_done();
+    job->wr = std::move(w);
+}
+}  // namespace
 
 // readers of contig bytes join a deferred host pass first (bwtmi_job_load_fasta_dev)
 #define TEXT_JOIN(job) const_cast<bwtmi_job *>(job)->j.text_join()
@@ -638,6 +754,7 @@ int bwtmi_job_free(bwtmi_job *job) {
     return guard([&] {
         if (!job) return;
         if (job->j.text_th.joinable()) job->j.text_th.join();   // its error dies with the job
+        if (job->wr) (void)job->wr->finish();   // a file still being written is finished (its error dies too)
         if (job->dev.bg_ctx) ctx_join(*job->dev.bg_ctx);   // its error stays for the ctx's next call
         if (job->dev.device >= 0) (void)hipSetDevice(job->dev.device);
         for (auto &d : job->dev.seqs) d.buf.release();
@@ -1293,70 +1410,36 @@ int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len) {
     });
 }
 
-// The file is written while it is being formatted: a part whose predecessors
-// are all formatted has a known offset, and the thread that completes the
-// prefix writes the parts it extends it by.  The content is that of one
-// open(path, 'w') + write (the file is overwritten in place, then cut).
+// The file is written while it is being formatted (FileWrite): a part whose
+// predecessors are all formatted has a known offset, and the writer thread
+// writes each run of such parts as it completes.
 int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path) {
     return guard([&] {
         BWTMI_STAGE("bwtmi:write");
         CHECK_ARG(job && path, "null argument");
-        pool_spin_for_job(job->j);
-        TEXT_JOIN(job);
-        OutFd out(path);
-        const int fd = out.fd;
-        Rendered R;
-        // The parts are written in file order as they complete, by ONE writer at
-        // a time with large pwritev calls (buffered writes to one file serialise
-        // on its inode lock: concurrent writers only contend, pwrite_run).  The
-        // thread that completes the next part in order becomes the writer while
-        // no other is; it keeps writing every run of completed parts, and the
-        // formatting threads meanwhile only mark theirs done.
-        std::mutex mu;
-        std::vector<uint8_t> done;
-        size_t next = 0, off = 0;
-        bool writing = false;
-        std::atomic<bool> bad{false};
-        std::vector<const char *> wp;
-        std::vector<size_t> wn;
-        auto write_header = [&] {
-            const char *hp = R.header.data();
-            const size_t hn = R.header.size();
-            return pwrite_run(fd, &hp, &hn, 1, 0);
-        };
-        const std::function<void(size_t)> on_part = [&](size_t k) {
-            std::unique_lock<std::mutex> lk(mu);
-            if (done.empty()) {   // first call: the parts vector and the header exist
-                done.assign(R.parts.size(), 0);
-                off = R.header.size();
-                if (!write_header()) bad = true;
-            }
-            done[k] = 1;
-            if (writing) return;   // the writer will take this part
-            writing = true;
-            while (next < done.size() && done[next]) {
-                const size_t at = off;
-                wp.clear();
-                wn.clear();
-                while (next < done.size() && done[next]) {
-                    wp.push_back(R.parts[next].data());
-                    wn.push_back(R.parts[next].size());
-                    off += R.parts[next].size();
-                    ++next;
-                }
-                lk.unlock();
-                if (!pwrite_run(fd, wp.data(), wn.data(), wp.size(), at)) bad = true;
-                lk.lock();
-            }
-            writing = false;
-        };
-        render_rows(job->j, fmt, nullptr, R, &on_part);
-        if (done.empty()) {   // no rows: the header alone
-            if (!write_header()) bad = true;
-            off = R.header.size();
-        }
-        if (bad) fail(BWTMI_E_IO, "short write to %s", path);   // ~OutFd cuts the file to 0
-        if (!out.finish(true, off)) fail(BWTMI_E_IO, "short write to %s", path);
+        write_join(job);
+        write_start(job, fmt, path);
+        write_join(job);
+    });
+}
+
+// The same, returning once every row is formatted: the writer finishes the
+// file behind the caller.  bwtmi_job_write_join waits for it and returns its
+// error; every later write of the job, and bwtmi_job_free, joins it first.
+int bwtmi_job_write_async(bwtmi_job *job, int fmt, const char *path) {
+    return guard([&] {
+        BWTMI_STAGE("bwtmi:write");
+        CHECK_ARG(job && path, "null argument");
+        write_join(job);
+        write_start(job, fmt, path);
+    });
+}
+
+int bwtmi_job_write_join(bwtmi_job *job) {
+    return guard([&] {
+        BWTMI_STAGE("bwtmi:write_join");
+        CHECK_ARG(job, "null argument");
+        write_join(job);
     });
 }
 

@@ -4,6 +4,8 @@
 // Python's "{x:.Nf}" and C's "%.Nf" both print the exact binary value rounded
 // half-to-even, so numeric columns are byte-identical.
 #include <algorithm>
+#include <map>
+#include <thread>
 #include <optional>
 #include <chrono>
 #include <cinttypes>
@@ -700,7 +702,12 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
     auto t2 = std::chrono::steady_clock::now();
     std::optional<StageRange> fr;
     fr.emplace("bwtmi:format");
+    // BWTMI_STATS=3: per-chunk timeline (thread, formatting, on_part) of this stage
+    struct Tl { double a, b, c; size_t th; };
+    std::vector<Tl> tl(stats_on(3) ? chunks.size() : 0);
+    auto now_ms = [t2] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count(); };
     run_tasks((int64_t)chunks.size(), host_threads(job.params), [&](int64_t ck) {
+        if (!tl.empty()) { tl[(size_t)ck].a = now_ms(); tl[(size_t)ck].th = std::hash<std::thread::id>()(std::this_thread::get_id()); }
         Out o;
         const Chunk &C = chunks[(size_t)ck];
         const int64_t a = C.a, b = C.b;
@@ -766,10 +773,28 @@ void render_rows(Job &job, int fmt, const int64_t *row_base, Rendered &out,
             }
         }
         out.parts[(size_t)ck] = o.finish();
+        if (!tl.empty()) tl[(size_t)ck].b = now_ms();
         if (on_part) (*on_part)((size_t)ck);
+        if (!tl.empty()) tl[(size_t)ck].c = now_ms();
     });
     fr.reset();
     auto t3 = std::chrono::steady_clock::now();
+    if (!tl.empty()) {
+        std::map<size_t, std::pair<double, double>> busy;   // thread -> (formatting, on_part)
+        double first = 1e30, last = 0, lastfmt = 0;
+        for (const Tl &x : tl) {
+            busy[x.th].first += x.b - x.a;
+            busy[x.th].second += x.c - x.b;
+            first = std::min(first, x.a);
+            last = std::max(last, x.c);
+            lastfmt = std::max(lastfmt, x.b);
+        }
+        std::string per;
+        for (auto &kv : busy) per += " " + std::to_string((int)(kv.second.first * 100) / 100.0).substr(0, 4) + "/" +
+                                     std::to_string((int)(kv.second.second * 100) / 100.0).substr(0, 4);
+        std::fprintf(stderr, "  format timeline: %zu chunks, first start %.2f, last format end %.2f, last end %.2f ms; "
+                     "threads (format/on_part ms):%s\n", tl.size(), first, lastfmt, last, per.c_str());
+    }
     job.stage_ms[6] = std::chrono::duration<double, std::milli>(t3 - t0).count();
     if (stats_on()) {
         auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };

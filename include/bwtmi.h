@@ -237,6 +237,16 @@ int64_t bwtmi_job_count(const bwtmi_job *job);
 /* render a format into a malloc'd buffer (free with bwtmi_free) or a file */
 int bwtmi_job_render(bwtmi_job *job, int fmt, char **out, int64_t *len);
 int bwtmi_job_write(bwtmi_job *job, int fmt, const char *path);
+/* bwtmi_job_write returning once every row is formatted: the job's writer
+ * thread finishes the file behind the caller (the header and each run of
+ * formatted rows are written as they complete, in file order).
+ * bwtmi_job_write_join waits for it and returns its error (BWTMI_E_IO: the file
+ * is cut to 0 bytes); the job's next write or write_async, and bwtmi_job_free,
+ * join it first (free drops the error).  Not in the reference: a caller that
+ * writes one file per job (bwt.py:4141-4198) can overlap the file's tail with
+ * its next job's load and scan. */
+int bwtmi_job_write_async(bwtmi_job *job, int fmt, const char *path);
+int bwtmi_job_write_join(bwtmi_job *job);
 /* Sharded output (one process per GPU, each owning whole fold units = contigs
  * with equal natural sort keys, bwt.py:22-36): the file is the concatenation,
  * in unit order, of every unit's rows (bwt.py:4147-4150), so each rank writes

@@ -622,6 +622,56 @@ def test_job_write_streams_the_rendered_file(tmp_path, built_lib):
     assert out.read_bytes() == j.render("bed")
 
 
+def test_job_write_in_background(tmp_path, built_lib):
+    """bwtmi_job_write_async: the call returns with the file's writer still
+    running; write_join gives the same file as bwtmi_job_write (over a longer
+    stale file), the job's next write joins the previous one first (the same
+    path rewritten back to back, another format), the job's records can be
+    reset and refilled while the file is finished, a freed job finishes its
+    file, and a failed write reports BWTMI_E_IO at the join."""
+    from bwtmi import synth
+    from bwtmi.records import Job
+    from bwtmi._lib import BwtmiError
+    seq = synth.generate_contig(300_000, 5, 0.02)
+    hits = oracle.strict_scan(seq[30:-30], 1, 1000, 0, 3)
+    out = tmp_path / "repeat.tab"
+    j = Job(min_copies=3, show_progress=True, threads=4)
+    j.add_contig("c1", seq, 30, 30)
+    j.add_hits(0, hits)
+    j.postprocess()
+    want = {f: j.render(f) for f in ("strfinder", "vcf", "bed")}
+    out.write_bytes(b"x" * (len(want["strfinder"]) + 999))
+    j.write("strfinder", str(out), background=True)
+    j.write_join()
+    assert out.read_bytes() == want["strfinder"]
+    for f in ("vcf", "strfinder", "bed"):   # each joins the one before
+        j.write(f, str(out), background=True)
+    j.write_join()
+    assert out.read_bytes() == want["bed"]
+    j.write("strfinder", str(out), background=True)
+    j.reset()                                   # the rendered rows belong to the writer
+    j.add_hits(0, hits[: len(hits) // 2])
+    j.postprocess()
+    j.write_join()
+    assert out.read_bytes() == want["strfinder"]
+    half = j.render("vcf")
+    j.write("vcf", str(out), background=True)
+    del j                                       # bwtmi_job_free finishes the file
+    assert out.read_bytes() == half
+    j = Job(min_copies=3)
+    j.add_contig("e", b"ACGT", 0, 0)
+    j.postprocess()
+    j.write("bed", str(out), background=True)
+    j.write_join()
+    assert out.read_bytes() == j.render("bed")
+    j.write_join()                              # nothing in flight: a no-op
+    full = "/dev/full"
+    if os.path.exists(full):                    # writes to /dev/full fail with ENOSPC
+        j.write("bed", full, background=True)
+        with pytest.raises(BwtmiError):
+            j.write_join()
+
+
 def test_bench_launches_n_ranks_without_a_launcher(tmp_path):
     """`bench.py --gpus N` with no WORLD_SIZE starts N rank processes with the
     launcher environment, each rank runs the body (here: a host-transport
