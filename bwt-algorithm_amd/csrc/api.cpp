@@ -1175,6 +1175,13 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
             if (P.min_copies <= 0) continue;                         // worker raises -> [] (bwt.py:3137)
             todo.push_back(i);
         }
+        // the screen drops hits only the final filter would see (nested.hip) for a
+        // contig that is a fold unit of its own: in a unit of several contigs the
+        // records interleave by position, and another contig's record between two
+        // breaks their merge chain (bwt.py:3222-3289)
+        J.assign_units();
+        std::vector<int32_t> unit_size((size_t)std::max<int32_t>(1, J.nunits), 0);
+        for (const Contig &ct : J.contigs) ++unit_size[(size_t)ct.unit];
         auto scan_one = [&](Ctx &lc, size_t i) {
             const Contig &ct = J.contigs[i];
             const int64_t len = ct.trimmed_len();
@@ -1195,7 +1202,8 @@ int bwtmi_job_scan(bwtmi_ctx *ctx, bwtmi_job *job) {
                          "injected failure (BWTMI_FAIL_CONTIG)");
                 strict_scan_device(lc, job->dev.seqs[i].buf.as<uint8_t>(), len, 1,
                                    (int32_t)std::min<int64_t>(U, INT32_MAX), P.min_copies, r,
-                                   screen && !t3 && len < (int64_t)UINT32_MAX);   // 32-bit hit lengths
+                                   screen && !t3 && len < (int64_t)UINT32_MAX,   // 32-bit hit lengths
+                                   unit_size[(size_t)ct.unit] == 1 ? P.min_copies : 0);
             } catch (const Error &e) {
                 if (e.code == BWTMI_E_HIP) throw;
                 J.errors[i] = e.msg;

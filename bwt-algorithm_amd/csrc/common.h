@@ -452,7 +452,7 @@ enum Knob {
     KN_RUNS_DENSE, KN_RUNS_UNTILED, KN_SA_SMALL, KN_SEG_LEVELS, KN_SCREEN_WIDE, KN_FM_BYTES, KN_LS_CAP,
     KN_HOST_SCREEN, KN_NO_PLAIN, KN_INDEX_LANES, KN_SCAN_LANES, KN_NO_AVX512, KN_POOL_SPIN_US,
     KN_UNIT_GROUP_THREADS, KN_STATS, KN_NUMA_BIND, KN_NUMA_SMT, KN_FAIL_MERGE_CHUNK, KN_HIST_S, KN_DEVICE_CHECKS,
-    KN_COUNT
+    KN_SCREEN_DROP, KN_COUNT
 };
 // a roctx range for the lifetime of the object (trace.cpp); names "bwtmi:<stage>"
 struct StageRange {

@@ -345,8 +345,9 @@ struct ScanResult {
 // d_text: device copy of the trimmed contig (n bytes, padded by >= 64 bytes).
 // screen: also run nested suppression + (start, end) sort + dedup on the
 // device (nested.hip) and return only the survivors, in that order.
+// drop_min_copies: passed to the screen (screen_hits_device)
 void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
-                        int32_t min_copies, ScanResult &out, bool screen = false);
+                        int32_t min_copies, ScanResult &out, bool screen = false, int32_t drop_min_copies = 0);
 // max_mismatch > 0: hits in emission order (host vector)
 void strict_scan_mm_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
                            int32_t max_mismatch, int32_t min_copies, HitVec &hits);
@@ -354,8 +355,10 @@ void strict_scan_mm_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min
 // ----- nested suppression / sort / dedup of one contig's strict hits (nested.hip)
 // maxlen: the hits' longest span, when the caller knows it (the strict scan's
 // compaction reduces it and reads it with the hit count); -1: reduced here
+// drop_min_copies > 0: also drop the kept hits the post-processing would only
+// carry to its final filter (k_drop_flags; the job's min_copies)
 void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
-                        ScreenedVec &out, int64_t maxlen = -1);
+                        ScreenedVec &out, int64_t maxlen = -1, int32_t drop_min_copies = 0);
 
 // ----- suffix array + BWT of ACGT* '$' texts (sa_dna.hip)
 bool sa_dna_eligible(uint8_t last, int64_t n, const int64_t *totals);

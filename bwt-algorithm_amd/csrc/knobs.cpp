@@ -27,6 +27,7 @@ constexpr KnobDef kDefs[KN_COUNT] = {
     {"NO_PLAIN", 0},            {"INDEX_LANES", 4},      {"SCAN_LANES", 4},     {"NO_AVX512", 0},
     {"POOL_SPIN_US", -1},       {"UNIT_GROUP_THREADS", 4}, {"STATS", 0},        {"NUMA_BIND", 0},
     {"NUMA_SMT", 0},            {"FAIL_MERGE_CHUNK", -1}, {"HIST_S", 0},         {"DEVICE_CHECKS", 0},
+    {"SCREEN_DROP", 1},
 };
 
 

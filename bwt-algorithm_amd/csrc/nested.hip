@@ -468,6 +468,68 @@ __global__ void k_final_flags(const int64_t *__restrict__ S, const int64_t *__re
     flag[k] = f ? 1u : 0u;
 }
 
+// ---- records the post-processing would only carry to its final filter.
+// A kept hit that fails the final filter on its own (bwt.py:3940-3944:
+// (end - start) // prim < min_copies or end - start < 6 -- an unmerged strict
+// record keeps its span and copies) and that no other record can reach leaves
+// the output unchanged when it is dropped here:
+//   merge (bwt.py:3222-3289): a merge needs same canonical motifs (equal
+//     motif lengths M) within a gap of M + 1.  A record built from records
+//     before the hit ends at most at max(e, s + M min_copies) + 2 ext(M) of
+//     one of them (the recompute's walk limit, motif.cpp / post.cpp, once for
+//     the merge and once for the refine; ext(M) = max(3M, 4 min(10, M/2 or 1))),
+//     A one-base record is the closed form: the run of its first base through
+//     its start, capped at the walk limit -- a unit-1 strict hit is a maximal
+//     run, so a record built from such hits ends at its first hit's end, and
+//     it has no mismatches to refine: its bound is its end.
+//     So with R = max over the earlier kept hits of that bound,
+//     start - R > M_hit + 1 keeps every earlier record out of reach; with
+//     next.start - end > max(M_hit, M_next) + 1 the hit merges with nothing
+//     after it, and neither does the record before it once it is gone (the
+//     removed hit's own gap lies between them);
+//   collapse (bwt.py:3499-3513) needs an overlap: the hit overlaps nothing, and
+//     nothing that was separated by it overlaps after it is gone.
+// R over the kept hits in screen order is an inclusive prefix max of reach()
+// (non-kept entries contribute nothing); cidx lists the kept hits' ranks, so
+// the next kept hit of rank k is cidx[pos[k] + 1].
+__device__ __forceinline__ int64_t screen_reach(int64_t s, int64_t e, int64_t m, int32_t mc) {
+    if (m == 1) return e;
+    const int64_t mi = m >= 4 ? min<int64_t>(10, m / 2) : 1;
+    const int64_t ext = max<int64_t>(3 * m, 4 * mi);
+    return max(e, s + m * (int64_t)mc) + 2 * ext;
+}
+__global__ void k_drop_reach(const int64_t *__restrict__ S, const int64_t *__restrict__ E,
+                             const int32_t *__restrict__ M, const uint32_t *__restrict__ flag,
+                             const uint32_t *__restrict__ pos, int64_t n, int32_t mc, int64_t *__restrict__ R,
+                             uint32_t *__restrict__ cidx) {
+    const int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (k >= n) return;
+    if (flag[k]) {
+        R[k] = screen_reach(S[k], E[k], max<int64_t>(1, M[k]), mc);
+        cidx[pos[k]] = (uint32_t)k;
+    } else {
+        R[k] = INT64_MIN;
+    }
+}
+// flag[k] cleared for a droppable kept hit (R: inclusive prefix max)
+__global__ void k_drop_flags(const int64_t *__restrict__ S, const int64_t *__restrict__ E,
+                             const int32_t *__restrict__ M, uint32_t *__restrict__ flag,
+                             const uint32_t *__restrict__ pos, const uint32_t *__restrict__ cidx,
+                             const int64_t *__restrict__ R, int64_t n, int32_t mc) {
+    const int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (k >= n || !flag[k]) return;
+    const int64_t s = S[k], e = E[k], m = max<int64_t>(1, M[k]), len = e - s;
+    if (len / m >= (int64_t)mc && len >= 6) return;   // passes the final filter: kept
+    if (k > 0 && R[k - 1] != INT64_MIN && s - R[k - 1] <= m + 1) return;
+    const uint32_t nk = pos[n], j = pos[k] + 1;
+    if (j < nk) {
+        const uint32_t q = cidx[j];
+        const int64_t mq = max<int64_t>(1, M[q]);
+        if (S[q] - e <= max(m, mq) + 1) return;
+    }
+    flag[k] = 0u;
+}
+
 // kept hits in screen order, one 64-bit word each (lbits >= 0: start | len << 32
 // | prim << (32 + lbits)) or two ({start, len | prim << 32}); common.h ScreenedVec
 __global__ void k_final_compact(const bwtmi_hit *__restrict__ H, const uint32_t *__restrict__ vpos,
@@ -520,7 +582,7 @@ static void screen_levels(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int32_t lm
 }
 
 void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text_len, int32_t lmax,
-                        ScreenedVec &out, int64_t maxlen_known) {
+                        ScreenedVec &out, int64_t maxlen_known, int32_t drop_min_copies) {
     out.clear();
     if (n <= 0) return;
     if (n >= (int64_t)UINT32_MAX) fail(BWTMI_E_ARG, "too many strict hits for one contig (%lld)", (long long)n);
@@ -591,10 +653,24 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     out.lbits = !wide && lbits + pbits <= 32 && bits_for((uint64_t)text_len) <= 32 ? lbits : -1;
     // the kept flags -> their order -> the packed records, and the kept count
     // with the screen's overflow flag (mb[1]) in the same stream wait
+    // records only the final filter would see are dropped here (k_drop_flags;
+    // BWTMI_SCREEN_DROP=0 keeps them): at C3 most kept hits are short runs
+    const bool drop = drop_min_copies > 0 && knob(KN_SCREEN_DROP) != 0;
+    if (drop) c.slot[S_IDX7].ensure((size_t)(n + 1) * 4);
     auto final_pass = [&] {
         KLAUNCH("k_final_flags", 0.0, k_final_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, kept, n, flag);
         HIPCHECK(hipMemsetAsync(flag + n, 0, 4, st));
         exclusive_scan<uint32_t>(c, flag, pos, n + 1);
+        if (drop) {
+            int64_t *R = c.slot[S_CAND_K].as<int64_t>();   // the sorted keys are spent
+            uint32_t *cidx = c.slot[S_IDX7].as<uint32_t>();
+            KLAUNCH("k_drop_reach", 0.0, k_drop_reach, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, flag, pos, n,
+                    drop_min_copies, R, cidx);
+            prefix_max(c, R, R, n, c.slot[S_IDX5].as<int64_t>());
+            KLAUNCH("k_drop_flags", 0.0, k_drop_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, flag, pos, cidx, R,
+                    n, drop_min_copies);
+            exclusive_scan<uint32_t>(c, flag, pos, n + 1);
+        }
         KLAUNCH("k_final_compact", 0.0, k_final_compact, dim3(blocks(n)), dim3(kB), 0, st, d_hits, vpos, flag, pos, n,
                 out.lbits, dout);
         HIPCHECK(hipGetLastError());

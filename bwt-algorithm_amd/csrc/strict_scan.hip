@@ -1108,7 +1108,7 @@ void strict_scan_mm_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min
 }
 
 void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_unit, int32_t max_unit,
-                        int32_t min_copies, ScanResult &res, bool screen) {
+                        int32_t min_copies, ScanResult &res, bool screen, int32_t drop_min_copies) {
     res.hits.clear();
     res.shits.clear();
     res.candidates = 0;
@@ -1156,7 +1156,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
         HIPCHECK(hipGetLastError());
         res.raw = nh;
         if (screen) {
-            screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.shits);
+            screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.shits, -1, drop_min_copies);
             c.kresolve();
             return;
         }
@@ -1322,7 +1322,7 @@ void strict_scan_device(Ctx &c, const uint8_t *d_text, int64_t n, int32_t min_un
     if (screen) {
         // records c.ev1 behind its kernels; its hits download may still be landing
         // (res.shits.wait), every kernel has finished
-        screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.shits, maxlen);
+        screen_hits_device(c, c.slot[S_HITS].as<bwtmi_hit>(), nh, n, lmax, res.shits, maxlen, drop_min_copies);
         if (c.timing && !res.shits.landing) HIPCHECK(hipEventRecord(c.ev1, st));
         if (!res.shits.landing) scan_wait(st);
         else if (c.timing) while (hipEventQuery(c.ev1) == hipErrorNotReady) __builtin_ia32_pause();

@@ -286,6 +286,28 @@ def test_device_screen_matches_host(gpu_ctx, case):
         assert _job_output(contigs, True, fmt="strfinder")[1] == _job_output(contigs, False, fmt="strfinder")[1]
 
 
+@pytest.mark.parametrize("mc", [1, 2, 4, 7])
+def test_screen_drop_matches_host(gpu_ctx, mc):
+    """The screen drops kept hits that fail the final filter and that no merge,
+    refine or collapse can reach (nested.hip k_drop_flags): the job's output
+    equals the host screen's (which keeps every hit) and the device screen's
+    with BWTMI_SCREEN_DROP=0, for other min_copies, imperfect arrays, N gaps and
+    a fold unit of several contigs; the drop removes hits."""
+    from bwtmi import _lib, synth
+    contigs = [("c1", synth.generate_contig(1_500_000, 20 + mc, 0.02)),
+               ("c2", synth.generate_contig(600_000, 30 + mc, 0.0, gaps="n1")),
+               ("p3", _planted(200_000, 40 + mc, b"ACGTN", max_unit=300, density=0.6))]
+    unit = [("chr01", _planted(60_000, 50 + mc)), ("CHR1", synth.generate_contig(80_000, 60 + mc, 0.03))]
+    for cs in (contigs, unit):
+        for fmt in ("strfinder", "vcf"):
+            rh, h = _job_output(cs, False, mc=mc, fmt=fmt)
+            rd, d = _job_output(cs, True, mc=mc, fmt=fmt)
+            with _lib.knobs(SCREEN_DROP=0):
+                rk, k = _job_output(cs, True, mc=mc, fmt=fmt)
+            assert rd == rh == rk
+            assert d == h == k, (mc, fmt)
+
+
 def test_screened_hits_landing_in_pieces(gpu_ctx):
     """The scan returns while its screened-hit download is still landing (in
     pieces, an event behind each; nested.hip).  A job reset or a rescan right
