@@ -458,16 +458,6 @@ __global__ __launch_bounds__(kB) void k_level_wave(const uint32_t *__restrict__ 
     if (lane == 0) kept[rank_of[idx]] = nested ? 0 : 1;
 }
 
-__global__ void k_final_flags(const int64_t *__restrict__ S, const int64_t *__restrict__ E,
-                              const int32_t *__restrict__ M, const uint8_t *__restrict__ kept, int64_t n,
-                              uint32_t *__restrict__ flag) {
-    const int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x;
-    if (k >= n) return;
-    bool f = kept[k] != 0;
-    if (f && k > 0 && S[k - 1] == S[k] && E[k - 1] == E[k] && M[k - 1] == M[k]) f = false;
-    flag[k] = f ? 1u : 0u;
-}
-
 // ---- records the post-processing would only carry to its final filter.
 // A kept hit that fails the final filter on its own (bwt.py:3940-3944:
 // (end - start) // prim < min_copies or end - start < 6 -- an unmerged strict
@@ -490,44 +480,49 @@ __global__ void k_final_flags(const int64_t *__restrict__ S, const int64_t *__re
 //   collapse (bwt.py:3499-3513) needs an overlap: the hit overlaps nothing, and
 //     nothing that was separated by it overlaps after it is gone.
 // R over the kept hits in screen order is an inclusive prefix max of reach()
-// (non-kept entries contribute nothing); cidx lists the kept hits' ranks, so
-// the next kept hit of rank k is cidx[pos[k] + 1].
+// (non-kept entries contribute nothing; k_final_flags writes it); the next
+// kept hit is found by a short probe forward (kept hits are dense: a probe
+// that finds none within kDropProbe ranks keeps the hit).
+constexpr int kDropProbe = 64;
 __device__ __forceinline__ int64_t screen_reach(int64_t s, int64_t e, int64_t m, int32_t mc) {
     if (m == 1) return e;
     const int64_t mi = m >= 4 ? min<int64_t>(10, m / 2) : 1;
     const int64_t ext = max<int64_t>(3 * m, 4 * mi);
     return max(e, s + m * (int64_t)mc) + 2 * ext;
 }
-__global__ void k_drop_reach(const int64_t *__restrict__ S, const int64_t *__restrict__ E,
+// out[k] = flag[k], cleared for a droppable kept hit (R: inclusive prefix max;
+// flag is read only, so every probe sees the kept set before the drop)
+__global__ void k_drop_flags(const int64_t *__restrict__ S, const int64_t *__restrict__ E,
                              const int32_t *__restrict__ M, const uint32_t *__restrict__ flag,
-                             const uint32_t *__restrict__ pos, int64_t n, int32_t mc, int64_t *__restrict__ R,
-                             uint32_t *__restrict__ cidx) {
+                             const int64_t *__restrict__ R, int64_t n, int32_t mc, uint32_t *__restrict__ out) {
     const int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x;
     if (k >= n) return;
-    if (flag[k]) {
-        R[k] = screen_reach(S[k], E[k], max<int64_t>(1, M[k]), mc);
-        cidx[pos[k]] = (uint32_t)k;
-    } else {
-        R[k] = INT64_MIN;
-    }
-}
-// flag[k] cleared for a droppable kept hit (R: inclusive prefix max)
-__global__ void k_drop_flags(const int64_t *__restrict__ S, const int64_t *__restrict__ E,
-                             const int32_t *__restrict__ M, uint32_t *__restrict__ flag,
-                             const uint32_t *__restrict__ pos, const uint32_t *__restrict__ cidx,
-                             const int64_t *__restrict__ R, int64_t n, int32_t mc) {
-    const int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x;
-    if (k >= n || !flag[k]) return;
+    const uint32_t f = flag[k];
+    out[k] = f;
+    if (!f) return;
     const int64_t s = S[k], e = E[k], m = max<int64_t>(1, M[k]), len = e - s;
     if (len / m >= (int64_t)mc && len >= 6) return;   // passes the final filter: kept
     if (k > 0 && R[k - 1] != INT64_MIN && s - R[k - 1] <= m + 1) return;
-    const uint32_t nk = pos[n], j = pos[k] + 1;
-    if (j < nk) {
-        const uint32_t q = cidx[j];
+    int64_t q = k + 1;
+    while (q < n && !flag[q] && q - k < kDropProbe) ++q;
+    if (q < n) {
+        if (!flag[q]) return;   // no kept hit within the probe: keep
         const int64_t mq = max<int64_t>(1, M[q]);
         if (S[q] - e <= max(m, mq) + 1) return;
     }
-    flag[k] = 0u;
+    out[k] = 0u;
+}
+
+// R (drop_mc > 0): the reach of each kept hit, INT64_MIN elsewhere (k_drop_flags)
+__global__ void k_final_flags(const int64_t *__restrict__ S, const int64_t *__restrict__ E,
+                              const int32_t *__restrict__ M, const uint8_t *__restrict__ kept, int64_t n,
+                              uint32_t *__restrict__ flag, int32_t drop_mc, int64_t *__restrict__ R) {
+    const int64_t k = (int64_t)blockIdx.x * kB + threadIdx.x;
+    if (k >= n) return;
+    bool f = kept[k] != 0;
+    if (f && k > 0 && S[k - 1] == S[k] && E[k - 1] == E[k] && M[k - 1] == M[k]) f = false;
+    flag[k] = f ? 1u : 0u;
+    if (drop_mc > 0) R[k] = f ? screen_reach(S[k], E[k], max<int64_t>(1, M[k]), drop_mc) : INT64_MIN;
 }
 
 // kept hits in screen order, one 64-bit word each (lbits >= 0: start | len << 32
@@ -658,20 +653,19 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     const bool drop = drop_min_copies > 0 && knob(KN_SCREEN_DROP) != 0;
     if (drop) c.slot[S_IDX7].ensure((size_t)(n + 1) * 4);
     auto final_pass = [&] {
-        KLAUNCH("k_final_flags", 0.0, k_final_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, kept, n, flag);
-        HIPCHECK(hipMemsetAsync(flag + n, 0, 4, st));
-        exclusive_scan<uint32_t>(c, flag, pos, n + 1);
+        int64_t *R = drop ? c.slot[S_CAND_K].as<int64_t>() : nullptr;   // (the sorted keys are spent)
+        KLAUNCH("k_final_flags", 0.0, k_final_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, kept, n, flag,
+                drop ? drop_min_copies : 0, R);
+        uint32_t *fl = flag;   // the flags the compaction takes
         if (drop) {
-            int64_t *R = c.slot[S_CAND_K].as<int64_t>();   // the sorted keys are spent
-            uint32_t *cidx = c.slot[S_IDX7].as<uint32_t>();
-            KLAUNCH("k_drop_reach", 0.0, k_drop_reach, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, flag, pos, n,
-                    drop_min_copies, R, cidx);
+            fl = c.slot[S_IDX7].as<uint32_t>();
             prefix_max(c, R, R, n, c.slot[S_IDX5].as<int64_t>());
-            KLAUNCH("k_drop_flags", 0.0, k_drop_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, flag, pos, cidx, R,
-                    n, drop_min_copies);
-            exclusive_scan<uint32_t>(c, flag, pos, n + 1);
+            KLAUNCH("k_drop_flags", 0.0, k_drop_flags, dim3(blocks(n)), dim3(kB), 0, st, S, E, M, flag, R, n,
+                    drop_min_copies, fl);
         }
-        KLAUNCH("k_final_compact", 0.0, k_final_compact, dim3(blocks(n)), dim3(kB), 0, st, d_hits, vpos, flag, pos, n,
+        HIPCHECK(hipMemsetAsync(fl + n, 0, 4, st));
+        exclusive_scan<uint32_t>(c, fl, pos, n + 1);
+        KLAUNCH("k_final_compact", 0.0, k_final_compact, dim3(blocks(n)), dim3(kB), 0, st, d_hits, vpos, fl, pos, n,
                 out.lbits, dout);
         HIPCHECK(hipGetLastError());
         HIPCHECK(hipMemcpyAsync(reinterpret_cast<uint32_t *>(mb), pos + n, 4, hipMemcpyDeviceToHost, st));
