@@ -248,6 +248,8 @@ def main():
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--host-load", action="store_true",
                     help="whole-file load on the host + upload (default: built on the device from the file image)")
+    ap.add_argument("--time-all-kernels", action="store_true",
+                    help="time every launch in the timed steps (default: only the dominant kernel; the table from the warmup)")
     ap.add_argument("--sync-write", action="store_true",
                     help="write each step's file before the step ends (bwtmi_job_write) instead of behind the next step")
     ap.add_argument("--pmc-summary", default=None,
@@ -337,8 +339,26 @@ def main():
         if c is not None:
             c.barrier()
 
-    for _ in range(a.warmup):
+    # Every launch is timed during the warmup steps after the first (the
+    # kernels_ms_per_step table and the choice of the dominant kernel); in the
+    # timed steps only the dominant kernel is (its live roofline): an event pair
+    # per launch leaves ~10 us of device idle between dependent launches, 0.7 ms
+    # in the scan call's 73 launches (r06ae, tools/scan_gaps.py).
+    warm_stats, warm_steps = {}, 0
+    for w in range(a.warmup):
+        if w == min(1, a.warmup - 1):
+            _lib.kernel_stats(ctx, enable=True, reset=True)
         step()
+        warm_steps += w >= min(1, a.warmup - 1)
+    if a.warmup:
+        warm_stats = _lib.kernel_stats(ctx, enable=False, reset=True)
+    dominant = ""
+    if warm_stats and not a.time_all_kernels:
+        with_b = {k: v for k, v in warm_stats.items() if v[2] > 0}
+        dominant = max(warm_stats.items(), key=lambda kv: kv[1][0])[0]
+        if warm_stats[dominant][2] <= 0 and with_b:
+            dominant = max(with_b.items(), key=lambda kv: kv[1][0])[0]
+    _lib.kernel_stats_filter(ctx, dominant)
     calls.clear()
     _lib.kernel_stats(ctx, enable=True, reset=True)
     sync()
@@ -350,6 +370,9 @@ def main():
     elapsed = time.perf_counter() - t0
     host1 = host_counters()
     kstats = _lib.kernel_stats(ctx, enable=False, reset=True)
+    _lib.kernel_stats_filter(ctx, "")
+    # the per-kernel table: the warmup's when the timed steps timed only the dominant kernel
+    table, table_steps = (warm_stats, warm_steps) if dominant else (kstats, a.steps)
     stages = job.stage_ms()
     if c is not None:
         import numpy as np
@@ -386,8 +409,10 @@ def main():
     value = total_bp / 1e6 / (elapsed / a.steps)
     per_call = {k: v / a.steps for k, v in calls.items()}
 
-    # dominant kernel = largest total device time in the timed steps (every launch is timed)
-    dev_ms = sum(v[0] for v in kstats.values())
+    # dominant kernel = largest total device time (over the warmup's timed
+    # launches; or the timed steps' with --time-all-kernels), its live time
+    # from the timed steps
+    dev_ms = sum(v[0] for v in table.values()) / max(1, table_steps) * a.steps
     roofline = None
     with_bytes = {k: v for k, v in kstats.items() if v[2] > 0}
     if with_bytes:
@@ -427,7 +452,7 @@ def main():
         for k, v in word_compares(w, max(120, min(w // 3, 1000))).items():
             wc[k] += v
     scan_names = ("k_runs", "k_runs_sparse", "k_streak_end")
-    scan_ms = sum(kstats[k][0] for k in scan_names if k in kstats) / a.steps
+    scan_ms = sum(table[k][0] for k in scan_names if k in table) / max(1, table_steps)
     scan_rate = None
     if scan_ms > 0:
         done = wc["dense"] + wc["sparse"]
@@ -491,8 +516,10 @@ def main():
                                "merge": round(stages[4], 2), "refine..filter": round(stages[5], 2),
                                "render": round(stages[6], 2)},
         "device_ms_per_step": round(dev_ms / a.steps, 3),
-        "kernels_ms_per_step": {k: round(v[0] / a.steps, 3) for k, v in
-                                sorted(kstats.items(), key=lambda kv: -kv[1][0])},
+        "kernels_ms_per_step": {k: round(v[0] / max(1, table_steps), 3) for k, v in
+                                sorted(table.items(), key=lambda kv: -kv[1][0])},
+        "kernels_ms_source": (f"warmup steps 2-{a.warmup} (every launch timed); in the timed steps only "
+                              f"{dominant} is timed" if dominant else "timed steps (every launch timed)"),
         "calls_ms_per_step": {k: round(v, 2) for k, v in per_call.items()},
         "host_per_step": {k: round((host1[k] - host0[k]) / a.steps, 1) for k in host1 if k in host0},
         "value_resident_text": round(total_bp / 1e6 / ((ms_step - load_up) / 1e3), 3) if ms_step > load_up else None,

@@ -53,6 +53,7 @@ _SIGS = {
     "bwtmi_free": (None, [_P]),
     "bwtmi_last_timing": (C.c_int, [_P, C.POINTER(C.c_double)]),
     "bwtmi_kernel_stats": (C.c_int, [_P, C.c_int, C.c_int, C.c_char_p, C.c_int64]),
+    "bwtmi_kernel_stats_filter": (C.c_int, [_P, C.c_char_p]),
     "bwtmi_strict_scan": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                     C.POINTER(C.POINTER(Hit)), C.POINTER(C.c_int64)]),
     "bwtmi_index_build": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_uint32, C.POINTER(_P)]),
@@ -293,6 +294,11 @@ def kernel_stats(h, enable: bool = True, reset: bool = True) -> dict:
         name, ms, n, b = line.split()
         out[name] = (float(ms), int(n), float(b))
     return out
+
+
+def kernel_stats_filter(h, name: str = "") -> None:
+    """Time only the launches named `name` ("" = every launch)."""
+    check(lib().bwtmi_kernel_stats_filter(h, name.encode() if name else None))
 
 
 def host_info() -> dict:

@@ -456,6 +456,7 @@ static Ctx &scan_lane(Ctx &c, size_t k) {
     }
     Ctx &l = *c.lanes[k - 1];
     l.ktiming = c.ktiming;
+    l.kfilter = c.kfilter;
     l.timing = c.timing;
     return l;
 }
@@ -507,6 +508,14 @@ int bwtmi_last_timing(bwtmi_ctx *ctx, double *out3) {
         out3[0] = ctx->c.last_total_ms;
         out3[1] = ctx->c.last_dom_ms;
         out3[2] = ctx->c.last_dom_launches;
+    });
+}
+
+int bwtmi_kernel_stats_filter(bwtmi_ctx *ctx, const char *name) {
+    return guard([&] {
+        CHECK_ARG(ctx, "null ctx");
+        ctx_wait(ctx->c);
+        ctx->c.kfilter = name ? name : "";
     });
 }
 

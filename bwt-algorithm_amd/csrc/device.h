@@ -116,6 +116,9 @@ struct Ctx {
     };
     std::vector<Pend> pending;
     std::vector<size_t> open;   // kbegin/kend nest (a stage timer around primitive timers)
+    // bwtmi_kernel_stats_filter: time only the launches of this name ("" = every
+    // launch); the others get no events, so they run back to back as untimed
+    std::string kfilter;
     std::vector<std::pair<std::string, KStat>> kstats;
     std::vector<hipEvent_t> evpool;   // reused across kresolve calls
     size_t evused = 0;
@@ -139,6 +142,10 @@ struct Ctx {
     // every kernel launch is a leaf timer (KLAUNCH); kbegin/kend must not nest
     void kbegin(const char *name, double alg_bytes = 0) {
         if (!ktiming) return;
+        if (!kfilter.empty() && kfilter != name) {
+            open.push_back(SIZE_MAX);   // (kend pops it without an event)
+            return;
+        }
         hipEvent_t a = pooled_event(), b = pooled_event();
         HIPCHECK(hipEventRecord(a, stream));
         open.push_back(pending.size());
@@ -146,8 +153,9 @@ struct Ctx {
     }
     void kend() {
         if (!ktiming || open.empty()) return;
-        HIPCHECK(hipEventRecord(pending[open.back()].b, stream));
+        const size_t i = open.back();
         open.pop_back();
+        if (i != SIZE_MAX) HIPCHECK(hipEventRecord(pending[i].b, stream));
     }
     void kresolve() {   // after a stream sync
         FILE *trace = ktrace_file();

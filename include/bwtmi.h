@@ -93,6 +93,9 @@ int bwtmi_last_timing(bwtmi_ctx *ctx, double *out3);
  * the call writes "name ms launches\n" lines of everything collected so far
  * into out (cap bytes, NUL-terminated) and resets when reset=1 */
 int bwtmi_kernel_stats(bwtmi_ctx *ctx, int enable, int reset, char *out, int64_t cap);
+/* time only the launches named `name` (NULL or "": every launch); the others
+ * then run without event records between them */
+int bwtmi_kernel_stats_filter(bwtmi_ctx *ctx, const char *name);
 
 /* ------------------------------------------------------------ strict scan
  * Replaces Tier2LCPFinder.find_long_unit_repeats_strict (bwt.py:1891-2001),

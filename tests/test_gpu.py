@@ -682,3 +682,28 @@ def test_index_12mbp_properties(gpu_ctx):
         assert occ[c][-1] == int((t == c).sum())
     off, pos = core.kmer_csr()
     assert off[-1] == n - 8
+
+
+def test_kernel_stats_filter(gpu_ctx):
+    """bwtmi_kernel_stats_filter: with a name set only those launches are timed
+    (bench.py's timed steps time only the dominant kernel), with "" every one;
+    the scan's results do not depend on it."""
+    from bwtmi import _lib
+    seq = _planted(200_000, 123)
+    ctx = _lib.ctx()
+    want = _gpu_hits(seq, 1, 1000, 3)
+    try:
+        _lib.kernel_stats_filter(ctx, "k_runs")
+        _lib.kernel_stats(ctx, enable=True, reset=True)
+        got = _gpu_hits(seq, 1, 1000, 3)
+        only = _lib.kernel_stats(ctx, enable=False, reset=True)
+        assert set(only) == {"k_runs"} and only["k_runs"][1] >= 1
+        assert got.shape == want.shape and (got == want).all()
+        _lib.kernel_stats_filter(ctx, "")
+        _lib.kernel_stats(ctx, enable=True, reset=True)
+        _gpu_hits(seq, 1, 1000, 3)
+        every = _lib.kernel_stats(ctx, enable=False, reset=True)
+        assert "k_runs" in every and len(every) > 3
+    finally:
+        _lib.kernel_stats_filter(ctx, "")
+        _lib.kernel_stats(ctx, enable=False, reset=True)
