@@ -62,13 +62,16 @@ __global__ void k_maxlen(const bwtmi_hit *__restrict__ H, int64_t n, unsigned lo
 }
 
 // position sort, stage 1 key: (len << mb) | (lmax - m); group key: lmax - m
+// sshift >= 0: the start goes above (len, g) in the same key, so one sort
+// orders by (start, len, g) -- what the two stable sorts give
 __global__ void k_keys(const bwtmi_hit *__restrict__ H, int64_t n, int mb, int64_t lmax, uint64_t *__restrict__ kpos,
-                       uint32_t *__restrict__ vpos, uint64_t *__restrict__ kgrp, uint32_t *__restrict__ vgrp) {
+                       uint32_t *__restrict__ vpos, uint64_t *__restrict__ kgrp, uint32_t *__restrict__ vgrp,
+                       int sshift) {
     const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
     if (i >= n) return;
     const bwtmi_hit h = H[i];
     const uint64_t g = (uint64_t)(lmax - h.prim_len);
-    kpos[i] = ((uint64_t)(h.end - h.start) << mb) | g;
+    kpos[i] = ((uint64_t)(h.end - h.start) << mb) | g | (sshift >= 0 ? (uint64_t)h.start << sshift : 0ull);
     vpos[i] = (uint32_t)i;
     kgrp[i] = g;
     vgrp[i] = (uint32_t)i;
@@ -629,11 +632,19 @@ void screen_hits_device(Ctx &c, const bwtmi_hit *d_hits, int64_t n, int64_t text
     if (lb + mb_bits > 64) fail(BWTMI_E_ARG, "span too long for the screen keys");
     auto round8 = [](int b) { return ((b + 7) / 8) * 8; };
 
+    // (start, len, g) in one key when it fits 64 bits (C3: 27 + 10 + 10 bits, 6
+    // passes instead of 3 + 4), else two stable sorts
+    const int sb = std::max(1, bits_for((uint64_t)text_len));   // start < text_len
+    const bool one_key = sb + lb + mb_bits <= 64;
     KLAUNCH("k_keys", 0.0, k_keys, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, mb_bits, (int64_t)lmax, kpos, vpos, kgrp,
-            vgrp);
-    radix_sort_pairs32(c, kpos, vpos, n, 0, round8(lb + mb_bits));
-    KLAUNCH("k_keys_start", 0.0, k_keys_start, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, kpos);
-    radix_sort_pairs32(c, kpos, vpos, n, 0, round8(std::max(1, bits_for((uint64_t)text_len))));   // start < text_len
+            vgrp, one_key ? lb + mb_bits : -1);
+    if (one_key) {
+        radix_sort_pairs32(c, kpos, vpos, n, 0, round8(sb + lb + mb_bits));
+    } else {
+        radix_sort_pairs32(c, kpos, vpos, n, 0, round8(lb + mb_bits));
+        KLAUNCH("k_keys_start", 0.0, k_keys_start, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, kpos);
+        radix_sort_pairs32(c, kpos, vpos, n, 0, round8(sb));
+    }
     KLAUNCH("k_gather", 0.0, k_gather, dim3(blocks(n)), dim3(kB), 0, st, d_hits, n, vpos, S, E, M, rank_of, kept);
     prefix_max(c, E, PME, n, c.slot[S_IDX5].as<int64_t>());
     // every level, segment by segment, in one launch (BWTMI_SEG_LEVELS=0: per-level launches)
