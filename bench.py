@@ -322,7 +322,9 @@ def main():
         if shared and world > 1:
             # each rank writes its own contigs' rows at offsets from two
             # all-reduces of per-unit sizes; no record leaves its GPU
-            timed("write", dist.write_sharded, c, job, "strfinder", out)
+            # (the pwrite lands behind the next step: joined before the next
+            # write's sizes all-reduce, and by sync() inside the timed region)
+            timed("write", dist.write_sharded, c, job, "strfinder", out, not a.sync_write)
         else:
             # repeat.tab, as the CLI writes it; the call returns once the rows are
             # formatted and the job's writer finishes the file behind the next
@@ -334,7 +336,7 @@ def main():
         timed("index_wait", job.wait, ctx)    # the FM index build ran behind the host work
 
     def sync():
-        job.write_join()
+        job.write_join()   # this rank's file write (every rank's, after the barrier below)
         _lib.lib().bwtmi_device_sync(local)
         if c is not None:
             c.barrier()
@@ -498,8 +500,9 @@ def main():
                    "contig_bp": wl["lengths"][0], "contigs": len(wl["lengths"]) * (1 if shared else world),
                    "parallelism": f"contig-shard x{world}", "index": not a.no_index,
                    "load": "host" if a.host_load else "device",
-                   "write": ("sharded pwrite in the step" if shared and world > 1 else
-                             "in the step" if a.sync_write else
+                   "write": ("in the step" if a.sync_write else
+                             "sharded: each rank's pwrite behind the next step, joined before the next write's "
+                             "sizes all-reduce and before the timed region ends" if shared and world > 1 else
                              "finished behind the next step's load and scan, joined before the file "
                              "is rewritten and before the timed region ends")},
         "roofline": roofline,

@@ -98,6 +98,7 @@ _SIGS = {
     "bwtmi_job_unit_rows": (C.c_int, [_P, _P]),
     "bwtmi_job_render_units": (C.c_int, [_P, C.c_int, _P, _P]),
     "bwtmi_job_write_units": (C.c_int, [_P, C.c_char_p, _P, C.c_int]),
+    "bwtmi_job_write_units_async": (C.c_int, [_P, C.c_char_p, _P, C.c_int]),
     "bwtmi_job_get_records": (C.c_int, [_P, _P, _P]),
     "bwtmi_job_get_string": (C.c_int64, [_P, C.c_int64, C.c_int, _P, C.c_int64]),
     "bwtmi_job_get_strings": (C.c_int64, [_P, C.c_int, _P, C.c_int64, _P]),

@@ -182,7 +182,7 @@ def assign(units: List[List[int]], weights: Sequence[int], world: int) -> List[L
     return [sorted(x) for x in out]
 
 
-def write_sharded(comm, job, fmt: str, path: str) -> int:
+def write_sharded(comm, job, fmt: str, path: str, background: bool = False) -> int:
     """Write the output file from every rank's own fold units, without moving
     records between ranks.  The file is the units' rows in unit (natural-key)
     order (bwt.py:4147-4150) and each unit lives on exactly one rank, so an
@@ -191,12 +191,20 @@ def write_sharded(comm, job, fmt: str, path: str) -> int:
     per-unit row counts first); rank 0 writes the header and sizes the file.
     Sizing commutes with the writes -- every rank writes inside [0, total), and
     ftruncate to total neither moves nor drops those bytes whenever it lands --
-    so only the end of the write needs a barrier.  Returns the file size."""
+    so only the end of the write needs a barrier.  Returns the file size.
+
+    background=True: each rank's pwrite runs behind the caller, and there is
+    no barrier: every rank joins its previous write before it enters the sizes
+    all-reduce, so once that returns no rank's earlier write is still landing
+    when rank 0 sizes the file and the ranks write again.  The caller joins
+    the last one with sharded_join()."""
     row_base = None
     if fmt == "vcf":
         rows = comm.allreduce(job.unit_rows())
         row_base = np.concatenate([[0], np.cumsum(rows)[:-1]]).astype(np.int64)
     local = job.render_units(fmt, row_base)
+    if background:
+        job.write_join()   # this rank's previous write (the all-reduce below then orders every rank's)
     sizes = comm.allreduce(np.ascontiguousarray(local[1:]))
     header = int(local[0])
     offsets = np.concatenate([[0, header], header + np.cumsum(sizes)[:-1]]).astype(np.int64)
@@ -209,9 +217,17 @@ def write_sharded(comm, job, fmt: str, path: str) -> int:
             os.ftruncate(fd, total)
         finally:
             os.close(fd)
-    job.write_units(path, offsets, write_header=(comm.rank == 0))
-    comm.barrier()
+    job.write_units(path, offsets, write_header=(comm.rank == 0), background=background)
+    if not background:
+        comm.barrier()
     return total
+
+
+def sharded_join(comm, job) -> None:
+    """Wait for this rank's background write (write_sharded(background=True)),
+    then for every rank's: afterwards the file is whole on every rank."""
+    job.write_join()
+    comm.barrier()
 
 
 def run_sharded(finder, job, scan_fn: Optional[Callable] = None):

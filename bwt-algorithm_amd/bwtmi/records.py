@@ -319,11 +319,14 @@ class Job:
             check(lib().bwtmi_job_render_units(self.h, _lib.FMT[fmt], rb, out.ctypes.data))
         return out
 
-    def write_units(self, path: str, offsets: np.ndarray, write_header: bool) -> None:
+    def write_units(self, path: str, offsets: np.ndarray, write_header: bool, background: bool = False) -> None:
+        """pwrite the rendered units at `offsets`; background=True returns at once
+        and write_join() waits for the job's writer (bwtmi_job_write_units_async)."""
         offsets = np.ascontiguousarray(offsets, dtype=np.int64)
         from . import profile
         with profile.stage("write"):
-            check(lib().bwtmi_job_write_units(self.h, path.encode(), offsets.ctypes.data, int(write_header)))
+            fn = lib().bwtmi_job_write_units_async if background else lib().bwtmi_job_write_units
+            check(fn(self.h, path.encode(), offsets.ctypes.data, int(write_header)))
 
     def export(self) -> bytes:
         p, n = C.c_void_p(), C.c_int64()

@@ -311,11 +311,19 @@ struct bwtmi_job {
     Job j;
     JobDev dev;
     std::unique_ptr<FileWrite> wr;   // a file still being written (bwtmi_job_write_async)
+    std::thread units_wr;            // rendered units still being written (bwtmi_job_write_units_async)
+    std::exception_ptr units_err;
 };
 
 namespace {
 // the job's file write in flight, if any: wait for it and report its error
 void write_join(bwtmi_job *job) {
+    if (job->units_wr.joinable()) job->units_wr.join();
+    if (job->units_err) {
+        std::exception_ptr e = job->units_err;
+        job->units_err = nullptr;
+        std::rethrow_exception(e);
+    }
     if (!job->wr) return;
     std::unique_ptr<FileWrite> w = std::move(job->wr);
     if (!w->finish()) fail(BWTMI_E_IO, "short write to %s", w->path.c_str());
@@ -764,6 +772,7 @@ int bwtmi_job_free(bwtmi_job *job) {
         if (!job) return;
         if (job->j.text_th.joinable()) job->j.text_th.join();   // its error dies with the job
         if (job->wr) (void)job->wr->finish();   // a file still being written is finished (its error dies too)
+        if (job->units_wr.joinable()) job->units_wr.join();
         if (job->dev.bg_ctx) ctx_join(*job->dev.bg_ctx);   // its error stays for the ctx's next call
         if (job->dev.device >= 0) (void)hipSetDevice(job->dev.device);
         for (auto &d : job->dev.seqs) d.buf.release();
@@ -1492,29 +1501,62 @@ int bwtmi_job_render_units(bwtmi_job *job, int fmt, const int64_t *row_base, int
     });
 }
 
+namespace {
+// the rendered units (bwtmi_job_render_units) as parts at their file offsets;
+// the job's rendering is handed over to them
+void units_parts(bwtmi_job *job, const int64_t *offsets, int write_header, std::vector<Text> &parts,
+                 std::vector<size_t> &at) {
+    Job &J = job->j;
+    Rendered &R = J.rendered;
+    std::vector<int64_t> fill((size_t)J.nunits, 0);
+    if (write_header && !R.header.empty()) {
+        parts.emplace_back(R.header.data(), R.header.size());
+        at.push_back((size_t)offsets[0]);
+    }
+    for (size_t k = 0; k < R.parts.size(); ++k) {
+        const int32_t u = R.part_unit[k];
+        at.push_back((size_t)(offsets[1 + u] + fill[(size_t)u]));
+        fill[(size_t)u] += (int64_t)R.parts[k].size();
+        parts.push_back(std::move(R.parts[k]));
+    }
+    R = Rendered();
+}
+}  // namespace
+
 int bwtmi_job_write_units(bwtmi_job *job, const char *path, const int64_t *offsets, int write_header) {
     return guard([&] {
         BWTMI_STAGE("bwtmi:write");
         CHECK_ARG(job && path && offsets, "null argument");
         pool_spin_for_job(job->j);
         TEXT_JOIN(job);
-        Job &J = job->j;
-        Rendered &R = J.rendered;
+        write_join(job);
         std::vector<Text> parts;
         std::vector<size_t> at;
-        std::vector<int64_t> fill((size_t)J.nunits, 0);
-        if (write_header && !R.header.empty()) {
-            parts.emplace_back(R.header.data(), R.header.size());
-            at.push_back((size_t)offsets[0]);
-        }
-        for (size_t k = 0; k < R.parts.size(); ++k) {
-            const int32_t u = R.part_unit[k];
-            at.push_back((size_t)(offsets[1 + u] + fill[(size_t)u]));
-            fill[(size_t)u] += (int64_t)R.parts[k].size();
-            parts.push_back(std::move(R.parts[k]));
-        }
-        R = Rendered();
-        pwrite_parts(path, false, parts, at, host_threads(J.params));
+        units_parts(job, offsets, write_header, parts, at);
+        pwrite_parts(path, false, parts, at, host_threads(job->j.params));
+    });
+}
+
+// The same behind the caller: the parts are written by the job's own thread;
+// bwtmi_job_write_join waits for it and returns its error (the job's next
+// write and bwtmi_job_free join it first).
+int bwtmi_job_write_units_async(bwtmi_job *job, const char *path, const int64_t *offsets, int write_header) {
+    return guard([&] {
+        BWTMI_STAGE("bwtmi:write");
+        CHECK_ARG(job && path && offsets, "null argument");
+        TEXT_JOIN(job);
+        write_join(job);
+        std::vector<Text> parts;
+        std::vector<size_t> at;
+        units_parts(job, offsets, write_header, parts, at);
+        const int nt = host_threads(job->j.params);
+        job->units_wr = std::thread([job, p = std::string(path), parts = std::move(parts), at = std::move(at), nt] {
+            try {
+                pwrite_parts(p.c_str(), false, parts, at, nt);
+            } catch (...) {
+                job->units_err = std::current_exception();
+            }
+        });
     });
 }
 

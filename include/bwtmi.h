@@ -267,6 +267,9 @@ int32_t bwtmi_job_unit_count(bwtmi_job *job);
 int bwtmi_job_unit_rows(bwtmi_job *job, int64_t *unit_rows);
 int bwtmi_job_render_units(bwtmi_job *job, int fmt, const int64_t *row_base, int64_t *bytes);
 int bwtmi_job_write_units(bwtmi_job *job, const char *path, const int64_t *offsets, int write_header);
+/* the same behind the caller (the job's thread pwrites the rendered units);
+ * bwtmi_job_write_join waits for it and returns its error */
+int bwtmi_job_write_units_async(bwtmi_job *job, const char *path, const int64_t *offsets, int write_header);
 /* final records as rows of int64: start, end, length, tier, n_copies_eval,
  * max_mm, score, flags (1: composition None / entropy 0.0, 2: k-mer scan piece),
  * chrom_id and doubles: copies, mismatch_rate, confidence, percent_matches,

@@ -571,6 +571,14 @@ def _sharded_write_worker(rank, world, port, fa, outdir):
     j.postprocess()
     for fmt in ("strfinder", "bed", "vcf", "trf_table", "trf_dat"):
         dist.write_sharded(c, j, fmt, os.path.join(outdir, f"{fmt}.out"))
+    # background pwrites: each joined before the next write's sizes all-reduce,
+    # the last by sharded_join; one file rewritten back to back (vcf, then the
+    # shorter bed: rank 0 cuts it only after every rank's vcf write has landed)
+    for fmt in ("strfinder", "bed", "vcf", "trf_table", "trf_dat"):
+        dist.write_sharded(c, j, fmt, os.path.join(outdir, f"bg_{fmt}.out"), background=True)
+    dist.write_sharded(c, j, "vcf", os.path.join(outdir, "bg_again.out"), background=True)
+    dist.write_sharded(c, j, "bed", os.path.join(outdir, "bg_again.out"), background=True)
+    dist.sharded_join(c, j)
     c.barrier()
     comm.close()
 
@@ -579,13 +587,18 @@ def _sharded_write_worker(rank, world, port, fa, outdir):
 def test_sharded_write_matches_single_process(tmp_path, golden_dir, built_lib, world, name):
     """Each rank writes its own fold units at exchanged offsets; the file equals
     the single-process output in every format (incl. global VCF row ids), also
-    over a longer stale file (rank 0 sizes it while the others write)."""
+    over a longer stale file (rank 0 sizes it while the others write), and with
+    the pwrites behind the caller (write_sharded(background=True))."""
     fa = os.path.join(golden_dir, "inputs", name)
     for fmt in ("strfinder", "bed", "vcf", "trf_table", "trf_dat"):
         (tmp_path / f"{fmt}.out").write_bytes(b"stale\n" * 200_000)
+        (tmp_path / f"bg_{fmt}.out").write_bytes(b"stale\n" * 200_000)
     _spawn(_sharded_write_worker, (world, _free_port(), fa, str(tmp_path)), world)
     for fmt in ("strfinder", "bed", "vcf", "trf_table", "trf_dat"):
-        assert (tmp_path / f"{fmt}.out").read_text() == post.run_file(fa, fmt), fmt
+        want = post.run_file(fa, fmt)
+        assert (tmp_path / f"{fmt}.out").read_text() == want, fmt
+        assert (tmp_path / f"bg_{fmt}.out").read_text() == want, fmt
+    assert (tmp_path / "bg_again.out").read_text() == post.run_file(fa, "bed")
 
 
 def test_shard_assignment_is_lpt_and_keeps_natural_key_units():

@@ -104,10 +104,13 @@ def main():
     worlds = [int(x) for x in os.environ.get("C4_SHARD_WORLDS", "8").split(",")]
     res = dict(workload="C4 shard: 8 x 12.5 Mbp FASTA, LPT shards of worlds %s" % worlds, host=_lib.host_info(),
                step="split load (part tables all-gathered) -> index + scan -> post-processing -> "
-                    "dist.write_sharded (2 all-reduces, rank-0 truncate, 2 barriers)",
+                    "dist.write_sharded (all-reduce of unit sizes, rank-0 truncate; each rank's pwrite behind the "
+                    "next step as bench.py runs it, joined before the next sizes all-reduce, the last one joined "
+                    "inside the last timed step; C4_SHARD_SYNC_WRITE=1: pwrite and barrier in the step)",
                collectives="RCCL all-reduce at world 1 per call" if rccl else "none (recorded results only)",
                runs=[])
     devload = os.environ.get("C4_SHARD_DEVLOAD", "1") == "1"   # device placement of the load (bench default)
+    bg_write = os.environ.get("C4_SHARD_SYNC_WRITE", "0") != "1"
     res["device_load"] = devload
     for W, T in [(w, t) for w in worlds for t in tlist]:
         ranks = [int(x) for x in os.environ["C4_SHARD_RANKS"].split(",")] if os.environ.get("C4_SHARD_RANKS") else range(W)
@@ -158,15 +161,17 @@ def main():
                 timed("upload", job.upload, ctx)
                 timed("scan", job.scan, ctx)
                 timed("postprocess", job.postprocess)
-                timed("write", dist.write_sharded, pc, job, "strfinder", out)
+                timed("write", dist.write_sharded, pc, job, "strfinder", out, bg_write)
                 timed("index_wait", job.wait, ctx)
             step()
             calls.clear()
             ts = []
             cpu0 = cgroup_cpu_us()
-            for _ in range(3):
+            for q in range(3):
                 t = time.perf_counter()
                 step()
+                if q == 2 and bg_write:   # the last step's file is whole inside its time
+                    timed("write_join", dist.sharded_join, pc, job)
                 ts.append((time.perf_counter() - t) * 1e3)
             cpu1 = cgroup_cpu_us()
             bp = sum(job.contig_weight(i) for i in job.select_shard(W, r))
