@@ -176,7 +176,7 @@ def main():
             cpu1 = cgroup_cpu_us()
             bp = sum(job.contig_weight(i) for i in job.select_shard(W, r))
             res["runs"].append(dict(world=W, threads=T, rank=r, shard_bp=bp, step_ms=round(max(ts), 2),
-                                    median_ms=round(sorted(ts)[1], 2),
+                                    median_ms=round(sorted(ts)[1], 2), mean_ms=round(sum(ts) / len(ts), 2),
                                     steps_ms=[round(x, 2) for x in ts], stage_ms=[round(x, 2) for x in job.stage_ms()],
                                     calls_ms={k: round(v / 3, 2) for k, v in calls.items()},
                                     cpu_ms_per_step=round((cpu1 - cpu0) / 3e3, 2) if cpu0 is not None and cpu1 is not None
@@ -185,6 +185,9 @@ def main():
     for W, T in [(w, t) for w in worlds for t in tlist]:
         worst = max(x["step_ms"] for x in res["runs"] if x["threads"] == T and x["world"] == W)
         res[f"worst_step_ms_{W}rank_at_{T}_threads"] = worst
+        # what bench.py's line would see: the slowest rank's time over the steps
+        res[f"worst_rank_mean_ms_{W}rank_at_{T}_threads"] = max(
+            x["mean_ms"] for x in res["runs"] if x["threads"] == T and x["world"] == W)
         res[f"projected_{W}rank_mbp_per_s_at_{T}_threads_per_rank"] = round(100.0 / (worst / 1e3), 1)
     with open(out_json, "w") as f:
         json.dump(res, f, indent=1)
