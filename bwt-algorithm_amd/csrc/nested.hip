@@ -261,7 +261,10 @@ __global__ __launch_bounds__(T) void k_seg_levels(const int64_t *__restrict__ S,
         // copy is the window's whenever a == w0 (nearly always), and the two
         // head searches below read LDS -- one round trip to memory per window
         // instead of three (head search, end search, copy).
-        const int64_t L0 = w0 + CAP < n ? CAP : n - w0;
+        // (the window and a quarter more: its segments nearly always end
+        // there; loading all CAP entries read twice what a window uses)
+        constexpr int64_t kLoad = WIN + WIN / 4 < CAP ? WIN + WIN / 4 : CAP;
+        const int64_t L0 = w0 + kLoad < n ? kLoad : n - w0;
         for (int i = tid; i < L0; i += T) {
             sS[i] = S[w0 + i];
             sE[i] = E[w0 + i];
