@@ -250,11 +250,10 @@ namespace {
 // ms), while a 60 us spin, also held through longer serial parts, cost the C3
 // line ~7 % on another box (r03z).  Auto (-1, the default): 200 us while the
 // calling job holds <= 32 Mbp (its regions are short and come back to back:
-// W=8 shard 6.3-6.6 vs 6.8-7.3 ms at 10 us, r05gd), else 300 us: with the
-// screen's drop the C3 post-processing regions are short too (r06y/r06z, same
-// box: 10 us 3243 / 3281 Mbp/s, 300 us 3557 / 3512 / 3700, 1000 us 3655 / 3710,
-// 3000 us 3547 / 3481; on a faster box r06aa, 10 us 3741 / 3802 vs 300 us
-// 3798 / 3790: no loss).  0 = block at once.
+// W=8 shard 6.3-6.6 vs 6.8-7.3 ms at 10 us, r05gd), else 10 us (C3 within
+// its run-to-run spread either way; round 6 tried 300 us: r06y favoured it,
+// but interleaved after a warm-up run on one box, r06ar, 300 us 3582 / 3543 /
+// 3679 vs 10 us 3447 / 3615 / 3767 Mbp/s -- no gain, more CPU).  0 = block at once.
 std::atomic<int64_t> g_auto_spin_ns{10000};
 inline int64_t pool_spin_ns() {
     const int64_t k = knob(KN_POOL_SPIN_US);
@@ -401,7 +400,7 @@ void pool_spin_for_job(const Job &job) {
     int64_t bases = 0;
     for (size_t i = 0; i < job.contigs.size(); ++i)
         if (job.selected.empty() || (i < job.selected.size() && job.selected[i])) bases += job.contigs[i].trimmed_len();
-    g_auto_spin_ns.store(bases <= 32000000 ? 200000 : 300000, std::memory_order_relaxed);
+    g_auto_spin_ns.store(bases <= 32000000 ? 200000 : 10000, std::memory_order_relaxed);
 }
 
 // fn(begin, end) over [0, n) in contiguous chunks
