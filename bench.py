@@ -236,8 +236,8 @@ def launch_ranks(n: int, argv, script: str = None) -> int:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=["auto"] + sorted(WORKLOADS), default="auto")
     ap.add_argument("--contig-bp", type=int, default=0, help="override every contig length (tests)")
     ap.add_argument("--cpu-sample-bp", type=int, default=30_000_000)
